@@ -1,0 +1,1567 @@
+"""CPU oracle: Coraza v3.3.3 rule evaluation restated in Python.
+
+TEST INFRASTRUCTURE ONLY.  Only `tests/`, `__graft_entry__.smoke()` and
+`bench.py`'s `cpu_baseline` leg may import this module, and only as the
+checker.  The product (the HIP engine behind `include/gpuinspect.h`) never
+routes through it.
+
+Reference anchors
+-----------------
+* The operator compiles each ConfigMap's SecLang with
+  `coraza.NewWAF(coraza.NewWAFConfig().WithDirectives(data))`
+  (/root/reference/internal/controller/ruleset_controller.go:158-171) and
+  joins the ConfigMaps with "\\n" (:173-176) before `Cache.Put` (:180-181).
+* The evaluation itself happens in the data plane (coraza-proxy-wasm,
+  config/samples/engine.yaml:12) running coraza/v3 v3.3.3 (go.mod:6).
+  That module is NOT vendored under /root/reference and no Go toolchain is
+  present, so every function below marked [upstream] restates the published
+  algorithm of the named coraza source file from knowledge of that module.
+  See DESIGN.md "Oracle" for the list of semantic choices that are
+  therefore "parity unpinned" beyond the reference's own KATs.
+* The KATs that *are* pinned come from the reference's tests:
+  test/integration/coreruleset_test.go:57-127, reconcile_test.go:43-88,
+  multiple_gateways_test.go:89-100, multi_engine_gateway_test.go:82-138,
+  test/framework/resources.go:122-127 (SimpleBlockRule) and
+  config/samples/README.md:36-60.  They live in tests/golden/kats.json.
+
+Evaluation model (mirrors coraza's Transaction):
+  ProcessURI -> AddRequestHeader* -> ProcessRequestHeaders (phase 1)
+  -> ProcessRequestBody (body processor, phase 2) -> MatchedRules/Interruption.
+"""
+
+from __future__ import annotations
+
+import posixpath
+import re
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from . import goregex
+
+# ---------------------------------------------------------------------------
+# Errors
+# ---------------------------------------------------------------------------
+
+
+class SecLangError(ValueError):
+    """A directive that coraza.NewWAF would reject (ruleset_controller.go:160)."""
+
+
+# ---------------------------------------------------------------------------
+# Variables (coraza internal/variables) -- name -> (kind, case_insensitive)
+# kind: 'single' | 'map' | 'names' | 'args' | 'argnames' | 'tx' | 'matched'
+# ---------------------------------------------------------------------------
+
+SINGLE_VARS = {
+    "REQUEST_METHOD", "REQUEST_PROTOCOL", "REQUEST_URI", "REQUEST_URI_RAW",
+    "REQUEST_LINE", "REQUEST_FILENAME", "REQUEST_BASENAME", "QUERY_STRING",
+    "REQUEST_BODY", "REQUEST_BODY_LENGTH", "REQBODY_ERROR", "REQBODY_ERROR_MSG",
+    "REQBODY_PROCESSOR", "MULTIPART_STRICT_ERROR", "ARGS_COMBINED_SIZE",
+    "FULL_REQUEST_LENGTH", "MATCHED_VAR", "MATCHED_VAR_NAME",
+    "REMOTE_ADDR", "REMOTE_PORT", "SERVER_NAME", "URLENCODED_ERROR",
+}
+MAP_VARS = {
+    # name: (source collection(s), case_insensitive_keys)
+    "ARGS_GET": (("ARGS_GET",), False),
+    "ARGS_POST": (("ARGS_POST",), False),
+    "ARGS": (("ARGS_GET", "ARGS_POST"), False),
+    "REQUEST_HEADERS": (("REQUEST_HEADERS",), True),
+    "REQUEST_COOKIES": (("REQUEST_COOKIES",), False),
+    "TX": (("TX",), True),
+    "MATCHED_VARS": (("MATCHED_VARS",), True),
+}
+NAMES_VARS = {
+    "ARGS_GET_NAMES": (("ARGS_GET",), False),
+    "ARGS_POST_NAMES": (("ARGS_POST",), False),
+    "ARGS_NAMES": (("ARGS_GET", "ARGS_POST"), False),
+    "REQUEST_HEADERS_NAMES": (("REQUEST_HEADERS",), True),
+    "REQUEST_COOKIES_NAMES": (("REQUEST_COOKIES",), False),
+    "MATCHED_VARS_NAMES": (("MATCHED_VARS",), True),
+}
+ALL_VARS = SINGLE_VARS | set(MAP_VARS) | set(NAMES_VARS)
+
+
+@dataclass
+class RuleVariable:
+    name: str
+    key: str = ""              # literal key ("" = whole collection)
+    key_rx: Optional[goregex.GoRegexp] = None
+    count: bool = False
+    exceptions: List[Tuple[str, Optional[goregex.GoRegexp]]] = field(default_factory=list)
+
+
+@dataclass
+class Operator:
+    name: str
+    arg: str
+    negate: bool
+    rx: Optional[goregex.GoRegexp] = None
+    phrases: Optional[List[bytes]] = None
+    byte_ok: Optional[List[bool]] = None
+    macro: Optional[list] = None
+
+
+@dataclass
+class SetVar:
+    key: list              # macro template for the key (after "tx.")
+    value: Optional[list]  # macro template; None for "!tx.x" (remove)
+    remove: bool = False
+
+
+@dataclass
+class Rule:
+    id: int = 0
+    phase: int = 2
+    line: int = 0
+    variables: List[RuleVariable] = field(default_factory=list)
+    op: Optional[Operator] = None
+    transforms: List[str] = field(default_factory=list)
+    disruptive: str = ""          # "" | deny | drop | pass | block | redirect | allow
+    status: int = 0
+    capture: bool = False
+    multimatch: bool = False
+    setvars: List[SetVar] = field(default_factory=list)
+    ctls: List[Tuple[str, str]] = field(default_factory=list)
+    nondisruptive_order: List[Tuple[str, object]] = field(default_factory=list)
+    skip: int = 0
+    skip_after: str = ""
+    secmark: str = ""
+    chain: Optional["Rule"] = None
+    parent_id: int = 0
+    has_chain_action: bool = False
+    tags: List[str] = field(default_factory=list)
+
+
+@dataclass
+class WafConfig:
+    rule_engine: str = "On"       # On | Off | DetectionOnly
+    request_body_access: bool = False
+    request_body_limit: int = 134217728
+    request_body_limit_action: str = "Reject"
+    rules: List[Rule] = field(default_factory=list)
+    default_actions: Dict[int, str] = field(default_factory=dict)
+
+
+# ---------------------------------------------------------------------------
+# SecLang parser  [upstream internal/seclang/{parser,directives,rule_parser}.go]
+# ---------------------------------------------------------------------------
+
+IGNORED_DIRECTIVES = {
+    "secresponsebodyaccess", "secresponsebodymimetype", "secresponsebodylimit",
+    "secresponsebodylimitaction", "secauditengine", "secauditlogtype",
+    "secauditlog", "secauditlogformat", "secauditlogparts",
+    "secauditlogrelevantstatus", "secauditlogstoragedir", "secauditlogdirmode",
+    "secauditlogfilemode", "secdebuglog", "secdebuglogLevel".lower(),
+    "seccomponentsignature", "secrequestbodyinmemorylimit", "sectmpdir",
+    "secdatadir", "secargumentseparator", "seccollectiontimeout",
+    "secrequestbodynofileslimit", "secuploaddir", "secuploadkeepfiles",
+    "secuploadfilemode", "secunicodemap", "secpcrematchlimit",
+    "secpcrematchlimitrecursion", "secstatusengine", "secconnengine",
+    "secserversignature", "sechttpblkey", "secwebappid", "secsensorid",
+    "secargumentslimit", "secrequestbodyjsondepthlimit", "secmarker_",
+}
+
+ACTION_TYPES = {
+    # disruptive
+    "deny": "disruptive", "drop": "disruptive", "pass": "disruptive",
+    "block": "disruptive", "redirect": "disruptive", "allow": "disruptive",
+    # flow
+    "chain": "flow", "skip": "flow", "skipafter": "flow",
+    # metadata
+    "id": "metadata", "phase": "metadata", "msg": "metadata", "tag": "metadata",
+    "severity": "metadata", "ver": "metadata", "rev": "metadata",
+    "maturity": "metadata", "accuracy": "metadata",
+    # data
+    "status": "data", "xmlns": "data",
+    # non-disruptive
+    "t": "nondisruptive", "setvar": "nondisruptive", "capture": "nondisruptive",
+    "log": "nondisruptive", "nolog": "nondisruptive", "auditlog": "nondisruptive",
+    "noauditlog": "nondisruptive", "logdata": "nondisruptive",
+    "multimatch": "nondisruptive", "ctl": "nondisruptive",
+    "expirevar": "nondisruptive", "initcol": "nondisruptive",
+    "sanitisearg": "nondisruptive", "sanitisematched": "nondisruptive",
+    "setenv": "nondisruptive", "append": "nondisruptive",
+}
+
+PHASE_NAMES = {"request": 2, "response": 4, "logging": 5}
+
+
+def _split_lines(text: str):
+    """parser.go parseString: trim each line, join '\\' continuations."""
+    buf = ""
+    lineno = 0
+    start = 0
+    for raw in text.split("\n"):
+        lineno += 1
+        line = raw.strip()
+        if not buf:
+            start = lineno
+        if line.endswith("\\"):
+            buf += line[:-1]
+        else:
+            buf += line
+            yield start, buf
+            buf = ""
+    if buf:
+        yield start, buf
+
+
+def _cut_quoted(s: str):
+    """rule_parser.go cutQuotedString: escapes are kept, \\" does not end it."""
+    if not s or s[0] != '"':
+        raise SecLangError("expected quoted string: %r" % s)
+    for i in range(1, len(s)):
+        if s[i] != '"':
+            continue
+        if s[i - 1] == "\\":
+            continue
+        return s[1:i], s[i + 1:]
+    raise SecLangError("expected terminating quote: %r" % s)
+
+
+def _parse_actions_list(s: str):
+    """Split `a,b:'x,y',c:d` into [(key, value)] (quotes stripped)."""
+    out = []
+    cur = ""
+    quote = False
+    for ch in s:
+        if ch == "'":
+            quote = not quote
+            cur += ch
+            continue
+        if ch == "," and not quote:
+            out.append(cur)
+            cur = ""
+            continue
+        cur += ch
+    if cur.strip():
+        out.append(cur)
+    res = []
+    for item in out:
+        item = item.strip()
+        if not item:
+            continue
+        if ":" in item:
+            k, v = item.split(":", 1)
+        else:
+            k, v = item, ""
+        k = k.strip().lower()
+        v = v.strip()
+        if len(v) >= 2 and v[0] == "'" and v[-1] == "'":
+            v = v[1:-1]
+        if k not in ACTION_TYPES:
+            raise SecLangError("unknown action %r" % k)
+        res.append((k, v))
+    return res
+
+
+def _parse_variables(s: str, rule: Rule):
+    parts = []
+    cur = ""
+    in_rx = False
+    i = 0
+    while i < len(s):
+        ch = s[i]
+        if ch == "/" and cur.endswith(":") and not in_rx:
+            in_rx = True
+            cur += ch
+        elif ch == "/" and in_rx:
+            in_rx = False
+            cur += ch
+        elif ch == "|" and not in_rx:
+            parts.append(cur)
+            cur = ""
+        else:
+            cur += ch
+        i += 1
+    parts.append(cur)
+    for p in parts:
+        p = p.strip()
+        if not p:
+            continue
+        neg = cnt = False
+        if p[0] == "!":
+            neg = True
+            p = p[1:]
+        elif p[0] == "&":
+            cnt = True
+            p = p[1:]
+        name, _, key = p.partition(":")
+        name = name.upper()
+        if name not in ALL_VARS:
+            raise SecLangError("unknown variable %r" % name)
+        key_rx = None
+        if len(key) >= 2 and key[0] == "'" and key[-1] == "'":
+            key = key[1:-1]
+        if len(key) > 2 and key[0] == "/" and key[-1] == "/":
+            try:
+                key_rx = goregex.compile_go(key[1:-1])
+            except goregex.RegexError as e:
+                raise SecLangError("invalid key regex %r: %s" % (key, e))
+            key = key[1:-1]
+        if neg:
+            # rule.go AddVariableNegation: applies to earlier vars of same type
+            matched = False
+            for rv in rule.variables:
+                if rv.name == name:
+                    rv.exceptions.append((key.lower(), key_rx))
+                    matched = True
+            if not matched:
+                raise SecLangError("cannot negate variable %s that is not targeted" % name)
+            continue
+        if name in SINGLE_VARS and key:
+            raise SecLangError("variable %s does not accept a key" % name)
+        rule.variables.append(RuleVariable(name=name, key=key if key_rx is None else "",
+                                           key_rx=key_rx, count=cnt))
+
+
+# macro templates [upstream internal/macro]: list of str | ("var", NAME, key)
+_MACRO_RE = re.compile(r"%\{([^}]+)\}")
+
+
+def parse_macro(s: str):
+    parts = []
+    pos = 0
+    for m in _MACRO_RE.finditer(s):
+        if m.start() > pos:
+            parts.append(s[pos:m.start()])
+        ref = m.group(1)
+        name, _, key = ref.partition(".")
+        parts.append(("var", name.upper(), key.lower()))
+        pos = m.end()
+    if pos < len(s):
+        parts.append(s[pos:])
+    return parts
+
+
+def _has_macro(parts):
+    return any(isinstance(p, tuple) for p in parts)
+
+
+def _parse_operator(opstr: str) -> Operator:
+    # rule_parser.go ParseOperator: default operator is @rx
+    if len(opstr) == 0 or (opstr[0] != "@" and (len(opstr) < 2 or opstr[1] != "@")):
+        opstr = "@rx " + opstr
+    raw, _, data = opstr.partition(" ")
+    raw = raw.strip()
+    data = data.strip()
+    negate = False
+    if raw.startswith("!@"):
+        negate = True
+        name = raw[2:]
+    elif raw.startswith("@"):
+        name = raw[1:]
+    else:
+        name = raw
+    name_l = name.lower()
+    op = Operator(name=name_l, arg=data, negate=negate)
+    if name_l == "rx":
+        try:
+            op.rx = goregex.rx_compile(data)
+        except goregex.RegexError as e:
+            raise SecLangError("invalid regex %r: %s" % (data, e))
+    elif name_l == "pm":
+        op.phrases = [p.encode().lower() for p in data.lower().split(" ") if p]
+    elif name_l in ("contains", "streq", "beginswith", "endswith", "within",
+                    "eq", "ge", "gt", "le", "lt", "containsword"):
+        op.macro = parse_macro(data)
+    elif name_l == "validatebyterange":
+        ok = [False] * 256
+        for part in data.split(","):
+            part = part.strip()
+            if not part:
+                continue
+            if "-" in part:
+                a, b = part.split("-", 1)
+                a, b = int(a), int(b)
+                if not (0 <= a <= 255 and 0 <= b <= 255 and a <= b):
+                    raise SecLangError("invalid byte range %r" % part)
+                for x in range(a, b + 1):
+                    ok[x] = True
+            else:
+                a = int(part)
+                if not 0 <= a <= 255:
+                    raise SecLangError("invalid byte %r" % part)
+                ok[a] = True
+        op.byte_ok = ok
+    elif name_l in ("unconditionalmatch", "nomatch", "validateurlencoding",
+                    "validateutf8encoding"):
+        pass
+    else:
+        raise SecLangError("unsupported operator @%s" % name)
+    return op
+
+
+TRANSFORMS_SUPPORTED = {
+    "none", "lowercase", "urldecode", "urldecodeuni", "htmlentitydecode",
+    "removenulls", "replacenulls", "removewhitespace", "compresswhitespace",
+    "replacecomments", "cmdline", "length", "trim", "trimleft", "trimright",
+    "normalizepath", "normalisepath", "normalizepathwin", "normalisepathwin",
+    "jsdecode",
+}
+
+
+def _apply_actions(rule: Rule, actions, is_child: bool):
+    for k, v in actions:
+        if k == "id":
+            rule.id = int(v)
+        elif k == "phase":
+            vl = v.lower()
+            rule.phase = PHASE_NAMES[vl] if vl in PHASE_NAMES else int(v)
+        elif k in ("deny", "drop", "pass", "block", "redirect", "allow"):
+            if k == "allow":
+                raise SecLangError("action allow is not supported")
+            rule.disruptive = k
+        elif k == "status":
+            rule.status = int(v)
+        elif k == "chain":
+            rule.has_chain_action = True
+        elif k == "skip":
+            rule.skip = int(v)
+        elif k == "skipafter":
+            rule.skip_after = v
+        elif k == "t":
+            tl = v.lower()
+            if tl == "none":
+                rule.transforms = []
+            else:
+                if tl not in TRANSFORMS_SUPPORTED:
+                    raise SecLangError("unsupported transformation t:%s" % v)
+                rule.transforms.append(tl)
+        elif k == "capture":
+            rule.capture = True
+        elif k == "multimatch":
+            rule.multimatch = True
+        elif k == "tag":
+            rule.tags.append(v)
+        elif k == "setvar":
+            sv = _parse_setvar(v)
+            rule.setvars.append(sv)
+            rule.nondisruptive_order.append(("setvar", sv))
+        elif k == "ctl":
+            name, _, val = v.partition("=")
+            name = name.strip()
+            cl = (name.lower(), val.strip())
+            if cl[0] not in ("ruleremovebyid", "ruleengine", "requestbodyprocessor",
+                             "requestbodyaccess", "forcerequestbodyvariable"):
+                raise SecLangError("unsupported ctl %s" % name)
+            rule.ctls.append(cl)
+            rule.nondisruptive_order.append(("ctl", cl))
+
+
+def _parse_setvar(v: str) -> SetVar:
+    # [upstream internal/actions/setvar.go] "tx.key=value", "!tx.key"
+    remove = False
+    if v.startswith("!"):
+        remove = True
+        v = v[1:]
+    col, _, rest = v.partition(".")
+    if col.strip().lower() != "tx":
+        raise SecLangError("setvar only supports the TX collection")
+    if remove:
+        return SetVar(key=parse_macro(rest.strip()), value=None, remove=True)
+    key, eq, value = rest.partition("=")
+    if not eq:
+        value = ""
+    return SetVar(key=parse_macro(key.strip()), value=parse_macro(value))
+
+
+def merge_default_actions(actions, defaults):
+    """[upstream rule_parser.go mergeActions]: default non-metadata,
+    non-disruptive actions are prepended; the default disruptive action is
+    appended only when the rule uses `block`."""
+    res = []
+    da = None
+    for k, v in defaults:
+        t = ACTION_TYPES[k]
+        if t == "disruptive":
+            da = (k, v)
+            continue
+        if t == "metadata":
+            continue
+        res.append((k, v))
+    has_block = False
+    for k, v in actions:
+        if k == "block":
+            has_block = True
+        res.append((k, v))
+    if has_block and da is not None:
+        res.append(da)
+    return res
+
+
+def parse_seclang(text: str) -> WafConfig:
+    cfg = WafConfig()
+    pending_parent: Optional[Rule] = None
+    chain_tail: Optional[Rule] = None
+    for lineno, line in _split_lines(text):
+        if not line or line[0] == "#":
+            continue
+        directive, _, opts = line.partition(" ")
+        if len(opts) >= 3 and opts[0] == '"' and opts[-1] == '"':
+            opts = opts.strip('"')
+        d = directive.lower()
+        if d == "secruleengine":
+            o = opts.strip().lower()
+            cfg.rule_engine = {"on": "On", "off": "Off", "detectiononly": "DetectionOnly"}[o]
+        elif d == "secrequestbodyaccess":
+            cfg.request_body_access = opts.strip().lower() == "on"
+        elif d == "secrequestbodylimit":
+            cfg.request_body_limit = int(opts.strip())
+        elif d == "secrequestbodylimitaction":
+            cfg.request_body_limit_action = opts.strip()
+        elif d == "secdefaultaction":
+            acts = _parse_actions_list(opts)
+            phase = 2
+            for k, v in acts:
+                if k == "phase":
+                    vl = v.lower()
+                    phase = PHASE_NAMES[vl] if vl in PHASE_NAMES else int(v)
+            cfg.default_actions[phase] = acts
+        elif d == "secmarker":
+            r = Rule(id=0, phase=0, line=lineno, secmark=opts.strip().strip('"'))
+            if pending_parent is not None:
+                raise SecLangError("SecMarker inside a chain")
+            cfg.rules.append(r)
+        elif d in ("secrule", "secaction"):
+            rule = Rule(line=lineno)
+            if d == "secrule":
+                rest = opts.lstrip()
+                if rest.startswith('"'):
+                    vars_s, rest = _cut_quoted(rest)
+                else:
+                    vars_s, _, rest = rest.partition(" ")
+                _parse_variables(vars_s, rule)
+                rest = rest.strip()
+                opstr, rest = _cut_quoted(rest)
+                rule.op = _parse_operator(opstr)
+                rest = rest.strip()
+                acts_s = rest.strip('"') if rest else ""
+            else:
+                acts_s = opts
+            actions = _parse_actions_list(acts_s) if acts_s else []
+            is_child = pending_parent is not None
+            if not is_child:
+                phase = 2
+                for k, v in actions:
+                    if k == "phase":
+                        vl = v.lower()
+                        phase = PHASE_NAMES[vl] if vl in PHASE_NAMES else int(v)
+                defaults = cfg.default_actions.get(phase)
+                if defaults:
+                    actions = merge_default_actions(actions, defaults)
+            _apply_actions(rule, actions, is_child)
+            if is_child:
+                rule.parent_id = pending_parent.id
+                rule.phase = pending_parent.phase
+                chain_tail.chain = rule
+                chain_tail = rule
+                if not rule.has_chain_action:
+                    pending_parent = None
+                    chain_tail = None
+            else:
+                if rule.id == 0:
+                    raise SecLangError("rule id is required (line %d)" % lineno)
+                cfg.rules.append(rule)
+                if rule.has_chain_action:
+                    pending_parent = rule
+                    chain_tail = rule
+        elif d in IGNORED_DIRECTIVES or d.startswith("secaudit") or d.startswith("secdebug"):
+            pass
+        else:
+            raise SecLangError("unknown directive %r" % directive)
+    if pending_parent is not None:
+        raise SecLangError("unterminated chain")
+    return cfg
+
+
+# ---------------------------------------------------------------------------
+# Transformations  [upstream internal/transformations/*.go, ModSecurity ports]
+# All operate on bytes.
+# ---------------------------------------------------------------------------
+
+_HEX = b"0123456789abcdefABCDEF"
+
+
+def _ishex(c: int) -> bool:
+    return (48 <= c <= 57) or (65 <= c <= 70) or (97 <= c <= 102)
+
+
+def _x2c(a: int, b: int) -> int:
+    return int(bytes([a, b]), 16)
+
+
+def t_lowercase(d: bytes) -> bytes:
+    # Go strings.ToLower: ASCII fast path, else strings.Map(unicode.ToLower)
+    if all(c < 0x80 for c in d):
+        return d.lower()
+    out = bytearray()
+    i, n = 0, len(d)
+    while i < n:
+        c = d[i]
+        if c < 0x80:
+            out.append(c + 32 if 65 <= c <= 90 else c)
+            i += 1
+            continue
+        r, w = goregex._decode_rune(d, i)
+        if r == 0xFFFD and w == 1:
+            out += "�".encode()
+        else:
+            out += chr(go_to_lower(r)).encode()
+        i += w
+    return bytes(out)
+
+
+def go_to_lower(r: int) -> int:
+    """unicode.ToLower (simple mapping)."""
+    if r == 0x130:
+        return 0x69
+    lo = chr(r).lower()
+    return ord(lo) if len(lo) == 1 else r
+
+
+def t_urldecode(d: bytes) -> bytes:
+    out = bytearray()
+    i, n = 0, len(d)
+    while i < n:
+        c = d[i]
+        if c == 0x25:
+            if i + 2 < n and _ishex(d[i + 1]) and _ishex(d[i + 2]):
+                out.append(_x2c(d[i + 1], d[i + 2]))
+                i += 3
+            else:
+                out.append(c)
+                i += 1
+        else:
+            out.append(0x20 if c == 0x2B else c)
+            i += 1
+    return bytes(out)
+
+
+def t_urldecodeuni(d: bytes) -> bytes:
+    out = bytearray()
+    i, n = 0, len(d)
+    while i < n:
+        c = d[i]
+        if c == 0x25:
+            if i + 1 < n and d[i + 1] in (0x75, 0x55):  # %u
+                if i + 5 < n:
+                    if all(_ishex(d[i + k]) for k in range(2, 6)):
+                        b = _x2c(d[i + 4], d[i + 5])
+                        if 0 < b < 0x5F and d[i + 2] in (0x66, 0x46) and d[i + 3] in (0x66, 0x46):
+                            b += 0x20
+                        out.append(b)
+                        i += 6
+                    else:
+                        out += d[i:i + 2]
+                        i += 2
+                else:
+                    out += d[i:i + 2]
+                    i += 2
+            else:
+                if i + 2 < n and _ishex(d[i + 1]) and _ishex(d[i + 2]):
+                    out.append(_x2c(d[i + 1], d[i + 2]))
+                    i += 3
+                else:
+                    out.append(c)
+                    i += 1
+        else:
+            out.append(0x20 if c == 0x2B else c)
+            i += 1
+    return bytes(out)
+
+
+def _isalnum(c):
+    return 48 <= c <= 57 or 65 <= c <= 90 or 97 <= c <= 122
+
+
+def _strtol_byte(digits: bytes, base: int) -> int:
+    v = int(digits, base)
+    if v > 0x7FFFFFFFFFFFFFFF:  # strtol/ParseInt saturate on overflow
+        v = 0x7FFFFFFFFFFFFFFF
+    return v & 0xFF
+
+
+def t_htmlentitydecode(d: bytes) -> bytes:
+    out = bytearray()
+    i, n = 0, len(d)
+    while i < n:
+        copy = 1
+        if d[i] == 0x26 and i + 1 < n:  # '&'
+            j = i + 1
+            if d[j] == 0x23:  # '#'
+                copy += 1
+                if j + 1 < n:
+                    j += 1
+                    if d[j] in (0x78, 0x58):  # x X
+                        copy += 1
+                        if j + 1 < n:
+                            j += 1
+                            k = j
+                            while j < n and _ishex(d[j]):
+                                j += 1
+                            if j > k:
+                                out.append(_strtol_byte(d[k:j], 16))
+                                i = j + 1 if (j < n and d[j] == 0x3B) else j
+                                continue
+                    else:
+                        k = j
+                        while j < n and 48 <= d[j] <= 57:
+                            j += 1
+                        if j > k:
+                            out.append(_strtol_byte(d[k:j], 10))
+                            i = j + 1 if (j < n and d[j] == 0x3B) else j
+                            continue
+            else:
+                k = j
+                while j < n and _isalnum(d[j]):
+                    j += 1
+                if j > k:
+                    name = d[k:j].lower()
+                    ent = {b"quot": 0x22, b"amp": 0x26, b"lt": 0x3C, b"gt": 0x3E, b"nbsp": 0xA0}.get(name)
+                    if ent is not None:
+                        out.append(ent)
+                        i = j + 1 if (j < n and d[j] == 0x3B) else j
+                        continue
+                    copy = j - k + 1
+        z = 0
+        while z < copy and i < n:
+            out.append(d[i])
+            i += 1
+            z += 1
+    return bytes(out)
+
+
+_WS = {0x20, 0x09, 0x0A, 0x0B, 0x0C, 0x0D}
+
+
+def t_removewhitespace(d: bytes) -> bytes:
+    return bytes(c for c in d if c not in _WS and c != 0xA0)
+
+
+def t_compresswhitespace(d: bytes) -> bytes:
+    out = bytearray()
+    inws = False
+    for c in d:
+        if c in _WS or c == 0xA0:
+            if not inws:
+                out.append(0x20)
+            inws = True
+        else:
+            inws = False
+            out.append(c)
+    return bytes(out)
+
+
+def t_replacecomments(d: bytes) -> bytes:
+    out = bytearray()
+    i, n = 0, len(d)
+    inc = False
+    while i < n:
+        if not inc:
+            if d[i] == 0x2F and i + 1 < n and d[i + 1] == 0x2A:
+                inc = True
+                i += 2
+            else:
+                out.append(d[i])
+                i += 1
+        else:
+            if d[i] == 0x2A and i + 1 < n and d[i + 1] == 0x2F:
+                inc = False
+                i += 2
+                out.append(0x20)
+            else:
+                i += 1
+    if inc:
+        out.append(0x20)
+    return bytes(out)
+
+
+def t_cmdline(d: bytes) -> bytes:
+    out = bytearray()
+    space = False
+    for c in d:
+        if c in (0x22, 0x27, 0x5C, 0x5E):
+            continue
+        if c in (0x20, 0x2C, 0x3B, 0x09, 0x0D, 0x0A):
+            if not space:
+                out.append(0x20)
+                space = True
+            continue
+        if c in (0x2F, 0x28):
+            if space:
+                out.pop()
+                space = False
+            out.append(c)
+            continue
+        out.append(c + 32 if 65 <= c <= 90 else c)
+        space = False
+    return bytes(out)
+
+
+_GO_SPACE = {0x09, 0x0A, 0x0B, 0x0C, 0x0D, 0x20, 0x85, 0xA0, 0x1680, 0x2028, 0x2029,
+             0x202F, 0x205F, 0x3000} | set(range(0x2000, 0x200B))
+
+
+def _trim_left(d: bytes) -> bytes:
+    i = 0
+    while i < len(d):
+        r, w = goregex._decode_rune(d, i)
+        if r == 0xFFFD and w == 1:
+            break
+        if r not in _GO_SPACE:
+            break
+        i += w
+    return d[i:]
+
+
+def _trim_right(d: bytes) -> bytes:
+    end = len(d)
+    while end > 0:
+        # find start of last rune (Go DecodeLastRune)
+        s = end - 1
+        while s > 0 and end - s < 4 and 0x80 <= d[s] <= 0xBF:
+            s -= 1
+        r, w = goregex._decode_rune(d, s)
+        if s + w != end:
+            r, w = 0xFFFD, 1
+            s = end - 1
+        if r not in _GO_SPACE or (r == 0xFFFD):
+            break
+        end = s
+    return d[:end]
+
+
+def t_normalizepath(d: bytes, win: bool = False) -> bytes:
+    if win:
+        d = d.replace(b"\\", b"/")
+    if len(d) < 1:
+        return d
+    clean = _go_path_clean(d)
+    if clean == b".":
+        return b""
+    if d[-1:] == b"/":
+        return clean + b"/"
+    return clean
+
+
+def _go_path_clean(p: bytes) -> bytes:
+    """Go path.Clean."""
+    if p == b"":
+        return b"."
+    rooted = p[:1] == b"/"
+    n = len(p)
+    out = bytearray()
+    r, dotdot = 0, 0
+    if rooted:
+        out.append(0x2F)
+        r, dotdot = 1, 1
+    while r < n:
+        if p[r] == 0x2F:
+            r += 1
+        elif p[r] == 0x2E and (r + 1 == n or p[r + 1] == 0x2F):
+            r += 1
+        elif p[r] == 0x2E and p[r + 1] == 0x2E and (r + 2 == n or p[r + 2] == 0x2F):
+            r += 2
+            if len(out) > dotdot:
+                w = len(out) - 1
+                while w > dotdot and out[w] != 0x2F:
+                    w -= 1
+                del out[w:]
+            elif not rooted:
+                if len(out) > 0:
+                    out.append(0x2F)
+                out += b".."
+                dotdot = len(out)
+        else:
+            if (rooted and len(out) != 1) or (not rooted and len(out) != 0):
+                out.append(0x2F)
+            while r < n and p[r] != 0x2F:
+                out.append(p[r])
+                r += 1
+    if len(out) == 0:
+        return b"."
+    return bytes(out)
+
+
+def _isodigit(c):
+    return 48 <= c <= 55
+
+
+def t_jsdecode(d: bytes) -> bytes:
+    out = bytearray()
+    i, n = 0, len(d)
+    while i < n:
+        if d[i] == 0x5C:
+            if i + 5 < n and d[i + 1] == 0x75 and all(_ishex(d[i + k]) for k in range(2, 6)):
+                b = _x2c(d[i + 4], d[i + 5])
+                if 0 < b < 0x5F and d[i + 2] in (0x66, 0x46) and d[i + 3] in (0x66, 0x46):
+                    b += 0x20
+                out.append(b)
+                i += 6
+            elif i + 3 < n and d[i + 1] == 0x78 and _ishex(d[i + 2]) and _ishex(d[i + 3]):
+                out.append(_x2c(d[i + 2], d[i + 3]))
+                i += 4
+            elif i + 1 < n and _isodigit(d[i + 1]):
+                j = 0
+                buf = bytearray()
+                while i + 1 + j < n and j < 3:
+                    buf.append(d[i + 1 + j])
+                    j += 1
+                    if not (i + 1 + j < n and _isodigit(d[i + 1 + j])):
+                        break
+                if j == 3 and buf[0] > 0x33:
+                    j = 2
+                    buf = buf[:2]
+                out.append(int(bytes(buf), 8) & 0xFF)
+                i += 1 + j
+            elif i + 1 < n:
+                c = d[i + 1]
+                c = {0x61: 7, 0x62: 8, 0x66: 12, 0x6E: 10, 0x72: 13, 0x74: 9, 0x76: 11}.get(c, c)
+                out.append(c)
+                i += 2
+            else:
+                out += d[i:]
+                i = n
+        else:
+            out.append(d[i])
+            i += 1
+    return bytes(out)
+
+
+TRANSFORM_FNS = {
+    "lowercase": t_lowercase,
+    "urldecode": t_urldecode,
+    "urldecodeuni": t_urldecodeuni,
+    "htmlentitydecode": t_htmlentitydecode,
+    "removenulls": lambda d: d.replace(b"\x00", b""),
+    "replacenulls": lambda d: d.replace(b"\x00", b" "),
+    "removewhitespace": t_removewhitespace,
+    "compresswhitespace": t_compresswhitespace,
+    "replacecomments": t_replacecomments,
+    "cmdline": t_cmdline,
+    "length": lambda d: str(len(d)).encode(),
+    "trim": lambda d: _trim_right(_trim_left(d)),
+    "trimleft": _trim_left,
+    "trimright": _trim_right,
+    "normalizepath": t_normalizepath,
+    "normalisepath": t_normalizepath,
+    "normalizepathwin": lambda d: t_normalizepath(d, True),
+    "normalisepathwin": lambda d: t_normalizepath(d, True),
+    "jsdecode": t_jsdecode,
+}
+
+
+# ---------------------------------------------------------------------------
+# Request model, URI parsing  [upstream corazawaf/transaction.go ProcessURI,
+# Go net/url Parse/String, coraza internal/url ParseQuery]
+# ---------------------------------------------------------------------------
+
+
+@dataclass
+class Request:
+    method: bytes
+    uri: bytes
+    proto: bytes = b"HTTP/1.1"
+    headers: List[Tuple[bytes, bytes]] = field(default_factory=list)
+    body: bytes = b""
+
+
+class UnsupportedInput(ValueError):
+    """Input outside the engine's supported subset (flagged, not guessed)."""
+
+
+def query_unescape(s: bytes) -> bytes:
+    """Lenient %XX / '+' decoding (invalid escapes kept verbatim)."""
+    out = bytearray()
+    i, n = 0, len(s)
+    while i < n:
+        c = s[i]
+        if c == 0x25 and i + 2 < n and _ishex(s[i + 1]) and _ishex(s[i + 2]):
+            out.append(_x2c(s[i + 1], s[i + 2]))
+            i += 3
+        elif c == 0x2B:
+            out.append(0x20)
+            i += 1
+        else:
+            out.append(c)
+            i += 1
+    return bytes(out)
+
+
+def parse_query(q: bytes, sep: int = 0x26):
+    """[upstream internal/url ParseQuery] -> list of (key, value) in order."""
+    out = []
+    while q:
+        i = q.find(bytes([sep]))
+        if i >= 0:
+            key, q = q[:i], q[i + 1:]
+        else:
+            key, q = q, b""
+        if key == b"":
+            continue
+        value = b""
+        j = key.find(b"=")
+        if j >= 0:
+            key, value = key[:j], key[j + 1:]
+        out.append((query_unescape(key), query_unescape(value)))
+    return out
+
+
+def _go_should_escape_path(c: int) -> bool:
+    if 65 <= c <= 90 or 97 <= c <= 122 or 48 <= c <= 57:
+        return False
+    if c in b"-_.~":
+        return False
+    if c in b"$&+,/:;=?@":
+        return c == 0x3F
+    return True
+
+
+def _go_escape_path(s: bytes) -> bytes:
+    out = bytearray()
+    for c in s:
+        if _go_should_escape_path(c):
+            out += b"%" + ("%02X" % c).encode()
+        else:
+            out.append(c)
+    return bytes(out)
+
+
+def _go_valid_encoded_path(s: bytes) -> bool:
+    for c in s:
+        if c in b"!$&'()*+,;=:@[]%":
+            continue
+        if _go_should_escape_path(c):
+            return False
+    return True
+
+
+def _go_unescape_path(s: bytes):
+    """net/url unescape(s, encodePath): strict; returns None on bad escape."""
+    out = bytearray()
+    i, n = 0, len(s)
+    while i < n:
+        if s[i] == 0x25:
+            if i + 2 >= n or not _ishex(s[i + 1]) or not _ishex(s[i + 2]):
+                return None
+            out.append(_x2c(s[i + 1], s[i + 2]))
+            i += 3
+        else:
+            out.append(s[i])
+            i += 1
+    return bytes(out)
+
+
+def process_uri(uri: bytes):
+    """Returns dict of URI-derived variables + ARGS_GET list.
+
+    Supported subset: origin-form ('/' not followed by '/') and '*'.
+    Anything else raises UnsupportedInput (the GPU engine flags the same
+    requests with GI_REQ_UNSUPPORTED_URI).
+    """
+    v = {"REQUEST_URI_RAW": uri}
+    u = uri
+    h = u.find(b"#")
+    if h >= 0:
+        u = u[:h]
+    args = []
+    ctl = any(c < 0x20 or c == 0x7F for c in u)
+    if ctl:
+        v["REQUEST_URI"] = u
+        path = u
+        query = b""
+    elif u == b"*":
+        v["REQUEST_URI"] = b"*"
+        path = b"*"
+        query = b""
+    else:
+        if not u.startswith(b"/") or u.startswith(b"//"):
+            raise UnsupportedInput("non origin-form request URI")
+        q = u.find(b"?")
+        force_q = False
+        if u.endswith(b"?") and u.count(b"?") == 1:
+            force_q = True
+            rest, query = u[:-1], b""
+        elif q >= 0:
+            rest, query = u[:q], u[q + 1:]
+        else:
+            rest, query = u, b""
+        p = _go_unescape_path(rest)
+        if p is None:
+            # url.Parse error -> raw uri, no GET args
+            v["REQUEST_URI"] = u
+            path = u
+            query = b""
+        else:
+            args = parse_query(query)
+            if _go_escape_path(p) == rest or _go_valid_encoded_path(rest):
+                esc = rest
+            else:
+                esc = _go_escape_path(p)
+            s = esc
+            if force_q or query:
+                s += b"?" + query
+            v["REQUEST_URI"] = s
+            path = p
+    v["REQUEST_FILENAME"] = path
+    v["QUERY_STRING"] = query
+    off = path.rfind(b"/")
+    if off != -1 and len(path) > off + 1:
+        v["REQUEST_BASENAME"] = path[off + 1:]
+    else:
+        v["REQUEST_BASENAME"] = path
+    return v, args
+
+
+def parse_cookies(value: bytes):
+    """[upstream] cookie header parsing: split ';', trim, cut '='."""
+    out = []
+    raw = value.strip(b" \t\r\n\v\f")
+    while raw:
+        part, sep, raw = raw.partition(b";")
+        part = part.strip(b" \t\r\n\v\f")
+        if not part:
+            continue
+        name, _, val = part.partition(b"=")
+        out.append((name, val))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Transaction + rule evaluation  [upstream corazawaf/{transaction,rulegroup,rule}.go]
+# ---------------------------------------------------------------------------
+
+
+def go_atoi(s: bytes):
+    """strconv.Atoi -> (value, ok)."""
+    m = re.fullmatch(rb"[+-]?[0-9]+", s)
+    if not m:
+        return 0, False
+    v = int(s)
+    if v > 2**63 - 1 or v < -2**63:
+        return (2**63 - 1 if v > 0 else -2**63), False
+    return v, True
+
+
+def _wrap64(v: int) -> int:
+    v &= (1 << 64) - 1
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+@dataclass
+class Verdict:
+    rule_id: int = 0
+    status: int = 0
+    action: str = ""
+    phase: int = 0
+    matched: List[int] = field(default_factory=list)
+    tx: Dict[str, bytes] = field(default_factory=dict)
+    unsupported: bool = False
+
+
+class Transaction:
+    def __init__(self, cfg: WafConfig):
+        self.cfg = cfg
+        self.rule_engine = cfg.rule_engine
+        self.body_access = cfg.request_body_access
+        self.interruption: Optional[Tuple[int, int, str, int]] = None
+        self.matched: List[int] = []
+        self.tx: Dict[bytes, bytes] = {}       # lowercase key -> value
+        self.skip_after = ""
+        self.skip = 0
+        self.removed: List[Tuple[int, int]] = []
+        self.single: Dict[str, bytes] = {k: b"" for k in SINGLE_VARS}
+        self.single["REQBODY_ERROR"] = b"0"
+        self.single["MULTIPART_STRICT_ERROR"] = b"0"
+        self.maps: Dict[str, List[Tuple[bytes, bytes]]] = {
+            "ARGS_GET": [], "ARGS_POST": [], "REQUEST_HEADERS": [],
+            "REQUEST_COOKIES": [], "MATCHED_VARS": []}
+        self.body = b""
+        self.phase = 0
+
+    # -- request population -------------------------------------------------
+    def process_request(self, req: Request):
+        v, args = process_uri(req.uri)
+        self.single.update(v)
+        self.single["REQUEST_METHOD"] = req.method
+        self.single["REQUEST_PROTOCOL"] = req.proto
+        self.single["REQUEST_LINE"] = req.method + b" " + req.uri + b" " + req.proto
+        self.maps["ARGS_GET"] = list(args)
+        for k, val in req.headers:
+            if k == b"":
+                continue
+            self.maps["REQUEST_HEADERS"].append((k, val))
+            kl = k.lower()
+            if kl == b"content-type":
+                vl = val.lower()
+                if vl.startswith(b"application/x-www-form-urlencoded"):
+                    self.single["REQBODY_PROCESSOR"] = b"URLENCODED"
+                elif vl.startswith(b"multipart/form-data"):
+                    self.single["REQBODY_PROCESSOR"] = b"MULTIPART"
+            elif kl == b"cookie":
+                self.maps["REQUEST_COOKIES"] += parse_cookies(val)
+        self.body = req.body
+
+    # -- collections ----------------------------------------------------------
+    def _tx_items(self):
+        return [(k, v) for k, v in self.tx.items()]
+
+    def _collection(self, src):
+        if src == "TX":
+            return self._tx_items()
+        return self.maps[src]
+
+    def get_field(self, rv: RuleVariable):
+        """tx.GetField: returns list of (key, value)."""
+        name = rv.name
+        if name in SINGLE_VARS:
+            vals = [(b"", self.single.get(name, b""))]
+        else:
+            if name in MAP_VARS:
+                srcs, ci = MAP_VARS[name]
+                names = False
+            else:
+                srcs, ci = NAMES_VARS[name]
+                names = True
+            items = []
+            for s in srcs:
+                items += self._collection(s)
+            if rv.key_rx is not None:
+                items = [(k, v) for k, v in items
+                         if rv.key_rx.match_string(k.lower() if ci else k)]
+            elif rv.key:
+                kk = rv.key.encode()
+                if ci:
+                    items = [(k, v) for k, v in items if k.lower() == kk.lower()]
+                else:
+                    items = [(k, v) for k, v in items if k == kk]
+            if names:
+                items = [(k, k) for k, v in items]
+            vals = items
+        if rv.exceptions:
+            kept = []
+            for k, v in vals:
+                lk = k.lower()
+                drop = False
+                for ek, erx in rv.exceptions:
+                    if erx is not None:
+                        if erx.match_string(lk):
+                            drop = True
+                            break
+                    elif ek.encode() == lk:
+                        drop = True
+                        break
+                if not drop:
+                    kept.append((k, v))
+            vals = kept
+        if rv.count:
+            vals = [(b"", str(len(vals)).encode())]
+        return vals
+
+    # -- macros ---------------------------------------------------------------
+    def expand(self, parts) -> bytes:
+        out = b""
+        for p in parts:
+            if isinstance(p, str):
+                out += p.encode()
+                continue
+            _, name, key = p
+            if name == "TX":
+                out += self.tx.get(key.encode(), b"")
+            elif name in SINGLE_VARS:
+                out += self.single.get(name, b"")
+            elif name in MAP_VARS:
+                srcs, ci = MAP_VARS[name]
+                for s in srcs:
+                    hit = [v for k, v in self._collection(s)
+                           if (k.lower() == key.encode() if ci else k == key.encode())]
+                    if hit:
+                        out += hit[0]
+                        break
+            else:
+                pass
+        return out
+
+    # -- operators ------------------------------------------------------------
+    def eval_op(self, rule: Rule, value: bytes) -> bool:
+        op = rule.op
+        n = op.name
+        if n == "rx":
+            if rule.capture:
+                m = op.rx.find_string_submatch(value)
+                if m is None:
+                    res = False
+                else:
+                    for i, c in enumerate(m):
+                        if i == 9:
+                            break
+                        self.tx[str(i).encode()] = c
+                    res = True
+            else:
+                res = op.rx.match_string(value)
+        elif n == "pm":
+            low = value.lower()
+            if rule.capture:
+                caps = _pm_find_all(op.phrases, low, value)
+                for i, c in enumerate(caps[:10]):
+                    self.tx[str(i).encode()] = c
+                res = len(caps) > 0
+            else:
+                res = any(p in low for p in op.phrases)
+        elif n == "contains":
+            res = self.expand(op.macro) in value
+        elif n == "containsword":
+            w = self.expand(op.macro)
+            res = _contains_word(value, w)
+        elif n == "streq":
+            res = value == self.expand(op.macro)
+        elif n == "beginswith":
+            res = value.startswith(self.expand(op.macro))
+        elif n == "endswith":
+            res = value.endswith(self.expand(op.macro))
+        elif n == "within":
+            res = value in self.expand(op.macro)
+        elif n in ("eq", "ge", "gt", "le", "lt"):
+            a, ok = go_atoi(self.expand(op.macro))
+            if not ok:
+                a = 0
+            b, ok = go_atoi(value)
+            if not ok:
+                b = 0
+            res = {"eq": b == a, "ge": b >= a, "gt": b > a, "le": b <= a, "lt": b < a}[n]
+        elif n == "unconditionalmatch":
+            res = True
+        elif n == "nomatch":
+            res = False
+        elif n == "validatebyterange":
+            res = any(not op.byte_ok[c] for c in value)
+        elif n == "validateurlencoding":
+            res = _invalid_url_encoding(value)
+        elif n == "validateutf8encoding":
+            try:
+                value.decode("utf-8")
+                res = False
+            except UnicodeDecodeError:
+                res = True
+        else:
+            raise AssertionError(n)
+        return (not res) if op.negate else res
+
+    # -- actions --------------------------------------------------------------
+    def run_setvar(self, sv: SetVar):
+        key = self.expand(sv.key).lower()
+        if sv.remove:
+            self.tx.pop(key, None)
+            return
+        value = self.expand(sv.value)
+        cur = self.tx.get(key, b"")
+        if len(value) == 0:
+            self.tx[key] = b""
+        elif value[:1] == b"+" or value[:1] == b"-":
+            me, ok = go_atoi(cur)
+            if not ok:
+                me = 0
+            vv, ok = go_atoi(value[1:])
+            if not ok:
+                return
+            r = me + vv if value[:1] == b"+" else me - vv
+            self.tx[key] = str(_wrap64(r)).encode()
+        else:
+            self.tx[key] = value
+
+    def run_ctl(self, name: str, val: str):
+        if name == "ruleremovebyid":
+            for part in val.split(" "):
+                part = part.strip()
+                if not part:
+                    continue
+                if "-" in part:
+                    a, b = part.split("-", 1)
+                    self.removed.append((int(a), int(b)))
+                else:
+                    self.removed.append((int(part), int(part)))
+        elif name == "ruleengine":
+            self.rule_engine = {"on": "On", "off": "Off", "detectiononly": "DetectionOnly"}[val.lower()]
+        elif name == "requestbodyprocessor":
+            self.single["REQBODY_PROCESSOR"] = val.upper().encode()
+        elif name == "requestbodyaccess":
+            self.body_access = val.lower() == "on"
+        elif name == "forcerequestbodyvariable":
+            pass
+
+    def run_nondisruptive(self, rule: Rule):
+        for kind, obj in rule.nondisruptive_order:
+            if kind == "setvar":
+                self.run_setvar(obj)
+            elif kind == "ctl":
+                self.run_ctl(*obj)
+
+    def transform(self, rule: Rule, value: bytes) -> bytes:
+        for t in rule.transforms:
+            value = TRANSFORM_FNS[t](value)
+        return value
+
+    def do_evaluate(self, rule: Rule) -> int:
+        """Rule.doEvaluate -> number of matched values (0 = no match)."""
+        nmatch = 0
+        if rule.op is None:
+            nmatch = 1
+            self.run_nondisruptive(rule)
+        else:
+            if rule.multimatch:
+                raise UnsupportedInput("multiMatch")
+            for rv in rule.variables:
+                for k, v in self.get_field(rv):
+                    tv = self.transform(rule, v)
+                    if self.eval_op(rule, tv):
+                        nmatch += 1
+                        self.single["MATCHED_VAR"] = tv
+                        self.single["MATCHED_VAR_NAME"] = (rv.name + (":" if k else "")).encode() + k
+                        self.run_nondisruptive(rule)
+        if nmatch == 0:
+            return 0
+        if rule.parent_id == 0:
+            nr = rule.chain
+            while nr is not None:
+                if self.do_evaluate(nr) == 0:
+                    return 0
+                nr = nr.chain
+            # flow + disruptive actions (disruptive only with engine On)
+            if rule.skip_after:
+                self.skip_after = rule.skip_after
+            if rule.skip:
+                self.skip = rule.skip
+            if rule.disruptive in ("deny", "drop", "redirect") and self.rule_engine == "On":
+                self.interruption = (rule.id, rule.status, rule.disruptive, self.phase)
+            if rule.id != 0:
+                self.matched.append(rule.id)
+        return nmatch
+
+    def eval_phase(self, phase: int):
+        """RuleGroup.Eval."""
+        if self.rule_engine == "Off":
+            return
+        self.phase = phase
+        for r in self.cfg.rules:
+            if self.interruption is not None:
+                break
+            if r.phase != 0 and r.phase != phase:
+                continue
+            if r.id != 0 and any(a <= r.id <= b for a, b in self.removed):
+                continue
+            if self.skip_after:
+                if r.secmark == self.skip_after:
+                    self.skip_after = ""
+                continue
+            if self.skip > 0:
+                self.skip -= 1
+                continue
+            if r.secmark:
+                continue
+            self.single["MATCHED_VAR"] = b""
+            self.single["MATCHED_VAR_NAME"] = b""
+            self.do_evaluate(r)
+
+    def process_request_body(self):
+        if self.rule_engine == "Off":
+            return
+        if self.interruption is not None:
+            return
+        if self.body_access and len(self.body) > 0:
+            if len(self.body) > self.cfg.request_body_limit:
+                raise UnsupportedInput("request body over SecRequestBodyLimit")
+            self.single["REQUEST_BODY_LENGTH"] = str(len(self.body)).encode()
+            rbp = self.single.get("REQBODY_PROCESSOR", b"")
+            if rbp == b"URLENCODED":
+                self.single["REQUEST_BODY"] = self.body
+                self.maps["ARGS_POST"] = parse_query(self.body)
+            elif rbp == b"":
+                pass
+            else:
+                raise UnsupportedInput("body processor %s" % rbp.decode())
+        self.eval_phase(2)
+
+
+def _pm_find_all(phrases, low: bytes, orig: bytes):
+    """Leftmost-longest non-overlapping matches (aho-corasick MatchKind)."""
+    out = []
+    i = 0
+    n = len(low)
+    while i < n:
+        best = None
+        for p in phrases:
+            if low.startswith(p, i):
+                if best is None or len(p) > len(best):
+                    best = p
+        if best is not None:
+            out.append(orig[i:i + len(best)])
+            i += len(best)
+        else:
+            i += 1
+    return out
+
+
+def _contains_word(value: bytes, w: bytes) -> bool:
+    if not w:
+        return True
+    i = value.find(w)
+    while i >= 0:
+        before = i == 0 or not (_isalnum(value[i - 1]) or value[i - 1] == 0x5F)
+        j = i + len(w)
+        after = j >= len(value) or not (_isalnum(value[j]) or value[j] == 0x5F)
+        if before and after:
+            return True
+        i = value.find(w, i + 1)
+    return False
+
+
+def _invalid_url_encoding(d: bytes) -> bool:
+    i, n = 0, len(d)
+    while i < n:
+        if d[i] == 0x25:
+            if i + 2 >= n:
+                return True
+            if _ishex(d[i + 1]) and _ishex(d[i + 2]):
+                i += 3
+            else:
+                return True
+        else:
+            i += 1
+    return False
+
+
+DEFAULT_TX_EXPORTS = (
+    "blocking_inbound_anomaly_score", "inbound_anomaly_score_pl1",
+    "inbound_anomaly_score_pl2", "inbound_anomaly_score_pl3",
+    "inbound_anomaly_score_pl4", "detection_inbound_anomaly_score",
+    "anomaly_score", "0",
+)
+
+
+def inspect(cfg: WafConfig, req: Request, exports=DEFAULT_TX_EXPORTS) -> Verdict:
+    """One full request: phase 1 then phase 2 (ProcessRequestHeaders/Body)."""
+    tx = Transaction(cfg)
+    out = Verdict()
+    try:
+        tx.process_request(req)
+        tx.eval_phase(1)
+        if tx.interruption is None:
+            tx.process_request_body()
+    except UnsupportedInput:
+        out.unsupported = True
+        return out
+    if tx.interruption is not None:
+        out.rule_id, out.status, out.action, out.phase = tx.interruption
+    out.matched = list(tx.matched)
+    for name in exports:
+        out.tx[name] = tx.tx.get(name.encode(), b"")
+    return out
+
+
+def compile_ruleset(configmaps: List[str]) -> WafConfig:
+    """ruleset_controller.go:158-181: validate each ConfigMap, then join with
+    '\\n' and compile the aggregate."""
+    for text in configmaps:
+        parse_seclang(text)
+    return parse_seclang("\n".join(configmaps))
