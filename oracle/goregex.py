@@ -283,6 +283,7 @@ class _Parser:
                 continue
             self._last_rep = False
             atom = self.parse_atom(box)
+            self._last_rep = False
             if atom is not None:
                 items.append(atom)
         items = [x for x in items if x is not None]
@@ -312,6 +313,9 @@ class _Parser:
         m = re.match(r"\{(\d+)(,(\d*))?\}", self.s[self.i:])
         if not m:
             return None
+        for g in (m.group(1), m.group(3)):
+            if g and len(g) > 1 and g[0] == "0":
+                return None  # Go parseInt: no leading zeros
         lo = int(m.group(1))
         if m.group(2) is None:
             hi = lo

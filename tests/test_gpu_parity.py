@@ -1,0 +1,79 @@
+"""GPU parity: the HIP engine vs the CPU oracle (bit-exact verdicts).
+
+* the reference's own KATs (tests/golden/kats.json);
+* config 1 (config/samples RuleSet) over seeded synthetic traffic;
+* the CRS-shaped PL1 ruleset over seeded synthetic traffic.
+"""
+import json
+import os
+
+import pytest
+
+import gpuinspect
+import traffic
+from oracle import compare, coraza
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+KATS = json.load(open(os.path.join(GOLDEN, "kats.json")))
+
+pytestmark = pytest.mark.gpu
+
+
+def _tx(r):
+    t = gpuinspect.Transaction()
+    t.process_uri(r["uri"], r["method"], r["proto"])
+    for k, v in r["headers"]:
+        t.add_request_header(k, v)
+    t.write_request_body(r["body"])
+    return t
+
+
+@pytest.mark.parametrize("sc", KATS["scenarios"], ids=[s["name"] for s in KATS["scenarios"]])
+def test_gpu_kats(sc):
+    rs = gpuinspect.Ruleset(gpuinspect.aggregate_configmaps(sc["configmaps"]))
+    eng = gpuinspect.Engine(rs)
+    res = eng.inspect([_tx(r) for r in sc["requests"]])
+    for i, r in enumerate(sc["requests"]):
+        it = res.interruption(i)
+        status = it["status"] if it else 200
+        assert status == r["expect_status"], (r["source"], r["uri"], it)
+        m = res.matched_rules(i)
+        for x in r["expect_matched"]:
+            assert x in m, (r["source"], m)
+        for x in r["expect_not_matched"]:
+            assert x not in m, (r["source"], m)
+
+
+def _parity(text, batch, n_check=None):
+    rs = gpuinspect.Ruleset(text)
+    eng = gpuinspect.Engine(rs, matched_cap=128)
+    res = eng.inspect(batch)
+    cfg = coraza.parse_seclang(text)
+    idx = range(batch.n_req) if n_check is None else range(min(n_check, batch.n_req))
+    orc = compare.oracle_verdicts(cfg, batch, rs.exports, idx)
+    bad = compare.compare(res, orc)
+    assert not bad, bad
+    return res
+
+
+def test_gpu_parity_samples_c1():
+    text = open(os.path.join(GOLDEN, "samples_ruleset.conf")).read()
+    batch = traffic.TrafficGen(traffic.SEED).batch(3000, attack_rate=0.3)
+    res = _parity(text, batch)
+    assert int(res.verdicts["match_cnt"].astype(bool).sum()) > 50  # attacks were seen
+
+
+def test_gpu_parity_edge_uris():
+    text = open(os.path.join(GOLDEN, "samples_ruleset.conf")).read()
+    uris = [b"/", b"*", b"/a b?x=1", b"/%zz?q=evilmonkey", b"/p%41th?a=%u0041&b=%uFF1Cscript%uFF1E",
+            b"/x?", b"/x??a=1", b"/x#frag?q=evilmonkey", b"//double?q=1", b"http://h/x",
+            b"/\x01ctl?q=evilmonkey", b"/caf\xc3\xa9?q=<script>alert(1)</script>",
+            b"/?q=select+*+from+users", b"/?=evilmonkey&&&a", b"/?q=%3Cscript%3E", b"/\xff\xfe?x=1"]
+    txs = []
+    for u in uris:
+        t = gpuinspect.Transaction(method=b"GET", uri=u)
+        t.add_request_header("Host", "x")
+        t.add_request_header("Cookie", " a=1; b ; =c;d=evilmonkey ")
+        txs.append(t)
+    _parity(text, gpuinspect.pack(txs))

@@ -1,0 +1,79 @@
+"""CPU-side checks of the product library (no GPU needed): the C-ABI loads
+and exports every symbol include/gpuinspect.h declares, the SecLang compiler
+accepts/rejects what the oracle accepts/rejects, and the @rx DFA compiler
+agrees with the oracle's Go-regexp restatement on random inputs."""
+import json
+import os
+import random
+import re
+
+import pytest
+
+import gpuinspect
+from oracle import coraza, goregex
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def test_header_symbols_exported():
+    lib = gpuinspect.load_library()
+    hdr = open(os.path.join(ROOT, "include", "gpuinspect.h")).read()
+    decl = set(re.findall(r"\b(gi_[a-z_0-9]+)\s*\(", hdr))
+    assert decl, "no declarations parsed"
+    assert decl == set(gpuinspect.EXPORTED_SYMBOLS), decl ^ set(gpuinspect.EXPORTED_SYMBOLS)
+    for name in decl:
+        assert hasattr(lib, name), name
+
+
+def test_kat_rulesets_compile():
+    kats = json.load(open(os.path.join(GOLDEN, "kats.json")))
+    for sc in kats["scenarios"]:
+        text = gpuinspect.aggregate_configmaps(sc["configmaps"])
+        rs = gpuinspect.Ruleset(text)
+        assert rs.info["n_rules"] >= 1
+
+
+BAD = [
+    ('SecRule ARGS "@rx (" "id:1,deny"', "parse"),
+    ('SecRule ARGS "@rx a" "id:1,bogus"', "parse"),
+    ('SecRule NOPE "@rx a" "id:1"', "parse"),
+    ('SecRule ARGS "@rx a" "phase:2,deny"', "parse"),  # no id
+    ('SecFoo bar', "parse"),
+    ('SecRule ARGS "@rx a" "id:1,chain"', "parse"),   # unterminated chain
+]
+
+
+@pytest.mark.parametrize("text,kind", BAD)
+def test_compile_rejects_like_oracle(text, kind):
+    with pytest.raises(coraza.SecLangError):
+        coraza.parse_seclang(text)
+    with pytest.raises(gpuinspect.SecLangError) as e:
+        gpuinspect.Ruleset(text)
+    assert e.value.code == gpuinspect.GI_EPARSE
+
+
+def test_unsupported_is_flagged_not_guessed():
+    with pytest.raises(gpuinspect.SecLangError) as e:
+        gpuinspect.Ruleset('SecRule ARGS "@detectSQLi" "id:1,deny"')
+    assert e.value.code == gpuinspect.GI_EUNSUPPORTED
+
+
+PATTERNS = [
+    r"(?i:(\b(select|union|insert|update|delete|drop)\b.*\b(from|into|where|table)\b))",
+    r"(?i:<script[^>]*>.*?</script>|javascript:|onerror\s*=|onload\s*=|<iframe)",
+    r"^(?:GET|HEAD)$", r"\bfoo\b", r"a.b", r"(?i)k", r"[^\x00-\x7f]", r"(?m)$\n^", r".{3}",
+    r"(?:^|[\\/])\.\.(?:[\\/]|$)", r"\Aab|cd\z", r"(?i)[a-z]+s$", r"\d+\s*=\s*\d+", r"(a|b){2,4}c",
+]
+
+
+@pytest.mark.parametrize("pat", PATTERNS)
+def test_regex_dfa_matches_oracle(pat):
+    rnd = random.Random(hash(pat) & 0xFFFF)
+    alpha = b"abcxzsSkK select from or = '\"\n<>/\\.-_0129\xc3\xa9\xe2\x84\xaa\xff\xc3\x41\xe1\x80"
+    g = goregex.compile_go("(?sm)" + pat)
+    for _ in range(800):
+        s = bytes(rnd.choice(alpha) for _ in range(rnd.randint(0, 20)))
+        rc, _ = gpuinspect.selftest_regex("(?sm)" + pat, s)
+        assert rc in (0, 1)
+        assert rc == int(g.match_string(s)), (pat, s)
