@@ -221,7 +221,8 @@ const std::map<std::string, int>& collection_ids() {
       {"REQUEST_HEADERS", V_REQUEST_HEADERS}, {"REQUEST_COOKIES", V_REQUEST_COOKIES},
       {"TX", V_TX}, {"ARGS_GET_NAMES", V_ARGS_GET_NAMES}, {"ARGS_POST_NAMES", V_ARGS_POST_NAMES},
       {"ARGS_NAMES", V_ARGS_NAMES}, {"REQUEST_HEADERS_NAMES", V_REQUEST_HEADERS_NAMES},
-      {"REQUEST_COOKIES_NAMES", V_REQUEST_COOKIES_NAMES}};
+      {"REQUEST_COOKIES_NAMES", V_REQUEST_COOKIES_NAMES}, {"XML", V_XML}, {"FILES", V_FILES},
+      {"FILES_NAMES", V_FILES_NAMES}};
   return m;
 }
 // variables the oracle knows but this engine does not evaluate yet
@@ -361,7 +362,8 @@ bool transform_code(const std::string& t, uint8_t* code) {
       {"cmdline", T_CMDLINE}, {"length", T_LENGTH}, {"trim", T_TRIM}, {"trimleft", T_TRIMLEFT},
       {"trimright", T_TRIMRIGHT}, {"normalizepath", T_NORMALIZEPATH},
       {"normalisepath", T_NORMALIZEPATH}, {"normalizepathwin", T_NORMALIZEPATHWIN},
-      {"normalisepathwin", T_NORMALIZEPATHWIN}, {"jsdecode", T_JSDECODE}};
+      {"normalisepathwin", T_NORMALIZEPATHWIN}, {"jsdecode", T_JSDECODE},
+      {"utf8tounicode", T_UTF8TOUNICODE}};
   auto it = m.find(t);
   if (it == m.end()) return false;
   *code = it->second;
@@ -886,7 +888,13 @@ struct Lower {
         a.a = lower(nd.ctl_value) == "on" ? 1 : 0;
         P->acts.push_back(a);
       }
-      // forcerequestbodyvariable: accepted, no effect on the supported processors
+      else if (nd.ctl_name == "forcerequestbodyvariable") {
+        DAction a{};
+        a.kind = A_CTL_FORCE_BODY;
+        std::string v = lower(nd.ctl_value);
+        a.a = (v == "on" || v == "true" || v == "1") ? 1 : 0;
+        P->acts.push_back(a);
+      }
     }
     d->act_count = (uint32_t)P->acts.size() - d->act_begin;
   }

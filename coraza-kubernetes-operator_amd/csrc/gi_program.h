@@ -43,6 +43,9 @@ enum VarId : uint8_t {
   V_ARGS_NAMES,
   V_REQUEST_HEADERS_NAMES,
   V_REQUEST_COOKIES_NAMES,
+  V_XML,  // XML body processor output: never populated (XML bodies are flagged unsupported)
+  V_FILES,        // multipart output: never populated (multipart bodies are flagged unsupported)
+  V_FILES_NAMES,
 };
 
 // Collection field kinds emitted by the collect stage.
@@ -89,6 +92,7 @@ enum TCode : uint8_t {
   T_NORMALIZEPATH,
   T_NORMALIZEPATHWIN,
   T_JSDECODE,
+  T_UTF8TOUNICODE,
 };
 
 enum Disruptive : uint8_t { D_NONE = 0, D_DENY = 1, D_DROP = 2, D_REDIRECT = 3, D_PASS = 4 };
@@ -102,6 +106,7 @@ enum ActKind : uint8_t {
   A_CTL_RULE_ENGINE,
   A_CTL_BODY_PROCESSOR,
   A_CTL_BODY_ACCESS,
+  A_CTL_FORCE_BODY,
 };
 
 enum EngineMode : uint8_t { ENGINE_OFF = 0, ENGINE_ON = 1, ENGINE_DETECTION_ONLY = 2 };

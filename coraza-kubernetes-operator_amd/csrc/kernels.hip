@@ -625,9 +625,39 @@ __device__ int64_t t_jsdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t
   return o;
 }
 
+// t:utf8toUnicode: valid multi-byte UTF-8 -> %uXXXX (lowercase hex, >= 4
+// digits); ASCII and invalid bytes copied.  [upstream utf8toUnicode.go]
+__device__ int64_t t_utf8tounicode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  uint32_t o = 0, i = 0;
+  const char* hx = "0123456789abcdef";
+  while (i < n) {
+    if (o + 8 > cap) return -1;
+    uint8_t c = s[i];
+    if (c < 0x80) {
+      d[o++] = c;
+      i++;
+      continue;
+    }
+    uint32_t w;
+    uint32_t r = decode_rune(s, n, i, &w);
+    if (r == 0xFFFD && w == 1) {
+      d[o++] = c;
+      i++;
+      continue;
+    }
+    d[o++] = '%';
+    d[o++] = 'u';
+    int nd = r > 0xFFFFF ? 6 : r > 0xFFFF ? 5 : 4;
+    for (int k = nd - 1; k >= 0; k--) d[o++] = hx[(r >> (4 * k)) & 15];
+    i += w;
+  }
+  return o;
+}
+
 __device__ int64_t apply_transform(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d,
                                    uint32_t cap) {
   switch (code) {
+    case T_UTF8TOUNICODE: return t_utf8tounicode(s, n, d, cap);
     case T_LOWERCASE: return t_lowercase(P, s, n, d, cap);
     case T_URLDECODE: return t_urldecode(s, n, d, cap);
     case T_URLDECODEUNI: return t_urldecodeuni(s, n, d, cap);
@@ -662,6 +692,7 @@ struct Tx {
   int64_t removed[8][2];
   uint32_t nremoved;
   uint8_t engine, body_access, body_proc, phase;
+  uint8_t force_body;
   int32_t skip_after;
   int32_t skip;
   int32_t int_rule, int_status;
@@ -1052,6 +1083,9 @@ __device__ void run_actions(Tx& t, const DRule& R) {
       case A_CTL_BODY_ACCESS:
         t.body_access = (uint8_t)a.a;
         break;
+      case A_CTL_FORCE_BODY:
+        t.force_body = (uint8_t)a.a;
+        break;
     }
   }
 }
@@ -1379,6 +1413,7 @@ __global__ void __launch_bounds__(128) k_inspect(DProgram P, DBatch B) {
     t.engine = P.rule_engine;
     t.body_access = P.body_access;
     t.body_proc = BP_NONE;
+    t.force_body = 0;
     t.phase = 0;
     t.skip_after = -1;
     t.skip = 0;
@@ -1446,6 +1481,10 @@ __global__ void __launch_bounds__(128) k_inspect(DProgram P, DBatch B) {
           } else {
             uint8_t* lb = tx_alloc(t, 24);
             if (lb) t.single[S_REQUEST_BODY_LENGTH] = {lb, go_itoa((int64_t)bn, lb)};
+            if (t.force_body && t.body_proc == BP_NONE) {
+              t.body_proc = BP_URLENCODED;
+              t.single[S_REQBODY_PROCESSOR] = {CS_URLENCODED, 10};
+            }
             if (t.body_proc == BP_URLENCODED) {
               t.single[S_REQUEST_BODY] = {D + rq.body.off, bn};
               parse_query(t, D + rq.body.off, bn, FK_ARG_POST);

@@ -155,7 +155,10 @@ class TrafficGen:
             q = self._args(na, att) if na else b""
             uri = path + (b"?" + q if q else b"")
             if post[i]:
-                body = self._urlencoded_body()
+                # an attack request carries its payload in the query (above)
+                # or, half of the time, in one body argument instead
+                body_attack = bool(attack[i]) and rng.random() < 0.5
+                body = self._urlencoded_body(body_attack)
                 parts += [b"POST", uri, b"HTTP/1.1", body]
                 k = self._headers(parts, path)
                 parts += [b"Content-Type", b"application/x-www-form-urlencoded", b"Content-Length",
@@ -166,18 +169,21 @@ class TrafficGen:
                 nh[i] = self._headers(parts, path)
         return parts, nh
 
-    def _urlencoded_body(self):
+    def _urlencoded_body(self, attack: bool):
         rng = self.rng
         target = int(np.exp(rng.uniform(np.log(4096), np.log(65536))))
         chunks = []
         size = 0
         while size < target:
             na = int(rng.integers(4, 16))
-            att = int(rng.integers(0, na)) if rng.random() < 0.05 else -1
-            c = self._args(na, att)
+            c = self._args(na, -1)
             chunks.append(c)
             size += len(c) + 1
-        return b"&".join(chunks)[:target].rstrip(b"%")
+        body = b"&".join(chunks)[:target].rstrip(b"%")
+        if attack:
+            k = int(rng.integers(0, len(chunks)))
+            body = b"&".join(chunks[:k] + [self._args(1, 0)] + chunks[k:])[:target + 300]
+        return body
 
     def batch(self, n: int, post_frac: float = 0.0, attack_rate: float = 0.05) -> "gpuinspect.PackedBatch":
         parts, nh = self.gen(n, post_frac, attack_rate)

@@ -69,6 +69,12 @@ MAP_VARS = {
     "REQUEST_COOKIES": (("REQUEST_COOKIES",), False),
     "TX": (("TX",), True),
     "MATCHED_VARS": (("MATCHED_VARS",), True),
+    # populated only by the XML body processor (not implemented: such
+    # requests are flagged unsupported), so always empty here
+    "XML": (("XML",), False),
+    # multipart file collections: populated only by the MULTIPART processor
+    # (not implemented: such requests are flagged unsupported)
+    "FILES": (("FILES",), False),
 }
 NAMES_VARS = {
     "ARGS_GET_NAMES": (("ARGS_GET",), False),
@@ -77,6 +83,7 @@ NAMES_VARS = {
     "REQUEST_HEADERS_NAMES": (("REQUEST_HEADERS",), True),
     "REQUEST_COOKIES_NAMES": (("REQUEST_COOKIES",), False),
     "MATCHED_VARS_NAMES": (("MATCHED_VARS",), True),
+    "FILES_NAMES": (("FILES",), False),
 }
 ALL_VARS = SINGLE_VARS | set(MAP_VARS) | set(NAMES_VARS)
 
@@ -400,7 +407,7 @@ TRANSFORMS_SUPPORTED = {
     "removenulls", "replacenulls", "removewhitespace", "compresswhitespace",
     "replacecomments", "cmdline", "length", "trim", "trimleft", "trimright",
     "normalizepath", "normalisepath", "normalizepathwin", "normalisepathwin",
-    "jsdecode",
+    "jsdecode", "utf8tounicode",
 }
 
 
@@ -932,7 +939,32 @@ def t_jsdecode(d: bytes) -> bytes:
     return bytes(out)
 
 
+def t_utf8tounicode(d: bytes) -> bytes:
+    """ModSecurity utf8_unicode_inplace_ex restated: every valid multi-byte
+    UTF-8 sequence becomes %uXXXX (lowercase hex, >= 4 digits); ASCII and
+    invalid bytes are copied.  [upstream utf8toUnicode.go, unverified]"""
+    if all(c < 0x80 for c in d):
+        return d
+    out = bytearray()
+    i, n = 0, len(d)
+    while i < n:
+        c = d[i]
+        if c < 0x80:
+            out.append(c)
+            i += 1
+            continue
+        r, w = goregex._decode_rune(d, i)
+        if r == 0xFFFD and w == 1:
+            out.append(c)
+            i += 1
+            continue
+        out += b"%u" + (b"%04x" % r)
+        i += w
+    return bytes(out)
+
+
 TRANSFORM_FNS = {
+    "utf8tounicode": t_utf8tounicode,
     "lowercase": t_lowercase,
     "urldecode": t_urldecode,
     "urldecodeuni": t_urldecodeuni,
@@ -1179,7 +1211,8 @@ class Transaction:
         self.single["MULTIPART_STRICT_ERROR"] = b"0"
         self.maps: Dict[str, List[Tuple[bytes, bytes]]] = {
             "ARGS_GET": [], "ARGS_POST": [], "REQUEST_HEADERS": [],
-            "REQUEST_COOKIES": [], "MATCHED_VARS": []}
+            "REQUEST_COOKIES": [], "MATCHED_VARS": [], "XML": [], "FILES": []}
+        self.force_body = False
         self.body = b""
         self.phase = 0
 
@@ -1391,7 +1424,7 @@ class Transaction:
         elif name == "requestbodyaccess":
             self.body_access = val.lower() == "on"
         elif name == "forcerequestbodyvariable":
-            pass
+            self.force_body = val.lower() in ("on", "true", "1")
 
     def run_nondisruptive(self, rule: Rule):
         for kind, obj in rule.nondisruptive_order:
@@ -1476,6 +1509,12 @@ class Transaction:
                 raise UnsupportedInput("request body over SecRequestBodyLimit")
             self.single["REQUEST_BODY_LENGTH"] = str(len(self.body)).encode()
             rbp = self.single.get("REQBODY_PROCESSOR", b"")
+            if self.force_body:
+                # [upstream transaction.go ProcessRequestBody]: forced variable
+                # with no processor -> URLENCODED
+                if rbp == b"":
+                    rbp = b"URLENCODED"
+                self.single["REQBODY_PROCESSOR"] = rbp
             if rbp == b"URLENCODED":
                 self.single["REQUEST_BODY"] = self.body
                 self.maps["ARGS_POST"] = parse_query(self.body)

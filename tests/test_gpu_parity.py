@@ -77,3 +77,40 @@ def test_gpu_parity_edge_uris():
         t.add_request_header("Cookie", " a=1; b ; =c;d=evilmonkey ")
         txs.append(t)
     _parity(text, gpuinspect.pack(txs))
+
+
+CRS = os.path.join(ROOT, "rulesets", "crs_pl1.conf")
+
+
+def test_gpu_parity_crs_pl1_get():
+    text = open(CRS).read()
+    batch = traffic.TrafficGen(traffic.SEED + 1).batch(1500, attack_rate=0.3)
+    res = _parity(text, batch)
+    assert int((res.verdicts["action"] != 0).sum()) > 50
+
+
+def test_gpu_parity_crs_pl1_mixed_post():
+    text = open(CRS).read()
+    batch = traffic.TrafficGen(traffic.SEED + 2).batch(200, post_frac=0.5, attack_rate=0.3)
+    _parity(text, batch)
+
+
+def test_gpu_parity_crs_pl1_kat_payloads():
+    """Every attack payload of the generator, raw and encoded, in every
+    position the CRS-shaped rules look at."""
+    text = open(CRS).read()
+    txs = []
+    for p in traffic.ATTACKS + [b"<script>alert(1)</script>", b"1 UNION SELECT username FROM users"]:
+        for enc in (False, True):
+            q = traffic._quote(p, enc)
+            t = gpuinspect.Transaction(method=b"GET", uri=b"/search?q=" + q)
+            t.add_request_header("Host", "www.example.com")
+            t.add_request_header("User-Agent", p)
+            t.add_request_header("Cookie", b"sid=" + q)
+            txs.append(t)
+            t2 = gpuinspect.Transaction(method=b"POST", uri=b"/form")
+            t2.add_request_header("Host", "www.example.com")
+            t2.add_request_header("Content-Type", "application/x-www-form-urlencoded")
+            t2.write_request_body(b"a=1&" + q + b"=x&b=" + q)
+            txs.append(t2)
+    _parity(text, gpuinspect.pack(txs))
