@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <sstream>
 #include <unordered_map>
 
@@ -628,6 +629,13 @@ struct Lower {
     h.nr_cnt = (uint32_t)d.nranges.size() / 3;
     P->nranges.insert(P->nranges.end(), d.nranges.begin(), d.nranges.end());
     h.byte_mode = d.byte_mode ? 1 : 0;
+    h.multi = d.multi ? 1 : 0;
+    if (d.multi) {
+      h.combo_off = (uint32_t)P->u8pool.size();
+      P->u8pool.insert(P->u8pool.end(), d.cls_combo.begin(), d.cls_combo.end());
+      h.acc_off = (uint32_t)P->u64pool.size();
+      P->u64pool.insert(P->u64pool.end(), d.acc.begin(), d.acc.end());
+    }
     if (!d.byte_mode && h.nr_cnt > 0) {
       uint32_t c0 = d.nranges[2];
       bool uni = true;
@@ -899,6 +907,224 @@ struct Lower {
     d->act_count = (uint32_t)P->acts.size() - d->act_begin;
   }
 
+  // ---------------------------------------------------- phase-A scan plan
+  struct PatEntry {
+    uint32_t slot;
+    bool negate;
+    int kind;  // 0 regex, 1 phrases (fold), 2 literal (case-sensitive)
+    std::string rx;
+    std::vector<std::string> phrases;
+  };
+  struct GroupBuild {
+    DGroup g;
+    std::vector<PatEntry> pats;
+    std::vector<DScanVal> vals;
+  };
+  std::vector<GroupBuild> gbuild;
+  std::map<std::string, size_t> gindex;
+
+  static bool immutable_single(int sid) {
+    return sid == S_REQUEST_METHOD || sid == S_REQUEST_PROTOCOL || sid == S_REQUEST_URI ||
+           sid == S_REQUEST_URI_RAW || sid == S_REQUEST_LINE || sid == S_REQUEST_FILENAME ||
+           sid == S_REQUEST_BASENAME || sid == S_QUERY_STRING;
+  }
+
+  // Returns the hit slot, or -1 when the link stays interpreter-only.
+  int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
+    if (!r.has_op) return -1;
+    const std::string& n = r.op_name;
+    bool scannable = n == "rx" || n == "pm" || n == "validatebyterange" || n == "validateurlencoding" ||
+                     n == "validateutf8encoding" || (n == "contains" && r.op_arg.find("%{") == std::string::npos);
+    if (!scannable) return -1;
+    bool bodydep = false;
+    for (auto& v : r.vars) {
+      if (v.count) return -1;
+      int sid = single_id(v.name);
+      if (sid >= 0 && !immutable_single(sid)) return -1;
+      if (sid < 0 && v.name == "TX") return -1;
+      if (v.name == "ARGS" || v.name == "ARGS_POST" || v.name == "ARGS_NAMES" || v.name == "ARGS_POST_NAMES")
+        bodydep = true;
+    }
+    const int32_t slot = (int32_t)P->n_hit_slots++;
+    if (bodydep) *flags |= RF_BODYDEP;
+    const DOp& o = P->ops[d.op];
+    const DVarRef* vrs = &P->vars[d.var_begin];
+    for (uint32_t vi = 0; vi < d.var_count; vi++) {
+      const DVarRef& vr = vrs[vi];
+      DGroup g{};
+      g.key_dfa = -1;
+      uint8_t mask = 0;
+      bool names = false;
+      if (vr.var < S_COUNT) {
+        g.src = SRC_SINGLE;
+        g.single = vr.var;
+      } else {
+        g.src = SRC_FIELDS;
+        switch (vr.var) {
+          case V_ARGS_GET: mask = 1 << FK_ARG_GET; break;
+          case V_ARGS: mask = 1 << FK_ARG_GET; break;  // ARG_POST fields only exist after phase 1
+          case V_REQUEST_HEADERS: mask = 1 << FK_HEADER; break;
+          case V_REQUEST_COOKIES: mask = 1 << FK_COOKIE; break;
+          case V_ARGS_GET_NAMES: mask = 1 << FK_ARG_GET; names = true; break;
+          case V_ARGS_NAMES: mask = 1 << FK_ARG_GET; names = true; break;
+          case V_REQUEST_HEADERS_NAMES: mask = 1 << FK_HEADER; names = true; break;
+          case V_REQUEST_COOKIES_NAMES: mask = 1 << FK_COOKIE; names = true; break;
+          default: break;  // ARGS_POST*, XML, FILES*: no values before the body phase
+        }
+        if (!mask) continue;
+        g.kind_mask = mask;
+        g.names = names;
+        g.key_mode = vr.key_mode;
+        g.ci = vr.ci;
+        g.key_dfa = vr.key_dfa;
+        g.key_off = vr.key_off;
+        g.key_len = vr.key_len;
+        g.exc_begin = vr.exc_begin;
+        g.exc_count = vr.exc_count;
+      }
+      g.tchain_off = d.tchain_off;
+      g.tchain_len = d.tchain_len;
+      // group identity: source, key filter, exclusions, chain
+      std::string key;
+      key.append((const char*)&g.src, 6);
+      if (g.key_mode == 1) key.append((const char*)&P->strpool[g.key_off], g.key_len);
+      key.push_back('|');
+      key.append(std::to_string(g.key_dfa));
+      key.push_back('|');
+      for (uint32_t e = 0; e < g.exc_count; e++) {
+        const DExc& x = P->excs[g.exc_begin + e];
+        key.append(std::to_string(x.dfa));
+        key.push_back(':');
+        key.append((const char*)&P->strpool[x.off], x.len);
+        key.push_back(',');
+      }
+      key.push_back('|');
+      key.append((const char*)&P->tchains[d.tchain_off], d.tchain_len);
+      auto it = gindex.find(key);
+      if (it == gindex.end()) {
+        it = gindex.emplace(key, gbuild.size()).first;
+        GroupBuild gb;
+        gb.g = g;
+        gbuild.push_back(gb);
+      }
+      GroupBuild& gb = gbuild[it->second];
+      if (o.kind == OP_VALIDATE_BYTE_RANGE || o.kind == OP_VALIDATE_URL_ENCODING || o.kind == OP_VALIDATE_UTF8) {
+        DScanVal sv{};
+        sv.kind = o.kind;
+        sv.negate = o.negate;
+        sv.slot = (uint32_t)slot;
+        for (int k = 0; k < 8; k++) sv.bits[k] = o.bits[k];
+        gb.vals.push_back(sv);
+        continue;
+      }
+      PatEntry pe;
+      pe.slot = (uint32_t)slot;
+      pe.negate = o.negate != 0;
+      if (o.kind == OP_RX) {
+        pe.kind = 0;
+        pe.rx = "(?sm)" + r.op_arg;
+      } else if (o.kind == OP_PM) {
+        pe.kind = 1;
+        std::string la = lower(r.op_arg);
+        size_t pos = 0;
+        while (pos <= la.size()) {
+          size_t sp = la.find(' ', pos);
+          if (sp == std::string::npos) sp = la.size();
+          if (sp > pos) pe.phrases.push_back(la.substr(pos, sp - pos));
+          pos = sp + 1;
+        }
+      } else {  // @contains literal
+        pe.kind = 2;
+        pe.phrases.push_back(r.op_arg);
+      }
+      gb.pats.push_back(pe);
+    }
+    return slot;
+  }
+
+  void emit_sdfa(GroupBuild& gb, const Dfa& d, const std::vector<const PatEntry*>& pes, std::vector<DScanDfa>* out) {
+    DScanDfa s{};
+    s.dfa = add_dfa(d);
+    s.pat_begin = (uint32_t)P->pats.size();
+    s.n_pat = (uint32_t)pes.size();
+    for (size_t k = 0; k < pes.size(); k++) {
+      P->pats.push_back(DPat{pes[k]->slot});
+      if (pes[k]->negate) s.neg_mask |= 1ull << k;
+    }
+    if (d.multi) P->n_union_dfas++;
+    out->push_back(s);
+    (void)gb;
+  }
+
+  void finish_groups() {
+    const uint32_t kUnionCap = 4096;
+    for (auto& gb : gbuild) {
+      std::vector<DScanDfa> sd;
+      std::vector<std::unique_ptr<Regex>> owned;
+      std::vector<const Regex*> cur;
+      std::vector<const PatEntry*> curp;
+      Dfa curd;
+      std::string err;
+      auto flush = [&]() {
+        if (cur.empty()) return;
+        emit_sdfa(gb, curd, curp, &sd);
+        cur.clear();
+        curp.clear();
+      };
+      for (auto& pe : gb.pats) {
+        auto re = std::make_unique<Regex>();
+        bool ok;
+        if (pe.kind == 0) {
+          ok = re_parse(pe.rx, re.get(), &err);
+          if (!ok) perr("invalid regex " + pe.rx + ": " + err);
+        } else {
+          ok = phrases_to_regex(pe.phrases, pe.kind == 1, re.get());
+        }
+        if (!ok) {
+          // non-ASCII phrase: its own byte-mode automaton
+          Dfa d;
+          if (!build_phrase_dfa(pe.phrases, pe.kind == 1, &d, &err, cap)) unsup(err);
+          emit_sdfa(gb, d, {&pe}, &sd);
+          continue;
+        }
+        cur.push_back(re.get());
+        curp.push_back(&pe);
+        Dfa trial;
+        if (cur.size() <= 64 && build_union_dfa(cur, &trial, &err, kUnionCap)) {
+          curd = std::move(trial);
+          owned.push_back(std::move(re));
+          continue;
+        }
+        cur.pop_back();
+        curp.pop_back();
+        flush();
+        cur.push_back(re.get());
+        curp.push_back(&pe);
+        if (build_union_dfa(cur, &trial, &err, kUnionCap)) {
+          curd = std::move(trial);
+          owned.push_back(std::move(re));
+          continue;
+        }
+        // too large for a union automaton: single sticky DFA
+        Dfa single;
+        if (!build_regex_dfa(*re, &single, &err, cap)) unsup("regex " + pe.rx + ": " + err);
+        emit_sdfa(gb, single, {&pe}, &sd);
+        cur.clear();
+        curp.clear();
+        owned.push_back(std::move(re));
+      }
+      flush();
+      DGroup g = gb.g;
+      g.sdfa_begin = (uint32_t)P->sdfas.size();
+      g.sdfa_count = (uint32_t)sd.size();
+      P->sdfas.insert(P->sdfas.end(), sd.begin(), sd.end());
+      g.val_begin = (uint32_t)P->svals.size();
+      g.val_count = (uint32_t)gb.vals.size();
+      P->svals.insert(P->svals.end(), gb.vals.begin(), gb.vals.end());
+      if (g.sdfa_count + g.val_count) P->groups.push_back(g);
+    }
+  }
+
   uint32_t rule(const IrRule& r, bool child) {
     DRule d{};
     d.id = r.id;
@@ -926,6 +1152,7 @@ struct Lower {
     }
     d.tchain_len = (uint32_t)P->tchains.size() - d.tchain_off;
     actions(r, &d);
+    d.hit_slot = plan(r, d, &d.flags);
     P->rules.push_back(d);
     return (uint32_t)P->rules.size() - 1;
   }
@@ -954,6 +1181,8 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
         prev = ci;
       }
     }
+    L.finish_groups();
+    if (out->u64pool.empty()) out->u64pool.push_back(0);
     out->rule_engine = waf.engine == "On" ? ENGINE_ON : waf.engine == "Off" ? ENGINE_OFF : ENGINE_DETECTION_ONLY;
     out->body_access = waf.body_access;
     out->body_limit = (uint64_t)waf.body_limit;

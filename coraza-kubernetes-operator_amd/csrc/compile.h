@@ -26,6 +26,13 @@ struct Program {
   std::vector<uint32_t> nranges;
   std::vector<uint8_t> strpool;
   std::vector<uint32_t> slot_names;  // (off, len) pairs into strpool
+  std::vector<uint64_t> u64pool;     // union-automaton accept masks
+  std::vector<DGroup> groups;        // phase-A scan plan
+  std::vector<DScanDfa> sdfas;
+  std::vector<DPat> pats;
+  std::vector<DScanVal> svals;
+  uint32_t n_hit_slots = 0;
+  uint32_t n_union_dfas = 0;
   std::vector<int32_t> exports;
   std::vector<std::string> export_names;
   uint32_t n_slots = 0, n_markers = 0;

@@ -9,7 +9,8 @@
 namespace gi {
 
 // Per-request scratch layout (computed by the host from request lengths when
-// the batch is staged; see runtime.cpp stage()).
+// the batch is staged; see runtime.cpp gi_stage_batch).  Region =
+// [256 B ReqHdr][cap_f fields][TX slots][cap_b bytes][2 x cap_t][2 x cap_mt].
 struct ReqLayout {
   uint64_t base;   // byte offset of the request's region in DBatch.scratch
   uint32_t cap_f;  // field records
@@ -29,8 +30,17 @@ struct DBatch {
   gi_verdict* verdicts;
   uint32_t* matched;
   unsigned long long* tally;  // gi_tally as 6 counters
+  uint32_t* hits;             // phase-A hit words [ceil(n_hit_slots/32)][n_req]
+  uint8_t* tscratch;          // k_scan transformation buffers (2 x tcap per resident thread)
+  uint32_t tcap;
 };
 
-void launch_inspect(const DProgram& P, const DBatch& B, hipStream_t stream);
+// Resident thread count of k_scan on the current device (grid-stride width).
+uint32_t scan_resident_threads();
+
+// k_collect -> k_scan -> k_eval on `stream`; ev (optional) = 2 events recorded
+// after k_collect and after k_scan.
+void launch_pipeline(const DProgram& P, const DBatch& B, uint32_t scan_threads, hipStream_t stream,
+                     hipEvent_t* ev);
 
 }  // namespace gi

@@ -97,7 +97,12 @@ enum TCode : uint8_t {
 
 enum Disruptive : uint8_t { D_NONE = 0, D_DENY = 1, D_DROP = 2, D_REDIRECT = 3, D_PASS = 4 };
 
-enum RuleFlags : uint8_t { RF_CHILD = 1, RF_MARKER = 2, RF_CAPTURE = 4 };
+enum RuleFlags : uint8_t {
+  RF_CHILD = 1,
+  RF_MARKER = 2,
+  RF_CAPTURE = 4,
+  RF_BODYDEP = 8,  // targets can see ARGS_POST: phase-A bits ignored once a body was parsed
+};
 
 enum ActKind : uint8_t {
   A_SETVAR = 1,
@@ -128,9 +133,53 @@ struct DRule {
   uint32_t act_begin, act_count;
   uint8_t phase;
   uint8_t disruptive;
-  uint8_t flags;
+  uint8_t flags;        // RuleFlags
   uint8_t _pad;
-  uint32_t _pad2[2];
+  int32_t hit_slot;     // phase-A hit bit (-1: evaluated by the interpreter only)
+  uint32_t _pad2;
+};
+
+// ------------------------------------------------------ phase-A scan plan
+// A scan group = one value source x key filter x exclusions x transformation
+// chain.  Every phase-A-eligible (rule link, target) pair contributes one
+// pattern to the group of its target; the group's patterns are packed into
+// union automata so each transformed value is scanned once per automaton.
+enum SrcKind : uint8_t { SRC_SINGLE = 1, SRC_FIELDS = 2 };
+
+struct DGroup {
+  uint8_t src;        // SrcKind
+  uint8_t single;     // SingleId (SRC_SINGLE)
+  uint8_t kind_mask;  // 1 << FieldKind (SRC_FIELDS)
+  uint8_t names;      // test the key instead of the value
+  uint8_t key_mode;   // 0 none, 1 literal, 2 regex
+  uint8_t ci;         // case-insensitive keys
+  uint8_t _pad[2];
+  int32_t key_dfa;
+  uint32_t key_off, key_len;
+  uint32_t exc_begin, exc_count;
+  uint32_t tchain_off, tchain_len;
+  uint32_t sdfa_begin, sdfa_count;  // DScanDfa
+  uint32_t val_begin, val_count;    // DScanVal
+};
+
+struct DScanDfa {
+  int32_t dfa;        // multi (union) or single sticky automaton
+  uint32_t pat_begin; // DPat, n_pat entries (bit k of the match mask)
+  uint32_t n_pat;
+  uint32_t _pad;
+  uint64_t neg_mask;  // patterns whose operator is negated
+};
+
+struct DPat {
+  uint32_t slot;      // hit slot of the rule link
+};
+
+struct DScanVal {     // @validateByteRange / @validateUrlEncoding / @validateUtf8Encoding
+  uint8_t kind;
+  uint8_t negate;
+  uint16_t _pad;
+  uint32_t slot;
+  uint32_t bits[8];
 };
 
 struct DVarRef {
@@ -192,7 +241,9 @@ struct DDfa {
   uint8_t byte_mode;
   uint8_t nonascii_uniform;  // every rune >= 0x80 maps to nonascii_cls
   uint8_t nonascii_cls;
-  uint8_t _pad;
+  uint8_t multi;             // union automaton (see regex.h)
+  uint32_t combo_off;        // u8 pool: per-class combo (multi)
+  uint32_t acc_off;          // u64 pool: 5 masks per state (multi)
 };
 
 // Everything the kernels need, as device pointers (filled by the context).
@@ -213,6 +264,13 @@ struct DProgram {
   const uint8_t* strpool;
   const uint32_t* lower_pairs;  // unicode.ToLower table (rune, lower) pairs
   const uint32_t* slot_names;   // (off, len) into strpool per TX slot
+  const uint64_t* u64pool;      // union-automaton accept masks
+  const DGroup* groups;
+  const DScanDfa* sdfas;
+  const DPat* pats;
+  const DScanVal* svals;
+  uint32_t n_groups;
+  uint32_t n_hit_slots;
   uint32_t n_lower_pairs;
   uint32_t n_top;
   uint32_t n_slots;

@@ -688,7 +688,10 @@ struct Tx {
   uint32_t cap_mt;
   uint8_t* txa;
   uint32_t ntx, cap_tx;
-  Str single[S_COUNT];
+  Str* single;               // ReqHdr::single (per-request, in HBM scratch)
+  const uint32_t* hits;      // phase-A hit words [slot/32][n_req]
+  uint32_t n_req, req;
+  bool has_post;             // ARGS_POST fields exist (phase-A bits of RF_BODYDEP links void)
   int64_t removed[8][2];
   uint32_t nremoved;
   uint8_t engine, body_access, body_proc, phase;
@@ -1246,6 +1249,12 @@ __device__ inline uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const
 // Rule.doEvaluate for one link -> number of matched values.
 __device__ uint32_t eval_rule(Tx& t, const DRule& R) {
   const DProgram& P = *t.P;
+  // phase-A filter: a clear hit bit proves no value matches (exact); a set
+  // bit (match or "maybe") falls through to the full evaluation below.
+  if (R.hit_slot >= 0 && !((R.flags & RF_BODYDEP) && t.has_post)) {
+    const uint32_t w = t.hits[(uint64_t)(R.hit_slot >> 5) * t.n_req + t.req];
+    if (!((w >> (R.hit_slot & 31)) & 1u)) return 0;
+  }
   if (R.op < 0) {
     run_actions(t, R);
     return 1;
@@ -1375,88 +1384,111 @@ __device__ void eval_phase(Tx& t, uint8_t phase) {
   }
 }
 
-// ---------------------------------------------------------------- kernel
-__global__ void __launch_bounds__(128) k_inspect(DProgram P, DBatch B) {
-  __shared__ unsigned long long red[6][2];
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (threadIdx.x < 12) (&red[0][0])[threadIdx.x] = 0;
-  __syncthreads();
-  unsigned long long my[6] = {0, 0, 0, 0, 0, 0};
-  if (r < B.n_req) {
-    const gi_request rq = B.reqs[r];
-    const ReqLayout L = B.layout[r];
-    uint8_t* base = B.scratch + L.base;
-    Tx t;
-    t.P = &P;
-    t.cap_f = L.cap_f;
-    t.fields = (Field*)base;
-    uint64_t off = (uint64_t)L.cap_f * sizeof(Field);
-    t.slots = (Slot*)(base + off);
-    off += ((uint64_t)P.n_slots * sizeof(Slot) + 15) & ~15ull;
-    t.bytes = base + off;
-    t.cap_b = L.cap_b;
-    off += (L.cap_b + 15) & ~15u;
-    t.t0 = base + off;
-    off += (L.cap_t + 15) & ~15u;
-    t.t1 = base + off;
-    off += (L.cap_t + 15) & ~15u;
-    t.cap_t = L.cap_t;
-    t.mt = base + off;
-    t.cap_mt = L.cap_mt;
-    off += (L.cap_mt + 15) & ~15u;
-    t.txa = base + off;
-    t.cap_tx = L.cap_mt;
-    t.nf = 0;
-    t.nb = 0;
-    t.ntx = 0;
-    t.nremoved = 0;
-    t.engine = P.rule_engine;
-    t.body_access = P.body_access;
-    t.body_proc = BP_NONE;
-    t.force_body = 0;
-    t.phase = 0;
-    t.skip_after = -1;
-    t.skip = 0;
-    t.interrupted = false;
-    t.int_rule = 0;
-    t.int_status = 0;
-    t.int_action = 0;
-    t.int_phase = 0;
-    t.flags = 0;
-    t.nmatched = 0;
-    t.mout = B.matched + (uint64_t)r * B.mcap;
-    t.mcap = B.mcap;
-    for (uint32_t s = 0; s < P.n_slots; s++) t.slots[s].state = 0;
-    for (uint32_t s = 0; s < S_COUNT; s++) t.single[s] = {CS_ZERO, 0};
-    t.single[S_REQBODY_ERROR] = {CS_ZERO, 1};
-    t.single[S_MULTIPART_STRICT_ERROR] = {CS_ZERO, 1};
+// ------------------------------------------------------ per-request state
+// Written by k_collect at the start of the request's HBM scratch region and
+// read by k_scan / k_eval.
+struct ReqHdr {
+  uint32_t nf;          // fields so far: [ARG_GET | HEADER | COOKIE | ARG_POST]
+  uint32_t nb;          // bytes arena used
+  uint16_t n_get, n_hdr, n_ck, flags;
+  uint8_t body_proc;
+  uint8_t _pad[7];
+  Str single[S_COUNT];
+};
+static_assert(sizeof(ReqHdr) <= 256, "ReqHdr must fit its 256-byte slot");
 
-    const uint8_t* D = B.data;
-    Str method{D + rq.method.off, rq.method.len};
-    Str uri{D + rq.uri.off, rq.uri.len};
-    Str proto{D + rq.proto.off, rq.proto.len};
-    t.single[S_REQUEST_METHOD] = method;
-    t.single[S_REQUEST_PROTOCOL] = proto;
-    // REQUEST_LINE = "METHOD URI PROTO"
-    uint8_t* ln = tx_alloc(t, method.n + uri.n + proto.n + 2);
-    if (ln) {
-      uint32_t k = 0;
-      for (uint32_t i = 0; i < method.n; i++) ln[k++] = method.p[i];
-      ln[k++] = ' ';
-      for (uint32_t i = 0; i < uri.n; i++) ln[k++] = uri.p[i];
-      ln[k++] = ' ';
-      for (uint32_t i = 0; i < proto.n; i++) ln[k++] = proto.p[i];
-      t.single[S_REQUEST_LINE] = {ln, k};
-    }
-    uint64_t scanned = (uint64_t)method.n + uri.n + proto.n + rq.body.len;
-    bool ok = process_uri(t, uri.p, uri.n);
+struct Region {
+  ReqHdr* hdr;
+  Field* fields;
+  Slot* slots;
+  uint8_t *bytes, *t0, *t1, *mt, *txa;
+  uint32_t cap_f, cap_b, cap_t, cap_mt;
+};
+
+__device__ inline Region region_of(const DProgram& P, const DBatch& B, uint32_t r) {
+  const ReqLayout L = B.layout[r];
+  uint8_t* base = B.scratch + L.base;
+  Region g;
+  g.hdr = (ReqHdr*)base;
+  uint64_t off = 256;
+  g.fields = (Field*)(base + off);
+  off += (uint64_t)L.cap_f * sizeof(Field);
+  g.slots = (Slot*)(base + off);
+  off += ((uint64_t)P.n_slots * sizeof(Slot) + 15) & ~15ull;
+  g.bytes = base + off;
+  off += (L.cap_b + 15) & ~15u;
+  g.t0 = base + off;
+  off += (L.cap_t + 15) & ~15u;
+  g.t1 = base + off;
+  off += (L.cap_t + 15) & ~15u;
+  g.mt = base + off;
+  off += (L.cap_mt + 15) & ~15u;
+  g.txa = base + off;
+  g.cap_f = L.cap_f;
+  g.cap_b = L.cap_b;
+  g.cap_t = L.cap_t;
+  g.cap_mt = L.cap_mt;
+  return g;
+}
+
+__device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
+  t.P = &P;
+  t.fields = g.fields;
+  t.cap_f = g.cap_f;
+  t.slots = g.slots;
+  t.bytes = g.bytes;
+  t.cap_b = g.cap_b;
+  t.t0 = g.t0;
+  t.t1 = g.t1;
+  t.cap_t = g.cap_t;
+  t.mt = g.mt;
+  t.cap_mt = g.cap_mt;
+  t.txa = g.txa;
+  t.cap_tx = g.cap_mt;
+  t.single = g.hdr->single;
+}
+
+// ------------------------------------------------ stage 1: k_collect
+// ProcessURI + AddRequestHeader* for one request per thread.  Fields are
+// grouped by kind so each scan group walks only its own range.
+__global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B.n_req) return;
+  const gi_request rq = B.reqs[r];
+  Region g = region_of(P, B, r);
+  Tx t;
+  tx_bind(t, P, g);
+  t.nf = 0;
+  t.nb = 0;
+  t.flags = 0;
+  t.body_proc = BP_NONE;
+  for (uint32_t s = 0; s < S_COUNT; s++) t.single[s] = {CS_ZERO, 0};
+  t.single[S_REQBODY_ERROR] = {CS_ZERO, 1};
+  t.single[S_MULTIPART_STRICT_ERROR] = {CS_ZERO, 1};
+  const uint8_t* D = B.data;
+  Str method{D + rq.method.off, rq.method.len};
+  Str uri{D + rq.uri.off, rq.uri.len};
+  Str proto{D + rq.proto.off, rq.proto.len};
+  t.single[S_REQUEST_METHOD] = method;
+  t.single[S_REQUEST_PROTOCOL] = proto;
+  uint8_t* ln = tx_alloc(t, method.n + uri.n + proto.n + 2);
+  if (ln) {
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < method.n; i++) ln[k++] = method.p[i];
+    ln[k++] = ' ';
+    for (uint32_t i = 0; i < uri.n; i++) ln[k++] = uri.p[i];
+    ln[k++] = ' ';
+    for (uint32_t i = 0; i < proto.n; i++) ln[k++] = proto.p[i];
+    t.single[S_REQUEST_LINE] = {ln, k};
+  }
+  const bool ok = process_uri(t, uri.p, uri.n);
+  const uint32_t n_get = t.nf;
+  if (ok) {
     for (uint32_t h = 0; h < rq.hdr_count; h++) {
       const gi_header hd = B.headers[rq.hdr_begin + h];
-      scanned += hd.name.len + hd.value.len;
-      if (!ok) continue;
+      if (hd.name.len == 0) continue;
       const uint8_t* k = D + hd.name.off;
       const uint8_t* v = D + hd.value.off;
-      if (hd.name.len == 0) continue;
       add_field(t, FK_HEADER, k, hd.name.len, v, hd.value.len);
       if (hd.name.len == 12 && starts_ci(k, 12, "content-type")) {
         if (starts_ci(v, hd.value.len, "application/x-www-form-urlencoded")) {
@@ -1466,13 +1498,242 @@ __global__ void __launch_bounds__(128) k_inspect(DProgram P, DBatch B) {
           t.body_proc = BP_MULTIPART;
           t.single[S_REQBODY_PROCESSOR] = {CS_MULTIPART, 9};
         }
-      } else if (hd.name.len == 6 && starts_ci(k, 6, "cookie")) {
-        parse_cookies(t, v, hd.value.len);
       }
     }
-    if (ok && !(t.flags & GI_REQ_ERROR_MASK)) {
+  }
+  const uint32_t n_hdr = t.nf - n_get;
+  if (ok) {
+    for (uint32_t h = 0; h < rq.hdr_count; h++) {
+      const gi_header hd = B.headers[rq.hdr_begin + h];
+      if (hd.name.len == 6 && starts_ci(D + hd.name.off, 6, "cookie"))
+        parse_cookies(t, D + hd.value.off, hd.value.len);
+    }
+  }
+  ReqHdr* H = g.hdr;
+  H->nf = t.nf;
+  H->nb = t.nb;
+  H->n_get = (uint16_t)n_get;
+  H->n_hdr = (uint16_t)n_hdr;
+  H->n_ck = (uint16_t)(t.nf - n_get - n_hdr);
+  H->flags = t.flags | ((t.nf > 0xFFFF) ? GI_REQ_OVERFLOW : 0);
+  H->body_proc = t.body_proc;
+}
+
+// ------------------------------------------------ stage 2: k_scan (phase A)
+// Multi-pattern scan of one union automaton over a value: the set of the
+// automaton's patterns that match somewhere in it.
+__device__ uint64_t dfa_scan(const DProgram& P, int32_t id, const uint8_t* s, uint32_t n) {
+  const DDfa d = P.dfas[id];
+  if (!d.multi) return dfa_match(P, id, s, n, false) ? 1ull : 0ull;
+  const uint16_t* __restrict__ tr = P.trans + d.trans_off;
+  const uint8_t* __restrict__ amap = P.u8pool + d.amap_off;
+  const uint8_t* __restrict__ combo = P.u8pool + d.combo_off;
+  const uint64_t* __restrict__ acc = P.u64pool + d.acc_off;
+  const uint32_t ncls = d.n_classes;
+  uint32_t st = d.start;
+  uint64_t m = 0;
+  uint32_t i = 0;
+  while (i < n) {
+    const uint8_t c = s[i];
+    uint32_t cls;
+    if (c < 0x80) {
+      cls = amap[c];
+      i++;
+    } else {
+      uint32_t w;
+      const uint32_t rr = decode_rune(s, n, i, &w);
+      i += w;
+      if (d.nonascii_uniform) {
+        cls = d.nonascii_cls;
+      } else {
+        const uint32_t* nr = P.nranges + d.nr_off;
+        uint32_t lo = 0, hi = d.nr_cnt;
+        cls = 0;
+        while (lo < hi) {
+          uint32_t mid = (lo + hi) >> 1;
+          if (nr[mid * 3 + 1] < rr) lo = mid + 1;
+          else hi = mid;
+        }
+        if (lo < d.nr_cnt && nr[lo * 3] <= rr) cls = nr[lo * 3 + 2];
+      }
+    }
+    const uint16_t tv = tr[st * ncls + cls];
+    if (tv & 0x8000) m |= acc[(uint64_t)st * 5 + combo[cls]];
+    st = tv & 0x7FFF;
+  }
+  return m | acc[(uint64_t)st * 5 + 4];
+}
+
+__device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
+  if (kind == OP_VALIDATE_BYTE_RANGE) {
+    for (uint32_t i = 0; i < n; i++)
+      if (!((bits[s[i] >> 5] >> (s[i] & 31)) & 1)) return true;
+    return false;
+  }
+  if (kind == OP_VALIDATE_URL_ENCODING) {
+    for (uint32_t i = 0; i < n;) {
+      if (s[i] == '%') {
+        if (i + 2 >= n) return true;
+        if (ishex(s[i + 1]) && ishex(s[i + 2])) i += 3;
+        else return true;
+      } else {
+        i++;
+      }
+    }
+    return false;
+  }
+  for (uint32_t i = 0; i < n;) {  // OP_VALIDATE_UTF8
+    uint32_t w;
+    uint32_t r = decode_rune(s, n, i, &w);
+    if (r == 0xFFFD && w == 1) return true;
+    i += w;
+  }
+  return false;
+}
+
+__device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
+  atomicOr(&B.hits[(uint64_t)(slot >> 5) * B.n_req + r], 1u << (slot & 31));
+}
+
+// transform (chain) + scan one value of a group; hit bits are emitted per
+// value (matches are rare); "maybe" (every pattern) on any overflow.
+__device__ void scan_value(const DProgram& P, const DBatch& B, uint32_t r, const DGroup& G, const uint8_t* v,
+                           uint32_t vn, uint8_t* s0, uint8_t* s1, uint32_t cap) {
+  const uint8_t* cur = v;
+  uint32_t cn = vn;
+  bool maybe = false;
+  for (uint32_t k = 0; k < G.tchain_len; k++) {
+    uint8_t* dst = (cur == s0) ? s1 : s0;
+    int64_t m = apply_transform(P, P.tchains[G.tchain_off + k], cur, cn, dst, cap);
+    if (m < 0) {
+      maybe = true;
+      break;
+    }
+    cur = dst;
+    cn = (uint32_t)m;
+  }
+  for (uint32_t d = 0; d < G.sdfa_count; d++) {
+    const DScanDfa sd = P.sdfas[G.sdfa_begin + d];
+    uint64_t m = maybe ? ~0ull : (dfa_scan(P, sd.dfa, cur, cn) ^ sd.neg_mask);
+    m &= sd.n_pat >= 64 ? ~0ull : ((1ull << sd.n_pat) - 1);
+    while (m) {
+      const int k = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      set_hit(B, P.pats[sd.pat_begin + k].slot, r);
+    }
+  }
+  for (uint32_t k = 0; k < G.val_count; k++) {
+    const DScanVal sv = P.svals[G.val_begin + k];
+    if (maybe || (validate_op(sv.kind, sv.bits, cur, cn) != (sv.negate != 0))) set_hit(B, sv.slot, r);
+  }
+}
+
+__device__ inline bool group_key_ok(const DProgram& P, const DGroup& G, const Field& f) {
+  if (G.key_mode == 1) {
+    if (G.ci ? !eq_ascii_ci(f.k, f.kn, P.strpool + G.key_off, G.key_len)
+             : !eq_bytes(f.k, f.kn, P.strpool + G.key_off, G.key_len))
+      return false;
+  } else if (G.key_mode == 2) {
+    if (!dfa_match(P, G.key_dfa, f.k, f.kn, G.ci != 0)) return false;
+  }
+  for (uint32_t e = 0; e < G.exc_count; e++) {
+    const DExc x = P.excs[G.exc_begin + e];
+    if (x.dfa >= 0) {
+      if (dfa_match(P, x.dfa, f.k, f.kn, true)) return false;
+    } else if (eq_ascii_ci(f.k, f.kn, P.strpool + x.off, x.len)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+// One work item = (scan group g, request r), group-major so a wavefront
+// walks 64 requests through the same automata.  Grid-stride over resident
+// threads; each thread owns two transformation buffers of B.tcap bytes.
+__global__ void __launch_bounds__(256) k_scan(DProgram P, DBatch B, uint64_t n_items) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+  uint8_t* s0 = B.tscratch + tid * 2ull * B.tcap;
+  uint8_t* s1 = s0 + B.tcap;
+  for (uint64_t item = tid; item < n_items; item += nthreads) {
+    const uint32_t g = (uint32_t)(item / B.n_req);
+    const uint32_t r = (uint32_t)(item - (uint64_t)g * B.n_req);
+    const DGroup G = P.groups[g];
+    const uint8_t* base = B.scratch + B.layout[r].base;
+    const ReqHdr* H = (const ReqHdr*)base;
+    if (H->flags & GI_REQ_ERROR_MASK) continue;
+    if (G.src == SRC_SINGLE) {
+      const Str v = H->single[G.single];
+      scan_value(P, B, r, G, v.p, v.n, s0, s1, B.tcap);
+    } else {
+      const Field* F = (const Field*)(base + 256);
+      const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck;
+      for (int kind = FK_ARG_GET; kind <= FK_COOKIE; kind++) {
+        if (!((G.kind_mask >> kind) & 1)) continue;
+        uint32_t b = 0, e = 0;
+        if (kind == FK_ARG_GET) { b = 0; e = n_get; }
+        else if (kind == FK_HEADER) { b = n_get; e = n_get + n_hdr; }
+        else if (kind == FK_COOKIE) { b = n_get + n_hdr; e = n_get + n_hdr + n_ck; }
+        else continue;
+        for (uint32_t i = b; i < e; i++) {
+          const Field f = F[i];
+          if (!group_key_ok(P, G, f)) continue;
+          if (G.names) scan_value(P, B, r, G, f.k, f.kn, s0, s1, B.tcap);
+          else scan_value(P, B, r, G, f.v, f.vn, s0, s1, B.tcap);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------ stage 3: k_eval (phase B)
+// RuleGroup.Eval(1) -> ProcessRequestBody -> RuleGroup.Eval(2) per request,
+// skipping every phase-A rule whose hit bit is clear.
+__global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
+  __shared__ unsigned long long red[6];
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (threadIdx.x < 6) red[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long my[6] = {0, 0, 0, 0, 0, 0};
+  if (r < B.n_req) {
+    const gi_request rq = B.reqs[r];
+    Region g = region_of(P, B, r);
+    ReqHdr* H = g.hdr;
+    Tx t;
+    tx_bind(t, P, g);
+    t.hits = B.hits;
+    t.n_req = B.n_req;
+    t.req = r;
+    t.has_post = false;
+    t.nf = H->nf;
+    t.nb = H->nb;
+    t.flags = H->flags;
+    t.body_proc = H->body_proc;
+    t.ntx = 0;
+    t.nremoved = 0;
+    t.engine = P.rule_engine;
+    t.body_access = P.body_access;
+    t.force_body = 0;
+    t.phase = 0;
+    t.skip_after = -1;
+    t.skip = 0;
+    t.interrupted = false;
+    t.int_rule = 0;
+    t.int_status = 0;
+    t.int_action = 0;
+    t.int_phase = 0;
+    t.nmatched = 0;
+    t.mout = B.matched + (uint64_t)r * B.mcap;
+    t.mcap = B.mcap;
+    for (uint32_t s = 0; s < P.n_slots; s++) t.slots[s].state = 0;
+    const uint8_t* D = B.data;
+    uint64_t scanned = (uint64_t)rq.method.len + rq.uri.len + rq.proto.len + rq.body.len;
+    for (uint32_t h = 0; h < rq.hdr_count; h++) {
+      const gi_header hd = B.headers[rq.hdr_begin + h];
+      scanned += hd.name.len + hd.value.len;
+    }
+    if (!(t.flags & GI_REQ_ERROR_MASK)) {
       eval_phase(t, 1);
-      // ProcessRequestBody
       if (!t.interrupted && t.engine != ENGINE_OFF && !(t.flags & GI_REQ_ERROR_MASK)) {
         const uint32_t bn = rq.body.len;
         if (t.body_access && bn > 0) {
@@ -1487,7 +1748,9 @@ __global__ void __launch_bounds__(128) k_inspect(DProgram P, DBatch B) {
             }
             if (t.body_proc == BP_URLENCODED) {
               t.single[S_REQUEST_BODY] = {D + rq.body.off, bn};
+              const uint32_t nf0 = t.nf;
               parse_query(t, D + rq.body.off, bn, FK_ARG_POST);
+              t.has_post = t.nf > nf0;
             } else if (t.body_proc != BP_NONE) {
               t.flags |= GI_REQ_UNSUPPORTED_BODY;
             }
@@ -1520,20 +1783,41 @@ __global__ void __launch_bounds__(128) k_inspect(DProgram P, DBatch B) {
     my[4] = scanned;
     my[5] = t.nmatched;
   }
-  // block reduction -> one atomic per block per counter
   for (int c = 0; c < 6; c++) {
     unsigned long long x = my[c];
     for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&red[c][0], x);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&red[c], x);
   }
   __syncthreads();
-  if (threadIdx.x < 6) atomicAdd(&B.tally[threadIdx.x], red[threadIdx.x][0]);
+  if (threadIdx.x < 6) atomicAdd(&B.tally[threadIdx.x], red[threadIdx.x]);
 }
 
-void launch_inspect(const DProgram& P, const DBatch& B, hipStream_t stream) {
-  const uint32_t threads = 128;
-  const uint32_t blocks = (B.n_req + threads - 1) / threads;
-  if (blocks) hipLaunchKernelGGL(k_inspect, dim3(blocks), dim3(threads), 0, stream, P, B);
+uint32_t scan_resident_threads() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  (void)hipGetDeviceProperties(&prop, dev);
+  int per_cu = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scan, 256, 0);
+  if (per_cu < 1) per_cu = 1;
+  return (uint32_t)prop.multiProcessorCount * (uint32_t)per_cu * 256u;
+}
+
+void launch_pipeline(const DProgram& P, const DBatch& B, uint32_t scan_threads, hipStream_t stream,
+                     hipEvent_t* ev) {
+  if (!B.n_req) return;
+  const uint32_t cb = (B.n_req + 255) / 256;
+  hipLaunchKernelGGL(k_collect, dim3(cb), dim3(256), 0, stream, P, B);
+  if (ev) (void)hipEventRecord(ev[0], stream);
+  const uint64_t items = (uint64_t)P.n_groups * B.n_req;
+  if (items) {
+    uint64_t blocks = (items + 255) / 256;
+    const uint64_t maxb = scan_threads / 256;
+    if (blocks > maxb) blocks = maxb;
+    hipLaunchKernelGGL(k_scan, dim3((uint32_t)blocks), dim3(256), 0, stream, P, B, items);
+  }
+  if (ev) (void)hipEventRecord(ev[1], stream);
+  hipLaunchKernelGGL(k_eval, dim3((B.n_req + 127) / 128), dim3(128), 0, stream, P, B);
 }
 
 }  // namespace gi

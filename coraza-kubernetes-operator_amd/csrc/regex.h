@@ -57,18 +57,39 @@ struct Regex {
 // (\p{..} Unicode groups).
 bool re_parse(const std::string& pattern, Regex* out, std::string* err);
 
-// A sticky-accept DFA: once `accept` is entered the scan can stop (match).
+// Two automaton shapes share this struct:
+//  * single (multi == false): sticky-accept DFA; once `accept` is entered the
+//    scan can stop (match).  end_accept[s]: match at end of input.
+//  * multi  (multi == true): union of n_pat patterns, no sticky state.  A
+//    transition whose u16 has bit 15 set completes matches *before* consuming
+//    the class; the matched set is acc[5*s + cls_combo[cls]] (combo = bit0
+//    next-is-'\n', bit1 next-is-word, the only facts ^ $ \b \B look at).
+//    acc[5*s + 4] is the set matched at end of input.
 struct Dfa {
   uint32_t n_states = 0, n_classes = 0, start = 0, accept = 0;
   bool byte_mode = false;               // phrase automata: bytes, no UTF-8 decode
+  bool multi = false;
+  uint32_t n_pat = 1;
   std::vector<uint16_t> trans;          // n_states * n_classes
-  std::vector<uint8_t> end_accept;      // per state: matches at end of input
+  std::vector<uint8_t> end_accept;      // per state: matches at end of input (single)
   std::vector<uint8_t> amap;            // 128 (rune mode) or 256 (byte mode)
   std::vector<uint32_t> nranges;        // rune mode: triples (lo, hi, cls), runes >= 0x80
+  std::vector<uint8_t> cls_combo;       // multi: per class, bit0 '\n', bit1 word char
+  std::vector<uint64_t> acc;            // multi: 5 masks per state
 };
 
 // Unanchored boolean search DFA for `re` (MatchString semantics).
 bool build_regex_dfa(const Regex& re, Dfa* out, std::string* err, uint32_t state_cap = 60000);
+
+// Union (multi-pattern) search DFA over up to 64 patterns: the scan reports,
+// for every pattern, whether it matches somewhere in the input.
+bool build_union_dfa(const std::vector<const Regex*>& pats, Dfa* out, std::string* err,
+                     uint32_t state_cap = 8192);
+
+// @pm phrase set / @contains literal as a regex AST (search semantics).
+// fold_ascii: ASCII-only case folding (aho-corasick AsciiCaseInsensitive).
+// Returns false if a phrase has a byte >= 0x80 (byte-mode automaton needed).
+bool phrases_to_regex(const std::vector<std::string>& phrases, bool fold_ascii, Regex* out);
 
 // Aho-Corasick phrase automaton as a byte DFA: matches iff any phrase occurs.
 // fold_ascii: ASCII case-insensitive (coraza @pm).
@@ -78,6 +99,8 @@ bool build_phrase_dfa(const std::vector<std::string>& phrases, bool fold_ascii, 
 // Host-side walk of a built DFA (compiler self-test only; never used by the
 // inspection path).
 bool dfa_host_match(const Dfa& d, const uint8_t* s, size_t n);
+// Multi automata: the set of patterns matching somewhere in s.
+uint64_t dfa_host_scan(const Dfa& d, const uint8_t* s, size_t n);
 
 // Go utf8.DecodeRune: returns rune, sets *w (invalid -> U+FFFD, width 1).
 uint32_t go_decode_rune(const uint8_t* s, size_t n, size_t i, int* w);

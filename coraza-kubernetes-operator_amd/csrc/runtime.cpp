@@ -68,7 +68,11 @@ struct gi_ctx {
   DProgram prog{};
   std::vector<DevBuf> pbufs;
   // batch buffers
-  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally;
+  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, hits, tscratch;
+  uint32_t scan_threads = 0;
+  uint32_t tcap = 2048;
+  uint32_t hit_words = 0;
+  hipEvent_t evs[2] = {nullptr, nullptr};
   uint32_t n_req = 0;
   bool staged = false, ran = false;
   gi_stats stats{};
@@ -113,10 +117,14 @@ int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ru
   rs->info.n_links = (uint32_t)P.rules.size();
   rs->info.n_dfas = (uint32_t)P.dfas.size();
   rs->info.n_tx_slots = P.n_slots;
+  rs->info.n_scan_groups = (uint32_t)P.groups.size();
+  rs->info.n_hit_slots = P.n_hit_slots;
+  rs->info.n_union_dfas = P.n_union_dfas;
   rs->info.program_bytes = P.rules.size() * sizeof(DRule) + P.vars.size() * sizeof(DVarRef) +
                            P.ops.size() * sizeof(DOp) + P.acts.size() * sizeof(DAction) +
                            P.trans.size() * 2 + P.u8pool.size() + P.nranges.size() * 4 + P.strpool.size() +
-                           P.dfas.size() * sizeof(DDfa) + P.tparts.size() * sizeof(DTmplPart);
+                           P.dfas.size() * sizeof(DDfa) + P.tparts.size() * sizeof(DTmplPart) +
+                           P.u64pool.size() * 8 + P.groups.size() * sizeof(DGroup) + P.sdfas.size() * sizeof(DScanDfa);
   *out = rs;
   return GI_OK;
 }
@@ -152,12 +160,14 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipEventCreate(&c->evs[0]);
+  if (e == hipSuccess) e = hipEventCreate(&c->evs[1]);
   if (e != hipSuccess) {
     delete c;
     return GI_ENODEV;
   }
   const Program& P = rs->prog;
-  c->pbufs.resize(16);
+  c->pbufs.resize(24);
   std::vector<uint32_t> lower;
   lower.reserve(GI_N_LOWER_PAIRS * 2);
   for (int i = 0; i < GI_N_LOWER_PAIRS; i++) {
@@ -189,6 +199,11 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   UP(strpool, P.strpool, uint8_t)
   UP(lower_pairs, lower, uint32_t)
   UP(slot_names, P.slot_names, uint32_t)
+  UP(u64pool, P.u64pool, uint64_t)
+  UP(groups, P.groups, DGroup)
+  UP(sdfas, P.sdfas, DScanDfa)
+  UP(pats, P.pats, DPat)
+  UP(svals, P.svals, DScanVal)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
@@ -204,6 +219,13 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->prog.rule_engine = P.rule_engine;
   c->prog.body_access = P.body_access;
   c->prog.body_limit = P.body_limit;
+  c->prog.n_groups = (uint32_t)P.groups.size();
+  c->prog.n_hit_slots = P.n_hit_slots;
+  c->scan_threads = scan_resident_threads();
+  if (c->tscratch.ensure((size_t)c->scan_threads * 2 * c->tcap) != hipSuccess) {
+    gi_ctx_free(c);
+    return GI_ENOMEM;
+  }
   *out = c;
   return GI_OK;
 }
@@ -213,8 +235,11 @@ void gi_ctx_free(gi_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& b : c->pbufs) b.release();
-  for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally})
+  for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally,
+                    &c->hits, &c->tscratch})
     b->release();
+  for (auto& ev : c->evs)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -273,7 +298,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     L.cap_b = (uint32_t)cap_b;
     L.cap_t = (uint32_t)cap_t;
     L.cap_mt = (uint32_t)cap_mt;
-    uint64_t sz = cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + (cap_b + 15) / 16 * 16 +
+    uint64_t sz = 256 + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + (cap_b + 15) / 16 * 16 +
                   2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
     off += (sz + 63) / 64 * 64;
   }
@@ -290,6 +315,9 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if ((e = c->matched.ensure(std::max<size_t>((size_t)n * c->mcap * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc matched");
   if ((e = c->tally.ensure(sizeof(gi_tally))) != hipSuccess) return hip_fail(c, e, "alloc tally");
+  c->hit_words = (c->rs->prog.n_hit_slots + 31) / 32;
+  if ((e = c->hits.ensure(std::max<size_t>((size_t)c->hit_words * n * 4, 16))) != hipSuccess)
+    return hip_fail(c, e, "alloc hits");
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && n) e = hipMemcpyAsync(c->reqs.p, in->reqs, n * sizeof(gi_request), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && in->n_headers)
@@ -323,10 +351,17 @@ int gi_run_staged(gi_ctx* c) {
   B.verdicts = (gi_verdict*)c->verdicts.p;
   B.matched = (uint32_t*)c->matched.p;
   B.tally = (unsigned long long*)c->tally.p;
+  B.hits = (uint32_t*)c->hits.p;
+  B.tscratch = (uint8_t*)c->tscratch.p;
+  B.tcap = c->tcap;
   (void)hipEventRecord(c->ev0, c->stream);
-  launch_inspect(c->prog, B, c->stream);
+  if (c->hit_words) {
+    e = hipMemsetAsync(c->hits.p, 0, (size_t)c->hit_words * c->n_req * 4, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "memset hits");
+  }
+  launch_pipeline(c->prog, B, c->scan_threads, c->stream, c->evs);
   e = hipGetLastError();
-  if (e != hipSuccess) return hip_fail(c, e, "launch k_inspect");
+  if (e != hipSuccess) return hip_fail(c, e, "launch pipeline");
   (void)hipEventRecord(c->ev1, c->stream);
   c->ran = true;
   c->stats.batches++;
@@ -341,6 +376,9 @@ int gi_sync(gi_ctx* c) {
   if (c->ran) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->stats.last_kernel_ms = ms;
+    if (c->n_req && hipEventElapsedTime(&ms, c->ev0, c->evs[0]) == hipSuccess) c->stats.last_collect_ms = ms;
+    if (c->n_req && hipEventElapsedTime(&ms, c->evs[0], c->evs[1]) == hipSuccess) c->stats.last_scan_ms = ms;
+    if (c->n_req && hipEventElapsedTime(&ms, c->evs[1], c->ev1) == hipSuccess) c->stats.last_eval_ms = ms;
   }
   return GI_OK;
 }

@@ -83,7 +83,9 @@ class _CompileOpts(ctypes.Structure):
 
 class _Info(ctypes.Structure):
     _fields_ = [("n_rules", ctypes.c_uint32), ("n_links", ctypes.c_uint32), ("n_dfas", ctypes.c_uint32),
-                ("n_tx_slots", ctypes.c_uint32), ("program_bytes", ctypes.c_uint64)]
+                ("n_tx_slots", ctypes.c_uint32), ("program_bytes", ctypes.c_uint64),
+                ("n_scan_groups", ctypes.c_uint32), ("n_hit_slots", ctypes.c_uint32),
+                ("n_union_dfas", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
 
 
 class _Batch(ctypes.Structure):
@@ -103,7 +105,9 @@ class _Tally(ctypes.Structure):
 
 class _Stats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("last_kernel_ms", ctypes.c_double),
-                ("last_stage_ms", ctypes.c_double), ("last_scratch_bytes", ctypes.c_uint64)]
+                ("last_stage_ms", ctypes.c_double), ("last_scratch_bytes", ctypes.c_uint64),
+                ("last_collect_ms", ctypes.c_double), ("last_scan_ms", ctypes.c_double),
+                ("last_eval_ms", ctypes.c_double)]
 
 
 _LIB = None

@@ -83,6 +83,10 @@ typedef struct {
   uint32_t n_dfas;
   uint32_t n_tx_slots;
   uint64_t program_bytes; /* device-resident artifact size */
+  uint32_t n_scan_groups; /* phase-A groups (source x key filter x transformation chain) */
+  uint32_t n_hit_slots;   /* rule links evaluated data-parallel in phase A */
+  uint32_t n_union_dfas;  /* multi-pattern automata among n_dfas */
+  uint32_t _pad;
 } gi_ruleset_info;
 
 /* A byte range inside gi_batch.data. */
@@ -149,6 +153,9 @@ typedef struct {
   double last_kernel_ms;   /* HIP-event time of the last inspection pipeline */
   double last_stage_ms;    /* H2D staging time of the last batch */
   uint64_t last_scratch_bytes;
+  double last_collect_ms;  /* k_collect (ProcessURI / headers / cookies) */
+  double last_scan_ms;     /* k_scan (phase A: transforms + union automata) */
+  double last_eval_ms;     /* k_eval (phase B: rule interpreter, body, verdicts) */
 } gi_stats;
 
 /* ------------------------------------------------------------ compile */
