@@ -129,11 +129,15 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
     eng.sync()
-    kern_ms = []
+    kern_ms, stage_ms = [], {"k_collect": [], "k_match": [], "k_eval": []}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        kern_ms.append(eng.stats()["last_kernel_ms"])
+        st = eng.stats()
+        kern_ms.append(st["last_kernel_ms"])
+        stage_ms["k_collect"].append(st["last_collect_ms"])
+        stage_ms["k_match"].append(st["last_scan_ms"])
+        stage_ms["k_eval"].append(st["last_eval_ms"])
     eng.sync()
     if dist is not None:
         torch.cuda.synchronize()
@@ -154,11 +158,23 @@ def main():
     value = total_req * args.steps / elapsed
     gbs = total_bytes * args.steps / elapsed / 1e9
 
-    # roofline of the dominant (only) kernel, k_inspect: algorithmic bytes per
-    # launch = raw request bytes read once + 80 B verdict + 4 B per matched id
+    # roofline of the dominant kernel (HIP events on the context stream).
+    # Algorithmic bytes per launch (DESIGN.md "Roofline"):
+    #   k_match: request line + header bytes (every value phase A scans is a
+    #            substring of those) + one 4-B hit word per (hit word, request);
+    #   k_eval : raw request bytes + 80-B verdict + 4 B per matched rule id.
     avg_kern_ms = float(np.mean(kern_ms))
-    alg_bytes = raw + 80 * batch.n_req + 4 * int(tally["matched_total"])
-    achieved = alg_bytes / (avg_kern_ms * 1e-3) / 1e9
+    avg_stage = {k: float(np.mean(v)) for k, v in stage_ms.items()}
+    body_bytes = int(batch.reqs["body"]["len"].sum())
+    hit_words = (rs.info["n_hit_slots"] + 31) // 32
+    alg = {
+        "k_match": raw - body_bytes + 4 * hit_words * batch.n_req,
+        "k_eval": raw + 80 * batch.n_req + 4 * int(tally["matched_total"]),
+        "k_collect": raw - body_bytes,
+    }
+    dom = max(("k_match", "k_eval"), key=lambda k: avg_stage[k])
+    alg_bytes = alg[dom]
+    achieved = alg_bytes / (avg_stage[dom] * 1e-3) / 1e9
     out = {
         "metric": "requests inspected/sec (node), CRS v4 PL1",
         "value": round(value, 1),
@@ -180,8 +196,10 @@ def main():
         "error_requests": int(tally["n_error"]),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                     "kernel": "k_inspect", "kernel_ms": round(avg_kern_ms, 4),
-                     "alg_bytes_per_launch": int(alg_bytes)},
+                     "kernel": dom, "kernel_ms": round(avg_stage[dom], 4),
+                     "alg_bytes_per_launch": int(alg_bytes),
+                     "stages_ms": {k: round(v, 4) for k, v in avg_stage.items()},
+                     "pipeline_kernel_ms": round(avg_kern_ms, 4)},
         "gen_s": round(t_gen, 1),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -914,14 +914,17 @@ struct Lower {
     int kind;  // 0 regex, 1 phrases (fold), 2 literal (case-sensitive)
     std::string rx;
     std::vector<std::string> phrases;
+    uint32_t fmask;  // admitting filters of the stream
   };
-  struct GroupBuild {
-    DGroup g;
+  struct StreamBuild {
+    DStream s;
+    std::vector<DFilter> filters;
+    std::vector<std::string> fkeys;
     std::vector<PatEntry> pats;
     std::vector<DScanVal> vals;
   };
-  std::vector<GroupBuild> gbuild;
-  std::map<std::string, size_t> gindex;
+  std::vector<StreamBuild> sbuild;
+  std::map<std::string, size_t> sindex;
 
   static bool immutable_single(int sid) {
     return sid == S_REQUEST_METHOD || sid == S_REQUEST_PROTOCOL || sid == S_REQUEST_URI ||
@@ -929,7 +932,9 @@ struct Lower {
            sid == S_REQUEST_BASENAME || sid == S_QUERY_STRING;
   }
 
-  // Returns the hit slot, or -1 when the link stays interpreter-only.
+  // Assigns a hit slot and registers the link's patterns, or returns -1 when
+  // the link stays interpreter-only (TX / count targets, macro arguments,
+  // operators without an automaton form, mutable singles).
   int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
     if (!r.has_op) return -1;
     const std::string& n = r.op_name;
@@ -951,15 +956,14 @@ struct Lower {
     const DVarRef* vrs = &P->vars[d.var_begin];
     for (uint32_t vi = 0; vi < d.var_count; vi++) {
       const DVarRef& vr = vrs[vi];
-      DGroup g{};
-      g.key_dfa = -1;
-      uint8_t mask = 0;
-      bool names = false;
+      DFilter f{};
+      f.key_dfa = -1;
+      f.single = GI_NO_SINGLE;
       if (vr.var < S_COUNT) {
-        g.src = SRC_SINGLE;
-        g.single = vr.var;
+        f.single = vr.var;
       } else {
-        g.src = SRC_FIELDS;
+        uint8_t mask = 0;
+        bool names = false;
         switch (vr.var) {
           case V_ARGS_GET: mask = 1 << FK_ARG_GET; break;
           case V_ARGS: mask = 1 << FK_ARG_GET; break;  // ARG_POST fields only exist after phase 1
@@ -972,54 +976,77 @@ struct Lower {
           default: break;  // ARGS_POST*, XML, FILES*: no values before the body phase
         }
         if (!mask) continue;
-        g.kind_mask = mask;
-        g.names = names;
-        g.key_mode = vr.key_mode;
-        g.ci = vr.ci;
-        g.key_dfa = vr.key_dfa;
-        g.key_off = vr.key_off;
-        g.key_len = vr.key_len;
-        g.exc_begin = vr.exc_begin;
-        g.exc_count = vr.exc_count;
+        f.kind_mask = mask;
+        f.names = names;
+        f.key_mode = vr.key_mode;
+        f.ci = vr.ci;
+        f.key_dfa = vr.key_dfa;
+        f.key_off = vr.key_off;
+        f.key_len = vr.key_len;
+        f.exc_begin = vr.exc_begin;
+        f.exc_count = vr.exc_count;
       }
-      g.tchain_off = d.tchain_off;
-      g.tchain_len = d.tchain_len;
-      // group identity: source, key filter, exclusions, chain
-      std::string key;
-      key.append((const char*)&g.src, 6);
-      if (g.key_mode == 1) key.append((const char*)&P->strpool[g.key_off], g.key_len);
-      key.push_back('|');
-      key.append(std::to_string(g.key_dfa));
-      key.push_back('|');
-      for (uint32_t e = 0; e < g.exc_count; e++) {
-        const DExc& x = P->excs[g.exc_begin + e];
-        key.append(std::to_string(x.dfa));
-        key.push_back(':');
-        key.append((const char*)&P->strpool[x.off], x.len);
-        key.push_back(',');
+      const std::string skey((const char*)&P->tchains[d.tchain_off], d.tchain_len);
+      std::string fkey((const char*)&f, 5);
+      if (f.key_mode == 1) fkey.append((const char*)&P->strpool[f.key_off], f.key_len);
+      fkey.append("|" + std::to_string(f.key_dfa) + "|");
+      for (uint32_t e = 0; e < f.exc_count; e++) {
+        const DExc& x = P->excs[f.exc_begin + e];
+        fkey.append(std::to_string(x.dfa) + ":");
+        fkey.append((const char*)&P->strpool[x.off], x.len);
+        fkey.push_back(',');
       }
-      key.push_back('|');
-      key.append((const char*)&P->tchains[d.tchain_off], d.tchain_len);
-      auto it = gindex.find(key);
-      if (it == gindex.end()) {
-        it = gindex.emplace(key, gbuild.size()).first;
-        GroupBuild gb;
-        gb.g = g;
-        gbuild.push_back(gb);
+      // find the stream part holding (or able to take) this filter
+      size_t si = SIZE_MAX;
+      uint32_t fid = 0;
+      for (int part = 0; si == SIZE_MAX; part++) {
+        std::string k = skey + "#" + std::to_string(part);
+        auto it = sindex.find(k);
+        if (it == sindex.end()) {
+          StreamBuild sb;
+          sb.s = DStream{};
+          sb.s.tchain_off = d.tchain_off;
+          sb.s.tchain_len = d.tchain_len;
+          sindex[k] = sbuild.size();
+          sbuild.push_back(sb);
+          it = sindex.find(k);
+        }
+        StreamBuild& sb = sbuild[it->second];
+        auto fit = std::find(sb.fkeys.begin(), sb.fkeys.end(), fkey);
+        if (fit != sb.fkeys.end()) {
+          si = it->second;
+          fid = (uint32_t)(fit - sb.fkeys.begin());
+        } else if (sb.fkeys.size() < GI_MAX_FILTERS) {
+          sb.fkeys.push_back(fkey);
+          sb.filters.push_back(f);
+          sb.s.kind_mask |= f.kind_mask;
+          si = it->second;
+          fid = (uint32_t)sb.fkeys.size() - 1;
+        }
       }
-      GroupBuild& gb = gbuild[it->second];
+      StreamBuild& sb = sbuild[si];
       if (o.kind == OP_VALIDATE_BYTE_RANGE || o.kind == OP_VALIDATE_URL_ENCODING || o.kind == OP_VALIDATE_UTF8) {
+        bool merged = false;
+        for (auto& sv : sb.vals)
+          if (sv.slot == (uint32_t)slot) sv.fmask |= 1u << fid, merged = true;
+        if (merged) continue;
         DScanVal sv{};
         sv.kind = o.kind;
         sv.negate = o.negate;
+        sv.fmask = 1u << fid;
         sv.slot = (uint32_t)slot;
         for (int k = 0; k < 8; k++) sv.bits[k] = o.bits[k];
-        gb.vals.push_back(sv);
+        sb.vals.push_back(sv);
         continue;
       }
+      bool merged = false;
+      for (auto& pe : sb.pats)
+        if (pe.slot == (uint32_t)slot) pe.fmask |= 1u << fid, merged = true;
+      if (merged) continue;
       PatEntry pe;
       pe.slot = (uint32_t)slot;
       pe.negate = o.negate != 0;
+      pe.fmask = 1u << fid;
       if (o.kind == OP_RX) {
         pe.kind = 0;
         pe.rx = "(?sm)" + r.op_arg;
@@ -1037,29 +1064,33 @@ struct Lower {
         pe.kind = 2;
         pe.phrases.push_back(r.op_arg);
       }
-      gb.pats.push_back(pe);
+      sb.pats.push_back(pe);
     }
     return slot;
   }
 
-  void emit_sdfa(GroupBuild& gb, const Dfa& d, const std::vector<const PatEntry*>& pes, std::vector<DScanDfa>* out) {
-    DScanDfa s{};
-    s.dfa = add_dfa(d);
-    s.pat_begin = (uint32_t)P->pats.size();
-    s.n_pat = (uint32_t)pes.size();
-    for (size_t k = 0; k < pes.size(); k++) {
-      P->pats.push_back(DPat{pes[k]->slot});
-      if (pes[k]->negate) s.neg_mask |= 1ull << k;
-    }
-    if (d.multi) P->n_union_dfas++;
-    out->push_back(s);
-    (void)gb;
+  struct AutoBuild {
+    Dfa d;
+    std::vector<const PatEntry*> pes;
+  };
+
+  static uint32_t img_bytes(const Dfa& d) {
+    uint32_t t = (d.n_states * d.n_classes * 2 + 15) & ~15u;
+    uint32_t a = ((uint32_t)d.amap.size() + 15) & ~15u;
+    uint32_t c = ((uint32_t)d.cls_combo.size() + 15) & ~15u;
+    return t + a + c;
   }
 
-  void finish_groups() {
-    const uint32_t kUnionCap = 4096;
-    for (auto& gb : gbuild) {
-      std::vector<DScanDfa> sd;
+  void finish_streams() {
+    const uint32_t kUnionTableBytes = 48 * 1024;  // LDS-resident union automata
+    std::ostringstream js;
+    js << "{\"streams\":[";
+    bool first_s = true;
+    for (auto& sb : sbuild) {
+      std::stable_sort(sb.pats.begin(), sb.pats.end(),
+                       [](const PatEntry& a, const PatEntry& b) { return a.fmask < b.fmask; });
+      // 1. automata: greedy union packing
+      std::vector<AutoBuild> autos;
       std::vector<std::unique_ptr<Regex>> owned;
       std::vector<const Regex*> cur;
       std::vector<const PatEntry*> curp;
@@ -1067,11 +1098,11 @@ struct Lower {
       std::string err;
       auto flush = [&]() {
         if (cur.empty()) return;
-        emit_sdfa(gb, curd, curp, &sd);
+        autos.push_back({std::move(curd), curp});
         cur.clear();
         curp.clear();
       };
-      for (auto& pe : gb.pats) {
+      for (auto& pe : sb.pats) {
         auto re = std::make_unique<Regex>();
         bool ok;
         if (pe.kind == 0) {
@@ -1080,17 +1111,16 @@ struct Lower {
         } else {
           ok = phrases_to_regex(pe.phrases, pe.kind == 1, re.get());
         }
-        if (!ok) {
-          // non-ASCII phrase: its own byte-mode automaton
+        if (!ok) {  // non-ASCII phrase: its own byte-mode automaton
           Dfa d;
           if (!build_phrase_dfa(pe.phrases, pe.kind == 1, &d, &err, cap)) unsup(err);
-          emit_sdfa(gb, d, {&pe}, &sd);
+          autos.push_back({std::move(d), {&pe}});
           continue;
         }
+        Dfa trial;
         cur.push_back(re.get());
         curp.push_back(&pe);
-        Dfa trial;
-        if (cur.size() <= 64 && build_union_dfa(cur, &trial, &err, kUnionCap)) {
+        if (cur.size() <= 64 && build_union_dfa(cur, &trial, &err, 16384) && img_bytes(trial) <= kUnionTableBytes) {
           curd = std::move(trial);
           owned.push_back(std::move(re));
           continue;
@@ -1100,29 +1130,118 @@ struct Lower {
         flush();
         cur.push_back(re.get());
         curp.push_back(&pe);
-        if (build_union_dfa(cur, &trial, &err, kUnionCap)) {
+        if (build_union_dfa(cur, &trial, &err, 16384) && img_bytes(trial) <= kUnionTableBytes) {
           curd = std::move(trial);
           owned.push_back(std::move(re));
           continue;
         }
-        // too large for a union automaton: single sticky DFA
+        // too large for an LDS union automaton: single sticky DFA (global tables)
         Dfa single;
         if (!build_regex_dfa(*re, &single, &err, cap)) unsup("regex " + pe.rx + ": " + err);
-        emit_sdfa(gb, single, {&pe}, &sd);
+        autos.push_back({std::move(single), {&pe}});
         cur.clear();
         curp.clear();
         owned.push_back(std::move(re));
       }
       flush();
-      DGroup g = gb.g;
-      g.sdfa_begin = (uint32_t)P->sdfas.size();
-      g.sdfa_count = (uint32_t)sd.size();
-      P->sdfas.insert(P->sdfas.end(), sd.begin(), sd.end());
-      g.val_begin = (uint32_t)P->svals.size();
-      g.val_count = (uint32_t)gb.vals.size();
-      P->svals.insert(P->svals.end(), gb.vals.begin(), gb.vals.end());
-      if (g.sdfa_count + g.val_count) P->groups.push_back(g);
+      // 2. stream record
+      DStream s = sb.s;
+      s.filt_begin = (uint32_t)P->filters.size();
+      s.filt_count = (uint32_t)sb.filters.size();
+      P->filters.insert(P->filters.end(), sb.filters.begin(), sb.filters.end());
+      const uint32_t sid = (uint32_t)P->streams.size();
+      P->streams.push_back(s);
+      if (!first_s) js << ",";
+      first_s = false;
+      js << "{\"chain\":[";
+      for (uint32_t k = 0; k < s.tchain_len; k++) js << (k ? "," : "") << (int)P->tchains[s.tchain_off + k];
+      js << "],\"kinds\":" << (int)s.kind_mask << ",\"filters\":[";
+      for (uint32_t k = 0; k < s.filt_count; k++) {
+        const DFilter& f = sb.filters[k];
+        js << (k ? "," : "") << "{\"single\":" << (int)(f.single == GI_NO_SINGLE ? -1 : f.single)
+           << ",\"kinds\":" << (int)f.kind_mask << ",\"names\":" << (int)f.names << ",\"key\":" << (int)f.key_mode
+           << ",\"exc\":" << f.exc_count << "}";
+      }
+      js << "]"
+         << ",\"vals\":" << sb.vals.size() << ",\"jobs\":[";
+      // 3. jobs: pack automata into LDS images
+      size_t a = 0;
+      bool first_j = true;
+      bool vals_done = sb.vals.empty();
+      while (a < autos.size() || !vals_done) {
+        DJob j{};
+        j.stream = sid;
+        j.img_off = (uint32_t)P->images.size();
+        j.jdfa_begin = (uint32_t)P->jdfas.size();
+        uint32_t used = 0;
+        if (!first_j) js << ",";
+        first_j = false;
+        js << "[";
+        bool first_d = true;
+        while (a < autos.size()) {
+          const Dfa& d = autos[a].d;
+          const uint32_t b = img_bytes(d);
+          const bool fits = b <= GI_JOB_LDS_BYTES;
+          if (fits && used + b > GI_JOB_LDS_BYTES) break;        // next job
+          if (!fits && j.jdfa_count > 0) break;                   // global automaton: own job
+          DJobDfa jd{};
+          jd.dfa = add_dfa(d);
+          jd.lds_trans = jd.lds_amap = jd.lds_combo = -1;
+          if (fits) {
+            jd.lds_trans = (int32_t)used;
+            const uint8_t* tp = (const uint8_t*)d.trans.data();
+            P->images.insert(P->images.end(), tp, tp + d.trans.size() * 2);
+            P->images.resize(j.img_off + ((used + d.trans.size() * 2 + 15) & ~15u), 0);
+            used = (uint32_t)(P->images.size() - j.img_off);
+            jd.lds_amap = (int32_t)used;
+            P->images.insert(P->images.end(), d.amap.begin(), d.amap.end());
+            P->images.resize(j.img_off + ((used + d.amap.size() + 15) & ~15u), 0);
+            used = (uint32_t)(P->images.size() - j.img_off);
+            if (d.multi) {
+              jd.lds_combo = (int32_t)used;
+              P->images.insert(P->images.end(), d.cls_combo.begin(), d.cls_combo.end());
+              P->images.resize(j.img_off + ((used + d.cls_combo.size() + 15) & ~15u), 0);
+              used = (uint32_t)(P->images.size() - j.img_off);
+            }
+          }
+          jd.pat_begin = (uint32_t)P->pats.size();
+          jd.n_pat = (uint32_t)autos[a].pes.size();
+          jd.fmask_off = (uint32_t)P->u64pool.size();
+          for (uint32_t fi = 0; fi < s.filt_count; fi++) P->u64pool.push_back(0);
+          for (size_t k = 0; k < autos[a].pes.size(); k++) {
+            const PatEntry* pe = autos[a].pes[k];
+            P->pats.push_back(DPat{pe->slot});
+            if (pe->negate) jd.neg_mask |= 1ull << k;
+            for (uint32_t fi = 0; fi < s.filt_count; fi++)
+              if ((pe->fmask >> fi) & 1) P->u64pool[jd.fmask_off + fi] |= 1ull << k;
+          }
+          if (d.multi) P->n_union_dfas++;
+          P->jdfas.push_back(jd);
+          j.jdfa_count++;
+          if (!first_d) js << ",";
+          first_d = false;
+          js << "{\"states\":" << d.n_states << ",\"classes\":" << d.n_classes << ",\"pats\":" << jd.n_pat
+             << ",\"lds\":" << (fits ? 1 : 0) << "}";
+          a++;
+          if (!fits) break;
+        }
+        js << "]";
+        j.img_bytes = used;
+        if (!vals_done) {
+          j.val_begin = (uint32_t)P->svals.size();
+          j.val_count = (uint32_t)sb.vals.size();
+          P->svals.insert(P->svals.end(), sb.vals.begin(), sb.vals.end());
+          vals_done = true;
+        }
+        P->max_img_bytes = std::max(P->max_img_bytes, j.img_bytes);
+        P->jobs.push_back(j);
+      }
+      js << "]}";
     }
+    js << "],\"jobs\":" << P->jobs.size() << ",\"hit_slots\":" << P->n_hit_slots
+       << ",\"image_bytes\":" << P->images.size() << "}";
+    P->plan_json = js.str();
+    if (P->images.empty()) P->images.resize(16, 0);
   }
 
   uint32_t rule(const IrRule& r, bool child) {
@@ -1181,7 +1300,7 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
         prev = ci;
       }
     }
-    L.finish_groups();
+    L.finish_streams();
     if (out->u64pool.empty()) out->u64pool.push_back(0);
     out->rule_engine = waf.engine == "On" ? ENGINE_ON : waf.engine == "Off" ? ENGINE_OFF : ENGINE_DETECTION_ONLY;
     out->body_access = waf.body_access;

@@ -27,12 +27,17 @@ struct Program {
   std::vector<uint8_t> strpool;
   std::vector<uint32_t> slot_names;  // (off, len) pairs into strpool
   std::vector<uint64_t> u64pool;     // union-automaton accept masks
-  std::vector<DGroup> groups;        // phase-A scan plan
-  std::vector<DScanDfa> sdfas;
+  std::vector<DStream> streams;      // phase-A scan plan
+  std::vector<DFilter> filters;
+  std::vector<DJob> jobs;
+  std::vector<DJobDfa> jdfas;
   std::vector<DPat> pats;
   std::vector<DScanVal> svals;
+  std::vector<uint8_t> images;
   uint32_t n_hit_slots = 0;
   uint32_t n_union_dfas = 0;
+  uint32_t max_img_bytes = 0;
+  std::string plan_json;             // human-readable scan plan (gi_ruleset_describe)
   std::vector<int32_t> exports;
   std::vector<std::string> export_names;
   uint32_t n_slots = 0, n_markers = 0;

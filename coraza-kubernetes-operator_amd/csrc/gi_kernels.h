@@ -31,15 +31,15 @@ struct DBatch {
   uint32_t* matched;
   unsigned long long* tally;  // gi_tally as 6 counters
   uint32_t* hits;             // phase-A hit words [ceil(n_hit_slots/32)][n_req]
-  uint8_t* tscratch;          // k_scan transformation buffers (2 x tcap per resident thread)
+  uint8_t* tscratch;          // k_match transformation buffers (2 x tcap per resident thread)
   uint32_t tcap;
 };
 
-// Resident thread count of k_scan on the current device (grid-stride width).
-uint32_t scan_resident_threads();
+// Resident thread count of k_match with lds_bytes of dynamic LDS per block.
+uint32_t scan_resident_threads(uint32_t lds_bytes);
 
 // k_collect -> k_scan -> k_eval on `stream`; ev (optional) = 2 events recorded
-// after k_collect and after k_scan.
+// after k_collect and after k_match.
 void launch_pipeline(const DProgram& P, const DBatch& B, uint32_t scan_threads, hipStream_t stream,
                      hipEvent_t* ev);
 

@@ -140,32 +140,54 @@ struct DRule {
 };
 
 // ------------------------------------------------------ phase-A scan plan
-// A scan group = one value source x key filter x exclusions x transformation
-// chain.  Every phase-A-eligible (rule link, target) pair contributes one
-// pattern to the group of its target; the group's patterns are packed into
-// union automata so each transformed value is scanned once per automaton.
-enum SrcKind : uint8_t { SRC_SINGLE = 1, SRC_FIELDS = 2 };
+// stream  = one transformation chain: every value some target of a phase-A
+//           rule link reads through that chain (values are transformed once
+//           per job and scanned by every automaton of the job);
+// filter  = one value source of the stream: a single variable, or a field
+//           kind set (key or value side) with a key selector + exclusions;
+// pattern = one phase-A-eligible rule link on the stream, admitted by the
+//           filters of its targets; a value feeds a pattern only through
+//           one of those filters;
+// job     = the automata of one stream whose tables fit one LDS image: a
+//           persistent workgroup loads the image once and sweeps requests.
+#define GI_MAX_FILTERS 32
+#define GI_JOB_LDS_BYTES 65536
+#define GI_NO_SINGLE 0xFF
 
-struct DGroup {
-  uint8_t src;        // SrcKind
-  uint8_t single;     // SingleId (SRC_SINGLE)
-  uint8_t kind_mask;  // 1 << FieldKind (SRC_FIELDS)
-  uint8_t names;      // test the key instead of the value
+struct DStream {
+  uint32_t tchain_off, tchain_len;
+  uint32_t filt_begin, filt_count;  // DFilter
+  uint8_t kind_mask;  // union of the field filters' kinds (1 << FieldKind)
+  uint8_t _pad[3];
+};
+
+struct DFilter {
+  uint8_t single;     // SingleId, or GI_NO_SINGLE for a field filter
+  uint8_t kind_mask;  // 1 << FieldKind
+  uint8_t names;      // the key is the value
   uint8_t key_mode;   // 0 none, 1 literal, 2 regex
   uint8_t ci;         // case-insensitive keys
-  uint8_t _pad[2];
+  uint8_t _pad[3];
   int32_t key_dfa;
   uint32_t key_off, key_len;
   uint32_t exc_begin, exc_count;
-  uint32_t tchain_off, tchain_len;
-  uint32_t sdfa_begin, sdfa_count;  // DScanDfa
-  uint32_t val_begin, val_count;    // DScanVal
 };
 
-struct DScanDfa {
-  int32_t dfa;        // multi (union) or single sticky automaton
+struct DJob {
+  uint32_t stream;
+  uint32_t img_off, img_bytes;     // LDS image (u8 image pool, 16-B aligned)
+  uint32_t jdfa_begin, jdfa_count; // DJobDfa
+  uint32_t val_begin, val_count;   // DScanVal
+};
+
+struct DJobDfa {
+  int32_t dfa;        // DDfa (start, classes, accept masks, rune ranges)
+  int32_t lds_trans;  // byte offset of the transition table in the image, -1: global
+  int32_t lds_amap;   // byte offset of the 128/256-entry class map in the image
+  int32_t lds_combo;  // byte offset of the per-class combo table (multi)
   uint32_t pat_begin; // DPat, n_pat entries (bit k of the match mask)
   uint32_t n_pat;
+  uint32_t fmask_off; // u64 pool: per stream filter, the patterns it admits
   uint32_t _pad;
   uint64_t neg_mask;  // patterns whose operator is negated
 };
@@ -177,8 +199,10 @@ struct DPat {
 struct DScanVal {     // @validateByteRange / @validateUrlEncoding / @validateUtf8Encoding
   uint8_t kind;
   uint8_t negate;
-  uint16_t _pad;
+  uint8_t _pad[2];
+  uint32_t fmask;     // admitting filters
   uint32_t slot;
+  uint32_t _pad2;
   uint32_t bits[8];
 };
 
@@ -265,12 +289,16 @@ struct DProgram {
   const uint32_t* lower_pairs;  // unicode.ToLower table (rune, lower) pairs
   const uint32_t* slot_names;   // (off, len) into strpool per TX slot
   const uint64_t* u64pool;      // union-automaton accept masks
-  const DGroup* groups;
-  const DScanDfa* sdfas;
+  const DStream* streams;
+  const DFilter* filters;
+  const DJob* jobs;
+  const DJobDfa* jdfas;
   const DPat* pats;
   const DScanVal* svals;
-  uint32_t n_groups;
+  const uint8_t* images;        // LDS images of the jobs
+  uint32_t n_jobs;
   uint32_t n_hit_slots;
+  uint32_t max_img_bytes;
   uint32_t n_lower_pairs;
   uint32_t n_top;
   uint32_t n_slots;

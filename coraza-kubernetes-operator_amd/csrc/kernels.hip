@@ -1386,7 +1386,7 @@ __device__ void eval_phase(Tx& t, uint8_t phase) {
 
 // ------------------------------------------------------ per-request state
 // Written by k_collect at the start of the request's HBM scratch region and
-// read by k_scan / k_eval.
+// read by k_match / k_eval.
 struct ReqHdr {
   uint32_t nf;          // fields so far: [ARG_GET | HEADER | COOKIE | ARG_POST]
   uint32_t nb;          // bytes arena used
@@ -1519,20 +1519,53 @@ __global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
   H->body_proc = t.body_proc;
 }
 
-// ------------------------------------------------ stage 2: k_scan (phase A)
-// Multi-pattern scan of one union automaton over a value: the set of the
-// automaton's patterns that match somewhere in it.
-__device__ uint64_t dfa_scan(const DProgram& P, int32_t id, const uint8_t* s, uint32_t n) {
-  const DDfa d = P.dfas[id];
-  if (!d.multi) return dfa_match(P, id, s, n, false) ? 1ull : 0ull;
-  const uint16_t* __restrict__ tr = P.trans + d.trans_off;
-  const uint8_t* __restrict__ amap = P.u8pool + d.amap_off;
-  const uint8_t* __restrict__ combo = P.u8pool + d.combo_off;
-  const uint64_t* __restrict__ acc = P.u64pool + d.acc_off;
+// ------------------------------------------------ stage 2: k_match (phase A)
+// Persistent kernel over units (job, tile of 256 requests), job-major.  A
+// workgroup copies the job's automaton image (<= 64 KB) into LDS once per job
+// change, then each thread walks one request: the stream's values are key-
+// filtered, transformed once and run through every automaton of the job whose
+// admitted patterns intersect the value's filter-pass mask.
+
+__device__ __forceinline__ uint32_t rune_class(const DProgram& P, const DDfa& d, uint32_t r) {
+  if (d.nonascii_uniform) return d.nonascii_cls;
+  const uint32_t* nr = P.nranges + d.nr_off;
+  uint32_t lo = 0, hi = d.nr_cnt;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (nr[mid * 3 + 1] < r) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < d.nr_cnt && nr[lo * 3] <= r) ? nr[lo * 3 + 2] : 0u;
+}
+
+// Bit k of the result: pattern k of the automaton matches somewhere in s.
+// Single (sticky) automata return bit 0 only.
+__device__ __forceinline__ uint64_t jdfa_scan(const DProgram& P, const DDfa& d, const uint16_t* __restrict__ tr,
+                                              const uint8_t* __restrict__ amap, const uint8_t* __restrict__ combo,
+                                              const uint8_t* __restrict__ s, uint32_t n) {
   const uint32_t ncls = d.n_classes;
   uint32_t st = d.start;
-  uint64_t m = 0;
   uint32_t i = 0;
+  if (!d.multi) {
+    while (i < n) {
+      if (st == d.accept) return 1;
+      const uint8_t c = s[i];
+      uint32_t cls;
+      if (d.byte_mode || c < 0x80) {
+        cls = amap[c];
+        i++;
+      } else {
+        uint32_t w;
+        const uint32_t rr = decode_rune(s, n, i, &w);
+        i += w;
+        cls = rune_class(P, d, rr);
+      }
+      st = tr[st * ncls + cls];
+    }
+    return P.u8pool[d.endacc_off + st] != 0 ? 1ull : 0ull;
+  }
+  const uint64_t* __restrict__ acc = P.u64pool + d.acc_off;
+  uint64_t m = 0;
   while (i < n) {
     const uint8_t c = s[i];
     uint32_t cls;
@@ -1543,19 +1576,7 @@ __device__ uint64_t dfa_scan(const DProgram& P, int32_t id, const uint8_t* s, ui
       uint32_t w;
       const uint32_t rr = decode_rune(s, n, i, &w);
       i += w;
-      if (d.nonascii_uniform) {
-        cls = d.nonascii_cls;
-      } else {
-        const uint32_t* nr = P.nranges + d.nr_off;
-        uint32_t lo = 0, hi = d.nr_cnt;
-        cls = 0;
-        while (lo < hi) {
-          uint32_t mid = (lo + hi) >> 1;
-          if (nr[mid * 3 + 1] < rr) lo = mid + 1;
-          else hi = mid;
-        }
-        if (lo < d.nr_cnt && nr[lo * 3] <= rr) cls = nr[lo * 3 + 2];
-      }
+      cls = rune_class(P, d, rr);
     }
     const uint16_t tv = tr[st * ncls + cls];
     if (tv & 0x8000) m |= acc[(uint64_t)st * 5 + combo[cls]];
@@ -1595,49 +1616,17 @@ __device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
   atomicOr(&B.hits[(uint64_t)(slot >> 5) * B.n_req + r], 1u << (slot & 31));
 }
 
-// transform (chain) + scan one value of a group; hit bits are emitted per
-// value (matches are rare); "maybe" (every pattern) on any overflow.
-__device__ void scan_value(const DProgram& P, const DBatch& B, uint32_t r, const DGroup& G, const uint8_t* v,
-                           uint32_t vn, uint8_t* s0, uint8_t* s1, uint32_t cap) {
-  const uint8_t* cur = v;
-  uint32_t cn = vn;
-  bool maybe = false;
-  for (uint32_t k = 0; k < G.tchain_len; k++) {
-    uint8_t* dst = (cur == s0) ? s1 : s0;
-    int64_t m = apply_transform(P, P.tchains[G.tchain_off + k], cur, cn, dst, cap);
-    if (m < 0) {
-      maybe = true;
-      break;
-    }
-    cur = dst;
-    cn = (uint32_t)m;
-  }
-  for (uint32_t d = 0; d < G.sdfa_count; d++) {
-    const DScanDfa sd = P.sdfas[G.sdfa_begin + d];
-    uint64_t m = maybe ? ~0ull : (dfa_scan(P, sd.dfa, cur, cn) ^ sd.neg_mask);
-    m &= sd.n_pat >= 64 ? ~0ull : ((1ull << sd.n_pat) - 1);
-    while (m) {
-      const int k = __ffsll((unsigned long long)m) - 1;
-      m &= m - 1;
-      set_hit(B, P.pats[sd.pat_begin + k].slot, r);
-    }
-  }
-  for (uint32_t k = 0; k < G.val_count; k++) {
-    const DScanVal sv = P.svals[G.val_begin + k];
-    if (maybe || (validate_op(sv.kind, sv.bits, cur, cn) != (sv.negate != 0))) set_hit(B, sv.slot, r);
-  }
-}
-
-__device__ inline bool group_key_ok(const DProgram& P, const DGroup& G, const Field& f) {
-  if (G.key_mode == 1) {
-    if (G.ci ? !eq_ascii_ci(f.k, f.kn, P.strpool + G.key_off, G.key_len)
-             : !eq_bytes(f.k, f.kn, P.strpool + G.key_off, G.key_len))
+// Key filter of a rule target (selector + exclusions), as field_in() applies it.
+__device__ inline bool filter_ok(const DProgram& P, const DFilter& F, const Field& f) {
+  if (F.key_mode == 1) {
+    if (F.ci ? !eq_ascii_ci(f.k, f.kn, P.strpool + F.key_off, F.key_len)
+             : !eq_bytes(f.k, f.kn, P.strpool + F.key_off, F.key_len))
       return false;
-  } else if (G.key_mode == 2) {
-    if (!dfa_match(P, G.key_dfa, f.k, f.kn, G.ci != 0)) return false;
+  } else if (F.key_mode == 2) {
+    if (!dfa_match(P, F.key_dfa, f.k, f.kn, F.ci != 0)) return false;
   }
-  for (uint32_t e = 0; e < G.exc_count; e++) {
-    const DExc x = P.excs[G.exc_begin + e];
+  for (uint32_t e = 0; e < F.exc_count; e++) {
+    const DExc x = P.excs[F.exc_begin + e];
     if (x.dfa >= 0) {
       if (dfa_match(P, x.dfa, f.k, f.kn, true)) return false;
     } else if (eq_ascii_ci(f.k, f.kn, P.strpool + x.off, x.len)) {
@@ -1647,40 +1636,116 @@ __device__ inline bool group_key_ok(const DProgram& P, const DGroup& G, const Fi
   return true;
 }
 
-// One work item = (scan group g, request r), group-major so a wavefront
-// walks 64 requests through the same automata.  Grid-stride over resident
-// threads; each thread owns two transformation buffers of B.tcap bytes.
-__global__ void __launch_bounds__(256) k_scan(DProgram P, DBatch B, uint64_t n_items) {
-  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
-  uint8_t* s0 = B.tscratch + tid * 2ull * B.tcap;
+// transform (chain) + match one value against the job; hit bits are emitted
+// per value (matches are rare); "maybe" (every admitted pattern) on overflow.
+__device__ void match_value(const DProgram& P, const DBatch& B, uint32_t r, const DStream& S, const DJob& J,
+                            const uint8_t* img, uint32_t fm, const uint8_t* v, uint32_t vn, uint8_t* s0,
+                            uint8_t* s1) {
+  const uint8_t* cur = v;
+  uint32_t cn = vn;
+  bool maybe = false;
+  bool ready = false;
+  for (uint32_t q = 0; q < J.jdfa_count + J.val_count; q++) {
+    uint64_t allowed = 0;
+    DJobDfa jd;
+    if (q < J.jdfa_count) {
+      jd = P.jdfas[J.jdfa_begin + q];
+      for (uint32_t f = fm; f; f &= f - 1) allowed |= P.u64pool[jd.fmask_off + (__ffs(f) - 1)];
+      if (!allowed) continue;
+    } else if (!(fm & P.svals[J.val_begin + q - J.jdfa_count].fmask)) {
+      continue;
+    }
+    if (!ready) {
+      ready = true;
+      for (uint32_t k = 0; k < S.tchain_len; k++) {
+        uint8_t* dst = (cur == s0) ? s1 : s0;
+        int64_t m = apply_transform(P, P.tchains[S.tchain_off + k], cur, cn, dst, B.tcap);
+        if (m < 0) {
+          maybe = true;
+          break;
+        }
+        cur = dst;
+        cn = (uint32_t)m;
+      }
+    }
+    if (q < J.jdfa_count) {
+      uint64_t m = allowed;
+      if (!maybe) {
+        const DDfa d = P.dfas[jd.dfa];
+        uint64_t x;
+        if (jd.lds_trans >= 0) {
+          x = jdfa_scan(P, d, (const uint16_t*)(img + jd.lds_trans), img + jd.lds_amap,
+                        img + (jd.lds_combo >= 0 ? jd.lds_combo : 0), cur, cn);
+        } else {
+          x = jdfa_scan(P, d, P.trans + d.trans_off, P.u8pool + d.amap_off, P.u8pool + d.combo_off, cur, cn);
+        }
+        m &= x ^ jd.neg_mask;
+      }
+      while (m) {
+        const int k = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        set_hit(B, P.pats[jd.pat_begin + k].slot, r);
+      }
+    } else {
+      const DScanVal& sv = P.svals[J.val_begin + q - J.jdfa_count];
+      if (maybe || (validate_op(sv.kind, sv.bits, cur, cn) != (sv.negate != 0))) set_hit(B, sv.slot, r);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_match(DProgram P, DBatch B, uint32_t n_tiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t img[];
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint8_t* s0 = B.tscratch + (uint64_t)tid * 2ull * B.tcap;
   uint8_t* s1 = s0 + B.tcap;
-  for (uint64_t item = tid; item < n_items; item += nthreads) {
-    const uint32_t g = (uint32_t)(item / B.n_req);
-    const uint32_t r = (uint32_t)(item - (uint64_t)g * B.n_req);
-    const DGroup G = P.groups[g];
+  const uint64_t n_units = (uint64_t)P.n_jobs * n_tiles;
+  uint32_t loaded = 0xFFFFFFFFu;
+  for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
+    const uint32_t j = (uint32_t)(u / n_tiles);
+    const uint32_t tile = (uint32_t)(u - (uint64_t)j * n_tiles);
+    const DJob J = P.jobs[j];
+    if (j != loaded) {  // block-uniform
+      __syncthreads();
+      const uint4* src = (const uint4*)(P.images + J.img_off);
+      for (uint32_t k = threadIdx.x; k < J.img_bytes / 16; k += blockDim.x) ((uint4*)img)[k] = src[k];
+      __syncthreads();
+      loaded = j;
+    }
+    const uint32_t r = tile * 256 + threadIdx.x;
+    if (r >= B.n_req) continue;
     const uint8_t* base = B.scratch + B.layout[r].base;
     const ReqHdr* H = (const ReqHdr*)base;
     if (H->flags & GI_REQ_ERROR_MASK) continue;
-    if (G.src == SRC_SINGLE) {
-      const Str v = H->single[G.single];
-      scan_value(P, B, r, G, v.p, v.n, s0, s1, B.tcap);
-    } else {
-      const Field* F = (const Field*)(base + 256);
-      const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck;
-      for (int kind = FK_ARG_GET; kind <= FK_COOKIE; kind++) {
-        if (!((G.kind_mask >> kind) & 1)) continue;
-        uint32_t b = 0, e = 0;
-        if (kind == FK_ARG_GET) { b = 0; e = n_get; }
-        else if (kind == FK_HEADER) { b = n_get; e = n_get + n_hdr; }
-        else if (kind == FK_COOKIE) { b = n_get + n_hdr; e = n_get + n_hdr + n_ck; }
-        else continue;
-        for (uint32_t i = b; i < e; i++) {
-          const Field f = F[i];
-          if (!group_key_ok(P, G, f)) continue;
-          if (G.names) scan_value(P, B, r, G, f.k, f.kn, s0, s1, B.tcap);
-          else scan_value(P, B, r, G, f.v, f.vn, s0, s1, B.tcap);
+    const DStream S = P.streams[J.stream];
+    for (uint32_t k = 0; k < S.filt_count; k++) {
+      const uint8_t sg = P.filters[S.filt_begin + k].single;
+      if (sg == GI_NO_SINGLE) continue;
+      const Str v = H->single[sg];
+      match_value(P, B, r, S, J, img, 1u << k, v.p, v.n, s0, s1);
+    }
+    if (!S.kind_mask) continue;
+    const Field* F = (const Field*)(base + 256);
+    const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck;
+    for (int kind = FK_ARG_GET; kind <= FK_COOKIE; kind++) {
+      if (!((S.kind_mask >> kind) & 1)) continue;
+      uint32_t b = 0, e = 0;
+      if (kind == FK_ARG_GET) { b = 0; e = n_get; }
+      else if (kind == FK_HEADER) { b = n_get; e = n_get + n_hdr; }
+      else if (kind == FK_COOKIE) { b = n_get + n_hdr; e = n_get + n_hdr + n_ck; }
+      else continue;
+      for (uint32_t i = b; i < e; i++) {
+        const Field f = F[i];
+        uint32_t fv = 0, fk = 0;
+        for (uint32_t k = 0; k < S.filt_count; k++) {
+          const DFilter Fl = P.filters[S.filt_begin + k];
+          if (Fl.single != GI_NO_SINGLE || !((Fl.kind_mask >> kind) & 1)) continue;
+          if (filter_ok(P, Fl, f)) {
+            if (Fl.names) fk |= 1u << k;
+            else fv |= 1u << k;
+          }
         }
+        if (fv) match_value(P, B, r, S, J, img, fv, f.v, f.vn, s0, s1);
+        if (fk) match_value(P, B, r, S, J, img, fk, f.k, f.kn, s0, s1);
       }
     }
   }
@@ -1792,13 +1857,13 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
   if (threadIdx.x < 6) atomicAdd(&B.tally[threadIdx.x], red[threadIdx.x]);
 }
 
-uint32_t scan_resident_threads() {
+uint32_t scan_resident_threads(uint32_t lds_bytes) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, dev);
   int per_cu = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scan, 256, 0);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_match, 256, lds_bytes);
   if (per_cu < 1) per_cu = 1;
   return (uint32_t)prop.multiProcessorCount * (uint32_t)per_cu * 256u;
 }
@@ -1809,12 +1874,13 @@ void launch_pipeline(const DProgram& P, const DBatch& B, uint32_t scan_threads, 
   const uint32_t cb = (B.n_req + 255) / 256;
   hipLaunchKernelGGL(k_collect, dim3(cb), dim3(256), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[0], stream);
-  const uint64_t items = (uint64_t)P.n_groups * B.n_req;
-  if (items) {
-    uint64_t blocks = (items + 255) / 256;
+  const uint32_t n_tiles = (B.n_req + 255) / 256;
+  const uint64_t units = (uint64_t)P.n_jobs * n_tiles;
+  if (units) {
+    uint64_t blocks = units;
     const uint64_t maxb = scan_threads / 256;
     if (blocks > maxb) blocks = maxb;
-    hipLaunchKernelGGL(k_scan, dim3((uint32_t)blocks), dim3(256), 0, stream, P, B, items);
+    hipLaunchKernelGGL(k_match, dim3((uint32_t)blocks), dim3(256), P.max_img_bytes, stream, P, B, n_tiles);
   }
   if (ev) (void)hipEventRecord(ev[1], stream);
   hipLaunchKernelGGL(k_eval, dim3((B.n_req + 127) / 128), dim3(128), 0, stream, P, B);

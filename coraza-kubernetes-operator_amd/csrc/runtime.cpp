@@ -117,14 +117,18 @@ int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ru
   rs->info.n_links = (uint32_t)P.rules.size();
   rs->info.n_dfas = (uint32_t)P.dfas.size();
   rs->info.n_tx_slots = P.n_slots;
-  rs->info.n_scan_groups = (uint32_t)P.groups.size();
+  rs->info.n_scan_jobs = (uint32_t)P.jobs.size();
+  rs->info.n_scan_streams = (uint32_t)P.streams.size();
   rs->info.n_hit_slots = P.n_hit_slots;
   rs->info.n_union_dfas = P.n_union_dfas;
   rs->info.program_bytes = P.rules.size() * sizeof(DRule) + P.vars.size() * sizeof(DVarRef) +
                            P.ops.size() * sizeof(DOp) + P.acts.size() * sizeof(DAction) +
                            P.trans.size() * 2 + P.u8pool.size() + P.nranges.size() * 4 + P.strpool.size() +
                            P.dfas.size() * sizeof(DDfa) + P.tparts.size() * sizeof(DTmplPart) +
-                           P.u64pool.size() * 8 + P.groups.size() * sizeof(DGroup) + P.sdfas.size() * sizeof(DScanDfa);
+                           P.u64pool.size() * 8 + P.streams.size() * sizeof(DStream) +
+                           P.filters.size() * sizeof(DFilter) + P.jobs.size() * sizeof(DJob) +
+                           P.jdfas.size() * sizeof(DJobDfa) + P.pats.size() * sizeof(DPat) +
+                           P.svals.size() * sizeof(DScanVal) + P.images.size();
   *out = rs;
   return GI_OK;
 }
@@ -147,6 +151,17 @@ int gi_ruleset_export_name(const gi_ruleset* rs, uint32_t i, char* buf, size_t c
   return GI_OK;
 }
 
+int64_t gi_ruleset_describe(const gi_ruleset* rs, char* buf, size_t cap) {
+  if (!rs) return GI_EINVAL;
+  const std::string& s = rs->prog.plan_json;
+  if (buf && cap) {
+    size_t k = std::min(cap - 1, s.size());
+    memcpy(buf, s.data(), k);
+    buf[k] = 0;
+  }
+  return (int64_t)s.size();
+}
+
 int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx** out) {
   if (!rs || !out) return GI_EINVAL;
   *out = nullptr;
@@ -167,7 +182,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
     return GI_ENODEV;
   }
   const Program& P = rs->prog;
-  c->pbufs.resize(24);
+  c->pbufs.resize(32);
   std::vector<uint32_t> lower;
   lower.reserve(GI_N_LOWER_PAIRS * 2);
   for (int i = 0; i < GI_N_LOWER_PAIRS; i++) {
@@ -200,8 +215,11 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   UP(lower_pairs, lower, uint32_t)
   UP(slot_names, P.slot_names, uint32_t)
   UP(u64pool, P.u64pool, uint64_t)
-  UP(groups, P.groups, DGroup)
-  UP(sdfas, P.sdfas, DScanDfa)
+  UP(streams, P.streams, DStream)
+  UP(filters, P.filters, DFilter)
+  UP(jobs, P.jobs, DJob)
+  UP(jdfas, P.jdfas, DJobDfa)
+  UP(images, P.images, uint8_t)
   UP(pats, P.pats, DPat)
   UP(svals, P.svals, DScanVal)
 #undef UP
@@ -219,9 +237,10 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->prog.rule_engine = P.rule_engine;
   c->prog.body_access = P.body_access;
   c->prog.body_limit = P.body_limit;
-  c->prog.n_groups = (uint32_t)P.groups.size();
+  c->prog.n_jobs = (uint32_t)P.jobs.size();
+  c->prog.max_img_bytes = P.max_img_bytes;
   c->prog.n_hit_slots = P.n_hit_slots;
-  c->scan_threads = scan_resident_threads();
+  c->scan_threads = scan_resident_threads(P.max_img_bytes);
   if (c->tscratch.ensure((size_t)c->scan_threads * 2 * c->tcap) != hipSuccess) {
     gi_ctx_free(c);
     return GI_ENOMEM;

@@ -21,6 +21,7 @@ every inspection call raises.
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
@@ -58,7 +59,7 @@ VERDICT_DT = np.dtype([("rule_id", "<i4"), ("status", "<i4"), ("action", "u1"), 
 assert REQUEST_DT.itemsize == 72 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 80
 
 EXPORTED_SYMBOLS = (
-    "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name",
+    "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name", "gi_ruleset_describe",
     "gi_ctx_create", "gi_ctx_free", "gi_last_error", "gi_inspect_batch", "gi_stage_batch",
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
     "gi_ctx_stream", "gi_selftest_regex",
@@ -84,8 +85,8 @@ class _CompileOpts(ctypes.Structure):
 class _Info(ctypes.Structure):
     _fields_ = [("n_rules", ctypes.c_uint32), ("n_links", ctypes.c_uint32), ("n_dfas", ctypes.c_uint32),
                 ("n_tx_slots", ctypes.c_uint32), ("program_bytes", ctypes.c_uint64),
-                ("n_scan_groups", ctypes.c_uint32), ("n_hit_slots", ctypes.c_uint32),
-                ("n_union_dfas", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+                ("n_scan_jobs", ctypes.c_uint32), ("n_hit_slots", ctypes.c_uint32),
+                ("n_union_dfas", ctypes.c_uint32), ("n_scan_streams", ctypes.c_uint32)]
 
 
 class _Batch(ctypes.Structure):
@@ -128,6 +129,8 @@ def load_library(path: str = LIB_PATH):
     lib.gi_ruleset_free.argtypes = [vp]
     lib.gi_ruleset_info_get.argtypes = [vp, ctypes.POINTER(_Info)]
     lib.gi_ruleset_export_name.argtypes = [vp, u32, ctypes.c_char_p, sz]
+    lib.gi_ruleset_describe.argtypes = [vp, ctypes.c_char_p, sz]
+    lib.gi_ruleset_describe.restype = ctypes.c_int64
     lib.gi_ctx_create.argtypes = [vp, ctypes.c_int, u32, ctypes.POINTER(vp)]
     lib.gi_ctx_free.argtypes = [vp]
     lib.gi_last_error.argtypes = [vp]
@@ -179,6 +182,14 @@ class Ruleset:
         info = _Info()
         lib.gi_ruleset_info_get(h, ctypes.byref(info))
         self.info = {k: getattr(info, k) for k, _ in _Info._fields_}
+
+    def describe(self):
+        """The phase-A scan plan as a dict (streams, jobs, automata sizes)."""
+        lib = self._lib
+        n = lib.gi_ruleset_describe(self._h, None, 0)
+        buf = ctypes.create_string_buffer(int(n) + 1)
+        lib.gi_ruleset_describe(self._h, buf, len(buf))
+        return json.loads(buf.value.decode())
 
     def __del__(self):
         h = getattr(self, "_h", None)

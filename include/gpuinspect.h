@@ -83,10 +83,10 @@ typedef struct {
   uint32_t n_dfas;
   uint32_t n_tx_slots;
   uint64_t program_bytes; /* device-resident artifact size */
-  uint32_t n_scan_groups; /* phase-A groups (source x key filter x transformation chain) */
+  uint32_t n_scan_jobs;   /* phase-A jobs (one LDS-resident automaton image each) */
   uint32_t n_hit_slots;   /* rule links evaluated data-parallel in phase A */
   uint32_t n_union_dfas;  /* multi-pattern automata among n_dfas */
-  uint32_t _pad;
+  uint32_t n_scan_streams; /* phase-A streams (value source x transformation chain) */
 } gi_ruleset_info;
 
 /* A byte range inside gi_batch.data. */
@@ -165,6 +165,10 @@ void gi_ruleset_free(gi_ruleset* rs);
 int gi_ruleset_info_get(const gi_ruleset* rs, gi_ruleset_info* out);
 /* ids of the exported TX names, in order (for result decoding) */
 int gi_ruleset_export_name(const gi_ruleset* rs, uint32_t i, char* buf, size_t cap);
+/* JSON description of the phase-A scan plan (streams, jobs, automata sizes).
+ * Writes at most cap bytes (NUL-terminated); returns the full length
+ * (excluding the NUL), or a negative GI_* code. */
+int64_t gi_ruleset_describe(const gi_ruleset* rs, char* buf, size_t cap);
 
 /* ------------------------------------------------------------ context */
 int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx** out);
