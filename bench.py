@@ -28,6 +28,7 @@ for p in (ROOT, PKG):
 import numpy as np  # noqa: E402
 
 import gpuinspect  # noqa: E402
+import shard  # noqa: E402
 import traffic  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
@@ -104,24 +105,18 @@ def main():
     rs = gpuinspect.Ruleset(text)
     eng = gpuinspect.Engine(rs, device=local, matched_cap=args.matched_cap)
     t_gen = time.perf_counter()
-    batch = traffic.TrafficGen(traffic.SEED + rank).batch(n_req, post_frac=post_frac)
+    batch = traffic.TrafficGen(shard.shard_seed(traffic.SEED, rank)).batch(n_req, post_frac=post_frac)
     t_gen = time.perf_counter() - t_gen
     raw = batch.raw_bytes()
     eng.stage(batch)
 
-    if dist is not None:
-        import torch
-        tally_dev = torch.zeros(6, dtype=torch.int64, device="cuda")
-        gathered = torch.zeros(6 * world, dtype=torch.int64, device="cuda")
+    gather = shard.TallyGather(dist, world, "cuda") if dist is not None else None
 
     def step():
         eng.run()
         eng.sync()
-        if dist is not None:
-            t = eng.tally()
-            tally_dev.copy_(torch.tensor([t[k] for k in ("n_req", "n_interrupted", "n_matched_any", "n_error",
-                                                         "bytes_scanned", "matched_total")], dtype=torch.int64))
-            dist.all_gather_into_tensor(gathered, tally_dev)
+        if gather is not None:
+            gather.push(eng.tally())
 
     for _ in range(args.warmup):
         step()
@@ -129,14 +124,15 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
     eng.sync()
-    kern_ms, stage_ms = [], {"k_collect": [], "k_match": [], "k_eval": []}
+    kern_ms, stage_ms = [], {"k_collect": [], "k_stream": [], "k_scan": [], "k_eval": []}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         st = eng.stats()
         kern_ms.append(st["last_kernel_ms"])
         stage_ms["k_collect"].append(st["last_collect_ms"])
-        stage_ms["k_match"].append(st["last_scan_ms"])
+        stage_ms["k_stream"].append(st["last_stream_ms"])
+        stage_ms["k_scan"].append(st["last_scan_ms"])
         stage_ms["k_eval"].append(st["last_eval_ms"])
     eng.sync()
     if dist is not None:
@@ -144,12 +140,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-        tot = gathered.view(world, 6).sum(0).tolist()
-        total_req = int(tot[0])
-        total_bytes = int(tot[4])
+        elapsed = shard.max_over_ranks(dist, elapsed, "cuda")
+        tot = gather.total()
+        total_req = tot["n_req"]
+        total_bytes = tot["bytes_scanned"]
     else:
         t = eng.tally()
         total_req, total_bytes = int(t["n_req"]), int(t["bytes_scanned"])
@@ -168,11 +162,12 @@ def main():
     body_bytes = int(batch.reqs["body"]["len"].sum())
     hit_words = (rs.info["n_hit_slots"] + 31) // 32
     alg = {
-        "k_match": raw - body_bytes + 4 * hit_words * batch.n_req,
+        "k_scan": raw - body_bytes + 4 * hit_words * batch.n_req,
+        "k_stream": raw - body_bytes,
         "k_eval": raw + 80 * batch.n_req + 4 * int(tally["matched_total"]),
         "k_collect": raw - body_bytes,
     }
-    dom = max(("k_match", "k_eval"), key=lambda k: avg_stage[k])
+    dom = max(("k_stream", "k_scan", "k_eval"), key=lambda k: avg_stage[k])
     alg_bytes = alg[dom]
     achieved = alg_bytes / (avg_stage[dom] * 1e-3) / 1e9
     out = {
@@ -193,6 +188,7 @@ def main():
                    "rules": rs.info["n_rules"], "dfas": rs.info["n_dfas"]},
         "gb_per_s_scanned": round(gbs, 3),
         "interrupted_frac": round(tally["n_interrupted"] / max(tally["n_req"], 1), 4),
+        "pa_void_requests": int(tally["n_pa_void"]),
         "error_requests": int(tally["n_error"]),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,

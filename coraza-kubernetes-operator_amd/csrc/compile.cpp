@@ -835,6 +835,7 @@ struct Lower {
         } else {
           x.off = str(e.first);
           x.len = (uint32_t)e.first.size();
+          x.hash = gi_fnv1a((const uint8_t*)e.first.data(), x.len, true);
         }
         P->excs.push_back(x);
       }
@@ -916,9 +917,11 @@ struct Lower {
     std::vector<std::string> phrases;
     uint32_t fmask;  // admitting filters of the stream
   };
+  std::map<std::string, uint32_t> gfilter_ids;  // global (deduplicated) filters: key -> id
   struct StreamBuild {
     DStream s;
     std::vector<DFilter> filters;
+    std::vector<uint8_t> gids;  // global filter id of each stream filter
     std::vector<std::string> fkeys;
     std::vector<PatEntry> pats;
     std::vector<DScanVal> vals;
@@ -983,6 +986,7 @@ struct Lower {
         f.key_dfa = vr.key_dfa;
         f.key_off = vr.key_off;
         f.key_len = vr.key_len;
+        if (vr.key_mode == 1) f.key_hash = gi_fnv1a(&P->strpool[vr.key_off], vr.key_len, false);
         f.exc_begin = vr.exc_begin;
         f.exc_count = vr.exc_count;
       }
@@ -1017,6 +1021,19 @@ struct Lower {
           si = it->second;
           fid = (uint32_t)(fit - sb.fkeys.begin());
         } else if (sb.fkeys.size() < GI_MAX_FILTERS) {
+          auto git = gfilter_ids.find(fkey);
+          if (git == gfilter_ids.end()) {
+            if (gfilter_ids.size() >= GI_MAX_GFILTERS) unsup("more than 64 distinct phase-A variable filters");
+            git = gfilter_ids.emplace(fkey, (uint32_t)P->filters.size()).first;
+            P->filters.push_back(f);
+            if (f.single != GI_NO_SINGLE) {
+              P->item_singles |= 1u << f.single;
+            } else {
+              for (int k = FK_ARG_GET; k <= FK_COOKIE; k++)
+                if ((f.kind_mask >> k) & 1) P->item_sides[k] |= f.names ? 2 : 1;
+            }
+          }
+          sb.gids.push_back((uint8_t)git->second);
           sb.fkeys.push_back(fkey);
           sb.filters.push_back(f);
           sb.s.kind_mask |= f.kind_mask;
@@ -1074,11 +1091,26 @@ struct Lower {
     std::vector<const PatEntry*> pes;
   };
 
+  static uint32_t al16(uint32_t x) { return (x + 15) & ~15u; }
+  // LDS footprint of one automaton in a job image (see DJob in gi_program.h)
   static uint32_t img_bytes(const Dfa& d) {
-    uint32_t t = (d.n_states * d.n_classes * 2 + 15) & ~15u;
-    uint32_t a = ((uint32_t)d.amap.size() + 15) & ~15u;
-    uint32_t c = ((uint32_t)d.cls_combo.size() + 15) & ~15u;
-    return t + a + c;
+    uint32_t t = al16(d.n_states * d.n_classes * 2);
+    uint32_t a = al16((uint32_t)d.amap.size());
+    uint32_t c = d.multi ? al16((uint32_t)d.cls_combo.size()) : 0;
+    uint32_t e = al16(d.n_states * (d.multi ? 8 : 1));
+    return t + a + c + e;
+  }
+  // automaton fits an LDS image at all (u16 state ids with the union flag bit,
+  // classes addressable through the joint u8-per-automaton class map)
+  static bool img_ok(const Dfa& d) { return d.n_states < 0x8000 && d.n_classes <= 255; }
+  static bool lds_ok(const Dfa& d, uint32_t nfilt) {
+    return img_ok(d) && GI_JAMAP_BYTES + img_bytes(d) + al16(nfilt * 8) + al16(d.n_pat * 4) <= GI_BIG_LDS_BYTES;
+  }
+  void img_put(uint32_t img_off, const void* p, size_t n, int32_t* at) {
+    *at = (int32_t)(P->images.size() - img_off);
+    const uint8_t* b = (const uint8_t*)p;
+    P->images.insert(P->images.end(), b, b + n);
+    P->images.resize(img_off + al16((uint32_t)(P->images.size() - img_off)), 0);
   }
 
   void finish_streams() {
@@ -1117,6 +1149,12 @@ struct Lower {
           autos.push_back({std::move(d), {&pe}});
           continue;
         }
+        if (pe.negate) {  // negated operators stay out of union automata (the scan emits union hits eagerly)
+          Dfa single;
+          if (!build_regex_dfa(*re, &single, &err, cap)) unsup("regex " + pe.rx + ": " + err);
+          autos.push_back({std::move(single), {&pe}});
+          continue;
+        }
         Dfa trial;
         cur.push_back(re.get());
         curp.push_back(&pe);
@@ -1146,10 +1184,15 @@ struct Lower {
       flush();
       // 2. stream record
       DStream s = sb.s;
-      s.filt_begin = (uint32_t)P->filters.size();
+      s.filt_begin = (uint32_t)P->sfilt.size();
       s.filt_count = (uint32_t)sb.filters.size();
-      P->filters.insert(P->filters.end(), sb.filters.begin(), sb.filters.end());
+      P->sfilt.insert(P->sfilt.end(), sb.gids.begin(), sb.gids.end());
       const uint32_t sid = (uint32_t)P->streams.size();
+      s.val_begin = (uint32_t)P->svals.size();
+      s.val_count = (uint32_t)sb.vals.size();
+      P->svals.insert(P->svals.end(), sb.vals.begin(), sb.vals.end());
+      s.job_begin = (uint32_t)P->jobs.size();
+      s.collapse = 1;  // cleared below by any automaton that tells non-ASCII runes apart
       P->streams.push_back(s);
       if (!first_s) js << ",";
       first_s = false;
@@ -1164,79 +1207,116 @@ struct Lower {
       }
       js << "]"
          << ",\"vals\":" << sb.vals.size() << ",\"jobs\":[";
-      // 3. jobs: pack automata into LDS images
+      // 3. jobs: pack up to GI_JOB_MAX_DFA automata per LDS image
+      const uint32_t nf = s.filt_count;
       size_t a = 0;
       bool first_j = true;
-      bool vals_done = sb.vals.empty();
-      while (a < autos.size() || !vals_done) {
+      while (a < autos.size()) {
+        // choose the automata of this job
+        std::vector<size_t> pick;
+        bool lds = true;
+        uint32_t need = GI_JAMAP_BYTES;
+        while (a < autos.size() && pick.size() < GI_JOB_MAX_DFA) {
+          const Dfa& d = autos[a].d;
+          if (!img_ok(d)) {  // no image form: its patterns are always "maybe" (k_eval decides)
+            for (const PatEntry* pe : autos[a].pes) P->always_slots.push_back(pe->slot);
+            a++;
+            continue;
+          }
+          if (!lds_ok(d, nf)) {
+            if (pick.empty()) {  // image too large for LDS: its own job, image read from HBM
+              pick.push_back(a++);
+              lds = false;
+            }
+            break;
+          }
+          const uint32_t b = img_bytes(d) + al16(nf * 8) + al16(d.n_pat * 4);
+          const uint32_t lim = pick.empty() ? GI_BIG_LDS_BYTES : GI_JOB_LDS_BYTES;
+          if (need + b > lim) break;
+          if (!pick.empty() && need + b > GI_JOB_LDS_BYTES) break;
+          need += b;
+          pick.push_back(a++);
+        }
+        if (pick.empty()) continue;
         DJob j{};
         j.stream = sid;
         j.img_off = (uint32_t)P->images.size();
         j.jdfa_begin = (uint32_t)P->jdfas.size();
-        uint32_t used = 0;
+        j.lds = lds ? 1 : 0;
         if (!first_j) js << ",";
         first_j = false;
         js << "[";
-        bool first_d = true;
-        while (a < autos.size()) {
-          const Dfa& d = autos[a].d;
-          const uint32_t b = img_bytes(d);
-          const bool fits = b <= GI_JOB_LDS_BYTES;
-          if (fits && used + b > GI_JOB_LDS_BYTES) break;        // next job
-          if (!fits && j.jdfa_count > 0) break;                   // global automaton: own job
+        std::vector<uint32_t> jam(GI_JAMAP_BYTES / 4, 0);
+        int32_t at = 0;
+        img_put(j.img_off, jam.data(), GI_JAMAP_BYTES, &at);  // filled below
+        std::vector<uint32_t> slots;
+        for (size_t q = 0; q < pick.size(); q++) {
+          const AutoBuild& ab = autos[pick[q]];
+          const Dfa& d = ab.d;
           DJobDfa jd{};
           jd.dfa = add_dfa(d);
-          jd.lds_trans = jd.lds_amap = jd.lds_combo = -1;
-          if (fits) {
-            jd.lds_trans = (int32_t)used;
-            const uint8_t* tp = (const uint8_t*)d.trans.data();
-            P->images.insert(P->images.end(), tp, tp + d.trans.size() * 2);
-            P->images.resize(j.img_off + ((used + d.trans.size() * 2 + 15) & ~15u), 0);
-            used = (uint32_t)(P->images.size() - j.img_off);
-            jd.lds_amap = (int32_t)used;
-            P->images.insert(P->images.end(), d.amap.begin(), d.amap.end());
-            P->images.resize(j.img_off + ((used + d.amap.size() + 15) & ~15u), 0);
-            used = (uint32_t)(P->images.size() - j.img_off);
+          jd.lds_trans = jd.lds_amap = jd.lds_combo = jd.lds_endacc = jd.lds_slots = -1;
+          {
+            std::vector<uint16_t> tr(d.trans);
+            if (!d.multi)  // absorbing accept row (already self-looping; made explicit)
+              for (uint32_t c = 0; c < d.n_classes; c++) tr[(size_t)d.accept * d.n_classes + c] = (uint16_t)d.accept;
+            img_put(j.img_off, tr.data(), tr.size() * 2, &jd.lds_trans);
+            img_put(j.img_off, d.amap.data(), d.amap.size(), &jd.lds_amap);
             if (d.multi) {
-              jd.lds_combo = (int32_t)used;
-              P->images.insert(P->images.end(), d.cls_combo.begin(), d.cls_combo.end());
-              P->images.resize(j.img_off + ((used + d.cls_combo.size() + 15) & ~15u), 0);
-              used = (uint32_t)(P->images.size() - j.img_off);
+              img_put(j.img_off, d.cls_combo.data(), d.cls_combo.size(), &jd.lds_combo);
+              std::vector<uint64_t> em(d.n_states);
+              for (uint32_t st = 0; st < d.n_states; st++) em[st] = d.acc[(size_t)st * 5 + 4];
+              img_put(j.img_off, em.data(), em.size() * 8, &jd.lds_endacc);
+            } else {
+              img_put(j.img_off, d.end_accept.data(), d.end_accept.size(), &jd.lds_endacc);
             }
+            for (uint32_t c = 0; c < 128; c++) jam[c] |= (uint32_t)d.amap[c] << (8 * q);
+            const DDfa& dd = P->dfas[jd.dfa];
+            if (!d.byte_mode && dd.nonascii_uniform) jam[128] |= (uint32_t)dd.nonascii_cls << (8 * q);
+            else P->streams[sid].collapse = 0;
+            jd.lds_slots = (int32_t)(slots.size() * 4);  // relative; rebased below
           }
           jd.pat_begin = (uint32_t)P->pats.size();
-          jd.n_pat = (uint32_t)autos[a].pes.size();
+          jd.n_pat = (uint32_t)ab.pes.size();
           jd.fmask_off = (uint32_t)P->u64pool.size();
-          for (uint32_t fi = 0; fi < s.filt_count; fi++) P->u64pool.push_back(0);
-          for (size_t k = 0; k < autos[a].pes.size(); k++) {
-            const PatEntry* pe = autos[a].pes[k];
+          for (uint32_t fi = 0; fi < nf; fi++) P->u64pool.push_back(0);
+          for (size_t k = 0; k < ab.pes.size(); k++) {
+            const PatEntry* pe = ab.pes[k];
             P->pats.push_back(DPat{pe->slot});
+            slots.push_back(pe->slot);
             if (pe->negate) jd.neg_mask |= 1ull << k;
-            for (uint32_t fi = 0; fi < s.filt_count; fi++)
+            for (uint32_t fi = 0; fi < nf; fi++)
               if ((pe->fmask >> fi) & 1) P->u64pool[jd.fmask_off + fi] |= 1ull << k;
           }
           if (d.multi) P->n_union_dfas++;
           P->jdfas.push_back(jd);
           j.jdfa_count++;
-          if (!first_d) js << ",";
-          first_d = false;
-          js << "{\"states\":" << d.n_states << ",\"classes\":" << d.n_classes << ",\"pats\":" << jd.n_pat
-             << ",\"lds\":" << (fits ? 1 : 0) << "}";
-          a++;
-          if (!fits) break;
+          js << (q ? "," : "") << "{\"states\":" << d.n_states << ",\"classes\":" << d.n_classes
+             << ",\"pats\":" << jd.n_pat << ",\"multi\":" << (d.multi ? 1 : 0) << ",\"lds\":" << (lds ? 1 : 0)
+             << "}";
+        }
+        {
+          memcpy(&P->images[j.img_off], jam.data(), GI_JAMAP_BYTES);
+          std::vector<uint64_t> fm((size_t)j.jdfa_count * nf);
+          for (uint32_t q = 0; q < j.jdfa_count; q++)
+            for (uint32_t fi = 0; fi < nf; fi++) fm[(size_t)q * nf + fi] = P->u64pool[P->jdfas[j.jdfa_begin + q].fmask_off + fi];
+          int32_t fo = 0, so = 0;
+          img_put(j.img_off, fm.data(), fm.size() * 8, &fo);
+          j.lds_fmask = (uint32_t)fo;
+          img_put(j.img_off, slots.data(), slots.size() * 4, &so);
+          for (uint32_t q = 0; q < j.jdfa_count; q++) P->jdfas[j.jdfa_begin + q].lds_slots += so;
         }
         js << "]";
-        j.img_bytes = used;
-        if (!vals_done) {
-          j.val_begin = (uint32_t)P->svals.size();
-          j.val_count = (uint32_t)sb.vals.size();
-          P->svals.insert(P->svals.end(), sb.vals.begin(), sb.vals.end());
-          vals_done = true;
+        j.img_bytes = (uint32_t)(P->images.size() - j.img_off);
+        j.big = j.img_bytes > GI_JOB_LDS_BYTES ? 1 : 0;
+        if (lds) {
+          if (j.big) P->max_big_img_bytes = std::max(P->max_big_img_bytes, j.img_bytes);
+          else P->max_img_bytes = std::max(P->max_img_bytes, j.img_bytes);
         }
-        P->max_img_bytes = std::max(P->max_img_bytes, j.img_bytes);
         P->jobs.push_back(j);
       }
-      js << "]}";
+      P->streams[sid].job_count = (uint32_t)P->jobs.size() - P->streams[sid].job_begin;
+      js << "],\"collapse\":" << (int)P->streams[sid].collapse << "}";
     }
     js << "],\"jobs\":" << P->jobs.size() << ",\"hit_slots\":" << P->n_hit_slots
        << ",\"image_bytes\":" << P->images.size() << "}";

@@ -28,7 +28,11 @@ struct Program {
   std::vector<uint32_t> slot_names;  // (off, len) pairs into strpool
   std::vector<uint64_t> u64pool;     // union-automaton accept masks
   std::vector<DStream> streams;      // phase-A scan plan
-  std::vector<DFilter> filters;
+  std::vector<DFilter> filters;      // global (deduplicated) phase-A variable filters
+  std::vector<uint8_t> sfilt;        // per stream filter: global filter id
+  uint8_t item_sides[8] = {0};       // per FieldKind: bit0 value side, bit1 key side is filtered
+  uint32_t item_singles = 0;         // single variables some filter reads (1 << SingleId)
+  std::vector<uint32_t> always_slots;  // hit slots without an automaton image (always set)
   std::vector<DJob> jobs;
   std::vector<DJobDfa> jdfas;
   std::vector<DPat> pats;
@@ -36,7 +40,8 @@ struct Program {
   std::vector<uint8_t> images;
   uint32_t n_hit_slots = 0;
   uint32_t n_union_dfas = 0;
-  uint32_t max_img_bytes = 0;
+  uint32_t max_img_bytes = 0;      // largest small-job LDS image
+  uint32_t max_big_img_bytes = 0;  // largest big-job LDS image
   std::string plan_json;             // human-readable scan plan (gi_ruleset_describe)
   std::vector<int32_t> exports;
   std::vector<std::string> export_names;

@@ -17,6 +17,9 @@ struct ReqLayout {
   uint32_t cap_b;  // decoded-bytes arena
   uint32_t cap_t;  // each of the two transformation buffers
   uint32_t cap_mt; // macro expansion scratch == TX string arena size
+  uint64_t pa_base;  // byte offset of the request's phase-A arena in DBatch.pa
+  uint32_t pa_cap;   // its capacity (overflow voids the request's phase-A bits)
+  uint32_t _pad;
 };
 
 struct DBatch {
@@ -29,18 +32,59 @@ struct DBatch {
   const ReqLayout* layout;
   gi_verdict* verdicts;
   uint32_t* matched;
-  unsigned long long* tally;  // gi_tally as 6 counters
+  unsigned long long* tally;  // gi_tally counters
   uint32_t* hits;             // phase-A hit words [ceil(n_hit_slots/32)][n_req]
-  uint8_t* tscratch;          // k_match transformation buffers (2 x tcap per resident thread)
-  uint32_t tcap;
+  // phase A (see kernels.hip "phase A")
+  uint32_t* bcounts;          // [k_collect blocks][GI_NB] item counts
+  uint32_t* boffs;            // [k_collect blocks][GI_NB] item offsets
+  uint32_t* ibk;              // [GI_NB] (base, count), [GI_NB] item-wave base, total item waves
+  void* items;                // Item[items_cap]
+  uint8_t* lscratch;          // per-lane HBM transformation buffers (2 x lcap per k_stream lane)
+  uint32_t lcap;
+  uint32_t* pool;             // queue-block words
+  uint64_t pool_cap;          // words
+  unsigned long long* pool_used;
+  uint2* qblk;                // [stream][qcap] queue blocks {word offset, nv | nw << 8}
+  uint32_t* qcount;           // [stream]
+  uint32_t qcap;
+  void* slow;                 // SlowEnt[slow_cap]
+  uint32_t* slow_count;
+  uint32_t slow_cap;
+  uint8_t* slow_bytes;
+  uint64_t slow_bytes_cap;
+  unsigned long long* slow_used;
+  unsigned long long* diag;   // optional diagnostic counters (gi_stats.diag)
+  uint32_t* dbg;              // debug-build bounds-violation record (-DGI_DEBUG)
+  uint64_t items_cap;
+  uint32_t n_hit_slots;
 };
 
-// Resident thread count of k_match with lds_bytes of dynamic LDS per block.
-uint32_t scan_resident_threads(uint32_t lds_bytes);
+// k_scan launch plan: job lists for the small-LDS and big-LDS launches.
+struct ScanLaunch {
+  const uint32_t* jobs[2];  // device job-index lists
+  uint32_t n_jobs[2];
+  uint32_t lds[2];          // dynamic LDS bytes per workgroup
+  uint32_t blocks[3];       // resident workgroups (persistent grid); [2] = HBM-image launch
+  uint32_t rpl[2];          // requests per lane per unit
+  const uint32_t* global_jobs;  // jobs whose image is read from HBM (too large for LDS)
+  uint32_t n_global;
+  uint32_t mode;                // debugging switches (GI_SCAN_MODE), 0 in production
+};
 
-// k_collect -> k_scan -> k_eval on `stream`; ev (optional) = 2 events recorded
-// after k_collect and after k_match.
-void launch_pipeline(const DProgram& P, const DBatch& B, uint32_t scan_threads, hipStream_t stream,
-                     hipEvent_t* ev);
+#define GI_STREAM_GRID 8192  // k_stream workgroups (64 lanes) per bucket launch (~8 waves/SIMD)
+#define GI_PCHUNK 2048       // pool words a k_stream wave reserves at a time
+#define GI_MAX_STREAMS 256   // streams a ruleset may have (k_stream keeps per-stream chunk state in LDS)
+
+// Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.
+uint32_t scan_resident_blocks(uint32_t lds_bytes);
+// Raise the dynamic-LDS limit of k_scan for images above 64 KiB.
+void scan_allow_lds(uint32_t lds_bytes);
+
+// k_collect -> k_stream -> k_scan (small, big) -> k_eval on `stream`;
+// ev (optional) = 3 events recorded after k_collect, k_stream and k_scan.
+// stop_after > 0 (debugging): launch only the first stop_after kernels and
+// synchronise after each, printing the first failing one.
+void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
+                     int stop_after = 0);
 
 }  // namespace gi

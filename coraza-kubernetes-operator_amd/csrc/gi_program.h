@@ -8,6 +8,11 @@
 #pragma once
 #include <stdint.h>
 
+#if !defined(__HIPCC__) && !defined(__host__)
+#define __host__
+#define __device__
+#endif
+
 namespace gi {
 
 // ------------------------------------------------------------- variables
@@ -141,24 +146,35 @@ struct DRule {
 
 // ------------------------------------------------------ phase-A scan plan
 // stream  = one transformation chain: every value some target of a phase-A
-//           rule link reads through that chain (values are transformed once
-//           per job and scanned by every automaton of the job);
+//           rule link reads through that chain.  k_stream transforms each
+//           admitted value ONCE per stream into the request's phase-A arena;
 // filter  = one value source of the stream: a single variable, or a field
 //           kind set (key or value side) with a key selector + exclusions;
 // pattern = one phase-A-eligible rule link on the stream, admitted by the
 //           filters of its targets; a value feeds a pattern only through
 //           one of those filters;
-// job     = the automata of one stream whose tables fit one LDS image: a
-//           persistent workgroup loads the image once and sweeps requests.
+// job     = up to GI_JOB_MAX_DFA automata of one stream whose tables fit one
+//           LDS image: a persistent k_scan workgroup loads the image once and
+//           sweeps the stream's arena segment of many requests, stepping the
+//           job's automata in lockstep over each value.
 #define GI_MAX_FILTERS 32
-#define GI_JOB_LDS_BYTES 65536
+#define GI_MAX_GFILTERS 64
+#define GI_JOB_LDS_BYTES 65536          // small jobs: 2 workgroups of 1024 per CU
+#define GI_BIG_LDS_BYTES (148 * 1024)   // big jobs: 1 workgroup of 1024 per CU (+ 8 KB k_scan block list)
+#define GI_JOB_MAX_DFA 4
+#define GI_JAMAP_BYTES 528              // joint class map: u32[129] (128 = collapsed non-ASCII rune), byte q = class in automaton q
+#define GI_RUNE_MARK 0x80               // a non-ASCII rune in a collapsed value
 #define GI_NO_SINGLE 0xFF
 
 struct DStream {
   uint32_t tchain_off, tchain_len;
   uint32_t filt_begin, filt_count;  // DFilter
+  uint32_t job_begin, job_count;    // DJob (contiguous per stream)
+  uint32_t val_begin, val_count;    // DScanVal: validate operators, evaluated by k_stream
   uint8_t kind_mask;  // union of the field filters' kinds (1 << FieldKind)
-  uint8_t _pad[3];
+  uint8_t collapse;   // every automaton maps all non-ASCII runes to one class: values are
+                      // rune-collapsed (each non-ASCII rune -> GI_RUNE_MARK) instead of slow
+  uint8_t _pad[2];
 };
 
 struct DFilter {
@@ -171,20 +187,96 @@ struct DFilter {
   int32_t key_dfa;
   uint32_t key_off, key_len;
   uint32_t exc_begin, exc_count;
+  uint32_t key_hash;  // gi_fnv1a of the literal key (as stored: lowercase when ci)
 };
 
+// FNV-1a over bytes (key prefilter of the phase-A filters; host and device).
+__host__ __device__ inline uint32_t gi_fnv1a(const uint8_t* s, uint32_t n, bool lower) {
+  uint32_t h = 2166136261u;
+  for (uint32_t i = 0; i < n; i++) {
+    uint8_t c = s[i];
+    if (lower && c >= 'A' && c <= 'Z') c += 32;
+    h = (h ^ c) * 16777619u;
+  }
+  return h;
+}
+
+// Byte summary of a value: which bytes that make some transformation
+// non-identity occur in it.  A transformation whose trigger set does not meet
+// the summary leaves the value unchanged, so it is skipped outright (exact).
+enum : uint32_t {
+  BS_PCT = 1u << 0, BS_PLUS = 1u << 1, BS_AMP = 1u << 2, BS_UPPER = 1u << 3, BS_HIGH = 1u << 4,
+  BS_NUL = 1u << 5, BS_WS = 1u << 6, BS_SLASH = 1u << 7, BS_BSLASH = 1u << 8, BS_DOT = 1u << 9,
+  BS_QUOTE = 1u << 10, BS_CARET = 1u << 11, BS_SEP = 1u << 12, BS_ALL = 0xFFFFFFFFu,
+};
+__host__ __device__ inline uint32_t byte_summary(uint8_t c) {
+  uint32_t m = 0;
+  m |= c == '%' ? BS_PCT : 0u;
+  m |= c == '+' ? BS_PLUS : 0u;
+  m |= c == '&' ? BS_AMP : 0u;
+  m |= (c >= 'A' && c <= 'Z') ? BS_UPPER : 0u;
+  m |= c >= 0x80 ? BS_HIGH : 0u;
+  m |= c == 0 ? BS_NUL : 0u;
+  m |= (c == ' ' || (c >= 9 && c <= 13)) ? BS_WS : 0u;
+  m |= c == '/' ? BS_SLASH : 0u;
+  m |= c == '\\' ? BS_BSLASH : 0u;
+  m |= c == '.' ? BS_DOT : 0u;
+  m |= (c == '"' || c == '\'') ? BS_QUOTE : 0u;
+  m |= c == '^' ? BS_CARET : 0u;
+  m |= (c == ',' || c == ';') ? BS_SEP : 0u;
+  return m;
+}
+// Bytes that can make transformation `code` change its input
+// ([upstream] internal/transformations/*.go, restated above).
+__host__ __device__ inline uint32_t transform_triggers(uint8_t code) {
+  switch (code) {
+    case T_LOWERCASE: return BS_UPPER | BS_HIGH;
+    case T_URLDECODE:
+    case T_URLDECODEUNI: return BS_PCT | BS_PLUS;
+    case T_HTMLENTITYDECODE: return BS_AMP;
+    case T_REMOVENULLS:
+    case T_REPLACENULLS: return BS_NUL;
+    case T_REMOVEWHITESPACE:
+    case T_COMPRESSWHITESPACE:
+    case T_TRIM:
+    case T_TRIMLEFT:
+    case T_TRIMRIGHT: return BS_WS | BS_HIGH;
+    case T_REPLACECOMMENTS: return BS_SLASH;
+    case T_CMDLINE: return BS_QUOTE | BS_BSLASH | BS_CARET | BS_WS | BS_SEP | BS_UPPER;
+    case T_NORMALIZEPATH: return BS_SLASH | BS_DOT;
+    case T_NORMALIZEPATHWIN: return BS_SLASH | BS_DOT | BS_BSLASH;
+    case T_JSDECODE: return BS_BSLASH;
+    case T_UTF8TOUNICODE: return BS_HIGH;
+    default: return BS_ALL;  // t:length and anything new: always run
+  }
+}
+
+// Image of an LDS job (byte offsets inside the job's image):
+//   [0, 512)      joint ASCII class map (u32 per byte < 0x80)
+//   per automaton: transitions u16[n_states][n_classes] (state index, bit 15 =
+//                  accepting transition of a union automaton; the absorbing
+//                  accept row of a single automaton loops to itself),
+//                  class map (128 rune-mode / 256 byte-mode), combo (union),
+//                  end-of-input accept (u8 per state single / u64 per state union)
+//   fmask         u64[jdfa_count][n_filters]: patterns each stream filter admits
+//   slots         u32 hit slot per pattern, automata concatenated
 struct DJob {
   uint32_t stream;
   uint32_t img_off, img_bytes;     // LDS image (u8 image pool, 16-B aligned)
   uint32_t jdfa_begin, jdfa_count; // DJobDfa
-  uint32_t val_begin, val_count;   // DScanVal
+  uint32_t lds_fmask;              // image offset of the fmask table
+  uint8_t lds;                     // 1: all automata in the image; 0: one automaton on global tables
+  uint8_t big;                     // image > GI_JOB_LDS_BYTES (big-LDS launch)
+  uint8_t _pad[2];
 };
 
 struct DJobDfa {
   int32_t dfa;        // DDfa (start, classes, accept masks, rune ranges)
-  int32_t lds_trans;  // byte offset of the transition table in the image, -1: global
-  int32_t lds_amap;   // byte offset of the 128/256-entry class map in the image
-  int32_t lds_combo;  // byte offset of the per-class combo table (multi)
+  int32_t lds_trans;  // image offsets (lds jobs), -1 otherwise
+  int32_t lds_amap;
+  int32_t lds_combo;
+  int32_t lds_endacc;
+  int32_t lds_slots;  // u32 hit slot per pattern
   uint32_t pat_begin; // DPat, n_pat entries (bit k of the match mask)
   uint32_t n_pat;
   uint32_t fmask_off; // u64 pool: per stream filter, the patterns it admits
@@ -221,6 +313,7 @@ struct DVarRef {
 struct DExc {
   int32_t dfa;       // regex exception (matched on the lowercased key) or -1
   uint32_t off, len; // literal exception (lowercase)
+  uint32_t hash;     // gi_fnv1a of the literal exception
 };
 
 struct DOp {
@@ -281,6 +374,7 @@ struct DProgram {
   const DTmplPart* tparts;
   const DTmpl* tmpls;
   const uint8_t* tchains;
+  const uint32_t* tchains32;    // the same codes widened (scalar-loadable in wave-uniform loops)
   const DDfa* dfas;
   const uint16_t* trans;
   const uint8_t* u8pool;
@@ -296,9 +390,17 @@ struct DProgram {
   const DPat* pats;
   const DScanVal* svals;
   const uint8_t* images;        // LDS images of the jobs
+  const uint32_t* sfilt;        // per stream filter: global filter id (filters[] is global)
+  const uint32_t* always_slots; // hit slots without an automaton image
+  uint32_t n_always;
+  uint32_t n_gfilters;
+  uint32_t item_singles;        // singles some filter reads (1 << SingleId)
+  uint8_t item_sides[8];        // per FieldKind: bit0 value side, bit1 key side
   uint32_t n_jobs;
   uint32_t n_hit_slots;
-  uint32_t max_img_bytes;
+  uint32_t max_img_bytes;       // largest small-job image
+  uint32_t max_big_img_bytes;   // largest big-job image (0: none)
+  uint32_t n_streams;
   uint32_t n_lower_pairs;
   uint32_t n_top;
   uint32_t n_slots;

@@ -13,6 +13,8 @@
 // function names the coraza source it restates.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "gi_kernels.h"
 
 namespace gi {
@@ -673,6 +675,11 @@ __device__ int64_t apply_transform(const DProgram& P, uint8_t code, const uint8_
   }
 }
 
+__device__ uint32_t value_summary(const uint8_t* s, uint32_t n) {
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < n; i++) m |= byte_summary(s[i]);
+  return m;
+}
 // ------------------------------------------------------------ transaction
 struct Tx {
   const DProgram* P;
@@ -692,7 +699,8 @@ struct Tx {
   const uint32_t* hits;      // phase-A hit words [slot/32][n_req]
   uint32_t n_req, req;
   bool has_post;             // ARGS_POST fields exist (phase-A bits of RF_BODYDEP links void)
-  int64_t removed[8][2];
+  bool pa_void;              // phase-A arena overflowed: no phase-A bit is trusted
+  int64_t (*removed)[2];     // ctl:ruleRemoveById ranges (8, in the request's scratch region)
   uint32_t nremoved;
   uint8_t engine, body_access, body_proc, phase;
   uint8_t force_body;
@@ -705,7 +713,6 @@ struct Tx {
   uint32_t nmatched;
   uint32_t* mout;
   uint32_t mcap;
-  uint8_t itoa_buf[24];
 };
 
 __device__ inline uint8_t* tx_alloc(Tx& t, uint32_t n) {
@@ -1191,15 +1198,19 @@ __device__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uint32_t vn, b
   const DProgram& P = *t.P;
   Str cur{v, vn};
   *ok = true;
+  uint32_t summ = R.tchain_len ? value_summary(v, vn) : 0u;
   for (uint32_t k = 0; k < R.tchain_len; k++) {
+    const uint8_t code = P.tchains[R.tchain_off + k];
+    if (!(summ & transform_triggers(code))) continue;  // identity on this value
     uint8_t* dst = (cur.p == t.t0) ? t.t1 : t.t0;
-    int64_t m = apply_transform(P, P.tchains[R.tchain_off + k], cur.p, cur.n, dst, t.cap_t);
+    int64_t m = apply_transform(P, code, cur.p, cur.n, dst, t.cap_t);
     if (m < 0) {
       t.flags |= GI_REQ_OVERFLOW;
       *ok = false;
       return {dst, 0};
     }
     cur = {dst, (uint32_t)m};
+    summ = value_summary(cur.p, cur.n);
   }
   return cur;
 }
@@ -1251,7 +1262,7 @@ __device__ uint32_t eval_rule(Tx& t, const DRule& R) {
   const DProgram& P = *t.P;
   // phase-A filter: a clear hit bit proves no value matches (exact); a set
   // bit (match or "maybe") falls through to the full evaluation below.
-  if (R.hit_slot >= 0 && !((R.flags & RF_BODYDEP) && t.has_post)) {
+  if (R.hit_slot >= 0 && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post)) {
     const uint32_t w = t.hits[(uint64_t)(R.hit_slot >> 5) * t.n_req + t.req];
     if (!((w >> (R.hit_slot & 31)) & 1u)) return 0;
   }
@@ -1259,10 +1270,10 @@ __device__ uint32_t eval_rule(Tx& t, const DRule& R) {
     run_actions(t, R);
     return 1;
   }
-  const DOp o = P.ops[R.op];
+  const DOp& o = P.ops[R.op];
   uint32_t nmatch = 0;
   for (uint32_t vi = 0; vi < R.var_count; vi++) {
-    const DVarRef vr = P.vars[R.var_begin + vi];
+    const DVarRef& vr = P.vars[R.var_begin + vi];
     if (vr.var < S_COUNT) {
       if (vr.count) {
         uint8_t one = '1';
@@ -1275,9 +1286,14 @@ __device__ uint32_t eval_rule(Tx& t, const DRule& R) {
     }
     if (vr.var == V_TX) {
       uint32_t cnt = 0;
-      for (uint32_t sid = 0; sid < P.n_slots; sid++) {
+      // a literal key names at most one slot: visit only that one
+      uint32_t sb = 0, se = P.n_slots;
+      if (vr.key_mode == 1) {
+        sb = vr.slot < 0 ? 0u : (uint32_t)vr.slot;
+        se = vr.slot < 0 ? 0u : (uint32_t)vr.slot + 1;
+      }
+      for (uint32_t sid = sb; sid < se; sid++) {
         if (t.slots[sid].state == 0) continue;
-        if (vr.key_mode == 1 && (int32_t)sid != vr.slot) continue;
         const uint8_t* nm = P.strpool + P.slot_names[sid * 2];
         uint32_t nn = P.slot_names[sid * 2 + 1];
         if (vr.key_mode == 2 && !dfa_match(P, vr.key_dfa, nm, nn, false)) continue;
@@ -1286,7 +1302,22 @@ __device__ uint32_t eval_rule(Tx& t, const DRule& R) {
           cnt++;
           continue;
         }
-        Str s = slot_str(t, t.slots[sid], t.itoa_buf);
+        const Slot sl = t.slots[sid];
+        if (sl.state == 1 && R.tchain_len == 0 && o.has_num && o.kind >= OP_EQ && o.kind <= OP_LT) {
+          // integer TX value against a numeric literal: eval_op would Atoi the
+          // canonical decimal back to sl.num, so compare directly
+          const int64_t a = o.num, b = sl.num;
+          bool res = o.kind == OP_EQ ? b == a : o.kind == OP_GE ? b >= a : o.kind == OP_GT ? b > a
+                     : o.kind == OP_LE ? b <= a : b < a;
+          if (o.negate) res = !res;
+          if (res) {
+            run_actions(t, R);
+            nmatch++;
+          }
+          continue;
+        }
+        uint8_t nb[24];
+        Str s = slot_str(t, sl, nb);
         nmatch += test_value(t, R, o, s.p, s.n);
       }
       if (vr.count) {
@@ -1380,6 +1411,9 @@ __device__ void eval_phase(Tx& t, uint8_t phase) {
       continue;
     }
     if (R.flags & RF_MARKER) continue;
+    if (R.hit_slot >= 0 && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
+        !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.n_req + t.req] >> (R.hit_slot & 31)) & 1u))
+      continue;  // phase A proved the first link matches nothing
     eval_top(t, ri);
   }
 }
@@ -1392,7 +1426,8 @@ struct ReqHdr {
   uint32_t nb;          // bytes arena used
   uint16_t n_get, n_hdr, n_ck, flags;
   uint8_t body_proc;
-  uint8_t _pad[7];
+  uint8_t pa_void;      // phase-A arena overflowed: k_eval ignores the hit bits
+  uint8_t _pad[6];
   Str single[S_COUNT];
 };
 static_assert(sizeof(ReqHdr) <= 256, "ReqHdr must fit its 256-byte slot");
@@ -1402,6 +1437,7 @@ struct Region {
   Field* fields;
   Slot* slots;
   uint8_t *bytes, *t0, *t1, *mt, *txa;
+  int64_t (*rm)[2];
   uint32_t cap_f, cap_b, cap_t, cap_mt;
 };
 
@@ -1415,6 +1451,8 @@ __device__ inline Region region_of(const DProgram& P, const DBatch& B, uint32_t 
   off += (uint64_t)L.cap_f * sizeof(Field);
   g.slots = (Slot*)(base + off);
   off += ((uint64_t)P.n_slots * sizeof(Slot) + 15) & ~15ull;
+  g.rm = (int64_t(*)[2])(base + off);
+  off += 128;
   g.bytes = base + off;
   off += (L.cap_b + 15) & ~15u;
   g.t0 = base + off;
@@ -1444,16 +1482,106 @@ __device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
   t.mt = g.mt;
   t.cap_mt = g.cap_mt;
   t.txa = g.txa;
+  t.removed = g.rm;
   t.cap_tx = g.cap_mt;
   t.single = g.hdr->single;
+}
+
+__device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
+  if (kind == OP_VALIDATE_BYTE_RANGE) {
+    for (uint32_t i = 0; i < n; i++)
+      if (!((bits[s[i] >> 5] >> (s[i] & 31)) & 1)) return true;
+    return false;
+  }
+  if (kind == OP_VALIDATE_URL_ENCODING) {
+    for (uint32_t i = 0; i < n;) {
+      if (s[i] == '%') {
+        if (i + 2 >= n) return true;
+        if (ishex(s[i + 1]) && ishex(s[i + 2])) i += 3;
+        else return true;
+      } else {
+        i++;
+      }
+    }
+    return false;
+  }
+  for (uint32_t i = 0; i < n;) {  // OP_VALIDATE_UTF8
+    uint32_t w;
+    uint32_t r = decode_rune(s, n, i, &w);
+    if (r == 0xFFFD && w == 1) return true;
+    i += w;
+  }
+  return false;
+}
+
+// Debug builds (-DGI_DEBUG): bounds violations are recorded in B.dbg
+// ([0] first source line, [1] count, [2..3] operands) and the access skipped.
+#ifdef GI_DEBUG
+__device__ __noinline__ void gi_dbg_fail(const DBatch& B, uint32_t line, uint64_t a, uint64_t b) {
+  if (!B.dbg) return;
+  if (atomicCAS(&B.dbg[0], 0u, line) == 0u) {
+    B.dbg[2] = (uint32_t)a;
+    B.dbg[3] = (uint32_t)b;
+  }
+  atomicAdd(&B.dbg[1], 1u);
+}
+#define GI_BOUND(cond, a, b)                        \
+  do {                                              \
+    if (!(cond)) {                                  \
+      gi_dbg_fail(B, __LINE__, (a), (b));           \
+      return;                                       \
+    }                                               \
+  } while (0)
+#else
+#define GI_BOUND(cond, a, b) \
+  do {                       \
+  } while (0)
+#endif
+
+__device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
+  GI_BOUND(r < B.n_req && slot < B.n_hit_slots, slot, r);
+  atomicOr(&B.hits[(uint64_t)(slot >> 5) * B.n_req + r], 1u << (slot & 31));
+}
+
+#define GI_NB 5  // item length buckets: <=16, <=32, <=64, <=128, >128 bytes
+__device__ __forceinline__ uint32_t item_bucket(uint32_t n) {
+  return n <= 16 ? 0u : n <= 32 ? 1u : n <= 64 ? 2u : n <= 128 ? 3u : 4u;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// rank of this lane among the lanes of mask below it
+__device__ __forceinline__ uint32_t mask_rank(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+  return x;
+}
+
+// Visits the items of one request: singles some filter reads, then the
+// (value, key) sides of every field kind some filter reads.
+template <class F>
+__device__ __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H, const Field* Fd, F&& f) {
+  for (uint32_t m = P.item_singles; m; m &= m - 1) {
+    const uint32_t sg = __ffs(m) - 1;
+    f((uint8_t)0, (uint8_t)sg, 0u, (uint32_t)0xFFFFFFFFu, H->single[sg].n);
+  }
+  const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck;
+  for (uint32_t i = 0; i < n_get + n_hdr + n_ck; i++) {
+    const uint8_t kind = i < n_get ? FK_ARG_GET : i < n_get + n_hdr ? FK_HEADER : FK_COOKIE;
+    const uint8_t sides = P.item_sides[kind];
+    const Field fl = Fd[i];
+    if (sides & 1) f(kind, (uint8_t)0, 0u, i, fl.vn);
+    if (sides & 2) f(kind, (uint8_t)0, 1u, i, fl.kn);
+  }
 }
 
 // ------------------------------------------------ stage 1: k_collect
 // ProcessURI + AddRequestHeader* for one request per thread.  Fields are
 // grouped by kind so each scan group walks only its own range.
-__global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= B.n_req) return;
+__device__ void collect_request(const DProgram& P, const DBatch& B, uint32_t r) {
   const gi_request rq = B.reqs[r];
   Region g = region_of(P, B, r);
   Tx t;
@@ -1517,14 +1645,396 @@ __global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
   H->n_ck = (uint16_t)(t.nf - n_get - n_hdr);
   H->flags = t.flags | ((t.nf > 0xFFFF) ? GI_REQ_OVERFLOW : 0);
   H->body_proc = t.body_proc;
+  H->pa_void = 0;
 }
 
-// ------------------------------------------------ stage 2: k_match (phase A)
-// Persistent kernel over units (job, tile of 256 requests), job-major.  A
-// workgroup copies the job's automaton image (<= 64 KB) into LDS once per job
-// change, then each thread walks one request: the stream's values are key-
-// filtered, transformed once and run through every automaton of the job whose
-// admitted patterns intersect the value's filter-pass mask.
+// ProcessURI + AddRequestHeader* for one request per thread, then the
+// per-block item counts per length bucket (k_ioffsets / k_items) and the hit
+// bits of links without an automaton image.
+__global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
+  __shared__ uint32_t hist[GI_NB];
+  if (threadIdx.x < GI_NB) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < B.n_req) {
+    collect_request(P, B, r);
+    if (P.n_streams) {
+      const ReqLayout L = B.layout[r];
+      const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
+      if (!(H->flags & GI_REQ_ERROR_MASK)) {
+        uint32_t c[GI_NB] = {0, 0, 0, 0, 0};
+        for_each_item(P, H, (const Field*)(B.scratch + L.base + 256),
+                      [&](uint8_t, uint8_t, uint32_t, uint32_t, uint32_t n) { c[item_bucket(n)]++; });
+        for (uint32_t b = 0; b < GI_NB; b++)
+          if (c[b]) atomicAdd(&hist[b], c[b]);
+      }
+      for (uint32_t k = 0; k < P.n_always; k++) set_hit(B, P.always_slots[k], r);
+    }
+  }
+  __syncthreads();
+  if (P.n_streams && threadIdx.x < GI_NB) B.bcounts[blockIdx.x * GI_NB + threadIdx.x] = hist[threadIdx.x];
+}
+
+
+// ============================================================== phase A
+// Data-parallel operator evaluation (SURVEY §2 rx_dfa_scan / ac_scan /
+// simple_ops).  Every rule link whose operator is a pure function of one
+// transformed value (@rx, @pm, @contains literal, @validate*) and whose
+// targets are immutable request variables gets a hit slot; phase A sets the
+// slot's bit for a request iff some admitted value matches (negated operators:
+// iff some admitted value does not).  A clear bit proves the link cannot
+// match, so k_eval skips it; a set bit is re-evaluated exactly by k_eval.
+//
+//   k_collect  fields per request + per-block item counts per length bucket
+//   k_ioffsets bucket bases + per-block offsets (one workgroup)
+//   k_items    item records (one per scanned (field, side) / single) into
+//              length-bucketed ranges
+//   k_stream   lane per item, wave per 64 items of one bucket: for every
+//              stream (transformation chain) the item's admitting filters are
+//              looked up in its global-filter mask, the chain runs once in
+//              lane-private LDS buffers, validate operators are evaluated, and
+//              the admitted values of the wave are written as ONE transposed
+//              queue block (word w of lane i at w * nv + i: coalesced reads)
+//   k_scan     LDS-resident automata images; a wave steps all automata of its
+//              job in lockstep over the 64 values of one queue block
+//   k_scan_slow non-ASCII values (rune decoding) and transformation
+//              overflows, on the global tables
+struct Item {  // 32 B
+  const uint8_t* kp;  // key (fields); nullptr for singles
+  const uint8_t* vp;  // scanned bytes: value side, key side or single
+  uint32_t kn, vn;
+  uint32_t req;
+  uint8_t kind;       // FieldKind, 0 = single
+  uint8_t single;     // SingleId (kind 0)
+  uint8_t side;       // 1: key side (the *_NAMES collections)
+  uint8_t _pad;
+};
+static_assert(sizeof(Item) == 32, "Item layout");
+
+__global__ void __launch_bounds__(1024) k_ioffsets(DBatch B, uint32_t n_blocks) {
+  // bcounts[blk * GI_NB + b] -> boffs (exclusive, bucket-major global order);
+  // ibk[2b] = bucket base, ibk[2b+1] = bucket count
+  __shared__ uint32_t part[1024];
+  __shared__ uint32_t base_s;
+  const uint32_t t = threadIdx.x;
+  const uint32_t chunk = (n_blocks + 1023) / 1024;
+  if (t == 0) base_s = 0;
+  __syncthreads();
+  for (uint32_t b = 0; b < GI_NB; b++) {
+    uint32_t sum = 0;
+    for (uint32_t k = t * chunk; k < min(n_blocks, (t + 1) * chunk); k++) sum += B.bcounts[k * GI_NB + b];
+    part[t] = sum;
+    __syncthreads();
+    if (t == 0) {
+      uint32_t run = 0;
+      for (uint32_t k = 0; k < 1024; k++) {
+        const uint32_t x = part[k];
+        part[k] = run;
+        run += x;
+      }
+      B.ibk[2 * b] = base_s;
+      B.ibk[2 * b + 1] = run;
+    }
+    __syncthreads();
+    uint32_t run = base_s + part[t];
+    for (uint32_t k = t * chunk; k < min(n_blocks, (t + 1) * chunk); k++) {
+      const uint32_t x = B.bcounts[k * GI_NB + b];
+      B.boffs[k * GI_NB + b] = run;
+      run += x;
+    }
+    __syncthreads();
+    if (t == 0) base_s += B.ibk[2 * b + 1];
+    __syncthreads();
+  }
+  if (t == 0) {  // item-wave (queue-block index) base per bucket, and the total
+    uint32_t iw = 0;
+    for (uint32_t b = 0; b < GI_NB; b++) {
+      B.ibk[2 * GI_NB + b] = iw;
+      iw += (B.ibk[2 * b + 1] + 63) / 64;
+    }
+    B.ibk[3 * GI_NB] = iw;
+  }
+}
+
+// One thread per request, same block shape as k_collect.
+__global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
+  __shared__ uint32_t rank[GI_NB];
+  if (threadIdx.x < GI_NB) rank[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < B.n_req) {
+    const ReqLayout L = B.layout[r];
+    const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
+    if (!(H->flags & GI_REQ_ERROR_MASK)) {
+      const Field* Fd = (const Field*)(B.scratch + L.base + 256);
+      const uint32_t* boff = B.boffs + blockIdx.x * GI_NB;
+      for_each_item(P, H, Fd, [&](uint8_t kind, uint8_t sg, uint32_t side, uint32_t fi, uint32_t n) {
+        const uint32_t b = item_bucket(n);
+        const uint32_t at = boff[b] + atomicAdd(&rank[b], 1u);
+        GI_BOUND(at < B.items_cap, at, B.items_cap);
+        Item it;
+        if (kind == 0) {
+          it.kp = nullptr;
+          it.kn = 0;
+          it.vp = H->single[sg].p;
+        } else {
+          const Field fl = Fd[fi];
+          it.kp = fl.k;
+          it.kn = fl.kn;
+          it.vp = side ? fl.k : fl.v;
+        }
+        it.vn = n;
+        it.req = r;
+        it.kind = kind;
+        it.single = sg;
+        it.side = (uint8_t)side;
+        it._pad = 0;
+        ((Item*)B.items)[at] = it;
+      });
+    }
+  }
+}
+
+// Global filters admitting the item (bit g of the result).
+__device__ uint64_t item_gmask(const DProgram& P, const Item& it) {
+  uint64_t m = 0;
+  // key hashes (read the key once): literal selectors / exceptions compare
+  // bytes only on a hash hit
+  const uint32_t hci = it.kind ? gi_fnv1a(it.kp, it.kn, true) : 0u;
+  const uint32_t hcs = it.kind ? gi_fnv1a(it.kp, it.kn, false) : 0u;
+  for (uint32_t g = 0; g < P.n_gfilters; g++) {
+    const DFilter F = P.filters[g];
+    if (it.kind == 0) {
+      if (F.single == it.single) m |= 1ull << g;
+      continue;
+    }
+    if (F.single != GI_NO_SINGLE || !((F.kind_mask >> it.kind) & 1) || F.names != it.side) continue;
+    if (F.key_mode == 1) {
+      if ((F.ci ? hci : hcs) != F.key_hash) continue;
+      if (F.ci ? !eq_ascii_ci(it.kp, it.kn, P.strpool + F.key_off, F.key_len)
+               : !eq_bytes(it.kp, it.kn, P.strpool + F.key_off, F.key_len))
+        continue;
+    } else if (F.key_mode == 2) {
+      if (!dfa_match(P, F.key_dfa, it.kp, it.kn, F.ci != 0)) continue;
+    }
+    bool ex = false;
+    for (uint32_t e = 0; e < F.exc_count && !ex; e++) {
+      const DExc x = P.excs[F.exc_begin + e];
+      ex = x.dfa >= 0 ? dfa_match(P, x.dfa, it.kp, it.kn, true)
+                      : (hci == x.hash && eq_ascii_ci(it.kp, it.kn, P.strpool + x.off, x.len));
+    }
+    if (!ex) m |= 1ull << g;
+  }
+  return m;
+}
+
+// The stream's validate operators (@validateByteRange / UrlEncoding / Utf8Encoding).
+__device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, const DStream& S, uint32_t fm, bool maybe,
+                            const uint8_t* v, uint32_t n) {
+  for (uint32_t q = 0; q < S.val_count; q++) {
+    const DScanVal& sv = P.svals[S.val_begin + q];
+    if (!(fm & sv.fmask)) continue;
+    if (maybe || (validate_op(sv.kind, sv.bits, v, n) != (sv.negate != 0))) set_hit(B, sv.slot, r);
+  }
+}
+
+// chain through two buffers of capacity cap; -1 on overflow.  summ = byte
+// summary of v: transformations it proves to be identities are skipped.
+__device__ __forceinline__ int64_t run_chain(const DProgram& P, const DStream& S, const uint8_t* v, uint32_t vn,
+                                             uint32_t summ, uint8_t* b0, uint8_t* b1, uint32_t cap,
+                                             const uint8_t** out) {
+  const uint8_t* cur = v;
+  uint32_t cn = vn;
+  for (uint32_t k = 0; k < S.tchain_len; k++) {
+    const uint8_t code = (uint8_t)P.tchains32[S.tchain_off + k];
+    if (!(summ & transform_triggers(code))) continue;
+    uint8_t* dst = (cur == b0) ? b1 : b0;
+    const int64_t m = apply_transform(P, code, cur, cn, dst, cap);
+    if (m < 0) return -1;
+    cur = dst;
+    cn = (uint32_t)m;
+    summ = value_summary(cur, cn);
+  }
+  *out = cur;
+  return cn;
+}
+
+__device__ __forceinline__ void void_request(const DBatch& B, uint32_t r) {
+  ReqHdr* H = (ReqHdr*)(B.scratch + B.layout[r].base);
+  H->pa_void = 1;
+}
+
+// Slow-list entry: the transformed bytes are copied into the slow arena.
+struct SlowEnt {
+  uint32_t req, stream, fm, flags;  // flags: bit0 maybe
+  uint64_t off;                     // byte offset in B.slow_bytes
+  uint32_t len, _pad;
+};
+
+// Collapse a value for a stream whose automata map every non-ASCII rune to one
+// class: each rune >= 0x80 (a valid UTF-8 sequence, or one invalid byte that
+// utf8.DecodeRune reads as U+FFFD) becomes one GI_RUNE_MARK byte, so the
+// lockstep scan steps exactly once per rune, as the rune-decoding scan does.
+__device__ uint32_t collapse_runes(const uint8_t* s, uint32_t n, uint8_t* d) {
+  uint32_t o = 0;
+  for (uint32_t i = 0; i < n;) {
+    if (s[i] < 0x80) {
+      d[o++] = s[i++];
+    } else {
+      uint32_t w;
+      (void)decode_rune(s, n, i, &w);
+      i += w;
+      d[o++] = GI_RUNE_MARK;
+    }
+  }
+  return o;
+}
+
+// IN = per-lane LDS copy of the item's bytes (bucket maximum); WT = per-lane
+// LDS transformation buffers.  IN == 0: long items, HBM buffers throughout.
+template <uint32_t IN, uint32_t WT>
+__global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bucket) {
+  constexpr uint32_t IS = IN ? IN + 4 : 0;  // lane strides = odd dword counts: conflict-free
+  __shared__ __attribute__((aligned(16))) uint8_t lb[IN ? 64 * (IS + 2 * WT) : 16];
+  // Queue block of (item-wave, stream) = qblk[stream][item-wave index]: no
+  // counter.  Pool words are reserved GI_PCHUNK at a time per wave (one
+  // workgroup = one wave), so the pool counter sees one atomic per chunk.
+  __shared__ unsigned long long pnext, pend;
+  const uint32_t lane = threadIdx.x;
+  if (lane == 0) pnext = pend = 0;
+  __syncthreads();
+  const uint32_t iw_base = B.ibk[2 * GI_NB + bucket];
+  const uint32_t base = B.ibk[2 * bucket], cnt = B.ibk[2 * bucket + 1];
+  uint8_t* g0 = B.lscratch + ((uint64_t)blockIdx.x * 64 + lane) * 2ull * B.lcap;
+  uint8_t* g1 = g0 + B.lcap;
+  uint8_t* li = IN ? lb + lane * IS : nullptr;
+  uint8_t* b0 = IN ? lb + 64 * IS + lane * WT : g0;
+  uint8_t* b1 = IN ? lb + 64 * (IS + WT) + lane * WT : g1;
+  const uint32_t cap = IN ? WT : B.lcap;
+  for (uint32_t w0 = blockIdx.x * 64; w0 < cnt; w0 += gridDim.x * 64) {
+    const uint32_t ii = w0 + lane;
+    Item it{};
+    uint64_t gm = 0;
+    const uint8_t* src = nullptr;
+    uint32_t summ = 0;
+    if (ii < cnt) {
+      GI_BOUND(base + ii < B.items_cap, base + ii, B.items_cap);
+      it = ((const Item*)B.items)[base + ii];
+      GI_BOUND(it.req < B.n_req, it.req, ii);
+      gm = item_gmask(P, it);
+      src = it.vp;
+      if (IN && it.vn <= IN) {  // stage the scanned bytes once for all streams
+        for (uint32_t i = 0; i < it.vn; i++) li[i] = it.vp[i];
+        src = li;
+      }
+      summ = value_summary(src, it.vn);
+    }
+    const uint32_t blk = iw_base + w0 / 64;
+    for (uint32_t s = 0; s < P.n_streams; s++) {
+      const DStream S = P.streams[s];
+      uint32_t fm = 0;
+      for (uint32_t k = 0; k < S.filt_count; k++) fm |= (uint32_t)((gm >> P.sfilt[S.filt_begin + k]) & 1ull) << k;
+      if (!__ballot(fm != 0)) {
+        if (lane == 0 && S.job_count && blk < B.qcap) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2(0u, 0u);
+        continue;
+      }
+      const uint8_t* cur = nullptr;
+      int64_t cn = 0;
+      bool maybe = false, glob = !IN;
+      if (fm) {
+        cn = run_chain(P, S, src, it.vn, summ, b0, b1, cap, &cur);
+        if (cn < 0 && IN) {
+          cn = run_chain(P, S, src, it.vn, summ, g0, g1, B.lcap, &cur);
+          glob = true;
+        }
+        if (cn < 0) {
+          maybe = true;
+          cur = src;
+          cn = 0;
+        }
+        if (S.val_count) stream_vals(P, B, it.req, S, fm, maybe, cur, (uint32_t)cn);
+      }
+      if (!S.job_count) continue;
+      bool slow = maybe;
+      if (fm && !maybe) {
+        uint32_t hi = 0;
+        if (cur == src) hi = (summ & BS_HIGH) ? 0x80u : 0u;
+        else
+          for (uint32_t i = 0; i < (uint32_t)cn; i++) hi |= cur[i];
+        if (hi & 0x80) {
+          if (S.collapse) {
+            uint8_t* dst = glob ? (cur == g0 ? g1 : g0) : (cur == b0 ? b1 : b0);
+            cn = collapse_runes(cur, (uint32_t)cn, dst);
+            cur = dst;
+          } else {
+            slow = true;
+          }
+        }
+      }
+      if (fm && slow) {  // per-value path (k_scan_slow)
+        const uint32_t k = atomicAdd(B.slow_count, 1u);
+        const unsigned long long off = atomicAdd(B.slow_used, (unsigned long long)((cn + 15) & ~15ll));
+        if (k >= B.slow_cap || off + (uint64_t)cn > B.slow_bytes_cap) {
+          void_request(B, it.req);
+        } else {
+          for (uint32_t i = 0; i < (uint32_t)cn; i++) B.slow_bytes[off + i] = cur[i];
+          SlowEnt e;
+          e.req = it.req;
+          e.stream = s;
+          e.fm = fm;
+          e.flags = maybe ? 1u : 0u;
+          e.off = off;
+          e.len = (uint32_t)cn;
+          e._pad = 0;
+          ((SlowEnt*)B.slow)[k] = e;
+        }
+      }
+      const bool out = fm && !slow;
+      const uint64_t om = __ballot(out);
+      if (!om) {
+        if (lane == 0 && blk < B.qcap) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2(0u, 0u);
+        continue;
+      }
+      const uint32_t nv = __popcll(om);
+      const uint32_t nw = wave_max(out ? ((uint32_t)cn + 3) / 4 : 0u);
+      const uint64_t words = (uint64_t)nv * (3 + nw);
+      unsigned long long woff = 0;
+      if (lane == 0) {
+        if (pnext + words > pend) {
+          const unsigned long long sz = words > GI_PCHUNK ? words : (unsigned long long)GI_PCHUNK;
+          const unsigned long long b0p = atomicAdd(B.pool_used, sz);
+          pnext = b0p;
+          pend = b0p + sz;
+        }
+        woff = pnext;
+        pnext += words;
+      }
+      woff = __shfl(woff, 0, 64);
+      if (blk >= B.qcap || woff + words > B.pool_cap) {  // out of queue space: exact fallback
+        if (out) void_request(B, it.req);
+        if (lane == 0 && blk < B.qcap) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2(0u, 0u);
+        continue;
+      }
+      if (lane == 0) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2((uint32_t)woff, nv | (nw << 8));
+      if (out) {
+        const uint32_t i = mask_rank(om);
+        uint32_t* q = B.pool + woff;
+        q[i] = it.req;
+        q[nv + i] = fm;
+        q[2 * nv + i] = (uint32_t)cn;
+        const uint32_t nwi = ((uint32_t)cn + 3) / 4;
+        for (uint32_t w = 0; w < nwi; w++) {
+          uint32_t x = 0;
+          for (uint32_t b = 0; b < 4; b++) {
+            const uint32_t at = 4 * w + b;
+            x |= (at < (uint32_t)cn ? (uint32_t)cur[at] : 0u) << (8 * b);
+          }
+          q[3 * nv + (uint64_t)w * nv + i] = x;
+        }
+      }
+    }
+  }
+}
 
 __device__ __forceinline__ uint32_t rune_class(const DProgram& P, const DDfa& d, uint32_t r) {
   if (d.nonascii_uniform) return d.nonascii_cls;
@@ -1538,38 +2048,21 @@ __device__ __forceinline__ uint32_t rune_class(const DProgram& P, const DDfa& d,
   return (lo < d.nr_cnt && nr[lo * 3] <= r) ? nr[lo * 3 + 2] : 0u;
 }
 
-// Bit k of the result: pattern k of the automaton matches somewhere in s.
-// Single (sticky) automata return bit 0 only.
-__device__ __forceinline__ uint64_t jdfa_scan(const DProgram& P, const DDfa& d, const uint16_t* __restrict__ tr,
-                                              const uint8_t* __restrict__ amap, const uint8_t* __restrict__ combo,
-                                              const uint8_t* __restrict__ s, uint32_t n) {
+// Bit k of the result: pattern k of the automaton matches somewhere in s
+// (global tables; rune decoding exactly like utf8.DecodeRune).
+__device__ uint64_t scan_full(const DProgram& P, const DDfa& d, const uint8_t* s, uint32_t n) {
+  const uint16_t* tr = P.trans + d.trans_off;
+  const uint8_t* amap = P.u8pool + d.amap_off;
+  const uint8_t* combo = P.u8pool + d.combo_off;
   const uint32_t ncls = d.n_classes;
   uint32_t st = d.start;
-  uint32_t i = 0;
-  if (!d.multi) {
-    while (i < n) {
-      if (st == d.accept) return 1;
-      const uint8_t c = s[i];
-      uint32_t cls;
-      if (d.byte_mode || c < 0x80) {
-        cls = amap[c];
-        i++;
-      } else {
-        uint32_t w;
-        const uint32_t rr = decode_rune(s, n, i, &w);
-        i += w;
-        cls = rune_class(P, d, rr);
-      }
-      st = tr[st * ncls + cls];
-    }
-    return P.u8pool[d.endacc_off + st] != 0 ? 1ull : 0ull;
-  }
-  const uint64_t* __restrict__ acc = P.u64pool + d.acc_off;
   uint64_t m = 0;
-  while (i < n) {
+  const uint64_t* acc = P.u64pool + d.acc_off;
+  for (uint32_t i = 0; i < n;) {
+    if (!d.multi && st == d.accept) return 1;
     const uint8_t c = s[i];
     uint32_t cls;
-    if (c < 0x80) {
+    if (d.byte_mode || c < 0x80) {
       cls = amap[c];
       i++;
     } else {
@@ -1578,176 +2071,219 @@ __device__ __forceinline__ uint64_t jdfa_scan(const DProgram& P, const DDfa& d, 
       i += w;
       cls = rune_class(P, d, rr);
     }
-    const uint16_t tv = tr[st * ncls + cls];
-    if (tv & 0x8000) m |= acc[(uint64_t)st * 5 + combo[cls]];
-    st = tv & 0x7FFF;
-  }
-  return m | acc[(uint64_t)st * 5 + 4];
-}
-
-__device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
-  if (kind == OP_VALIDATE_BYTE_RANGE) {
-    for (uint32_t i = 0; i < n; i++)
-      if (!((bits[s[i] >> 5] >> (s[i] & 31)) & 1)) return true;
-    return false;
-  }
-  if (kind == OP_VALIDATE_URL_ENCODING) {
-    for (uint32_t i = 0; i < n;) {
-      if (s[i] == '%') {
-        if (i + 2 >= n) return true;
-        if (ishex(s[i + 1]) && ishex(s[i + 2])) i += 3;
-        else return true;
-      } else {
-        i++;
-      }
-    }
-    return false;
-  }
-  for (uint32_t i = 0; i < n;) {  // OP_VALIDATE_UTF8
-    uint32_t w;
-    uint32_t r = decode_rune(s, n, i, &w);
-    if (r == 0xFFFD && w == 1) return true;
-    i += w;
-  }
-  return false;
-}
-
-__device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
-  atomicOr(&B.hits[(uint64_t)(slot >> 5) * B.n_req + r], 1u << (slot & 31));
-}
-
-// Key filter of a rule target (selector + exclusions), as field_in() applies it.
-__device__ inline bool filter_ok(const DProgram& P, const DFilter& F, const Field& f) {
-  if (F.key_mode == 1) {
-    if (F.ci ? !eq_ascii_ci(f.k, f.kn, P.strpool + F.key_off, F.key_len)
-             : !eq_bytes(f.k, f.kn, P.strpool + F.key_off, F.key_len))
-      return false;
-  } else if (F.key_mode == 2) {
-    if (!dfa_match(P, F.key_dfa, f.k, f.kn, F.ci != 0)) return false;
-  }
-  for (uint32_t e = 0; e < F.exc_count; e++) {
-    const DExc x = P.excs[F.exc_begin + e];
-    if (x.dfa >= 0) {
-      if (dfa_match(P, x.dfa, f.k, f.kn, true)) return false;
-    } else if (eq_ascii_ci(f.k, f.kn, P.strpool + x.off, x.len)) {
-      return false;
-    }
-  }
-  return true;
-}
-
-// transform (chain) + match one value against the job; hit bits are emitted
-// per value (matches are rare); "maybe" (every admitted pattern) on overflow.
-__device__ void match_value(const DProgram& P, const DBatch& B, uint32_t r, const DStream& S, const DJob& J,
-                            const uint8_t* img, uint32_t fm, const uint8_t* v, uint32_t vn, uint8_t* s0,
-                            uint8_t* s1) {
-  const uint8_t* cur = v;
-  uint32_t cn = vn;
-  bool maybe = false;
-  bool ready = false;
-  for (uint32_t q = 0; q < J.jdfa_count + J.val_count; q++) {
-    uint64_t allowed = 0;
-    DJobDfa jd;
-    if (q < J.jdfa_count) {
-      jd = P.jdfas[J.jdfa_begin + q];
-      for (uint32_t f = fm; f; f &= f - 1) allowed |= P.u64pool[jd.fmask_off + (__ffs(f) - 1)];
-      if (!allowed) continue;
-    } else if (!(fm & P.svals[J.val_begin + q - J.jdfa_count].fmask)) {
-      continue;
-    }
-    if (!ready) {
-      ready = true;
-      for (uint32_t k = 0; k < S.tchain_len; k++) {
-        uint8_t* dst = (cur == s0) ? s1 : s0;
-        int64_t m = apply_transform(P, P.tchains[S.tchain_off + k], cur, cn, dst, B.tcap);
-        if (m < 0) {
-          maybe = true;
-          break;
-        }
-        cur = dst;
-        cn = (uint32_t)m;
-      }
-    }
-    if (q < J.jdfa_count) {
-      uint64_t m = allowed;
-      if (!maybe) {
-        const DDfa d = P.dfas[jd.dfa];
-        uint64_t x;
-        if (jd.lds_trans >= 0) {
-          x = jdfa_scan(P, d, (const uint16_t*)(img + jd.lds_trans), img + jd.lds_amap,
-                        img + (jd.lds_combo >= 0 ? jd.lds_combo : 0), cur, cn);
-        } else {
-          x = jdfa_scan(P, d, P.trans + d.trans_off, P.u8pool + d.amap_off, P.u8pool + d.combo_off, cur, cn);
-        }
-        m &= x ^ jd.neg_mask;
-      }
-      while (m) {
-        const int k = __ffsll((unsigned long long)m) - 1;
-        m &= m - 1;
-        set_hit(B, P.pats[jd.pat_begin + k].slot, r);
-      }
+    const uint32_t tv = tr[st * ncls + cls];
+    if (d.multi) {
+      if (tv & 0x8000) m |= acc[(uint64_t)st * 5 + combo[cls]];
+      st = tv & 0x7FFF;
     } else {
-      const DScanVal& sv = P.svals[J.val_begin + q - J.jdfa_count];
-      if (maybe || (validate_op(sv.kind, sv.bits, cur, cn) != (sv.negate != 0))) set_hit(B, sv.slot, r);
+      st = tv;
+    }
+  }
+  if (d.multi) return m | acc[(uint64_t)st * 5 + 4];
+  return P.u8pool[d.endacc_off + st] ? 1ull : 0ull;
+}
+
+// Per-value path on global tables: every automaton of job J over one value.
+__device__ void scan_value_global(const DProgram& P, const DBatch& B, uint32_t r, const DJob& J, uint32_t fm,
+                                  bool maybe, const uint8_t* v, uint32_t n) {
+  for (uint32_t q = 0; q < J.jdfa_count; q++) {
+    const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
+    uint64_t al = 0;
+    for (uint32_t f = fm; f; f &= f - 1) al |= P.u64pool[jd.fmask_off + (__ffs(f) - 1)];
+    if (!al) continue;
+    uint64_t x = al;
+    if (!maybe) x &= scan_full(P, P.dfas[jd.dfa], v, n) ^ jd.neg_mask;
+    while (x) {
+      const int k = __ffsll((unsigned long long)x) - 1;
+      x &= x - 1;
+      set_hit(B, P.pats[jd.pat_begin + k].slot, r);
     }
   }
 }
 
-__global__ void __launch_bounds__(256) k_match(DProgram P, DBatch B, uint32_t n_tiles) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t img[];
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  uint8_t* s0 = B.tscratch + (uint64_t)tid * 2ull * B.tcap;
-  uint8_t* s1 = s0 + B.tcap;
-  const uint64_t n_units = (uint64_t)P.n_jobs * n_tiles;
+// Patterns of automaton q the admitting filters fm let through (image table).
+__device__ __forceinline__ uint64_t img_allowed(const uint8_t* img, uint32_t fmask_off, uint32_t nf, uint32_t q,
+                                                uint32_t fm) {
+  uint64_t a = 0;
+  for (uint32_t f = fm; f; f &= f - 1) a |= *(const uint64_t*)(img + fmask_off + 8 * (q * nf + (__ffs(f) - 1)));
+  return a;
+}
+
+__device__ __forceinline__ void emit_img(const DBatch& B, uint32_t r, const uint8_t* img, uint32_t slots_off,
+                                         uint64_t x) {
+  while (x) {
+    const int k = __ffsll((unsigned long long)x) - 1;
+    x &= x - 1;
+    set_hit(B, *(const uint32_t*)(img + slots_off + 4 * k), r);
+  }
+}
+
+// Accepting transition of union automaton q (rare): emit its matches now.
+__device__ void union_accept(const DProgram& P, const DBatch& B, uint32_t r, const DJob& J, const uint8_t* img,
+                             uint32_t nf, uint32_t q, uint32_t fm, uint32_t st, uint32_t cls) {
+  const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
+  const DDfa d = P.dfas[jd.dfa];
+  const uint64_t x = P.u64pool[d.acc_off + st * 5 + img[jd.lds_combo + cls]] & img_allowed(img, J.lds_fmask, nf, q, fm);
+  if (x) emit_img(B, r, img, jd.lds_slots, x);
+}
+
+// End of a value: end-of-input matches of every automaton (negation applied).
+__device__ void value_end(const DProgram& P, const DBatch& B, uint32_t r, const DJob& J, const uint8_t* img,
+                          uint32_t nf, uint32_t K, uint32_t fm, const uint32_t* st) {
+  for (uint32_t q = 0; q < K; q++) {
+    const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
+    GI_BOUND(st[q] < P.dfas[jd.dfa].n_states, st[q], q);
+    const uint64_t al = img_allowed(img, J.lds_fmask, nf, q, fm);
+    if (!al) continue;
+    const DDfa d = P.dfas[jd.dfa];
+    uint64_t bits;
+    if (d.multi) bits = *(const uint64_t*)(img + jd.lds_endacc + 8 * st[q]);
+    else bits = img[jd.lds_endacc + st[q]] ? 1ull : 0ull;
+    const uint64_t x = (bits ^ jd.neg_mask) & al;
+    if (x) emit_img(B, r, img, jd.lds_slots, x);
+  }
+}
+
+// One automaton step (q uniform): class from the joint map, transition from the image.
+#define SCAN_STEP(q)                                                                        \
+  if ((q) < K) {                                                                            \
+    const uint32_t cls = (jm >> (8 * (q))) & 0xFFu;                                         \
+    const uint32_t tv = *(const uint16_t*)(img + (trn[q] & 0xFFFFFu) + 2 * (st[q] * (trn[q] >> 20) + cls)); \
+    if ((umask >> (q)) & 1u) {                                                              \
+      if (tv & 0x8000u) union_accept(P, B, req, J, img, nf, (q), fm, st[q], cls);          \
+      st[q] = tv & 0x7FFFu;                                                                 \
+    } else {                                                                                \
+      st[q] = tv;                                                                           \
+    }                                                                                       \
+  }
+
+// One wave scans one queue block (<= 64 values of the job's stream).
+__device__ __forceinline__ void scan_qblock(const DProgram& P, const DBatch& B, const DJob& J, const uint8_t* img,
+                                            uint32_t K, const uint32_t* trn, const uint32_t* st0, uint32_t umask,
+                                            uint32_t nf, uint2 d, uint32_t mode) {
+  const uint32_t lane = lane_id();
+  const uint32_t woff = d.x, nv = d.y & 0xFFu, nw = d.y >> 8;
+  if (nv == 0) return;
+  GI_BOUND(nv <= 64 && (uint64_t)woff + (uint64_t)(3 + nw) * nv <= B.pool_cap, woff, d.y);
+  const uint32_t* q = B.pool + woff;
+  uint32_t req = 0, fm = 0, len = 0;
+  bool act = false;
+  if (lane < nv) {
+    req = q[lane];
+    fm = q[nv + lane];
+    len = q[2 * nv + lane];
+    GI_BOUND(req < B.n_req && len <= 4 * nw, req, len);
+    uint64_t any = 0;
+    for (uint32_t k = 0; k < K; k++) any |= img_allowed(img, J.lds_fmask, nf, k, fm);
+    act = any != 0;
+  }
+  if (mode & 2) return;
+  if (mode & 16) umask = 0;
+  uint32_t st[GI_JOB_MAX_DFA];
+#pragma unroll
+  for (uint32_t k = 0; k < GI_JOB_MAX_DFA; k++) st[k] = st0[k];
+  const uint32_t* jam = (const uint32_t*)img;
+  const uint32_t* wp = q + 3 * nv + lane;
+  for (uint32_t w = 0; w < nw; w++) {
+    if (act && 4 * w < len && !(mode & 4)) {
+      const uint32_t wd = wp[(uint64_t)w * nv];
+      const uint32_t nb = min(4u, len - 4 * w);
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) {
+        if (b < nb) {
+          const uint32_t jm = jam[(wd >> (8 * b)) & 0xFFu];  // ASCII or GI_RUNE_MARK
+          SCAN_STEP(0)
+          SCAN_STEP(1)
+          SCAN_STEP(2)
+          SCAN_STEP(3)
+        }
+      }
+    }
+  }
+  if (act && !(mode & 8)) value_end(P, B, req, J, img, nf, K, fm, st);
+}
+
+// Persistent kernel over units (job, 1024 queue-block entries), job-major.
+// Each wave reads 64 entries of its job's stream list (one per lane) and scans
+// the non-empty ones one after the other.  LDS: the job image is copied once
+// per job change; !LDS: the image is read from HBM (automata too large for LDS).
+template <bool LDS>
+__global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint32_t* __restrict__ jl, uint32_t n_jl,
+                                               uint32_t mode) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t simg[];
+  __shared__ uint2 clist[1024];
+  __shared__ uint32_t wcnt[16];
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nwv = blockDim.x >> 6;
+  const uint32_t n_iw = min(B.ibk[3 * GI_NB], B.qcap);
+  const uint32_t per_unit = blockDim.x;  // entries per unit
+  const uint32_t nu_job = (n_iw + per_unit - 1) / per_unit;
+  const uint64_t n_units = (uint64_t)nu_job * n_jl;
   uint32_t loaded = 0xFFFFFFFFu;
   for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
-    const uint32_t j = (uint32_t)(u / n_tiles);
-    const uint32_t tile = (uint32_t)(u - (uint64_t)j * n_tiles);
+    const uint32_t jj = (uint32_t)(u / nu_job);
+    const uint32_t chunk = (uint32_t)(u - (uint64_t)jj * nu_job);
+    const uint32_t j = jl[jj];
     const DJob J = P.jobs[j];
-    if (j != loaded) {  // block-uniform
-      __syncthreads();
-      const uint4* src = (const uint4*)(P.images + J.img_off);
-      for (uint32_t k = threadIdx.x; k < J.img_bytes / 16; k += blockDim.x) ((uint4*)img)[k] = src[k];
-      __syncthreads();
-      loaded = j;
+    const uint8_t* img = P.images + J.img_off;
+    if (LDS) {
+      if (j != loaded) {  // block-uniform
+        __syncthreads();
+        const uint4* src = (const uint4*)(P.images + J.img_off);
+        for (uint32_t k = threadIdx.x; k < (J.img_bytes + 15) / 16; k += blockDim.x) ((uint4*)simg)[k] = src[k];
+        __syncthreads();
+        loaded = j;
+      }
+      img = simg;
     }
-    const uint32_t r = tile * 256 + threadIdx.x;
-    if (r >= B.n_req) continue;
-    const uint8_t* base = B.scratch + B.layout[r].base;
-    const ReqHdr* H = (const ReqHdr*)base;
-    if (H->flags & GI_REQ_ERROR_MASK) continue;
-    const DStream S = P.streams[J.stream];
-    for (uint32_t k = 0; k < S.filt_count; k++) {
-      const uint8_t sg = P.filters[S.filt_begin + k].single;
-      if (sg == GI_NO_SINGLE) continue;
-      const Str v = H->single[sg];
-      match_value(P, B, r, S, J, img, 1u << k, v.p, v.n, s0, s1);
+    if (mode & 1) continue;
+    // compact the unit's non-empty queue blocks into LDS, then deal them out
+    // to the 16 waves round-robin (balanced within the workgroup)
+    const uint32_t e = chunk * per_unit + wv * 64 + lane;
+    uint2 mine = make_uint2(0u, 0u);
+    if (e < n_iw) mine = B.qblk[(uint64_t)J.stream * B.qcap + e];
+    const uint64_t live = __ballot((mine.y & 0xFFu) != 0);
+    if (lane == 0) wcnt[wv] = __popcll(live);
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+    for (uint32_t w = 0; w < nwv; w++) {
+      const uint32_t c = wcnt[w];
+      wbase += w < wv ? c : 0u;
+      total += c;
     }
-    if (!S.kind_mask) continue;
-    const Field* F = (const Field*)(base + 256);
-    const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck;
-    for (int kind = FK_ARG_GET; kind <= FK_COOKIE; kind++) {
-      if (!((S.kind_mask >> kind) & 1)) continue;
-      uint32_t b = 0, e = 0;
-      if (kind == FK_ARG_GET) { b = 0; e = n_get; }
-      else if (kind == FK_HEADER) { b = n_get; e = n_get + n_hdr; }
-      else if (kind == FK_COOKIE) { b = n_get + n_hdr; e = n_get + n_hdr + n_ck; }
-      else continue;
-      for (uint32_t i = b; i < e; i++) {
-        const Field f = F[i];
-        uint32_t fv = 0, fk = 0;
-        for (uint32_t k = 0; k < S.filt_count; k++) {
-          const DFilter Fl = P.filters[S.filt_begin + k];
-          if (Fl.single != GI_NO_SINGLE || !((Fl.kind_mask >> kind) & 1)) continue;
-          if (filter_ok(P, Fl, f)) {
-            if (Fl.names) fk |= 1u << k;
-            else fv |= 1u << k;
-          }
-        }
-        if (fv) match_value(P, B, r, S, J, img, fv, f.v, f.vn, s0, s1);
-        if (fk) match_value(P, B, r, S, J, img, fk, f.k, f.kn, s0, s1);
+    if ((mine.y & 0xFFu) != 0) clist[wbase + mask_rank(live)] = mine;
+    __syncthreads();
+    const uint32_t nf = P.streams[J.stream].filt_count;
+    const uint32_t K = J.jdfa_count;
+    uint32_t trn[GI_JOB_MAX_DFA], st0[GI_JOB_MAX_DFA], umask = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < GI_JOB_MAX_DFA; k++) {
+      trn[k] = 0;
+      st0[k] = 0;
+      if (k < K) {
+        const DJobDfa jd = P.jdfas[J.jdfa_begin + k];
+        const DDfa d = P.dfas[jd.dfa];
+        trn[k] = (uint32_t)jd.lds_trans | (d.n_classes << 20);
+        st0[k] = d.start;
+        if (d.multi) umask |= 1u << k;
       }
     }
+    for (uint32_t i = wv; i < total; i += nwv) scan_qblock(P, B, J, img, K, trn, st0, umask, nf, clist[i], mode);
+    __syncthreads();  // clist / wcnt reuse
+  }
+}
+
+// Slow values (non-ASCII / "maybe"), one thread per list entry: every job of
+// the value's stream on the global tables.
+__global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
+  const uint32_t n = min(*B.slow_count, B.slow_cap);
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const SlowEnt x = ((const SlowEnt*)B.slow)[e];
+    GI_BOUND(x.req < B.n_req && x.stream < P.n_streams && x.off + x.len <= B.slow_bytes_cap, x.req, x.stream);
+    const DStream S = P.streams[x.stream];
+    for (uint32_t j = S.job_begin; j < S.job_begin + S.job_count; j++)
+      scan_value_global(P, B, x.req, P.jobs[j], x.fm, (x.flags & 1) != 0, B.slow_bytes + x.off, x.len);
   }
 }
 
@@ -1755,11 +2291,11 @@ __global__ void __launch_bounds__(256) k_match(DProgram P, DBatch B, uint32_t n_
 // RuleGroup.Eval(1) -> ProcessRequestBody -> RuleGroup.Eval(2) per request,
 // skipping every phase-A rule whose hit bit is clear.
 __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
-  __shared__ unsigned long long red[6];
+  __shared__ unsigned long long red[7];
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (threadIdx.x < 6) red[threadIdx.x] = 0;
+  if (threadIdx.x < 7) red[threadIdx.x] = 0;
   __syncthreads();
-  unsigned long long my[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
   if (r < B.n_req) {
     const gi_request rq = B.reqs[r];
     Region g = region_of(P, B, r);
@@ -1770,6 +2306,7 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
     t.n_req = B.n_req;
     t.req = r;
     t.has_post = false;
+    t.pa_void = H->pa_void != 0;
     t.nf = H->nf;
     t.nb = H->nb;
     t.flags = H->flags;
@@ -1847,43 +2384,73 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
     my[3] = (t.flags & GI_REQ_ERROR_MASK) ? 1 : 0;
     my[4] = scanned;
     my[5] = t.nmatched;
+    my[6] = t.pa_void ? 1 : 0;
   }
-  for (int c = 0; c < 6; c++) {
+  for (int c = 0; c < 7; c++) {
     unsigned long long x = my[c];
     for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
     if ((threadIdx.x & 63) == 0) atomicAdd(&red[c], x);
   }
   __syncthreads();
-  if (threadIdx.x < 6) atomicAdd(&B.tally[threadIdx.x], red[threadIdx.x]);
+  if (threadIdx.x < 7) atomicAdd(&B.tally[threadIdx.x], red[threadIdx.x]);
 }
 
-uint32_t scan_resident_threads(uint32_t lds_bytes) {
+void scan_allow_lds(uint32_t lds_bytes) {
+  if (lds_bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+}
+
+uint32_t scan_resident_blocks(uint32_t lds_bytes) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, dev);
   int per_cu = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_match, 256, lds_bytes);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scan<true>, 1024, lds_bytes);
   if (per_cu < 1) per_cu = 1;
-  return (uint32_t)prop.multiProcessorCount * (uint32_t)per_cu * 256u;
+  return (uint32_t)prop.multiProcessorCount * (uint32_t)per_cu;
 }
 
-void launch_pipeline(const DProgram& P, const DBatch& B, uint32_t scan_threads, hipStream_t stream,
-                     hipEvent_t* ev) {
+#define GI_LAUNCH(name, ...)                                                              \
+  do {                                                                                    \
+    if (stop_after && ++nk > stop_after) return;                                          \
+    hipLaunchKernelGGL(__VA_ARGS__);                                                      \
+    if (stop_after) {                                                                     \
+      hipError_t e_ = hipStreamSynchronize(stream);                                       \
+      fprintf(stderr, "GI_STOP_AFTER: kernel %d %s -> %s\n", nk, name, hipGetErrorString(e_)); \
+      if (e_ != hipSuccess) return;                                                       \
+    }                                                                                     \
+  } while (0)
+
+void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
+                     int stop_after) {
   if (!B.n_req) return;
+  int nk = 0;
   const uint32_t cb = (B.n_req + 255) / 256;
-  hipLaunchKernelGGL(k_collect, dim3(cb), dim3(256), 0, stream, P, B);
+  GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[0], stream);
-  const uint32_t n_tiles = (B.n_req + 255) / 256;
-  const uint64_t units = (uint64_t)P.n_jobs * n_tiles;
-  if (units) {
-    uint64_t blocks = units;
-    const uint64_t maxb = scan_threads / 256;
-    if (blocks > maxb) blocks = maxb;
-    hipLaunchKernelGGL(k_match, dim3((uint32_t)blocks), dim3(256), P.max_img_bytes, stream, P, B, n_tiles);
+  if (P.n_streams) {
+    GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(1), dim3(1024), 0, stream, B, cb);
+    GI_LAUNCH("k_items", k_items, dim3(cb), dim3(256), 0, stream, P, B);
+    GI_LAUNCH("k_stream0", (k_stream<16, 20>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 0u);
+    GI_LAUNCH("k_stream1", (k_stream<32, 36>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 1u);
+    GI_LAUNCH("k_stream2", (k_stream<64, 68>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 2u);
+    GI_LAUNCH("k_stream3", (k_stream<128, 132>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
+    GI_LAUNCH("k_stream4", (k_stream<0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
+    if (ev) (void)hipEventRecord(ev[1], stream);
+    for (int big = 0; big < 2; big++)
+      if (S.n_jobs[big])
+        GI_LAUNCH("k_scan", k_scan<true>, dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B, S.jobs[big],
+                  S.n_jobs[big], S.mode);
+    if (S.n_global)
+      GI_LAUNCH("k_scan_hbm", k_scan<false>, dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
+                S.n_global, S.mode);
+    GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
+  } else if (ev) {
+    (void)hipEventRecord(ev[1], stream);
   }
-  if (ev) (void)hipEventRecord(ev[1], stream);
-  hipLaunchKernelGGL(k_eval, dim3((B.n_req + 127) / 128), dim3(128), 0, stream, P, B);
+  if (ev) (void)hipEventRecord(ev[2], stream);
+  GI_LAUNCH("k_eval", k_eval, dim3((B.n_req + 127) / 128), dim3(128), 0, stream, P, B);
 }
 
 }  // namespace gi

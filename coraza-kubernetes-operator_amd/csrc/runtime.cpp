@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -56,6 +58,14 @@ const std::vector<std::string> kDefaultExports = {
     "inbound_anomaly_score_pl3", "inbound_anomaly_score_pl4", "detection_inbound_anomaly_score",
     "anomaly_score", "0"};
 
+// Phase-A arena sizing factor (GI_PA_FACTOR overrides; see gi_stage_batch).
+// Queue-pool sizing factor (GI_POOL_FACTOR overrides; see gi_stage_batch).
+double pool_factor_env() {
+  const char* v = getenv("GI_POOL_FACTOR");
+  double f = v ? atof(v) : 0.0;
+  return f > 0 ? f : 1.0;
+}
+
 }  // namespace
 
 struct gi_ctx {
@@ -68,11 +78,16 @@ struct gi_ctx {
   DProgram prog{};
   std::vector<DevBuf> pbufs;
   // batch buffers
-  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, hits, tscratch;
-  uint32_t scan_threads = 0;
-  uint32_t tcap = 2048;
+  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, hits, joblist;
+  // phase A
+  DevBuf bcounts, boffs, items, lscratch, pool, qblk, ctr, slow, slow_bytes;
+  uint32_t lcap = 0, qcap = 0, slow_cap = 0;
+  uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0;
+  bool diag_on = false;
+  int stop_after = 0;  // debugging: launch only the first N pipeline kernels, synchronising after each
+  ScanLaunch scan{};
   uint32_t hit_words = 0;
-  hipEvent_t evs[2] = {nullptr, nullptr};
+  hipEvent_t evs[3] = {nullptr, nullptr, nullptr};
   uint32_t n_req = 0;
   bool staged = false, ran = false;
   gi_stats stats{};
@@ -171,12 +186,15 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->rs = rs;
   c->device = device;
   c->mcap = matched_cap ? matched_cap : 64;
+  c->diag_on = getenv("GI_DIAG") && atoi(getenv("GI_DIAG")) > 0;
+  c->stop_after = getenv("GI_STOP_AFTER") ? atoi(getenv("GI_STOP_AFTER")) : 0;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e == hipSuccess) e = hipEventCreate(&c->evs[0]);
   if (e == hipSuccess) e = hipEventCreate(&c->evs[1]);
+  if (e == hipSuccess) e = hipEventCreate(&c->evs[2]);
   if (e != hipSuccess) {
     delete c;
     return GI_ENODEV;
@@ -222,6 +240,11 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   UP(images, P.images, uint8_t)
   UP(pats, P.pats, DPat)
   UP(svals, P.svals, DScanVal)
+  std::vector<uint32_t> sfilt32(P.sfilt.begin(), P.sfilt.end());
+  std::vector<uint32_t> tch32(P.tchains.begin(), P.tchains.end());
+  UP(sfilt, sfilt32, uint32_t)
+  UP(tchains32, tch32, uint32_t)
+  UP(always_slots, P.always_slots, uint32_t)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
@@ -239,12 +262,46 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->prog.body_limit = P.body_limit;
   c->prog.n_jobs = (uint32_t)P.jobs.size();
   c->prog.max_img_bytes = P.max_img_bytes;
+  c->prog.max_big_img_bytes = P.max_big_img_bytes;
+  c->prog.n_streams = (uint32_t)P.streams.size();
+  if (c->prog.n_streams > GI_MAX_STREAMS) {
+    gi_ctx_free(c);
+    return GI_EINVAL;
+  }
+  c->prog.n_always = (uint32_t)P.always_slots.size();
+  c->prog.n_gfilters = (uint32_t)P.filters.size();
+  c->prog.item_singles = P.item_singles;
+  for (int k = 0; k < 8; k++) c->prog.item_sides[k] = P.item_sides[k];
   c->prog.n_hit_slots = P.n_hit_slots;
-  c->scan_threads = scan_resident_threads(P.max_img_bytes);
-  if (c->tscratch.ensure((size_t)c->scan_threads * 2 * c->tcap) != hipSuccess) {
+  // k_scan plan: LDS jobs that fit the small image go to the 2-per-CU launch,
+  // the rest (big images, global-table automata) to the 1-per-CU launch.
+  std::vector<uint32_t> jl[3];
+  const bool force_hbm = getenv("GI_SCAN_HBM") && atoi(getenv("GI_SCAN_HBM")) > 0;  // debugging
+  for (uint32_t j = 0; j < P.jobs.size(); j++)
+    jl[(force_hbm || !P.jobs[j].lds) ? 2 : P.jobs[j].big ? 1 : 0].push_back(j);
+  std::vector<uint32_t> all(jl[0]);
+  all.insert(all.end(), jl[1].begin(), jl[1].end());
+  all.insert(all.end(), jl[2].begin(), jl[2].end());
+  if (upload(&c->joblist, all, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
     gi_ctx_free(c);
     return GI_ENOMEM;
   }
+  for (int b = 0; b < 2; b++) {
+    c->scan.jobs[b] = (const uint32_t*)c->joblist.p + (b ? jl[0].size() : 0);
+    c->scan.n_jobs[b] = (uint32_t)jl[b].size();
+    c->scan.lds[b] = b ? std::max<uint32_t>(P.max_big_img_bytes, 16) : std::max<uint32_t>(P.max_img_bytes, 16);
+    scan_allow_lds(c->scan.lds[b]);
+    c->scan.blocks[b] = scan_resident_blocks(c->scan.lds[b]);
+    c->scan.rpl[b] = 4;
+  }
+  c->scan.global_jobs = (const uint32_t*)c->joblist.p + jl[0].size() + jl[1].size();
+  c->scan.n_global = (uint32_t)jl[2].size();
+  c->scan.blocks[2] = scan_resident_blocks(16);
+  c->scan.mode = getenv("GI_SCAN_MODE") ? (uint32_t)atoi(getenv("GI_SCAN_MODE")) : 0u;
+  if (c->stop_after)
+    fprintf(stderr, "scan plan: small %u jobs lds %u blocks %u | big %u jobs lds %u blocks %u | hbm %u jobs blocks %u\n",
+            c->scan.n_jobs[0], c->scan.lds[0], c->scan.blocks[0], c->scan.n_jobs[1], c->scan.lds[1],
+            c->scan.blocks[1], c->scan.n_global, c->scan.blocks[2]);
   *out = c;
   return GI_OK;
 }
@@ -255,7 +312,8 @@ void gi_ctx_free(gi_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& b : c->pbufs) b.release();
   for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally,
-                    &c->hits, &c->tscratch})
+                    &c->hits, &c->joblist, &c->bcounts, &c->boffs, &c->items, &c->lscratch, &c->pool, &c->qblk,
+                    &c->ctr, &c->slow, &c->slow_bytes})
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
@@ -277,8 +335,11 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   const uint32_t n = in->n_req;
   // validate spans and lay out per-request scratch (lengths only)
   std::vector<ReqLayout> lay(n);
-  uint64_t off = 0;
+  uint64_t off = 0, items_cap = 0, raw_total = 0;
+  uint32_t max_cap_t = 64;
   const uint32_t nslots = c->rs->prog.n_slots;
+  const Program& PG = c->rs->prog;
+  const uint32_t n_single_items = (uint32_t)__builtin_popcount(PG.item_singles);
   for (uint32_t r = 0; r < n; r++) {
     const gi_request& q = in->reqs[r];
     const gi_span* sp[4] = {&q.method, &q.uri, &q.proto, &q.body};
@@ -287,12 +348,13 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if ((uint64_t)q.hdr_begin + q.hdr_count > in->n_headers) return fail(c, GI_EINVAL, "header range out of range");
     uint64_t maxv = std::max<uint64_t>({(uint64_t)q.uri.len * 3 + 2, (uint64_t)q.method.len + q.uri.len + q.proto.len + 2,
                                         (uint64_t)q.body.len, 64});
-    uint64_t cookie = 0, ncookie = 0;
+    uint64_t cookie = 0, ncookie = 0, hdr_bytes = 0;
     for (uint32_t h = 0; h < q.hdr_count; h++) {
       const gi_header& hd = in->headers[q.hdr_begin + h];
       if (hd.name.off + hd.name.len > in->data_len || hd.value.off + hd.value.len > in->data_len)
         return fail(c, GI_EINVAL, "header span out of range");
       maxv = std::max<uint64_t>(maxv, std::max(hd.name.len, hd.value.len));
+      hdr_bytes += hd.name.len + hd.value.len;
       if (hd.name.len == 6) {
         const uint8_t* nm = in->data + hd.name.off;
         bool ck = true;
@@ -311,13 +373,22 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     uint64_t cap_mt = 2 * maxv + 512;
     if (cap_f > 0xFFFFFFFFull || cap_b > 0xFFFFFFFFull || cap_t > 0xFFFFFFFFull || cap_mt > 0xFFFFFFFFull)
       return fail(c, GI_EINVAL, "request too large");
+    // phase-A items: at most both sides of every field (GET args, headers,
+    // cookies; POST args appear after phase 1) plus the filtered singles
+    const uint64_t pre_body_fields = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie);
+    items_cap += 2 * pre_body_fields + n_single_items;
+    raw_total += (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
+    max_cap_t = (uint32_t)std::max<uint64_t>(max_cap_t, cap_t);
     ReqLayout& L = lay[r];
+    L.pa_base = 0;
+    L.pa_cap = 0;
+    L._pad = 0;
     L.base = off;
     L.cap_f = (uint32_t)cap_f;
     L.cap_b = (uint32_t)cap_b;
     L.cap_t = (uint32_t)cap_t;
     L.cap_mt = (uint32_t)cap_mt;
-    uint64_t sz = 256 + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + (cap_b + 15) / 16 * 16 +
+    uint64_t sz = 256 + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + 128 + (cap_b + 15) / 16 * 16 +
                   2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
     off += (sz + 63) / 64 * 64;
   }
@@ -334,9 +405,37 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if ((e = c->matched.ensure(std::max<size_t>((size_t)n * c->mcap * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc matched");
   if ((e = c->tally.ensure(sizeof(gi_tally))) != hipSuccess) return hip_fail(c, e, "alloc tally");
-  c->hit_words = (c->rs->prog.n_hit_slots + 31) / 32;
+  c->hit_words = (PG.n_hit_slots + 31) / 32;
   if ((e = c->hits.ensure(std::max<size_t>((size_t)c->hit_words * n * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc hits");
+  if (!PG.streams.empty()) {
+    // phase A: items, per-lane transformation scratch, queue pool + blocks,
+    // slow list.  Pool / slow-list overflow only voids the phase-A bits of the
+    // requests concerned (k_eval then evaluates their rules in full).
+    const uint32_t cb = (n + 255) / 256;
+    const uint32_t ns = (uint32_t)PG.streams.size();
+    c->items_cap = std::max<uint64_t>(items_cap, 1);
+    c->lcap = (std::min<uint32_t>(max_cap_t, 4096) + 15) & ~15u;
+    // chunked reservations leave at most one partial chunk per (k_stream
+    // wave, launch) unused: both capacities carry that slack
+    const uint64_t waves = (uint64_t)GI_STREAM_GRID * 5;
+    c->qcap = (uint32_t)std::min<uint64_t>(c->items_cap / 64 + 8, 0xFFFFFFFull);  // item-waves
+    const double pf = pool_factor_env();
+    c->pool_cap = std::min<uint64_t>((uint64_t)(pf * (1024.0 * n + 8.0 * raw_total)) + waves * GI_PCHUNK + 4096,
+                                     0xFFFFFFF0ull);
+    c->slow_cap = (uint32_t)std::min<uint64_t>(4ull * n + 4096, 0x7FFFFFFFull);
+    c->slow_bytes_cap = 64ull * c->slow_cap;
+    if ((e = c->bcounts.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc bcounts");
+    if ((e = c->boffs.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc boffs");
+    if ((e = c->items.ensure(32ull * c->items_cap)) != hipSuccess) return hip_fail(c, e, "alloc items");
+    if ((e = c->lscratch.ensure((uint64_t)GI_STREAM_GRID * 64 * 2 * c->lcap)) != hipSuccess)
+      return hip_fail(c, e, "alloc lane scratch");
+    if ((e = c->pool.ensure(4ull * c->pool_cap)) != hipSuccess) return hip_fail(c, e, "alloc queue pool");
+    if ((e = c->qblk.ensure(8ull * ns * c->qcap)) != hipSuccess) return hip_fail(c, e, "alloc queue blocks");
+    if ((e = c->ctr.ensure(160 + 4ull * ns)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+    if ((e = c->slow.ensure(32ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
+    if ((e = c->slow_bytes.ensure(c->slow_bytes_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
+  }
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && n) e = hipMemcpyAsync(c->reqs.p, in->reqs, n * sizeof(gi_request), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && in->n_headers)
@@ -348,6 +447,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   c->staged = true;
   c->ran = false;
   c->stats.last_scratch_bytes = off;
+  c->stats.last_pa_bytes = 4ull * c->pool_cap;
   c->stats.last_stage_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return GI_OK;
@@ -371,14 +471,44 @@ int gi_run_staged(gi_ctx* c) {
   B.matched = (uint32_t*)c->matched.p;
   B.tally = (unsigned long long*)c->tally.p;
   B.hits = (uint32_t*)c->hits.p;
-  B.tscratch = (uint8_t*)c->tscratch.p;
-  B.tcap = c->tcap;
+  {
+    // counters (bytes): [0] pool words used, [8] slow bytes used, [16] slow
+    // entries, [64] item buckets {(base, count) x5, item-wave base x5, item
+    // waves}, [128] debug record, [160] qcount[stream] (unused)
+    uint8_t* cp = (uint8_t*)c->ctr.p;
+    B.bcounts = (uint32_t*)c->bcounts.p;
+    B.boffs = (uint32_t*)c->boffs.p;
+    B.ibk = (uint32_t*)(cp + 64);
+    B.items = c->items.p;
+    B.lscratch = (uint8_t*)c->lscratch.p;
+    B.lcap = c->lcap;
+    B.pool = (uint32_t*)c->pool.p;
+    B.pool_cap = c->pool_cap;
+    B.pool_used = (unsigned long long*)cp;
+    B.qblk = (uint2*)c->qblk.p;
+    B.qcount = (uint32_t*)(cp + 160);
+    B.qcap = c->qcap;
+    B.slow = c->slow.p;
+    B.slow_count = (uint32_t*)(cp + 16);
+    B.slow_cap = c->slow_cap;
+    B.slow_bytes = (uint8_t*)c->slow_bytes.p;
+    B.slow_bytes_cap = c->slow_bytes_cap;
+    B.slow_used = (unsigned long long*)(cp + 8);
+    B.diag = nullptr;
+    B.items_cap = c->items_cap;
+    B.n_hit_slots = c->rs->prog.n_hit_slots;
+    B.dbg = (uint32_t*)(cp + 128);  // 4 words (only written by -DGI_DEBUG builds)
+  }
   (void)hipEventRecord(c->ev0, c->stream);
+  if (c->ctr.p) {
+    e = hipMemsetAsync(c->ctr.p, 0, c->ctr.cap, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "memset counters");
+  }
   if (c->hit_words) {
     e = hipMemsetAsync(c->hits.p, 0, (size_t)c->hit_words * c->n_req * 4, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "memset hits");
   }
-  launch_pipeline(c->prog, B, c->scan_threads, c->stream, c->evs);
+  launch_pipeline(c->prog, B, c->scan, c->stream, c->evs, c->stop_after);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(c, e, "launch pipeline");
   (void)hipEventRecord(c->ev1, c->stream);
@@ -396,8 +526,26 @@ int gi_sync(gi_ctx* c) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->stats.last_kernel_ms = ms;
     if (c->n_req && hipEventElapsedTime(&ms, c->ev0, c->evs[0]) == hipSuccess) c->stats.last_collect_ms = ms;
-    if (c->n_req && hipEventElapsedTime(&ms, c->evs[0], c->evs[1]) == hipSuccess) c->stats.last_scan_ms = ms;
-    if (c->n_req && hipEventElapsedTime(&ms, c->evs[1], c->ev1) == hipSuccess) c->stats.last_eval_ms = ms;
+    if (c->n_req && hipEventElapsedTime(&ms, c->evs[0], c->evs[1]) == hipSuccess) c->stats.last_stream_ms = ms;
+    if (c->n_req && hipEventElapsedTime(&ms, c->evs[1], c->evs[2]) == hipSuccess) c->stats.last_scan_ms = ms;
+    if (c->n_req && hipEventElapsedTime(&ms, c->evs[2], c->ev1) == hipSuccess) c->stats.last_eval_ms = ms;
+#ifdef GI_DEBUG
+    if (c->ctr.p) {
+      uint32_t dbg[4];
+      if (hipMemcpy(dbg, (uint8_t*)c->ctr.p + 128, 16, hipMemcpyDeviceToHost) == hipSuccess && dbg[1])
+        fprintf(stderr, "GI_DEBUG bounds: line %u count %u a=%u b=%u\n", dbg[0], dbg[1], dbg[2], dbg[3]);
+    }
+#endif
+    if (c->diag_on && c->ctr.p) {  // pool words, slow bytes, slow entries, items per bucket
+      uint64_t h[16];
+      if (hipMemcpy(h, c->ctr.p, 128, hipMemcpyDeviceToHost) == hipSuccess) {
+        const uint32_t* ib = (const uint32_t*)(h + 8);
+        c->stats.diag[0] = h[0];
+        c->stats.diag[1] = h[1];
+        c->stats.diag[2] = h[2] & 0xFFFFFFFFull;
+        for (int b = 0; b < 5; b++) c->stats.diag[3 + b] = ib[2 * b + 1];
+      }
+    }
   }
   return GI_OK;
 }
@@ -452,3 +600,124 @@ int gi_selftest_regex(const char* pattern, size_t plen, const uint8_t* s, size_t
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ plan self-test
+// Host emulation of k_scan over every job image (compiler self-test only; the
+// inspection path never runs on the host): structural bounds of each image
+// and, on pseudo-random ASCII inputs, the image walk (joint class map, u16
+// transitions, end-of-input tables, slot table) against the global tables
+// the per-value path uses.  Returns 0 or the number of the first failed check.
+namespace {
+uint64_t host_scan_global(const Program& P, const DDfa& d, const uint8_t* s, size_t n) {
+  const uint16_t* tr = &P.trans[d.trans_off];
+  const uint8_t* amap = &P.u8pool[d.amap_off];
+  uint32_t st = d.start;
+  uint64_t m = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (!d.multi && st == d.accept) return 1;
+    const uint32_t cls = amap[s[i]];
+    const uint32_t tv = tr[(size_t)st * d.n_classes + cls];
+    if (d.multi) {
+      if (tv & 0x8000) m |= P.u64pool[d.acc_off + (size_t)st * 5 + P.u8pool[d.combo_off + cls]];
+      st = tv & 0x7FFF;
+    } else {
+      st = tv;
+    }
+  }
+  if (d.multi) return m | P.u64pool[d.acc_off + (size_t)st * 5 + 4];
+  return P.u8pool[d.endacc_off + st] ? 1 : 0;
+}
+}  // namespace
+
+extern "C" int gi_selftest_plan(const gi_ruleset* rs, char* err, size_t errcap) {
+  if (!rs) return GI_EINVAL;
+  const Program& P = rs->prog;
+  auto bad = [&](int code, const std::string& m) {
+    if (err && errcap) snprintf(err, errcap, "%s", m.c_str());
+    return code;
+  };
+  uint64_t rng = 0x9E3779B97F4A7C15ull;
+  auto rnd = [&]() {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return rng;
+  };
+  for (size_t j = 0; j < P.jobs.size(); j++) {
+    const DJob& J = P.jobs[j];
+    if (J.stream >= P.streams.size()) return bad(1, "job stream");
+    if ((uint64_t)J.img_off + J.img_bytes > P.images.size()) return bad(2, "image range");
+    if (J.jdfa_count == 0 || J.jdfa_count > GI_JOB_MAX_DFA) return bad(3, "automata per job");
+    const uint8_t* img = &P.images[J.img_off];
+    const uint32_t nf = P.streams[J.stream].filt_count;
+    if ((uint64_t)J.lds_fmask + 8ull * J.jdfa_count * nf > J.img_bytes) return bad(4, "fmask table");
+    if (J.lds && (J.big ? J.img_bytes > GI_BIG_LDS_BYTES + 4096 : J.img_bytes > GI_JOB_LDS_BYTES))
+      return bad(5, "lds image size");
+    for (uint32_t q = 0; q < J.jdfa_count; q++) {
+      const DJobDfa& jd = P.jdfas[J.jdfa_begin + q];
+      const DDfa& d = P.dfas[jd.dfa];
+      const uint64_t tb = 2ull * d.n_states * d.n_classes;
+      if (jd.lds_trans < 0 || (uint64_t)jd.lds_trans + tb > J.img_bytes) return bad(6, "transitions");
+      if (jd.lds_amap < 0 || (uint64_t)jd.lds_amap + 128 > J.img_bytes) return bad(7, "class map");
+      if (jd.lds_endacc < 0 || (uint64_t)jd.lds_endacc + (d.multi ? 8ull : 1ull) * d.n_states > J.img_bytes)
+        return bad(8, "end accept");
+      if (jd.lds_slots < 0 || (uint64_t)jd.lds_slots + 4ull * jd.n_pat > J.img_bytes) return bad(9, "slots");
+      if (d.multi && (jd.lds_combo < 0 || (uint64_t)jd.lds_combo + d.n_classes > J.img_bytes)) return bad(10, "combo");
+      if (d.start >= d.n_states) return bad(11, "start state");
+      const uint16_t* tr = (const uint16_t*)(img + jd.lds_trans);
+      for (uint64_t k = 0; k < (uint64_t)d.n_states * d.n_classes; k++) {
+        const uint32_t nx = d.multi ? (tr[k] & 0x7FFFu) : tr[k];
+        if (nx >= d.n_states) return bad(12, "transition target");
+      }
+      for (uint32_t c = 0; c < 128; c++) {
+        const uint32_t jc = (((const uint32_t*)img)[c] >> (8 * q)) & 0xFF;
+        if (jc >= d.n_classes || jc != img[jd.lds_amap + c]) return bad(13, "joint class map");
+      }
+      if (P.streams[J.stream].collapse &&
+          (d.byte_mode || !d.nonascii_uniform || ((((const uint32_t*)img)[128] >> (8 * q)) & 0xFF) != d.nonascii_cls))
+        return bad(20, "collapsed stream with a rune-distinguishing automaton");
+      for (uint32_t k = 0; k < jd.n_pat; k++)
+        if (*(const uint32_t*)(img + jd.lds_slots + 4 * k) != P.pats[jd.pat_begin + k].slot) return bad(14, "slot table");
+      // image walk == global-table walk on random ASCII strings
+      uint8_t s[96];
+      for (int trial = 0; trial < 64; trial++) {
+        const size_t n = rnd() % sizeof(s);
+        for (size_t i = 0; i < n; i++) s[i] = (uint8_t)(32 + rnd() % 95);
+        uint32_t st = d.start;
+        uint64_t m = 0;
+        for (size_t i = 0; i < n; i++) {
+          const uint32_t cls = (((const uint32_t*)img)[s[i] & 0x7F] >> (8 * q)) & 0xFF;
+          const uint32_t tv = tr[(size_t)st * d.n_classes + cls];
+          if (d.multi) {
+            if (tv & 0x8000) m |= P.u64pool[d.acc_off + (size_t)st * 5 + img[jd.lds_combo + cls]];
+            st = tv & 0x7FFF;
+          } else {
+            st = tv;
+          }
+        }
+        const uint64_t bits = d.multi ? (m | *(const uint64_t*)(img + jd.lds_endacc + 8 * st))
+                                      : (img[jd.lds_endacc + st] ? 1ull : 0ull);
+        if (bits != host_scan_global(P, d, s, n)) return bad(15, "image walk differs from the global tables");
+      }
+    }
+  }
+  for (size_t s = 0; s < P.streams.size(); s++) {
+    const DStream& S = P.streams[s];
+    if ((uint64_t)S.filt_begin + S.filt_count > P.sfilt.size()) return bad(16, "stream filters");
+    for (uint32_t k = 0; k < S.filt_count; k++)
+      if (P.sfilt[S.filt_begin + k] >= P.filters.size()) return bad(17, "global filter id");
+    if ((uint64_t)S.job_begin + S.job_count > P.jobs.size()) return bad(18, "stream jobs");
+    for (uint32_t j = S.job_begin; j < S.job_begin + S.job_count; j++)
+      if (P.jobs[j].stream != s) return bad(19, "job/stream mismatch");
+  }
+  return 0;
+}
+
+// Transformation identity triggers (compiler/kernel self-test): triggers[code]
+// for code < n_codes and the byte summary of every byte value.
+extern "C" int gi_selftest_triggers(uint32_t* triggers, uint32_t n_codes, uint32_t* byte_summaries) {
+  if (!triggers || !byte_summaries) return GI_EINVAL;
+  for (uint32_t c = 0; c < n_codes; c++) triggers[c] = transform_triggers((uint8_t)c);
+  for (uint32_t b = 0; b < 256; b++) byte_summaries[b] = byte_summary((uint8_t)b);
+  return GI_OK;
+}

@@ -62,7 +62,7 @@ EXPORTED_SYMBOLS = (
     "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name", "gi_ruleset_describe",
     "gi_ctx_create", "gi_ctx_free", "gi_last_error", "gi_inspect_batch", "gi_stage_batch",
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
-    "gi_ctx_stream", "gi_selftest_regex",
+    "gi_ctx_stream", "gi_selftest_regex", "gi_selftest_plan", "gi_selftest_triggers",
 )
 
 
@@ -101,14 +101,16 @@ class _Results(ctypes.Structure):
 class _Tally(ctypes.Structure):
     _fields_ = [("n_req", ctypes.c_uint64), ("n_interrupted", ctypes.c_uint64),
                 ("n_matched_any", ctypes.c_uint64), ("n_error", ctypes.c_uint64),
-                ("bytes_scanned", ctypes.c_uint64), ("matched_total", ctypes.c_uint64)]
+                ("bytes_scanned", ctypes.c_uint64), ("matched_total", ctypes.c_uint64),
+                ("n_pa_void", ctypes.c_uint64)]
 
 
 class _Stats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("last_kernel_ms", ctypes.c_double),
                 ("last_stage_ms", ctypes.c_double), ("last_scratch_bytes", ctypes.c_uint64),
                 ("last_collect_ms", ctypes.c_double), ("last_scan_ms", ctypes.c_double),
-                ("last_eval_ms", ctypes.c_double)]
+                ("last_eval_ms", ctypes.c_double), ("last_stream_ms", ctypes.c_double),
+                ("last_pa_bytes", ctypes.c_uint64), ("diag", ctypes.c_uint64 * 8)]
 
 
 _LIB = None
@@ -146,6 +148,8 @@ def load_library(path: str = LIB_PATH):
     lib.gi_ctx_stream.argtypes = [vp]
     lib.gi_ctx_stream.restype = vp
     lib.gi_selftest_regex.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(u32)]
+    lib.gi_selftest_plan.argtypes = [vp, ctypes.c_char_p, sz]
+    lib.gi_selftest_triggers.argtypes = [ctypes.POINTER(u32), u32, ctypes.POINTER(u32)]
     _LIB = lib
     return lib
 
@@ -182,6 +186,12 @@ class Ruleset:
         info = _Info()
         lib.gi_ruleset_info_get(h, ctypes.byref(info))
         self.info = {k: getattr(info, k) for k, _ in _Info._fields_}
+
+    def selftest_plan(self):
+        """Host emulation of the phase-A scan images (compiler self-test)."""
+        err = ctypes.create_string_buffer(256)
+        rc = self._lib.gi_selftest_plan(self._h, err, 256)
+        return rc, err.value.decode()
 
     def describe(self):
         """The phase-A scan plan as a dict (streams, jobs, automata sizes)."""
@@ -380,7 +390,9 @@ class Engine:
     def stats(self) -> dict:
         s = _Stats()
         self._check(self._lib.gi_stats_get(self._h, ctypes.byref(s)), "gi_stats_get")
-        return {k: getattr(s, k) for k, _ in _Stats._fields_}
+        out = {k: getattr(s, k) for k, _ in _Stats._fields_}
+        out["diag"] = list(out["diag"])
+        return out
 
     def stream(self) -> int:
         return int(self._lib.gi_ctx_stream(self._h) or 0)
@@ -392,6 +404,15 @@ class Engine:
 
     def __del__(self):
         self.close()
+
+
+def selftest_triggers(n_codes: int = 32):
+    """(triggers[code], byte_summary[256]) as the kernels use them."""
+    lib = load_library()
+    t = (ctypes.c_uint32 * n_codes)()
+    b = (ctypes.c_uint32 * 256)()
+    lib.gi_selftest_triggers(t, n_codes, b)
+    return list(t), list(b)
 
 
 def selftest_regex(pattern: str, data: bytes):

@@ -146,6 +146,7 @@ typedef struct {
   uint64_t n_error;
   uint64_t bytes_scanned; /* sum of raw request bytes (method+uri+proto+headers+body) */
   uint64_t matched_total;
+  uint64_t n_pa_void;     /* requests whose phase-A arena overflowed (evaluated exhaustively) */
 } gi_tally;
 
 typedef struct {
@@ -154,8 +155,12 @@ typedef struct {
   double last_stage_ms;    /* H2D staging time of the last batch */
   uint64_t last_scratch_bytes;
   double last_collect_ms;  /* k_collect (ProcessURI / headers / cookies) */
-  double last_scan_ms;     /* k_scan (phase A: transforms + union automata) */
+  double last_scan_ms;     /* k_scan (phase A: automata over the transformed values) */
   double last_eval_ms;     /* k_eval (phase B: rule interpreter, body, verdicts) */
+  double last_stream_ms;   /* k_stream (phase A: filters + transformation chains) */
+  uint64_t last_pa_bytes;  /* phase-A arena bytes reserved for the batch */
+  uint64_t diag[8];        /* diagnostic counters of the last batch (GI_DIAG=1): phase-A
+                              arena bytes needed, values, max per-request need, capacity */
 } gi_stats;
 
 /* ------------------------------------------------------------ compile */
@@ -197,6 +202,12 @@ void* gi_ctx_stream(gi_ctx* ctx);
  * Compiler self-tests only: run a host-built automaton on the host.  These
  * never take part in gi_inspect_* (which only runs on the GPU). */
 int gi_selftest_regex(const char* pattern, size_t plen, const uint8_t* s, size_t n, uint32_t* n_states);
+/* Host emulation of the phase-A scan over every job image of a compiled
+ * ruleset (bounds + image walk vs the global tables).  0 = consistent. */
+int gi_selftest_plan(const gi_ruleset* rs, char* err, size_t errcap);
+/* The transformation identity-trigger table the kernels use (triggers[code],
+ * code < n_codes) and the byte summary of every byte value (256 entries). */
+int gi_selftest_triggers(uint32_t* triggers, uint32_t n_codes, uint32_t* byte_summaries);
 
 #ifdef __cplusplus
 }

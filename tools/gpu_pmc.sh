@@ -11,7 +11,7 @@ script="$1"; shift
 case "$script" in /*) ;; *) script="$R/$script" ;; esac
 for pmc in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES" \
            "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH GRBM_GUI_ACTIVE" \
-           "FETCH_SIZE TCC_HIT_sum TCC_MISS_sum" \
+           "FETCH_SIZE" \
            "WRITE_SIZE"; do
   i=$((i+1))
   mkdir -p "$R/gpurun_out/pmc/p$i"
