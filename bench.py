@@ -152,24 +152,22 @@ def main():
     value = total_req * args.steps / elapsed
     gbs = total_bytes * args.steps / elapsed / 1e9
 
-    # roofline of the dominant kernel (HIP events on the context stream).
-    # Algorithmic bytes per launch (DESIGN.md "Roofline"):
-    #   k_match: request line + header bytes (every value phase A scans is a
-    #            substring of those) + one 4-B hit word per (hit word, request);
-    #   k_eval : raw request bytes + 80-B verdict + 4 B per matched rule id.
+    # Roofline of the dominant single kernel (HIP events on the context
+    # stream).  Algorithmic bytes per launch:
+    #   k_eval : raw request bytes + 80-B verdict + 4 B per matched rule id
+    # (the stages k_stream / k_scan are several launches each and are reported
+    # as stage times beside it).
     avg_kern_ms = float(np.mean(kern_ms))
     avg_stage = {k: float(np.mean(v)) for k, v in stage_ms.items()}
-    body_bytes = int(batch.reqs["body"]["len"].sum())
-    hit_words = (rs.info["n_hit_slots"] + 31) // 32
-    alg = {
-        "k_scan": raw - body_bytes + 4 * hit_words * batch.n_req,
-        "k_stream": raw - body_bytes,
-        "k_eval": raw + 80 * batch.n_req + 4 * int(tally["matched_total"]),
-        "k_collect": raw - body_bytes,
-    }
-    dom = max(("k_stream", "k_scan", "k_eval"), key=lambda k: avg_stage[k])
-    alg_bytes = alg[dom]
+    dom = "k_eval"
+    alg_bytes = raw + 80 * batch.n_req + 4 * int(tally["matched_total"])
     achieved = alg_bytes / (avg_stage[dom] * 1e-3) / 1e9
+    hbm_traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+    if os.path.exists(tpath):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)
+        tj = json.load(open(tpath))
+        if tj.get("kernel") == dom and tj.get("requests") == batch.n_req:
+            hbm_traffic = tj["hbm_bytes_per_launch"]
     out = {
         "metric": "requests inspected/sec (node), CRS v4 PL1",
         "value": round(value, 1),
@@ -191,7 +189,7 @@ def main():
         "pa_void_requests": int(tally["n_pa_void"]),
         "error_requests": int(tally["n_error"]),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": hbm_traffic,
                      "kernel": dom, "kernel_ms": round(avg_stage[dom], 4),
                      "alg_bytes_per_launch": int(alg_bytes),
                      "stages_ms": {k: round(v, 4) for k, v in avg_stage.items()},
