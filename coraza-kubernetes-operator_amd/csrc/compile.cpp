@@ -845,6 +845,39 @@ struct Lower {
     d->var_count = (uint32_t)P->vars.size() - d->var_begin;
   }
 
+  // setvar fast forms (DAction.a = SV_*, .b operand); anything else stays
+  // SV_GENERIC and runs the macro-expanding path (run_setvar).
+  void classify_setvar(DAction* a) {
+    const DTmpl& tm = P->tmpls[a->tmpl];
+    auto lit_of = [&](const DTmplPart& p) {
+      return std::string((const char*)&P->strpool[p.off], p.len);
+    };
+    a->a = SV_GENERIC;
+    if (tm.part_count == 1 && P->tparts[tm.part_begin].kind == TP_LIT) {
+      const std::string l = lit_of(P->tparts[tm.part_begin]);
+      int64_t v;
+      if (l.empty()) return;
+      if (l[0] == '+' || l[0] == '-') {
+        if (go_atoi(l.substr(1), &v)) {
+          a->a = l[0] == '+' ? SV_ADD_CONST : SV_SUB_CONST;
+          a->b = v;
+        }
+      } else if (go_atoi(l, &v) && std::to_string(v) == l) {
+        a->a = SV_SET_INT;
+        a->b = v;
+      }
+      return;
+    }
+    if (tm.part_count == 2 && P->tparts[tm.part_begin].kind == TP_LIT && P->tparts[tm.part_begin + 1].kind == TP_TX &&
+        P->tparts[tm.part_begin + 1].slot >= 0) {
+      const std::string l = lit_of(P->tparts[tm.part_begin]);
+      if (l == "+" || l == "-") {
+        a->a = l == "+" ? SV_ADD_SLOT : SV_SUB_SLOT;
+        a->b = P->tparts[tm.part_begin + 1].slot;
+      }
+    }
+  }
+
   void actions(const IrRule& r, DRule* d) {
     d->act_begin = (uint32_t)P->acts.size();
     for (auto& nd : r.nd) {
@@ -854,6 +887,7 @@ struct Lower {
         a.kind = nd.sv_remove ? A_SETVAR_DEL : A_SETVAR;
         a.slot = slot(nd.sv_key);
         a.tmpl = nd.sv_remove ? -1 : tmpl(nd.sv_value);
+        if (a.kind == A_SETVAR) classify_setvar(&a);
         P->acts.push_back(a);
       } else if (nd.ctl_name == "ruleremovebyid") {
         std::stringstream ss(nd.ctl_value);
@@ -944,21 +978,26 @@ struct Lower {
     bool scannable = n == "rx" || n == "pm" || n == "validatebyterange" || n == "validateurlencoding" ||
                      n == "validateutf8encoding" || (n == "contains" && r.op_arg.find("%{") == std::string::npos);
     if (!scannable) return -1;
-    bool bodydep = false;
+    bool bodydep = false, residual = false;
     for (auto& v : r.vars) {
       if (v.count) return -1;
       int sid = single_id(v.name);
-      if (sid >= 0 && !immutable_single(sid)) return -1;
+      if (sid >= 0 && !immutable_single(sid)) residual = true;  // tested by k_eval on a clear bit
       if (sid < 0 && v.name == "TX") return -1;
       if (v.name == "ARGS" || v.name == "ARGS_POST" || v.name == "ARGS_NAMES" || v.name == "ARGS_POST_NAMES")
         bodydep = true;
     }
     const int32_t slot = (int32_t)P->n_hit_slots++;
     if (bodydep) *flags |= RF_BODYDEP;
+    if (residual) *flags |= RF_RESIDUAL;
     const DOp& o = P->ops[d.op];
-    const DVarRef* vrs = &P->vars[d.var_begin];
+    DVarRef* vrs = &P->vars[d.var_begin];
     for (uint32_t vi = 0; vi < d.var_count; vi++) {
-      const DVarRef& vr = vrs[vi];
+      DVarRef& vr = vrs[vi];
+      if (vr.var < S_COUNT && !immutable_single(vr.var)) {
+        vr.residual = 1;
+        continue;
+      }
       DFilter f{};
       f.key_dfa = -1;
       f.single = GI_NO_SINGLE;

@@ -8,6 +8,8 @@
 
 namespace gi {
 
+struct Slot;  // TX variable (kernels.hip)
+
 // Per-request scratch layout (computed by the host from request lengths when
 // the batch is staged; see runtime.cpp gi_stage_batch).  Region =
 // [256 B ReqHdr][cap_f fields][TX slots][cap_b bytes][2 x cap_t][2 x cap_mt].
@@ -34,6 +36,7 @@ struct DBatch {
   uint32_t* matched;
   unsigned long long* tally;  // gi_tally counters
   uint32_t* hits;             // phase-A hit words [ceil(n_hit_slots/32)][n_req]
+  Slot* txslots;       // TX variables [n_slots][n_req] (k_eval)
   // phase A (see kernels.hip "phase A")
   uint32_t* bcounts;          // [k_collect blocks][GI_NB] item counts
   uint32_t* boffs;            // [k_collect blocks][GI_NB] item offsets
@@ -55,6 +58,7 @@ struct DBatch {
   unsigned long long* slow_used;
   unsigned long long* diag;   // optional diagnostic counters (gi_stats.diag)
   uint32_t* dbg;              // debug-build bounds-violation record (-DGI_DEBUG)
+  unsigned long long* prof;   // GI_PROF=1: k_eval cycle / rule counters (stderr at gi_sync)
   uint64_t items_cap;
   uint32_t n_hit_slots;
 };

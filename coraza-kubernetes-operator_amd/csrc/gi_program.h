@@ -15,6 +15,28 @@
 
 namespace gi {
 
+// Program records are immutable for the life of a context: reading them
+// through the constant address space lets the compiler use scalar loads for
+// wave-uniform indices (rule walk, operators, actions).
+#if defined(__HIPCC__)
+#define GI_CONST(T, p) ((const __attribute__((address_space(4))) T*)(p))
+// copy record i of array p (sizeof(T) % 4 == 0) through the constant space
+template <class T>
+__device__ __forceinline__ T gi_cload(const T* p, uint64_t i) {
+  static_assert(sizeof(T) % 4 == 0, "record size");
+  const __attribute__((address_space(4))) uint32_t* q =
+      (const __attribute__((address_space(4))) uint32_t*)(p + i);
+  uint32_t w[sizeof(T) / 4];
+#pragma unroll
+  for (uint32_t k = 0; k < sizeof(T) / 4; k++) w[k] = q[k];
+  T v;
+  __builtin_memcpy(&v, w, sizeof(T));
+  return v;
+}
+#else
+#define GI_CONST(T, p) ((const T*)(p))
+#endif
+
 // ------------------------------------------------------------- variables
 // Scalar variables ("collection.Single" in coraza) -- per-request table index.
 enum SingleId : uint8_t {
@@ -107,6 +129,7 @@ enum RuleFlags : uint8_t {
   RF_MARKER = 2,
   RF_CAPTURE = 4,
   RF_BODYDEP = 8,  // targets can see ARGS_POST: phase-A bits ignored once a body was parsed
+  RF_RESIDUAL = 16,  // some targets are residual (DVarRef.residual): a clear bit still tests them
 };
 
 enum ActKind : uint8_t {
@@ -117,6 +140,16 @@ enum ActKind : uint8_t {
   A_CTL_BODY_PROCESSOR,
   A_CTL_BODY_ACCESS,
   A_CTL_FORCE_BODY,
+};
+
+// setvar fast forms (DAction.a for A_SETVAR)
+enum SetvarForm : int64_t {
+  SV_GENERIC = 0,
+  SV_SET_INT = 1,    // =<canonical integer literal b>
+  SV_ADD_CONST = 2,  // =+<integer literal b>
+  SV_SUB_CONST = 3,  // =-<integer literal b>
+  SV_ADD_SLOT = 4,   // =+%{tx.<slot b>}
+  SV_SUB_SLOT = 5,   // =-%{tx.<slot b>}
 };
 
 enum EngineMode : uint8_t { ENGINE_OFF = 0, ENGINE_ON = 1, ENGINE_DETECTION_ONLY = 2 };
@@ -307,7 +340,9 @@ struct DVarRef {
   uint32_t key_off, key_len;  // literal key in string pool (lowercased when ci)
   uint32_t exc_begin, exc_count;
   int32_t slot;      // TX literal key -> slot
-  uint32_t _pad;
+  uint8_t residual;  // a body-phase single (REQUEST_BODY, ...) of a phase-A link: phase A does
+                     // not see it, so a clear hit bit leaves it for k_eval to test
+  uint8_t _pad[3];
 };
 
 struct DExc {
@@ -403,6 +438,7 @@ struct DProgram {
   uint32_t n_streams;
   uint32_t n_lower_pairs;
   uint32_t n_top;
+  uint32_t top_begin[2], top_end[2];  // per-phase walks in top[] (phase 1, phase 2)
   uint32_t n_slots;
   uint32_t n_markers;
   int32_t exports[8];           // TX slot per export, -1 = none

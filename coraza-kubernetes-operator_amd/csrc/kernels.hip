@@ -685,7 +685,8 @@ struct Tx {
   const DProgram* P;
   Field* fields;
   uint32_t nf, cap_f;
-  Slot* slots;
+  Slot* slots;               // TX slot 0 of this request; slot s at slots[s * n_req] (request-major SoA:
+                             // the lanes of a wave walk the same rule, so they touch the same slot)
   uint8_t* bytes;
   uint32_t nb, cap_b;
   uint8_t* t0;
@@ -713,7 +714,13 @@ struct Tx {
   uint32_t nmatched;
   uint32_t* mout;
   uint32_t mcap;
+  bool profon;               // GI_PROF counters (diagnostics)
+  uint32_t prof_visits, prof_evals, prof_rules;
+  uint64_t prof_eval_cyc, prof_act_cyc;
+  unsigned long long* prof_rule_cyc;  // [rule link] cycles (GI_PROF)
 };
+
+#define TXS(t, s) ((t).slots[(uint64_t)(s) * (t).n_req])
 
 __device__ inline uint8_t* tx_alloc(Tx& t, uint32_t n) {
   if (t.nb + n > t.cap_b) {
@@ -755,7 +762,7 @@ __device__ uint32_t query_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
 }
 
 // coraza internal/url ParseQuery(query, '&') -> fields of `kind`
-__device__ void parse_query(Tx& t, const uint8_t* q, uint32_t n, uint8_t kind) {
+__device__ __forceinline__ void parse_query(Tx& t, const uint8_t* q, uint32_t n, uint8_t kind) {
   uint32_t i = 0;
   while (i < n) {
     uint32_t j = i;
@@ -950,7 +957,7 @@ __device__ inline bool starts_ci(const uint8_t* s, uint32_t n, const char* lit) 
 }
 
 // ------------------------------------------------------------ TX / macros
-__device__ Str slot_str(Tx& t, const Slot& s, uint8_t* buf) {
+__device__ __forceinline__ Str slot_str(Tx& t, const Slot& s, uint8_t* buf) {
   if (s.state == 1) return {buf, go_itoa(s.num, buf)};
   if (s.state == 2) return {s.p, s.n};
   return {buf, 0};
@@ -967,7 +974,7 @@ __device__ int64_t slot_int(const Slot& s, bool* ok) {
 
 // Expand a %{..} template.  *persistent: result points into the program's
 // string pool (safe to keep in TX); otherwise into the macro scratch.
-__device__ Str expand(Tx& t, int32_t tid, bool* persistent) {
+__device__ __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
   const DProgram& P = *t.P;
   *persistent = false;
   if (tid < 0) return {t.mt, 0};
@@ -985,7 +992,7 @@ __device__ Str expand(Tx& t, int32_t tid, bool* persistent) {
     if (p.kind == TP_LIT) {
       s = {P.strpool + p.off, p.len};
     } else if (p.kind == TP_TX) {
-      s = slot_str(t, t.slots[p.slot], nb);
+      s = slot_str(t, TXS(t, p.slot), nb);
     } else if (p.kind == TP_SINGLE) {
       s = t.single[p.single];
     } else if (p.kind == TP_HEADER) {
@@ -1006,12 +1013,37 @@ __device__ Str expand(Tx& t, int32_t tid, bool* persistent) {
 }
 
 // setvar [upstream internal/actions/setvar.go]
-__device__ void run_setvar(Tx& t, const DAction& a) {
-  Slot& sl = t.slots[a.slot];
+__device__ __forceinline__ void run_setvar(Tx& t, const DAction& a) {
+  Slot& sl = TXS(t, a.slot);
   if (a.kind == A_SETVAR_DEL) {
     sl.state = 0;
     return;
   }
+  // fast forms: same results as the expanding path below, without strings
+  if (a.a == SV_SET_INT) {
+    sl.state = 1;
+    sl.num = a.b;
+    return;
+  }
+  if (a.a != SV_GENERIC) {
+    int64_t vv = a.b;
+    if (a.a == SV_ADD_SLOT || a.a == SV_SUB_SLOT) {
+      const Slot& src = TXS(t, a.b);
+      if (src.state == 0) return;  // "+" alone: Atoi("") fails, no change
+      if (src.state != 1) goto generic;
+      vv = src.num;
+    }
+    {
+      bool ok;
+      int64_t me = slot_int(sl, &ok);
+      if (!ok) me = 0;
+      const bool add = a.a == SV_ADD_CONST || a.a == SV_ADD_SLOT;
+      sl.state = 1;
+      sl.num = (int64_t)(add ? (uint64_t)me + (uint64_t)vv : (uint64_t)me - (uint64_t)vv);
+      return;
+    }
+  }
+generic:
   bool pers;
   Str v = expand(t, a.tmpl, &pers);
   if (v.n == 0) {
@@ -1061,10 +1093,18 @@ __device__ void run_setvar(Tx& t, const DAction& a) {
   sl.n = v.n;
 }
 
-__device__ void run_actions(Tx& t, const DRule& R) {
+__device__ __forceinline__ void run_actions(Tx& t, const DRule& R) {
   const DProgram& P = *t.P;
+  const uint64_t c0 = t.profon ? clock64() : 0;
+  struct ProfEnd {
+    Tx& t;
+    uint64_t c0;
+    __device__ ~ProfEnd() {
+      if (t.profon) t.prof_act_cyc += clock64() - c0;
+    }
+  } prof_end{t, c0};
   for (uint32_t k = 0; k < R.act_count; k++) {
-    const DAction a = P.acts[R.act_begin + k];
+    const DAction a = gi_cload(P.acts, R.act_begin + k);
     switch (a.kind) {
       case A_SETVAR:
       case A_SETVAR_DEL:
@@ -1115,7 +1155,7 @@ __device__ bool contains_word(const uint8_t* v, uint32_t vn, const uint8_t* w, u
   return false;
 }
 
-__device__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, uint32_t n) {
+__device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, uint32_t n) {
   const DProgram& P = *t.P;
   bool res = false;
   switch (o.kind) {
@@ -1194,7 +1234,7 @@ __device__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, uint32_t n) {
 
 // ------------------------------------------------------------ evaluation
 // Apply the rule's transformation chain; returns the value to test.
-__device__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uint32_t vn, bool* ok) {
+__device__ __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uint32_t vn, bool* ok) {
   const DProgram& P = *t.P;
   Str cur{v, vn};
   *ok = true;
@@ -1215,7 +1255,7 @@ __device__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uint32_t vn, b
   return cur;
 }
 
-__device__ inline bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
+__device__ __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
   const DProgram& P = *t.P;
   for (uint32_t e = 0; e < vr.exc_count; e++) {
     const DExc x = P.excs[vr.exc_begin + e];
@@ -1246,7 +1286,7 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
 }
 
 // Test one value: transform, operator, per-match actions.  Returns 1 on match.
-__device__ inline uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn) {
+__device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn) {
   bool ok;
   Str tv = transform(t, R, v, vn, &ok);
   if (!ok) return 0;
@@ -1258,22 +1298,38 @@ __device__ inline uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const
 }
 
 // Rule.doEvaluate for one link -> number of matched values.
-__device__ uint32_t eval_rule(Tx& t, const DRule& R) {
+__device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   const DProgram& P = *t.P;
   // phase-A filter: a clear hit bit proves no value matches (exact); a set
   // bit (match or "maybe") falls through to the full evaluation below.
   if (R.hit_slot >= 0 && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post)) {
     const uint32_t w = t.hits[(uint64_t)(R.hit_slot >> 5) * t.n_req + t.req];
-    if (!((w >> (R.hit_slot & 31)) & 1u)) return 0;
+    if (!((w >> (R.hit_slot & 31)) & 1u)) {
+      if (!(R.flags & RF_RESIDUAL)) return 0;
+      // phase A cleared every other target: only the residual (body-phase)
+      // singles can match; test them without side effects, and evaluate the
+      // whole link in order only if one does
+      const DOp o = gi_cload(P.ops, (uint64_t)R.op);
+      bool any = false;
+      for (uint32_t vi = 0; vi < R.var_count && !any; vi++) {
+        const DVarRef vr = gi_cload(P.vars, R.var_begin + vi);
+        if (!vr.residual) continue;
+        bool ok;
+        const Str sv = t.single[vr.var];
+        const Str tv = transform(t, R, sv.p, sv.n, &ok);
+        any = ok && eval_op(t, o, tv.p, tv.n);
+      }
+      if (!any) return 0;
+    }
   }
   if (R.op < 0) {
     run_actions(t, R);
     return 1;
   }
-  const DOp& o = P.ops[R.op];
+  const DOp o = gi_cload(P.ops, (uint64_t)R.op);
   uint32_t nmatch = 0;
   for (uint32_t vi = 0; vi < R.var_count; vi++) {
-    const DVarRef& vr = P.vars[R.var_begin + vi];
+    const DVarRef vr = gi_cload(P.vars, R.var_begin + vi);
     if (vr.var < S_COUNT) {
       if (vr.count) {
         uint8_t one = '1';
@@ -1293,7 +1349,7 @@ __device__ uint32_t eval_rule(Tx& t, const DRule& R) {
         se = vr.slot < 0 ? 0u : (uint32_t)vr.slot + 1;
       }
       for (uint32_t sid = sb; sid < se; sid++) {
-        if (t.slots[sid].state == 0) continue;
+        if (TXS(t, sid).state == 0) continue;
         const uint8_t* nm = P.strpool + P.slot_names[sid * 2];
         uint32_t nn = P.slot_names[sid * 2 + 1];
         if (vr.key_mode == 2 && !dfa_match(P, vr.key_dfa, nm, nn, false)) continue;
@@ -1302,7 +1358,7 @@ __device__ uint32_t eval_rule(Tx& t, const DRule& R) {
           cnt++;
           continue;
         }
-        const Slot sl = t.slots[sid];
+        const Slot sl = TXS(t, sid);
         if (sl.state == 1 && R.tchain_len == 0 && o.has_num && o.kind >= OP_EQ && o.kind <= OP_LT) {
           // integer TX value against a numeric literal: eval_op would Atoi the
           // canonical decimal back to sl.num, so compare directly
@@ -1358,14 +1414,24 @@ __device__ uint32_t eval_rule(Tx& t, const DRule& R) {
   return nmatch;
 }
 
-__device__ void eval_top(Tx& t, uint32_t ri) {
+__device__ __forceinline__ void eval_top(Tx& t, uint32_t ri) {
   const DProgram& P = *t.P;
-  const DRule R = P.rules[ri];
-  if (eval_rule(t, R) == 0) return;
-  for (int32_t ci = R.chain_next; ci >= 0; ci = P.rules[ci].chain_next) {
-    const DRule C = P.rules[ci];
-    if (eval_rule(t, C) == 0) return;
+  const DRule R = gi_cload(P.rules, ri);
+  // the rule and its chain links; all must match (one eval_rule call site)
+  t.prof_evals++;
+  for (int32_t ci = (int32_t)ri; ci >= 0;) {
+    const DRule C = gi_cload(P.rules, (uint64_t)ci);
+    const uint64_t c0 = t.profon ? clock64() : 0;
+    const uint32_t nm = eval_rule(t, C);
+    if (t.profon) {
+      const uint64_t dc = clock64() - c0;
+      t.prof_eval_cyc += dc;
+      if (ci < 1000) atomicAdd(&t.prof_rule_cyc[ci], (unsigned long long)dc);
+    }
+    if (nm == 0) return;
+    ci = C.chain_next;
   }
+  t.prof_rules++;
   if (R.skip_after >= 0) t.skip_after = R.skip_after;
   if (R.skip) t.skip = R.skip;
   if ((R.disruptive == D_DENY || R.disruptive == D_DROP || R.disruptive == D_REDIRECT) && t.engine == ENGINE_ON) {
@@ -1384,17 +1450,16 @@ __device__ void eval_top(Tx& t, uint32_t ri) {
 }
 
 // RuleGroup.Eval [upstream corazawaf/rulegroup.go]
-__device__ void eval_phase(Tx& t, uint8_t phase) {
+__device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
   const DProgram& P = *t.P;
   if (t.engine == ENGINE_OFF) return;
   t.phase = phase;
-  for (uint32_t k = 0; k < P.n_top; k++) {
+  for (uint32_t k = P.top_begin[phase - 1]; k < P.top_end[phase - 1]; k++) {
     if (t.interrupted) break;
     if (t.flags & GI_REQ_ERROR_MASK) break;
-    const uint32_t ri = P.top[k];
-    const DRule& R = P.rules[ri];
-    const uint8_t rph = R.phase;
-    if (rph != 0 && rph != phase) continue;
+    const uint32_t ri = GI_CONST(uint32_t, P.top)[k];
+    const DRule R = gi_cload(P.rules, ri);
+    t.prof_visits++;
     const int32_t id = R.id;
     if (id != 0 && t.nremoved) {
       bool rm = false;
@@ -1411,7 +1476,7 @@ __device__ void eval_phase(Tx& t, uint8_t phase) {
       continue;
     }
     if (R.flags & RF_MARKER) continue;
-    if (R.hit_slot >= 0 && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
+    if (R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.n_req + t.req] >> (R.hit_slot & 31)) & 1u))
       continue;  // phase A proved the first link matches nothing
     eval_top(t, ri);
@@ -2297,14 +2362,20 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
   __syncthreads();
   unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
   if (r < B.n_req) {
+    const uint64_t c_start = B.prof ? clock64() : 0;
     const gi_request rq = B.reqs[r];
     Region g = region_of(P, B, r);
     ReqHdr* H = g.hdr;
     Tx t;
+    t.prof_visits = t.prof_evals = t.prof_rules = 0;
+    t.prof_eval_cyc = t.prof_act_cyc = 0;
+    t.profon = B.prof != nullptr;
+    t.prof_rule_cyc = B.prof ? B.prof + 16 : nullptr;
     tx_bind(t, P, g);
     t.hits = B.hits;
     t.n_req = B.n_req;
     t.req = r;
+    t.slots = B.txslots + r;
     t.has_post = false;
     t.pa_void = H->pa_void != 0;
     t.nf = H->nf;
@@ -2327,16 +2398,18 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
     t.nmatched = 0;
     t.mout = B.matched + (uint64_t)r * B.mcap;
     t.mcap = B.mcap;
-    for (uint32_t s = 0; s < P.n_slots; s++) t.slots[s].state = 0;
+    for (uint32_t s = 0; s < P.n_slots; s++) TXS(t, s).state = 0;
     const uint8_t* D = B.data;
     uint64_t scanned = (uint64_t)rq.method.len + rq.uri.len + rq.proto.len + rq.body.len;
     for (uint32_t h = 0; h < rq.hdr_count; h++) {
       const gi_header hd = B.headers[rq.hdr_begin + h];
       scanned += hd.name.len + hd.value.len;
     }
-    if (!(t.flags & GI_REQ_ERROR_MASK)) {
-      eval_phase(t, 1);
-      if (!t.interrupted && t.engine != ENGINE_OFF && !(t.flags & GI_REQ_ERROR_MASK)) {
+    const uint64_t c_init = B.prof ? clock64() : 0;
+    // phase 1, ProcessRequestBody, phase 2 (one eval_phase call site)
+    for (uint8_t ph = 1; ph <= 2 && !(t.flags & GI_REQ_ERROR_MASK); ph++) {
+      if (ph == 2) {
+        if (t.interrupted || t.engine == ENGINE_OFF) break;
         const uint32_t bn = rq.body.len;
         if (t.body_access && bn > 0) {
           if (bn > P.body_limit) {
@@ -2358,8 +2431,20 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
             }
           }
         }
-        if (!(t.flags & GI_REQ_ERROR_MASK)) eval_phase(t, 2);
+        if (t.flags & GI_REQ_ERROR_MASK) break;
       }
+      const uint64_t c0 = B.prof ? clock64() : 0;
+      eval_phase(t, ph);
+      if (B.prof) atomicAdd(&B.prof[ph], (unsigned long long)(clock64() - c0));
+    }
+    if (B.prof) {
+      atomicAdd(&B.prof[0], (unsigned long long)(c_init - c_start));
+      atomicAdd(&B.prof[3], (unsigned long long)(clock64() - c_start));
+      atomicAdd(&B.prof[4], (unsigned long long)t.prof_visits);
+      atomicAdd(&B.prof[5], (unsigned long long)t.prof_evals);
+      atomicAdd(&B.prof[6], (unsigned long long)t.prof_rules);
+      atomicAdd(&B.prof[7], (unsigned long long)t.prof_eval_cyc);
+      atomicAdd(&B.prof[8], (unsigned long long)t.prof_act_cyc);
     }
     gi_verdict v;
     v.rule_id = t.interrupted ? t.int_rule : 0;
@@ -2372,7 +2457,7 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
       int64_t x = 0;
       if (e < P.n_exports && P.exports[e] >= 0) {
         bool okk;
-        x = slot_int(t.slots[P.exports[e]], &okk);
+        x = slot_int(TXS(t, P.exports[e]), &okk);
         if (!okk) x = 0;
       }
       v.tx_export[e] = x;

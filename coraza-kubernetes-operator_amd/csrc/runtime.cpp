@@ -78,12 +78,13 @@ struct gi_ctx {
   DProgram prog{};
   std::vector<DevBuf> pbufs;
   // batch buffers
-  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, hits, joblist;
+  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, hits, joblist, txslots;
   // phase A
   DevBuf bcounts, boffs, items, lscratch, pool, qblk, ctr, slow, slow_bytes;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0;
   uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0;
-  bool diag_on = false;
+  bool diag_on = false, prof_on = false;
+  DevBuf prof;
   int stop_after = 0;  // debugging: launch only the first N pipeline kernels, synchronising after each
   ScanLaunch scan{};
   uint32_t hit_words = 0;
@@ -187,6 +188,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->device = device;
   c->mcap = matched_cap ? matched_cap : 64;
   c->diag_on = getenv("GI_DIAG") && atoi(getenv("GI_DIAG")) > 0;
+  c->prof_on = getenv("GI_PROF") && atoi(getenv("GI_PROF")) > 0;
   c->stop_after = getenv("GI_STOP_AFTER") ? atoi(getenv("GI_STOP_AFTER")) : 0;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -217,7 +219,16 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
     k++;                                                    \
   }
   UP(rules, P.rules, DRule)
-  UP(top, P.top, uint32_t)
+  // per-phase rule walks: rules of that phase plus phase-0 records (SecMarker),
+  // in file order -- what RuleGroup.Eval(phase) visits
+  std::vector<uint32_t> top_ph;
+  uint32_t n_ph1 = 0;
+  for (int ph = 1; ph <= 2; ph++) {
+    for (uint32_t ri : P.top)
+      if (P.rules[ri].phase == 0 || P.rules[ri].phase == ph) top_ph.push_back(ri);
+    if (ph == 1) n_ph1 = (uint32_t)top_ph.size();
+  }
+  UP(top, top_ph, uint32_t)
   UP(vars, P.vars, DVarRef)
   UP(excs, P.excs, DExc)
   UP(ops, P.ops, DOp)
@@ -253,6 +264,10 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   }
   c->prog.n_lower_pairs = GI_N_LOWER_PAIRS;
   c->prog.n_top = (uint32_t)P.top.size();
+  c->prog.top_begin[0] = 0;
+  c->prog.top_end[0] = n_ph1;
+  c->prog.top_begin[1] = n_ph1;
+  c->prog.top_end[1] = (uint32_t)top_ph.size();
   c->prog.n_slots = P.n_slots;
   c->prog.n_markers = P.n_markers;
   c->prog.n_exports = (uint32_t)P.exports.size();
@@ -311,8 +326,9 @@ void gi_ctx_free(gi_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& b : c->pbufs) b.release();
+  c->prof.release();
   for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally,
-                    &c->hits, &c->joblist, &c->bcounts, &c->boffs, &c->items, &c->lscratch, &c->pool, &c->qblk,
+                    &c->hits, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes})
     b->release();
   for (auto& ev : c->evs)
@@ -405,6 +421,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if ((e = c->matched.ensure(std::max<size_t>((size_t)n * c->mcap * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc matched");
   if ((e = c->tally.ensure(sizeof(gi_tally))) != hipSuccess) return hip_fail(c, e, "alloc tally");
+  if ((e = c->txslots.ensure(std::max<uint64_t>(24ull * PG.n_slots * n, 64))) != hipSuccess)
+    return hip_fail(c, e, "alloc tx slots");
   c->hit_words = (PG.n_hit_slots + 31) / 32;
   if ((e = c->hits.ensure(std::max<size_t>((size_t)c->hit_words * n * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc hits");
@@ -471,6 +489,7 @@ int gi_run_staged(gi_ctx* c) {
   B.matched = (uint32_t*)c->matched.p;
   B.tally = (unsigned long long*)c->tally.p;
   B.hits = (uint32_t*)c->hits.p;
+  B.txslots = (Slot*)c->txslots.p;
   {
     // counters (bytes): [0] pool words used, [8] slow bytes used, [16] slow
     // entries, [64] item buckets {(base, count) x5, item-wave base x5, item
@@ -495,6 +514,11 @@ int gi_run_staged(gi_ctx* c) {
     B.slow_bytes_cap = c->slow_bytes_cap;
     B.slow_used = (unsigned long long*)(cp + 8);
     B.diag = nullptr;
+    B.prof = nullptr;
+    if (c->prof_on && c->prof.ensure(128 + 8000) == hipSuccess) {
+      B.prof = (unsigned long long*)c->prof.p;
+      (void)hipMemsetAsync(c->prof.p, 0, 128 + 8000, c->stream);
+    }
     B.items_cap = c->items_cap;
     B.n_hit_slots = c->rs->prog.n_hit_slots;
     B.dbg = (uint32_t*)(cp + 128);  // 4 words (only written by -DGI_DEBUG builds)
@@ -536,6 +560,28 @@ int gi_sync(gi_ctx* c) {
         fprintf(stderr, "GI_DEBUG bounds: line %u count %u a=%u b=%u\n", dbg[0], dbg[1], dbg[2], dbg[3]);
     }
 #endif
+    if (c->prof_on && c->prof.p) {
+      unsigned long long h[16];
+      if (hipMemcpy(h, c->prof.p, 128, hipMemcpyDeviceToHost) == hipSuccess && c->n_req) {
+        const double n = c->n_req;
+        fprintf(stderr,
+                "GI_PROF k_eval per request: init %.0f cyc, phase1 %.0f, phase2 %.0f, total %.0f; rule visits %.1f, "
+                "evaluated %.1f, matched %.1f; eval_rule %.0f cyc, actions %.0f cyc\n",
+                h[0] / n, h[1] / n, h[2] / n, h[3] / n, h[4] / n, h[5] / n, h[6] / n, h[7] / n, h[8] / n);
+        std::vector<unsigned long long> rc(1000);
+        if (hipMemcpy(rc.data(), (uint8_t*)c->prof.p + 128, 8000, hipMemcpyDeviceToHost) == hipSuccess) {
+          std::vector<std::pair<unsigned long long, uint32_t>> v;
+          for (uint32_t i = 0; i < 1000 && i < c->rs->prog.rules.size(); i++) v.push_back({rc[i], i});
+          std::sort(v.rbegin(), v.rend());
+          for (int k = 0; k < 12 && k < (int)v.size(); k++) {
+            const DRule& R = c->rs->prog.rules[v[k].second];
+            fprintf(stderr, "  rule link %u id %d phase %d hit_slot %d op %d vars %u chain %u: %.0f cyc/req\n",
+                    v[k].second, R.id, R.phase, R.hit_slot, R.op >= 0 ? c->rs->prog.ops[R.op].kind : -1,
+                    R.var_count, R.tchain_len, v[k].first / n);
+          }
+        }
+      }
+    }
     if (c->diag_on && c->ctr.p) {  // pool words, slow bytes, slow entries, items per bucket
       uint64_t h[16];
       if (hipMemcpy(h, c->ctr.p, 128, hipMemcpyDeviceToHost) == hipSuccess) {
