@@ -949,7 +949,7 @@ struct Lower {
     int kind;  // 0 regex, 1 phrases (fold), 2 literal (case-sensitive)
     std::string rx;
     std::vector<std::string> phrases;
-    uint32_t fmask;  // admitting filters of the stream
+    uint64_t fmask;  // admitting filters (global filter ids)
   };
   std::map<std::string, uint32_t> gfilter_ids;  // global (deduplicated) filters: key -> id
   struct StreamBuild {
@@ -1084,12 +1084,12 @@ struct Lower {
       if (o.kind == OP_VALIDATE_BYTE_RANGE || o.kind == OP_VALIDATE_URL_ENCODING || o.kind == OP_VALIDATE_UTF8) {
         bool merged = false;
         for (auto& sv : sb.vals)
-          if (sv.slot == (uint32_t)slot) sv.fmask |= 1u << fid, merged = true;
+          if (sv.slot == (uint32_t)slot) sv.fmask |= 1ull << sb.gids[fid], merged = true;
         if (merged) continue;
         DScanVal sv{};
         sv.kind = o.kind;
         sv.negate = o.negate;
-        sv.fmask = 1u << fid;
+        sv.fmask = 1ull << sb.gids[fid];
         sv.slot = (uint32_t)slot;
         for (int k = 0; k < 8; k++) sv.bits[k] = o.bits[k];
         sb.vals.push_back(sv);
@@ -1097,12 +1097,12 @@ struct Lower {
       }
       bool merged = false;
       for (auto& pe : sb.pats)
-        if (pe.slot == (uint32_t)slot) pe.fmask |= 1u << fid, merged = true;
+        if (pe.slot == (uint32_t)slot) pe.fmask |= 1ull << sb.gids[fid], merged = true;
       if (merged) continue;
       PatEntry pe;
       pe.slot = (uint32_t)slot;
       pe.negate = o.negate != 0;
-      pe.fmask = 1u << fid;
+      pe.fmask = 1ull << sb.gids[fid];
       if (o.kind == OP_RX) {
         pe.kind = 0;
         pe.rx = "(?sm)" + r.op_arg;
@@ -1226,6 +1226,8 @@ struct Lower {
       s.filt_begin = (uint32_t)P->sfilt.size();
       s.filt_count = (uint32_t)sb.filters.size();
       P->sfilt.insert(P->sfilt.end(), sb.gids.begin(), sb.gids.end());
+      s.gmask = 0;
+      for (uint8_t g : sb.gids) s.gmask |= 1ull << g;
       const uint32_t sid = (uint32_t)P->streams.size();
       s.val_begin = (uint32_t)P->svals.size();
       s.val_count = (uint32_t)sb.vals.size();
@@ -1247,7 +1249,7 @@ struct Lower {
       js << "]"
          << ",\"vals\":" << sb.vals.size() << ",\"jobs\":[";
       // 3. jobs: pack up to GI_JOB_MAX_DFA automata per LDS image
-      const uint32_t nf = s.filt_count;
+      const uint32_t nf = (uint32_t)P->filters.size();  // fmask tables are indexed by global filter id
       size_t a = 0;
       bool first_j = true;
       while (a < autos.size()) {

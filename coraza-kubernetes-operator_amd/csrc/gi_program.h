@@ -204,6 +204,7 @@ struct DStream {
   uint32_t filt_begin, filt_count;  // DFilter
   uint32_t job_begin, job_count;    // DJob (contiguous per stream)
   uint32_t val_begin, val_count;    // DScanVal: validate operators, evaluated by k_stream
+  uint64_t gmask;     // the stream's filters as global filter ids
   uint8_t kind_mask;  // union of the field filters' kinds (1 << FieldKind)
   uint8_t collapse;   // every automaton maps all non-ASCII runes to one class: values are
                       // rune-collapsed (each non-ASCII rune -> GI_RUNE_MARK) instead of slow
@@ -291,7 +292,7 @@ __host__ __device__ inline uint32_t transform_triggers(uint8_t code) {
 //                  accept row of a single automaton loops to itself),
 //                  class map (128 rune-mode / 256 byte-mode), combo (union),
 //                  end-of-input accept (u8 per state single / u64 per state union)
-//   fmask         u64[jdfa_count][n_filters]: patterns each stream filter admits
+//   fmask         u64[jdfa_count][n_gfilters]: patterns each (global) filter admits
 //   slots         u32 hit slot per pattern, automata concatenated
 struct DJob {
   uint32_t stream;
@@ -312,7 +313,7 @@ struct DJobDfa {
   int32_t lds_slots;  // u32 hit slot per pattern
   uint32_t pat_begin; // DPat, n_pat entries (bit k of the match mask)
   uint32_t n_pat;
-  uint32_t fmask_off; // u64 pool: per stream filter, the patterns it admits
+  uint32_t fmask_off; // u64 pool: per global filter, the patterns it admits
   uint32_t _pad;
   uint64_t neg_mask;  // patterns whose operator is negated
 };
@@ -325,9 +326,8 @@ struct DScanVal {     // @validateByteRange / @validateUrlEncoding / @validateUt
   uint8_t kind;
   uint8_t negate;
   uint8_t _pad[2];
-  uint32_t fmask;     // admitting filters
   uint32_t slot;
-  uint32_t _pad2;
+  uint64_t fmask;     // admitting filters (global filter ids)
   uint32_t bits[8];
 };
 

@@ -656,8 +656,8 @@ __device__ int64_t t_utf8tounicode(const uint8_t* s, uint32_t n, uint8_t* d, uin
   return o;
 }
 
-__device__ int64_t apply_transform(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d,
-                                   uint32_t cap) {
+__device__ __forceinline__ int64_t apply_transform_inl(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n,
+                                                      uint8_t* d, uint32_t cap) {
   switch (code) {
     case T_UTF8TOUNICODE: return t_utf8tounicode(s, n, d, cap);
     case T_LOWERCASE: return t_lowercase(P, s, n, d, cap);
@@ -675,9 +675,22 @@ __device__ int64_t apply_transform(const DProgram& P, uint8_t code, const uint8_
   }
 }
 
+// Out-of-line instance (generic pointers): k_eval, HBM buffers.  k_stream's
+// LDS path inlines apply_transform_inl so every buffer access is a ds_* op.
+__device__ __noinline__ int64_t apply_transform(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n,
+                                                uint8_t* d, uint32_t cap) {
+  return apply_transform_inl(P, code, s, n, d, cap);
+}
+
 __device__ uint32_t value_summary(const uint8_t* s, uint32_t n) {
   uint32_t m = 0;
   for (uint32_t i = 0; i < n; i++) m |= byte_summary(s[i]);
+  return m;
+}
+// the same through a 256-entry table (k_stream keeps it in LDS)
+__device__ __forceinline__ uint32_t value_summary_lut(const uint16_t* lut, const uint8_t* s, uint32_t n) {
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < n; i++) m |= lut[s[i]];
   return m;
 }
 // ------------------------------------------------------------ transaction
@@ -1868,7 +1881,7 @@ __device__ uint64_t item_gmask(const DProgram& P, const Item& it) {
   const uint32_t hci = it.kind ? gi_fnv1a(it.kp, it.kn, true) : 0u;
   const uint32_t hcs = it.kind ? gi_fnv1a(it.kp, it.kn, false) : 0u;
   for (uint32_t g = 0; g < P.n_gfilters; g++) {
-    const DFilter F = P.filters[g];
+    const DFilter F = gi_cload(P.filters, g);
     if (it.kind == 0) {
       if (F.single == it.single) m |= 1ull << g;
       continue;
@@ -1894,7 +1907,7 @@ __device__ uint64_t item_gmask(const DProgram& P, const Item& it) {
 }
 
 // The stream's validate operators (@validateByteRange / UrlEncoding / Utf8Encoding).
-__device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, const DStream& S, uint32_t fm, bool maybe,
+__device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, const DStream& S, uint64_t fm, bool maybe,
                             const uint8_t* v, uint32_t n) {
   for (uint32_t q = 0; q < S.val_count; q++) {
     const DScanVal& sv = P.svals[S.val_begin + q];
@@ -1905,20 +1918,21 @@ __device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, cons
 
 // chain through two buffers of capacity cap; -1 on overflow.  summ = byte
 // summary of v: transformations it proves to be identities are skipped.
+template <bool INL>
 __device__ __forceinline__ int64_t run_chain(const DProgram& P, const DStream& S, const uint8_t* v, uint32_t vn,
                                              uint32_t summ, uint8_t* b0, uint8_t* b1, uint32_t cap,
-                                             const uint8_t** out) {
+                                             const uint8_t** out, const uint16_t* lut) {
   const uint8_t* cur = v;
   uint32_t cn = vn;
   for (uint32_t k = 0; k < S.tchain_len; k++) {
-    const uint8_t code = (uint8_t)P.tchains32[S.tchain_off + k];
+    const uint8_t code = (uint8_t)GI_CONST(uint32_t, P.tchains32)[S.tchain_off + k];
     if (!(summ & transform_triggers(code))) continue;
     uint8_t* dst = (cur == b0) ? b1 : b0;
-    const int64_t m = apply_transform(P, code, cur, cn, dst, cap);
+    const int64_t m = INL ? apply_transform_inl(P, code, cur, cn, dst, cap) : apply_transform(P, code, cur, cn, dst, cap);
     if (m < 0) return -1;
     cur = dst;
     cn = (uint32_t)m;
-    summ = value_summary(cur, cn);
+    summ = value_summary_lut(lut, cur, cn);
   }
   *out = cur;
   return cn;
@@ -1931,9 +1945,9 @@ __device__ __forceinline__ void void_request(const DBatch& B, uint32_t r) {
 
 // Slow-list entry: the transformed bytes are copied into the slow arena.
 struct SlowEnt {
-  uint32_t req, stream, fm, flags;  // flags: bit0 maybe
-  uint64_t off;                     // byte offset in B.slow_bytes
-  uint32_t len, _pad;
+  uint32_t req, stream, flags, len;  // flags: bit0 maybe
+  uint64_t off;                      // byte offset in B.slow_bytes
+  uint64_t fm;                       // admitting filters (global ids)
 };
 
 // Collapse a value for a stream whose automata map every non-ASCII rune to one
@@ -1965,8 +1979,10 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
   // counter.  Pool words are reserved GI_PCHUNK at a time per wave (one
   // workgroup = one wave), so the pool counter sees one atomic per chunk.
   __shared__ unsigned long long pnext, pend;
+  __shared__ uint16_t sumlut[256];  // byte_summary of every byte value
   const uint32_t lane = threadIdx.x;
   if (lane == 0) pnext = pend = 0;
+  for (uint32_t b = lane; b < 256; b += 64) sumlut[b] = (uint16_t)byte_summary((uint8_t)b);
   __syncthreads();
   const uint32_t iw_base = B.ibk[2 * GI_NB + bucket];
   const uint32_t base = B.ibk[2 * bucket], cnt = B.ibk[2 * bucket + 1];
@@ -1976,7 +1992,10 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
   uint8_t* b0 = IN ? lb + 64 * IS + lane * WT : g0;
   uint8_t* b1 = IN ? lb + 64 * (IS + WT) + lane * WT : g1;
   const uint32_t cap = IN ? WT : B.lcap;
+  uint64_t pc_item = 0, pc_chain = 0, pc_out = 0, pc_loop = 0, pc_tot = 0, pc_fm = 0, pc_run = 0, pc_slow = 0;
+  const uint64_t pc_start = B.prof ? clock64() : 0;
   for (uint32_t w0 = blockIdx.x * 64; w0 < cnt; w0 += gridDim.x * 64) {
+    const uint64_t c_a = B.prof ? clock64() : 0;
     const uint32_t ii = w0 + lane;
     Item it{};
     uint64_t gm = 0;
@@ -1988,28 +2007,34 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
       GI_BOUND(it.req < B.n_req, it.req, ii);
       gm = item_gmask(P, it);
       src = it.vp;
-      if (IN && it.vn <= IN) {  // stage the scanned bytes once for all streams
-        for (uint32_t i = 0; i < it.vn; i++) li[i] = it.vp[i];
+      if (IN) {  // stage the scanned bytes once for all streams (bucket: vn <= IN)
+        const uint32_t n = min(it.vn, IN);
+        for (uint32_t i = 0; i < n; i++) li[i] = it.vp[i];
         src = li;
       }
-      summ = value_summary(src, it.vn);
+      summ = value_summary_lut(sumlut, src, it.vn);
     }
     const uint32_t blk = iw_base + w0 / 64;
+    const uint64_t c_b = B.prof ? clock64() : 0;
+    pc_item += c_b - c_a;
     for (uint32_t s = 0; s < P.n_streams; s++) {
-      const DStream S = P.streams[s];
-      uint32_t fm = 0;
-      for (uint32_t k = 0; k < S.filt_count; k++) fm |= (uint32_t)((gm >> P.sfilt[S.filt_begin + k]) & 1ull) << k;
+      const uint64_t c_s0 = B.prof ? clock64() : 0;
+      const DStream S = gi_cload(P.streams, s);
+      const uint64_t fm = gm & S.gmask;
       if (!__ballot(fm != 0)) {
         if (lane == 0 && S.job_count && blk < B.qcap) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2(0u, 0u);
         continue;
       }
+      const uint64_t c_sa = B.prof ? clock64() : 0;
+      pc_fm += c_sa - c_s0;
       const uint8_t* cur = nullptr;
       int64_t cn = 0;
       bool maybe = false, glob = !IN;
       if (fm) {
-        cn = run_chain(P, S, src, it.vn, summ, b0, b1, cap, &cur);
+        cn = run_chain<IN != 0>(P, S, src, it.vn, summ, b0, b1, cap, &cur, sumlut);
+        if (B.prof) pc_run += clock64() - c_sa;
         if (cn < 0 && IN) {
-          cn = run_chain(P, S, src, it.vn, summ, g0, g1, B.lcap, &cur);
+          cn = run_chain<false>(P, S, src, it.vn, summ, g0, g1, B.lcap, &cur, sumlut);
           glob = true;
         }
         if (cn < 0) {
@@ -2019,14 +2044,15 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
         }
         if (S.val_count) stream_vals(P, B, it.req, S, fm, maybe, cur, (uint32_t)cn);
       }
+      const uint64_t c_s1 = B.prof ? clock64() : 0;
+      pc_chain += c_s1 - c_s0;
       if (!S.job_count) continue;
       bool slow = maybe;
       if (fm && !maybe) {
-        uint32_t hi = 0;
-        if (cur == src) hi = (summ & BS_HIGH) ? 0x80u : 0u;
-        else
-          for (uint32_t i = 0; i < (uint32_t)cn; i++) hi |= cur[i];
-        if (hi & 0x80) {
+        // byte summary of the chain output (run_chain leaves it current in
+        // the identity case; recompute otherwise)
+        const uint32_t osum = (cur == src) ? summ : value_summary_lut(sumlut, cur, (uint32_t)cn);
+        if (osum & BS_HIGH) {
           if (S.collapse) {
             uint8_t* dst = glob ? (cur == g0 ? g1 : g0) : (cur == b0 ? b1 : b0);
             cn = collapse_runes(cur, (uint32_t)cn, dst);
@@ -2050,10 +2076,11 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
           e.flags = maybe ? 1u : 0u;
           e.off = off;
           e.len = (uint32_t)cn;
-          e._pad = 0;
           ((SlowEnt*)B.slow)[k] = e;
         }
       }
+      const uint64_t c_s2 = B.prof ? clock64() : 0;
+      pc_slow += c_s2 - c_s1;
       const bool out = fm && !slow;
       const uint64_t om = __ballot(out);
       if (!om) {
@@ -2062,7 +2089,7 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
       }
       const uint32_t nv = __popcll(om);
       const uint32_t nw = wave_max(out ? ((uint32_t)cn + 3) / 4 : 0u);
-      const uint64_t words = (uint64_t)nv * (3 + nw);
+      const uint64_t words = (uint64_t)nv * (4 + nw);
       unsigned long long woff = 0;
       if (lane == 0) {
         if (pnext + words > pend) {
@@ -2085,8 +2112,9 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
         const uint32_t i = mask_rank(om);
         uint32_t* q = B.pool + woff;
         q[i] = it.req;
-        q[nv + i] = fm;
-        q[2 * nv + i] = (uint32_t)cn;
+        q[nv + i] = (uint32_t)fm;
+        q[2 * nv + i] = (uint32_t)(fm >> 32);
+        q[3 * nv + i] = (uint32_t)cn;
         const uint32_t nwi = ((uint32_t)cn + 3) / 4;
         for (uint32_t w = 0; w < nwi; w++) {
           uint32_t x = 0;
@@ -2094,10 +2122,23 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
             const uint32_t at = 4 * w + b;
             x |= (at < (uint32_t)cn ? (uint32_t)cur[at] : 0u) << (8 * b);
           }
-          q[3 * nv + (uint64_t)w * nv + i] = x;
+          q[4 * nv + (uint64_t)w * nv + i] = x;
         }
       }
+      if (B.prof) pc_out += clock64() - c_s2;
     }
+    if (B.prof) pc_loop += clock64() - c_b;
+  }
+  if (B.prof && lane == 0) {
+    pc_tot = clock64() - pc_start;
+    atomicAdd(&B.prof[40 + 5 * bucket + 0], (unsigned long long)pc_item);
+    atomicAdd(&B.prof[40 + 5 * bucket + 1], (unsigned long long)pc_chain);
+    atomicAdd(&B.prof[40 + 5 * bucket + 2], (unsigned long long)pc_out);
+    atomicAdd(&B.prof[40 + 5 * bucket + 3], (unsigned long long)pc_loop);
+    atomicAdd(&B.prof[40 + 5 * bucket + 4], (unsigned long long)pc_tot);
+    atomicAdd(&B.prof[80 + 3 * bucket + 0], (unsigned long long)pc_fm);
+    atomicAdd(&B.prof[80 + 3 * bucket + 1], (unsigned long long)pc_run);
+    atomicAdd(&B.prof[80 + 3 * bucket + 2], (unsigned long long)pc_slow);
   }
 }
 
@@ -2149,12 +2190,12 @@ __device__ uint64_t scan_full(const DProgram& P, const DDfa& d, const uint8_t* s
 }
 
 // Per-value path on global tables: every automaton of job J over one value.
-__device__ void scan_value_global(const DProgram& P, const DBatch& B, uint32_t r, const DJob& J, uint32_t fm,
+__device__ void scan_value_global(const DProgram& P, const DBatch& B, uint32_t r, const DJob& J, uint64_t fm,
                                   bool maybe, const uint8_t* v, uint32_t n) {
   for (uint32_t q = 0; q < J.jdfa_count; q++) {
     const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
     uint64_t al = 0;
-    for (uint32_t f = fm; f; f &= f - 1) al |= P.u64pool[jd.fmask_off + (__ffs(f) - 1)];
+    for (uint64_t f = fm; f; f &= f - 1) al |= P.u64pool[jd.fmask_off + (__ffsll((unsigned long long)f) - 1)];
     if (!al) continue;
     uint64_t x = al;
     if (!maybe) x &= scan_full(P, P.dfas[jd.dfa], v, n) ^ jd.neg_mask;
@@ -2168,9 +2209,10 @@ __device__ void scan_value_global(const DProgram& P, const DBatch& B, uint32_t r
 
 // Patterns of automaton q the admitting filters fm let through (image table).
 __device__ __forceinline__ uint64_t img_allowed(const uint8_t* img, uint32_t fmask_off, uint32_t nf, uint32_t q,
-                                                uint32_t fm) {
+                                                uint64_t fm) {
   uint64_t a = 0;
-  for (uint32_t f = fm; f; f &= f - 1) a |= *(const uint64_t*)(img + fmask_off + 8 * (q * nf + (__ffs(f) - 1)));
+  for (uint64_t f = fm; f; f &= f - 1)
+    a |= *(const uint64_t*)(img + fmask_off + 8 * (q * nf + (__ffsll((unsigned long long)f) - 1)));
   return a;
 }
 
@@ -2185,22 +2227,22 @@ __device__ __forceinline__ void emit_img(const DBatch& B, uint32_t r, const uint
 
 // Accepting transition of union automaton q (rare): emit its matches now.
 __device__ void union_accept(const DProgram& P, const DBatch& B, uint32_t r, const DJob& J, const uint8_t* img,
-                             uint32_t nf, uint32_t q, uint32_t fm, uint32_t st, uint32_t cls) {
-  const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
-  const DDfa d = P.dfas[jd.dfa];
+                             uint32_t nf, uint32_t q, uint64_t fm, uint32_t st, uint32_t cls) {
+  const DJobDfa jd = gi_cload(P.jdfas, J.jdfa_begin + q);
+  const DDfa d = gi_cload(P.dfas, (uint64_t)jd.dfa);
   const uint64_t x = P.u64pool[d.acc_off + st * 5 + img[jd.lds_combo + cls]] & img_allowed(img, J.lds_fmask, nf, q, fm);
   if (x) emit_img(B, r, img, jd.lds_slots, x);
 }
 
 // End of a value: end-of-input matches of every automaton (negation applied).
 __device__ void value_end(const DProgram& P, const DBatch& B, uint32_t r, const DJob& J, const uint8_t* img,
-                          uint32_t nf, uint32_t K, uint32_t fm, const uint32_t* st) {
+                          uint32_t nf, uint32_t K, uint64_t fm, const uint32_t* st) {
   for (uint32_t q = 0; q < K; q++) {
-    const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
+    const DJobDfa jd = gi_cload(P.jdfas, J.jdfa_begin + q);
     GI_BOUND(st[q] < P.dfas[jd.dfa].n_states, st[q], q);
     const uint64_t al = img_allowed(img, J.lds_fmask, nf, q, fm);
     if (!al) continue;
-    const DDfa d = P.dfas[jd.dfa];
+    const DDfa d = gi_cload(P.dfas, (uint64_t)jd.dfa);
     uint64_t bits;
     if (d.multi) bits = *(const uint64_t*)(img + jd.lds_endacc + 8 * st[q]);
     else bits = img[jd.lds_endacc + st[q]] ? 1ull : 0ull;
@@ -2229,14 +2271,15 @@ __device__ __forceinline__ void scan_qblock(const DProgram& P, const DBatch& B, 
   const uint32_t lane = lane_id();
   const uint32_t woff = d.x, nv = d.y & 0xFFu, nw = d.y >> 8;
   if (nv == 0) return;
-  GI_BOUND(nv <= 64 && (uint64_t)woff + (uint64_t)(3 + nw) * nv <= B.pool_cap, woff, d.y);
+  GI_BOUND(nv <= 64 && (uint64_t)woff + (uint64_t)(4 + nw) * nv <= B.pool_cap, woff, d.y);
   const uint32_t* q = B.pool + woff;
-  uint32_t req = 0, fm = 0, len = 0;
+  uint32_t req = 0, len = 0;
+  uint64_t fm = 0;
   bool act = false;
   if (lane < nv) {
     req = q[lane];
-    fm = q[nv + lane];
-    len = q[2 * nv + lane];
+    fm = (uint64_t)q[nv + lane] | ((uint64_t)q[2 * nv + lane] << 32);
+    len = q[3 * nv + lane];
     GI_BOUND(req < B.n_req && len <= 4 * nw, req, len);
     uint64_t any = 0;
     for (uint32_t k = 0; k < K; k++) any |= img_allowed(img, J.lds_fmask, nf, k, fm);
@@ -2248,7 +2291,7 @@ __device__ __forceinline__ void scan_qblock(const DProgram& P, const DBatch& B, 
 #pragma unroll
   for (uint32_t k = 0; k < GI_JOB_MAX_DFA; k++) st[k] = st0[k];
   const uint32_t* jam = (const uint32_t*)img;
-  const uint32_t* wp = q + 3 * nv + lane;
+  const uint32_t* wp = q + 4 * nv + lane;
   for (uint32_t w = 0; w < nw; w++) {
     if (act && 4 * w < len && !(mode & 4)) {
       const uint32_t wd = wp[(uint64_t)w * nv];
@@ -2290,7 +2333,7 @@ __global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint3
     const uint32_t jj = (uint32_t)(u / nu_job);
     const uint32_t chunk = (uint32_t)(u - (uint64_t)jj * nu_job);
     const uint32_t j = jl[jj];
-    const DJob J = P.jobs[j];
+    const DJob J = gi_cload(P.jobs, j);
     const uint8_t* img = P.images + J.img_off;
     if (LDS) {
       if (j != loaded) {  // block-uniform
@@ -2319,7 +2362,7 @@ __global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint3
     }
     if ((mine.y & 0xFFu) != 0) clist[wbase + mask_rank(live)] = mine;
     __syncthreads();
-    const uint32_t nf = P.streams[J.stream].filt_count;
+    const uint32_t nf = P.n_gfilters;  // fmask tables are indexed by global filter id
     const uint32_t K = J.jdfa_count;
     uint32_t trn[GI_JOB_MAX_DFA], st0[GI_JOB_MAX_DFA], umask = 0;
 #pragma unroll
@@ -2327,8 +2370,8 @@ __global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint3
       trn[k] = 0;
       st0[k] = 0;
       if (k < K) {
-        const DJobDfa jd = P.jdfas[J.jdfa_begin + k];
-        const DDfa d = P.dfas[jd.dfa];
+        const DJobDfa jd = gi_cload(P.jdfas, J.jdfa_begin + k);
+        const DDfa d = gi_cload(P.dfas, (uint64_t)jd.dfa);
         trn[k] = (uint32_t)jd.lds_trans | (d.n_classes << 20);
         st0[k] = d.start;
         if (d.multi) umask |= 1u << k;
@@ -2370,7 +2413,7 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
     t.prof_visits = t.prof_evals = t.prof_rules = 0;
     t.prof_eval_cyc = t.prof_act_cyc = 0;
     t.profon = B.prof != nullptr;
-    t.prof_rule_cyc = B.prof ? B.prof + 16 : nullptr;
+    t.prof_rule_cyc = B.prof ? B.prof + 128 : nullptr;
     tx_bind(t, P, g);
     t.hits = B.hits;
     t.n_req = B.n_req;

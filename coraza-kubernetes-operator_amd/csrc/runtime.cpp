@@ -515,9 +515,9 @@ int gi_run_staged(gi_ctx* c) {
     B.slow_used = (unsigned long long*)(cp + 8);
     B.diag = nullptr;
     B.prof = nullptr;
-    if (c->prof_on && c->prof.ensure(128 + 8000) == hipSuccess) {
+    if (c->prof_on && c->prof.ensure(1024 + 8000) == hipSuccess) {
       B.prof = (unsigned long long*)c->prof.p;
-      (void)hipMemsetAsync(c->prof.p, 0, 128 + 8000, c->stream);
+      (void)hipMemsetAsync(c->prof.p, 0, 1024 + 8000, c->stream);
     }
     B.items_cap = c->items_cap;
     B.n_hit_slots = c->rs->prog.n_hit_slots;
@@ -561,15 +561,22 @@ int gi_sync(gi_ctx* c) {
     }
 #endif
     if (c->prof_on && c->prof.p) {
-      unsigned long long h[16];
-      if (hipMemcpy(h, c->prof.p, 128, hipMemcpyDeviceToHost) == hipSuccess && c->n_req) {
+      unsigned long long h[128];
+      if (hipMemcpy(h, c->prof.p, 1024, hipMemcpyDeviceToHost) == hipSuccess && c->n_req) {
+        for (int b = 0; b < 5; b++)
+          fprintf(stderr, "GI_PROF k_stream bucket %d (sum over waves, Mcyc): item %.1f chain %.1f out %.1f loop %.1f total %.1f\n",
+                  b, h[40 + 5 * b] / 1e6, h[41 + 5 * b] / 1e6, h[42 + 5 * b] / 1e6, h[43 + 5 * b] / 1e6,
+                  h[44 + 5 * b] / 1e6);
+        for (int b = 0; b < 5; b++)
+          fprintf(stderr, "GI_PROF k_stream bucket %d: fm+ballot %.1f run_chain(lane max) %.1f slowcheck+collapse %.1f\n", b,
+                  h[80 + 3 * b] / 1e6, h[81 + 3 * b] / 1e6, h[82 + 3 * b] / 1e6);
         const double n = c->n_req;
         fprintf(stderr,
                 "GI_PROF k_eval per request: init %.0f cyc, phase1 %.0f, phase2 %.0f, total %.0f; rule visits %.1f, "
                 "evaluated %.1f, matched %.1f; eval_rule %.0f cyc, actions %.0f cyc\n",
                 h[0] / n, h[1] / n, h[2] / n, h[3] / n, h[4] / n, h[5] / n, h[6] / n, h[7] / n, h[8] / n);
         std::vector<unsigned long long> rc(1000);
-        if (hipMemcpy(rc.data(), (uint8_t*)c->prof.p + 128, 8000, hipMemcpyDeviceToHost) == hipSuccess) {
+        if (hipMemcpy(rc.data(), (uint8_t*)c->prof.p + 1024, 8000, hipMemcpyDeviceToHost) == hipSuccess) {
           std::vector<std::pair<unsigned long long, uint32_t>> v;
           for (uint32_t i = 0; i < 1000 && i < c->rs->prog.rules.size(); i++) v.push_back({rc[i], i});
           std::sort(v.rbegin(), v.rend());
@@ -695,7 +702,7 @@ extern "C" int gi_selftest_plan(const gi_ruleset* rs, char* err, size_t errcap) 
     if ((uint64_t)J.img_off + J.img_bytes > P.images.size()) return bad(2, "image range");
     if (J.jdfa_count == 0 || J.jdfa_count > GI_JOB_MAX_DFA) return bad(3, "automata per job");
     const uint8_t* img = &P.images[J.img_off];
-    const uint32_t nf = P.streams[J.stream].filt_count;
+    const uint32_t nf = (uint32_t)P.filters.size();
     if ((uint64_t)J.lds_fmask + 8ull * J.jdfa_count * nf > J.img_bytes) return bad(4, "fmask table");
     if (J.lds && (J.big ? J.img_bytes > GI_BIG_LDS_BYTES + 4096 : J.img_bytes > GI_JOB_LDS_BYTES))
       return bad(5, "lds image size");
@@ -750,8 +757,12 @@ extern "C" int gi_selftest_plan(const gi_ruleset* rs, char* err, size_t errcap) 
   for (size_t s = 0; s < P.streams.size(); s++) {
     const DStream& S = P.streams[s];
     if ((uint64_t)S.filt_begin + S.filt_count > P.sfilt.size()) return bad(16, "stream filters");
-    for (uint32_t k = 0; k < S.filt_count; k++)
+    uint64_t gm = 0;
+    for (uint32_t k = 0; k < S.filt_count; k++) {
       if (P.sfilt[S.filt_begin + k] >= P.filters.size()) return bad(17, "global filter id");
+      gm |= 1ull << P.sfilt[S.filt_begin + k];
+    }
+    if (gm != S.gmask) return bad(21, "stream filter mask");
     if ((uint64_t)S.job_begin + S.job_count > P.jobs.size()) return bad(18, "stream jobs");
     for (uint32_t j = S.job_begin; j < S.job_begin + S.job_count; j++)
       if (P.jobs[j].stream != s) return bad(19, "job/stream mismatch");
