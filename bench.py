@@ -33,6 +33,13 @@ import traffic  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
+# launch name (gi_stats) -> kernel name as rocprofv3 reports it
+ROCPROF_NAMES = {
+    "k_stream0": "k_stream<16u, 20u>", "k_stream1": "k_stream<32u, 36u>", "k_stream2": "k_stream<64u, 68u>",
+    "k_stream3": "k_stream<128u, 132u>", "k_stream4": "k_stream<0u, 0u>", "k_scan": "k_scan<true>",
+    "k_scan_big": "k_scan<true>", "k_scan_hbm": "k_scan<false>",
+}
+
 CONFIGS = {
     # name: (ruleset file, default n_req, post_frac, description)
     "c2": ("rulesets/crs_pl1.conf", 1_000_000, 0.0,
@@ -125,6 +132,7 @@ def main():
         torch.cuda.synchronize()
     eng.sync()
     kern_ms, stage_ms = [], {"k_collect": [], "k_stream": [], "k_scan": [], "k_eval": []}
+    launch_ms, launch_bytes = {}, {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -134,6 +142,9 @@ def main():
         stage_ms["k_stream"].append(st["last_stream_ms"])
         stage_ms["k_scan"].append(st["last_scan_ms"])
         stage_ms["k_eval"].append(st["last_eval_ms"])
+        for ln in st["launches"]:
+            launch_ms.setdefault(ln["name"], []).append(ln["ms"])
+            launch_bytes[ln["name"]] = ln["alg_bytes"]
     eng.sync()
     if dist is not None:
         torch.cuda.synchronize()
@@ -152,16 +163,15 @@ def main():
     value = total_req * args.steps / elapsed
     gbs = total_bytes * args.steps / elapsed / 1e9
 
-    # Roofline of the dominant single kernel (HIP events on the context
-    # stream).  Algorithmic bytes per launch:
-    #   k_eval : raw request bytes + 80-B verdict + 4 B per matched rule id
-    # (the stages k_stream / k_scan are several launches each and are reported
-    # as stage times beside it).
+    # Roofline of the dominant single kernel launch (HIP events recorded on the
+    # context stream around every launch; DESIGN.md §4 defines each kernel's
+    # algorithmic bytes per launch, counted on the device).
     avg_kern_ms = float(np.mean(kern_ms))
     avg_stage = {k: float(np.mean(v)) for k, v in stage_ms.items()}
-    dom = "k_eval"
-    alg_bytes = raw + 80 * batch.n_req + 4 * int(tally["matched_total"])
-    achieved = alg_bytes / (avg_stage[dom] * 1e-3) / 1e9
+    avg_launch = {k: float(np.mean(v)) for k, v in launch_ms.items()}
+    dom = max(avg_launch, key=lambda k: avg_launch[k])
+    alg_bytes = launch_bytes[dom]
+    achieved = alg_bytes / (avg_launch[dom] * 1e-3) / 1e9
     hbm_traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.exists(tpath):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)
@@ -190,8 +200,11 @@ def main():
         "error_requests": int(tally["n_error"]),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": hbm_traffic,
-                     "kernel": dom, "kernel_ms": round(avg_stage[dom], 4),
-                     "alg_bytes_per_launch": int(alg_bytes),
+                     "kernel": dom, "rocprof_kernel": ROCPROF_NAMES.get(dom, dom),
+                     "kernel_ms": round(avg_launch[dom], 4), "alg_bytes_per_launch": int(alg_bytes),
+                     "launches": {k: {"ms": round(v, 4), "alg_bytes": int(launch_bytes[k]),
+                                      "GB/s": round(launch_bytes[k] / (v * 1e-3) / 1e9, 2) if v > 0 else None}
+                                  for k, v in avg_launch.items()},
                      "stages_ms": {k: round(v, 4) for k, v in avg_stage.items()},
                      "pipeline_kernel_ms": round(avg_kern_ms, 4)},
         "gen_s": round(t_gen, 1),

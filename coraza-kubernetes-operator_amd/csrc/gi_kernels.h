@@ -48,7 +48,8 @@ struct DBatch {
   uint64_t pool_cap;          // words
   unsigned long long* pool_used;
   uint2* qblk;                // [stream][qcap] queue blocks {word offset, nv | nw << 8}
-  uint32_t* qcount;           // [stream]
+  unsigned long long* acct;   // algorithmic-byte counters: [0..5) item bytes per bucket, [5..10) queue
+                              // words written per k_stream bucket, [10..13) queue words read per k_scan launch
   uint32_t qcap;
   void* slow;                 // SlowEnt[slow_cap]
   uint32_t* slow_count;
@@ -86,9 +87,18 @@ void scan_allow_lds(uint32_t lds_bytes);
 
 // k_collect -> k_stream -> k_scan (small, big) -> k_eval on `stream`;
 // ev (optional) = 3 events recorded after k_collect, k_stream and k_scan.
+// Per-launch HIP events of one pipeline run (ev[0] before the first launch,
+// ev[k + 1] after launch k).
+#define GI_MAX_LAUNCHES 16
+struct LaunchLog {
+  hipEvent_t ev[GI_MAX_LAUNCHES + 1];
+  const char* name[GI_MAX_LAUNCHES];
+  int n;
+};
+
 // stop_after > 0 (debugging): launch only the first stop_after kernels and
 // synchronise after each, printing the first failing one.
 void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
-                     int stop_after = 0);
+                     int stop_after = 0, LaunchLog* log = nullptr);
 
 }  // namespace gi

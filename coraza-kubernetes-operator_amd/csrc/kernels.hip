@@ -1837,7 +1837,8 @@ __global__ void __launch_bounds__(1024) k_ioffsets(DBatch B, uint32_t n_blocks) 
 // One thread per request, same block shape as k_collect.
 __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
   __shared__ uint32_t rank[GI_NB];
-  if (threadIdx.x < GI_NB) rank[threadIdx.x] = 0;
+  __shared__ unsigned long long ibytes[GI_NB];
+  if (threadIdx.x < GI_NB) rank[threadIdx.x] = 0, ibytes[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < B.n_req) {
@@ -1868,9 +1869,12 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
         it.side = (uint8_t)side;
         it._pad = 0;
         ((Item*)B.items)[at] = it;
+        atomicAdd(&ibytes[b], (unsigned long long)n);
       });
     }
   }
+  __syncthreads();
+  if (threadIdx.x < GI_NB && ibytes[threadIdx.x]) atomicAdd(&B.acct[threadIdx.x], ibytes[threadIdx.x]);
 }
 
 // Global filters admitting the item (bit g of the result).
@@ -1993,6 +1997,7 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
   uint8_t* b1 = IN ? lb + 64 * (IS + WT) + lane * WT : g1;
   const uint32_t cap = IN ? WT : B.lcap;
   uint64_t pc_item = 0, pc_chain = 0, pc_out = 0, pc_loop = 0, pc_tot = 0, pc_fm = 0, pc_run = 0, pc_slow = 0;
+  uint64_t wwords = 0;  // queue words this wave wrote (algorithmic-byte accounting)
   const uint64_t pc_start = B.prof ? clock64() : 0;
   for (uint32_t w0 = blockIdx.x * 64; w0 < cnt; w0 += gridDim.x * 64) {
     const uint64_t c_a = B.prof ? clock64() : 0;
@@ -2091,6 +2096,7 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
       const uint32_t nw = wave_max(out ? ((uint32_t)cn + 3) / 4 : 0u);
       const uint64_t words = (uint64_t)nv * (4 + nw);
       unsigned long long woff = 0;
+      wwords += words;
       if (lane == 0) {
         if (pnext + words > pend) {
           const unsigned long long sz = words > GI_PCHUNK ? words : (unsigned long long)GI_PCHUNK;
@@ -2129,6 +2135,7 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
     }
     if (B.prof) pc_loop += clock64() - c_b;
   }
+  if (lane == 0 && wwords) atomicAdd(&B.acct[5 + bucket], (unsigned long long)wwords);
   if (B.prof && lane == 0) {
     pc_tot = clock64() - pc_start;
     atomicAdd(&B.prof[40 + 5 * bucket + 0], (unsigned long long)pc_item);
@@ -2317,7 +2324,8 @@ __device__ __forceinline__ void scan_qblock(const DProgram& P, const DBatch& B, 
 // per job change; !LDS: the image is read from HBM (automata too large for LDS).
 template <bool LDS>
 __global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint32_t* __restrict__ jl, uint32_t n_jl,
-                                               uint32_t mode) {
+                                               uint32_t mode, uint32_t acct_slot) {
+  uint64_t rwords = 0;  // queue words this wave read (algorithmic-byte accounting)
   extern __shared__ __attribute__((aligned(16))) uint8_t simg[];
   __shared__ uint2 clist[1024];
   __shared__ uint32_t wcnt[16];
@@ -2377,9 +2385,14 @@ __global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint3
         if (d.multi) umask |= 1u << k;
       }
     }
-    for (uint32_t i = wv; i < total; i += nwv) scan_qblock(P, B, J, img, K, trn, st0, umask, nf, clist[i], mode);
+    for (uint32_t i = wv; i < total; i += nwv) {
+      const uint2 d = clist[i];
+      rwords += (uint64_t)(d.y & 0xFFu) * (4 + (d.y >> 8));
+      scan_qblock(P, B, J, img, K, trn, st0, umask, nf, d, mode);
+    }
     __syncthreads();  // clist / wcnt reuse
   }
+  if ((threadIdx.x & 63) == 0 && rwords) atomicAdd(&B.acct[10 + acct_slot], (unsigned long long)rwords);
 }
 
 // Slow values (non-ASCII / "maybe"), one thread per list entry: every job of
@@ -2539,21 +2552,30 @@ uint32_t scan_resident_blocks(uint32_t lds_bytes) {
   return (uint32_t)prop.multiProcessorCount * (uint32_t)per_cu;
 }
 
-#define GI_LAUNCH(name, ...)                                                              \
+#define GI_LAUNCH(nm, ...)                                                                \
   do {                                                                                    \
-    if (stop_after && ++nk > stop_after) return;                                          \
+    if (stop_after && nk + 1 > stop_after) return;                                        \
+    nk++;                                                                                 \
     hipLaunchKernelGGL(__VA_ARGS__);                                                      \
+    if (log && log->n < GI_MAX_LAUNCHES) {                                                \
+      log->name[log->n] = nm;                                                             \
+      (void)hipEventRecord(log->ev[++log->n], stream);                                    \
+    }                                                                                     \
     if (stop_after) {                                                                     \
       hipError_t e_ = hipStreamSynchronize(stream);                                       \
-      fprintf(stderr, "GI_STOP_AFTER: kernel %d %s -> %s\n", nk, name, hipGetErrorString(e_)); \
+      fprintf(stderr, "GI_STOP_AFTER: kernel %d %s -> %s\n", nk, nm, hipGetErrorString(e_));   \
       if (e_ != hipSuccess) return;                                                       \
     }                                                                                     \
   } while (0)
 
 void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
-                     int stop_after) {
+                     int stop_after, LaunchLog* log) {
   if (!B.n_req) return;
   int nk = 0;
+  if (log) {
+    log->n = 0;
+    (void)hipEventRecord(log->ev[0], stream);
+  }
   const uint32_t cb = (B.n_req + 255) / 256;
   GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[0], stream);
@@ -2568,11 +2590,11 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
     if (ev) (void)hipEventRecord(ev[1], stream);
     for (int big = 0; big < 2; big++)
       if (S.n_jobs[big])
-        GI_LAUNCH("k_scan", k_scan<true>, dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B, S.jobs[big],
-                  S.n_jobs[big], S.mode);
+        GI_LAUNCH(big ? "k_scan_big" : "k_scan", k_scan<true>, dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P,
+                  B, S.jobs[big], S.n_jobs[big], S.mode, (uint32_t)big);
     if (S.n_global)
       GI_LAUNCH("k_scan_hbm", k_scan<false>, dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
-                S.n_global, S.mode);
+                S.n_global, S.mode, 2u);
     GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
   } else if (ev) {
     (void)hipEventRecord(ev[1], stream);

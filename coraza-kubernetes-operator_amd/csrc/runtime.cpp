@@ -89,6 +89,8 @@ struct gi_ctx {
   ScanLaunch scan{};
   uint32_t hit_words = 0;
   hipEvent_t evs[3] = {nullptr, nullptr, nullptr};
+  LaunchLog log{};
+  uint64_t raw_nobody = 0, raw_all = 0;  // batch bytes (algorithmic-byte accounting)
   uint32_t n_req = 0;
   bool staged = false, ran = false;
   gi_stats stats{};
@@ -197,6 +199,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   if (e == hipSuccess) e = hipEventCreate(&c->evs[0]);
   if (e == hipSuccess) e = hipEventCreate(&c->evs[1]);
   if (e == hipSuccess) e = hipEventCreate(&c->evs[2]);
+  for (int k = 0; k <= GI_MAX_LAUNCHES && e == hipSuccess; k++) e = hipEventCreate(&c->log.ev[k]);
   if (e != hipSuccess) {
     delete c;
     return GI_ENODEV;
@@ -333,6 +336,8 @@ void gi_ctx_free(gi_ctx* c) {
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : c->log.ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -351,7 +356,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   const uint32_t n = in->n_req;
   // validate spans and lay out per-request scratch (lengths only)
   std::vector<ReqLayout> lay(n);
-  uint64_t off = 0, items_cap = 0, raw_total = 0;
+  uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0;
   uint32_t max_cap_t = 64;
   const uint32_t nslots = c->rs->prog.n_slots;
   const Program& PG = c->rs->prog;
@@ -394,6 +399,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     const uint64_t pre_body_fields = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie);
     items_cap += 2 * pre_body_fields + n_single_items;
     raw_total += (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
+    raw_body += q.body.len;
     max_cap_t = (uint32_t)std::max<uint64_t>(max_cap_t, cap_t);
     ReqLayout& L = lay[r];
     L.pa_base = 0;
@@ -450,7 +456,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       return hip_fail(c, e, "alloc lane scratch");
     if ((e = c->pool.ensure(4ull * c->pool_cap)) != hipSuccess) return hip_fail(c, e, "alloc queue pool");
     if ((e = c->qblk.ensure(8ull * ns * c->qcap)) != hipSuccess) return hip_fail(c, e, "alloc queue blocks");
-    if ((e = c->ctr.ensure(160 + 4ull * ns)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+    if ((e = c->ctr.ensure(160 + 8 * 16)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+    (void)ns;
     if ((e = c->slow.ensure(32ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
   }
@@ -466,6 +473,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   c->ran = false;
   c->stats.last_scratch_bytes = off;
   c->stats.last_pa_bytes = 4ull * c->pool_cap;
+  c->raw_nobody = raw_total;
+  c->raw_all = raw_total + raw_body;
   c->stats.last_stage_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return GI_OK;
@@ -493,7 +502,8 @@ int gi_run_staged(gi_ctx* c) {
   {
     // counters (bytes): [0] pool words used, [8] slow bytes used, [16] slow
     // entries, [64] item buckets {(base, count) x5, item-wave base x5, item
-    // waves}, [128] debug record, [160] qcount[stream] (unused)
+    // waves}, [128] debug record, [160] acct: item bytes per bucket x5, queue
+    // words written per k_stream bucket x5, queue words read per k_scan launch x3
     uint8_t* cp = (uint8_t*)c->ctr.p;
     B.bcounts = (uint32_t*)c->bcounts.p;
     B.boffs = (uint32_t*)c->boffs.p;
@@ -505,7 +515,7 @@ int gi_run_staged(gi_ctx* c) {
     B.pool_cap = c->pool_cap;
     B.pool_used = (unsigned long long*)cp;
     B.qblk = (uint2*)c->qblk.p;
-    B.qcount = (uint32_t*)(cp + 160);
+    B.acct = (unsigned long long*)(cp + 160);
     B.qcap = c->qcap;
     B.slow = c->slow.p;
     B.slow_count = (uint32_t*)(cp + 16);
@@ -532,7 +542,7 @@ int gi_run_staged(gi_ctx* c) {
     e = hipMemsetAsync(c->hits.p, 0, (size_t)c->hit_words * c->n_req * 4, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "memset hits");
   }
-  launch_pipeline(c->prog, B, c->scan, c->stream, c->evs, c->stop_after);
+  launch_pipeline(c->prog, B, c->scan, c->stream, c->evs, c->stop_after, &c->log);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(c, e, "launch pipeline");
   (void)hipEventRecord(c->ev1, c->stream);
@@ -553,6 +563,36 @@ int gi_sync(gi_ctx* c) {
     if (c->n_req && hipEventElapsedTime(&ms, c->evs[0], c->evs[1]) == hipSuccess) c->stats.last_stream_ms = ms;
     if (c->n_req && hipEventElapsedTime(&ms, c->evs[1], c->evs[2]) == hipSuccess) c->stats.last_scan_ms = ms;
     if (c->n_req && hipEventElapsedTime(&ms, c->evs[2], c->ev1) == hipSuccess) c->stats.last_eval_ms = ms;
+    // per-launch HIP-event times and algorithmic bytes
+    uint64_t acct[16] = {0};
+    if (c->ctr.p) (void)hipMemcpy(acct, (uint8_t*)c->ctr.p + 160, 128, hipMemcpyDeviceToHost);
+    uint32_t ibk[16] = {0};
+    if (c->ctr.p) (void)hipMemcpy(ibk, (uint8_t*)c->ctr.p + 64, 64, hipMemcpyDeviceToHost);
+    gi_tally tl{};
+    (void)hipMemcpy(&tl, c->tally.p, sizeof(tl), hipMemcpyDeviceToHost);
+    c->stats.n_launches = (uint32_t)c->log.n;
+    uint64_t slow_bytes = 0;
+    if (c->ctr.p) (void)hipMemcpy(&slow_bytes, (uint8_t*)c->ctr.p + 8, 8, hipMemcpyDeviceToHost);
+    for (int k = 0; k < c->log.n; k++) {
+      float lm = 0;
+      (void)hipEventElapsedTime(&lm, c->log.ev[k], c->log.ev[k + 1]);
+      c->stats.launch_ms[k] = lm;
+      const std::string nm = c->log.name[k];
+      snprintf(c->stats.launch_name[k], sizeof(c->stats.launch_name[k]), "%s", nm.c_str());
+      uint64_t ab = 0;
+      if (nm == "k_collect") ab = c->raw_nobody + 256ull * c->n_req;  // request bytes in, ReqHdr out
+      else if (nm == "k_items") ab = 32ull * (ibk[1] + ibk[3] + ibk[5] + ibk[7] + ibk[9]);  // item records out
+      else if (nm == "k_ioffsets") ab = 8ull * 5 * ((c->n_req + 255) / 256);             // block counts in, offsets out
+      else if (nm.rfind("k_stream", 0) == 0) {
+        const int b = nm.back() - '0';
+        ab = acct[b] + 32ull * ibk[2 * b + 1] + 4ull * acct[5 + b];  // item bytes + records in, queue words out
+      } else if (nm == "k_scan") ab = 4ull * acct[10];
+      else if (nm == "k_scan_big") ab = 4ull * acct[11];
+      else if (nm == "k_scan_hbm") ab = 4ull * acct[12];
+      else if (nm == "k_scan_slow") ab = slow_bytes;
+      else if (nm == "k_eval") ab = c->raw_all + (uint64_t)sizeof(gi_verdict) * c->n_req + 4ull * tl.matched_total;
+      c->stats.launch_alg_bytes[k] = ab;
+    }
 #ifdef GI_DEBUG
     if (c->ctr.p) {
       uint32_t dbg[4];

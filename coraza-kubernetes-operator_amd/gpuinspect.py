@@ -110,7 +110,10 @@ class _Stats(ctypes.Structure):
                 ("last_stage_ms", ctypes.c_double), ("last_scratch_bytes", ctypes.c_uint64),
                 ("last_collect_ms", ctypes.c_double), ("last_scan_ms", ctypes.c_double),
                 ("last_eval_ms", ctypes.c_double), ("last_stream_ms", ctypes.c_double),
-                ("last_pa_bytes", ctypes.c_uint64), ("diag", ctypes.c_uint64 * 8)]
+                ("last_pa_bytes", ctypes.c_uint64), ("diag", ctypes.c_uint64 * 8),
+                ("n_launches", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
+                ("launch_ms", ctypes.c_double * 16), ("launch_alg_bytes", ctypes.c_uint64 * 16),
+                ("launch_name", (ctypes.c_char * 16) * 16)]
 
 
 _LIB = None
@@ -390,8 +393,10 @@ class Engine:
     def stats(self) -> dict:
         s = _Stats()
         self._check(self._lib.gi_stats_get(self._h, ctypes.byref(s)), "gi_stats_get")
-        out = {k: getattr(s, k) for k, _ in _Stats._fields_}
+        out = {k: getattr(s, k) for k, _ in _Stats._fields_ if not k.startswith("launch") and k != "_pad"}
         out["diag"] = list(out["diag"])
+        out["launches"] = [{"name": s.launch_name[k].value.decode(), "ms": s.launch_ms[k],
+                            "alg_bytes": int(s.launch_alg_bytes[k])} for k in range(s.n_launches)]
         return out
 
     def stream(self) -> int:

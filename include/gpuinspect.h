@@ -159,8 +159,12 @@ typedef struct {
   double last_eval_ms;     /* k_eval (phase B: rule interpreter, body, verdicts) */
   double last_stream_ms;   /* k_stream (phase A: filters + transformation chains) */
   uint64_t last_pa_bytes;  /* phase-A arena bytes reserved for the batch */
-  uint64_t diag[8];        /* diagnostic counters of the last batch (GI_DIAG=1): phase-A
-                              arena bytes needed, values, max per-request need, capacity */
+  uint64_t diag[8];        /* diagnostic counters of the last batch (GI_DIAG=1) */
+  uint32_t n_launches;     /* kernel launches of the last pipeline run */
+  uint32_t _pad;
+  double launch_ms[16];    /* HIP-event time of each launch */
+  uint64_t launch_alg_bytes[16]; /* algorithmic bytes each launch must move */
+  char launch_name[16][16];
 } gi_stats;
 
 /* ------------------------------------------------------------ compile */

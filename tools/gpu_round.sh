@@ -11,7 +11,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 gpurun_out/pytest_gpu.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
-timeout -k 10 300 python -u tools/pmc_traffic.py --config c2 --n-req 1000000 --out gpurun_out/traffic_c2.json > gpurun_out/traffic.log 2>&1 || { tail -20 gpurun_out/traffic.log; exit 1; }
+timeout -k 10 400 python -u tools/pmc_traffic.py --config c2 --n-req 1000000 --out gpurun_out/traffic_c2.json > gpurun_out/traffic.log 2>&1 || { tail -20 gpurun_out/traffic.log; exit 1; }
 tail -1 gpurun_out/traffic.log
 timeout -k 10 400 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json

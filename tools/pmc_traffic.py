@@ -40,11 +40,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--n-req", type=int, default=1000000)
-    ap.add_argument("--kernel", default="k_eval")
+    ap.add_argument("--kernel", default="", help="launch name (default: the dominant launch of a bench run)")
     ap.add_argument("--out", default="", help="also write the JSON here (e.g. under gpurun_out/)")
     args = ap.parse_args()
     base = os.path.join(ROOT, "gpurun_out", "traffic")
     os.makedirs(base, exist_ok=True)
+    sys.path.insert(0, ROOT)
+    import bench  # noqa: E402  (launch-name -> rocprof kernel-name map)
+    if not args.kernel:  # the dominant launch of a short bench run
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", args.config, "--n-req",
+                            str(args.n_req), "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
+                           check=True, capture_output=True, text=True)
+        args.kernel = json.loads(r.stdout.strip().splitlines()[-1])["roofline"]["kernel"]
+    launch = args.kernel
+    args.kernel = bench.ROCPROF_NAMES.get(launch, launch)
     fetch = run_pass("FETCH_SIZE", args, os.path.join(base, "fetch"))
     write = run_pass("WRITE_SIZE", args, os.path.join(base, "write"))
     if not fetch or not write:
@@ -54,7 +63,7 @@ def main():
     write.sort()
     f_kb = fetch[len(fetch) // 2]
     w_kb = write[len(write) // 2]
-    out = {"kernel": args.kernel, "config": args.config, "requests": args.n_req,
+    out = {"kernel": launch, "rocprof_kernel": args.kernel, "config": args.config, "requests": args.n_req,
            "fetch_size_kb_raw": f_kb, "write_size_kb": w_kb,
            "hbm_bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
            "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as reported",
