@@ -36,8 +36,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # launch name (gi_stats) -> kernel name as rocprofv3 reports it
 ROCPROF_NAMES = {
     "k_stream0": "k_stream<16u, 20u>", "k_stream1": "k_stream<32u, 36u>", "k_stream2": "k_stream<64u, 68u>",
-    "k_stream3": "k_stream<128u, 132u>", "k_stream4": "k_stream<0u, 0u>", "k_scan": "k_scan<true>",
-    "k_scan_big": "k_scan<true>", "k_scan_hbm": "k_scan<false>",
+    "k_stream3": "k_stream<128u, 132u>", "k_stream4": "k_stream<0u, 0u>", "k_scan": "k_scan<true, false>",
+    "k_scan_big": "k_scan<true, true>", "k_scan_hbm": "k_scan<false, false>",
 }
 
 CONFIGS = {
@@ -132,7 +132,7 @@ def main():
         torch.cuda.synchronize()
     eng.sync()
     kern_ms, stage_ms = [], {"k_collect": [], "k_stream": [], "k_scan": [], "k_eval": []}
-    launch_ms, launch_bytes = {}, {}
+    launch_ms, launch_bytes, launch_steps = {}, {}, {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -145,6 +145,7 @@ def main():
         for ln in st["launches"]:
             launch_ms.setdefault(ln["name"], []).append(ln["ms"])
             launch_bytes[ln["name"]] = ln["alg_bytes"]
+            launch_steps[ln["name"]] = ln["steps"]
     eng.sync()
     if dist is not None:
         torch.cuda.synchronize()
@@ -172,6 +173,11 @@ def main():
     dom = max(avg_launch, key=lambda k: avg_launch[k])
     alg_bytes = launch_bytes[dom]
     achieved = alg_bytes / (avg_launch[dom] * 1e-3) / 1e9
+    # SURVEY.md §8(d) figure: raw request bytes once + verdict record + 4 B per
+    # matched id, over the whole pipeline
+    req_bytes = raw + 16 * batch.n_req + 4 * int(tally["matched_total"])
+    req_gbs = req_bytes / (avg_kern_ms * 1e-3) / 1e9
+    steps_s = launch_steps.get(dom, 0) / (avg_launch[dom] * 1e-3)
     hbm_traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.exists(tpath):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)
@@ -202,6 +208,13 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": hbm_traffic,
                      "kernel": dom, "rocprof_kernel": ROCPROF_NAMES.get(dom, dom),
                      "kernel_ms": round(avg_launch[dom], 4), "alg_bytes_per_launch": int(alg_bytes),
+                     "alg_bytes_def": "bytes the launch must move once: for k_scan, every queue word "
+                                      "(transformed value + 16 B lane header) of its streams read once",
+                     "secondary": {"bound": "valu/lds (automaton steps)", "byte_steps_per_launch": int(launch_steps.get(dom, 0)),
+                                   "byte_steps_per_s": round(steps_s, 1)},
+                     "pipeline_request_bytes": {"def": "SURVEY.md 8(d): raw request bytes + 16 B verdict + 4 B x matched ids",
+                                                "bytes": int(req_bytes), "GB/s": round(req_gbs, 3),
+                                                "frac": round(req_gbs / HBM_PEAK_GBS, 6)},
                      "launches": {k: {"ms": round(v, 4), "alg_bytes": int(launch_bytes[k]),
                                       "GB/s": round(launch_bytes[k] / (v * 1e-3) / 1e9, 2) if v > 0 else None}
                                   for k, v in avg_launch.items()},

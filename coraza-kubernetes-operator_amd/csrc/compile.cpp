@@ -1008,14 +1008,17 @@ struct Lower {
         bool names = false;
         switch (vr.var) {
           case V_ARGS_GET: mask = 1 << FK_ARG_GET; break;
-          case V_ARGS: mask = 1 << FK_ARG_GET; break;  // ARG_POST fields only exist after phase 1
+          // ARG_POST items come from k_collect's speculative body parse
+          case V_ARGS: mask = (1 << FK_ARG_GET) | (1 << FK_ARG_POST); break;
+          case V_ARGS_POST: mask = 1 << FK_ARG_POST; break;
+          case V_ARGS_POST_NAMES: mask = 1 << FK_ARG_POST; names = true; break;
           case V_REQUEST_HEADERS: mask = 1 << FK_HEADER; break;
           case V_REQUEST_COOKIES: mask = 1 << FK_COOKIE; break;
           case V_ARGS_GET_NAMES: mask = 1 << FK_ARG_GET; names = true; break;
-          case V_ARGS_NAMES: mask = 1 << FK_ARG_GET; names = true; break;
+          case V_ARGS_NAMES: mask = (1 << FK_ARG_GET) | (1 << FK_ARG_POST); names = true; break;
           case V_REQUEST_HEADERS_NAMES: mask = 1 << FK_HEADER; names = true; break;
           case V_REQUEST_COOKIES_NAMES: mask = 1 << FK_COOKIE; names = true; break;
-          default: break;  // ARGS_POST*, XML, FILES*: no values before the body phase
+          default: break;  // XML, FILES*: no phase-A values (their processors are not implemented)
         }
         if (!mask) continue;
         f.kind_mask = mask;

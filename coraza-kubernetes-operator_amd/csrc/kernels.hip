@@ -5,7 +5,7 @@
 //              net/url re-encoding of REQUEST_URI) into a per-request field
 //              table in HBM scratch
 //   phase 1  : RuleGroup.Eval(1) -- the rule interpreter below
-//   body     : ProcessRequestBody (URLENCODED -> ARGS_POST)
+//   body     : ProcessRequestBody (URLENCODED / JSON -> ARGS_POST)
 //   phase 2  : RuleGroup.Eval(2)
 //   verdict  : Interruption + matched rule ids + exported TX scores,
 //              block-reduced tallies (one atomic per block per counter)
@@ -712,7 +712,7 @@ struct Tx {
   Str* single;               // ReqHdr::single (per-request, in HBM scratch)
   const uint32_t* hits;      // phase-A hit words [slot/32][n_req]
   uint32_t n_req, req;
-  bool has_post;             // ARGS_POST fields exist (phase-A bits of RF_BODYDEP links void)
+  bool has_post;             // ARGS_POST fields phase A did not see (phase-A bits of RF_BODYDEP links void)
   bool pa_void;              // phase-A arena overflowed: no phase-A bit is trusted
   int64_t (*removed)[2];     // ctl:ruleRemoveById ranges (8, in the request's scratch region)
   uint32_t nremoved;
@@ -795,6 +795,305 @@ __device__ __forceinline__ void parse_query(Tx& t, const uint8_t* q, uint32_t n,
     }
     i = j + 1;
   }
+}
+
+// ------------------------------------------------------------ JSON body
+// coraza internal/bodyprocessors/json.go (readJSON / readItems over
+// tidwall/gjson v1.18.0), restated as one iterative pass per request:
+// ARGS_POST "json.<k1>.<k2>..." (object members unescaped, array indices
+// decimal), strings unescaped, numbers / true / false raw, null "", and a
+// non-empty array's own key = its element count after its elements.  A key
+// written twice is one entry (Go map + ARGS_POST SetIndex(key, 0)) at the
+// first write's position holding the last write's value.
+// Bodies outside RFC 8259, with a scalar root, nested deeper than
+// GI_JSON_MAX_DEPTH, or whose flattened keys + unescaped strings + array
+// counts exceed 4 x body + 1024 bytes (the arena runtime.cpp reserves; deep
+// nesting makes the keys quadratic) are flagged GI_REQ_UNSUPPORTED_BODY
+// (oracle: json_flatten).
+#define GI_JSON_MAX_DEPTH 64
+
+struct JFrame {
+  uint32_t koff, kn;  // the container's own key (offset into t.bytes)
+  uint32_t count;     // members / elements seen
+  uint32_t is_arr;
+};
+
+__device__ inline bool json_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+__device__ inline uint32_t hex4(const uint8_t* s) {
+  return (hexv(s[0]) << 12) | (hexv(s[1]) << 8) | (hexv(s[2]) << 4) | hexv(s[3]);
+}
+
+// Validates the string whose opening quote is at s[i]; returns the index
+// after the closing quote (0 on error) and whether it holds escapes.
+__device__ uint32_t json_string_end(const uint8_t* s, uint32_t n, uint32_t i, bool* esc) {
+  *esc = false;
+  i++;
+  while (i < n) {
+    const uint8_t c = s[i];
+    if (c == '"') return i + 1;
+    if (c < 0x20) return 0;
+    if (c == '\\') {
+      if (i + 1 >= n) return 0;
+      const uint8_t e = s[i + 1];
+      *esc = true;
+      if (e == 'u') {
+        if (i + 6 > n || !ishex(s[i + 2]) || !ishex(s[i + 3]) || !ishex(s[i + 4]) || !ishex(s[i + 5])) return 0;
+        i += 6;
+        continue;
+      }
+      if (e != '"' && e != '\\' && e != '/' && e != 'b' && e != 'f' && e != 'n' && e != 'r' && e != 't') return 0;
+      i += 2;
+      continue;
+    }
+    i++;
+  }
+  return 0;
+}
+
+__device__ inline uint32_t utf8_put(uint32_t r, uint8_t* d) {
+  if ((r >= 0xD800 && r <= 0xDFFF) || r > 0x10FFFF) r = 0xFFFD;
+  if (r < 0x80) { d[0] = (uint8_t)r; return 1; }
+  if (r < 0x800) { d[0] = 0xC0 | (r >> 6); d[1] = 0x80 | (r & 0x3F); return 2; }
+  if (r < 0x10000) {
+    d[0] = 0xE0 | (r >> 12); d[1] = 0x80 | ((r >> 6) & 0x3F); d[2] = 0x80 | (r & 0x3F);
+    return 3;
+  }
+  d[0] = 0xF0 | (r >> 18); d[1] = 0x80 | ((r >> 12) & 0x3F); d[2] = 0x80 | ((r >> 6) & 0x3F); d[3] = 0x80 | (r & 0x3F);
+  return 4;
+}
+
+// gjson unescape of a validated string body; never longer than its input.
+__device__ uint32_t json_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
+  uint32_t o = 0, i = 0;
+  while (i < n) {
+    const uint8_t c = s[i];
+    if (c != '\\') {
+      d[o++] = c;
+      i++;
+      continue;
+    }
+    const uint8_t e = s[i + 1];
+    if (e != 'u') {
+      d[o++] = e == 'b' ? 8 : e == 'f' ? 12 : e == 'n' ? 10 : e == 'r' ? 13 : e == 't' ? 9 : e;
+      i += 2;
+      continue;
+    }
+    uint32_t r = hex4(s + i + 2);
+    i += 6;
+    if (r >= 0xD800 && r < 0xE000) {  // utf16.IsSurrogate: consume a following \uXXXX
+      if (n - i >= 6 && s[i] == '\\' && s[i + 1] == 'u') {
+        const uint32_t r2 = hex4(s + i + 2);
+        i += 6;
+        r = (r < 0xDC00 && r2 >= 0xDC00 && r2 < 0xE000) ? 0x10000 + ((r - 0xD800) << 10) + (r2 - 0xDC00) : 0xFFFD;
+      } else {
+        r = 0xFFFD;
+      }
+    }
+    o += utf8_put(r, d + o);
+  }
+  return o;
+}
+
+// gjson validnumber at s[i]; returns the end index (0 on error).
+__device__ uint32_t json_number_end(const uint8_t* s, uint32_t n, uint32_t i) {
+  if (i < n && s[i] == '-') i++;
+  if (i >= n || s[i] < '0' || s[i] > '9') return 0;
+  if (s[i] == '0') {
+    i++;
+  } else {
+    while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+  }
+  if (i < n && s[i] == '.') {
+    i++;
+    if (i >= n || s[i] < '0' || s[i] > '9') return 0;
+    while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+  }
+  if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+    i++;
+    if (i < n && (s[i] == '+' || s[i] == '-')) i++;
+    if (i >= n || s[i] < '0' || s[i] > '9') return 0;
+    while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+  }
+  return i;
+}
+
+__device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+// Fold repeated keys of fields [f0, t.nf) (first position, last value) with
+// an open-addressing table in the transform scratch t.t1.
+__device__ __noinline__ void json_fold_keys(Tx& t, uint32_t f0) {
+  const uint32_t nf = t.nf - f0;
+  const uint32_t tsize = t.cap_t / 4;  // > body/2 + 2 >= nf (runtime.cpp sizing)
+  if (nf < 2) return;
+  if (nf >= tsize) {
+    t.flags |= GI_REQ_OVERFLOW;
+    return;
+  }
+  uint32_t* tab = (uint32_t*)t.t1;
+  for (uint32_t k = 0; k < tsize; k++) tab[k] = 0;
+  bool any = false;
+  for (uint32_t i = f0; i < t.nf; i++) {
+    Field& f = t.fields[i];
+    uint32_t h = gi_fnv1a(f.k, f.kn, false) % tsize;
+    while (true) {
+      const uint32_t e = tab[h];
+      if (e == 0) {
+        tab[h] = i + 1;
+        break;
+      }
+      Field& g = t.fields[e - 1];
+      if (g.kn == f.kn && bytes_equal(g.k, f.k, f.kn)) {
+        g.v = f.v;
+        g.vn = f.vn;
+        f.kind = 0;  // folded into g
+        any = true;
+        break;
+      }
+      h = h + 1 == tsize ? 0 : h + 1;
+    }
+  }
+  if (!any) return;
+  uint32_t o = f0;
+  for (uint32_t i = f0; i < t.nf; i++)
+    if (t.fields[i].kind) t.fields[o++] = t.fields[i];
+  t.nf = o;
+}
+
+__device__ __noinline__ void parse_json_body(Tx& t, const uint8_t* s, uint32_t n) {
+  const uint32_t f0 = t.nf;
+  JFrame* st = (JFrame*)tx_alloc(t, (GI_JSON_MAX_DEPTH + 1) * sizeof(JFrame) + 8);
+  if (!st) return;
+  st = (JFrame*)(((uintptr_t)st + 7) & ~(uintptr_t)7);
+  uint8_t* root = tx_alloc(t, 4);
+  if (!root) return;
+  root[0] = 'j'; root[1] = 's'; root[2] = 'o'; root[3] = 'n';
+  uint32_t i = 0;
+  while (i < n && json_ws(s[i])) i++;
+  if (i >= n || (s[i] != '{' && s[i] != '[')) {
+    t.flags |= GI_REQ_UNSUPPORTED_BODY;
+    return;
+  }
+  uint32_t d = 1;
+  st[0] = {(uint32_t)(root - t.bytes), 4, 0, s[i] == '[' ? 1u : 0u};
+  const uint64_t lim = 4ull * n + 1024;
+  uint64_t jb = 0;  // flattened bytes (keys, unescaped strings, counts)
+  i++;
+  bool bad = false;
+  while (d > 0 && !bad && !(t.flags & GI_REQ_ERROR_MASK)) {
+    JFrame& F = st[d - 1];
+    while (i < n && json_ws(s[i])) i++;
+    if (i >= n) { bad = true; break; }
+    if (s[i] == (F.is_arr ? ']' : '}')) {
+      i++;
+      if (F.is_arr && F.count) {
+        uint8_t* nb = tx_alloc(t, 12);
+        if (!nb) return;
+        const uint32_t dn = go_itoa((int64_t)F.count, nb);
+        t.nb -= 12 - dn;
+        jb += dn;
+        if (jb > lim) { bad = true; break; }
+        add_field(t, FK_ARG_POST, t.bytes + F.koff, F.kn, nb, dn);
+      }
+      d--;
+      continue;
+    }
+    if (F.count) {
+      if (s[i] != ',') { bad = true; break; }
+      i++;
+      while (i < n && json_ws(s[i])) i++;
+    }
+    // the element's key: parent key + '.' + member name / index
+    uint8_t* key;
+    uint32_t kn;
+    if (F.is_arr) {
+      key = tx_alloc(t, F.kn + 12);
+      if (!key) return;
+      for (uint32_t k = 0; k < F.kn; k++) key[k] = t.bytes[F.koff + k];
+      key[F.kn] = '.';
+      kn = F.kn + 1 + go_itoa((int64_t)F.count, key + F.kn + 1);
+      t.nb -= F.kn + 12 - kn;  // give back the unused tail
+      jb += kn;
+      if (jb > lim) { bad = true; break; }
+    } else {
+      if (i >= n || s[i] != '"') { bad = true; break; }
+      bool esc;
+      const uint32_t e = json_string_end(s, n, i, &esc);
+      if (!e) { bad = true; break; }
+      const uint32_t rn = e - i - 2;
+      key = tx_alloc(t, F.kn + 1 + rn);
+      if (!key) return;
+      for (uint32_t k = 0; k < F.kn; k++) key[k] = t.bytes[F.koff + k];
+      key[F.kn] = '.';
+      uint32_t sn = rn;
+      if (esc) {
+        sn = json_unescape(s + i + 1, rn, key + F.kn + 1);
+      } else {
+        for (uint32_t k = 0; k < rn; k++) key[F.kn + 1 + k] = s[i + 1 + k];
+      }
+      kn = F.kn + 1 + sn;
+      t.nb -= rn - sn;
+      jb += kn;
+      if (jb > lim) { bad = true; break; }
+      i = e;
+      while (i < n && json_ws(s[i])) i++;
+      if (i >= n || s[i] != ':') { bad = true; break; }
+      i++;
+      while (i < n && json_ws(s[i])) i++;
+    }
+    F.count++;
+    if (i >= n) { bad = true; break; }
+    const uint8_t c = s[i];
+    if (c == '{' || c == '[') {
+      if (d >= GI_JSON_MAX_DEPTH) { bad = true; break; }
+      st[d++] = {(uint32_t)(key - t.bytes), kn, 0, c == '[' ? 1u : 0u};
+      i++;
+    } else if (c == '"') {
+      bool esc;
+      const uint32_t e = json_string_end(s, n, i, &esc);
+      if (!e) { bad = true; break; }
+      const uint32_t rn = e - i - 2;
+      if (esc) {
+        uint8_t* v = tx_alloc(t, rn);
+        if (!v && rn) return;
+        const uint32_t vn = json_unescape(s + i + 1, rn, v);
+        t.nb -= rn - vn;
+        jb += vn;
+        if (jb > lim) { bad = true; break; }
+        add_field(t, FK_ARG_POST, key, kn, v, vn);
+      } else {
+        add_field(t, FK_ARG_POST, key, kn, s + i + 1, rn);
+      }
+      i = e;
+    } else if (c == 't' || c == 'f' || c == 'n') {
+      const uint32_t ln = c == 'f' ? 5 : 4;
+      const char* lit = c == 't' ? "true" : c == 'f' ? "false" : "null";
+      if (i + ln > n) { bad = true; break; }
+      for (uint32_t k = 0; k < ln; k++)
+        if (s[i + k] != (uint8_t)lit[k]) bad = true;
+      if (bad) break;
+      add_field(t, FK_ARG_POST, key, kn, s + i, c == 'n' ? 0 : ln);
+      i += ln;
+    } else {
+      const uint32_t e = json_number_end(s, n, i);
+      if (!e) { bad = true; break; }
+      add_field(t, FK_ARG_POST, key, kn, s + i, e - i);
+      i = e;
+    }
+  }
+  if (!bad && d == 0) {
+    while (i < n && json_ws(s[i])) i++;
+    bad = i != n;
+  }
+  if (bad || d != 0) {
+    t.flags |= GI_REQ_UNSUPPORTED_BODY;
+    return;
+  }
+  if (!(t.flags & GI_REQ_ERROR_MASK)) json_fold_keys(t, f0);
 }
 
 // net/url shouldEscape(c, encodePath)
@@ -967,6 +1266,12 @@ __device__ inline bool starts_ci(const uint8_t* s, uint32_t n, const char* lit) 
   for (; lit[i]; i++)
     if (i >= n || alower(s[i]) != (uint8_t)lit[i]) return false;
   return true;
+}
+
+__device__ inline bool contains_ci(const uint8_t* s, uint32_t n, const char* lit) {
+  for (uint32_t i = 0; i < n; i++)
+    if (starts_ci(s + i, n - i, lit)) return true;
+  return false;
 }
 
 // ------------------------------------------------------------ TX / macros
@@ -1505,7 +1810,9 @@ struct ReqHdr {
   uint16_t n_get, n_hdr, n_ck, flags;
   uint8_t body_proc;
   uint8_t pa_void;      // phase-A arena overflowed: k_eval ignores the hit bits
-  uint8_t _pad[6];
+  uint8_t spec_proc;    // body processor k_collect parsed the body with (BP_NONE: none)
+  uint8_t _pad;
+  uint32_t n_post;      // its ARG_POST fields, after the phase-1 fields (phase-A items)
   Str single[S_COUNT];
 };
 static_assert(sizeof(ReqHdr) <= 256, "ReqHdr must fit its 256-byte slot");
@@ -1646,9 +1953,9 @@ __device__ __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H
     const uint32_t sg = __ffs(m) - 1;
     f((uint8_t)0, (uint8_t)sg, 0u, (uint32_t)0xFFFFFFFFu, H->single[sg].n);
   }
-  const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck;
-  for (uint32_t i = 0; i < n_get + n_hdr + n_ck; i++) {
-    const uint8_t kind = i < n_get ? FK_ARG_GET : i < n_get + n_hdr ? FK_HEADER : FK_COOKIE;
+  const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck, n_pre = n_get + n_hdr + n_ck;
+  for (uint32_t i = 0; i < n_pre + H->n_post; i++) {
+    const uint8_t kind = i < n_get ? FK_ARG_GET : i < n_get + n_hdr ? FK_HEADER : i < n_pre ? FK_COOKIE : FK_ARG_POST;
     const uint8_t sides = P.item_sides[kind];
     const Field fl = Fd[i];
     if (sides & 1) f(kind, (uint8_t)0, 0u, i, fl.vn);
@@ -1717,13 +2024,48 @@ __device__ void collect_request(const DProgram& P, const DBatch& B, uint32_t r) 
   }
   ReqHdr* H = g.hdr;
   H->nf = t.nf;
-  H->nb = t.nb;
   H->n_get = (uint16_t)n_get;
   H->n_hdr = (uint16_t)n_hdr;
   H->n_ck = (uint16_t)(t.nf - n_get - n_hdr);
   H->flags = t.flags | ((t.nf > 0xFFFF) ? GI_REQ_OVERFLOW : 0);
   H->body_proc = t.body_proc;
   H->pa_void = 0;
+  // Speculative ProcessRequestBody so phase A also scans ARGS_POST: the
+  // processor Content-Type implies (Coraza's own URLENCODED default, or JSON
+  // for a "json" media type as the CRS ctl:requestBodyProcessor rules pick
+  // it).  The fields sit after the phase-1 fields; k_eval uses them (and
+  // trusts the hit bits of links that read ARGS_POST) only if phase 1 ends
+  // with the same processor, and parses the body itself otherwise.
+  uint8_t sp = BP_NONE;
+  const uint32_t bn = rq.body.len;
+  if (ok && P.body_access && bn > 0 && bn <= P.body_limit && !(t.flags & GI_REQ_ERROR_MASK)) {
+    sp = t.body_proc;
+    if (sp == BP_NONE) {
+      for (uint32_t h = 0; h < rq.hdr_count && sp == BP_NONE; h++) {
+        const gi_header hd = B.headers[rq.hdr_begin + h];
+        if (hd.name.len == 12 && starts_ci(D + hd.name.off, 12, "content-type") &&
+            contains_ci(D + hd.value.off, hd.value.len, "json"))
+          sp = BP_JSON;
+      }
+    }
+    if (sp == BP_URLENCODED || sp == BP_JSON) {
+      const uint32_t nf0 = t.nf, nb0 = t.nb;
+      const uint16_t fl0 = t.flags;
+      if (sp == BP_URLENCODED) parse_query(t, D + rq.body.off, bn, FK_ARG_POST);
+      else parse_json_body(t, D + rq.body.off, bn);
+      if (t.flags != fl0) {  // not parsable as guessed: k_eval decides
+        t.nf = nf0;
+        t.nb = nb0;
+        t.flags = fl0;
+        sp = BP_NONE;
+      }
+    } else {
+      sp = BP_NONE;
+    }
+  }
+  H->spec_proc = sp;
+  H->n_post = t.nf - H->nf;
+  H->nb = t.nb;
 }
 
 // ProcessURI + AddRequestHeader* for one request per thread, then the
@@ -2322,10 +2664,13 @@ __device__ __forceinline__ void scan_qblock(const DProgram& P, const DBatch& B, 
 // Each wave reads 64 entries of its job's stream list (one per lane) and scans
 // the non-empty ones one after the other.  LDS: the job image is copied once
 // per job change; !LDS: the image is read from HBM (automata too large for LDS).
-template <bool LDS>
+// BIG: the 1-workgroup-per-CU launch of images above 64 KB (its own symbol,
+// so per-kernel profiles keep the two launches apart).
+template <bool LDS, bool BIG>
 __global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint32_t* __restrict__ jl, uint32_t n_jl,
                                                uint32_t mode, uint32_t acct_slot) {
-  uint64_t rwords = 0;  // queue words this wave read (algorithmic-byte accounting)
+  uint64_t rwords = 0;  // queue words of this launch's streams, each counted once (algorithmic bytes)
+  uint64_t rsteps = 0;  // automaton byte-steps (padded words x 4 x automata of the job)
   extern __shared__ __attribute__((aligned(16))) uint8_t simg[];
   __shared__ uint2 clist[1024];
   __shared__ uint32_t wcnt[16];
@@ -2385,14 +2730,19 @@ __global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint3
         if (d.multi) umask |= 1u << k;
       }
     }
+    // jl is sorted by stream: only the first job of a stream counts its words
+    const bool first = jj == 0 || gi_cload(P.jobs, jl[jj - 1]).stream != J.stream;
     for (uint32_t i = wv; i < total; i += nwv) {
       const uint2 d = clist[i];
-      rwords += (uint64_t)(d.y & 0xFFu) * (4 + (d.y >> 8));
+      const uint64_t w = (uint64_t)(d.y & 0xFFu) * (4 + (d.y >> 8));
+      rwords += first ? w : 0;
+      rsteps += (uint64_t)(d.y & 0xFFu) * (d.y >> 8) * 4 * K;
       scan_qblock(P, B, J, img, K, trn, st0, umask, nf, d, mode);
     }
     __syncthreads();  // clist / wcnt reuse
   }
   if ((threadIdx.x & 63) == 0 && rwords) atomicAdd(&B.acct[10 + acct_slot], (unsigned long long)rwords);
+  if ((threadIdx.x & 63) == 0 && rsteps) atomicAdd(&B.acct[13 + acct_slot], (unsigned long long)rsteps);
 }
 
 // Slow values (non-ASCII / "maybe"), one thread per list entry: every job of
@@ -2477,11 +2827,16 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
               t.body_proc = BP_URLENCODED;
               t.single[S_REQBODY_PROCESSOR] = {CS_URLENCODED, 10};
             }
-            if (t.body_proc == BP_URLENCODED) {
+            if (t.body_proc == BP_URLENCODED || t.body_proc == BP_JSON) {
               t.single[S_REQUEST_BODY] = {D + rq.body.off, bn};
-              const uint32_t nf0 = t.nf;
-              parse_query(t, D + rq.body.off, bn, FK_ARG_POST);
-              t.has_post = t.nf > nf0;
+              if (t.body_proc == H->spec_proc) {
+                t.nf += H->n_post;  // k_collect's fields, already in phase A
+              } else {
+                const uint32_t nf0 = t.nf;
+                if (t.body_proc == BP_URLENCODED) parse_query(t, D + rq.body.off, bn, FK_ARG_POST);
+                else parse_json_body(t, D + rq.body.off, bn);
+                t.has_post = t.nf > nf0;
+              }
             } else if (t.body_proc != BP_NONE) {
               t.flags |= GI_REQ_UNSUPPORTED_BODY;
             }
@@ -2537,8 +2892,12 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
 }
 
 void scan_allow_lds(uint32_t lds_bytes) {
-  if (lds_bytes > 65536)
-    (void)hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  if (lds_bytes > 65536) {
+    (void)hipFuncSetAttribute((const void*)k_scan<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_bytes);
+    (void)hipFuncSetAttribute((const void*)k_scan<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_bytes);
+  }
 }
 
 uint32_t scan_resident_blocks(uint32_t lds_bytes) {
@@ -2547,7 +2906,7 @@ uint32_t scan_resident_blocks(uint32_t lds_bytes) {
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, dev);
   int per_cu = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scan<true>, 1024, lds_bytes);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scan<true, false>, 1024, lds_bytes);
   if (per_cu < 1) per_cu = 1;
   return (uint32_t)prop.multiProcessorCount * (uint32_t)per_cu;
 }
@@ -2590,10 +2949,16 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
     if (ev) (void)hipEventRecord(ev[1], stream);
     for (int big = 0; big < 2; big++)
       if (S.n_jobs[big])
-        GI_LAUNCH(big ? "k_scan_big" : "k_scan", k_scan<true>, dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P,
-                  B, S.jobs[big], S.n_jobs[big], S.mode, (uint32_t)big);
+      {
+        if (big)
+          GI_LAUNCH("k_scan_big", (k_scan<true, true>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
+                    S.jobs[big], S.n_jobs[big], S.mode, 1u);
+        else
+          GI_LAUNCH("k_scan", (k_scan<true, false>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
+                    S.jobs[big], S.n_jobs[big], S.mode, 0u);
+      }
     if (S.n_global)
-      GI_LAUNCH("k_scan_hbm", k_scan<false>, dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
+      GI_LAUNCH("k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
                 S.n_global, S.mode, 2u);
     GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
   } else if (ev) {

@@ -297,6 +297,9 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   const bool force_hbm = getenv("GI_SCAN_HBM") && atoi(getenv("GI_SCAN_HBM")) > 0;  // debugging
   for (uint32_t j = 0; j < P.jobs.size(); j++)
     jl[(force_hbm || !P.jobs[j].lds) ? 2 : P.jobs[j].big ? 1 : 0].push_back(j);
+  // by stream, so k_scan can count each stream's queue words once per launch
+  for (auto& l : jl)
+    std::stable_sort(l.begin(), l.end(), [&](uint32_t a, uint32_t b) { return P.jobs[a].stream < P.jobs[b].stream; });
   std::vector<uint32_t> all(jl[0]);
   all.insert(all.end(), jl[1].begin(), jl[1].end());
   all.insert(all.end(), jl[2].begin(), jl[2].end());
@@ -356,7 +359,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   const uint32_t n = in->n_req;
   // validate spans and lay out per-request scratch (lengths only)
   std::vector<ReqLayout> lay(n);
-  uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0;
+  uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0;
   uint32_t max_cap_t = 64;
   const uint32_t nslots = c->rs->prog.n_slots;
   const Program& PG = c->rs->prog;
@@ -388,8 +391,29 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
         }
       }
     }
-    uint64_t cap_f = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie) + (q.body.len / 2 + 2);
+    // ARGS_POST fields a body can yield: urlencoded <= '&' + 1; JSON <=
+    // ',' + 2 '[' + '{' + 1 (elements past the first of a container need a
+    // comma, and each non-empty array adds its own count entry)
+    uint64_t post_fields = 0;
+    if (q.body.len) {
+      const uint8_t* bd = in->data + q.body.off;
+      uint64_t seps = 0;
+      for (uint32_t k = 0; k < q.body.len; k++) {
+        const uint8_t ch = bd[k];
+        seps += (ch == '&') + (ch == ',') + 2 * (ch == '[') + (ch == '{');
+      }
+      post_fields = std::min<uint64_t>(seps + 2, q.body.len / 2 + 2);
+    }
+    uint64_t cap_f = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie) + post_fields;
     uint64_t cap_b = 4ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96;
+    {  // a JSON-looking body: room for the flattened "json.a.b" keys + parser stack
+      const uint8_t* bd = in->data + q.body.off;
+      uint32_t k = 0;
+      while (k < q.body.len && (bd[k] == ' ' || bd[k] == '\t' || bd[k] == '\n' || bd[k] == '\r')) k++;
+      // kernels.hip parse_json_body: flattened bytes <= 4n + 1024, one
+      // transient allocation <= that again + n, parser stack 1048 B
+      if (k < q.body.len && (bd[k] == '{' || bd[k] == '[')) cap_b += 8ull * q.body.len + 4200;
+    }
     uint64_t cap_t = 3 * maxv + 64;
     uint64_t cap_mt = 2 * maxv + 512;
     if (cap_f > 0xFFFFFFFFull || cap_b > 0xFFFFFFFFull || cap_t > 0xFFFFFFFFull || cap_mt > 0xFFFFFFFFull)
@@ -397,7 +421,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     // phase-A items: at most both sides of every field (GET args, headers,
     // cookies; POST args appear after phase 1) plus the filtered singles
     const uint64_t pre_body_fields = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie);
-    items_cap += 2 * pre_body_fields + n_single_items;
+    items_cap += 2 * (pre_body_fields + (PG.body_access ? post_fields : 0)) + n_single_items;
+    post_total += PG.body_access ? post_fields : 0;
     raw_total += (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
     raw_body += q.body.len;
     max_cap_t = (uint32_t)std::max<uint64_t>(max_cap_t, cap_t);
@@ -445,9 +470,10 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     const uint64_t waves = (uint64_t)GI_STREAM_GRID * 5;
     c->qcap = (uint32_t)std::min<uint64_t>(c->items_cap / 64 + 8, 0xFFFFFFFull);  // item-waves
     const double pf = pool_factor_env();
-    c->pool_cap = std::min<uint64_t>((uint64_t)(pf * (1024.0 * n + 8.0 * raw_total)) + waves * GI_PCHUNK + 4096,
-                                     0xFFFFFFF0ull);
-    c->slow_cap = (uint32_t)std::min<uint64_t>(4ull * n + 4096, 0x7FFFFFFFull);
+    c->pool_cap = std::min<uint64_t>(
+        (uint64_t)(pf * (1024.0 * n + 8.0 * raw_total + 4.0 * raw_body + 64.0 * post_total)) + waves * GI_PCHUNK + 4096,
+        0xFFFFFFF0ull);
+    c->slow_cap = (uint32_t)std::min<uint64_t>(4ull * n + 4096 + post_total / 4, 0x7FFFFFFFull);
     c->slow_bytes_cap = 64ull * c->slow_cap;
     if ((e = c->bcounts.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc bcounts");
     if ((e = c->boffs.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc boffs");
@@ -586,12 +612,13 @@ int gi_sync(gi_ctx* c) {
       else if (nm.rfind("k_stream", 0) == 0) {
         const int b = nm.back() - '0';
         ab = acct[b] + 32ull * ibk[2 * b + 1] + 4ull * acct[5 + b];  // item bytes + records in, queue words out
-      } else if (nm == "k_scan") ab = 4ull * acct[10];
+      } else if (nm == "k_scan") ab = 4ull * acct[10];  // each stream's queue words once
       else if (nm == "k_scan_big") ab = 4ull * acct[11];
       else if (nm == "k_scan_hbm") ab = 4ull * acct[12];
       else if (nm == "k_scan_slow") ab = slow_bytes;
       else if (nm == "k_eval") ab = c->raw_all + (uint64_t)sizeof(gi_verdict) * c->n_req + 4ull * tl.matched_total;
       c->stats.launch_alg_bytes[k] = ab;
+      c->stats.launch_steps[k] = nm == "k_scan" ? acct[13] : nm == "k_scan_big" ? acct[14] : nm == "k_scan_hbm" ? acct[15] : 0;
     }
 #ifdef GI_DEBUG
     if (c->ctr.p) {

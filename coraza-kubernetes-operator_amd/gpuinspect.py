@@ -113,7 +113,7 @@ class _Stats(ctypes.Structure):
                 ("last_pa_bytes", ctypes.c_uint64), ("diag", ctypes.c_uint64 * 8),
                 ("n_launches", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
                 ("launch_ms", ctypes.c_double * 16), ("launch_alg_bytes", ctypes.c_uint64 * 16),
-                ("launch_name", (ctypes.c_char * 16) * 16)]
+                ("launch_name", (ctypes.c_char * 16) * 16), ("launch_steps", ctypes.c_uint64 * 16)]
 
 
 _LIB = None
@@ -396,7 +396,8 @@ class Engine:
         out = {k: getattr(s, k) for k, _ in _Stats._fields_ if not k.startswith("launch") and k != "_pad"}
         out["diag"] = list(out["diag"])
         out["launches"] = [{"name": s.launch_name[k].value.decode(), "ms": s.launch_ms[k],
-                            "alg_bytes": int(s.launch_alg_bytes[k])} for k in range(s.n_launches)]
+                            "alg_bytes": int(s.launch_alg_bytes[k]), "steps": int(s.launch_steps[k])}
+                           for k in range(s.n_launches)]
         return out
 
     def stream(self) -> int:

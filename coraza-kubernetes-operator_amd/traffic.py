@@ -5,7 +5,9 @@ Seed 0xC0A2A, numpy PCG64.  C1/C2: GET requests, path from 20 templates,
 [1, 256] over URL-safe ASCII with ~15 % percent-escapes), ~10 browser-like
 headers (~600 B incl. a Cookie with 0-4 pairs), 5 % of requests carry an
 attack payload in a random argument.  C3 adds 50 % POST requests with
-4-64 KB application/x-www-form-urlencoded bodies.
+4-64 KB bodies: 60 % application/x-www-form-urlencoded, 40 % application/json
+(objects nested to depth <= 4: strings -- 15 % with JSON escapes --, numbers,
+booleans, nulls, arrays).
 
 Produces the packed gi_batch layout directly (gpuinspect.pack_parts) so a
 million requests build in seconds.
@@ -82,11 +84,86 @@ def _quote(s: bytes, full: bool) -> bytes:
     return bytes(out)
 
 
+JSON_ESCAPES = [b"\\u00e9", b"\\n", b"\\\"", b"\\\\", b"\\/", b"\\t", b"\\u20ac", b"\\ud83d\\ude00", b"%2F", b"%C3%A9"]
+N_SUBTREES = 2048
+
+
+def json_quote(b: bytes) -> bytes:
+    """A JSON string literal for raw bytes (ASCII payloads)."""
+    out = bytearray(b'"')
+    for c in b:
+        if c == 0x22 or c == 0x5C:
+            out += b"\\" + bytes([c])
+        elif c < 0x20:
+            out += b"\\u%04x" % c
+        else:
+            out.append(c)
+    out += b'"'
+    return bytes(out)
+
+
 class TrafficGen:
     def __init__(self, seed: int = SEED):
         self.rng = np.random.Generator(np.random.PCG64(seed))
         self.pool = URLSAFE[self.rng.integers(0, len(URLSAFE), 1 << 22)].tobytes()
         self.kpool = KEYCHARS[self.rng.integers(0, len(KEYCHARS), 1 << 20)].tobytes()
+        self._subtrees = None
+
+    def _jkey(self):
+        rng = self.rng
+        o = int(rng.integers(0, len(self.kpool) - 16))
+        return self.kpool[o:o + int(rng.integers(3, 13))]
+
+    def _jscalar(self):
+        rng = self.rng
+        r = rng.random()
+        if r < 0.55:
+            n = int(np.clip(rng.lognormal(2.5, 0.8), 1, 256))
+            o = int(rng.integers(0, len(self.pool) - 260))
+            v = self.pool[o:o + n]
+            if rng.random() < 0.15:
+                v = v[: n // 2] + JSON_ESCAPES[int(rng.integers(0, len(JSON_ESCAPES)))] + v[n // 2:]
+            return b'"' + v + b'"'
+        if r < 0.8:
+            if rng.random() < 0.7:
+                return str(int(rng.integers(-100000, 1000000))).encode()
+            return b"%.3f" % float(rng.normal(0, 1000))
+        if r < 0.9:
+            return b"true" if rng.random() < 0.5 else b"false"
+        return b"null"
+
+    def _jvalue(self, depth):
+        rng = self.rng
+        r = rng.random()
+        if depth < 4 and r < 0.3:
+            n = int(rng.integers(1, 6))
+            return b"{" + b",".join(b'"' + self._jkey() + b'":' + self._jvalue(depth + 1) for _ in range(n)) + b"}"
+        if depth < 4 and r < 0.45:
+            n = int(rng.integers(0, 8))
+            return b"[" + b",".join(self._jvalue(depth + 1) for _ in range(n)) + b"]"
+        return self._jscalar()
+
+    def _json_body(self, attack: bool):
+        """{"<key>_<i>": subtree, ...} up to a log-uniform 4-64 KB; the
+        subtrees (depth <= 3 below the root object: <= 4 levels) come from a seeded pool."""
+        rng = self.rng
+        if self._subtrees is None:
+            self._subtrees = [self._jvalue(1) for _ in range(N_SUBTREES)]
+        target = int(np.exp(rng.uniform(np.log(4096), np.log(65536))))
+        picks = rng.integers(0, N_SUBTREES, 1 + target // 40)
+        members = []
+        size = 2
+        for i, p in enumerate(picks):
+            m = b'"' + self._jkey() + b"_%d" % i + b'":' + self._subtrees[int(p)]
+            members.append(m)
+            size += len(m) + 1
+            if size >= target:
+                break
+        if attack:
+            pay = ATTACKS[int(rng.integers(0, len(ATTACKS)))]
+            k = int(rng.integers(0, len(members) + 1))
+            members.insert(k, b'"' + self._jkey() + b'":{"' + self._jkey() + b'":' + json_quote(pay) + b"}")
+        return b"{" + b",".join(members) + b"}"
 
     def _args(self, n_args, attack_at):
         rng = self.rng
@@ -138,7 +215,7 @@ class TrafficGen:
         t = PATHS[int(rng.integers(0, len(PATHS)))]
         return t % int(rng.integers(1, 100000)) if b"%d" in t else t
 
-    def gen(self, n: int, post_frac: float = 0.0, attack_rate: float = 0.05):
+    def gen(self, n: int, post_frac: float = 0.0, attack_rate: float = 0.05, json_frac: float = 0.4):
         """Return (parts, nh) for gpuinspect.pack_parts."""
         rng = self.rng
         parts = []
@@ -158,11 +235,12 @@ class TrafficGen:
                 # an attack request carries its payload in the query (above)
                 # or, half of the time, in one body argument instead
                 body_attack = bool(attack[i]) and rng.random() < 0.5
-                body = self._urlencoded_body(body_attack)
+                is_json = rng.random() < json_frac
+                body = self._json_body(body_attack) if is_json else self._urlencoded_body(body_attack)
                 parts += [b"POST", uri, b"HTTP/1.1", body]
                 k = self._headers(parts, path)
-                parts += [b"Content-Type", b"application/x-www-form-urlencoded", b"Content-Length",
-                          str(len(body)).encode()]
+                ctype = b"application/json" if is_json else b"application/x-www-form-urlencoded"
+                parts += [b"Content-Type", ctype, b"Content-Length", str(len(body)).encode()]
                 nh[i] = k + 2
             else:
                 parts += [b"GET", uri, b"HTTP/1.1", b""]
@@ -185,8 +263,9 @@ class TrafficGen:
             body = b"&".join(chunks[:k] + [self._args(1, 0)] + chunks[k:])[:target + 300]
         return body
 
-    def batch(self, n: int, post_frac: float = 0.0, attack_rate: float = 0.05) -> "gpuinspect.PackedBatch":
-        parts, nh = self.gen(n, post_frac, attack_rate)
+    def batch(self, n: int, post_frac: float = 0.0, attack_rate: float = 0.05,
+              json_frac: float = 0.4) -> "gpuinspect.PackedBatch":
+        parts, nh = self.gen(n, post_frac, attack_rate, json_frac)
         return gpuinspect.pack_parts(parts, nh)
 
 

@@ -51,7 +51,7 @@ extern "C" {
 
 /* per-request verdict flags (gi_verdict.flags) */
 #define GI_REQ_UNSUPPORTED_URI 0x1   /* request-target outside the supported forms */
-#define GI_REQ_UNSUPPORTED_BODY 0x2  /* body processor not implemented (JSON/XML/MULTIPART) */
+#define GI_REQ_UNSUPPORTED_BODY 0x2  /* body processor not implemented (XML/MULTIPART) or JSON outside RFC 8259 */
 #define GI_REQ_BODY_LIMIT 0x4        /* body over SecRequestBodyLimit */
 #define GI_REQ_OVERFLOW 0x8          /* internal per-request capacity exceeded */
 #define GI_REQ_MATCH_TRUNC 0x10      /* more matched rules than matched_cap */
@@ -165,6 +165,7 @@ typedef struct {
   double launch_ms[16];    /* HIP-event time of each launch */
   uint64_t launch_alg_bytes[16]; /* algorithmic bytes each launch must move */
   char launch_name[16][16];
+  uint64_t launch_steps[16];     /* automaton byte-steps of each k_scan launch (secondary bound) */
 } gi_stats;
 
 /* ------------------------------------------------------------ compile */

@@ -1168,6 +1168,218 @@ def parse_cookies(value: bytes):
 # ---------------------------------------------------------------------------
 
 
+JSON_MAX_DEPTH = 64  # engine limit (gjson itself recurses without one): deeper -> UnsupportedInput
+
+
+def JSON_FLAT_LIMIT(n: int) -> int:
+    """Engine limit on flattened JSON bytes (kernels.hip parse_json_body)."""
+    return 4 * n + 1024
+_JSON_WS = b" \t\n\r"
+_JSON_SIMPLE_ESC = {0x22: 0x22, 0x5C: 0x5C, 0x2F: 0x2F, 0x62: 0x08, 0x66: 0x0C, 0x6E: 0x0A, 0x72: 0x0D, 0x74: 0x09}
+
+
+def _utf8(r: int) -> bytes:
+    """Go utf8.EncodeRune (surrogates and out-of-range -> U+FFFD)."""
+    if 0xD800 <= r <= 0xDFFF or r > 0x10FFFF:
+        r = 0xFFFD
+    return chr(r).encode("utf-8")
+
+
+def _json_unescape(raw: bytes) -> bytes:
+    """[upstream tidwall/gjson v1.18.0 unescape] on a validated string body.
+
+    A \\uXXXX in the surrogate range consumes a directly following \\uXXXX
+    and decodes the pair with utf16.DecodeRune (U+FFFD unless high+low);
+    a lone surrogate encodes as U+FFFD."""
+    out = bytearray()
+    i, n = 0, len(raw)
+    while i < n:
+        c = raw[i]
+        if c != 0x5C:
+            out.append(c)
+            i += 1
+            continue
+        e = raw[i + 1]
+        if e != 0x75:
+            out.append(_JSON_SIMPLE_ESC[e])
+            i += 2
+            continue
+        r = int(raw[i + 2:i + 6], 16)
+        i += 6
+        if 0xD800 <= r < 0xE000:
+            if n - i >= 6 and raw[i] == 0x5C and raw[i + 1] == 0x75:
+                r2 = int(raw[i + 2:i + 6], 16)
+                i += 6
+                if 0xD800 <= r < 0xDC00 and 0xDC00 <= r2 < 0xE000:
+                    r = 0x10000 + ((r - 0xD800) << 10) + (r2 - 0xDC00)
+                else:
+                    r = 0xFFFD
+            else:
+                r = 0xFFFD
+        out += _utf8(r)
+    return bytes(out)
+
+
+class _JsonInvalid(Exception):
+    pass
+
+
+class _JsonReader:
+    """RFC 8259 recursive-descent reader (the grammar gjson.Valid accepts)."""
+
+    def __init__(self, s: bytes):
+        self.s = s
+        self.i = 0
+
+    def ws(self):
+        s, i = self.s, self.i
+        while i < len(s) and s[i] in _JSON_WS:
+            i += 1
+        self.i = i
+
+    def peek(self) -> int:
+        if self.i >= len(self.s):
+            raise _JsonInvalid()
+        return self.s[self.i]
+
+    def expect(self, c: int):
+        if self.peek() != c:
+            raise _JsonInvalid()
+        self.i += 1
+
+    def string(self) -> bytes:
+        """Returns the unescaped contents of the string at self.i (sets
+        self.escaped)."""
+        self.expect(0x22)
+        s, start = self.s, self.i
+        i, esc = start, False
+        while True:
+            if i >= len(s):
+                raise _JsonInvalid()
+            c = s[i]
+            if c == 0x22:
+                break
+            if c < 0x20:
+                raise _JsonInvalid()
+            if c == 0x5C:
+                esc = True
+                if i + 1 >= len(s):
+                    raise _JsonInvalid()
+                e = s[i + 1]
+                if e == 0x75:
+                    h = s[i + 2:i + 6]
+                    if len(h) != 4 or not all(_ishex(x) for x in h):
+                        raise _JsonInvalid()
+                    i += 6
+                    continue
+                if e not in _JSON_SIMPLE_ESC:
+                    raise _JsonInvalid()
+                i += 2
+                continue
+            i += 1
+        self.i = i + 1
+        raw = s[start:i]
+        self.escaped = esc
+        return _json_unescape(raw) if esc else raw
+
+    def number(self) -> bytes:
+        s, start = self.s, self.i
+        m = re.compile(rb"-?(?:0|[1-9][0-9]*)(?:\.[0-9]+)?(?:[eE][+-]?[0-9]+)?").match(s, start)
+        if m is None or m.end() == start:
+            raise _JsonInvalid()
+        self.i = m.end()
+        return s[start:self.i]
+
+
+def json_flatten(body: bytes):
+    """[upstream coraza internal/bodyprocessors/json.go readJSON/readItems].
+
+    ARGS_POST entries of a JSON request body, in the order readItems writes
+    them into its result map: "json" + ".key" (object member, unescaped) or
+    ".N" (array index) per level; strings unescaped, numbers / true / false
+    as their raw text, null as ""; a non-empty array also writes its own
+    key = element count after its elements.  Coraza then copies the Go map
+    into ARGS_POST (case-sensitive keys, as MAP_VARS above) with
+    SetIndex(key, 0, value) in (random) map order; this engine fixes the
+    order to the first write of a key, holding the last value written.
+    Returns None where this engine flags the body unsupported: not valid
+    JSON, a scalar at the root, nesting deeper than JSON_MAX_DEPTH, or more
+    than 4 x len(body) + 1024 flattened bytes (every element's key, every
+    string value that held escapes, every array count)."""
+    rd = _JsonReader(body)
+    res: Dict[bytes, Tuple[bytes, bytes]] = {}
+    flat = [0]
+
+    def put(key: bytes, val: bytes):
+        res[key] = (key, val)
+
+    def value(key: bytes, depth: int):
+        c = rd.peek()
+        if c == 0x7B or c == 0x5B:
+            container(key, depth + 1)
+        elif c == 0x22:
+            v = rd.string()
+            if rd.escaped:
+                flat[0] += len(v)
+            put(key, v)
+        elif c == 0x74 or c == 0x66 or c == 0x6E:
+            for lit in (b"true", b"false", b"null"):
+                if rd.s.startswith(lit, rd.i):
+                    rd.i += len(lit)
+                    put(key, b"" if lit == b"null" else lit)
+                    return
+            raise _JsonInvalid()
+        else:
+            put(key, rd.number())
+
+    def container(key: bytes, depth: int):
+        if depth > JSON_MAX_DEPTH:
+            raise _JsonInvalid()
+        is_arr = rd.peek() == 0x5B
+        close = 0x5D if is_arr else 0x7D
+        rd.i += 1
+        count = 0
+        rd.ws()
+        if rd.peek() == close:
+            rd.i += 1
+            return
+        while True:
+            rd.ws()
+            if is_arr:
+                sub = key + b"." + str(count).encode()
+            else:
+                name = rd.string()
+                rd.ws()
+                rd.expect(0x3A)
+                rd.ws()
+                sub = key + b"." + name
+            flat[0] += len(sub)
+            value(sub, depth)
+            count += 1
+            rd.ws()
+            c = rd.peek()
+            rd.i += 1
+            if c == close:
+                break
+            if c != 0x2C:
+                raise _JsonInvalid()
+        if is_arr:
+            put(key, str(count).encode())
+            flat[0] += len(str(count))
+
+    try:
+        rd.ws()
+        if rd.peek() not in (0x7B, 0x5B):
+            return None
+        container(b"json", 1)
+        rd.ws()
+        if rd.i != len(body) or flat[0] > JSON_FLAT_LIMIT(len(body)):
+            return None
+    except (_JsonInvalid, RecursionError):
+        return None
+    return list(res.values())
+
+
 def go_atoi(s: bytes):
     """strconv.Atoi -> (value, ok)."""
     m = re.fullmatch(rb"[+-]?[0-9]+", s)
@@ -1518,6 +1730,14 @@ class Transaction:
             if rbp == b"URLENCODED":
                 self.single["REQUEST_BODY"] = self.body
                 self.maps["ARGS_POST"] = parse_query(self.body)
+            elif rbp == b"JSON":
+                # [upstream json.go ProcessRequest]: ARGS_POST from readJSON,
+                # the raw body kept as REQUEST_BODY
+                args = json_flatten(self.body)
+                if args is None:
+                    raise UnsupportedInput("JSON body outside the supported grammar")
+                self.single["REQUEST_BODY"] = self.body
+                self.maps["ARGS_POST"] = args
             elif rbp == b"":
                 pass
             else:
