@@ -46,8 +46,8 @@ CONFIGS = {
            "CRS-shaped v4 PL1 ruleset (rulesets/crs_pl1.conf) x 1M synthetic GET with query args"),
     "c1": ("tests/golden/samples_ruleset.conf", 10_000, 0.0,
            "config/samples RuleSet x 10k synthetic GET"),
-    "c3": ("rulesets/crs_pl1.conf", 100_000, 0.5,
-           "CRS-shaped v4 PL1 x mixed GET/POST (4-64 KB urlencoded bodies)"),
+    "c3": ("rulesets/crs_pl1.conf", 50_000, 0.5,
+           "CRS-shaped v4 PL1 x mixed GET/POST (50% POST, 4-64 KB bodies: 60% urlencoded, 40% JSON)"),
 }
 
 

@@ -1397,7 +1397,21 @@ struct Lower {
     actions(r, &d);
     d.hit_slot = plan(r, d, &d.flags);
     P->rules.push_back(d);
-    return (uint32_t)P->rules.size() - 1;
+    const uint32_t idx = (uint32_t)P->rules.size() - 1;
+    if (d.hit_slot >= 0 && (d.flags & RF_RESIDUAL) && d.phase >= 2 && d.op >= 0)
+      for (uint32_t vi = 0; vi < d.var_count; vi++)
+        if (P->vars[d.var_begin + vi].var == S_REQUEST_BODY && P->vars[d.var_begin + vi].residual) {
+          P->body_links.push_back(idx);
+          std::stable_sort(P->body_links.begin(), P->body_links.end(), [&](uint32_t a, uint32_t b) {
+            const DRule &x = P->rules[a], &y = P->rules[b];
+            return std::lexicographical_compare(P->tchains.begin() + x.tchain_off,
+                                                P->tchains.begin() + x.tchain_off + x.tchain_len,
+                                                P->tchains.begin() + y.tchain_off,
+                                                P->tchains.begin() + y.tchain_off + y.tchain_len);
+          });
+          break;
+        }
+    return idx;
   }
 };
 

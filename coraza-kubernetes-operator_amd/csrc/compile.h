@@ -32,6 +32,7 @@ struct Program {
   std::vector<uint8_t> sfilt;        // per stream filter: global filter id
   uint8_t item_sides[8] = {0};       // per FieldKind: bit0 value side, bit1 key side is filtered
   uint32_t item_singles = 0;         // single variables some filter reads (1 << SingleId)
+  std::vector<uint32_t> body_links;    // phase>=2 phase-A links with a residual REQUEST_BODY target (k_body)
   std::vector<uint32_t> always_slots;  // hit slots without an automaton image (always set)
   std::vector<DJob> jobs;
   std::vector<DJobDfa> jdfas;

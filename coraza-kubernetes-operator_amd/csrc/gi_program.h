@@ -427,6 +427,8 @@ struct DProgram {
   const uint8_t* images;        // LDS images of the jobs
   const uint32_t* sfilt;        // per stream filter: global filter id (filters[] is global)
   const uint32_t* always_slots; // hit slots without an automaton image
+  const uint32_t* body_links;   // links k_body tests on the speculative REQUEST_BODY
+  uint32_t n_body_links;
   uint32_t n_always;
   uint32_t n_gfilters;
   uint32_t item_singles;        // singles some filter reads (1 << SingleId)

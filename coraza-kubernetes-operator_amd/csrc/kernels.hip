@@ -40,7 +40,7 @@ struct Slot {
   uint32_t state;  // 0 unset, 1 integer (canonical decimal), 2 string
 };
 
-__device__ __constant__ uint8_t kConstStrs[] = "0\0URLENCODED\0JSON\0XML\0MULTIPART\0";
+__device__ __constant__ uint8_t kConstStrs[] = "0\0URLENCODED\0JSON\0XML\0MULTIPART\0\0\0\0\0\0\0\0";  // padded for load_u32u
 #define CS_ZERO (kConstStrs + 0)
 #define CS_URLENCODED (kConstStrs + 2)
 #define CS_JSON (kConstStrs + 13)
@@ -175,6 +175,17 @@ __device__ inline uint32_t encode_rune(uint32_t r, uint8_t* o) {
   return 4;
 }
 
+// Four bytes at p (any alignment) from two aligned dword loads: long values
+// are read a word per load instead of a byte per load.  May read up to 7
+// bytes past p (every buffer is padded: runtime.cpp).
+__device__ __forceinline__ uint32_t load_u32u(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t lo = w[0];
+  return sh ? __builtin_amdgcn_alignbyte(w[1], lo, sh) : lo;
+}
+
 // --------------------------------------------------------------- DFA scan
 // Sticky-accept DFA over rune classes (rune mode: Go UTF-8 decoding) or
 // bytes (phrase automata).  fold: ASCII-lowercase bytes before the lookup.
@@ -185,17 +196,29 @@ __device__ bool dfa_match(const DProgram& P, int32_t id, const uint8_t* s, uint3
   const uint32_t ncls = d.n_classes;
   uint32_t st = d.start;
   uint32_t i = 0;
+  uint32_t win = 0, wbeg = 0, wend = 0;  // s[wbeg, wend) in win
   if (d.byte_mode) {
     while (i < n) {
       if (st == d.accept) return true;
-      uint8_t c = s[i++];
+      if (i >= wend) {
+        win = load_u32u(s + i);
+        wbeg = i;
+        wend = i + 4;
+      }
+      uint8_t c = (uint8_t)(win >> (8 * (i - wbeg)));
+      i++;
       if (fold) c = alower(c);
       st = tr[st * ncls + amap[c]];
     }
   } else {
     while (i < n) {
       if (st == d.accept) return true;
-      uint8_t c = s[i];
+      if (i >= wend) {
+        win = load_u32u(s + i);
+        wbeg = i;
+        wend = i + 4;
+      }
+      uint8_t c = (uint8_t)(win >> (8 * (i - wbeg)));
       uint32_t cls;
       if (c < 0x80) {
         if (fold) c = alower(c);
@@ -244,11 +267,23 @@ __device__ uint32_t lower_rune(const DProgram& P, uint32_t r) {
 // Go strings.ToLower
 __device__ int64_t t_lowercase(const DProgram& P, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   bool ascii = true;
-  for (uint32_t i = 0; i < n; i++)
-    if (s[i] >= 0x80) { ascii = false; break; }
+  for (uint32_t i = 0; i < n && ascii; i += 4) {
+    uint32_t x = load_u32u(s + i);
+    if (n - i < 4) x &= (1u << (8 * (n - i))) - 1u;
+    ascii = !(x & 0x80808080u);
+  }
   if (ascii) {
     if (n > cap) return -1;
-    for (uint32_t i = 0; i < n; i++) d[i] = alower(s[i]);
+    if (!((uintptr_t)d & 3) && ((n + 3) & ~3u) <= cap) {  // SWAR: ASCII 'A'-'Z' | 0x20, a word at a time
+      for (uint32_t i = 0; i < n; i += 4) {
+        const uint32_t x = load_u32u(s + i);
+        const uint32_t ge_a = (x & 0x7F7F7F7Fu) + 0x3F3F3F3Fu;  // bit 7: byte >= 'A'
+        const uint32_t gt_z = (x & 0x7F7F7F7Fu) + 0x25252525u;  // bit 7: byte > 'Z'
+        *(uint32_t*)(d + i) = x | (((ge_a ^ gt_z) & ~x & 0x80808080u) >> 2);
+      }
+    } else {
+      for (uint32_t i = 0; i < n; i++) d[i] = alower(s[i]);
+    }
     return n;
   }
   uint32_t o = 0, i = 0;
@@ -684,7 +719,13 @@ __device__ __noinline__ int64_t apply_transform(const DProgram& P, uint8_t code,
 
 __device__ uint32_t value_summary(const uint8_t* s, uint32_t n) {
   uint32_t m = 0;
-  for (uint32_t i = 0; i < n; i++) m |= byte_summary(s[i]);
+  uint32_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    const uint32_t x = load_u32u(s + i);
+    m |= byte_summary((uint8_t)x) | byte_summary((uint8_t)(x >> 8)) | byte_summary((uint8_t)(x >> 16)) |
+         byte_summary((uint8_t)(x >> 24));
+  }
+  for (; i < n; i++) m |= byte_summary(s[i]);
   return m;
 }
 // the same through a 256-entry table (k_stream keeps it in LDS)
@@ -713,6 +754,7 @@ struct Tx {
   const uint32_t* hits;      // phase-A hit words [slot/32][n_req]
   uint32_t n_req, req;
   bool has_post;             // ARGS_POST fields phase A did not see (phase-A bits of RF_BODYDEP links void)
+  bool body_spec;            // the body went through k_collect's processor: k_body tested REQUEST_BODY
   bool pa_void;              // phase-A arena overflowed: no phase-A bit is trusted
   int64_t (*removed)[2];     // ctl:ruleRemoveById ranges (8, in the request's scratch region)
   uint32_t nremoved;
@@ -774,24 +816,44 @@ __device__ uint32_t query_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
   return o;
 }
 
-// coraza internal/url ParseQuery(query, '&') -> fields of `kind`
+// coraza internal/url ParseQuery(query, '&') -> fields of `kind`.  A key or
+// value without '%' / '+' is its own decoding: the field points into the
+// request bytes, and only escaped parts are decoded into the arena.
 __device__ __forceinline__ void parse_query(Tx& t, const uint8_t* q, uint32_t n, uint8_t kind) {
   uint32_t i = 0;
   while (i < n) {
-    uint32_t j = i;
-    while (j < n && q[j] != '&') j++;
+    uint32_t j = i, e = 0xFFFFFFFFu;
+    bool kesc = false, vesc = false;
+    for (; j < n; j++) {
+      const uint8_t c = q[j];
+      if (c == '&') break;
+      if (c == '=' && e == 0xFFFFFFFFu) e = j;
+      else if (c == '%' || c == '+') (e == 0xFFFFFFFFu ? kesc : vesc) = true;
+    }
     if (j > i) {
-      uint32_t e = i;
-      while (e < j && q[e] != '=') e++;
+      if (e == 0xFFFFFFFFu) e = j;
       const uint8_t* k = q + i;
-      uint32_t kn = e - i;
+      const uint32_t kn = e - i;
       const uint8_t* v = q + (e < j ? e + 1 : j);
-      uint32_t vn = e < j ? j - e - 1 : 0;
-      uint8_t* dk = tx_alloc(t, kn + vn);
-      if (!dk) return;
-      uint32_t dkn = query_unescape(k, kn, dk);
-      uint32_t dvn = query_unescape(v, vn, dk + dkn);
-      add_field(t, kind, dk, dkn, dk + dkn, dvn);
+      const uint32_t vn = e < j ? j - e - 1 : 0;
+      const uint8_t* dk = k;
+      uint32_t dkn = kn;
+      const uint8_t* dv = v;
+      uint32_t dvn = vn;
+      if (kesc || vesc) {
+        uint8_t* d = tx_alloc(t, (kesc ? kn : 0) + (vesc ? vn : 0));
+        if (!d) return;
+        if (kesc) {
+          dkn = query_unescape(k, kn, d);
+          dk = d;
+          d += dkn;
+        }
+        if (vesc) {
+          dvn = query_unescape(v, vn, d);
+          dv = d;
+        }
+      }
+      add_field(t, kind, dk, dkn, dv, dvn);
     }
     i = j + 1;
   }
@@ -1632,6 +1694,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
       for (uint32_t vi = 0; vi < R.var_count && !any; vi++) {
         const DVarRef vr = gi_cload(P.vars, R.var_begin + vi);
         if (!vr.residual) continue;
+        if (vr.var == S_REQUEST_BODY && t.body_spec && R.phase >= 2) continue;  // k_body's bit
         bool ok;
         const Str sv = t.single[vr.var];
         const Str tv = transform(t, R, sv.p, sv.n, &ok);
@@ -1929,6 +1992,10 @@ __device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
 }
 
 #define GI_NB 5  // item length buckets: <=16, <=32, <=64, <=128, >128 bytes
+// qblk entry {pool word offset, nv | nw << 8 | shared}: shared = the block was
+// written for an earlier stream of the same item-wave (raw item bytes)
+#define GI_QB_SHARED 0x80000000u
+#define GI_QB_NW_MASK 0x7FFFFFu
 __device__ __forceinline__ uint32_t item_bucket(uint32_t n) {
   return n <= 16 ? 0u : n <= 32 ? 1u : n <= 64 ? 2u : n <= 128 ? 3u : 4u;
 }
@@ -2364,6 +2431,13 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
     const uint32_t blk = iw_base + w0 / 64;
     const uint64_t c_b = B.prof ? clock64() : 0;
     pc_item += c_b - c_a;
+    // Blocks whose every value left its chain unchanged hold the raw item
+    // bytes: a later stream with the same lane set points its qblk entry at
+    // the earlier block instead of writing it again (the lane header carries
+    // the stream-independent filter mask gm; each job's fmask table ignores
+    // filters of other streams).
+    uint64_t rom0 = 0, rom1 = 0;
+    uint32_t rq0 = 0, rq1 = 0, rw0 = 0, rw1 = 0;
     for (uint32_t s = 0; s < P.n_streams; s++) {
       const uint64_t c_s0 = B.prof ? clock64() : 0;
       const DStream S = gi_cload(P.streams, s);
@@ -2436,9 +2510,16 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
       }
       const uint32_t nv = __popcll(om);
       const uint32_t nw = wave_max(out ? ((uint32_t)cn + 3) / 4 : 0u);
-      const uint64_t words = (uint64_t)nv * (4 + nw);
+      const bool raw = __ballot(out && cur != src) == 0;  // every output is the staged item
+      if (raw && (om == rom0 || om == rom1)) {
+        if (lane == 0 && blk < B.qcap)
+          B.qblk[(uint64_t)s * B.qcap + blk] = om == rom0 ? make_uint2(rw0, rq0) : make_uint2(rw1, rq1);
+        continue;
+      }
+      // blocks start on 16-byte cells: qblk holds the cell index (64 GB of pool)
+      const uint64_t words = ((uint64_t)nv * (4 + nw) + 3) & ~3ull;
       unsigned long long woff = 0;
-      wwords += words;
+      wwords += (uint64_t)nv * (4 + nw);
       if (lane == 0) {
         if (pnext + words > pend) {
           const unsigned long long sz = words > GI_PCHUNK ? words : (unsigned long long)GI_PCHUNK;
@@ -2455,13 +2536,17 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
         if (lane == 0 && blk < B.qcap) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2(0u, 0u);
         continue;
       }
-      if (lane == 0) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2((uint32_t)woff, nv | (nw << 8));
+      if (lane == 0) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2((uint32_t)(woff >> 2), nv | (nw << 8));
+      if (raw) {  // remember it (two most recent lane sets)
+        rom1 = rom0, rq1 = rq0, rw1 = rw0;
+        rom0 = om, rq0 = nv | (nw << 8) | GI_QB_SHARED, rw0 = (uint32_t)(woff >> 2);
+      }
       if (out) {
         const uint32_t i = mask_rank(om);
         uint32_t* q = B.pool + woff;
         q[i] = it.req;
-        q[nv + i] = (uint32_t)fm;
-        q[2 * nv + i] = (uint32_t)(fm >> 32);
+        q[nv + i] = (uint32_t)gm;
+        q[2 * nv + i] = (uint32_t)(gm >> 32);
         q[3 * nv + i] = (uint32_t)cn;
         const uint32_t nwi = ((uint32_t)cn + 3) / 4;
         for (uint32_t w = 0; w < nwi; w++) {
@@ -2618,9 +2703,10 @@ __device__ __forceinline__ void scan_qblock(const DProgram& P, const DBatch& B, 
                                             uint32_t K, const uint32_t* trn, const uint32_t* st0, uint32_t umask,
                                             uint32_t nf, uint2 d, uint32_t mode) {
   const uint32_t lane = lane_id();
-  const uint32_t woff = d.x, nv = d.y & 0xFFu, nw = d.y >> 8;
+  const uint64_t woff = (uint64_t)d.x << 2;
+  const uint32_t nv = d.y & 0xFFu, nw = (d.y >> 8) & GI_QB_NW_MASK;
   if (nv == 0) return;
-  GI_BOUND(nv <= 64 && (uint64_t)woff + (uint64_t)(4 + nw) * nv <= B.pool_cap, woff, d.y);
+  GI_BOUND(nv <= 64 && woff + (uint64_t)(4 + nw) * nv <= B.pool_cap, d.x, d.y);
   const uint32_t* q = B.pool + woff;
   uint32_t req = 0, len = 0;
   uint64_t fm = 0;
@@ -2734,15 +2820,63 @@ __global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint3
     const bool first = jj == 0 || gi_cload(P.jobs, jl[jj - 1]).stream != J.stream;
     for (uint32_t i = wv; i < total; i += nwv) {
       const uint2 d = clist[i];
-      const uint64_t w = (uint64_t)(d.y & 0xFFu) * (4 + (d.y >> 8));
-      rwords += first ? w : 0;
-      rsteps += (uint64_t)(d.y & 0xFFu) * (d.y >> 8) * 4 * K;
+      const uint32_t dnw = (d.y >> 8) & GI_QB_NW_MASK;
+      const uint64_t w = (uint64_t)(d.y & 0xFFu) * (4 + dnw);
+      rwords += (first && !(d.y & GI_QB_SHARED)) ? w : 0;  // a shared block is counted at its writer
+      rsteps += (uint64_t)(d.y & 0xFFu) * dnw * 4 * K;
       scan_qblock(P, B, J, img, K, trn, st0, umask, nf, d, mode);
     }
     __syncthreads();  // clist / wcnt reuse
   }
   if ((threadIdx.x & 63) == 0 && rwords) atomicAdd(&B.acct[10 + acct_slot], (unsigned long long)rwords);
   if ((threadIdx.x & 63) == 0 && rsteps) atomicAdd(&B.acct[13 + acct_slot], (unsigned long long)rsteps);
+}
+
+// REQUEST_BODY targets of phase-2 links (residual: the variable only exists
+// after ProcessRequestBody), tested on the speculative body of k_collect: one
+// thread per (request, link), side-effect free (transformation chain +
+// operator), a match or a chain overflow sets the link's hit bit.  k_eval
+// relies on these bits only when phase 1 ended with k_collect's processor
+// (REQUEST_BODY is then exactly the body).
+__global__ void __launch_bounds__(256) k_body(DProgram P, DBatch B) {
+  // request-major (the body stays in cache across links; the lanes of a wave
+  // walk the same link list); a link whose chain equals the previous one's
+  // reuses its output (compile.cpp orders body_links by chain)
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B.n_req) return;
+  const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
+  if (H->spec_proc == BP_NONE || (H->flags & GI_REQ_ERROR_MASK)) return;
+  const Region g = region_of(P, B, r);
+  Tx t;
+  t.P = &P;
+  t.t0 = g.t0;
+  t.t1 = g.t1;
+  t.cap_t = g.cap_t;
+  const gi_span bs = B.reqs[r].body;
+  Str tv{nullptr, 0};
+  bool ok = true;
+  uint32_t prev_off = 0xFFFFFFFFu, prev_len = 0;
+  for (uint32_t k = 0; k < P.n_body_links; k++) {
+    const DRule R = gi_cload(P.rules, (uint64_t)P.body_links[k]);
+    const DOp o = gi_cload(P.ops, (uint64_t)R.op);
+    const uint64_t c0 = B.prof ? clock64() : 0;
+    bool same = R.tchain_len == prev_len;
+    for (uint32_t q = 0; same && q < R.tchain_len; q++)
+      same = P.tchains[R.tchain_off + q] == P.tchains[prev_off + q];
+    if (!same) {
+      t.flags = 0;
+      tv = transform(t, R, B.data + bs.off, bs.len, &ok);
+      prev_off = R.tchain_off;
+      prev_len = R.tchain_len;
+    }
+    const uint64_t c1 = B.prof ? clock64() : 0;
+    const bool hit = !ok || eval_op(t, o, tv.p, tv.n);
+    if (hit) set_hit(B, (uint32_t)R.hit_slot, r);
+    if (B.prof && k < 16) {  // GI_PROF: cycles per link (transform, operator)
+      atomicAdd(&B.prof[96 + 2 * k], (unsigned long long)(c1 - c0));
+      atomicAdd(&B.prof[97 + 2 * k], (unsigned long long)(clock64() - c1));
+    }
+  }
 }
 
 // Slow values (non-ASCII / "maybe"), one thread per list entry: every job of
@@ -2783,6 +2917,7 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
     t.req = r;
     t.slots = B.txslots + r;
     t.has_post = false;
+    t.body_spec = false;
     t.pa_void = H->pa_void != 0;
     t.nf = H->nf;
     t.nb = H->nb;
@@ -2831,6 +2966,7 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
               t.single[S_REQUEST_BODY] = {D + rq.body.off, bn};
               if (t.body_proc == H->spec_proc) {
                 t.nf += H->n_post;  // k_collect's fields, already in phase A
+                t.body_spec = true;
               } else {
                 const uint32_t nf0 = t.nf;
                 if (t.body_proc == BP_URLENCODED) parse_query(t, D + rq.body.off, bn, FK_ARG_POST);
@@ -2961,6 +3097,7 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
       GI_LAUNCH("k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
                 S.n_global, S.mode, 2u);
     GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
+    if (P.n_body_links) GI_LAUNCH("k_body", k_body, dim3((B.n_req + 255) / 256), dim3(256), 0, stream, P, B);
   } else if (ev) {
     (void)hipEventRecord(ev[1], stream);
   }

@@ -259,6 +259,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   UP(sfilt, sfilt32, uint32_t)
   UP(tchains32, tch32, uint32_t)
   UP(always_slots, P.always_slots, uint32_t)
+  UP(body_links, P.body_links, uint32_t)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
@@ -287,6 +288,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
     return GI_EINVAL;
   }
   c->prog.n_always = (uint32_t)P.always_slots.size();
+  c->prog.n_body_links = (uint32_t)P.body_links.size();
   c->prog.n_gfilters = (uint32_t)P.filters.size();
   c->prog.item_singles = P.item_singles;
   for (int k = 0; k < 8; k++) c->prog.item_sides[k] = P.item_sides[k];
@@ -441,12 +443,13 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   }
   hipError_t e = hipSuccess;
   hipStream_t s = c->stream;
-  if ((e = c->data.ensure(std::max<uint64_t>(in->data_len, 16))) != hipSuccess) return hip_fail(c, e, "alloc data");
+  // +16: word-granular readers may touch up to 7 bytes past a value's end
+  if ((e = c->data.ensure(std::max<uint64_t>(in->data_len + 16, 16))) != hipSuccess) return hip_fail(c, e, "alloc data");
   if ((e = c->reqs.ensure(std::max<size_t>(n * sizeof(gi_request), 16))) != hipSuccess) return hip_fail(c, e, "alloc reqs");
   if ((e = c->hdrs.ensure(std::max<size_t>(in->n_headers * sizeof(gi_header), 16))) != hipSuccess)
     return hip_fail(c, e, "alloc headers");
   if ((e = c->layout.ensure(std::max<size_t>(n * sizeof(ReqLayout), 16))) != hipSuccess) return hip_fail(c, e, "alloc layout");
-  if ((e = c->scratch.ensure(std::max<uint64_t>(off, 64))) != hipSuccess) return hip_fail(c, e, "alloc scratch");
+  if ((e = c->scratch.ensure(std::max<uint64_t>(off + 64, 64))) != hipSuccess) return hip_fail(c, e, "alloc scratch");
   if ((e = c->verdicts.ensure(std::max<size_t>(n * sizeof(gi_verdict), 16))) != hipSuccess)
     return hip_fail(c, e, "alloc verdicts");
   if ((e = c->matched.ensure(std::max<size_t>((size_t)n * c->mcap * 4, 16))) != hipSuccess)
@@ -471,21 +474,21 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     c->qcap = (uint32_t)std::min<uint64_t>(c->items_cap / 64 + 8, 0xFFFFFFFull);  // item-waves
     const double pf = pool_factor_env();
     c->pool_cap = std::min<uint64_t>(
-        (uint64_t)(pf * (1024.0 * n + 8.0 * raw_total + 4.0 * raw_body + 64.0 * post_total)) + waves * GI_PCHUNK + 4096,
-        0xFFFFFFF0ull);
+        (uint64_t)(pf * (1024.0 * n + 8.0 * raw_total + (post_total ? 24.0 * raw_body : 0.0))) + waves * GI_PCHUNK + 4096,
+        0x3FFFFFFF0ull);  // qblk cell indices: 2^32 x 16 B
     c->slow_cap = (uint32_t)std::min<uint64_t>(4ull * n + 4096 + post_total / 4, 0x7FFFFFFFull);
     c->slow_bytes_cap = 64ull * c->slow_cap;
     if ((e = c->bcounts.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc bcounts");
     if ((e = c->boffs.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc boffs");
     if ((e = c->items.ensure(32ull * c->items_cap)) != hipSuccess) return hip_fail(c, e, "alloc items");
-    if ((e = c->lscratch.ensure((uint64_t)GI_STREAM_GRID * 64 * 2 * c->lcap)) != hipSuccess)
+    if ((e = c->lscratch.ensure((uint64_t)GI_STREAM_GRID * 64 * 2 * c->lcap + 64)) != hipSuccess)
       return hip_fail(c, e, "alloc lane scratch");
     if ((e = c->pool.ensure(4ull * c->pool_cap)) != hipSuccess) return hip_fail(c, e, "alloc queue pool");
     if ((e = c->qblk.ensure(8ull * ns * c->qcap)) != hipSuccess) return hip_fail(c, e, "alloc queue blocks");
     if ((e = c->ctr.ensure(160 + 8 * 16)) != hipSuccess) return hip_fail(c, e, "alloc counters");
     (void)ns;
     if ((e = c->slow.ensure(32ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
-    if ((e = c->slow_bytes.ensure(c->slow_bytes_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
+    if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
   }
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && n) e = hipMemcpyAsync(c->reqs.p, in->reqs, n * sizeof(gi_request), hipMemcpyHostToDevice, s);
@@ -616,6 +619,7 @@ int gi_sync(gi_ctx* c) {
       else if (nm == "k_scan_big") ab = 4ull * acct[11];
       else if (nm == "k_scan_hbm") ab = 4ull * acct[12];
       else if (nm == "k_scan_slow") ab = slow_bytes;
+      else if (nm == "k_body") ab = c->raw_all - c->raw_nobody;  // request bodies
       else if (nm == "k_eval") ab = c->raw_all + (uint64_t)sizeof(gi_verdict) * c->n_req + 4ull * tl.matched_total;
       c->stats.launch_alg_bytes[k] = ab;
       c->stats.launch_steps[k] = nm == "k_scan" ? acct[13] : nm == "k_scan_big" ? acct[14] : nm == "k_scan_hbm" ? acct[15] : 0;
@@ -637,6 +641,12 @@ int gi_sync(gi_ctx* c) {
         for (int b = 0; b < 5; b++)
           fprintf(stderr, "GI_PROF k_stream bucket %d: fm+ballot %.1f run_chain(lane max) %.1f slowcheck+collapse %.1f\n", b,
                   h[80 + 3 * b] / 1e6, h[81 + 3 * b] / 1e6, h[82 + 3 * b] / 1e6);
+        for (uint32_t k = 0; k < 16 && k < c->rs->prog.body_links.size(); k++) {
+          const DRule& R = c->rs->prog.rules[c->rs->prog.body_links[k]];
+          fprintf(stderr, "GI_PROF k_body link %u id %d chain %u op %d: transform %.1f Mcyc, operator %.1f Mcyc (sum)\n",
+                  c->rs->prog.body_links[k], R.id, R.tchain_len, c->rs->prog.ops[R.op].kind, h[96 + 2 * k] / 1e6,
+                  h[97 + 2 * k] / 1e6);
+        }
         const double n = c->n_req;
         fprintf(stderr,
                 "GI_PROF k_eval per request: init %.0f cyc, phase1 %.0f, phase2 %.0f, total %.0f; rule visits %.1f, "
