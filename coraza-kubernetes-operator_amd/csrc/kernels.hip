@@ -777,7 +777,9 @@ struct Tx {
 
 #define TXS(t, s) ((t).slots[(uint64_t)(s) * (t).n_req])
 
-__device__ inline uint8_t* tx_alloc(Tx& t, uint32_t n) {
+// tx_alloc / add_field serve Tx and the body parser's JsonCtx alike
+template <class C>
+__device__ inline uint8_t* tx_alloc(C& t, uint32_t n) {
   if (t.nb + n > t.cap_b) {
     t.flags |= GI_REQ_OVERFLOW;
     return nullptr;
@@ -787,7 +789,8 @@ __device__ inline uint8_t* tx_alloc(Tx& t, uint32_t n) {
   return p;
 }
 
-__device__ inline void add_field(Tx& t, uint8_t kind, const uint8_t* k, uint32_t kn, const uint8_t* v, uint32_t vn) {
+template <class C>
+__device__ inline void add_field(C& t, uint8_t kind, const uint8_t* k, uint32_t kn, const uint8_t* v, uint32_t vn) {
   if (t.nf >= t.cap_f) {
     t.flags |= GI_REQ_OVERFLOW;
     return;
@@ -988,7 +991,8 @@ __device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t 
 
 // Fold repeated keys of fields [f0, t.nf) (first position, last value) with
 // an open-addressing table in the transform scratch t.t1.
-__device__ __noinline__ void json_fold_keys(Tx& t, uint32_t f0) {
+template <class C>
+__device__ __forceinline__ void json_fold_keys(C& t, uint32_t f0) {
   const uint32_t nf = t.nf - f0;
   const uint32_t tsize = t.cap_t / 4;  // > body/2 + 2 >= nf (runtime.cpp sizing)
   if (nf < 2) return;
@@ -1026,7 +1030,8 @@ __device__ __noinline__ void json_fold_keys(Tx& t, uint32_t f0) {
   t.nf = o;
 }
 
-__device__ __noinline__ void parse_json_body(Tx& t, const uint8_t* s, uint32_t n) {
+template <class C>
+__device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t n) {
   const uint32_t f0 = t.nf;
   JFrame* st = (JFrame*)tx_alloc(t, (GI_JSON_MAX_DEPTH + 1) * sizeof(JFrame) + 8);
   if (!st) return;
@@ -1156,6 +1161,22 @@ __device__ __noinline__ void parse_json_body(Tx& t, const uint8_t* s, uint32_t n
     return;
   }
   if (!(t.flags & GI_REQ_ERROR_MASK)) json_fold_keys(t, f0);
+}
+
+// The parser state k_eval hands to the out-of-line instance: passing the
+// whole Tx by reference would pin it in scratch memory for the entire kernel.
+struct JsonCtx {
+  Field* fields;
+  uint32_t nf, cap_f;
+  uint8_t* bytes;
+  uint32_t nb, cap_b;
+  uint8_t* t1;
+  uint32_t cap_t;
+  uint16_t flags;
+};
+
+__device__ __noinline__ void parse_json_body_ool(JsonCtx* c, const uint8_t* s, uint32_t n) {
+  parse_json_body(*c, s, n);
 }
 
 // net/url shouldEscape(c, encodePath)
@@ -2970,7 +2991,13 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
               } else {
                 const uint32_t nf0 = t.nf;
                 if (t.body_proc == BP_URLENCODED) parse_query(t, D + rq.body.off, bn, FK_ARG_POST);
-                else parse_json_body(t, D + rq.body.off, bn);
+                else {
+                  JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
+                  parse_json_body_ool(&jc, D + rq.body.off, bn);
+                  t.nf = jc.nf;
+                  t.nb = jc.nb;
+                  t.flags = jc.flags;
+                }
                 t.has_post = t.nf > nf0;
               }
             } else if (t.body_proc != BP_NONE) {
