@@ -2706,65 +2706,86 @@ __device__ void value_end(const DProgram& P, const DBatch& B, uint32_t r, const 
   }
 }
 
-// One automaton step (q uniform): class from the joint map, transition from the image.
-#define SCAN_STEP(q)                                                                        \
-  if ((q) < K) {                                                                            \
-    const uint32_t cls = (jm >> (8 * (q))) & 0xFFu;                                         \
-    const uint32_t tv = *(const uint16_t*)(img + (trn[q] & 0xFFFFFu) + 2 * (st[q] * (trn[q] >> 20) + cls)); \
-    if ((umask >> (q)) & 1u) {                                                              \
-      if (tv & 0x8000u) union_accept(P, B, req, J, img, nf, (q), fm, st[q], cls);          \
-      st[q] = tv & 0x7FFFu;                                                                 \
-    } else {                                                                                \
-      st[q] = tv;                                                                           \
-    }                                                                                       \
-  }
-
-// One wave scans one queue block (<= 64 values of the job's stream).
-__device__ __forceinline__ void scan_qblock(const DProgram& P, const DBatch& B, const DJob& J, const uint8_t* img,
-                                            uint32_t K, const uint32_t* trn, const uint32_t* st0, uint32_t umask,
-                                            uint32_t nf, uint2 d, uint32_t mode) {
+// One wave scans NB queue blocks (<= 64 values each, the job's stream) at
+// once: each lane steps NB independent values, so NB transition chains
+// overlap their LDS latency (the automata of one value are already stepped
+// in lockstep).
+template <uint32_t NB>
+__device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B, const DJob& J, const uint8_t* img,
+                                             uint32_t K, const uint32_t* trn, const uint32_t* st0, uint32_t umask,
+                                             uint32_t nf, const uint2* d, uint32_t mode) {
   const uint32_t lane = lane_id();
-  const uint64_t woff = (uint64_t)d.x << 2;
-  const uint32_t nv = d.y & 0xFFu, nw = (d.y >> 8) & GI_QB_NW_MASK;
-  if (nv == 0) return;
-  GI_BOUND(nv <= 64 && woff + (uint64_t)(4 + nw) * nv <= B.pool_cap, d.x, d.y);
-  const uint32_t* q = B.pool + woff;
-  uint32_t req = 0, len = 0;
-  uint64_t fm = 0;
-  bool act = false;
-  if (lane < nv) {
-    req = q[lane];
-    fm = (uint64_t)q[nv + lane] | ((uint64_t)q[2 * nv + lane] << 32);
-    len = q[3 * nv + lane];
-    GI_BOUND(req < B.n_req && len <= 4 * nw, req, len);
-    uint64_t any = 0;
-    for (uint32_t k = 0; k < K; k++) any |= img_allowed(img, J.lds_fmask, nf, k, fm);
-    act = any != 0;
+  uint32_t req[NB], len[NB], nwl[NB], nwmax = 0, p0[NB], p1[NB];
+  uint64_t fm[NB];
+  const uint32_t* wp[NB];
+  uint32_t st[NB][GI_JOB_MAX_DFA];
+#pragma unroll
+  for (uint32_t j = 0; j < NB; j++) {
+    const uint64_t woff = (uint64_t)d[j].x << 2;
+    const uint32_t nv = d[j].y & 0xFFu, nw = (d[j].y >> 8) & GI_QB_NW_MASK;
+    GI_BOUND(nv <= 64 && woff + (uint64_t)(4 + nw) * nv <= B.pool_cap, d[j].x, d[j].y);
+    const uint32_t* q = B.pool + woff;
+    req[j] = 0;
+    len[j] = 0;
+    fm[j] = 0;
+    bool act = false;
+    if (lane < nv) {
+      req[j] = q[lane];
+      fm[j] = (uint64_t)q[nv + lane] | ((uint64_t)q[2 * nv + lane] << 32);
+      len[j] = q[3 * nv + lane];
+      GI_BOUND(req[j] < B.n_req && len[j] <= 4 * nw, req[j], len[j]);
+      uint64_t any = 0;
+      for (uint32_t k = 0; k < K; k++) any |= img_allowed(img, J.lds_fmask, nf, k, fm[j]);
+      act = any != 0;
+    }
+    if (mode & 2) act = false;
+    nwl[j] = (act && !(mode & 4)) ? (len[j] + 3) / 4 : 0u;
+    if (!act) len[j] = 0xFFFFFFFFu;  // marks an idle lane (no value_end)
+    nwmax = max(nwmax, nw);
+    wp[j] = q + 4 * nv + lane;
+    // this lane's words, loaded two ahead of the automaton steps
+    p0[j] = nwl[j] > 0 ? wp[j][0] : 0u;
+    p1[j] = nwl[j] > 1 ? wp[j][nv] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < GI_JOB_MAX_DFA; k++) st[j][k] = st0[k];
   }
-  if (mode & 2) return;
   if (mode & 16) umask = 0;
-  uint32_t st[GI_JOB_MAX_DFA];
-#pragma unroll
-  for (uint32_t k = 0; k < GI_JOB_MAX_DFA; k++) st[k] = st0[k];
   const uint32_t* jam = (const uint32_t*)img;
-  const uint32_t* wp = q + 4 * nv + lane;
-  for (uint32_t w = 0; w < nw; w++) {
-    if (act && 4 * w < len && !(mode & 4)) {
-      const uint32_t wd = wp[(uint64_t)w * nv];
-      const uint32_t nb = min(4u, len - 4 * w);
+  for (uint32_t w = 0; w < nwmax; w++) {
+    uint32_t wd[NB];
 #pragma unroll
-      for (uint32_t b = 0; b < 4; b++) {
-        if (b < nb) {
-          const uint32_t jm = jam[(wd >> (8 * b)) & 0xFFu];  // ASCII or GI_RUNE_MARK
-          SCAN_STEP(0)
-          SCAN_STEP(1)
-          SCAN_STEP(2)
-          SCAN_STEP(3)
+    for (uint32_t j = 0; j < NB; j++) {
+      const uint32_t nv = d[j].y & 0xFFu;
+      wd[j] = p0[j];
+      p0[j] = p1[j];
+      p1[j] = w + 2 < nwl[j] ? wp[j][(uint64_t)(w + 2) * nv] : 0u;
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+#pragma unroll
+      for (uint32_t j = 0; j < NB; j++) {
+        if (w < nwl[j] && 4 * w + b < len[j]) {
+          const uint32_t jm = jam[(wd[j] >> (8 * b)) & 0xFFu];  // ASCII or GI_RUNE_MARK
+#pragma unroll
+          for (uint32_t q = 0; q < GI_JOB_MAX_DFA; q++) {
+            if (q < K) {
+              const uint32_t cls = (jm >> (8 * q)) & 0xFFu;
+              const uint32_t tv = *(const uint16_t*)(img + (trn[q] & 0xFFFFFu) + 2 * (st[j][q] * (trn[q] >> 20) + cls));
+              if ((umask >> q) & 1u) {
+                if (tv & 0x8000u) union_accept(P, B, req[j], J, img, nf, q, fm[j], st[j][q], cls);
+                st[j][q] = tv & 0x7FFFu;
+              } else {
+                st[j][q] = tv;
+              }
+            }
+          }
         }
       }
     }
   }
-  if (act && !(mode & 8)) value_end(P, B, req, J, img, nf, K, fm, st);
+#pragma unroll
+  for (uint32_t j = 0; j < NB; j++)
+    if (len[j] != 0xFFFFFFFFu && !(mode & 8)) value_end(P, B, req[j], J, img, nf, K, fm[j], st[j]);
 }
 
 // Persistent kernel over units (job, 1024 queue-block entries), job-major.
@@ -2774,7 +2795,7 @@ __device__ __forceinline__ void scan_qblock(const DProgram& P, const DBatch& B, 
 // BIG: the 1-workgroup-per-CU launch of images above 64 KB (its own symbol,
 // so per-kernel profiles keep the two launches apart).
 template <bool LDS, bool BIG>
-__global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint32_t* __restrict__ jl, uint32_t n_jl,
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_scan(DProgram P, DBatch B, const uint32_t* __restrict__ jl, uint32_t n_jl,
                                                uint32_t mode, uint32_t acct_slot) {
   uint64_t rwords = 0;  // queue words of this launch's streams, each counted once (algorithmic bytes)
   uint64_t rsteps = 0;  // automaton byte-steps (padded words x 4 x automata of the job)
@@ -2839,13 +2860,18 @@ __global__ void __launch_bounds__(1024) k_scan(DProgram P, DBatch B, const uint3
     }
     // jl is sorted by stream: only the first job of a stream counts its words
     const bool first = jj == 0 || gi_cload(P.jobs, jl[jj - 1]).stream != J.stream;
-    for (uint32_t i = wv; i < total; i += nwv) {
-      const uint2 d = clist[i];
-      const uint32_t dnw = (d.y >> 8) & GI_QB_NW_MASK;
-      const uint64_t w = (uint64_t)(d.y & 0xFFu) * (4 + dnw);
-      rwords += (first && !(d.y & GI_QB_SHARED)) ? w : 0;  // a shared block is counted at its writer
-      rsteps += (uint64_t)(d.y & 0xFFu) * dnw * 4 * K;
-      scan_qblock(P, B, J, img, K, trn, st0, umask, nf, d, mode);
+    for (uint32_t i = wv; i < total; i += 2 * nwv) {  // two blocks per wave at a time
+      uint2 d[2];
+      d[0] = clist[i];
+      d[1] = i + nwv < total ? clist[i + nwv] : make_uint2(0u, 0u);
+#pragma unroll
+      for (uint32_t j = 0; j < 2; j++) {
+        const uint32_t dnw = (d[j].y >> 8) & GI_QB_NW_MASK;
+        const uint64_t w = (uint64_t)(d[j].y & 0xFFu) * (4 + dnw);
+        rwords += (first && !(d[j].y & GI_QB_SHARED)) ? w : 0;  // a shared block is counted at its writer
+        rsteps += (uint64_t)(d[j].y & 0xFFu) * dnw * 4 * K;
+      }
+      scan_qblocks<2>(P, B, J, img, K, trn, st0, umask, nf, d, mode);
     }
     __syncthreads();  // clist / wcnt reuse
   }

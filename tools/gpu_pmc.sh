@@ -9,10 +9,12 @@ cd /tmp
 i=0
 script="$1"; shift
 case "$script" in /*) ;; *) script="$R/$script" ;; esac
-for pmc in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES" \
-           "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH GRBM_GUI_ACTIVE" \
-           "FETCH_SIZE" \
-           "WRITE_SIZE"; do
+NPASS=${PMC_NPASS:-4}  # 2: the SQ passes only
+PASSES=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES"
+        "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH GRBM_GUI_ACTIVE"
+        "FETCH_SIZE"
+        "WRITE_SIZE")
+for pmc in "${PASSES[@]:0:$NPASS}"; do
   i=$((i+1))
   mkdir -p "$R/gpurun_out/pmc/p$i"
   timeout -k 10 -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d "$R/gpurun_out/pmc/p$i" -o run -- python3 "$script" "$@" > "$R/gpurun_out/pmc/p$i.log" 2>&1
