@@ -2442,9 +2442,9 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
       GI_BOUND(it.req < B.n_req, it.req, ii);
       gm = item_gmask(P, it);
       src = it.vp;
-      if (IN) {  // stage the scanned bytes once for all streams (bucket: vn <= IN)
+      if (IN) {  // stage the scanned bytes once for all streams (bucket: vn <= IN), a word at a time
         const uint32_t n = min(it.vn, IN);
-        for (uint32_t i = 0; i < n; i++) li[i] = it.vp[i];
+        for (uint32_t i = 0; i < n; i += 4) *(uint32_t*)(li + i) = load_u32u(it.vp + i);
         src = li;
       }
       summ = value_summary_lut(sumlut, src, it.vn);
@@ -2570,13 +2570,21 @@ __global__ void __launch_bounds__(64) k_stream(DProgram P, DBatch B, uint32_t bu
         q[2 * nv + i] = (uint32_t)(gm >> 32);
         q[3 * nv + i] = (uint32_t)cn;
         const uint32_t nwi = ((uint32_t)cn + 3) / 4;
-        for (uint32_t w = 0; w < nwi; w++) {
-          uint32_t x = 0;
-          for (uint32_t b = 0; b < 4; b++) {
-            const uint32_t at = 4 * w + b;
-            x |= (at < (uint32_t)cn ? (uint32_t)cur[at] : 0u) << (8 * b);
+        if (IN && !glob) {  // cur is a lane buffer in LDS (dword-aligned): a word per read
+          for (uint32_t w = 0; w < nwi; w++) {
+            uint32_t x = ((const uint32_t*)cur)[w];
+            if (4 * w + 4 > (uint32_t)cn) x &= (1u << (8 * ((uint32_t)cn - 4 * w))) - 1u;
+            q[4 * nv + (uint64_t)w * nv + i] = x;
           }
-          q[4 * nv + (uint64_t)w * nv + i] = x;
+        } else {
+          for (uint32_t w = 0; w < nwi; w++) {
+            uint32_t x = 0;
+            for (uint32_t b = 0; b < 4; b++) {
+              const uint32_t at = 4 * w + b;
+              x |= (at < (uint32_t)cn ? (uint32_t)cur[at] : 0u) << (8 * b);
+            }
+            q[4 * nv + (uint64_t)w * nv + i] = x;
+          }
         }
       }
       if (B.prof) pc_out += clock64() - c_s2;
