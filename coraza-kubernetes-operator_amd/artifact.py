@@ -1,0 +1,92 @@
+"""GPU artifact next to the RuleSet cache entry, and the data plane's hot swap.
+
+SURVEY §8f rows 1 and 4.
+
+* Artifact emitter.  The operator compiles a RuleSet once per cache entry
+  (next to `r.Cache.Put(cacheKey, aggregatedRules.String())`,
+  internal/controller/ruleset_controller.go:179-181).  It serves the compiled
+  program (gi_ruleset_save) beside the entry's `rules`.
+  * `entry()` builds that JSON object: RuleSetEntry's fields `uuid`,
+    `timestamp`, `rules` (internal/rulesets/cache/cache.go:32-36; JSON names
+    from server.go:35) plus `gpu_artifact` (base64), `gpu_artifact_version`
+    and `gpu_source_digest`.
+* Hot swap.  The data plane polls `GET /rules/<key>/latest` and reloads when
+  the UUID changes (server.go:163-181; pollIntervalSeconds,
+  config/samples/engine.yaml:18; KATs reconcile_test.go:72-88).
+  * `RulesetPoller.poll()` does the same against any fetch functions.
+  * It loads the artifact when it matches the entry's rules (source digest +
+    version), recompiles `rules` otherwise, and swaps the engine's program
+    with gi_ctx_swap_ruleset.
+"""
+
+from __future__ import annotations
+
+import base64
+from typing import Callable, Dict, Optional, Sequence
+
+import gpuinspect
+
+ARTIFACT_VERSION = 1
+
+
+def fnv64(data: bytes, h: int = 1469598103934665603) -> int:
+    for c in data:
+        h = ((h ^ c) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def source_digest(rules: str, exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS) -> int:
+    """The digest gi_compile stores in the artifact (runtime.cpp gi_compile)."""
+    data = rules.encode() + b"".join(b"\0export:" + e.encode() for e in exports)
+    return fnv64(data)
+
+
+def entry(uuid: str, timestamp: str, rules: str, ruleset: Optional[gpuinspect.Ruleset] = None) -> Dict:
+    """RuleSetEntry JSON plus the GPU artifact of `rules`."""
+    rs = ruleset if ruleset is not None else gpuinspect.Ruleset(rules)
+    return {"uuid": uuid, "timestamp": timestamp, "rules": rules,
+            "gpu_artifact": base64.b64encode(rs.save()).decode(),
+            "gpu_artifact_version": ARTIFACT_VERSION,
+            "gpu_source_digest": "%016x" % rs.info["source_digest"]}
+
+
+def ruleset_from_entry(e: Dict, exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS) -> gpuinspect.Ruleset:
+    """The entry's program: its artifact if it belongs to `rules`, else a compile."""
+    art = e.get("gpu_artifact")
+    want = source_digest(e["rules"], exports)
+    if art and e.get("gpu_artifact_version") == ARTIFACT_VERSION and \
+            e.get("gpu_source_digest") == "%016x" % want:
+        try:
+            rs = gpuinspect.Ruleset.load(base64.b64decode(art))
+            if rs.info["source_digest"] == want:
+                return rs
+        except gpuinspect.SecLangError:
+            pass  # corrupted / other build: recompile below
+    return gpuinspect.Ruleset(e["rules"], tx_exports=exports)
+
+
+class RulesetPoller:
+    """Reloads an engine's ruleset when the cache's latest UUID changes."""
+
+    def __init__(self, engine, fetch_latest: Callable[[], Dict], fetch_entry: Callable[[str], Dict],
+                 exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS):
+        self.engine = engine
+        self.fetch_latest = fetch_latest  # -> {"uuid", "timestamp"} (handleLatest)
+        self.fetch_entry = fetch_entry    # uuid -> entry() (handleGetRules)
+        self.exports = tuple(exports)
+        self.uuid: Optional[str] = None
+        self.ruleset: Optional[gpuinspect.Ruleset] = None
+        self.loaded_from_artifact = False
+
+    def poll(self) -> bool:
+        """True when a new ruleset was swapped in."""
+        latest = self.fetch_latest()
+        if latest["uuid"] == self.uuid:
+            return False
+        e = self.fetch_entry(latest["uuid"])
+        rs = ruleset_from_entry(e, self.exports)
+        self.loaded_from_artifact = rs.text is None
+        self.engine.swap(rs)
+        self.ruleset = rs  # the engine borrows it: keep it alive
+        self.uuid = latest["uuid"]
+        return True

@@ -49,6 +49,7 @@ struct Program {
   uint32_t n_slots = 0, n_markers = 0;
   uint8_t rule_engine = 1, body_access = 0;
   uint64_t body_limit = 134217728;
+  uint64_t source_digest = 0;  // FNV-1a 64 of the SecLang text and the export list (artifact identity)
 };
 
 // Returns 0, -1 (parse error) or -2 (unsupported); *err holds the message.

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/gpuinspect.h"
+#include "artifact.h"
 #include "compile.h"
 #include "gi_kernels.h"
 #include "unicode_tables.h"
@@ -107,29 +108,7 @@ static int hip_fail(gi_ctx* c, hipError_t e, const char* what) {
 
 extern "C" {
 
-int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ruleset** out, char* err,
-               size_t errcap) {
-  if (!seclang || !out) return GI_EINVAL;
-  *out = nullptr;
-  std::vector<std::string> exports;
-  if (opts && opts->tx_exports) {
-    for (const char* const* p = opts->tx_exports; *p; p++) exports.push_back(*p);
-  } else {
-    exports = kDefaultExports;
-  }
-  if (exports.size() > GI_MAX_EXPORTS) exports.resize(GI_MAX_EXPORTS);
-  auto* rs = new gi_ruleset();
-  std::string msg;
-  int rc = compile_program(std::string(seclang, n), exports, opts ? opts->dfa_state_cap : 0, &rs->prog, &msg);
-  if (rc != 0) {
-    if (err && errcap) {
-      size_t k = std::min(errcap - 1, msg.size());
-      memcpy(err, msg.data(), k);
-      err[k] = 0;
-    }
-    delete rs;
-    return rc == -1 ? GI_EPARSE : GI_EUNSUPPORTED;
-  }
+static void fill_info(gi_ruleset* rs) {
   const Program& P = rs->prog;
   rs->info.n_rules = (uint32_t)P.top.size();
   rs->info.n_links = (uint32_t)P.rules.size();
@@ -147,6 +126,62 @@ int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ru
                            P.filters.size() * sizeof(DFilter) + P.jobs.size() * sizeof(DJob) +
                            P.jdfas.size() * sizeof(DJobDfa) + P.pats.size() * sizeof(DPat) +
                            P.svals.size() * sizeof(DScanVal) + P.images.size();
+  rs->info.source_digest = P.source_digest;
+}
+
+int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ruleset** out, char* err,
+               size_t errcap) {
+  if (!seclang || !out) return GI_EINVAL;
+  *out = nullptr;
+  std::vector<std::string> exports;
+  if (opts && opts->tx_exports) {
+    for (const char* const* p = opts->tx_exports; *p; p++) exports.push_back(*p);
+  } else {
+    exports = kDefaultExports;
+  }
+  if (exports.size() > GI_MAX_EXPORTS) exports.resize(GI_MAX_EXPORTS);
+  auto* rs = new gi_ruleset();
+  std::string msg;
+  std::string digest_input(seclang, n);
+  for (const auto& x : exports) digest_input.append("\0export:", 8).append(x);
+  int rc = compile_program(std::string(seclang, n), exports, opts ? opts->dfa_state_cap : 0, &rs->prog, &msg);
+  if (rc != 0) {
+    if (err && errcap) {
+      size_t k = std::min(errcap - 1, msg.size());
+      memcpy(err, msg.data(), k);
+      err[k] = 0;
+    }
+    delete rs;
+    return rc == -1 ? GI_EPARSE : GI_EUNSUPPORTED;
+  }
+  rs->prog.source_digest = gi::fnv64((const uint8_t*)digest_input.data(), digest_input.size());
+  fill_info(rs);
+  *out = rs;
+  return GI_OK;
+}
+
+int64_t gi_ruleset_save(const gi_ruleset* rs, uint8_t* buf, size_t cap) {
+  if (!rs) return GI_EINVAL;
+  const std::vector<uint8_t> a = gi::serialize_program(rs->prog);
+  if (buf && cap) memcpy(buf, a.data(), std::min(cap, a.size()));
+  return (int64_t)a.size();
+}
+
+int gi_ruleset_load(const uint8_t* buf, size_t n, gi_ruleset** out, char* err, size_t errcap) {
+  if (!buf || !out) return GI_EINVAL;
+  *out = nullptr;
+  auto* rs = new gi_ruleset();
+  std::string msg;
+  if (!gi::deserialize_program(buf, n, &rs->prog, &msg)) {
+    if (err && errcap) {
+      size_t k = std::min(errcap - 1, msg.size());
+      memcpy(err, msg.data(), k);
+      err[k] = 0;
+    }
+    delete rs;
+    return GI_EINVAL;
+  }
+  fill_info(rs);
   *out = rs;
   return GI_OK;
 }
@@ -180,30 +215,11 @@ int64_t gi_ruleset_describe(const gi_ruleset* rs, char* buf, size_t cap) {
   return (int64_t)s.size();
 }
 
-int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx** out) {
-  if (!rs || !out) return GI_EINVAL;
-  *out = nullptr;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return GI_ENODEV;
-  auto* c = new gi_ctx();
-  c->rs = rs;
-  c->device = device;
-  c->mcap = matched_cap ? matched_cap : 64;
-  c->diag_on = getenv("GI_DIAG") && atoi(getenv("GI_DIAG")) > 0;
-  c->prof_on = getenv("GI_PROF") && atoi(getenv("GI_PROF")) > 0;
-  c->stop_after = getenv("GI_STOP_AFTER") ? atoi(getenv("GI_STOP_AFTER")) : 0;
-  hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  if (e == hipSuccess) e = hipEventCreate(&c->evs[0]);
-  if (e == hipSuccess) e = hipEventCreate(&c->evs[1]);
-  if (e == hipSuccess) e = hipEventCreate(&c->evs[2]);
-  for (int k = 0; k <= GI_MAX_LAUNCHES && e == hipSuccess; k++) e = hipEventCreate(&c->log.ev[k]);
-  if (e != hipSuccess) {
-    delete c;
-    return GI_ENODEV;
-  }
+// Uploads (or replaces) the context's device copy of a compiled ruleset.
+// Program buffers are reused when large enough; the staged batch is dropped
+// (its scratch layout depends on the program).
+static int load_program(gi_ctx* c, const gi_ruleset* rs) {
+  hipError_t e = hipSuccess;
   const Program& P = rs->prog;
   c->pbufs.resize(32);
   std::vector<uint32_t> lower;
@@ -214,7 +230,6 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   }
   hipStream_t s = c->stream;
   int k = 0;
-  e = hipSuccess;
 #define UP(field, vec, T)                                   \
   if (e == hipSuccess) {                                    \
     e = upload(&c->pbufs[k], vec, s);                       \
@@ -262,10 +277,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   UP(body_links, P.body_links, uint32_t)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) {
-    gi_ctx_free(c);
-    return GI_ENODEV;
-  }
+  if (e != hipSuccess) return GI_ENODEV;
   c->prog.n_lower_pairs = GI_N_LOWER_PAIRS;
   c->prog.n_top = (uint32_t)P.top.size();
   c->prog.top_begin[0] = 0;
@@ -283,10 +295,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->prog.max_img_bytes = P.max_img_bytes;
   c->prog.max_big_img_bytes = P.max_big_img_bytes;
   c->prog.n_streams = (uint32_t)P.streams.size();
-  if (c->prog.n_streams > GI_MAX_STREAMS) {
-    gi_ctx_free(c);
-    return GI_EINVAL;
-  }
+  if (c->prog.n_streams > GI_MAX_STREAMS) return GI_EINVAL;
   c->prog.n_always = (uint32_t)P.always_slots.size();
   c->prog.n_body_links = (uint32_t)P.body_links.size();
   c->prog.n_gfilters = (uint32_t)P.filters.size();
@@ -305,10 +314,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   std::vector<uint32_t> all(jl[0]);
   all.insert(all.end(), jl[1].begin(), jl[1].end());
   all.insert(all.end(), jl[2].begin(), jl[2].end());
-  if (upload(&c->joblist, all, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
-    gi_ctx_free(c);
-    return GI_ENOMEM;
-  }
+  if (upload(&c->joblist, all, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return GI_ENOMEM;
   for (int b = 0; b < 2; b++) {
     c->scan.jobs[b] = (const uint32_t*)c->joblist.p + (b ? jl[0].size() : 0);
     c->scan.n_jobs[b] = (uint32_t)jl[b].size();
@@ -321,11 +327,55 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->scan.n_global = (uint32_t)jl[2].size();
   c->scan.blocks[2] = scan_resident_blocks(16);
   c->scan.mode = getenv("GI_SCAN_MODE") ? (uint32_t)atoi(getenv("GI_SCAN_MODE")) : 0u;
+  c->rs = rs;
+  c->staged = false;
+  c->ran = false;
+  return GI_OK;
+}
+
+int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx** out) {
+  if (!rs || !out) return GI_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return GI_ENODEV;
+  auto* c = new gi_ctx();
+  c->rs = rs;
+  c->device = device;
+  c->mcap = matched_cap ? matched_cap : 64;
+  c->diag_on = getenv("GI_DIAG") && atoi(getenv("GI_DIAG")) > 0;
+  c->prof_on = getenv("GI_PROF") && atoi(getenv("GI_PROF")) > 0;
+  c->stop_after = getenv("GI_STOP_AFTER") ? atoi(getenv("GI_STOP_AFTER")) : 0;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipEventCreate(&c->evs[0]);
+  if (e == hipSuccess) e = hipEventCreate(&c->evs[1]);
+  if (e == hipSuccess) e = hipEventCreate(&c->evs[2]);
+  for (int k = 0; k <= GI_MAX_LAUNCHES && e == hipSuccess; k++) e = hipEventCreate(&c->log.ev[k]);
+  if (e != hipSuccess) {
+    delete c;
+    return GI_ENODEV;
+  }
+  const int rc = load_program(c, rs);
+  if (rc != GI_OK) {
+    gi_ctx_free(c);
+    return rc;
+  }
   if (c->stop_after)
     fprintf(stderr, "scan plan: small %u jobs lds %u blocks %u | big %u jobs lds %u blocks %u | hbm %u jobs blocks %u\n",
             c->scan.n_jobs[0], c->scan.lds[0], c->scan.blocks[0], c->scan.n_jobs[1], c->scan.lds[1],
             c->scan.blocks[1], c->scan.n_global, c->scan.blocks[2]);
   *out = c;
+  return GI_OK;
+}
+
+int gi_ctx_swap_ruleset(gi_ctx* c, const gi_ruleset* rs) {
+  if (!c || !rs) return GI_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return GI_ENODEV;
+  const int rc = load_program(c, rs);
+  if (rc != GI_OK) return fail(c, rc, "ruleset upload failed");
   return GI_OK;
 }
 

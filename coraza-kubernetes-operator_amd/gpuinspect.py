@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "gi_ctx_create", "gi_ctx_free", "gi_last_error", "gi_inspect_batch", "gi_stage_batch",
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
     "gi_ctx_stream", "gi_selftest_regex", "gi_selftest_plan", "gi_selftest_triggers",
+    "gi_ruleset_save", "gi_ruleset_load", "gi_ctx_swap_ruleset",
 )
 
 
@@ -86,7 +87,8 @@ class _Info(ctypes.Structure):
     _fields_ = [("n_rules", ctypes.c_uint32), ("n_links", ctypes.c_uint32), ("n_dfas", ctypes.c_uint32),
                 ("n_tx_slots", ctypes.c_uint32), ("program_bytes", ctypes.c_uint64),
                 ("n_scan_jobs", ctypes.c_uint32), ("n_hit_slots", ctypes.c_uint32),
-                ("n_union_dfas", ctypes.c_uint32), ("n_scan_streams", ctypes.c_uint32)]
+                ("n_union_dfas", ctypes.c_uint32), ("n_scan_streams", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
+                ("source_digest", ctypes.c_uint64)]
 
 
 class _Batch(ctypes.Structure):
@@ -137,6 +139,10 @@ def load_library(path: str = LIB_PATH):
     lib.gi_ruleset_describe.argtypes = [vp, ctypes.c_char_p, sz]
     lib.gi_ruleset_describe.restype = ctypes.c_int64
     lib.gi_ctx_create.argtypes = [vp, ctypes.c_int, u32, ctypes.POINTER(vp)]
+    lib.gi_ctx_swap_ruleset.argtypes = [vp, vp]
+    lib.gi_ruleset_save.argtypes = [vp, ctypes.c_void_p, sz]
+    lib.gi_ruleset_save.restype = ctypes.c_int64
+    lib.gi_ruleset_load.argtypes = [ctypes.c_void_p, sz, ctypes.POINTER(vp), ctypes.c_char_p, sz]
     lib.gi_ctx_free.argtypes = [vp]
     lib.gi_last_error.argtypes = [vp]
     lib.gi_last_error.restype = ctypes.c_char_p
@@ -186,9 +192,44 @@ class Ruleset:
         if rc != GI_OK:
             raise SecLangError(rc, err.value.decode(errors="replace"))
         self._h = h
+        self._load_info()
+
+    def _load_info(self):
         info = _Info()
-        lib.gi_ruleset_info_get(h, ctypes.byref(info))
-        self.info = {k: getattr(info, k) for k, _ in _Info._fields_}
+        self._lib.gi_ruleset_info_get(self._h, ctypes.byref(info))
+        self.info = {k: getattr(info, k) for k, _ in _Info._fields_ if not k.startswith("_")}
+
+    def save(self) -> bytes:
+        """The GPU artifact (gi_ruleset_save): the compiled program as one blob."""
+        n = self._lib.gi_ruleset_save(self._h, None, 0)
+        if n < 0:
+            raise EngineError("gi_ruleset_save failed (%d)" % n)
+        buf = ctypes.create_string_buffer(int(n))
+        self._lib.gi_ruleset_save(self._h, buf, int(n))
+        return buf.raw
+
+    @classmethod
+    def load(cls, artifact: bytes) -> "Ruleset":
+        """A ruleset from a GPU artifact (gi_ruleset_load), without recompiling."""
+        lib = load_library()
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        rc = lib.gi_ruleset_load(artifact, len(artifact), ctypes.byref(h), err, 512)
+        if rc != GI_OK:
+            raise SecLangError(rc, err.value.decode(errors="replace"))
+        self = cls.__new__(cls)
+        self._lib = lib
+        self.text = None
+        self._h = h
+        self._load_info()
+        names = []
+        buf = ctypes.create_string_buffer(256)
+        for i in range(MAX_EXPORTS):
+            if lib.gi_ruleset_export_name(h, i, buf, 256) != GI_OK:
+                break
+            names.append(buf.value.decode())
+        self.exports = tuple(names)
+        return self
 
     def selftest_plan(self):
         """Host emulation of the phase-A scan images (compiler self-test)."""
@@ -353,6 +394,13 @@ class Engine:
         if rc != GI_OK:
             raise EngineError("gi_ctx_create failed (%d): no usable HIP device %d" % (rc, device))
         self._h = h
+        self._staged = None
+
+    def swap(self, ruleset: Ruleset):
+        """Hot swap (gi_ctx_swap_ruleset): later batches run `ruleset`; a staged
+        batch is dropped."""
+        self._check(self._lib.gi_ctx_swap_ruleset(self._h, ruleset._h), "gi_ctx_swap_ruleset")
+        self.ruleset = ruleset
         self._staged = None
 
     def _check(self, rc, what):

@@ -87,6 +87,8 @@ typedef struct {
   uint32_t n_hit_slots;   /* rule links evaluated data-parallel in phase A */
   uint32_t n_union_dfas;  /* multi-pattern automata among n_dfas */
   uint32_t n_scan_streams; /* phase-A streams (value source x transformation chain) */
+  uint32_t _pad;
+  uint64_t source_digest;  /* FNV-1a 64 of the SecLang text + export list the ruleset was compiled from */
 } gi_ruleset_info;
 
 /* A byte range inside gi_batch.data. */
@@ -175,6 +177,20 @@ void gi_ruleset_free(gi_ruleset* rs);
 int gi_ruleset_info_get(const gi_ruleset* rs, gi_ruleset_info* out);
 /* ids of the exported TX names, in order (for result decoding) */
 int gi_ruleset_export_name(const gi_ruleset* rs, uint32_t i, char* buf, size_t cap);
+/* GPU artifact of a compiled ruleset (the compile path's artifact
+ * emitter): the whole compiled program as one versioned, checksummed blob,
+ * served next to RuleSetEntry.Rules (internal/rulesets/cache/cache.go:32-36)
+ * and keyed like it by the entry UUID (cache.go:81-100), so a data plane that
+ * polls GET /rules/<key>/latest (server.go:163-181) loads the program instead
+ * of recompiling the SecLang text.
+ *   gi_ruleset_save  writes at most cap bytes; returns the artifact size (call
+ *                    with cap 0 to size the buffer) or a negative GI_* code.
+ *   gi_ruleset_load  GI_EINVAL + message for a truncated, corrupted or
+ *                    other-version artifact.  Artifacts are trusted like the
+ *                    SecLang text they come from (same producer). */
+int64_t gi_ruleset_save(const gi_ruleset* rs, uint8_t* buf, size_t cap);
+int gi_ruleset_load(const uint8_t* buf, size_t n, gi_ruleset** out, char* err, size_t errcap);
+
 /* JSON description of the phase-A scan plan (streams, jobs, automata sizes).
  * Writes at most cap bytes (NUL-terminated); returns the full length
  * (excluding the NUL), or a negative GI_* code. */
@@ -182,6 +198,11 @@ int64_t gi_ruleset_describe(const gi_ruleset* rs, char* buf, size_t cap);
 
 /* ------------------------------------------------------------ context */
 int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx** out);
+/* Hot swap: the ctx evaluates rs from the next staged batch on (the data
+ * plane's live reload when /latest reports a new UUID, server.go:163-181;
+ * KATs reconcile_test.go:72-88).  Device buffers are reused; a staged batch
+ * is dropped and must be staged again.  rs must outlive its use by the ctx. */
+int gi_ctx_swap_ruleset(gi_ctx* ctx, const gi_ruleset* rs);
 void gi_ctx_free(gi_ctx* ctx);
 const char* gi_last_error(const gi_ctx* ctx);
 
