@@ -2406,7 +2406,7 @@ __device__ uint32_t collapse_runes(const uint8_t* s, uint32_t n, uint8_t* d) {
 // IN = per-lane LDS copy of the item's bytes (bucket maximum); WT = per-lane
 // LDS transformation buffers.  IN == 0: long items, HBM buffers throughout.
 template <uint32_t IN, uint32_t WT>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stream(DProgram P, DBatch B, uint32_t bucket) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) k_stream(DProgram P, DBatch B, uint32_t bucket) {
   constexpr uint32_t IS = IN ? IN + 4 : 0;  // lane strides = odd dword counts: conflict-free
   __shared__ __attribute__((aligned(16))) uint8_t lb[IN ? 64 * (IS + 2 * WT) : 16];
   // Queue block of (item-wave, stream) = qblk[stream][item-wave index]: no

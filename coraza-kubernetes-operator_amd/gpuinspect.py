@@ -29,7 +29,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgpuinspect.so")
+LIB_PATH = os.environ.get("GI_LIB") or os.path.join(HERE, "libgpuinspect.so")  # GI_LIB: A/B builds
 
 GI_OK = 0
 GI_EPARSE = -1
