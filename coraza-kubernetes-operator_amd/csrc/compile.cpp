@@ -972,8 +972,10 @@ struct Lower {
   // Assigns a hit slot and registers the link's patterns, or returns -1 when
   // the link stays interpreter-only (TX / count targets, macro arguments,
   // operators without an automaton form, mutable singles).
+  bool no_scan = false;  // the current top-level rule sits behind a paranoia gate (gated_rules)
+
   int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
-    if (!r.has_op) return -1;
+    if (!r.has_op || no_scan) return -1;
     const std::string& n = r.op_name;
     bool scannable = n == "rx" || n == "pm" || n == "validatebyterange" || n == "validateurlencoding" ||
                      n == "validateutf8encoding" || (n == "contains" && r.op_arg.find("%{") == std::string::npos);
@@ -1417,6 +1419,67 @@ struct Lower {
 
 }  // namespace
 
+// Rules phase A need not scan: those behind a CRS-style paranoia gate
+//   SecRule TX:<X> "@lt N" "...,skipAfter:<M>"
+// whose TX:<X> every setvar in the program sets to the same integer K < N.
+// Such a region is skipped at run time for every request; dropping its links
+// from phase A only saves scan work.  If a request does reach one (a ctl or
+// a TX write this analysis does not see), the link has no hit slot and the
+// interpreter evaluates it in full, so results never depend on the guess.
+// Returns, per top-level rule, true = keep out of phase A.
+static std::vector<bool> gated_rules(const IrWaf& waf) {
+  std::vector<bool> out(waf.rules.size(), false);
+  std::map<std::string, std::string> val;  // tx var -> integer text ("" = unknown)
+  auto lower = [](std::string x) {
+    for (auto& c : x) c = (char)tolower((unsigned char)c);
+    return x;
+  };
+  auto is_int = [](const std::string& x) {
+    if (x.empty()) return false;
+    for (size_t i = (x[0] == '-' ? 1 : 0); i < x.size(); i++)
+      if (!isdigit((unsigned char)x[i])) return false;
+    return x != "-";
+  };
+  auto note = [&](const IrRule& r) {
+    for (const IrNd& a : r.nd) {
+      if (!a.is_setvar) {
+        if (!a.ctl_name.empty()) val["*ctl"] = "";
+        continue;
+      }
+      const std::string k = lower(a.sv_key);  // setvar keys are TX names (the "tx." is parsed off)
+      std::string v = a.sv_remove ? std::string() : a.sv_value;
+      if (v.size() > 5 && v.rfind("%{", 0) == 0 && v.back() == '}') {
+        std::string ref = lower(v.substr(2, v.size() - 3));
+        if (ref.rfind("tx.", 0) == 0 && val.count(ref.substr(3))) v = val[ref.substr(3)];
+        else v = "";
+      }
+      if (!is_int(v) || v[0] == '+' || (val.count(k) && val[k] != v)) v = "";
+      val[k] = v;
+    }
+  };
+  for (const IrRule& r : waf.rules) {
+    note(r);
+    for (const IrRule& c : r.children) note(c);
+  }
+  std::map<std::string, size_t> marker_at;
+  for (size_t i = 0; i < waf.rules.size(); i++)
+    if (!waf.rules[i].secmark.empty()) marker_at[waf.rules[i].secmark] = i;
+  for (size_t i = 0; i < waf.rules.size(); i++) {
+    const IrRule& g = waf.rules[i];
+    if (g.has_chain || g.skip_after.empty() || !g.has_op || g.op_neg || lower(g.op_name) != "lt" ||
+        g.vars.size() != 1 || g.vars[0].count || g.vars[0].key_rx || lower(g.vars[0].name) != "tx")
+      continue;
+    auto it = val.find(lower(g.vars[0].key));
+    auto mk = marker_at.find(g.skip_after);
+    if (it == val.end() || it->second.empty() || !is_int(g.op_arg) || mk == marker_at.end() || mk->second <= i)
+      continue;
+    if (!(std::stoll(it->second) < std::stoll(g.op_arg))) continue;
+    for (size_t j = i + 1; j < mk->second; j++)
+      if (waf.rules[j].phase == g.phase) out[j] = true;
+  }
+  return out;
+}
+
 int compile_program(const std::string& text, const std::vector<std::string>& exports, uint32_t cap,
                     Program* out, std::string* err) {
   try {
@@ -1428,7 +1491,10 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
     // block inherits the phase's default disruptive action through merge_defaults:
     // the merged list then holds "block" followed by the default action; the last
     // disruptive action wins (apply_actions), so nothing else is needed here.
-    for (auto& r : waf.rules) {
+    const std::vector<bool> gated = gated_rules(waf);
+    for (size_t ti = 0; ti < waf.rules.size(); ti++) {
+      const IrRule& r = waf.rules[ti];
+      L.no_scan = gated[ti];
       uint32_t idx = L.rule(r, false);
       out->top.push_back(idx);
       uint32_t prev = idx;

@@ -114,3 +114,30 @@ def test_gpu_parity_crs_pl1_kat_payloads():
             t2.write_request_body(b"a=1&" + q + b"=x&b=" + q)
             txs.append(t2)
     _parity(text, gpuinspect.pack(txs))
+
+
+GATED = """SecRuleEngine On
+SecAction "id:1,phase:1,pass,nolog,setvar:tx.pl=1"
+SecRule REQUEST_HEADERS:X-Open "@streq yes" "id:2,phase:1,pass,nolog,ctl:ruleRemoveById=10"
+SecRule TX:PL "@lt 2" "id:10,phase:1,pass,nolog,skipAfter:END-PL2"
+SecRule ARGS "@rx evil" "id:11,phase:1,deny,status:403"
+SecMarker END-PL2
+SecRule ARGS "@rx monkey" "id:12,phase:1,deny,status:403"
+"""
+
+
+def test_gpu_parity_gated_region_reached():
+    """Rule 11 sits behind a paranoia-style gate the compiler keeps out of
+    phase A; a request that removes the gate (ctl:ruleRemoveById) reaches it
+    and must still be evaluated exactly."""
+    assert gpuinspect.Ruleset(GATED).info["n_hit_slots"] == 1  # only rule 12 is scanned
+    txs = []
+    for uri in (b"/?a=evil", b"/?a=monkey", b"/?a=safe"):
+        for open_ in (False, True):
+            t = gpuinspect.Transaction(method=b"GET", uri=uri)
+            t.add_request_header("Host", "x")
+            if open_:
+                t.add_request_header("X-Open", "yes")
+            txs.append(t)
+    res = _parity(GATED, gpuinspect.pack(txs))
+    assert [int(v["status"]) for v in res.verdicts] == [0, 403, 403, 403, 0, 0]
