@@ -973,6 +973,7 @@ struct Lower {
   // the link stays interpreter-only (TX / count targets, macro arguments,
   // operators without an automaton form, mutable singles).
   bool no_scan = false;  // the current top-level rule sits behind a paranoia gate (gated_rules)
+  bool capture_seen = true;  // some rule, macro or export can read TX:0-TX:9 (capture_observable)
 
   int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
     if (!r.has_op || no_scan) return -1;
@@ -1381,7 +1382,8 @@ struct Lower {
     d.phase = (uint8_t)r.phase;
     d.flags = (child ? RF_CHILD : 0) | (r.secmark.empty() ? 0 : RF_MARKER);
     d.op = -1;
-    if (r.capture) unsup("capture is not supported yet");
+    if (r.capture && capture_seen)
+      unsup("capture is not supported yet when a rule, macro or export reads TX:0-TX:9");
     if (r.multimatch) unsup("multiMatch is not supported yet");
     const std::string& dis = r.disruptive;
     d.disruptive = dis == "deny" ? D_DENY : dis == "drop" ? D_DROP : dis == "redirect" ? D_REDIRECT
@@ -1480,6 +1482,54 @@ static std::vector<bool> gated_rules(const IrWaf& waf) {
   return out;
 }
 
+// `capture` (coraza internal/actions/capture.go; internal/operators/rx.go and
+// pm.go fill TX.0-TX.9 on a match) changes nothing but the TX.0-TX.9 values:
+// the operator's boolean result is the same with or without it.  When no
+// rule target, no macro in an operator argument / setvar / ctl, and no
+// exported name can read those keys, the action is unobservable in every
+// output this engine produces (interruption, matched ids, exported TX
+// integers) and the program drops it.  CRS uses it that way in most
+// detection rules (its only reader there is logdata, which is not an output).
+// Conservative: a whole-collection or regex-keyed TX target (counted or not) counts
+// as a reader.
+static bool capture_observable(const IrWaf& waf, const std::vector<std::string>& exports) {
+  auto lower = [](std::string x) {
+    for (auto& c : x) c = (char)tolower((unsigned char)c);
+    return x;
+  };
+  auto digit_key = [](const std::string& k) { return k.size() == 1 && k[0] >= '0' && k[0] <= '9'; };
+  auto macro_reads = [&](const std::string& s) {
+    const std::string l = lower(s);
+    for (size_t p = l.find("%{"); p != std::string::npos; p = l.find("%{", p + 2)) {
+      size_t q = p + 2;
+      while (q < l.size() && (l[q] == ' ' || l[q] == '\t')) q++;
+      if (l.compare(q, 2, "tx") == 0 && q + 3 < l.size() && (l[q + 2] == '.' || l[q + 2] == ':') &&
+          isdigit((unsigned char)l[q + 3]))
+        return true;
+    }
+    return false;
+  };
+  auto reads = [&](const IrRule& r) {
+    for (const IrVar& v : r.vars)
+      if (lower(v.name) == "tx" && (v.key.empty() || v.key_rx || digit_key(v.key))) return true;
+    if (r.has_op && macro_reads(r.op_arg)) return true;
+    for (const IrNd& a : r.nd)
+      if (macro_reads(a.sv_key) || macro_reads(a.sv_value) || macro_reads(a.ctl_value)) return true;
+    return false;
+  };
+  for (const std::string& e : exports) {
+    std::string k = lower(e);
+    if (k.rfind("tx.", 0) == 0) k = k.substr(3);
+    if (digit_key(k)) return true;
+  }
+  for (const IrRule& r : waf.rules) {
+    if (reads(r)) return true;
+    for (const IrRule& c : r.children)
+      if (reads(c)) return true;
+  }
+  return false;
+}
+
 int compile_program(const std::string& text, const std::vector<std::string>& exports, uint32_t cap,
                     Program* out, std::string* err) {
   try {
@@ -1492,6 +1542,7 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
     // the merged list then holds "block" followed by the default action; the last
     // disruptive action wins (apply_actions), so nothing else is needed here.
     const std::vector<bool> gated = gated_rules(waf);
+    L.capture_seen = capture_observable(waf, exports);
     for (size_t ti = 0; ti < waf.rules.size(); ti++) {
       const IrRule& r = waf.rules[ti];
       L.no_scan = gated[ti];

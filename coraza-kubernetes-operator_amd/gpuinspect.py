@@ -171,7 +171,7 @@ def aggregate_configmaps(texts: Sequence[str]) -> str:
 DEFAULT_EXPORTS = (
     "blocking_inbound_anomaly_score", "inbound_anomaly_score_pl1", "inbound_anomaly_score_pl2",
     "inbound_anomaly_score_pl3", "inbound_anomaly_score_pl4", "detection_inbound_anomaly_score",
-    "anomaly_score", "0",
+    "anomaly_score",
 )
 
 

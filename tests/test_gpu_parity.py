@@ -141,3 +141,25 @@ def test_gpu_parity_gated_region_reached():
             txs.append(t)
     res = _parity(GATED, gpuinspect.pack(txs))
     assert [int(v["status"]) for v in res.verdicts] == [0, 403, 403, 403, 0, 0]
+
+
+CAPTURE = """SecRuleEngine On
+SecRule ARGS|REQUEST_HEADERS:User-Agent "@rx (?i)(union)\\s+(select)" "id:1,phase:2,pass,capture,t:none,t:urlDecodeUni,\\
+    logdata:'Matched Data: %{TX.0} found within %{MATCHED_VAR_NAME}',setvar:'tx.anomaly_score=+5'"
+SecRule ARGS "@pm evilmonkey sinister" "id:2,phase:2,pass,capture,t:lowercase,setvar:'tx.anomaly_score=+3'"
+SecRule TX:ANOMALY_SCORE "@ge 5" "id:3,phase:2,deny,status:403"
+"""
+
+
+def test_gpu_parity_capture_logdata_only():
+    """capture feeding only logdata (the CRS pattern) is dropped by the compiler;
+    verdicts, matched ids and scores stay identical to the oracle, which runs
+    the capture (FindStringSubmatch / phrase captures into TX.0-TX.9)."""
+    txs = []
+    for q in (b"1+UNION+SELECT+x", b"a%20union%20%20select", b"EvilMonkey", b"safe", b"sinister+union+select"):
+        t = gpuinspect.Transaction(method=b"GET", uri=b"/?q=" + q)
+        t.add_request_header("Host", "x")
+        t.add_request_header("User-Agent", "Mozilla/5.0")
+        txs.append(t)
+    res = _parity(CAPTURE, gpuinspect.pack(txs))
+    assert [int(v["status"]) for v in res.verdicts] == [403, 403, 0, 0, 403]

@@ -77,3 +77,44 @@ def test_regex_dfa_matches_oracle(pat):
         rc, _ = gpuinspect.selftest_regex("(?sm)" + pat, s)
         assert rc in (0, 1)
         assert rc == int(g.match_string(s)), (pat, s)
+
+
+CAPTURE_LOGDATA = """SecRuleEngine On
+SecRule ARGS "@rx (?i)(union)\\s+(select)" "id:1,phase:2,pass,capture,t:none,t:urlDecodeUni,\\
+    logdata:'Matched Data: %{TX.0} found within %{MATCHED_VAR_NAME}',setvar:'tx.score=+5'"
+SecRule TX:SCORE "@ge 5" "id:2,phase:2,deny,status:403"
+"""
+
+
+def test_capture_without_reader_compiles():
+    """capture whose TX.0-TX.9 only feed logdata (the CRS pattern) is exact to drop."""
+    rs = gpuinspect.Ruleset(CAPTURE_LOGDATA)
+    assert rs.info["n_rules"] == 2
+
+
+CAPTURE_READ = [
+    # a chained link reads the captured value (CRS 920420-style)
+    'SecRule REQUEST_HEADERS:Content-Type "@rx ^([^;]+)" "id:1,phase:1,deny,capture,chain"\n'
+    'SecRule TX:1 "!@within text/plain" ""',
+    # a macro in an operator argument / setvar reads it
+    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture,setvar:tx.seen=%{tx.1}"',
+    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule ARGS "@streq %{TX.0}" "id:2,phase:2,deny"',
+    # whole-collection / regex-keyed TX targets can see TX.0
+    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule TX "@rx aa" "id:2,phase:2,deny"',
+    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule TX:/^[0-9]$/ "@rx aa" "id:2,phase:2,deny"',
+    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule &TX:0 "@eq 1" "id:2,phase:2,deny"',
+]
+
+
+@pytest.mark.parametrize("text", CAPTURE_READ)
+def test_capture_with_reader_is_unsupported(text):
+    coraza.parse_seclang(text)  # valid SecLang
+    with pytest.raises(gpuinspect.SecLangError) as e:
+        gpuinspect.Ruleset(text)
+    assert e.value.code == gpuinspect.GI_EUNSUPPORTED
+
+
+def test_capture_exported_is_unsupported():
+    with pytest.raises(gpuinspect.SecLangError) as e:
+        gpuinspect.Ruleset(CAPTURE_LOGDATA, tx_exports=["score", "0"])
+    assert e.value.code == gpuinspect.GI_EUNSUPPORTED
