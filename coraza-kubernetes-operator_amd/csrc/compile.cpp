@@ -97,6 +97,7 @@ struct IrRule {
   std::string disruptive;
   int status = 0;
   bool capture = false, multimatch = false;
+  std::vector<std::string> phrases;  // @pmFromFile: the data file's phrases (lowercased)
   std::vector<IrNd> nd;
   int skip = 0;
   std::string skip_after, secmark;
@@ -315,6 +316,29 @@ void parse_variables(const std::string& s, IrRule* rule) {
   }
 }
 
+// @pmFromFile data files of the compile in progress (compile_program).
+thread_local const std::map<std::string, std::string>* g_data_files = nullptr;
+
+// coraza internal/operators/pm_from_file.go: bufio.Scanner lines ('\n', a
+// trailing '\r' dropped), strings.TrimSpace, empty lines and '#' comments
+// skipped, strings.ToLower; then the same ASCII case-insensitive
+// aho-corasick matcher as @pm.
+std::vector<std::string> pm_file_phrases(const std::string& data) {
+  std::vector<std::string> out;
+  size_t pos = 0;
+  while (pos < data.size()) {
+    size_t nl = data.find('\n', pos);
+    if (nl == std::string::npos) nl = data.size();
+    std::string l = data.substr(pos, nl - pos);
+    pos = nl + 1;
+    if (!l.empty() && l.back() == '\r') l.pop_back();
+    l = trim(l);
+    if (l.empty() || l[0] == '#') continue;
+    out.push_back(lower(l));
+  }
+  return out;
+}
+
 void parse_operator(std::string opstr, IrRule* rule) {
   if (opstr.empty() || (opstr[0] != '@' && (opstr.size() < 2 || opstr[1] != '@'))) opstr = "@rx " + opstr;
   std::string raw, data;
@@ -342,11 +366,15 @@ void parse_operator(std::string opstr, IrRule* rule) {
   static const char* known[] = {"rx", "pm", "contains", "containsword", "streq", "beginswith",
                                 "endswith", "within", "eq", "ge", "gt", "le", "lt",
                                 "unconditionalmatch", "nomatch", "validatebyterange",
-                                "validateurlencoding", "validateutf8encoding"};
+                                "validateurlencoding", "validateutf8encoding", "pmfromfile"};
   bool ok = false;
   for (auto* k : known)
     if (rule->op_name == k) ok = true;
   if (!ok) unsup("unsupported operator @" + name);
+  if (rule->op_name == "pmfromfile") {
+    if (!g_data_files || !g_data_files->count(data)) perr("open " + data + ": no such file or directory");
+    rule->phrases = pm_file_phrases(g_data_files->at(data));
+  }
   if (rule->op_name == "rx") {
     Regex re;
     std::string err;
@@ -751,6 +779,11 @@ struct Lower {
         pos = sp + 1;
       }
       o.dfa = phrase_dfa(phrases, true, "pm:" + la);
+    } else if (n == "pmfromfile") {
+      o.kind = OP_PM;
+      std::string key = "pmf:";
+      for (auto& p : r.phrases) key.append(p).push_back('\n');
+      o.dfa = phrase_dfa(r.phrases, true, key);
     } else if (n == "unconditionalmatch") {
       o.kind = OP_UNCONDITIONAL;
     } else if (n == "nomatch") {
@@ -978,7 +1011,7 @@ struct Lower {
   int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
     if (!r.has_op || no_scan) return -1;
     const std::string& n = r.op_name;
-    bool scannable = n == "rx" || n == "pm" || n == "validatebyterange" || n == "validateurlencoding" ||
+    bool scannable = n == "rx" || n == "pm" || n == "pmfromfile" || n == "validatebyterange" || n == "validateurlencoding" ||
                      n == "validateutf8encoding" || (n == "contains" && r.op_arg.find("%{") == std::string::npos);
     if (!scannable) return -1;
     bool bodydep = false, residual = false;
@@ -1112,6 +1145,9 @@ struct Lower {
       if (o.kind == OP_RX) {
         pe.kind = 0;
         pe.rx = "(?sm)" + r.op_arg;
+      } else if (o.kind == OP_PM && r.op_name == "pmfromfile") {
+        pe.kind = 1;
+        pe.phrases = r.phrases;
       } else if (o.kind == OP_PM) {
         pe.kind = 1;
         std::string la = lower(r.op_arg);
@@ -1531,7 +1567,11 @@ static bool capture_observable(const IrWaf& waf, const std::vector<std::string>&
 }
 
 int compile_program(const std::string& text, const std::vector<std::string>& exports, uint32_t cap,
-                    Program* out, std::string* err) {
+                    Program* out, std::string* err, const std::map<std::string, std::string>* data_files) {
+  struct FilesScope {
+    explicit FilesScope(const std::map<std::string, std::string>* f) { g_data_files = f; }
+    ~FilesScope() { g_data_files = nullptr; }
+  } files_scope(data_files);
   try {
     IrWaf waf = parse_seclang(text);
     Lower L;

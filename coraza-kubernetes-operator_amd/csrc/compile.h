@@ -2,6 +2,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <map>
 #include <string>
 #include <vector>
 
@@ -53,7 +54,10 @@ struct Program {
 };
 
 // Returns 0, -1 (parse error) or -2 (unsupported); *err holds the message.
+// data_files: @pmFromFile contents by the name the rule gives (Coraza reads
+// them from the rules' directory; here the caller supplies them).
 int compile_program(const std::string& text, const std::vector<std::string>& exports, uint32_t dfa_cap,
-                    Program* out, std::string* err);
+                    Program* out, std::string* err,
+                    const std::map<std::string, std::string>* data_files = nullptr);
 
 }  // namespace gi

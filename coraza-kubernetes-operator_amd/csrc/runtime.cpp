@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -57,7 +58,7 @@ hipError_t upload(DevBuf* b, const std::vector<T>& v, hipStream_t s) {
 const std::vector<std::string> kDefaultExports = {
     "blocking_inbound_anomaly_score", "inbound_anomaly_score_pl1", "inbound_anomaly_score_pl2",
     "inbound_anomaly_score_pl3", "inbound_anomaly_score_pl4", "detection_inbound_anomaly_score",
-    "anomaly_score", "0"};
+    "anomaly_score"};
 
 // Phase-A arena sizing factor (GI_PA_FACTOR overrides; see gi_stage_batch).
 // Queue-pool sizing factor (GI_POOL_FACTOR overrides; see gi_stage_batch).
@@ -144,7 +145,24 @@ int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ru
   std::string msg;
   std::string digest_input(seclang, n);
   for (const auto& x : exports) digest_input.append("\0export:", 8).append(x);
-  int rc = compile_program(std::string(seclang, n), exports, opts ? opts->dfa_state_cap : 0, &rs->prog, &msg);
+  std::map<std::string, std::string> data_files;
+  if (opts && opts->n_data_files) {
+    if (!opts->data_file_names || !opts->data_file_data || !opts->data_file_lens) {
+      delete rs;
+      return GI_EINVAL;
+    }
+    for (uint32_t i = 0; i < opts->n_data_files; i++) {
+      if (!opts->data_file_names[i] || (!opts->data_file_data[i] && opts->data_file_lens[i])) {
+        delete rs;
+        return GI_EINVAL;
+      }
+      std::string body(opts->data_file_data[i] ? opts->data_file_data[i] : "", opts->data_file_lens[i]);
+      digest_input.append("\0file:", 6).append(opts->data_file_names[i]).append("\0", 1).append(body);
+      data_files[opts->data_file_names[i]] = std::move(body);
+    }
+  }
+  int rc = compile_program(std::string(seclang, n), exports, opts ? opts->dfa_state_cap : 0, &rs->prog, &msg,
+                           &data_files);
   if (rc != 0) {
     if (err && errcap) {
       size_t k = std::min(errcap - 1, msg.size());

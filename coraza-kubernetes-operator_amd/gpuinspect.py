@@ -80,7 +80,9 @@ class EngineError(RuntimeError):
 
 
 class _CompileOpts(ctypes.Structure):
-    _fields_ = [("tx_exports", ctypes.POINTER(ctypes.c_char_p)), ("dfa_state_cap", ctypes.c_uint32)]
+    _fields_ = [("tx_exports", ctypes.POINTER(ctypes.c_char_p)), ("dfa_state_cap", ctypes.c_uint32),
+                ("n_data_files", ctypes.c_uint32), ("data_file_names", ctypes.POINTER(ctypes.c_char_p)),
+                ("data_file_data", ctypes.POINTER(ctypes.c_char_p)), ("data_file_lens", ctypes.POINTER(ctypes.c_size_t))]
 
 
 class _Info(ctypes.Structure):
@@ -178,13 +180,24 @@ DEFAULT_EXPORTS = (
 class Ruleset:
     """A compiled RuleSet (immutable; share across Engines like a coraza WAF)."""
 
-    def __init__(self, text: str, tx_exports: Optional[Sequence[str]] = None, dfa_state_cap: int = 0):
+    def __init__(self, text: str, tx_exports: Optional[Sequence[str]] = None, dfa_state_cap: int = 0,
+                 data_files: Optional[dict] = None):
+        """data_files: {name: bytes} for @pmFromFile (Coraza reads them from the
+        rules' directory, internal/operators/pm_from_file.go)."""
         lib = load_library()
         self._lib = lib
         self.text = text
         self.exports = tuple(tx_exports) if tx_exports is not None else DEFAULT_EXPORTS
         arr = (ctypes.c_char_p * (len(self.exports) + 1))(*[e.encode() for e in self.exports], None)
-        opts = _CompileOpts(ctypes.cast(arr, ctypes.POINTER(ctypes.c_char_p)), dfa_state_cap)
+        files = sorted((data_files or {}).items())
+        nf = len(files)
+        names = (ctypes.c_char_p * max(nf, 1))(*[k.encode() for k, _ in files])
+        blobs = (ctypes.c_char_p * max(nf, 1))(*[bytes(v) for _, v in files])
+        lens = (ctypes.c_size_t * max(nf, 1))(*[len(v) for _, v in files])
+        opts = _CompileOpts(ctypes.cast(arr, ctypes.POINTER(ctypes.c_char_p)), dfa_state_cap, nf,
+                            ctypes.cast(names, ctypes.POINTER(ctypes.c_char_p)),
+                            ctypes.cast(blobs, ctypes.POINTER(ctypes.c_char_p)),
+                            ctypes.cast(lens, ctypes.POINTER(ctypes.c_size_t)))
         h = ctypes.c_void_p()
         err = ctypes.create_string_buffer(4096)
         raw = text.encode()

@@ -75,6 +75,15 @@ typedef struct {
    * detection_inbound_anomaly_score, anomaly_score, 0) */
   const char* const* tx_exports;
   uint32_t dfa_state_cap; /* 0 = default (60000) */
+  /* @pmFromFile data files (coraza internal/operators/pm_from_file.go reads
+   * them from disk; the reference build strips those rules because it is
+   * built with no_fs_access, Makefile:43).  The caller passes each file the
+   * rules name as (name, bytes); a rule naming a file not given here fails
+   * with GI_EPARSE, like a missing file in Coraza. */
+  uint32_t n_data_files;
+  const char* const* data_file_names;
+  const char* const* data_file_data;
+  const size_t* data_file_lens;
 } gi_compile_opts;
 
 typedef struct {

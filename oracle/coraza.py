@@ -348,7 +348,22 @@ def _has_macro(parts):
     return any(isinstance(p, tuple) for p in parts)
 
 
-def _parse_operator(opstr: str) -> Operator:
+def pm_file_phrases(data: bytes):
+    """coraza internal/operators/pm_from_file.go: bufio.Scanner lines (a
+    trailing '\\r' dropped), strings.TrimSpace, skip empty lines and '#'
+    comments, strings.ToLower (ASCII here, like the @pm matcher's folding)."""
+    out = []
+    for line in data.split(b"\n"):
+        if line.endswith(b"\r"):
+            line = line[:-1]
+        line = line.strip(b" \t\n\v\f\r")
+        if not line or line[:1] == b"#":
+            continue
+        out.append(line.lower())
+    return out
+
+
+def _parse_operator(opstr: str, data_files=None) -> Operator:
     # rule_parser.go ParseOperator: default operator is @rx
     if len(opstr) == 0 or (opstr[0] != "@" and (len(opstr) < 2 or opstr[1] != "@")):
         opstr = "@rx " + opstr
@@ -372,6 +387,10 @@ def _parse_operator(opstr: str) -> Operator:
             raise SecLangError("invalid regex %r: %s" % (data, e))
     elif name_l == "pm":
         op.phrases = [p.encode().lower() for p in data.lower().split(" ") if p]
+    elif name_l == "pmfromfile":
+        if data_files is None or data not in data_files:
+            raise SecLangError("open %s: no such file or directory" % data)
+        op.phrases = pm_file_phrases(data_files[data])
     elif name_l in ("contains", "streq", "beginswith", "endswith", "within",
                     "eq", "ge", "gt", "le", "lt", "containsword"):
         op.macro = parse_macro(data)
@@ -500,7 +519,7 @@ def merge_default_actions(actions, defaults):
     return res
 
 
-def parse_seclang(text: str) -> WafConfig:
+def parse_seclang(text: str, data_files=None) -> WafConfig:
     cfg = WafConfig()
     pending_parent: Optional[Rule] = None
     chain_tail: Optional[Rule] = None
@@ -544,7 +563,7 @@ def parse_seclang(text: str) -> WafConfig:
                 _parse_variables(vars_s, rule)
                 rest = rest.strip()
                 opstr, rest = _cut_quoted(rest)
-                rule.op = _parse_operator(opstr)
+                rule.op = _parse_operator(opstr, data_files)
                 rest = rest.strip()
                 acts_s = rest.strip('"') if rest else ""
             else:
@@ -1548,7 +1567,7 @@ class Transaction:
                     res = True
             else:
                 res = op.rx.match_string(value)
-        elif n == "pm":
+        elif n in ("pm", "pmfromfile"):
             low = value.lower()
             if rule.capture:
                 caps = _pm_find_all(op.phrases, low, value)

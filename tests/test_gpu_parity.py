@@ -163,3 +163,42 @@ def test_gpu_parity_capture_logdata_only():
         txs.append(t)
     res = _parity(CAPTURE, gpuinspect.pack(txs))
     assert [int(v["status"]) for v in res.verdicts] == [403, 403, 0, 0, 403]
+
+
+PMF_RULES = """SecRuleEngine On
+SecRule ARGS|REQUEST_HEADERS:User-Agent "@pmFromFile scanners.data" "id:10,phase:2,deny,status:403,t:none,t:lowercase"
+SecRule ARGS_NAMES "!@pmFromFile allow.data" "id:11,phase:2,pass"
+SecRule ARGS "@pmFromFile empty.data" "id:12,phase:2,deny,status:403"
+"""
+PMF_FILES = {
+    "scanners.data": b"# scanner user agents\r\nNikto\r\n  sqlmap  \n\n#comment\nunion select\nEvil Monkey",
+    "allow.data": b"q\nid\n",
+    "empty.data": b"# nothing\n\n",
+}
+
+
+def test_gpu_parity_pmfromfile():
+    """@pmFromFile (coraza pm_from_file.go): phrases from a caller-supplied
+    data file, the same ASCII case-insensitive matcher as @pm, phase-A
+    scanned; GPU vs oracle over seeded traffic plus targeted values."""
+    rs = gpuinspect.Ruleset(PMF_RULES, data_files=PMF_FILES)
+    eng = gpuinspect.Engine(rs, matched_cap=128)
+    txs = []
+    for q in (b"q=NIKTO", b"id=1+UNION+SELECT+2", b"q=evil%20monkey", b"q=safe", b"x=1", b"q=sqlmap&id=2", b"q="):
+        t = gpuinspect.Transaction(method=b"GET", uri=b"/?" + q)
+        t.add_request_header("Host", "x")
+        t.add_request_header("User-Agent", "Mozilla/5.0")
+        txs.append(t)
+    t = gpuinspect.Transaction(method=b"GET", uri=b"/")
+    t.add_request_header("User-Agent", "sqlmap/1.7")
+    txs.append(t)
+    batch = gpuinspect.pack(txs)
+    res = eng.inspect(batch)
+    cfg = coraza.parse_seclang(PMF_RULES, PMF_FILES)
+    bad = compare.compare(res, compare.oracle_verdicts(cfg, batch, rs.exports, range(batch.n_req)))
+    assert not bad, bad
+    assert [int(v["status"]) for v in res.verdicts] == [403, 403, 403, 0, 0, 403, 0, 403]
+    big = traffic.TrafficGen(traffic.SEED + 7).batch(1000, attack_rate=0.3)
+    res = eng.inspect(big)
+    bad = compare.compare(res, compare.oracle_verdicts(cfg, big, rs.exports, range(big.n_req)))
+    assert not bad, bad

@@ -118,3 +118,34 @@ def test_capture_exported_is_unsupported():
     with pytest.raises(gpuinspect.SecLangError) as e:
         gpuinspect.Ruleset(CAPTURE_LOGDATA, tx_exports=["score", "0"])
     assert e.value.code == gpuinspect.GI_EUNSUPPORTED
+
+
+PMF_RULES = """SecRuleEngine On
+SecRule ARGS|REQUEST_HEADERS:User-Agent "@pmFromFile scanners.data" "id:10,phase:2,deny,status:403,t:none,t:lowercase"
+SecRule ARGS "!@pmFromFile allow.data" "id:11,phase:2,pass"
+"""
+PMF_FILES = {
+    "scanners.data": b"# scanner user agents\r\nNikto\r\n  sqlmap  \n\n#comment\nunion select\nEvil Monkey",
+    "allow.data": b"ok\nfine\n",
+}
+
+
+def test_pm_file_phrases_restatement():
+    assert coraza.pm_file_phrases(PMF_FILES["scanners.data"]) == [
+        b"nikto", b"sqlmap", b"union select", b"evil monkey"]
+    assert coraza.pm_file_phrases(b"") == []
+
+
+def test_pmfromfile_compiles_with_data_files():
+    coraza.parse_seclang(PMF_RULES, PMF_FILES)
+    rs = gpuinspect.Ruleset(PMF_RULES, data_files=PMF_FILES)
+    assert rs.info["n_rules"] == 2 and rs.info["n_hit_slots"] == 2  # both links are phase-A scanned
+
+
+def test_pmfromfile_missing_file_is_a_parse_error():
+    with pytest.raises(coraza.SecLangError):
+        coraza.parse_seclang(PMF_RULES, {"scanners.data": b"x"})
+    with pytest.raises(gpuinspect.SecLangError) as e:
+        gpuinspect.Ruleset(PMF_RULES, data_files={"scanners.data": b"x"})
+    assert e.value.code == gpuinspect.GI_EPARSE
+    assert "allow.data" in str(e.value)
