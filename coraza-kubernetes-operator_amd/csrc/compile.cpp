@@ -1009,7 +1009,9 @@ struct Lower {
   bool capture_seen = true;  // some rule, macro or export can read TX:0-TX:9 (capture_observable)
 
   int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
-    if (!r.has_op || no_scan) return -1;
+    // multiMatch links test every intermediate value, not the one a stream
+    // produces: interpreter only
+    if (!r.has_op || no_scan || r.multimatch) return -1;
     const std::string& n = r.op_name;
     bool scannable = n == "rx" || n == "pm" || n == "pmfromfile" || n == "validatebyterange" || n == "validateurlencoding" ||
                      n == "validateutf8encoding" || (n == "contains" && r.op_arg.find("%{") == std::string::npos);
@@ -1420,7 +1422,7 @@ struct Lower {
     d.op = -1;
     if (r.capture && capture_seen)
       unsup("capture is not supported yet when a rule, macro or export reads TX:0-TX:9");
-    if (r.multimatch) unsup("multiMatch is not supported yet");
+    if (r.multimatch) d.flags |= RF_MULTIMATCH;
     const std::string& dis = r.disruptive;
     d.disruptive = dis == "deny" ? D_DENY : dis == "drop" ? D_DROP : dis == "redirect" ? D_REDIRECT
                    : dis == "pass" ? D_PASS : D_NONE;

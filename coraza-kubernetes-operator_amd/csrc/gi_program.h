@@ -130,6 +130,7 @@ enum RuleFlags : uint8_t {
   RF_CAPTURE = 4,
   RF_BODYDEP = 8,  // targets can see ARGS_POST: phase-A bits ignored once a body was parsed
   RF_RESIDUAL = 16,  // some targets are residual (DVarRef.residual): a clear bit still tests them
+  RF_MULTIMATCH = 32,  // multiMatch: the operator runs on the value and after every transformation
 };
 
 enum ActKind : uint8_t {

@@ -1635,12 +1635,14 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
 
 // ------------------------------------------------------------ evaluation
 // Apply the rule's transformation chain; returns the value to test.
-__device__ __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uint32_t vn, bool* ok) {
+__device__ __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uint32_t vn, bool* ok,
+                                       uint32_t kmax = 0xffffffffu) {
   const DProgram& P = *t.P;
   Str cur{v, vn};
   *ok = true;
-  uint32_t summ = R.tchain_len ? value_summary(v, vn) : 0u;
-  for (uint32_t k = 0; k < R.tchain_len; k++) {
+  const uint32_t kn = min(kmax, R.tchain_len);
+  uint32_t summ = kn ? value_summary(v, vn) : 0u;
+  for (uint32_t k = 0; k < kn; k++) {
     const uint8_t code = P.tchains[R.tchain_off + k];
     if (!(summ & transform_triggers(code))) continue;  // identity on this value
     uint8_t* dst = (cur.p == t.t0) ? t.t1 : t.t0;
@@ -1686,16 +1688,25 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
   return false;
 }
 
-// Test one value: transform, operator, per-match actions.  Returns 1 on match.
+// Test one value: transform, operator, per-match actions.  Returns the number of matches.
+// multiMatch (coraza internal/corazawaf/rule.go executeTransformationsMultimatch):
+// the operator runs on the untransformed value and again after each
+// transformation of the chain; every match counts and runs the actions.  One
+// eval_op / run_actions site serves both forms (the Tx stays in registers).
 __device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn) {
-  bool ok;
-  Str tv = transform(t, R, v, vn, &ok);
-  if (!ok) return 0;
-  if (eval_op(t, o, tv.p, tv.n)) {
-    run_actions(t, R);
-    return 1;
+  // candidate kk = the value after the first kk transformations (a multiMatch
+  // link re-runs the short chain prefix per candidate: few registers, rare path)
+  uint32_t nm = 0;
+  for (uint32_t kk = (R.flags & RF_MULTIMATCH) ? 0u : R.tchain_len; kk <= R.tchain_len; kk++) {
+    bool ok;
+    const Str tv = transform(t, R, v, vn, &ok, kk);
+    if (!ok) break;
+    if (eval_op(t, o, tv.p, tv.n)) {
+      run_actions(t, R);
+      nm++;
+    }
   }
-  return 0;
+  return nm;
 }
 
 // Rule.doEvaluate for one link -> number of matched values.

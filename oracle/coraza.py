@@ -1676,16 +1676,23 @@ class Transaction:
             nmatch = 1
             self.run_nondisruptive(rule)
         else:
-            if rule.multimatch:
-                raise UnsupportedInput("multiMatch")
             for rv in rule.variables:
                 for k, v in self.get_field(rv):
-                    tv = self.transform(rule, v)
-                    if self.eval_op(rule, tv):
-                        nmatch += 1
-                        self.single["MATCHED_VAR"] = tv
-                        self.single["MATCHED_VAR_NAME"] = (rv.name + (":" if k else "")).encode() + k
-                        self.run_nondisruptive(rule)
+                    if rule.multimatch:
+                        # rule.go executeTransformationsMultimatch: the value,
+                        # then the value after each transformation
+                        cands = [v]
+                        for t in rule.transforms:
+                            v = TRANSFORM_FNS[t](v)
+                            cands.append(v)
+                    else:
+                        cands = [self.transform(rule, v)]
+                    for tv in cands:
+                        if self.eval_op(rule, tv):
+                            nmatch += 1
+                            self.single["MATCHED_VAR"] = tv
+                            self.single["MATCHED_VAR_NAME"] = (rv.name + (":" if k else "")).encode() + k
+                            self.run_nondisruptive(rule)
         if nmatch == 0:
             return 0
         if rule.parent_id == 0:

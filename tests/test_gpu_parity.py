@@ -202,3 +202,31 @@ def test_gpu_parity_pmfromfile():
     res = eng.inspect(big)
     bad = compare.compare(res, compare.oracle_verdicts(cfg, big, rs.exports, range(big.n_req)))
     assert not bad, bad
+
+
+MULTI = """SecRuleEngine On
+SecRule ARGS "@rx ^abc$" "id:1,phase:2,pass,multiMatch,t:lowercase,setvar:'tx.anomaly_score=+1'"
+SecRule ARGS "@contains %3c" "id:2,phase:2,pass,multiMatch,t:none,t:urlDecodeUni,t:lowercase,setvar:'tx.anomaly_score=+10'"
+SecRule ARGS|REQUEST_HEADERS:User-Agent "@rx <script" "id:3,phase:2,pass,multiMatch,t:urlDecodeUni,t:htmlEntityDecode,setvar:'tx.anomaly_score=+100'"
+SecRule ARGS "@rx ^abc$" "id:4,phase:2,pass,t:lowercase,setvar:'tx.anomaly_score=+1000'"
+SecRule TX:ANOMALY_SCORE "@ge 1002" "id:9,phase:2,deny,status:403"
+"""
+
+
+def test_gpu_parity_multimatch():
+    """multiMatch (rule.go executeTransformationsMultimatch): the operator runs
+    on the raw value and after every transformation, each match counting (and
+    running setvar) once; interpreter-only links.  The exported anomaly_score
+    pins the match counts; GPU vs oracle."""
+    txs = []
+    for q in (b"a=ABC", b"a=abc", b"a=%253c", b"a=%253C", b"a=%253Cscript", b"a=%26lt;script", b"a=safe", b"a=abc&b=ABC"):
+        t = gpuinspect.Transaction(method=b"GET", uri=b"/?" + q)
+        t.add_request_header("Host", "x")
+        t.add_request_header("User-Agent", "Mozilla/5.0")
+        txs.append(t)
+    res = _parity(MULTI, gpuinspect.pack(txs))
+    ai = list(gpuinspect.DEFAULT_EXPORTS).index("anomaly_score")
+    scores = [int(v["tx_export"][ai]) for v in res.verdicts]
+    assert scores[:2] == [1001, 1002]
+    batch = traffic.TrafficGen(traffic.SEED + 9).batch(800, attack_rate=0.3)
+    _parity(MULTI, batch)
