@@ -149,3 +149,11 @@ def test_pmfromfile_missing_file_is_a_parse_error():
         gpuinspect.Ruleset(PMF_RULES, data_files={"scanners.data": b"x"})
     assert e.value.code == gpuinspect.GI_EPARSE
     assert "allow.data" in str(e.value)
+
+
+def test_multimatch_links_are_interpreter_only():
+    text = ('SecRule ARGS "@rx ^abc$" "id:1,phase:2,pass,multiMatch,t:lowercase"\n'
+            'SecRule ARGS "@rx ^abc$" "id:2,phase:2,pass,t:lowercase"')
+    coraza.parse_seclang(text)
+    rs = gpuinspect.Ruleset(text)
+    assert rs.info["n_rules"] == 2 and rs.info["n_hit_slots"] == 1  # only rule 2 is phase-A scanned
