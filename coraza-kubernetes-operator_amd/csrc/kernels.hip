@@ -3169,12 +3169,17 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
       GI_LAUNCH("k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
                 S.n_global, S.mode, 2u);
     GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
-    if (P.n_body_links) GI_LAUNCH("k_body", k_body, dim3((B.n_req + 255) / 256), dim3(256), 0, stream, P, B);
+    // one wave per workgroup: a body batch (C3: 25k POSTs of 50k) has too few
+    // requests to fill 256 CUs with 4-wave workgroups
+    if (P.n_body_links) GI_LAUNCH("k_body", k_body, dim3((B.n_req + 63) / 64), dim3(64), 0, stream, P, B);
   } else if (ev) {
     (void)hipEventRecord(ev[1], stream);
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
-  GI_LAUNCH("k_eval", k_eval, dim3((B.n_req + 127) / 128), dim3(128), 0, stream, P, B);
+  {  // small batches (fewer than 4 workgroups of 128 per CU): one wave per workgroup to spread over all CUs
+    const uint32_t ev_bs = (B.n_req + 127) / 128 < 1024 ? 64u : 128u;
+    GI_LAUNCH("k_eval", k_eval, dim3((B.n_req + ev_bs - 1) / ev_bs), dim3(ev_bs), 0, stream, P, B);
+  }
 }
 
 }  // namespace gi
