@@ -26,7 +26,7 @@ from typing import Callable, Dict, Optional, Sequence
 
 import gpuinspect
 
-ARTIFACT_VERSION = 1
+ARTIFACT_VERSION = 2  # csrc/artifact.h kArtifactVersion
 
 
 def fnv64(data: bytes, h: int = 1469598103934665603) -> int:
@@ -35,25 +35,34 @@ def fnv64(data: bytes, h: int = 1469598103934665603) -> int:
     return h
 
 
-def source_digest(rules: str, exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS) -> int:
-    """The digest gi_compile stores in the artifact (runtime.cpp gi_compile)."""
+def source_digest(rules: str, exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS,
+                  data_files: Optional[Dict[str, bytes]] = None) -> int:
+    """The digest gi_compile stores in the artifact (runtime.cpp gi_compile):
+    the rules text, the export list, the compiler revision and the
+    @pmFromFile data files (by name, in the order Ruleset passes them)."""
     data = rules.encode() + b"".join(b"\0export:" + e.encode() for e in exports)
+    data += b"\0compiler:" + gpuinspect.compiler_rev().encode()
+    for name, body in sorted((data_files or {}).items()):
+        data += b"\0file:" + name.encode() + b"\0" + bytes(body)
     return fnv64(data)
 
 
-def entry(uuid: str, timestamp: str, rules: str, ruleset: Optional[gpuinspect.Ruleset] = None) -> Dict:
+def entry(uuid: str, timestamp: str, rules: str, ruleset: Optional[gpuinspect.Ruleset] = None,
+          data_files: Optional[Dict[str, bytes]] = None) -> Dict:
     """RuleSetEntry JSON plus the GPU artifact of `rules`."""
-    rs = ruleset if ruleset is not None else gpuinspect.Ruleset(rules)
+    rs = ruleset if ruleset is not None else gpuinspect.Ruleset(rules, data_files=data_files)
     return {"uuid": uuid, "timestamp": timestamp, "rules": rules,
             "gpu_artifact": base64.b64encode(rs.save()).decode(),
             "gpu_artifact_version": ARTIFACT_VERSION,
             "gpu_source_digest": "%016x" % rs.info["source_digest"]}
 
 
-def ruleset_from_entry(e: Dict, exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS) -> gpuinspect.Ruleset:
-    """The entry's program: its artifact if it belongs to `rules`, else a compile."""
+def ruleset_from_entry(e: Dict, exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS,
+                       data_files: Optional[Dict[str, bytes]] = None) -> gpuinspect.Ruleset:
+    """The entry's program: its artifact if it belongs to `rules` (and to the
+    data files the poller holds), else a compile of `rules`."""
     art = e.get("gpu_artifact")
-    want = source_digest(e["rules"], exports)
+    want = source_digest(e["rules"], exports, data_files)
     if art and e.get("gpu_artifact_version") == ARTIFACT_VERSION and \
             e.get("gpu_source_digest") == "%016x" % want:
         try:
@@ -62,18 +71,22 @@ def ruleset_from_entry(e: Dict, exports: Sequence[str] = gpuinspect.DEFAULT_EXPO
                 return rs
         except gpuinspect.SecLangError:
             pass  # corrupted / other build: recompile below
-    return gpuinspect.Ruleset(e["rules"], tx_exports=exports)
+    return gpuinspect.Ruleset(e["rules"], tx_exports=exports, data_files=data_files)
 
 
 class RulesetPoller:
     """Reloads an engine's ruleset when the cache's latest UUID changes."""
 
     def __init__(self, engine, fetch_latest: Callable[[], Dict], fetch_entry: Callable[[str], Dict],
-                 exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS):
+                 exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS,
+                 data_files: Optional[Dict[str, bytes]] = None):
+        """data_files: the @pmFromFile files the rules name ({name: bytes});
+        they are part of the artifact's source digest and of a recompile."""
         self.engine = engine
         self.fetch_latest = fetch_latest  # -> {"uuid", "timestamp"} (handleLatest)
         self.fetch_entry = fetch_entry    # uuid -> entry() (handleGetRules)
         self.exports = tuple(exports)
+        self.data_files = dict(data_files or {})
         self.uuid: Optional[str] = None
         self.ruleset: Optional[gpuinspect.Ruleset] = None
         self.loaded_from_artifact = False
@@ -84,7 +97,7 @@ class RulesetPoller:
         if latest["uuid"] == self.uuid:
             return False
         e = self.fetch_entry(latest["uuid"])
-        rs = ruleset_from_entry(e, self.exports)
+        rs = ruleset_from_entry(e, self.exports, self.data_files)
         self.loaded_from_artifact = rs.text is None
         self.engine.swap(rs)
         self.ruleset = rs  # the engine borrows it: keep it alive

@@ -12,6 +12,8 @@
 
 #include <string.h>
 
+#include "../../include/gpuinspect.h"
+
 namespace gi {
 
 uint64_t fnv64(const uint8_t* p, size_t n, uint64_t h) {
@@ -28,7 +30,10 @@ struct Scalars {
   uint32_t item_singles, n_hit_slots, n_union_dfas, max_img_bytes, max_big_img_bytes, n_slots, n_markers;
   uint8_t rule_engine, body_access, _pad[6];
   uint64_t body_limit, source_digest;
+  uint64_t compiler_rev;  // fnv64 of kCompilerRev
 };
+
+uint64_t compiler_rev_hash() { return fnv64((const uint8_t*)kCompilerRev, strlen(kCompilerRev)); }
 
 // One entry per Program vector: tag, member.  Order = file order.
 #define GI_ART_VECTORS(X)                                                                                     \
@@ -87,6 +92,7 @@ std::vector<uint8_t> serialize_program(const Program& P) {
   s.body_access = P.body_access;
   s.body_limit = P.body_limit;
   s.source_digest = P.source_digest;
+  s.compiler_rev = compiler_rev_hash();
   w.section(kTagScalars, sizeof(Scalars), 1, &s);
   w.section(kTagPlan, 1, P.plan_json.size(), P.plan_json.data());
   std::string names;
@@ -155,6 +161,7 @@ bool deserialize_program(const uint8_t* buf, size_t n, Program* P, std::string* 
         if (esz != sizeof(Scalars) || cnt != 1) return bad("scalars");
         Scalars s;
         memcpy(&s, p, sizeof(s));
+        if (s.compiler_rev != compiler_rev_hash()) return bad("written by another compiler revision");
         memcpy(out.item_sides, s.item_sides, 8);
         out.item_singles = s.item_singles;
         out.n_hit_slots = s.n_hit_slots;
@@ -191,20 +198,174 @@ bool deserialize_program(const uint8_t* buf, size_t n, Program* P, std::string* 
   }
   if (!seen_scalars) return bad("no scalars section");
   if (off != n) return bad("trailing bytes");
+  if (out.exports.size() != out.export_names.size()) return bad("exports");
   // cross-references the kernels trust: indices must stay inside their tables
-  for (uint32_t t : out.top)
-    if (t >= out.rules.size()) return bad("top-level rule index");
-  for (uint32_t t : out.body_links)
-    if (t >= out.rules.size()) return bad("body link index");
-  for (const DRule& r : out.rules) {
-    if ((uint64_t)r.var_begin + r.var_count > out.vars.size() || (r.op >= 0 && (uint32_t)r.op >= out.ops.size()) ||
-        (uint64_t)r.act_begin + r.act_count > out.acts.size() ||
-        (uint64_t)r.tchain_off + r.tchain_len > out.tchains.size() ||
-        (r.chain_next >= 0 && (uint32_t)r.chain_next >= out.rules.size()))
+  std::string verr;
+  if (!validate_program(out, &verr)) return bad(verr);
+  *P = std::move(out);
+  return true;
+}
+
+bool validate_program(const Program& P, std::string* err) {
+  auto bad = [&](const std::string& m) {
+    *err = m;
+    return false;
+  };
+  auto in = [](uint64_t off, uint64_t len, size_t size) { return off <= size && len <= size - off; };
+  const size_t nrules = P.rules.size(), ndfa = P.dfas.size(), nstr = P.strpool.size(), ntm = P.tmpls.size();
+  const uint32_t nslot = P.n_slots, nhit = P.n_hit_slots;
+  if (P.slot_names.size() < 2ull * nslot) return bad("slot names");
+  for (uint32_t s = 0; s < nslot; s++)
+    if (!in(P.slot_names[2 * s], P.slot_names[2 * s + 1], nstr)) return bad("slot name range");
+  if (P.exports.size() > GI_MAX_EXPORTS) return bad("export count");
+  for (int32_t x : P.exports)
+    if (x >= (int32_t)nslot) return bad("export slot");
+  if (P.item_singles >> S_COUNT) return bad("item singles");
+  // automata
+  for (size_t i = 0; i < ndfa; i++) {
+    const DDfa& d = P.dfas[i];
+    if (d.n_states == 0 || d.n_states > 32768 || d.n_classes == 0 || d.n_classes > 256 || d.start >= d.n_states)
+      return bad("automaton shape");
+    const uint64_t nt = (uint64_t)d.n_states * d.n_classes;
+    if (!in(d.trans_off, nt, P.trans.size())) return bad("automaton transitions");
+    for (uint64_t k = 0; k < nt; k++) {
+      const uint32_t nx = d.multi ? (P.trans[d.trans_off + k] & 0x7FFFu) : P.trans[d.trans_off + k];
+      if (nx >= d.n_states) return bad("automaton transition target");
+    }
+    const uint32_t amn = d.byte_mode ? 256 : 128;
+    if (!in(d.amap_off, amn, P.u8pool.size())) return bad("automaton class map");
+    for (uint32_t k = 0; k < amn; k++)
+      if (P.u8pool[d.amap_off + k] >= d.n_classes) return bad("automaton class");
+    if (!in(d.nr_off, 3ull * d.nr_cnt, P.nranges.size())) return bad("automaton rune ranges");
+    for (uint32_t k = 0; k < d.nr_cnt; k++)
+      if (P.nranges[d.nr_off + 3 * k + 2] >= d.n_classes) return bad("automaton rune class");
+    if (d.nonascii_cls >= d.n_classes) return bad("automaton non-ASCII class");
+    if (d.multi) {
+      if (!in(d.combo_off, d.n_classes, P.u8pool.size())) return bad("automaton combos");
+      for (uint32_t k = 0; k < d.n_classes; k++)
+        if (P.u8pool[d.combo_off + k] > 4) return bad("automaton combo");
+      if (!in(d.acc_off, 5ull * d.n_states, P.u64pool.size())) return bad("automaton accept masks");
+    } else if (!in(d.endacc_off, d.n_states, P.u8pool.size())) {
+      return bad("automaton end accept");
+    }
+  }
+  auto single_dfa = [&](int32_t id) { return id >= 0 && (size_t)id < ndfa && !P.dfas[id].multi; };
+  // templates
+  for (const DTmpl& t : P.tmpls)
+    if (!in(t.part_begin, t.part_count, P.tparts.size())) return bad("template parts");
+  for (const DTmplPart& p : P.tparts) {
+    if (p.kind == TP_TX && (p.slot < 0 || (uint32_t)p.slot >= nslot)) return bad("template TX slot");
+    if (p.kind == TP_SINGLE && p.single >= S_COUNT) return bad("template variable");
+    if ((p.kind == TP_LIT || p.kind == TP_HEADER) && !in(p.off, p.len, nstr)) return bad("template string");
+  }
+  // rule records
+  for (uint32_t t : P.top)
+    if (t >= nrules) return bad("top-level rule index");
+  for (const DRule& r : P.rules) {
+    if (!in(r.var_begin, r.var_count, P.vars.size()) || (r.op >= 0 && (uint32_t)r.op >= P.ops.size()) ||
+        !in(r.act_begin, r.act_count, P.acts.size()) || !in(r.tchain_off, r.tchain_len, P.tchains.size()) ||
+        (r.chain_next >= 0 && (uint32_t)r.chain_next >= nrules) || r.phase > 5 ||
+        (r.hit_slot >= 0 && (uint32_t)r.hit_slot >= nhit) || r.hit_slot < -1)
       return bad("rule record out of range");
   }
-  if (out.exports.size() != out.export_names.size()) return bad("exports");
-  *P = std::move(out);
+  for (uint32_t t : P.body_links)
+    if (t >= nrules || P.rules[t].op < 0 || P.rules[t].hit_slot < 0) return bad("body link");
+  for (const DVarRef& v : P.vars) {
+    if (v.key_mode == 1 && !in(v.key_off, v.key_len, nstr)) return bad("variable key");
+    if (v.key_mode == 2 && !single_dfa(v.key_dfa)) return bad("variable key automaton");
+    if (v.key_mode > 2) return bad("variable key mode");
+    if (!in(v.exc_begin, v.exc_count, P.excs.size())) return bad("variable exceptions");
+    if (v.var == V_TX && v.slot >= (int32_t)nslot) return bad("variable TX slot");
+  }
+  for (const DExc& x : P.excs) {
+    if (x.dfa >= 0 ? !single_dfa(x.dfa) : !in(x.off, x.len, nstr)) return bad("exception");
+  }
+  for (const DOp& o : P.ops) {
+    if ((o.kind == OP_RX || o.kind == OP_PM) && !single_dfa(o.dfa)) return bad("operator automaton");
+    if (o.dfa >= 0 && !single_dfa(o.dfa)) return bad("operator automaton index");
+    if (o.tmpl >= 0 && (size_t)o.tmpl >= ntm) return bad("operator template");
+    if (o.arg_is_lit && !in(o.lit_off, o.lit_len, nstr)) return bad("operator literal");
+  }
+  for (const DAction& a : P.acts) {
+    if (a.kind == A_SETVAR || a.kind == A_SETVAR_DEL) {
+      if (a.slot < 0 || (uint32_t)a.slot >= nslot) return bad("setvar slot");
+      if (a.tmpl >= 0 && (size_t)a.tmpl >= ntm) return bad("setvar template");
+      if ((a.a == SV_ADD_SLOT || a.a == SV_SUB_SLOT) && (a.b < 0 || (uint64_t)a.b >= nslot)) return bad("setvar source");
+    }
+  }
+  // phase-A scan plan
+  if (P.streams.size() > GI_MAX_STREAMS || P.filters.size() > GI_MAX_GFILTERS) return bad("scan plan size");
+  const uint32_t ngf = (uint32_t)P.filters.size();
+  for (const DFilter& f : P.filters) {
+    if (f.single != GI_NO_SINGLE && f.single >= S_COUNT) return bad("filter variable");
+    if (f.key_mode == 1 && !in(f.key_off, f.key_len, nstr)) return bad("filter key");
+    if (f.key_mode == 2 && !single_dfa(f.key_dfa)) return bad("filter key automaton");
+    if (!in(f.exc_begin, f.exc_count, P.excs.size())) return bad("filter exceptions");
+  }
+  for (uint8_t g : P.sfilt)
+    if (g >= ngf) return bad("stream filter id");
+  for (const DStream& s : P.streams) {
+    if (!in(s.tchain_off, s.tchain_len, P.tchains.size()) || !in(s.filt_begin, s.filt_count, P.sfilt.size()) ||
+        !in(s.job_begin, s.job_count, P.jobs.size()) || !in(s.val_begin, s.val_count, P.svals.size()))
+      return bad("stream record");
+  }
+  for (const DScanVal& v : P.svals)
+    if (v.slot >= nhit) return bad("validate slot");
+  for (const DPat& p : P.pats)
+    if (p.slot >= nhit) return bad("pattern slot");
+  for (uint32_t s : P.always_slots)
+    if (s >= nhit) return bad("always slot");
+  if (P.max_img_bytes > GI_JOB_LDS_BYTES || P.max_big_img_bytes > GI_BIG_LDS_BYTES + 4096) return bad("image limits");
+  for (const DJob& J : P.jobs) {
+    if (J.stream >= P.streams.size() || !in(J.img_off, J.img_bytes, P.images.size()) ||
+        !in(J.jdfa_begin, J.jdfa_count, P.jdfas.size()) || J.jdfa_count == 0 || J.jdfa_count > GI_JOB_MAX_DFA)
+      return bad("job record");
+    if (J.lds && J.img_bytes > (J.big ? P.max_big_img_bytes : P.max_img_bytes)) return bad("job image size");
+    const uint8_t* img = P.images.data() + J.img_off;
+    if (!in(J.lds_fmask, 8ull * J.jdfa_count * ngf, J.img_bytes) || J.img_bytes < 4 * 129) return bad("job fmask table");
+    for (uint32_t q = 0; q < J.jdfa_count; q++) {
+      const DJobDfa& jd = P.jdfas[J.jdfa_begin + q];
+      if (jd.dfa < 0 || (size_t)jd.dfa >= ndfa) return bad("job automaton");
+      const DDfa& d = P.dfas[jd.dfa];
+      if (jd.n_pat == 0 || jd.n_pat > 64 || !in(jd.pat_begin, jd.n_pat, P.pats.size()) ||
+          !in(jd.fmask_off, ngf, P.u64pool.size()))
+        return bad("job automaton patterns");
+      const uint64_t pm = jd.n_pat == 64 ? ~0ull : (1ull << jd.n_pat) - 1;
+      if (jd.neg_mask & ~pm) return bad("job negation mask");
+      for (uint32_t g = 0; g < ngf; g++) {
+        uint64_t m;
+        memcpy(&m, img + J.lds_fmask + 8ull * (q * ngf + g), 8);
+        if ((m | P.u64pool[jd.fmask_off + g]) & ~pm) return bad("job filter mask");
+      }
+      if (!J.lds) continue;
+      const uint64_t tb = 2ull * d.n_states * d.n_classes;
+      if (jd.lds_trans < 0 || !in((uint32_t)jd.lds_trans, tb, J.img_bytes) || (jd.lds_trans & 1)) return bad("image transitions");
+      if (jd.lds_endacc < 0 || !in((uint32_t)jd.lds_endacc, (d.multi ? 8ull : 1ull) * d.n_states, J.img_bytes) ||
+          (d.multi && (jd.lds_endacc & 7)))
+        return bad("image end accept");
+      if (jd.lds_slots < 0 || !in((uint32_t)jd.lds_slots, 4ull * jd.n_pat, J.img_bytes) || (jd.lds_slots & 3))
+        return bad("image slots");
+      if (d.multi && (jd.lds_combo < 0 || !in((uint32_t)jd.lds_combo, d.n_classes, J.img_bytes))) return bad("image combos");
+      for (uint64_t k = 0; k < (uint64_t)d.n_states * d.n_classes; k++) {
+        uint16_t tv;
+        memcpy(&tv, img + jd.lds_trans + 2 * k, 2);
+        if ((d.multi ? (tv & 0x7FFFu) : tv) >= d.n_states) return bad("image transition target");
+      }
+      for (uint32_t c = 0; c <= 128; c++) {
+        uint32_t jm;
+        memcpy(&jm, img + 4 * c, 4);
+        if (((jm >> (8 * q)) & 0xFFu) >= d.n_classes) return bad("image joint class map");
+      }
+      if (d.multi)
+        for (uint32_t c = 0; c < d.n_classes; c++)
+          if (img[jd.lds_combo + c] > 4) return bad("image combo");
+      for (uint32_t k = 0; k < jd.n_pat; k++) {
+        uint32_t sl;
+        memcpy(&sl, img + jd.lds_slots + 4 * k, 4);
+        if (sl >= nhit) return bad("image slot");
+      }
+    }
+  }
   return true;
 }
 

@@ -15,7 +15,7 @@
 
 namespace gi {
 
-constexpr uint32_t kArtifactVersion = 1;
+constexpr uint32_t kArtifactVersion = 2;
 
 // FNV-1a 64 (artifact checksum and SecLang source digest).
 uint64_t fnv64(const uint8_t* p, size_t n, uint64_t h = 1469598103934665603ull);
@@ -23,5 +23,10 @@ uint64_t fnv64(const uint8_t* p, size_t n, uint64_t h = 1469598103934665603ull);
 std::vector<uint8_t> serialize_program(const Program& P);
 // false + *err on a malformed, truncated, corrupted or foreign-version blob.
 bool deserialize_program(const uint8_t* buf, size_t n, Program* P, std::string* err);
+// Cross-reference check of a Program: every index and offset a kernel
+// dereferences (rule / variable / operator / action / template records,
+// automata tables, LDS job images, scan plan, hit slots, TX slots) lies inside
+// its table.  false + *err names the first violation.
+bool validate_program(const Program& P, std::string* err);
 
 }  // namespace gi

@@ -11,6 +11,13 @@
 
 namespace gi {
 
+// Compiler revision: bumped on every change to what a given SecLang text
+// compiles to (record semantics, phase-A eligibility, capture policy, ...),
+// even when the record layout stays the same.  gi_compile folds it into the
+// source digest and the artifact stores it, so an artifact written by another
+// compiler revision is rejected (and recompiled from the rules text).
+constexpr const char* kCompilerRev = "gi-seclang-compiler/2";
+
 struct Program {
   std::vector<DRule> rules;
   std::vector<uint32_t> top;

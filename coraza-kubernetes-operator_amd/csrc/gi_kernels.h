@@ -78,7 +78,6 @@ struct ScanLaunch {
 
 #define GI_STREAM_GRID 8192  // k_stream workgroups (64 lanes) per bucket launch (~8 waves/SIMD)
 #define GI_PCHUNK 2048       // pool words a k_stream wave reserves at a time
-#define GI_MAX_STREAMS 256   // streams a ruleset may have (k_stream keeps per-stream chunk state in LDS)
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.
 uint32_t scan_resident_blocks(uint32_t lds_bytes);

@@ -192,6 +192,7 @@ struct DRule {
 //           sweeps the stream's arena segment of many requests, stepping the
 //           job's automata in lockstep over each value.
 #define GI_MAX_FILTERS 32
+#define GI_MAX_STREAMS 256  // streams a ruleset may have (k_stream keeps per-stream chunk state in LDS)
 #define GI_MAX_GFILTERS 64
 #define GI_JOB_LDS_BYTES 65536          // small jobs: 2 workgroups of 1024 per CU
 #define GI_BIG_LDS_BYTES (148 * 1024)   // big jobs: 1 workgroup of 1024 per CU (+ 8 KB k_scan block list)

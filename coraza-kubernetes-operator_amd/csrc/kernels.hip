@@ -1691,20 +1691,42 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
 // Test one value: transform, operator, per-match actions.  Returns the number of matches.
 // multiMatch (coraza internal/corazawaf/rule.go executeTransformationsMultimatch):
 // the operator runs on the untransformed value and again after each
-// transformation of the chain; every match counts and runs the actions.  One
-// eval_op / run_actions site serves both forms (the Tx stays in registers).
+// transformation of the chain that changed the value (an unchanged step adds
+// no candidate); every match counts and runs the actions.  One eval_op /
+// run_actions site serves both forms (the Tx stays in registers).
 __device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn) {
-  // candidate kk = the value after the first kk transformations (a multiMatch
-  // link re-runs the short chain prefix per candidate: few registers, rare path)
   uint32_t nm = 0;
-  for (uint32_t kk = (R.flags & RF_MULTIMATCH) ? 0u : R.tchain_len; kk <= R.tchain_len; kk++) {
-    bool ok;
-    const Str tv = transform(t, R, v, vn, &ok, kk);
-    if (!ok) break;
-    if (eval_op(t, o, tv.p, tv.n)) {
+  bool ok = true;
+  Str cur{v, vn};
+  uint32_t k = R.tchain_len;  // transformations applied so far
+  if (R.flags & RF_MULTIMATCH) {
+    k = 0;
+  } else {
+    cur = transform(t, R, v, vn, &ok);
+    if (!ok) return 0;
+  }
+  while (true) {
+    if (eval_op(t, o, cur.p, cur.n)) {
       run_actions(t, R);
       nm++;
     }
+    // the next candidate: the first remaining transformation that changes cur
+    bool next = false;
+    while (k < R.tchain_len && !next) {
+      const uint8_t code = t.P->tchains[R.tchain_off + k];
+      k++;
+      if (!(value_summary(cur.p, cur.n) & transform_triggers(code))) continue;  // identity
+      uint8_t* dst = (cur.p == t.t0) ? t.t1 : t.t0;
+      const int64_t m = apply_transform(*t.P, code, cur.p, cur.n, dst, t.cap_t);
+      if (m < 0) {
+        t.flags |= GI_REQ_OVERFLOW;
+        return nm;
+      }
+      if ((uint32_t)m == cur.n && eq_bytes(dst, (uint32_t)m, cur.p, cur.n)) continue;  // unchanged
+      cur = {dst, (uint32_t)m};
+      next = true;
+    }
+    if (!next) break;
   }
   return nm;
 }

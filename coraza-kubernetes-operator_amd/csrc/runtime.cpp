@@ -145,6 +145,7 @@ int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ru
   std::string msg;
   std::string digest_input(seclang, n);
   for (const auto& x : exports) digest_input.append("\0export:", 8).append(x);
+  digest_input.append("\0compiler:", 10).append(kCompilerRev);
   std::map<std::string, std::string> data_files;
   if (opts && opts->n_data_files) {
     if (!opts->data_file_names || !opts->data_file_data || !opts->data_file_lens) {
@@ -206,6 +207,8 @@ int gi_ruleset_load(const uint8_t* buf, size_t n, gi_ruleset** out, char* err, s
 
 void gi_ruleset_free(gi_ruleset* rs) { delete rs; }
 
+const char* gi_compiler_rev(void) { return kCompilerRev; }
+
 int gi_ruleset_info_get(const gi_ruleset* rs, gi_ruleset_info* out) {
   if (!rs || !out) return GI_EINVAL;
   *out = rs->info;
@@ -234,12 +237,23 @@ int64_t gi_ruleset_describe(const gi_ruleset* rs, char* buf, size_t cap) {
 }
 
 // Uploads (or replaces) the context's device copy of a compiled ruleset.
-// Program buffers are reused when large enough; the staged batch is dropped
-// (its scratch layout depends on the program).
+// The new program is validated and uploaded into fresh buffers first; the
+// context switches to it (and frees the old buffers) only once every step
+// succeeded, so a failed swap leaves the old ruleset fully in place.  The
+// staged batch is dropped (its scratch layout depends on the program).
 static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   hipError_t e = hipSuccess;
   const Program& P = rs->prog;
-  c->pbufs.resize(32);
+  if (P.streams.size() > GI_MAX_STREAMS) return fail(c, GI_EINVAL, "ruleset has more phase-A streams than supported");
+  std::vector<DevBuf> nbufs(32);
+  DevBuf njoblist;
+  DProgram np{};
+  ScanLaunch nscan{};
+  auto discard = [&](int code, const char* what) {
+    for (auto& b : nbufs) b.release();
+    njoblist.release();
+    return fail(c, code, what);
+  };
   std::vector<uint32_t> lower;
   lower.reserve(GI_N_LOWER_PAIRS * 2);
   for (int i = 0; i < GI_N_LOWER_PAIRS; i++) {
@@ -250,8 +264,8 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   int k = 0;
 #define UP(field, vec, T)                                   \
   if (e == hipSuccess) {                                    \
-    e = upload(&c->pbufs[k], vec, s);                       \
-    c->prog.field = (const T*)c->pbufs[k].p;                \
+    e = upload(&nbufs[k], vec, s);                          \
+    np.field = (const T*)nbufs[k].p;                        \
     k++;                                                    \
   }
   UP(rules, P.rules, DRule)
@@ -295,31 +309,30 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   UP(body_links, P.body_links, uint32_t)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return GI_ENODEV;
-  c->prog.n_lower_pairs = GI_N_LOWER_PAIRS;
-  c->prog.n_top = (uint32_t)P.top.size();
-  c->prog.top_begin[0] = 0;
-  c->prog.top_end[0] = n_ph1;
-  c->prog.top_begin[1] = n_ph1;
-  c->prog.top_end[1] = (uint32_t)top_ph.size();
-  c->prog.n_slots = P.n_slots;
-  c->prog.n_markers = P.n_markers;
-  c->prog.n_exports = (uint32_t)P.exports.size();
-  for (int i = 0; i < 8; i++) c->prog.exports[i] = i < (int)P.exports.size() ? P.exports[i] : -1;
-  c->prog.rule_engine = P.rule_engine;
-  c->prog.body_access = P.body_access;
-  c->prog.body_limit = P.body_limit;
-  c->prog.n_jobs = (uint32_t)P.jobs.size();
-  c->prog.max_img_bytes = P.max_img_bytes;
-  c->prog.max_big_img_bytes = P.max_big_img_bytes;
-  c->prog.n_streams = (uint32_t)P.streams.size();
-  if (c->prog.n_streams > GI_MAX_STREAMS) return GI_EINVAL;
-  c->prog.n_always = (uint32_t)P.always_slots.size();
-  c->prog.n_body_links = (uint32_t)P.body_links.size();
-  c->prog.n_gfilters = (uint32_t)P.filters.size();
-  c->prog.item_singles = P.item_singles;
-  for (int k = 0; k < 8; k++) c->prog.item_sides[k] = P.item_sides[k];
-  c->prog.n_hit_slots = P.n_hit_slots;
+  if (e != hipSuccess) return discard(e == hipErrorOutOfMemory ? GI_ENOMEM : GI_ENODEV, "ruleset upload failed");
+  np.n_lower_pairs = GI_N_LOWER_PAIRS;
+  np.n_top = (uint32_t)P.top.size();
+  np.top_begin[0] = 0;
+  np.top_end[0] = n_ph1;
+  np.top_begin[1] = n_ph1;
+  np.top_end[1] = (uint32_t)top_ph.size();
+  np.n_slots = P.n_slots;
+  np.n_markers = P.n_markers;
+  np.n_exports = (uint32_t)P.exports.size();
+  for (int i = 0; i < 8; i++) np.exports[i] = i < (int)P.exports.size() ? P.exports[i] : -1;
+  np.rule_engine = P.rule_engine;
+  np.body_access = P.body_access;
+  np.body_limit = P.body_limit;
+  np.n_jobs = (uint32_t)P.jobs.size();
+  np.max_img_bytes = P.max_img_bytes;
+  np.max_big_img_bytes = P.max_big_img_bytes;
+  np.n_streams = (uint32_t)P.streams.size();
+  np.n_always = (uint32_t)P.always_slots.size();
+  np.n_body_links = (uint32_t)P.body_links.size();
+  np.n_gfilters = (uint32_t)P.filters.size();
+  np.item_singles = P.item_singles;
+  for (int k = 0; k < 8; k++) np.item_sides[k] = P.item_sides[k];
+  np.n_hit_slots = P.n_hit_slots;
   // k_scan plan: LDS jobs that fit the small image go to the 2-per-CU launch,
   // the rest (big images, global-table automata) to the 1-per-CU launch.
   std::vector<uint32_t> jl[3];
@@ -332,19 +345,27 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   std::vector<uint32_t> all(jl[0]);
   all.insert(all.end(), jl[1].begin(), jl[1].end());
   all.insert(all.end(), jl[2].begin(), jl[2].end());
-  if (upload(&c->joblist, all, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return GI_ENOMEM;
+  if (upload(&njoblist, all, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return discard(GI_ENOMEM, "scan plan upload failed");
   for (int b = 0; b < 2; b++) {
-    c->scan.jobs[b] = (const uint32_t*)c->joblist.p + (b ? jl[0].size() : 0);
-    c->scan.n_jobs[b] = (uint32_t)jl[b].size();
-    c->scan.lds[b] = b ? std::max<uint32_t>(P.max_big_img_bytes, 16) : std::max<uint32_t>(P.max_img_bytes, 16);
-    scan_allow_lds(c->scan.lds[b]);
-    c->scan.blocks[b] = scan_resident_blocks(c->scan.lds[b]);
-    c->scan.rpl[b] = 4;
+    nscan.jobs[b] = (const uint32_t*)njoblist.p + (b ? jl[0].size() : 0);
+    nscan.n_jobs[b] = (uint32_t)jl[b].size();
+    nscan.lds[b] = b ? std::max<uint32_t>(P.max_big_img_bytes, 16) : std::max<uint32_t>(P.max_img_bytes, 16);
+    scan_allow_lds(nscan.lds[b]);
+    nscan.blocks[b] = scan_resident_blocks(nscan.lds[b]);
+    nscan.rpl[b] = 4;
   }
-  c->scan.global_jobs = (const uint32_t*)c->joblist.p + jl[0].size() + jl[1].size();
-  c->scan.n_global = (uint32_t)jl[2].size();
-  c->scan.blocks[2] = scan_resident_blocks(16);
-  c->scan.mode = getenv("GI_SCAN_MODE") ? (uint32_t)atoi(getenv("GI_SCAN_MODE")) : 0u;
+  nscan.global_jobs = (const uint32_t*)njoblist.p + jl[0].size() + jl[1].size();
+  nscan.n_global = (uint32_t)jl[2].size();
+  nscan.blocks[2] = scan_resident_blocks(16);
+  nscan.mode = getenv("GI_SCAN_MODE") ? (uint32_t)atoi(getenv("GI_SCAN_MODE")) : 0u;
+  // commit: the context now runs the new program; the old buffers go
+  for (auto& b : c->pbufs) b.release();
+  c->joblist.release();
+  c->pbufs.swap(nbufs);
+  c->joblist = njoblist;
+  c->prog = np;
+  c->scan = nscan;
   c->rs = rs;
   c->staged = false;
   c->ran = false;

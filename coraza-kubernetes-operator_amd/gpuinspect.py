@@ -63,7 +63,7 @@ EXPORTED_SYMBOLS = (
     "gi_ctx_create", "gi_ctx_free", "gi_last_error", "gi_inspect_batch", "gi_stage_batch",
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
     "gi_ctx_stream", "gi_selftest_regex", "gi_selftest_plan", "gi_selftest_triggers",
-    "gi_ruleset_save", "gi_ruleset_load", "gi_ctx_swap_ruleset",
+    "gi_ruleset_save", "gi_ruleset_load", "gi_ctx_swap_ruleset", "gi_compiler_rev",
 )
 
 
@@ -145,6 +145,8 @@ def load_library(path: str = LIB_PATH):
     lib.gi_ruleset_save.argtypes = [vp, ctypes.c_void_p, sz]
     lib.gi_ruleset_save.restype = ctypes.c_int64
     lib.gi_ruleset_load.argtypes = [ctypes.c_void_p, sz, ctypes.POINTER(vp), ctypes.c_char_p, sz]
+    lib.gi_compiler_rev.argtypes = []
+    lib.gi_compiler_rev.restype = ctypes.c_char_p
     lib.gi_ctx_free.argtypes = [vp]
     lib.gi_last_error.argtypes = [vp]
     lib.gi_last_error.restype = ctypes.c_char_p
@@ -163,6 +165,11 @@ def load_library(path: str = LIB_PATH):
     lib.gi_selftest_triggers.argtypes = [ctypes.POINTER(u32), u32, ctypes.POINTER(u32)]
     _LIB = lib
     return lib
+
+
+def compiler_rev() -> str:
+    """The compiler revision folded into every source digest and artifact."""
+    return load_library().gi_compiler_rev().decode()
 
 
 def aggregate_configmaps(texts: Sequence[str]) -> str:

@@ -194,11 +194,17 @@ int gi_ruleset_export_name(const gi_ruleset* rs, uint32_t i, char* buf, size_t c
  * of recompiling the SecLang text.
  *   gi_ruleset_save  writes at most cap bytes; returns the artifact size (call
  *                    with cap 0 to size the buffer) or a negative GI_* code.
- *   gi_ruleset_load  GI_EINVAL + message for a truncated, corrupted or
- *                    other-version artifact.  Artifacts are trusted like the
- *                    SecLang text they come from (same producer). */
+ *   gi_ruleset_load  GI_EINVAL + message for a truncated, corrupted,
+ *                    other-version or other-compiler artifact, and for one
+ *                    whose records index outside their tables (every index
+ *                    and offset a kernel dereferences is bounds-checked: the
+ *                    checksum is not authentication). */
 int64_t gi_ruleset_save(const gi_ruleset* rs, uint8_t* buf, size_t cap);
 int gi_ruleset_load(const uint8_t* buf, size_t n, gi_ruleset** out, char* err, size_t errcap);
+/* Compiler revision string.  It is part of every source digest and artifact:
+ * an artifact from another compiler revision fails gi_ruleset_load, and the
+ * data plane recompiles RuleSetEntry.Rules instead. */
+const char* gi_compiler_rev(void);
 
 /* JSON description of the phase-A scan plan (streams, jobs, automata sizes).
  * Writes at most cap bytes (NUL-terminated); returns the full length

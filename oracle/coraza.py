@@ -1680,11 +1680,14 @@ class Transaction:
                 for k, v in self.get_field(rv):
                     if rule.multimatch:
                         # rule.go executeTransformationsMultimatch: the value,
-                        # then the value after each transformation
+                        # then the value after each transformation that
+                        # changed it (an unchanged step adds no candidate)
                         cands = [v]
                         for t in rule.transforms:
-                            v = TRANSFORM_FNS[t](v)
-                            cands.append(v)
+                            nv = TRANSFORM_FNS[t](v)
+                            if nv != v:
+                                cands.append(nv)
+                                v = nv
                     else:
                         cands = [self.transform(rule, v)]
                     for tv in cands:

@@ -50,6 +50,86 @@ def test_artifact_rejects_damage():
             gpuinspect.Ruleset.load(b)
 
 
+def _sections(blob):
+    """{tag: (payload offset of the records, elem size, count)} of an artifact
+    (csrc/artifact.cpp layout: 40-byte header, then tag/esz/count sections)."""
+    import struct
+    out, off = {}, 40
+    nsec = struct.unpack_from("<I", blob, 12)[0]
+    for _ in range(nsec):
+        tag, esz, cnt = struct.unpack_from("<IIQ", blob, off)
+        off += 16
+        out[tag] = (off, esz, cnt)
+        off += (esz * cnt + 7) & ~7
+    return out
+
+
+def _reseal(buf):
+    import struct
+    struct.pack_into("<Q", buf, 24, artifact.fnv64(bytes(buf[40:])))
+    return bytes(buf)
+
+
+_BLOBS = {}
+
+
+def _crs_blob():
+    if "crs" not in _BLOBS:
+        _BLOBS["crs"] = gpuinspect.Ruleset(TEXTS["crs_pl1"]).save()
+    return _BLOBS["crs"]
+
+
+# (section tag, record index, byte offset in the record, u32 value) -> an index
+# or offset some kernel dereferences, pushed outside its table
+_CORRUPT = [
+    (1, 0, 24, 0xFFFF0000),   # DRule.var_begin
+    (1, 0, 32, 0x7FFF0000),   # DRule.op
+    (1, 0, 56, 0x7FFF0000),   # DRule.hit_slot
+    (1, 0, 12, 0x7FFF0000),   # DRule.chain_next
+    (2, 0, 0, 0x7FFF0000),    # top-level rule index
+    (5, 0, 4, 0x7FFF0000),    # DOp.dfa
+    (10, 0, 16, 0xFFFF0000),  # DDfa.trans_off
+    (10, 0, 0, 0x00FFFFFF),   # DDfa.n_states
+    (11, 0, 0, 0x7FFF7FFF),   # transition targets
+    (22, 0, 4, 0xFFFF0000),   # DJob.img_off
+    (22, 0, 0, 0x7FFF0000),   # DJob.stream
+    (23, 0, 0, 0x7FFF0000),   # DJobDfa.dfa
+    (24, 0, 0, 0x7FFF0000),   # DPat.slot
+    (17, 0, 16, 0x7FFF0000),  # DStream.job_begin
+    (19, 0, 0, 0x000000FF),   # stream filter id (u8 section: whole first word)
+    (27, 0, 0, 0x7FFF0000),   # export slot
+]
+
+
+@pytest.mark.parametrize("case", _CORRUPT, ids=["%d.%d+%d" % c[:3] for c in _CORRUPT])
+def test_artifact_rejects_out_of_range_records(case):
+    """A checksummed but malformed artifact is rejected before any kernel sees
+    it: every index / offset a kernel dereferences is bounds-checked
+    (csrc/artifact.cpp validate_program)."""
+    import struct
+    blob = _crs_blob()
+    tag, rec, at, val = case
+    off, esz, cnt = _sections(blob)[tag]
+    assert cnt > rec
+    buf = bytearray(blob)
+    if esz == 1:
+        buf[off + rec] = val & 0xFF
+    else:
+        struct.pack_into("<I", buf, off + rec * esz + at, val)
+    with pytest.raises(gpuinspect.SecLangError, match="invalid GPU artifact"):
+        gpuinspect.Ruleset.load(_reseal(buf))
+
+
+def test_artifact_other_compiler_revision():
+    blob = gpuinspect.Ruleset(TEXTS["samples"]).save()
+    off, esz, _ = _sections(blob)[100]  # scalars: compiler_rev is the last u64
+    buf = bytearray(blob)
+    buf[off + esz - 1] ^= 0x5A
+    with pytest.raises(gpuinspect.SecLangError, match="compiler revision"):
+        gpuinspect.Ruleset.load(_reseal(buf))
+    assert gpuinspect.compiler_rev()
+
+
 def test_source_digest():
     rs = gpuinspect.Ruleset(TEXTS["samples"])
     assert rs.info["source_digest"] == artifact.source_digest(TEXTS["samples"])
@@ -87,6 +167,24 @@ def test_poller_reloads_on_new_uuid():
     put("b", "\n".join(KATS["reconcile_add_sinister"]["configmaps"]))
     assert p.poll() and p.uuid == "b" and len(eng.swaps) == 2
     assert eng.swaps[0].info["n_rules"] == 1 and eng.swaps[-1].info["n_rules"] == 2
+
+
+PMF = 'SecRule ARGS "@pmFromFile bad.data" "id:7,phase:2,deny,status:403"'
+
+
+def test_poller_pmfromfile_entry():
+    """A ruleset with @pmFromFile: the data files are part of the digest, so the
+    artifact is used when the poller holds the same files and a recompile with
+    those files happens otherwise (never a SecLangError inside poll)."""
+    files = {"bad.data": b"evilmonkey\nsinister\n"}
+    e = artifact.entry("u1", "t", PMF, data_files=files)
+    assert artifact.ruleset_from_entry(e, data_files=files).text is None
+    other = {"bad.data": b"maniacal\n"}
+    assert artifact.ruleset_from_entry(e, data_files=other).text == PMF
+    eng = _FakeEngine()
+    p = artifact.RulesetPoller(eng, lambda: {"uuid": "u1", "timestamp": "t"}, lambda u: e, data_files=files)
+    assert p.poll() and p.loaded_from_artifact
+    assert eng.swaps[0].info["source_digest"] == artifact.source_digest(PMF, data_files=files)
 
 
 def _tx(uri):

@@ -215,9 +215,11 @@ SecRule TX:ANOMALY_SCORE "@ge 1002" "id:9,phase:2,deny,status:403"
 
 def test_gpu_parity_multimatch():
     """multiMatch (rule.go executeTransformationsMultimatch): the operator runs
-    on the raw value and after every transformation, each match counting (and
-    running setvar) once; interpreter-only links.  The exported anomaly_score
-    pins the match counts; GPU vs oracle."""
+    on the raw value and after every transformation that changed the value,
+    each match counting (and running setvar) once; interpreter-only links.
+    The exported anomaly_score pins the match counts: a=ABC matches rule 1
+    once (after t:lowercase), a=abc once (raw; lowercase is a no-op and adds
+    no candidate), so neither reaches 1002; GPU vs oracle."""
     txs = []
     for q in (b"a=ABC", b"a=abc", b"a=%253c", b"a=%253C", b"a=%253Cscript", b"a=%26lt;script", b"a=safe", b"a=abc&b=ABC"):
         t = gpuinspect.Transaction(method=b"GET", uri=b"/?" + q)
@@ -227,6 +229,8 @@ def test_gpu_parity_multimatch():
     res = _parity(MULTI, gpuinspect.pack(txs))
     ai = list(gpuinspect.DEFAULT_EXPORTS).index("anomaly_score")
     scores = [int(v["tx_export"][ai]) for v in res.verdicts]
-    assert scores[:2] == [1001, 1002]
+    assert scores[:2] == [1001, 1001]
+    assert [int(v["status"]) for v in res.verdicts][:2] == [0, 0]
+    assert scores[7] == 2002 and int(res.verdicts[7]["status"]) == 403
     batch = traffic.TrafficGen(traffic.SEED + 9).batch(800, attack_rate=0.3)
     _parity(MULTI, batch)
