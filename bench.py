@@ -1,15 +1,21 @@
 """Benchmark: requests inspected/s + GB/s scanned on MI355X (BASELINE.json metric).
 
 One "step" = one pass of the inspection pipeline (gi_run_staged: collect ->
-phase 1 -> body -> phase 2 -> verdicts + tallies) over one batch of synthetic
-requests already resident in HBM, plus (N > 1) the RCCL all-gather of the
-per-GPU tally.  Requests are sharded with no data-path collective: each rank
+phase A -> phase 1 -> body -> phase 2 -> verdicts + tallies) over one batch
+of synthetic requests already resident in HBM, plus (N > 1) the RCCL
+all-gather of the per-GPU tally (7 counters + score histogram + per-rule
+match counts).  Requests are sharded with no data-path collective: each rank
 inspects its own batch (weak scaling).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3] [--n-req R]
 
 N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).
 Prints ONE JSON line on rank 0.
+
+Self-check: the verdicts of the timed batch are compared with the CPU oracle
+on the cpu_baseline sample (`parity_sample`); a mismatch is reported, never
+hidden.  `e2e` times one more pass including host staging (layout + H2D of
+pageable buffers) and the verdict D2H.
 """
 
 import argparse
@@ -52,37 +58,46 @@ CONFIGS = {
 
 
 def _oracle_worker(args):
-    text, blob, idx = args
+    text, blob, idx, exports = args
     from oracle import coraza
     cfg = coraza.parse_seclang(text)
     data, reqs, headers = blob
     b = gpuinspect.PackedBatch(data, reqs, headers)
+    out = {}
     t0 = time.perf_counter()
     for i in idx:
         t = b.request(i)
-        coraza.inspect(cfg, coraza.Request(t.method, t.uri, t.proto, list(t.headers), t.body))
-    return time.perf_counter() - t0, len(idx)
+        out[i] = coraza.inspect(cfg, coraza.Request(t.method, t.uri, t.proto, list(t.headers), t.body), exports)
+    return time.perf_counter() - t0, out
 
 
-def cpu_baseline(text, batch, budget_s=15.0, procs=16):
-    """The CPU oracle (port) on a bounded sample of the same workload."""
-    n_sample = min(batch.n_req, 4000)
+def oracle_sample(text, batch, exports, budget_s=15.0, procs=16, n_max=4000):
+    """The CPU oracle over a bounded sample of the batch: (verdicts by request
+    index, wall seconds, processes).  Sized from a 100-request calibration to
+    about budget_s of wall time."""
     blob = (batch.data, batch.reqs, batch.headers)
-    # calibrate on 100 requests, then size the sample for ~budget_s wall
-    dt, n = _oracle_worker((text, blob, range(100)))
-    per = dt / max(n, 1)
+    dt, _ = _oracle_worker((text, blob, range(100), exports))
+    per = dt / 100
     procs = max(1, min(procs, os.cpu_count() or 1))
-    n_sample = int(min(n_sample * procs, max(200, budget_s * procs / max(per, 1e-6))))
-    n_sample = min(n_sample, batch.n_req)
+    n_sample = int(min(n_max * procs, max(200, budget_s * procs / max(per, 1e-6)), batch.n_req))
     chunks = [range(k, n_sample, procs) for k in range(procs)]
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(procs) as pool:
-        outs = pool.map(_oracle_worker, [(text, blob, c) for c in chunks])
+        outs = pool.map(_oracle_worker, [(text, blob, c, exports) for c in chunks])
     wall = time.perf_counter() - t0
-    done = sum(o[1] for o in outs)
-    return {"value": round(done / wall, 1), "unit": "requests/s", "cores": procs, "kind": "port",
-            "sample": "%d requests of the benchmark batch, oracle/coraza.py (pure-Python Coraza "
-                      "restatement, CPython re for @rx) in %d processes" % (done, procs)}
+    verdicts = {}
+    for _, o in outs:
+        verdicts.update(o)
+    return verdicts, wall, procs
+
+
+def parity(res, verdicts):
+    from oracle import compare
+    bad = compare.compare(res, verdicts, max_report=10 ** 9)
+    return {"n": len(verdicts), "mismatches": len({b[0] for b in bad}),
+            "first": [str(b)[:300] for b in bad[:3]],
+            "def": "timed batch's GPU verdicts vs oracle/coraza.py on the same requests: interruption, "
+                   "ordered matched ids, exported TX values, unsupported flag (oracle/compare.py)"}
 
 
 def main():
@@ -117,13 +132,13 @@ def main():
     raw = batch.raw_bytes()
     eng.stage(batch)
 
-    gather = shard.TallyGather(dist, world, "cuda") if dist is not None else None
+    gather = shard.TallyGather(dist, world, "cuda", n_rules=rs.info["n_rules"]) if dist is not None else None
 
     def step():
         eng.run()
         eng.sync()
         if gather is not None:
-            gather.push(eng.tally())
+            gather.push(eng.tally(), eng.tally_detail())
 
     for _ in range(args.warmup):
         step()
@@ -131,17 +146,13 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
     eng.sync()
-    kern_ms, stage_ms = [], {"k_collect": [], "k_stream": [], "k_scan": [], "k_eval": []}
+    kern_ms = []
     launch_ms, launch_bytes, launch_steps = {}, {}, {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         st = eng.stats()
         kern_ms.append(st["last_kernel_ms"])
-        stage_ms["k_collect"].append(st["last_collect_ms"])
-        stage_ms["k_stream"].append(st["last_stream_ms"])
-        stage_ms["k_scan"].append(st["last_scan_ms"])
-        stage_ms["k_eval"].append(st["last_eval_ms"])
         for ln in st["launches"]:
             launch_ms.setdefault(ln["name"], []).append(ln["ms"])
             launch_bytes[ln["name"]] = ln["alg_bytes"]
@@ -151,39 +162,37 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    tally = eng.tally()
+    detail = eng.tally_detail()
     if dist is not None:
         elapsed = shard.max_over_ranks(dist, elapsed, "cuda")
         tot = gather.total()
         total_req = tot["n_req"]
         total_bytes = tot["bytes_scanned"]
+        node_tally = tot
     else:
-        t = eng.tally()
-        total_req, total_bytes = int(t["n_req"]), int(t["bytes_scanned"])
-    tally = eng.tally()
+        total_req, total_bytes = int(tally["n_req"]), int(tally["bytes_scanned"])
+        node_tally = dict(tally, **detail)
     ms_per_step = elapsed / args.steps * 1e3
     value = total_req * args.steps / elapsed
     gbs = total_bytes * args.steps / elapsed / 1e9
 
-    # Roofline of the dominant single kernel launch (HIP events recorded on the
-    # context stream around every launch; DESIGN.md §4 defines each kernel's
-    # algorithmic bytes per launch, counted on the device).
-    avg_kern_ms = float(np.mean(kern_ms))
-    avg_stage = {k: float(np.mean(v)) for k, v in stage_ms.items()}
+    # Roofline of the dominant launch (HIP events recorded on the context
+    # stream around every launch).  achieved = SURVEY.md §8(d) algorithmic
+    # bytes of the batch (raw request bytes once + 16 B verdict + 4 B per
+    # matched id) / the dominant launch's average time.
     avg_launch = {k: float(np.mean(v)) for k, v in launch_ms.items()}
     dom = max(avg_launch, key=lambda k: avg_launch[k])
-    alg_bytes = launch_bytes[dom]
-    achieved = alg_bytes / (avg_launch[dom] * 1e-3) / 1e9
-    # SURVEY.md §8(d) figure: raw request bytes once + verdict record + 4 B per
-    # matched id, over the whole pipeline
     req_bytes = raw + 16 * batch.n_req + 4 * int(tally["matched_total"])
-    req_gbs = req_bytes / (avg_kern_ms * 1e-3) / 1e9
-    steps_s = launch_steps.get(dom, 0) / (avg_launch[dom] * 1e-3)
+    achieved = req_bytes / (avg_launch[dom] * 1e-3) / 1e9
+    avg_kern_ms = float(np.mean(kern_ms))
     hbm_traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.exists(tpath):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)
         tj = json.load(open(tpath))
         if tj.get("kernel") == dom and tj.get("requests") == batch.n_req:
             hbm_traffic = tj["hbm_bytes_per_launch"]
+    steps_s = launch_steps.get(dom, 0) / (avg_launch[dom] * 1e-3)
     out = {
         "metric": "requests inspected/sec (node), CRS v4 PL1",
         "value": round(value, 1),
@@ -204,26 +213,63 @@ def main():
         "interrupted_frac": round(tally["n_interrupted"] / max(tally["n_req"], 1), 4),
         "pa_void_requests": int(tally["n_pa_void"]),
         "error_requests": int(tally["n_error"]),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": hbm_traffic,
-                     "kernel": dom, "rocprof_kernel": ROCPROF_NAMES.get(dom, dom),
-                     "kernel_ms": round(avg_launch[dom], 4), "alg_bytes_per_launch": int(alg_bytes),
-                     "alg_bytes_def": "bytes the launch must move once: for k_scan, every queue word "
-                                      "(transformed value + 16 B lane header) of its streams read once",
-                     "secondary": {"bound": "valu/lds (automaton steps)", "byte_steps_per_launch": int(launch_steps.get(dom, 0)),
-                                   "byte_steps_per_s": round(steps_s, 1)},
-                     "pipeline_request_bytes": {"def": "SURVEY.md 8(d): raw request bytes + 16 B verdict + 4 B x matched ids",
-                                                "bytes": int(req_bytes), "GB/s": round(req_gbs, 3),
-                                                "frac": round(req_gbs / HBM_PEAK_GBS, 6)},
-                     "launches": {k: {"ms": round(v, 4), "alg_bytes": int(launch_bytes[k]),
-                                      "GB/s": round(launch_bytes[k] / (v * 1e-3) / 1e9, 2) if v > 0 else None}
-                                  for k, v in avg_launch.items()},
-                     "stages_ms": {k: round(v, 4) for k, v in avg_stage.items()},
-                     "pipeline_kernel_ms": round(avg_kern_ms, 4)},
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": hbm_traffic,
+            "kernel": dom, "rocprof_kernel": ROCPROF_NAMES.get(dom, dom), "kernel_ms": round(avg_launch[dom], 4),
+            "alg_bytes_per_launch": int(req_bytes),
+            "alg_bytes_def": "SURVEY.md 8(d): sum of raw request bytes (method+uri+proto+headers+body, each "
+                             "once) + 16 B verdict + 4 B x matched ids, for the whole batch the launch processes",
+            "pipeline": {"ms": round(avg_kern_ms, 4), "GB/s": round(req_bytes / (avg_kern_ms * 1e-3) / 1e9, 3),
+                         "frac": round(req_bytes / (avg_kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)},
+            "secondary": {
+                "bound": "lds/valu (automaton steps, transformation chains)",
+                "byte_steps_per_launch": int(launch_steps.get(dom, 0)), "byte_steps_per_s": round(steps_s, 1),
+                "queue_bytes_def": "bytes the launch itself must move once (DESIGN.md §4): item bytes + records "
+                                   "in, transformed queue words out (k_stream); queue words in (k_scan)",
+                "launches": {k: {"ms": round(v, 4), "queue_bytes": int(launch_bytes[k]),
+                                 "GB/s": round(launch_bytes[k] / (v * 1e-3) / 1e9, 2) if v > 0 else None}
+                             for k, v in avg_launch.items()}},
+        },
+        "tally": {"n_req": int(node_tally["n_req"]), "n_interrupted": int(node_tally["n_interrupted"]),
+                  "matched_total": int(node_tally["matched_total"]),
+                  "score_hist_nonzero": {str(b): int(x) for b, x in enumerate(node_tally["score_hist"]) if x},
+                  "top_rules": sorted(([int(i), int(h)] for i, h in zip(detail["rule_ids"], node_tally["rule_hits"]) if h),
+                                      key=lambda x: -x[1])[:8]},
         "gen_s": round(t_gen, 1),
     }
+    # Host-inclusive pass: stage (layout + H2D of pageable numpy buffers) +
+    # pipeline + D2H of verdicts and matched ids.  Never `value`.
+    t1 = time.perf_counter()
+    eng.stage(batch)
+    t2 = time.perf_counter()
+    eng.run()
+    eng.sync()
+    t3 = time.perf_counter()
+    res = eng.fetch()
+    t4 = time.perf_counter()
+    out["e2e"] = {"requests_per_s": round(batch.n_req / (t4 - t1), 1), "ms": round((t4 - t1) * 1e3, 2),
+                  "stage_ms": round((t2 - t1) * 1e3, 2), "run_ms": round((t3 - t2) * 1e3, 2),
+                  "fetch_ms": round((t4 - t3) * 1e3, 2),
+                  "GB/s": round(raw / (t4 - t1) / 1e9, 3),
+                  "def": "one pass incl. gi_stage_batch (host layout + H2D, pageable) and gi_fetch_results (D2H), per GPU"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(text, batch)
+        verdicts, wall, procs = oracle_sample(text, batch, rs.exports)
+        out["cpu_baseline"] = {
+            "value": round(len(verdicts) / wall, 1), "unit": "requests/s", "cores": procs, "kind": "port",
+            "sample": "%d requests of the benchmark batch, oracle/coraza.py (pure-Python Coraza restatement, "
+                      "CPython re for @rx) in %d processes" % (len(verdicts), procs)}
+        out["parity_sample"] = parity(res, verdicts)
+    elif world > 1:
+        # every rank checks a small sample of its own batch against the oracle
+        from oracle import compare, coraza
+        cfg = coraza.parse_seclang(text)
+        idx = range(0, batch.n_req, max(1, batch.n_req // 128))
+        ps = parity(res, compare.oracle_verdicts(cfg, batch, rs.exports, idx))
+        import torch
+        t = torch.tensor([ps["n"], ps["mismatches"]], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        out["parity_sample"] = dict(ps, n=int(t[0]), mismatches=int(t[1]), first=ps["first"] if rank == 0 else [])
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

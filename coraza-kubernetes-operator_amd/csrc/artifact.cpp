@@ -265,7 +265,7 @@ bool validate_program(const Program& P, std::string* err) {
     if (!in(r.var_begin, r.var_count, P.vars.size()) || (r.op >= 0 && (uint32_t)r.op >= P.ops.size()) ||
         !in(r.act_begin, r.act_count, P.acts.size()) || !in(r.tchain_off, r.tchain_len, P.tchains.size()) ||
         (r.chain_next >= 0 && (uint32_t)r.chain_next >= nrules) || r.phase > 5 ||
-        (r.hit_slot >= 0 && (uint32_t)r.hit_slot >= nhit) || r.hit_slot < -1)
+        (r.hit_slot >= 0 && (uint32_t)r.hit_slot >= nhit) || r.hit_slot < -1 || r.top_idx >= P.top.size())
       return bad("rule record out of range");
   }
   for (uint32_t t : P.body_links)

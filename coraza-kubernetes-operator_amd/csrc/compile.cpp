@@ -1589,6 +1589,7 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
       const IrRule& r = waf.rules[ti];
       L.no_scan = gated[ti];
       uint32_t idx = L.rule(r, false);
+      out->rules[idx].top_idx = (uint32_t)out->top.size();
       out->top.push_back(idx);
       uint32_t prev = idx;
       for (auto& c : r.children) {

@@ -35,6 +35,7 @@ struct DBatch {
   gi_verdict* verdicts;
   uint32_t* matched;
   unsigned long long* tally;  // gi_tally counters
+  uint32_t* tally_ext;        // [GI_SCORE_BINS] score histogram, then [n_top] per-rule match counts
   uint32_t* hits;             // phase-A hit words [ceil(n_hit_slots/32)][n_req]
   Slot* txslots;       // TX variables [n_slots][n_req] (k_eval)
   // phase A (see kernels.hip "phase A")
@@ -76,6 +77,7 @@ struct ScanLaunch {
   uint32_t mode;                // debugging switches (GI_SCAN_MODE), 0 in production
 };
 
+#define GI_RHIST_LDS 1024     // per-rule match counts k_eval aggregates in LDS (more rules: global atomics)
 #define GI_STREAM_GRID 8192  // k_stream workgroups (64 lanes) per bucket launch (~8 waves/SIMD)
 #define GI_PCHUNK 2048       // pool words a k_stream wave reserves at a time
 

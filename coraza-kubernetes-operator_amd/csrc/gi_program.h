@@ -175,7 +175,7 @@ struct DRule {
   uint8_t flags;        // RuleFlags
   uint8_t _pad;
   int32_t hit_slot;     // phase-A hit bit (-1: evaluated by the interpreter only)
-  uint32_t _pad2;
+  uint32_t top_idx;     // position in the top-level rule list (per-rule hit tally); chain links: 0
 };
 
 // ------------------------------------------------------ phase-A scan plan

@@ -769,6 +769,7 @@ struct Tx {
   uint32_t nmatched;
   uint32_t* mout;
   uint32_t mcap;
+  uint32_t* rhist;           // per-rule match counts (LDS when the ruleset is small)
   bool profon;               // GI_PROF counters (diagnostics)
   uint32_t prof_visits, prof_evals, prof_rules;
   uint64_t prof_eval_cyc, prof_act_cyc;
@@ -1881,6 +1882,7 @@ __device__ __forceinline__ void eval_top(Tx& t, uint32_t ri) {
     if (t.nmatched < t.mcap) t.mout[t.nmatched] = (uint32_t)R.id;
     else t.flags |= GI_REQ_MATCH_TRUNC;
     t.nmatched++;
+    atomicAdd(&t.rhist[R.top_idx], 1u);
   }
 }
 
@@ -2985,8 +2987,13 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
 // skipping every phase-A rule whose hit bit is clear.
 __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
   __shared__ unsigned long long red[7];
+  // block-aggregated detail tally: score histogram + per-rule match counts
+  __shared__ uint32_t shist[GI_SCORE_BINS + GI_RHIST_LDS];
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool rh_lds = P.n_top <= GI_RHIST_LDS;
+  const uint32_t n_sh = GI_SCORE_BINS + (rh_lds ? P.n_top : 0u);
   if (threadIdx.x < 7) red[threadIdx.x] = 0;
+  for (uint32_t i = threadIdx.x; i < n_sh; i += blockDim.x) shist[i] = 0;
   __syncthreads();
   unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
   if (r < B.n_req) {
@@ -3027,6 +3034,7 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
     t.nmatched = 0;
     t.mout = B.matched + (uint64_t)r * B.mcap;
     t.mcap = B.mcap;
+    t.rhist = rh_lds ? shist + GI_SCORE_BINS : B.tally_ext + GI_SCORE_BINS;
     for (uint32_t s = 0; s < P.n_slots; s++) TXS(t, s).state = 0;
     const uint8_t* D = B.data;
     uint64_t scanned = (uint64_t)rq.method.len + rq.uri.len + rq.proto.len + rq.body.len;
@@ -3104,6 +3112,7 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
       v.tx_export[e] = x;
     }
     B.verdicts[r] = v;
+    atomicAdd(&shist[(uint32_t)min(max(v.tx_export[0], (int64_t)0), (int64_t)(GI_SCORE_BINS - 1))], 1u);
     my[0] = 1;
     my[1] = t.interrupted ? 1 : 0;
     my[2] = t.nmatched ? 1 : 0;
@@ -3119,6 +3128,8 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
   }
   __syncthreads();
   if (threadIdx.x < 7) atomicAdd(&B.tally[threadIdx.x], red[threadIdx.x]);
+  for (uint32_t i = threadIdx.x; i < n_sh; i += blockDim.x)
+    if (shist[i]) atomicAdd(&B.tally_ext[i], shist[i]);
 }
 
 void scan_allow_lds(uint32_t lds_bytes) {

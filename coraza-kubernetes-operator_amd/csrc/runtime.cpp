@@ -80,7 +80,7 @@ struct gi_ctx {
   DProgram prog{};
   std::vector<DevBuf> pbufs;
   // batch buffers
-  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, hits, joblist, txslots;
+  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, tally_ext, hits, joblist, txslots;
   // phase A
   DevBuf bcounts, boffs, items, lscratch, pool, qblk, ctr, slow, slow_bytes;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0;
@@ -424,7 +424,7 @@ void gi_ctx_free(gi_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& b : c->pbufs) b.release();
   c->prof.release();
-  for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally,
+  for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext,
                     &c->hits, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes})
     b->release();
@@ -544,6 +544,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if ((e = c->matched.ensure(std::max<size_t>((size_t)n * c->mcap * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc matched");
   if ((e = c->tally.ensure(sizeof(gi_tally))) != hipSuccess) return hip_fail(c, e, "alloc tally");
+  if ((e = c->tally_ext.ensure(4ull * (GI_SCORE_BINS + PG.top.size()))) != hipSuccess)
+    return hip_fail(c, e, "alloc detail tally");
   if ((e = c->txslots.ensure(std::max<uint64_t>(24ull * PG.n_slots * n, 64))) != hipSuccess)
     return hip_fail(c, e, "alloc tx slots");
   c->hit_words = (PG.n_hit_slots + 31) / 32;
@@ -603,6 +605,8 @@ int gi_run_staged(gi_ctx* c) {
   if (!c->staged) return fail(c, GI_ESTATE, "gi_run_staged before gi_stage_batch");
   (void)hipSetDevice(c->device);
   hipError_t e = hipMemsetAsync(c->tally.p, 0, sizeof(gi_tally), c->stream);
+  if (e == hipSuccess)
+    e = hipMemsetAsync(c->tally_ext.p, 0, 4ull * (GI_SCORE_BINS + c->rs->prog.top.size()), c->stream);
   if (e != hipSuccess) return hip_fail(c, e, "memset tally");
   DBatch B;
   B.data = (const uint8_t*)c->data.p;
@@ -615,6 +619,7 @@ int gi_run_staged(gi_ctx* c) {
   B.verdicts = (gi_verdict*)c->verdicts.p;
   B.matched = (uint32_t*)c->matched.p;
   B.tally = (unsigned long long*)c->tally.p;
+  B.tally_ext = (uint32_t*)c->tally_ext.p;
   B.hits = (uint32_t*)c->hits.p;
   B.txslots = (Slot*)c->txslots.p;
   {
@@ -791,6 +796,28 @@ int gi_tally_get(gi_ctx* c, gi_tally* out) {
   if (rc != GI_OK) return rc;
   hipError_t e = hipMemcpy(out, c->tally.p, sizeof(gi_tally), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return hip_fail(c, e, "fetch tally");
+  return GI_OK;
+}
+
+int gi_tally_detail_get(gi_ctx* c, uint64_t* score_hist, uint32_t* rule_ids, uint64_t* rule_hits, uint32_t cap,
+                        uint32_t* n_rules) {
+  if (!c) return GI_EINVAL;
+  if (!c->ran) return fail(c, GI_ESTATE, "no batch has run");
+  const Program& P = c->rs->prog;
+  const uint32_t nt = (uint32_t)P.top.size();
+  if (n_rules) *n_rules = nt;
+  if ((rule_ids || rule_hits) && cap < nt) return fail(c, GI_ETRUNC, "rule tally capacity too small");
+  int rc = gi_sync(c);
+  if (rc != GI_OK) return rc;
+  std::vector<uint32_t> h(GI_SCORE_BINS + nt);
+  hipError_t e = hipMemcpy(h.data(), c->tally_ext.p, 4 * h.size(), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(c, e, "fetch detail tally");
+  if (score_hist)
+    for (int b = 0; b < GI_SCORE_BINS; b++) score_hist[b] = h[b];
+  for (uint32_t k = 0; k < nt; k++) {
+    if (rule_ids) rule_ids[k] = (uint32_t)P.rules[P.top[k]].id;
+    if (rule_hits) rule_hits[k] = h[GI_SCORE_BINS + k];
+  }
   return GI_OK;
 }
 

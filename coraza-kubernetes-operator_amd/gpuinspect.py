@@ -63,8 +63,9 @@ EXPORTED_SYMBOLS = (
     "gi_ctx_create", "gi_ctx_free", "gi_last_error", "gi_inspect_batch", "gi_stage_batch",
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
     "gi_ctx_stream", "gi_selftest_regex", "gi_selftest_plan", "gi_selftest_triggers",
-    "gi_ruleset_save", "gi_ruleset_load", "gi_ctx_swap_ruleset", "gi_compiler_rev",
+    "gi_ruleset_save", "gi_ruleset_load", "gi_ctx_swap_ruleset", "gi_compiler_rev", "gi_tally_detail_get",
 )
+SCORE_BINS = 64  # GI_SCORE_BINS
 
 
 class SecLangError(ValueError):
@@ -158,6 +159,8 @@ def load_library(path: str = LIB_PATH):
     lib.gi_fetch_results.argtypes = [vp, ctypes.POINTER(_Results)]
     lib.gi_tally_get.argtypes = [vp, ctypes.POINTER(_Tally)]
     lib.gi_stats_get.argtypes = [vp, ctypes.POINTER(_Stats)]
+    lib.gi_tally_detail_get.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u32), ctypes.POINTER(u64), u32,
+                                        ctypes.POINTER(u32)]
     lib.gi_ctx_stream.argtypes = [vp]
     lib.gi_ctx_stream.restype = vp
     lib.gi_selftest_regex.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(u32)]
@@ -312,6 +315,19 @@ class PackedBatch:
                    + r["body"]["len"].sum() + self.headers["name"]["len"].sum()
                    + self.headers["value"]["len"].sum())
 
+    def request_bytes(self) -> np.ndarray:
+        """Raw bytes of each request (SURVEY §8(d) B_req)."""
+        r = self.reqs
+        per = (r["method"]["len"].astype(np.int64) + r["uri"]["len"] + r["proto"]["len"] + r["body"]["len"])
+        hl = self.headers["name"]["len"].astype(np.int64) + self.headers["value"]["len"]
+        hs = np.concatenate([[0], np.cumsum(hl)])
+        b = r["hdr_begin"].astype(np.int64)
+        return per + hs[b + r["hdr_count"]] - hs[b]
+
+    def take(self, lo: int, hi: int) -> "PackedBatch":
+        """Requests [lo, hi) as their own batch (a shard of this one)."""
+        return pack([self.request(i) for i in range(lo, hi)])
+
     def to_ctypes(self) -> _Batch:
         return _Batch(self.n_req, self.data.ctypes.data, len(self.data), self.reqs.ctypes.data,
                       self.headers.ctypes.data, len(self.headers))
@@ -457,6 +473,18 @@ class Engine:
         t = _Tally()
         self._check(self._lib.gi_tally_get(self._h, ctypes.byref(t)), "gi_tally_get")
         return {k: getattr(t, k) for k, _ in _Tally._fields_}
+
+    def tally_detail(self) -> dict:
+        """Score histogram (first export, clamped to [0, 63]) and per top-level
+        rule match counts of the last batch (gi_tally_detail_get)."""
+        n = ctypes.c_uint32(0)
+        self._check(self._lib.gi_tally_detail_get(self._h, None, None, None, 0, ctypes.byref(n)), "gi_tally_detail_get")
+        hist = (ctypes.c_uint64 * SCORE_BINS)()
+        ids = (ctypes.c_uint32 * max(n.value, 1))()
+        hits = (ctypes.c_uint64 * max(n.value, 1))()
+        self._check(self._lib.gi_tally_detail_get(self._h, hist, ids, hits, n.value, ctypes.byref(n)),
+                    "gi_tally_detail_get")
+        return {"score_hist": list(hist), "rule_ids": list(ids)[:n.value], "rule_hits": list(hits)[:n.value]}
 
     def stats(self) -> dict:
         s = _Stats()

@@ -160,6 +160,13 @@ typedef struct {
   uint64_t n_pa_void;     /* requests whose phase-A arena overflowed (evaluated exhaustively) */
 } gi_tally;
 
+/* Detail tallies of the last batch (what the multi-GPU tally
+ * all-gathers besides gi_tally): a histogram of the first exported TX value
+ * (default: blocking_inbound_anomaly_score) clamped to [0, GI_SCORE_BINS-1],
+ * and per top-level rule (file order, ids as in MatchedRules) the number of
+ * requests whose matched-rule list holds it. */
+#define GI_SCORE_BINS 64
+
 typedef struct {
   uint64_t batches;
   double last_kernel_ms;   /* HIP-event time of the last inspection pipeline */
@@ -235,6 +242,11 @@ int gi_run_staged(gi_ctx* ctx);
 int gi_sync(gi_ctx* ctx);
 int gi_fetch_results(gi_ctx* ctx, gi_results* out);
 int gi_tally_get(gi_ctx* ctx, gi_tally* out);
+/* score_hist: GI_SCORE_BINS entries (may be NULL).  rule_ids / rule_hits:
+ * cap entries each (may be NULL); *n_rules = the ruleset's top-level rules
+ * (GI_ETRUNC when cap is smaller and the arrays are given). */
+int gi_tally_detail_get(gi_ctx* ctx, uint64_t* score_hist, uint32_t* rule_ids, uint64_t* rule_hits, uint32_t cap,
+                        uint32_t* n_rules);
 int gi_stats_get(gi_ctx* ctx, gi_stats* out);
 /* Opaque hipStream_t of the ctx (for HIP-event timing by the caller). */
 void* gi_ctx_stream(gi_ctx* ctx);

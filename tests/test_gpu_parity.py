@@ -234,3 +234,29 @@ def test_gpu_parity_multimatch():
     assert scores[7] == 2002 and int(res.verdicts[7]["status"]) == 403
     batch = traffic.TrafficGen(traffic.SEED + 9).batch(800, attack_rate=0.3)
     _parity(MULTI, batch)
+
+
+def test_gpu_tally_detail():
+    """Detail tally (gi_tally_detail_get): the per-rule match counts equal the
+    matched-rule lists counted on the host, the score histogram equals the
+    first export's values binned on the host (SURVEY §8(e) tally)."""
+    text = open(CRS).read()
+    batch = traffic.TrafficGen(traffic.SEED + 11).batch(3000, post_frac=0.2, attack_rate=0.3)
+    rs = gpuinspect.Ruleset(text)
+    eng = gpuinspect.Engine(rs, matched_cap=128)
+    res = eng.inspect(batch)
+    d = eng.tally_detail()
+    assert len(d["rule_ids"]) == rs.info["n_rules"] == len(d["rule_hits"])
+    want = {}
+    for i in range(batch.n_req):
+        for rid in set(res.matched_rules(i)):
+            want[rid] = want.get(rid, 0) + res.matched_rules(i).count(rid)
+    got = {}
+    for rid, h in zip(d["rule_ids"], d["rule_hits"]):
+        if rid:
+            got[rid] = got.get(rid, 0) + h
+    assert {k: v for k, v in got.items() if v} == want
+    import numpy as np
+    b = np.clip(res.verdicts["tx_export"][:, 0], 0, 63)
+    assert d["score_hist"] == [int((b == k).sum()) for k in range(64)]
+    assert sum(want.values()) == int(eng.tally()["matched_total"])
