@@ -40,12 +40,15 @@ struct Slot {
   uint32_t state;  // 0 unset, 1 integer (canonical decimal), 2 string
 };
 
-__device__ __constant__ uint8_t kConstStrs[] = "0\0URLENCODED\0JSON\0XML\0MULTIPART\0\0\0\0\0\0\0\0";  // padded for load_u32u
+__device__ __constant__ uint8_t kConstStrs[] =
+    "0\0URLENCODED\0JSON\0XML\0MULTIPART\0" "1\0JSON: invalid JSON\0\0\0\0\0\0\0\0";  // padded for load_u32u
 #define CS_ZERO (kConstStrs + 0)
 #define CS_URLENCODED (kConstStrs + 2)
 #define CS_JSON (kConstStrs + 13)
 #define CS_XML (kConstStrs + 18)
 #define CS_MULTIPART (kConstStrs + 22)
+#define CS_ONE (kConstStrs + 32)
+#define CS_JSON_ERR (kConstStrs + 34)
 
 __device__ inline bool ishex(uint8_t c) {
   return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
@@ -871,11 +874,13 @@ __device__ __forceinline__ void parse_query(Tx& t, const uint8_t* q, uint32_t n,
 // non-empty array's own key = its element count after its elements.  A key
 // written twice is one entry (Go map + ARGS_POST SetIndex(key, 0)) at the
 // first write's position holding the last write's value.
-// Bodies outside RFC 8259, with a scalar root, nested deeper than
-// GI_JSON_MAX_DEPTH, or whose flattened keys + unescaped strings + array
-// counts exceed 4 x body + 1024 bytes (the arena runtime.cpp reserves; deep
-// nesting makes the keys quadratic) are flagged GI_REQ_UNSUPPORTED_BODY
-// (oracle: json_flatten).
+// Read left to right; the first of these events decides (oracle: json_flatten):
+//  * a syntax error (not RFC 8259 JSON: gjson.Valid false) -> GI_REQ_BODY_ERROR:
+//    readJSON's error, so the caller sets REQBODY_ERROR and drops ARGS_POST;
+//  * an engine limit -> GI_REQ_UNSUPPORTED_BODY: a scalar root value, nesting
+//    deeper than GI_JSON_MAX_DEPTH, or flattened keys + unescaped strings +
+//    array counts over 4 x body + 1024 bytes (the arena runtime.cpp reserves;
+//    deep nesting makes the keys quadratic).
 #define GI_JSON_MAX_DEPTH 64
 
 struct JFrame {
@@ -1043,7 +1048,9 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
   uint32_t i = 0;
   while (i < n && json_ws(s[i])) i++;
   if (i >= n || (s[i] != '{' && s[i] != '[')) {
-    t.flags |= GI_REQ_UNSUPPORTED_BODY;
+    const uint8_t c0 = i < n ? s[i] : 0;
+    const bool scalar = i < n && (c0 == '"' || c0 == '-' || (c0 >= '0' && c0 <= '9') || c0 == 't' || c0 == 'f' || c0 == 'n');
+    t.flags |= scalar ? GI_REQ_UNSUPPORTED_BODY : GI_REQ_BODY_ERROR;
     return;
   }
   uint32_t d = 1;
@@ -1051,8 +1058,9 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
   const uint64_t lim = 4ull * n + 1024;
   uint64_t jb = 0;  // flattened bytes (keys, unescaped strings, counts)
   i++;
-  bool bad = false;
-  while (d > 0 && !bad && !(t.flags & GI_REQ_ERROR_MASK)) {
+  bool bad = false;     // syntax error
+  bool limit = false;   // engine limit
+  while (d > 0 && !bad && !limit && !(t.flags & GI_REQ_ERROR_MASK)) {
     JFrame& F = st[d - 1];
     while (i < n && json_ws(s[i])) i++;
     if (i >= n) { bad = true; break; }
@@ -1064,7 +1072,7 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
         const uint32_t dn = go_itoa((int64_t)F.count, nb);
         t.nb -= 12 - dn;
         jb += dn;
-        if (jb > lim) { bad = true; break; }
+        if (jb > lim) { limit = true; break; }
         add_field(t, FK_ARG_POST, t.bytes + F.koff, F.kn, nb, dn);
       }
       d--;
@@ -1086,7 +1094,7 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
       kn = F.kn + 1 + go_itoa((int64_t)F.count, key + F.kn + 1);
       t.nb -= F.kn + 12 - kn;  // give back the unused tail
       jb += kn;
-      if (jb > lim) { bad = true; break; }
+      if (jb > lim) { limit = true; break; }
     } else {
       if (i >= n || s[i] != '"') { bad = true; break; }
       bool esc;
@@ -1106,7 +1114,7 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
       kn = F.kn + 1 + sn;
       t.nb -= rn - sn;
       jb += kn;
-      if (jb > lim) { bad = true; break; }
+      if (jb > lim) { limit = true; break; }
       i = e;
       while (i < n && json_ws(s[i])) i++;
       if (i >= n || s[i] != ':') { bad = true; break; }
@@ -1117,7 +1125,7 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
     if (i >= n) { bad = true; break; }
     const uint8_t c = s[i];
     if (c == '{' || c == '[') {
-      if (d >= GI_JSON_MAX_DEPTH) { bad = true; break; }
+      if (d >= GI_JSON_MAX_DEPTH) { limit = true; break; }
       st[d++] = {(uint32_t)(key - t.bytes), kn, 0, c == '[' ? 1u : 0u};
       i++;
     } else if (c == '"') {
@@ -1131,7 +1139,7 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
         const uint32_t vn = json_unescape(s + i + 1, rn, v);
         t.nb -= rn - vn;
         jb += vn;
-        if (jb > lim) { bad = true; break; }
+        if (jb > lim) { limit = true; break; }
         add_field(t, FK_ARG_POST, key, kn, v, vn);
       } else {
         add_field(t, FK_ARG_POST, key, kn, s + i + 1, rn);
@@ -1153,12 +1161,16 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
       i = e;
     }
   }
-  if (!bad && d == 0) {
+  if (!bad && !limit && d == 0) {
     while (i < n && json_ws(s[i])) i++;
     bad = i != n;
   }
-  if (bad || d != 0) {
+  if (limit) {
     t.flags |= GI_REQ_UNSUPPORTED_BODY;
+    return;
+  }
+  if (bad || d != 0) {
+    t.flags |= GI_REQ_BODY_ERROR;
     return;
   }
   if (!(t.flags & GI_REQ_ERROR_MASK)) json_fold_keys(t, f0);
@@ -1697,37 +1709,45 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
 // run_actions site serves both forms (the Tx stays in registers).
 __device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn) {
   uint32_t nm = 0;
-  bool ok = true;
-  Str cur{v, vn};
-  uint32_t k = R.tchain_len;  // transformations applied so far
-  if (R.flags & RF_MULTIMATCH) {
-    k = 0;
-  } else {
-    cur = transform(t, R, v, vn, &ok);
+  const uint8_t* cp = v;  // current candidate
+  uint32_t cn = vn;
+  uint32_t k = 0;         // transformations applied so far
+  if (!(R.flags & RF_MULTIMATCH)) {
+    bool ok;
+    const Str tv = transform(t, R, v, vn, &ok);
     if (!ok) return 0;
+    cp = tv.p;
+    cn = tv.n;
+    k = R.tchain_len;
   }
-  while (true) {
-    if (eval_op(t, o, cur.p, cur.n)) {
-      run_actions(t, R);
-      nm++;
+  // `fresh` = cp is a candidate not yet tested.  The loop body has no
+  // continue: a candidate search written with continue/break was
+  // miscompiled here (a lane's candidate update after an early loop exit was
+  // lost while other lanes of the wave took the identity path).
+  for (bool fresh = true;; k++) {
+    if (fresh) {
+      if (eval_op(t, o, cp, cn)) {
+        run_actions(t, R);
+        nm++;
+      }
     }
-    // the next candidate: the first remaining transformation that changes cur
-    bool next = false;
-    while (k < R.tchain_len && !next) {
-      const uint8_t code = t.P->tchains[R.tchain_off + k];
-      k++;
-      if (!(value_summary(cur.p, cur.n) & transform_triggers(code))) continue;  // identity
-      uint8_t* dst = (cur.p == t.t0) ? t.t1 : t.t0;
-      const int64_t m = apply_transform(*t.P, code, cur.p, cur.n, dst, t.cap_t);
+    if (k >= R.tchain_len) break;
+    const uint8_t code = t.P->tchains[R.tchain_off + k];
+    bool changed = false;
+    if (value_summary(cp, cn) & transform_triggers(code)) {  // else an identity on cp
+      uint8_t* dst = (cp == t.t0) ? t.t1 : t.t0;
+      const int64_t m = apply_transform(*t.P, code, cp, cn, dst, t.cap_t);
       if (m < 0) {
         t.flags |= GI_REQ_OVERFLOW;
-        return nm;
+        break;
       }
-      if ((uint32_t)m == cur.n && eq_bytes(dst, (uint32_t)m, cur.p, cur.n)) continue;  // unchanged
-      cur = {dst, (uint32_t)m};
-      next = true;
+      changed = !((uint32_t)m == cn && eq_bytes(dst, (uint32_t)m, cp, cn));  // unchanged: no candidate
+      if (changed) {
+        cp = dst;
+        cn = (uint32_t)m;
+      }
     }
-    if (!next) break;
+    fresh = changed;
   }
   return nm;
 }
@@ -3072,6 +3092,15 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
                   t.nf = jc.nf;
                   t.nb = jc.nb;
                   t.flags = jc.flags;
+                  if (t.flags & GI_REQ_BODY_ERROR) {
+                    // readJSON's error -> generateRequestBodyError: REQBODY_ERROR "1",
+                    // REQBODY_ERROR_MSG "<processor>: <error>", no ARGS_POST, no REQUEST_BODY;
+                    // phase 2 still runs (CRS base rule 200002 denies with 400)
+                    t.nf = nf0;
+                    t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
+                    t.single[S_REQBODY_ERROR_MSG] = {CS_JSON_ERR, 18};
+                    t.single[S_REQUEST_BODY] = {CS_ZERO, 0};
+                  }
                 }
                 t.has_post = t.nf > nf0;
               }

@@ -45,6 +45,7 @@ GI_REQ_UNSUPPORTED_BODY = 0x2
 GI_REQ_BODY_LIMIT = 0x4
 GI_REQ_OVERFLOW = 0x8
 GI_REQ_MATCH_TRUNC = 0x10
+GI_REQ_BODY_ERROR = 0x20
 GI_REQ_ERROR_MASK = 0x0F
 
 ACTIONS = {0: "", 1: "deny", 2: "drop", 3: "redirect"}

@@ -51,10 +51,11 @@ extern "C" {
 
 /* per-request verdict flags (gi_verdict.flags) */
 #define GI_REQ_UNSUPPORTED_URI 0x1   /* request-target outside the supported forms */
-#define GI_REQ_UNSUPPORTED_BODY 0x2  /* body processor not implemented (XML/MULTIPART) or JSON outside RFC 8259 */
+#define GI_REQ_UNSUPPORTED_BODY 0x2  /* body processor not implemented, or a body beyond the engine's limits */
 #define GI_REQ_BODY_LIMIT 0x4        /* body over SecRequestBodyLimit */
 #define GI_REQ_OVERFLOW 0x8          /* internal per-request capacity exceeded */
 #define GI_REQ_MATCH_TRUNC 0x10      /* more matched rules than matched_cap */
+#define GI_REQ_BODY_ERROR 0x20       /* the body processor rejected the body: REQBODY_ERROR=1 (verdict valid) */
 #define GI_REQ_ERROR_MASK 0x0F       /* verdict is not valid when any of these is set */
 
 /* interruption action (coraza types.Interruption.Action) */

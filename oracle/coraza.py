@@ -1310,6 +1310,12 @@ class _JsonReader:
         return s[start:self.i]
 
 
+class JsonBodyError(ValueError):
+    """The body is not JSON (gjson.Valid false): [upstream json.go readJSON]
+    returns an error, ProcessRequestBody calls generateRequestBodyError and
+    still evaluates phase 2 (REQBODY_ERROR=1, no ARGS_POST)."""
+
+
 def json_flatten(body: bytes):
     """[upstream coraza internal/bodyprocessors/json.go readJSON/readItems].
 
@@ -1321,80 +1327,97 @@ def json_flatten(body: bytes):
     into ARGS_POST (case-sensitive keys, as MAP_VARS above) with
     SetIndex(key, 0, value) in (random) map order; this engine fixes the
     order to the first write of a key, holding the last value written.
-    Returns None where this engine flags the body unsupported: not valid
-    JSON, a scalar at the root, nesting deeper than JSON_MAX_DEPTH, or more
-    than 4 x len(body) + 1024 flattened bytes (every element's key, every
-    string value that held escapes, every array count)."""
+
+    Read left to right; the first of these events decides:
+      * a syntax error (not RFC 8259 JSON; gjson.Valid false) -> JsonBodyError;
+      * an engine limit -> None (flagged unsupported): a scalar root value,
+        nesting deeper than JSON_MAX_DEPTH, more than 4 x len(body) + 1024
+        flattened bytes (every element's key, every string value that held
+        escapes, every array count).
+    The event order is the device parser's (kernels.hip parse_json_body)."""
     rd = _JsonReader(body)
     res: Dict[bytes, Tuple[bytes, bytes]] = {}
-    flat = [0]
+    lim = JSON_FLAT_LIMIT(len(body))
+    flat = 0
+    n = len(body)
+
+    class _Limit(Exception):
+        pass
 
     def put(key: bytes, val: bytes):
         res[key] = (key, val)
 
-    def value(key: bytes, depth: int):
-        c = rd.peek()
-        if c == 0x7B or c == 0x5B:
-            container(key, depth + 1)
-        elif c == 0x22:
-            v = rd.string()
-            if rd.escaped:
-                flat[0] += len(v)
-            put(key, v)
-        elif c == 0x74 or c == 0x66 or c == 0x6E:
-            for lit in (b"true", b"false", b"null"):
-                if rd.s.startswith(lit, rd.i):
-                    rd.i += len(lit)
-                    put(key, b"" if lit == b"null" else lit)
-                    return
-            raise _JsonInvalid()
-        else:
-            put(key, rd.number())
-
-    def container(key: bytes, depth: int):
-        if depth > JSON_MAX_DEPTH:
-            raise _JsonInvalid()
-        is_arr = rd.peek() == 0x5B
-        close = 0x5D if is_arr else 0x7D
-        rd.i += 1
-        count = 0
+    try:
         rd.ws()
-        if rd.peek() == close:
-            rd.i += 1
-            return
-        while True:
+        if rd.i >= n:
+            raise _JsonInvalid()
+        c0 = body[rd.i]
+        if c0 not in (0x7B, 0x5B):
+            if c0 in b'"-0123456789tfn':
+                return None  # a (possibly valid) scalar root: engine limit
+            raise _JsonInvalid()
+        # frame: [key, count, is_arr]
+        st = [[b"json", 0, c0 == 0x5B]]
+        rd.i += 1
+        while st:
+            F = st[-1]
             rd.ws()
-            if is_arr:
-                sub = key + b"." + str(count).encode()
+            c = rd.peek()
+            if c == (0x5D if F[2] else 0x7D):
+                rd.i += 1
+                if F[2] and F[1]:
+                    cnt = str(F[1]).encode()
+                    flat += len(cnt)
+                    if flat > lim:
+                        raise _Limit()
+                    put(F[0], cnt)
+                st.pop()
+                continue
+            if F[1]:
+                rd.expect(0x2C)
+                rd.ws()
+            if F[2]:
+                key = F[0] + b"." + str(F[1]).encode()
+                flat += len(key)
+                if flat > lim:
+                    raise _Limit()
             else:
                 name = rd.string()
+                key = F[0] + b"." + name
+                flat += len(key)
+                if flat > lim:
+                    raise _Limit()
                 rd.ws()
                 rd.expect(0x3A)
                 rd.ws()
-                sub = key + b"." + name
-            flat[0] += len(sub)
-            value(sub, depth)
-            count += 1
-            rd.ws()
+            F[1] += 1
             c = rd.peek()
-            rd.i += 1
-            if c == close:
-                break
-            if c != 0x2C:
-                raise _JsonInvalid()
-        if is_arr:
-            put(key, str(count).encode())
-            flat[0] += len(str(count))
-
-    try:
+            if c == 0x7B or c == 0x5B:
+                if len(st) >= JSON_MAX_DEPTH:
+                    raise _Limit()
+                st.append([key, 0, c == 0x5B])
+                rd.i += 1
+            elif c == 0x22:
+                v = rd.string()
+                if rd.escaped:
+                    flat += len(v)
+                    if flat > lim:
+                        raise _Limit()
+                put(key, v)
+            elif c in (0x74, 0x66, 0x6E):
+                lit = b"true" if c == 0x74 else b"false" if c == 0x66 else b"null"
+                if not rd.s.startswith(lit, rd.i):
+                    raise _JsonInvalid()
+                rd.i += len(lit)
+                put(key, b"" if lit == b"null" else lit)
+            else:
+                put(key, rd.number())
         rd.ws()
-        if rd.peek() not in (0x7B, 0x5B):
-            return None
-        container(b"json", 1)
-        rd.ws()
-        if rd.i != len(body) or flat[0] > JSON_FLAT_LIMIT(len(body)):
-            return None
-    except (_JsonInvalid, RecursionError):
+        if rd.i != n:
+            raise _JsonInvalid()
+    except _JsonInvalid:
+        raise JsonBodyError("invalid JSON")
+    except _Limit:
         return None
     return list(res.values())
 
@@ -1761,11 +1784,21 @@ class Transaction:
                 self.maps["ARGS_POST"] = parse_query(self.body)
             elif rbp == b"JSON":
                 # [upstream json.go ProcessRequest]: ARGS_POST from readJSON,
-                # the raw body kept as REQUEST_BODY
-                args = json_flatten(self.body)
-                if args is None:
-                    raise UnsupportedInput("JSON body outside the supported grammar")
-                self.single["REQUEST_BODY"] = self.body
+                # the raw body kept as REQUEST_BODY.  A body that is not JSON:
+                # readJSON's error -> generateRequestBodyError (REQBODY_ERROR
+                # "1", REQBODY_ERROR_MSG "<processor>: <error>"), no ARGS_POST,
+                # no REQUEST_BODY, and phase 2 still runs (CRS base rule
+                # 200002 then denies with 400).
+                try:
+                    args = json_flatten(self.body)
+                except JsonBodyError as e:
+                    self.single["REQBODY_ERROR"] = b"1"
+                    self.single["REQBODY_ERROR_MSG"] = b"JSON: " + str(e).encode()
+                    args = []
+                else:
+                    if args is None:
+                        raise UnsupportedInput("JSON body beyond the engine's limits")
+                    self.single["REQUEST_BODY"] = self.body
                 self.maps["ARGS_POST"] = args
             elif rbp == b"":
                 pass

@@ -49,7 +49,8 @@ VECTORS = [
     ('{"café": "ü"}'.encode(), [("json.café".encode(), "ü".encode())]),
 ]
 
-INVALID = [b"", b"1", b'"s"', b"null", b"{", b'{"a":1,}', b"[1,]", b"[01]", b"[1.]", b"[.5]", b"[-]",
+SCALAR_ROOTS = [b"1", b'"s"', b"null", b" -2 "]  # engine limit: flagged unsupported
+INVALID = [b"", b"  ", b"x", b"{", b'{"a":1,}', b"[1,]", b"[01]", b"[1.]", b"[.5]", b"[-]",
            b"[1e]", b'{"a" 1}', b"{a:1}", b"[tru]", b"[nul]", b'["\\x"]', b'["\\u12"]', b'["a\nb"]',
            b"[1] x", b"[1][2]", b"{'a':1}", b"[1 2]", b'{"a":1 "b":2}']
 
@@ -61,7 +62,36 @@ def test_oracle_json_flatten(body, want):
 
 @pytest.mark.parametrize("body", INVALID, ids=[str(i) for i in range(len(INVALID))])
 def test_oracle_json_invalid(body):
+    """Not JSON: readJSON's error -> REQBODY_ERROR (not an engine limit)."""
+    with pytest.raises(coraza.JsonBodyError):
+        coraza.json_flatten(body)
+
+
+@pytest.mark.parametrize("body", SCALAR_ROOTS, ids=[str(i) for i in range(len(SCALAR_ROOTS))])
+def test_oracle_json_scalar_root(body):
     assert coraza.json_flatten(body) is None
+
+
+def test_oracle_json_first_event_decides():
+    """Left to right, the first of {syntax error, engine limit} decides."""
+    deep_then_bad = b"[" * (coraza.JSON_MAX_DEPTH + 1) + b"x"
+    assert coraza.json_flatten(deep_then_bad) is None
+    bad_then_deep = b"[x" + b"[" * (coraza.JSON_MAX_DEPTH + 1)
+    with pytest.raises(coraza.JsonBodyError):
+        coraza.json_flatten(bad_then_deep)
+
+
+def test_oracle_json_body_error_verdict():
+    """CRS base rule 200002 (REQBODY_ERROR !@eq 0 -> deny 400,
+    generate_coreruleset_configmaps.py:73-81) fires on a body that is not JSON."""
+    cfg = coraza.parse_seclang(open(CRS).read())
+    req = coraza.Request(b"POST", b"/api", b"HTTP/1.1", [(b"Host", b"x"), (b"Content-Type", b"application/json")],
+                         b'{"a": 1,}')
+    v = coraza.inspect(cfg, req)
+    assert not v.unsupported and (v.rule_id, v.status, v.phase) == (200002, 400, 2)
+    ok = coraza.Request(b"POST", b"/api", b"HTTP/1.1", [(b"Host", b"x"), (b"Content-Type", b"application/json")],
+                        b'{"a": 1}')
+    assert coraza.inspect(cfg, ok).status == 0
 
 
 def test_oracle_json_depth_limit():
@@ -105,7 +135,7 @@ def _parity(text, batch):
 @pytest.mark.gpu
 def test_gpu_json_edge_bodies():
     text = open(CRS).read()
-    bodies = [b for b, _ in VECTORS] + INVALID
+    bodies = [b for b, _ in VECTORS] + INVALID + SCALAR_ROOTS
     deep = b"[" * 64 + b'"<script>alert(1)</script>"' + b"]" * 64
     bodies += [deep, deep + b" " * 1100, b"[" * 65 + b"]" * 65,
                b'{"q": "1 UNION SELECT username, password FROM users"}',
@@ -118,9 +148,16 @@ def test_gpu_json_edge_bodies():
     txs = [_json_tx(b) for b in bodies]
     txs += [_json_tx(b, ctype=b"application/vnd.api+json") for b in bodies[:4]]
     res, orc = _parity(text, gpuinspect.pack(txs))
-    # invalid bodies are flagged, valid ones evaluated
-    assert sum(1 for o in orc.values() if o.unsupported) >= len(INVALID)
-    assert int((res.verdicts["action"] != 0).sum()) >= 5
+    # bodies that are not JSON get Coraza's verdict: REQBODY_ERROR -> rule 200002 -> 400
+    nv = len(VECTORS)
+    for k in range(nv, nv + len(INVALID)):
+        assert (int(res.verdicts[k]["rule_id"]), int(res.verdicts[k]["status"])) == (200002, 400), bodies[k]
+        assert int(res.verdicts[k]["flags"]) & gpuinspect.GI_REQ_BODY_ERROR
+    # engine limits (scalar roots, nesting deeper than 64) stay flagged
+    assert all(int(res.verdicts[k]["flags"]) & gpuinspect.GI_REQ_UNSUPPORTED_BODY
+               for k in range(nv + len(INVALID), nv + len(INVALID) + len(SCALAR_ROOTS)))
+    assert sum(1 for o in orc.values() if o.unsupported) == len(SCALAR_ROOTS) + 2  # + 65 deep, + 64 deep w/o room
+    assert int((res.verdicts["action"] != 0).sum()) >= 5 + len(INVALID)
 
 
 @pytest.mark.gpu
