@@ -1039,20 +1039,20 @@ __device__ __forceinline__ void json_fold_keys(C& t, uint32_t f0) {
 template <class C>
 __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t n) {
   const uint32_t f0 = t.nf;
+  uint32_t i = 0;
+  while (i < n && json_ws(s[i])) i++;
+  if (i >= n || (s[i] != '{' && s[i] != '[')) {  // (before any allocation: runtime.cpp sizes
+    const uint8_t c0 = i < n ? s[i] : 0;          // the parser arena for '{' / '[' bodies only)
+    const bool scalar = i < n && (c0 == '"' || c0 == '-' || (c0 >= '0' && c0 <= '9') || c0 == 't' || c0 == 'f' || c0 == 'n');
+    t.flags |= scalar ? GI_REQ_UNSUPPORTED_BODY : GI_REQ_BODY_ERROR;
+    return;
+  }
   JFrame* st = (JFrame*)tx_alloc(t, (GI_JSON_MAX_DEPTH + 1) * sizeof(JFrame) + 8);
   if (!st) return;
   st = (JFrame*)(((uintptr_t)st + 7) & ~(uintptr_t)7);
   uint8_t* root = tx_alloc(t, 4);
   if (!root) return;
   root[0] = 'j'; root[1] = 's'; root[2] = 'o'; root[3] = 'n';
-  uint32_t i = 0;
-  while (i < n && json_ws(s[i])) i++;
-  if (i >= n || (s[i] != '{' && s[i] != '[')) {
-    const uint8_t c0 = i < n ? s[i] : 0;
-    const bool scalar = i < n && (c0 == '"' || c0 == '-' || (c0 >= '0' && c0 <= '9') || c0 == 't' || c0 == 'f' || c0 == 'n');
-    t.flags |= scalar ? GI_REQ_UNSUPPORTED_BODY : GI_REQ_BODY_ERROR;
-    return;
-  }
   uint32_t d = 1;
   st[0] = {(uint32_t)(root - t.bytes), 4, 0, s[i] == '[' ? 1u : 0u};
   const uint64_t lim = 4ull * n + 1024;
