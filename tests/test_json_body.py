@@ -150,14 +150,16 @@ def test_gpu_json_edge_bodies():
     res, orc = _parity(text, gpuinspect.pack(txs))
     # bodies that are not JSON get Coraza's verdict: REQBODY_ERROR -> rule 200002 -> 400
     nv = len(VECTORS)
+    # (an empty body is never processed: ProcessRequestBody skips empty bodies)
     for k in range(nv, nv + len(INVALID)):
-        assert (int(res.verdicts[k]["rule_id"]), int(res.verdicts[k]["status"])) == (200002, 400), bodies[k]
-        assert int(res.verdicts[k]["flags"]) & gpuinspect.GI_REQ_BODY_ERROR
+        want = (200002, 400) if bodies[k] else (0, 0)
+        assert (int(res.verdicts[k]["rule_id"]), int(res.verdicts[k]["status"])) == want, bodies[k]
+        assert bool(int(res.verdicts[k]["flags"]) & gpuinspect.GI_REQ_BODY_ERROR) == bool(bodies[k])
     # engine limits (scalar roots, nesting deeper than 64) stay flagged
     assert all(int(res.verdicts[k]["flags"]) & gpuinspect.GI_REQ_UNSUPPORTED_BODY
                for k in range(nv + len(INVALID), nv + len(INVALID) + len(SCALAR_ROOTS)))
     assert sum(1 for o in orc.values() if o.unsupported) == len(SCALAR_ROOTS) + 2  # + 65 deep, + 64 deep w/o room
-    assert int((res.verdicts["action"] != 0).sum()) >= 5 + len(INVALID)
+    assert int((res.verdicts["action"] != 0).sum()) >= 5 + len(INVALID) - 1
 
 
 @pytest.mark.gpu
