@@ -132,7 +132,7 @@ def main():
     raw = batch.raw_bytes()
     eng.stage(batch)
 
-    gather = shard.TallyGather(dist, world, "cuda", n_rules=rs.info["n_rules"]) if dist is not None else None
+    gather = shard.TallyGather(dist, world, "cuda", n_rules=eng.tally_rule_count()) if dist is not None else None
 
     def step():
         eng.run()

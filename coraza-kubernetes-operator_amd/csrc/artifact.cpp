@@ -40,14 +40,15 @@ uint64_t compiler_rev_hash() { return fnv64((const uint8_t*)kCompilerRev, strlen
   X(1, rules) X(2, top) X(3, vars) X(4, excs) X(5, ops) X(6, acts) X(7, tparts) X(8, tmpls) X(9, tchains)    \
   X(10, dfas) X(11, trans) X(12, u8pool) X(13, nranges) X(14, strpool) X(15, slot_names) X(16, u64pool)     \
   X(17, streams) X(18, filters) X(19, sfilt) X(20, body_links) X(21, always_slots) X(22, jobs) X(23, jdfas) \
-  X(24, pats) X(25, svals) X(26, images) X(27, exports)
+  X(24, pats) X(25, svals) X(26, images) X(27, exports) X(28, nfas)
 
 constexpr uint32_t kTagScalars = 100, kTagPlan = 101, kTagExportNames = 102;
 
 uint64_t layout_signature() {
   const uint64_t sz[] = {sizeof(DRule), sizeof(DVarRef), sizeof(DExc), sizeof(DOp), sizeof(DAction),
                          sizeof(DTmplPart), sizeof(DTmpl), sizeof(DDfa), sizeof(DStream), sizeof(DFilter),
-                         sizeof(DJob), sizeof(DJobDfa), sizeof(DPat), sizeof(DScanVal), sizeof(Scalars)};
+                         sizeof(DJob), sizeof(DJobDfa), sizeof(DPat), sizeof(DScanVal), sizeof(Scalars),
+                         sizeof(DNfa)};
   return fnv64((const uint8_t*)sz, sizeof(sz));
 }
 
@@ -250,6 +251,19 @@ bool validate_program(const Program& P, std::string* err) {
     }
   }
   auto single_dfa = [&](int32_t id) { return id >= 0 && (size_t)id < ndfa && !P.dfas[id].multi; };
+  for (const DNfa& f : P.nfas) {
+    const uint64_t W = f.words;
+    if (W == 0 || W > GI_NFA_MAX_WORDS || (uint64_t)f.n_pos + 1 > 64 * W || f.n_classes == 0 || f.n_classes > 256)
+      return bad("nfa shape");
+    if (!in(f.amap_off, 128, P.u8pool.size()) || !in(f.combo_off, f.n_classes, P.u8pool.size()) ||
+        !in(f.nr_off, 3ull * f.nr_cnt, P.nranges.size()) || !in(f.cm_off, f.n_classes * W, P.u64pool.size()) ||
+        !in(f.follow_off, ((uint64_t)f.n_pos + 1) * 16 * W, P.u64pool.size()))
+      return bad("nfa tables");
+    for (uint32_t k = 0; k < 128; k++)
+      if (P.u8pool[f.amap_off + k] >= f.n_classes) return bad("nfa class");
+    for (uint32_t k = 0; k < f.nr_cnt; k++)
+      if (P.nranges[f.nr_off + 3 * k + 2] >= f.n_classes) return bad("nfa rune class");
+  }
   // templates
   for (const DTmpl& t : P.tmpls)
     if (!in(t.part_begin, t.part_count, P.tparts.size())) return bad("template parts");
@@ -265,7 +279,7 @@ bool validate_program(const Program& P, std::string* err) {
     if (!in(r.var_begin, r.var_count, P.vars.size()) || (r.op >= 0 && (uint32_t)r.op >= P.ops.size()) ||
         !in(r.act_begin, r.act_count, P.acts.size()) || !in(r.tchain_off, r.tchain_len, P.tchains.size()) ||
         (r.chain_next >= 0 && (uint32_t)r.chain_next >= nrules) || r.phase > 5 ||
-        (r.hit_slot >= 0 && (uint32_t)r.hit_slot >= nhit) || r.hit_slot < -1 || r.top_idx >= P.top.size())
+        (r.hit_slot >= 0 && (uint32_t)r.hit_slot >= nhit) || r.hit_slot < -1)
       return bad("rule record out of range");
   }
   for (uint32_t t : P.body_links)
@@ -281,8 +295,9 @@ bool validate_program(const Program& P, std::string* err) {
     if (x.dfa >= 0 ? !single_dfa(x.dfa) : !in(x.off, x.len, nstr)) return bad("exception");
   }
   for (const DOp& o : P.ops) {
-    if ((o.kind == OP_RX || o.kind == OP_PM) && !single_dfa(o.dfa)) return bad("operator automaton");
+    if ((o.kind == OP_RX || o.kind == OP_PM) && !single_dfa(o.dfa) && o.nfa < 0) return bad("operator automaton");
     if (o.dfa >= 0 && !single_dfa(o.dfa)) return bad("operator automaton index");
+    if (o.nfa >= 0 && (size_t)o.nfa >= P.nfas.size()) return bad("operator nfa index");
     if (o.tmpl >= 0 && (size_t)o.tmpl >= ntm) return bad("operator template");
     if (o.arg_is_lit && !in(o.lit_off, o.lit_len, nstr)) return bad("operator literal");
   }

@@ -392,7 +392,11 @@ bool transform_code(const std::string& t, uint8_t* code) {
       {"trimright", T_TRIMRIGHT}, {"normalizepath", T_NORMALIZEPATH},
       {"normalisepath", T_NORMALIZEPATH}, {"normalizepathwin", T_NORMALIZEPATHWIN},
       {"normalisepathwin", T_NORMALIZEPATHWIN}, {"jsdecode", T_JSDECODE},
-      {"utf8tounicode", T_UTF8TOUNICODE}};
+      {"utf8tounicode", T_UTF8TOUNICODE}, {"base64decode", T_BASE64DECODE},
+      {"base64decodeext", T_BASE64DECODEEXT}, {"base64encode", T_BASE64ENCODE}, {"hexdecode", T_HEXDECODE},
+      {"hexencode", T_HEXENCODE}, {"sha1", T_SHA1}, {"md5", T_MD5}, {"urlencode", T_URLENCODE},
+      {"cssdecode", T_CSSDECODE}, {"escapeseqdecode", T_ESCAPESEQDECODE},
+      {"removecommentschar", T_REMOVECOMMENTSCHAR}};
   auto it = m.find(t);
   if (it == m.end()) return false;
   *code = it->second;
@@ -615,7 +619,8 @@ struct Lower {
   Program* P;
   std::map<std::string, int> slots;
   std::map<std::string, int> markers;
-  std::map<std::string, int> dfa_cache;
+  std::map<std::string, int> dfa_cache;  // -1: no DFA (state cap), see nfa_cache
+  std::map<std::string, int> nfa_cache;
   uint32_t cap;
 
   uint32_t str(const std::string& s) {
@@ -676,18 +681,53 @@ struct Lower {
     P->dfas.push_back(h);
     return (int)P->dfas.size() - 1;
   }
-  int regex_dfa(const std::string& pattern) {
+  // The sticky search DFA of `pattern`.  When it exceeds the state cap and
+  // `nfa` is given (an @rx operator), the exact matcher is the pattern's NFA
+  // tables instead (*nfa = DNfa index, returns -1); key / exception regexes
+  // have no such fallback.
+  int regex_dfa(const std::string& pattern, int32_t* nfa = nullptr) {
     std::string key = "rx:" + pattern;
     auto it = dfa_cache.find(key);
-    if (it != dfa_cache.end()) return it->second;
+    if (it != dfa_cache.end()) {
+      if (it->second < 0 && nfa) *nfa = nfa_cache[key];
+      return it->second;
+    }
     Regex re;
     std::string err;
     if (!re_parse(pattern, &re, &err)) perr("invalid regex " + pattern + ": " + err);
     Dfa d;
-    if (!build_regex_dfa(re, &d, &err, cap)) unsup("regex " + pattern + ": " + err);
+    if (!build_regex_dfa(re, &d, &err, cap)) {
+      if (!nfa) unsup("regex " + pattern + ": " + err);
+      NfaTables t;
+      std::string nerr;
+      if (!build_nfa_tables(re, &t, &nerr)) unsup("regex " + pattern + ": " + err + "; " + nerr);
+      *nfa = add_nfa(t);
+      nfa_cache[key] = *nfa;
+      dfa_cache[key] = -1;
+      return -1;
+    }
     int id = add_dfa(d);
     dfa_cache[key] = id;
     return id;
+  }
+  int add_nfa(const NfaTables& t) {
+    DNfa h{};
+    h.n_classes = t.n_classes;
+    h.n_pos = t.n_pos;
+    h.words = t.words;
+    h.amap_off = (uint32_t)P->u8pool.size();
+    P->u8pool.insert(P->u8pool.end(), t.amap.begin(), t.amap.end());
+    h.combo_off = (uint32_t)P->u8pool.size();
+    P->u8pool.insert(P->u8pool.end(), t.cls_combo.begin(), t.cls_combo.end());
+    h.nr_off = (uint32_t)P->nranges.size();
+    h.nr_cnt = (uint32_t)t.nranges.size() / 3;
+    P->nranges.insert(P->nranges.end(), t.nranges.begin(), t.nranges.end());
+    h.cm_off = P->u64pool.size();
+    P->u64pool.insert(P->u64pool.end(), t.cm.begin(), t.cm.end());
+    h.follow_off = P->u64pool.size();
+    P->u64pool.insert(P->u64pool.end(), t.follow.begin(), t.follow.end());
+    P->nfas.push_back(h);
+    return (int)P->nfas.size() - 1;
   }
   int phrase_dfa(const std::vector<std::string>& phrases, bool fold, const std::string& key) {
     auto it = dfa_cache.find(key);
@@ -761,12 +801,13 @@ struct Lower {
     DOp o{};
     o.negate = r.op_neg ? 1 : 0;
     o.dfa = -1;
+    o.nfa = -1;
     o.tmpl = -1;
     const std::string& n = r.op_name;
     const std::string& a = r.op_arg;
     if (n == "rx") {
       o.kind = OP_RX;
-      o.dfa = regex_dfa("(?sm)" + a);
+      o.dfa = regex_dfa("(?sm)" + a, &o.nfa);
     } else if (n == "pm") {
       o.kind = OP_PM;
       std::vector<std::string> phrases;
@@ -1217,6 +1258,21 @@ struct Lower {
         cur.clear();
         curp.clear();
       };
+      // A pattern's phase-A automaton: its exact DFA, or -- when that exceeds
+      // the state cap -- the DFA of a superset relaxation (regex.h
+      // relax_regex): a prefilter, since the hit bit only has to be a superset
+      // (k_eval re-evaluates the link exactly, on the NFA tables).  A negated
+      // operator has no superset filter: false (the link is always "maybe").
+      auto single_or_relaxed = [&](const PatEntry& pe, const Regex& re, Dfa* out) -> bool {
+        if (build_regex_dfa(re, out, &err, cap)) return true;
+        if (pe.negate || pe.kind != 0) return false;
+        for (int lvl = 1; lvl <= 3; lvl++) {
+          Regex rr = re;
+          relax_regex(&rr, lvl);
+          if (build_regex_dfa(rr, out, &err, cap)) return true;
+        }
+        return false;
+      };
       for (auto& pe : sb.pats) {
         auto re = std::make_unique<Regex>();
         bool ok;
@@ -1234,7 +1290,10 @@ struct Lower {
         }
         if (pe.negate) {  // negated operators stay out of union automata (the scan emits union hits eagerly)
           Dfa single;
-          if (!build_regex_dfa(*re, &single, &err, cap)) unsup("regex " + pe.rx + ": " + err);
+          if (!single_or_relaxed(pe, *re, &single)) {  // no automaton: the link is always "maybe"
+            P->always_slots.push_back(pe.slot);
+            continue;
+          }
           autos.push_back({std::move(single), {&pe}});
           continue;
         }
@@ -1258,10 +1317,13 @@ struct Lower {
         }
         // too large for an LDS union automaton: single sticky DFA (global tables)
         Dfa single;
-        if (!build_regex_dfa(*re, &single, &err, cap)) unsup("regex " + pe.rx + ": " + err);
-        autos.push_back({std::move(single), {&pe}});
         cur.clear();
         curp.clear();
+        if (!single_or_relaxed(pe, *re, &single)) {  // no automaton: the link is always "maybe"
+          P->always_slots.push_back(pe.slot);
+          continue;
+        }
+        autos.push_back({std::move(single), {&pe}});
         owned.push_back(std::move(re));
       }
       flush();
@@ -1589,7 +1651,6 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
       const IrRule& r = waf.rules[ti];
       L.no_scan = gated[ti];
       uint32_t idx = L.rule(r, false);
-      out->rules[idx].top_idx = (uint32_t)out->top.size();
       out->top.push_back(idx);
       uint32_t prev = idx;
       for (auto& c : r.children) {

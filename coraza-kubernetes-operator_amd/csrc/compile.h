@@ -16,7 +16,7 @@ namespace gi {
 // even when the record layout stays the same.  gi_compile folds it into the
 // source digest and the artifact stores it, so an artifact written by another
 // compiler revision is rejected (and recompiled from the rules text).
-constexpr const char* kCompilerRev = "gi-seclang-compiler/3";
+constexpr const char* kCompilerRev = "gi-seclang-compiler/4";
 
 struct Program {
   std::vector<DRule> rules;
@@ -29,6 +29,7 @@ struct Program {
   std::vector<DTmpl> tmpls;
   std::vector<uint8_t> tchains;
   std::vector<DDfa> dfas;
+  std::vector<DNfa> nfas;
   std::vector<uint16_t> trans;
   std::vector<uint8_t> u8pool;
   std::vector<uint32_t> nranges;

@@ -222,19 +222,23 @@ void minimize(Dfa* d) {
   d->acc.swap(acc);
 }
 
-// Shared subset construction over a list of patterns.
-bool build_core(const std::vector<const Regex*>& pats, bool multi, Dfa* out, std::string* err,
-                uint32_t state_cap) {
-  *out = Dfa();
-  out->multi = multi;
-  out->n_pat = (uint32_t)pats.size();
-  if (multi && pats.size() > 64) {
-    *err = "too many patterns for one union automaton";
-    return false;
-  }
-  // 1. rune-class partition over every set of every pattern + word chars + '\n'
+// Rune-class partition over every set of every pattern + word chars + '\n':
+// the alphabet of both the DFA and the NFA tables.
+struct ClassPart {
+  std::vector<std::vector<int>> node_set;  // per pattern: node -> class-set id
+  uint32_t ncls = 0;
+  std::vector<uint8_t> amap;                // 128 ASCII entries
+  std::vector<uint32_t> nranges;            // (lo, hi, cls) for runes >= 0x80
+  std::vector<uint8_t> cls_combo;           // bit0 '\n', bit1 word char
+  std::vector<std::vector<uint64_t>> set_bits;  // class-set id -> classes it holds
+  uint32_t cls_nl = 0;
+  std::vector<uint8_t> cls_word;
+};
+
+bool partition_classes(const std::vector<const Regex*>& pats, ClassPart* cp, std::string* err) {
   std::vector<const RuneSet*> sets = {&kWord, &kNl};
-  std::vector<std::vector<int>> node_set(pats.size());
+  std::vector<std::vector<int>>& node_set = cp->node_set;
+  node_set.assign(pats.size(), {});
   {
     std::unordered_map<std::string, int> uniq;
     for (size_t p = 0; p < pats.size(); p++) {
@@ -287,35 +291,62 @@ bool build_core(const std::vector<const Regex*>& pats, bool multi, Dfa* out, std
     *err = "automaton needs more than 255 rune classes";
     return false;
   }
-  out->n_classes = ncls;
-  out->amap.assign(128, 0);
+  cp->ncls = ncls;
+  cp->amap.assign(128, 0);
   for (size_t b = 0; b + 1 < bounds.size(); b++) {
     uint32_t lo = bounds[b], hi = bounds[b + 1] - 1;
     if (lo < 0x80) {
-      for (uint32_t c = lo; c <= hi && c < 0x80; c++) out->amap[c] = (uint8_t)interval_class[b];
+      for (uint32_t c = lo; c <= hi && c < 0x80; c++) cp->amap[c] = (uint8_t)interval_class[b];
     } else {
       uint32_t cl = interval_class[b];
-      size_t m = out->nranges.size();
-      if (m >= 3 && out->nranges[m - 1] == cl && out->nranges[m - 2] + 1 == lo) {
-        out->nranges[m - 2] = hi;
+      size_t m = cp->nranges.size();
+      if (m >= 3 && cp->nranges[m - 1] == cl && cp->nranges[m - 2] + 1 == lo) {
+        cp->nranges[m - 2] = hi;
       } else {
-        out->nranges.push_back(lo);
-        out->nranges.push_back(hi);
-        out->nranges.push_back(cl);
+        cp->nranges.push_back(lo);
+        cp->nranges.push_back(hi);
+        cp->nranges.push_back(cl);
       }
     }
   }
-  const uint32_t cls_nl = out->amap['\n'];
-  std::vector<uint8_t> cls_word(ncls);
+  const uint32_t cls_nl = cp->amap['\n'];
+  cp->cls_nl = cls_nl;
+  std::vector<uint8_t>& cls_word = cp->cls_word;
+  cls_word.assign(ncls, 0);
   for (uint32_t c = 0; c < ncls; c++) cls_word[c] = (uint8_t)class_sig[c][0];
-  out->cls_combo.assign(ncls, 0);
-  for (uint32_t c = 0; c < ncls; c++) out->cls_combo[c] = (c == cls_nl ? 1 : 0) | (cls_word[c] ? 2 : 0);
+  cp->cls_combo.assign(ncls, 0);
+  for (uint32_t c = 0; c < ncls; c++) cp->cls_combo[c] = (c == cls_nl ? 1 : 0) | (cls_word[c] ? 2 : 0);
   const size_t words = (ncls + 63) / 64;
-  std::vector<std::vector<uint64_t>> set_bits(nsets, std::vector<uint64_t>(words, 0));
+  std::vector<std::vector<uint64_t>>& set_bits = cp->set_bits;
+  set_bits.assign(nsets, std::vector<uint64_t>(words, 0));
   for (uint32_t c = 0; c < ncls; c++)
     for (size_t si = 0; si < nsets; si++)
       if (class_sig[c][si]) set_bits[si][c >> 6] |= 1ull << (c & 63);
 
+  return true;
+}
+
+// Shared subset construction over a list of patterns.
+bool build_core(const std::vector<const Regex*>& pats, bool multi, Dfa* out, std::string* err,
+                uint32_t state_cap) {
+  *out = Dfa();
+  out->multi = multi;
+  out->n_pat = (uint32_t)pats.size();
+  if (multi && pats.size() > 64) {
+    *err = "too many patterns for one union automaton";
+    return false;
+  }
+  ClassPart cp;
+  if (!partition_classes(pats, &cp, err)) return false;
+  const std::vector<std::vector<int>>& node_set = cp.node_set;
+  const uint32_t ncls = cp.ncls;
+  out->n_classes = ncls;
+  out->amap = cp.amap;
+  out->nranges = cp.nranges;
+  out->cls_combo = cp.cls_combo;
+  const uint32_t cls_nl = cp.cls_nl;
+  const std::vector<uint8_t>& cls_word = cp.cls_word;
+  const std::vector<std::vector<uint64_t>>& set_bits = cp.set_bits;
   // 2. Thompson NFA; one MATCH per pattern
   std::vector<Inst> prog;
   std::vector<int> starts;
@@ -481,6 +512,143 @@ bool build_regex_dfa(const Regex& re, Dfa* out, std::string* err, uint32_t state
 
 bool build_union_dfa(const std::vector<const Regex*>& pats, Dfa* out, std::string* err, uint32_t state_cap) {
   return build_core(pats, true, out, err, state_cap);
+}
+
+// Position tables of the Thompson NFA (exact matcher for patterns whose DFA
+// exceeds the state cap).  Positions = the NFA's class instructions.  The
+// assertions between two runes depend only on what the previous and the next
+// rune are (nothing / '\n' / word char / other), so the epsilon closure after
+// a position is tabulated for those 16 combinations.
+bool build_nfa_tables(const Regex& re, NfaTables* out, std::string* err, uint32_t max_pos) {
+  *out = NfaTables();
+  ClassPart cp;
+  if (!partition_classes({&re}, &cp, err)) return false;
+  std::vector<Inst> prog;
+  NfaBuilder nb(re, prog, cp.node_set[0], 400000);
+  Frag f = nb.compile(re.root);
+  Inst m;
+  m.op = I_MATCH;
+  m.arg = 0;
+  const int mpc = nb.emit(m);
+  nb.patch(f.outs, mpc);
+  if (nb.overflow) {
+    *err = "regex too large";
+    return false;
+  }
+  std::vector<int> pos_of(prog.size(), -1), pc_of;
+  for (size_t pc = 0; pc < prog.size(); pc++)
+    if (prog[pc].op == I_CLASS) {
+      pos_of[pc] = (int)pc_of.size();
+      pc_of.push_back((int)pc);
+    }
+  const uint32_t np = (uint32_t)pc_of.size();
+  if (np > max_pos) {
+    *err = "NFA exceeds position cap";
+    return false;
+  }
+  const uint32_t W = (np + 1 + 63) / 64;  // + the match bit (bit np)
+  out->n_classes = cp.ncls;
+  out->n_pos = np;
+  out->words = W;
+  out->amap = cp.amap;
+  out->nranges = cp.nranges;
+  out->cls_combo = cp.cls_combo;
+  out->cm.assign((size_t)cp.ncls * W, 0);
+  for (uint32_t p = 0; p < np; p++) {
+    const std::vector<uint64_t>& bits = cp.set_bits[prog[pc_of[p]].arg];
+    for (uint32_t c = 0; c < cp.ncls; c++)
+      if (bits[c >> 6] >> (c & 63) & 1) out->cm[(size_t)c * W + (p >> 6)] |= 1ull << (p & 63);
+  }
+  out->follow.assign((size_t)(np + 1) * 16 * W, 0);
+  std::vector<uint32_t> mark(prog.size(), 0);
+  uint32_t gen = 0;
+  std::vector<int> stack;
+  for (uint32_t row = 0; row <= np; row++) {
+    for (uint32_t combo = 0; combo < 16; combo++) {
+      const uint32_t prev = combo >> 2, next = combo & 3;  // 0 none, 1 '\n', 2 word, 3 other
+      uint8_t cond = 0;
+      if (prev == 0) cond |= AS_BOT | AS_BOL;
+      if (prev == 1) cond |= AS_BOL;
+      if (next == 0) cond |= AS_EOT | AS_EOL;
+      if (next == 1) cond |= AS_EOL;
+      cond |= ((prev == 2) != (next == 2)) ? AS_WB : AS_NWB;
+      uint64_t* dst = &out->follow[((size_t)row * 16 + combo) * W];
+      gen++;
+      stack.clear();
+      stack.push_back(row == np ? f.start : prog[pc_of[row]].out);
+      while (!stack.empty()) {
+        const int pc = stack.back();
+        stack.pop_back();
+        if (pc < 0 || mark[pc] == gen) continue;
+        mark[pc] = gen;
+        const Inst& in = prog[pc];
+        switch (in.op) {
+          case I_MATCH: dst[np >> 6] |= 1ull << (np & 63); break;
+          case I_CLASS: dst[pos_of[pc] >> 6] |= 1ull << (pos_of[pc] & 63); break;
+          case I_NOP: stack.push_back(in.out); break;
+          case I_SPLIT:
+            stack.push_back(in.out1);
+            stack.push_back(in.out);
+            break;
+          case I_EMPTY:
+            if ((in.assert_kind & cond) == in.assert_kind) stack.push_back(in.out);
+            break;
+        }
+      }
+    }
+  }
+  return true;
+}
+
+// Superset relaxations of a regex, for a phase-A prefilter automaton when the
+// exact DFA exceeds the state cap: level 1 unbounds counted repetitions
+// ({m,n} -> {m,}), level 2 also drops assertions (^ $ \b \B), level 3 also
+// lowers repetition minima to 1.  Each step only removes constraints, so the
+// relaxed language contains the original one.
+void relax_regex(Regex* re, int level) {
+  for (ReNode& n : re->nodes) {
+    if (n.kind == N_REPEAT && n.max != -1 && n.max > n.min && level >= 1) n.max = -1;
+    if (n.kind == N_REPEAT && level >= 3 && n.min > 1) {
+      n.min = 1;
+      n.max = -1;
+    }
+    if (n.kind == N_ASSERT && level >= 2) n.kind = N_EMPTY;
+  }
+}
+
+// Host walk of the NFA tables (compiler self-test; the device runs the same
+// algorithm in kernels.hip nfa_match).
+bool nfa_host_match(const NfaTables& t, const uint8_t* s, size_t n) {
+  const uint32_t W = t.words;
+  std::vector<uint64_t> T(W, 0), S(W);
+  uint32_t prev = 0;
+  size_t i = 0;
+  for (;;) {
+    uint32_t cls = 0, next = 0;
+    int w = 1;
+    if (i < n) {
+      const uint32_t r = s[i] < 0x80 ? s[i] : go_decode_rune(s, n, i, &w);
+      if (r < 0x80) {
+        cls = t.amap[r];
+      } else {
+        for (size_t k = 0; k + 2 < t.nranges.size(); k += 3)
+          if (t.nranges[k] <= r && r <= t.nranges[k + 1]) cls = t.nranges[k + 2];
+      }
+      next = (t.cls_combo[cls] & 1) ? 1 : (t.cls_combo[cls] & 2) ? 2 : 3;
+    }
+    const uint32_t combo = prev * 4 + next;
+    for (uint32_t k = 0; k < W; k++) S[k] = t.follow[((size_t)t.n_pos * 16 + combo) * W + k];
+    for (uint32_t k = 0; k < W; k++)
+      for (uint64_t b = T[k]; b; b &= b - 1) {
+        const uint32_t p = k * 64 + __builtin_ctzll(b);
+        for (uint32_t j = 0; j < W; j++) S[j] |= t.follow[((size_t)p * 16 + combo) * W + j];
+      }
+    if (S[t.n_pos >> 6] >> (t.n_pos & 63) & 1) return true;
+    if (i >= n) return false;
+    for (uint32_t k = 0; k < W; k++) T[k] = S[k] & t.cm[(size_t)cls * W + k];
+    prev = next;
+    i += w;
+  }
 }
 
 bool phrases_to_regex(const std::vector<std::string>& phrases, bool fold_ascii, Regex* out) {

@@ -35,7 +35,7 @@ struct DBatch {
   gi_verdict* verdicts;
   uint32_t* matched;
   unsigned long long* tally;  // gi_tally counters
-  uint32_t* tally_ext;        // [GI_SCORE_BINS] score histogram, then [n_top] per-rule match counts
+  uint32_t* tally_ext;        // [GI_SCORE_BINS] score histogram, then per distinct rule id match counts
   uint32_t* hits;             // phase-A hit words [ceil(n_hit_slots/32)][n_req]
   Slot* txslots;       // TX variables [n_slots][n_req] (k_eval)
   // phase A (see kernels.hip "phase A")
@@ -99,7 +99,8 @@ struct LaunchLog {
 
 // stop_after > 0 (debugging): launch only the first stop_after kernels and
 // synchronise after each, printing the first failing one.
+// tally_ids: the ruleset's distinct rule ids, ascending (k_tally bins).
 void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
-                     int stop_after = 0, LaunchLog* log = nullptr);
+                     int stop_after, LaunchLog* log, const uint32_t* tally_ids, uint32_t n_tally_ids);
 
 }  // namespace gi

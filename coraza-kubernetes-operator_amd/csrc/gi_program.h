@@ -120,6 +120,19 @@ enum TCode : uint8_t {
   T_NORMALIZEPATHWIN,
   T_JSDECODE,
   T_UTF8TOUNICODE,
+  // out-of-line group (kernels.hip t_ext): decoders / encoders / digests
+  T_BASE64DECODE,
+  T_BASE64DECODEEXT,
+  T_BASE64ENCODE,
+  T_HEXDECODE,
+  T_HEXENCODE,
+  T_SHA1,
+  T_MD5,
+  T_URLENCODE,
+  T_CSSDECODE,
+  T_ESCAPESEQDECODE,
+  T_REMOVECOMMENTSCHAR,
+  T_COUNT
 };
 
 enum Disruptive : uint8_t { D_NONE = 0, D_DENY = 1, D_DROP = 2, D_REDIRECT = 3, D_PASS = 4 };
@@ -175,7 +188,7 @@ struct DRule {
   uint8_t flags;        // RuleFlags
   uint8_t _pad;
   int32_t hit_slot;     // phase-A hit bit (-1: evaluated by the interpreter only)
-  uint32_t top_idx;     // position in the top-level rule list (per-rule hit tally); chain links: 0
+  uint32_t _pad2;
 };
 
 // ------------------------------------------------------ phase-A scan plan
@@ -281,7 +294,9 @@ __host__ __device__ inline uint32_t transform_triggers(uint8_t code) {
     case T_CMDLINE: return BS_QUOTE | BS_BSLASH | BS_CARET | BS_WS | BS_SEP | BS_UPPER;
     case T_NORMALIZEPATH: return BS_SLASH | BS_DOT;
     case T_NORMALIZEPATHWIN: return BS_SLASH | BS_DOT | BS_BSLASH;
-    case T_JSDECODE: return BS_BSLASH;
+    case T_JSDECODE:
+    case T_CSSDECODE:
+    case T_ESCAPESEQDECODE: return BS_BSLASH;
     case T_UTF8TOUNICODE: return BS_HIGH;
     default: return BS_ALL;  // t:length and anything new: always run
   }
@@ -359,10 +374,25 @@ struct DOp {
   uint8_t arg_is_lit;  // template is a single literal (no macro)
   uint8_t has_num;     // literal numeric arg parsed at compile time (Atoi ok)
   int32_t dfa;
+  int32_t nfa;         // @rx whose DFA exceeds the state cap: exact NFA tables (DNfa), else -1
   int32_t tmpl;
   uint32_t lit_off, lit_len;
+  uint32_t _pad;
   int64_t num;
   uint32_t bits[8];    // @validateByteRange allowed-byte bitmap
+};
+
+// Exact matcher of an @rx whose DFA exceeds the state cap (regex.h
+// NfaTables): position bitsets of `words` u64 each, bit n_pos = match.
+#define GI_NFA_MAX_WORDS 64  // 4095 positions
+struct DNfa {
+  uint32_t n_classes, n_pos, words, nr_cnt;
+  uint32_t amap_off;    // u8 pool: 128 ASCII classes
+  uint32_t combo_off;   // u8 pool: per class bit0 '\n', bit1 word char
+  uint32_t nr_off;      // u32 pool (nranges): (lo, hi, cls) triples
+  uint32_t _pad;
+  uint64_t cm_off;      // u64 pool: [n_classes][words]
+  uint64_t follow_off;  // u64 pool: [n_pos + 1][16][words]
 };
 
 struct DAction {
@@ -413,6 +443,7 @@ struct DProgram {
   const uint8_t* tchains;
   const uint32_t* tchains32;    // the same codes widened (scalar-loadable in wave-uniform loops)
   const DDfa* dfas;
+  const DNfa* nfas;
   const uint16_t* trans;
   const uint8_t* u8pool;
   const uint32_t* nranges;

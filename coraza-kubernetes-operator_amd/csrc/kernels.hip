@@ -13,6 +13,7 @@
 // function names the coraza source it restates.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 
 #include "gi_kernels.h"
@@ -249,6 +250,58 @@ __device__ bool dfa_match(const DProgram& P, int32_t id, const uint8_t* s, uint3
     }
   }
   return P.u8pool[d.endacc_off + st] != 0;
+}
+
+// Exact NFA simulation for an @rx whose DFA exceeds the state cap (regex.h
+// NfaTables): T = positions consumed by the previous rune; before each rune
+// the epsilon closure from T and from the start (unanchored search) is the
+// union of precomputed rows for (previous, next) rune kinds, which is what
+// ^ $ \b \B look at; a closure holding the match bit is a match.
+__device__ __noinline__ bool nfa_match(const DProgram& P, int32_t id, const uint8_t* s, uint32_t n) {
+  const DNfa N = P.nfas[id];
+  const uint32_t W = N.words;
+  const uint8_t* amap = P.u8pool + N.amap_off;
+  const uint8_t* combo = P.u8pool + N.combo_off;
+  const uint32_t* nr = P.nranges + N.nr_off;
+  const uint64_t* cm = P.u64pool + N.cm_off;
+  const uint64_t* F = P.u64pool + N.follow_off;
+  uint64_t T[GI_NFA_MAX_WORDS], S[GI_NFA_MAX_WORDS];
+  for (uint32_t k = 0; k < W; k++) T[k] = 0;
+  uint32_t prev = 0, i = 0;
+  for (;;) {
+    uint32_t cls = 0, next = 0, w = 1;
+    if (i < n) {
+      const uint8_t c = s[i];
+      if (c < 0x80) {
+        cls = amap[c];
+      } else {
+        const uint32_t r = decode_rune(s, n, i, &w);
+        uint32_t lo = 0, hi = N.nr_cnt;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (nr[mid * 3 + 1] < r) lo = mid + 1;
+          else hi = mid;
+        }
+        cls = (lo < N.nr_cnt && nr[lo * 3] <= r) ? nr[lo * 3 + 2] : 0u;
+      }
+      const uint8_t cb = combo[cls];
+      next = (cb & 1) ? 1u : (cb & 2) ? 2u : 3u;
+    }
+    const uint32_t cmb = prev * 4 + next;
+    const uint64_t* st = F + ((uint64_t)N.n_pos * 16 + cmb) * W;
+    for (uint32_t k = 0; k < W; k++) S[k] = st[k];
+    for (uint32_t k = 0; k < W; k++)
+      for (uint64_t b = T[k]; b; b &= b - 1) {
+        const uint64_t* row = F + ((uint64_t)(k * 64 + __ffsll((unsigned long long)b) - 1) * 16 + cmb) * W;
+        for (uint32_t j = 0; j < W; j++) S[j] |= row[j];
+      }
+    if ((S[N.n_pos >> 6] >> (N.n_pos & 63)) & 1) return true;
+    if (i >= n) return false;
+    const uint64_t* cr = cm + (uint64_t)cls * W;
+    for (uint32_t k = 0; k < W; k++) T[k] = S[k] & cr[k];
+    prev = next;
+    i += w;
+  }
 }
 
 // ----------------------------------------------------------- transforms
@@ -694,6 +747,335 @@ __device__ int64_t t_utf8tounicode(const uint8_t* s, uint32_t n, uint8_t* d, uin
   return o;
 }
 
+// ------------------------------------------------ out-of-line transforms
+// Decoders / encoders / digests [upstream internal/transformations/
+// base64decode.go, base64decodeext.go, base64encode.go, hexdecode.go,
+// hexencode.go, sha1.go, md5.go, urlencode.go, cssdecode.go,
+// escapeseqdecode.go, removecommentschar.go; ModSecurity ports].  Kept out of
+// line so k_stream's inlined LDS chains do not carry their code.
+
+__device__ inline int b64_val(uint8_t c) {
+  if (c >= 'A' && c <= 'Z') return c - 'A';
+  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+  if (c >= '0' && c <= '9') return c - '0' + 52;
+  if (c == '+') return 62;
+  if (c == '/') return 63;
+  return -1;
+}
+
+// ext = false: base64decode (CR/LF skipped, stop at the first other byte
+// outside the alphabet); ext = true: base64decodeext (every such byte skipped)
+__device__ int64_t t_b64decode(bool ext, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  if (n > cap) return -1;
+  uint32_t o = 0, x = 0, k = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t c = s[i];
+    const int v = b64_val(c);
+    if (v < 0) {
+      if (ext || c == '\r' || c == '\n') continue;
+      break;
+    }
+    x = (x << 6) | (uint32_t)v;
+    if (++k == 4) {
+      d[o++] = (uint8_t)(x >> 16);
+      d[o++] = (uint8_t)(x >> 8);
+      d[o++] = (uint8_t)x;
+      x = k = 0;
+    }
+  }
+  if (k == 2) {
+    d[o++] = (uint8_t)((x << 12) >> 16);
+  } else if (k == 3) {
+    x <<= 6;
+    d[o++] = (uint8_t)(x >> 16);
+    d[o++] = (uint8_t)(x >> 8);
+  }
+  return o;
+}
+
+__device__ int64_t t_b64encode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  const char* al = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  const uint64_t out = 4ull * ((n + 2) / 3);
+  if (out > cap) return -1;
+  uint32_t o = 0, i = 0;
+  for (; i + 3 <= n; i += 3) {
+    const uint32_t x = ((uint32_t)s[i] << 16) | ((uint32_t)s[i + 1] << 8) | s[i + 2];
+    d[o++] = al[x >> 18]; d[o++] = al[(x >> 12) & 63]; d[o++] = al[(x >> 6) & 63]; d[o++] = al[x & 63];
+  }
+  if (n - i == 1) {
+    const uint32_t x = (uint32_t)s[i] << 16;
+    d[o++] = al[x >> 18]; d[o++] = al[(x >> 12) & 63]; d[o++] = '='; d[o++] = '=';
+  } else if (n - i == 2) {
+    const uint32_t x = ((uint32_t)s[i] << 16) | ((uint32_t)s[i + 1] << 8);
+    d[o++] = al[x >> 18]; d[o++] = al[(x >> 12) & 63]; d[o++] = al[(x >> 6) & 63]; d[o++] = '=';
+  }
+  return o;
+}
+
+// hex.DecodeString; an error (odd length, non-hex byte) keeps the value
+// (rule.go executeTransformations skips a failed transformation)
+__device__ int64_t t_hexdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  if (n > cap) return -1;
+  bool ok = (n & 1) == 0;
+  for (uint32_t i = 0; i < n && ok; i++) ok = ishex(s[i]);
+  if (!ok) {
+    for (uint32_t i = 0; i < n; i++) d[i] = s[i];
+    return n;
+  }
+  for (uint32_t i = 0; i < n; i += 2) d[i / 2] = x2c(s[i], s[i + 1]);
+  return n / 2;
+}
+
+__device__ int64_t t_hexencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  if (2ull * n > cap) return -1;
+  const char* hx = "0123456789abcdef";
+  for (uint32_t i = 0; i < n; i++) {
+    d[2 * i] = hx[s[i] >> 4];
+    d[2 * i + 1] = hx[s[i] & 15];
+  }
+  return 2 * n;
+}
+
+__device__ int64_t t_urlencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  const char* hx = "0123456789abcdef";
+  uint32_t o = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (o + 3 > cap) return -1;
+    const uint8_t c = s[i];
+    if (c == ' ') {
+      d[o++] = '+';
+    } else if (c == '*' || isalnum_(c)) {
+      d[o++] = c;
+    } else {
+      d[o++] = '%';
+      d[o++] = hx[c >> 4];
+      d[o++] = hx[c & 15];
+    }
+  }
+  return o;
+}
+
+__device__ inline bool c_isspace(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
+
+// ModSecurity css_decode_inplace
+__device__ int64_t t_cssdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  if (n > cap) return -1;
+  uint32_t o = 0, i = 0;
+  while (i < n) {
+    if (s[i] != '\\') {
+      d[o++] = s[i++];
+      continue;
+    }
+    if (i + 1 >= n) {  // trailing backslash: dropped
+      i++;
+      continue;
+    }
+    i++;
+    uint32_t j = 0;
+    while (j < 6 && i + j < n && ishex(s[i + j])) j++;
+    if (j == 0) {
+      if (s[i] != '\n') d[o++] = s[i];
+      i++;
+      continue;
+    }
+    uint8_t v;
+    if (j == 1) {
+      v = hexv(s[i]);
+    } else {
+      v = x2c(s[i + j - 2], s[i + j - 1]);
+      const bool full = j == 4 || (j == 5 && s[i] == '0') || (j == 6 && s[i] == '0' && s[i + 1] == '0');
+      if (full && v > 0 && v < 0x5F && (s[i + j - 3] | 0x20) == 'f' && (s[i + j - 4] | 0x20) == 'f') v += 0x20;
+    }
+    d[o++] = v;
+    if (i + j < n && c_isspace(s[i + j])) j++;
+    i += j;
+  }
+  return o;
+}
+
+// ModSecurity ansi_c_sequences_decode_inplace
+__device__ int64_t t_escapeseqdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  if (n > cap) return -1;
+  uint32_t o = 0, i = 0;
+  while (i < n) {
+    if (s[i] != '\\' || i + 1 >= n) {
+      d[o++] = s[i++];
+      continue;
+    }
+    const uint8_t e = s[i + 1];
+    int c = -1;
+    switch (e) {
+      case 'a': c = 7; break;
+      case 'b': c = 8; break;
+      case 'f': c = 12; break;
+      case 'n': c = 10; break;
+      case 'r': c = 13; break;
+      case 't': c = 9; break;
+      case 'v': c = 11; break;
+      case '\\': case '?': case '\'': case '"': c = e; break;
+    }
+    if (c >= 0) {
+      d[o++] = (uint8_t)c;
+      i += 2;
+      continue;
+    }
+    if (e == 'x' || e == 'X') {
+      if (i + 3 < n && ishex(s[i + 2]) && ishex(s[i + 3])) {
+        d[o++] = x2c(s[i + 2], s[i + 3]);
+        i += 4;
+        continue;
+      }
+    } else if (isodigit(e)) {
+      uint32_t j = 0, v = 0;
+      while (i + 1 + j < n && j < 3) {
+        v = v * 8 + (s[i + 1 + j] - '0');
+        j++;
+        if (!(i + 1 + j < n && isodigit(s[i + 1 + j]))) break;
+      }
+      d[o++] = (uint8_t)v;
+      i += 1 + j;
+      continue;
+    }
+    d[o++] = e;  // unrecognised escape: the escaped byte
+    i += 2;
+  }
+  return o;
+}
+
+// ModSecurity remove_comments_char
+__device__ int64_t t_removecommentschar(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  if (n > cap) return -1;
+  uint32_t o = 0, i = 0;
+  while (i < n) {
+    const uint8_t c = s[i];
+    const uint8_t c1 = i + 1 < n ? s[i + 1] : 0;
+    if ((c == '/' && c1 == '*') || (c == '*' && c1 == '/')) {
+      i += 2;
+    } else if (c == '<' && c1 == '!' && i + 3 < n && s[i + 2] == '-' && s[i + 3] == '-') {
+      i += 4;
+    } else if (c == '-' && c1 == '-' && i + 2 < n && s[i + 2] == '>') {
+      i += 3;
+    } else if (c == '-' && c1 == '-') {
+      i += 2;
+    } else if (c == '#') {
+      i += 1;
+    } else {
+      d[o++] = c;
+      i++;
+    }
+  }
+  return o;
+}
+
+// Message padding shared by SHA-1 (big-endian length) and MD5 (little-endian):
+// 64-byte block b of the padded message s (n bytes).
+__device__ inline void digest_block(const uint8_t* s, uint32_t n, uint32_t b, bool be, uint32_t* w) {
+  uint8_t blk[64];
+  const uint64_t bits = (uint64_t)n * 8;
+  const uint32_t nb = (n + 9 + 63) / 64;
+  for (uint32_t k = 0; k < 64; k++) {
+    const uint32_t at = b * 64 + k;
+    uint8_t v = at < n ? s[at] : at == n ? 0x80 : 0;
+    if (b == nb - 1 && k >= 56) v = be ? (uint8_t)(bits >> (8 * (63 - k))) : (uint8_t)(bits >> (8 * (k - 56)));
+    blk[k] = v;
+  }
+  for (uint32_t k = 0; k < 16; k++)
+    w[k] = be ? ((uint32_t)blk[4 * k] << 24) | ((uint32_t)blk[4 * k + 1] << 16) | ((uint32_t)blk[4 * k + 2] << 8) | blk[4 * k + 3]
+              : ((uint32_t)blk[4 * k + 3] << 24) | ((uint32_t)blk[4 * k + 2] << 16) | ((uint32_t)blk[4 * k + 1] << 8) | blk[4 * k];
+}
+
+__device__ inline uint32_t rotl(uint32_t x, uint32_t c) { return (x << c) | (x >> (32 - c)); }
+
+__device__ int64_t t_sha1(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  if (cap < 20) return -1;
+  uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+  const uint32_t nb = (n + 9 + 63) / 64;
+  for (uint32_t b = 0; b < nb; b++) {
+    uint32_t w[16];
+    digest_block(s, n, b, true, w);
+    uint32_t a = h[0], bb = h[1], c = h[2], dd = h[3], e = h[4];
+    for (uint32_t t = 0; t < 80; t++) {
+      uint32_t wt;
+      if (t < 16) {
+        wt = w[t];
+      } else {
+        wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+        w[t & 15] = wt;
+      }
+      uint32_t f, k;
+      if (t < 20) { f = (bb & c) | (~bb & dd); k = 0x5A827999u; }
+      else if (t < 40) { f = bb ^ c ^ dd; k = 0x6ED9EBA1u; }
+      else if (t < 60) { f = (bb & c) | (bb & dd) | (c & dd); k = 0x8F1BBCDCu; }
+      else { f = bb ^ c ^ dd; k = 0xCA62C1D6u; }
+      const uint32_t tmp = rotl(a, 5) + f + e + k + wt;
+      e = dd; dd = c; c = rotl(bb, 30); bb = a; a = tmp;
+    }
+    h[0] += a; h[1] += bb; h[2] += c; h[3] += dd; h[4] += e;
+  }
+  for (uint32_t k = 0; k < 5; k++) {
+    d[4 * k] = (uint8_t)(h[k] >> 24); d[4 * k + 1] = (uint8_t)(h[k] >> 16);
+    d[4 * k + 2] = (uint8_t)(h[k] >> 8); d[4 * k + 3] = (uint8_t)h[k];
+  }
+  return 20;
+}
+
+__device__ __constant__ uint32_t kMd5K[64] = {
+    0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+    0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+    0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+    0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+    0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+    0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+    0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+    0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+__device__ __constant__ uint8_t kMd5S[16] = {7, 12, 17, 22, 5, 9, 14, 20, 4, 11, 16, 23, 6, 10, 15, 21};
+
+__device__ int64_t t_md5(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  if (cap < 16) return -1;
+  uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  const uint32_t nb = (n + 9 + 63) / 64;
+  for (uint32_t b = 0; b < nb; b++) {
+    uint32_t w[16];
+    digest_block(s, n, b, false, w);
+    uint32_t a = h[0], bb = h[1], c = h[2], dd = h[3];
+    for (uint32_t i = 0; i < 64; i++) {
+      uint32_t f, g;
+      if (i < 16) { f = (bb & c) | (~bb & dd); g = i; }
+      else if (i < 32) { f = (dd & bb) | (~dd & c); g = (5 * i + 1) & 15; }
+      else if (i < 48) { f = bb ^ c ^ dd; g = (3 * i + 5) & 15; }
+      else { f = c ^ (bb | ~dd); g = (7 * i) & 15; }
+      const uint32_t tmp = dd;
+      dd = c;
+      c = bb;
+      bb = bb + rotl(a + f + kMd5K[i] + w[g], kMd5S[(i >> 4) * 4 + (i & 3)]);
+      a = tmp;
+    }
+    h[0] += a; h[1] += bb; h[2] += c; h[3] += dd;
+  }
+  for (uint32_t k = 0; k < 4; k++) {
+    d[4 * k] = (uint8_t)h[k]; d[4 * k + 1] = (uint8_t)(h[k] >> 8);
+    d[4 * k + 2] = (uint8_t)(h[k] >> 16); d[4 * k + 3] = (uint8_t)(h[k] >> 24);
+  }
+  return 16;
+}
+
+__device__ __noinline__ int64_t t_ext(uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+  switch (code) {
+    case T_BASE64DECODE: return t_b64decode(false, s, n, d, cap);
+    case T_BASE64DECODEEXT: return t_b64decode(true, s, n, d, cap);
+    case T_BASE64ENCODE: return t_b64encode(s, n, d, cap);
+    case T_HEXDECODE: return t_hexdecode(s, n, d, cap);
+    case T_HEXENCODE: return t_hexencode(s, n, d, cap);
+    case T_SHA1: return t_sha1(s, n, d, cap);
+    case T_MD5: return t_md5(s, n, d, cap);
+    case T_URLENCODE: return t_urlencode(s, n, d, cap);
+    case T_CSSDECODE: return t_cssdecode(s, n, d, cap);
+    case T_ESCAPESEQDECODE: return t_escapeseqdecode(s, n, d, cap);
+    case T_REMOVECOMMENTSCHAR: return t_removecommentschar(s, n, d, cap);
+  }
+  return -1;
+}
+
 __device__ __forceinline__ int64_t apply_transform_inl(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n,
                                                       uint8_t* d, uint32_t cap) {
   switch (code) {
@@ -709,7 +1091,7 @@ __device__ __forceinline__ int64_t apply_transform_inl(const DProgram& P, uint8_
     case T_NORMALIZEPATH: return t_normpath(false, s, n, d, cap);
     case T_NORMALIZEPATHWIN: return t_normpath(true, s, n, d, cap);
     case T_JSDECODE: return t_jsdecode(s, n, d, cap);
-    default: return t_simple(code, s, n, d, cap);
+    default: return code >= T_BASE64DECODE ? t_ext(code, s, n, d, cap) : t_simple(code, s, n, d, cap);
   }
 }
 
@@ -772,7 +1154,6 @@ struct Tx {
   uint32_t nmatched;
   uint32_t* mout;
   uint32_t mcap;
-  uint32_t* rhist;           // per-rule match counts (LDS when the ruleset is small)
   bool profon;               // GI_PROF counters (diagnostics)
   uint32_t prof_visits, prof_evals, prof_rules;
   uint64_t prof_eval_cyc, prof_act_cyc;
@@ -1575,7 +1956,7 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
   switch (o.kind) {
     case OP_RX:
     case OP_PM:
-      res = dfa_match(P, o.dfa, s, n, false);
+      res = o.nfa >= 0 ? nfa_match(P, o.nfa, s, n) : dfa_match(P, o.dfa, s, n, false);
       break;
     case OP_UNCONDITIONAL:
       res = true;
@@ -1902,7 +2283,6 @@ __device__ __forceinline__ void eval_top(Tx& t, uint32_t ri) {
     if (t.nmatched < t.mcap) t.mout[t.nmatched] = (uint32_t)R.id;
     else t.flags |= GI_REQ_MATCH_TRUNC;
     t.nmatched++;
-    atomicAdd(&t.rhist[R.top_idx], 1u);
   }
 }
 
@@ -3007,13 +3387,8 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
 // skipping every phase-A rule whose hit bit is clear.
 __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
   __shared__ unsigned long long red[7];
-  // block-aggregated detail tally: score histogram + per-rule match counts
-  __shared__ uint32_t shist[GI_SCORE_BINS + GI_RHIST_LDS];
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool rh_lds = P.n_top <= GI_RHIST_LDS;
-  const uint32_t n_sh = GI_SCORE_BINS + (rh_lds ? P.n_top : 0u);
   if (threadIdx.x < 7) red[threadIdx.x] = 0;
-  for (uint32_t i = threadIdx.x; i < n_sh; i += blockDim.x) shist[i] = 0;
   __syncthreads();
   unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
   if (r < B.n_req) {
@@ -3054,7 +3429,6 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
     t.nmatched = 0;
     t.mout = B.matched + (uint64_t)r * B.mcap;
     t.mcap = B.mcap;
-    t.rhist = rh_lds ? shist + GI_SCORE_BINS : B.tally_ext + GI_SCORE_BINS;
     for (uint32_t s = 0; s < P.n_slots; s++) TXS(t, s).state = 0;
     const uint8_t* D = B.data;
     uint64_t scanned = (uint64_t)rq.method.len + rq.uri.len + rq.proto.len + rq.body.len;
@@ -3141,7 +3515,6 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
       v.tx_export[e] = x;
     }
     B.verdicts[r] = v;
-    atomicAdd(&shist[(uint32_t)min(max(v.tx_export[0], (int64_t)0), (int64_t)(GI_SCORE_BINS - 1))], 1u);
     my[0] = 1;
     my[1] = t.interrupted ? 1 : 0;
     my[2] = t.nmatched ? 1 : 0;
@@ -3157,8 +3530,71 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
   }
   __syncthreads();
   if (threadIdx.x < 7) atomicAdd(&B.tally[threadIdx.x], red[threadIdx.x]);
-  for (uint32_t i = threadIdx.x; i < n_sh; i += blockDim.x)
-    if (shist[i]) atomicAdd(&B.tally_ext[i], shist[i]);
+}
+
+// Detail tally: histogram of the first exported TX value and
+// the match count of every rule id, from the verdicts and matched-id rows k_eval
+// wrote.  Lanes walk their request's matched list in step; the lists share
+// long prefixes (the CRS initialisation SecActions match every request), so
+// equal bins are first aggregated across the wave (one LDS atomic per distinct
+// bin per step instead of 64 on one address).
+__device__ __forceinline__ void wave_hist_add(uint32_t* hist, int32_t b) {
+  uint64_t active = __ballot(b >= 0);
+  while (active) {
+    const int leader = __ffsll((unsigned long long)active) - 1;
+    const int32_t lb = __shfl(b, leader, 64);
+    const uint64_t same = __ballot(b == lb) & active;
+    if (lane_id() == (uint32_t)leader) atomicAdd(&hist[lb], (uint32_t)__popcll(same));
+    active &= ~same;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_tally(DBatch B, const uint32_t* __restrict__ ids, uint32_t n_ids) {
+  extern __shared__ uint32_t sh[];  // [n_ids] sorted ids | [GI_SCORE_BINS + n_ids] counts (LDS mode)
+  const bool lds = n_ids <= GI_RHIST_LDS;
+  const uint32_t* tid = lds ? sh : ids;
+  uint32_t* hist = lds ? sh + n_ids : B.tally_ext;
+  if (lds) {
+    for (uint32_t i = threadIdx.x; i < n_ids; i += blockDim.x) sh[i] = ids[i];
+    for (uint32_t i = threadIdx.x; i < GI_SCORE_BINS + n_ids; i += blockDim.x) hist[i] = 0;
+  }
+  __syncthreads();
+  // whole waves stay in the loop together (the aggregation uses ballots)
+  const uint32_t n_waves_total = (B.n_req + 63) / 64;
+  const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  const uint32_t stride_w = gridDim.x * blockDim.x / 64;
+  for (uint32_t w = wv; w < n_waves_total; w += stride_w) {
+    const uint32_t r = w * 64 + lane_id();
+    uint32_t cnt = 0;
+    int32_t sb = -1;
+    if (r < B.n_req) {
+      const gi_verdict v = B.verdicts[r];
+      cnt = min(v.match_cnt, B.mcap);
+      sb = (int32_t)min(max(v.tx_export[0], (int64_t)0), (int64_t)(GI_SCORE_BINS - 1));
+    }
+    wave_hist_add(hist, sb);
+    const uint32_t steps = wave_max(cnt);
+    const uint32_t* row = B.matched + (uint64_t)r * B.mcap;
+    for (uint32_t j = 0; j < steps; j++) {
+      int32_t b = -1;
+      if (j < cnt) {
+        const uint32_t id = row[j];
+        uint32_t lo = 0, hi = n_ids;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (tid[mid] < id) lo = mid + 1;
+          else hi = mid;
+        }
+        if (lo < n_ids && tid[lo] == id) b = (int32_t)(GI_SCORE_BINS + lo);
+      }
+      wave_hist_add(hist, b);
+    }
+  }
+  if (lds) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < GI_SCORE_BINS + n_ids; i += blockDim.x)
+      if (hist[i]) atomicAdd(&B.tally_ext[i], hist[i]);
+  }
 }
 
 void scan_allow_lds(uint32_t lds_bytes) {
@@ -3198,7 +3634,7 @@ uint32_t scan_resident_blocks(uint32_t lds_bytes) {
   } while (0)
 
 void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
-                     int stop_after, LaunchLog* log) {
+                     int stop_after, LaunchLog* log, const uint32_t* tally_ids, uint32_t n_tally_ids) {
   if (!B.n_req) return;
   int nk = 0;
   if (log) {
@@ -3241,6 +3677,11 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
   {  // small batches (fewer than 4 workgroups of 128 per CU): one wave per workgroup to spread over all CUs
     const uint32_t ev_bs = (B.n_req + 127) / 128 < 1024 ? 64u : 128u;
     GI_LAUNCH("k_eval", k_eval, dim3((B.n_req + ev_bs - 1) / ev_bs), dim3(ev_bs), 0, stream, P, B);
+  }
+  {
+    const uint32_t lds = n_tally_ids <= GI_RHIST_LDS ? 4 * (2 * n_tally_ids + GI_SCORE_BINS) : 0;
+    const uint32_t nb = std::min<uint32_t>((B.n_req + 255) / 256, 2048);
+    GI_LAUNCH("k_tally", k_tally, dim3(nb), dim3(256), lds, stream, B, tally_ids, n_tally_ids);
   }
 }
 

@@ -332,11 +332,13 @@ struct Parser {
     return true;
   }
 
+  // A flag group (?i) persists to the end of the enclosing group, across '|'
+  // (Go regexp/syntax): the branches share one flags variable.
   bool parse_alt(int flags, int* out) {
     std::vector<int> branches;
     for (;;) {
       int b;
-      if (!parse_concat(flags, &b)) return false;
+      if (!parse_concat(&flags, &b)) return false;
       branches.push_back(b);
       if (peek() == '|') {
         i++;
@@ -355,7 +357,7 @@ struct Parser {
     return true;
   }
 
-  bool parse_concat(int flags, int* out) {
+  bool parse_concat(int* flags, int* out) {
     std::vector<int> items;
     last_rep = false;
     while (!eof()) {
@@ -365,7 +367,7 @@ struct Parser {
         if (items.empty()) return fail("missing argument to repetition operator");
         i++;
         int lo = c == '+' ? 1 : 0, hi = c == '?' ? 1 : -1;
-        if (!apply_repeat(&items, lo, hi, flags)) return false;
+        if (!apply_repeat(&items, lo, hi, *flags)) return false;
         continue;
       }
       if (c == '{') {
@@ -376,17 +378,17 @@ struct Parser {
             return fail("invalid repeat count");
           if (items.empty()) return fail("missing argument to repetition operator");
           i = after;
-          if (!apply_repeat(&items, lo, hi, flags)) return false;
+          if (!apply_repeat(&items, lo, hi, *flags)) return false;
           continue;
         }
         i++;
-        items.push_back(lit('{', flags));
+        items.push_back(lit('{', *flags));
         last_rep = false;
         continue;
       }
       last_rep = false;
       int atom = -1;
-      if (!parse_atom(&flags, &atom)) return false;
+      if (!parse_atom(flags, &atom)) return false;
       if (atom >= 0) items.push_back(atom);
     }
     if (items.empty()) {

@@ -96,6 +96,28 @@ bool phrases_to_regex(const std::vector<std::string>& phrases, bool fold_ascii, 
 bool build_phrase_dfa(const std::vector<std::string>& phrases, bool fold_ascii, Dfa* out,
                       std::string* err, uint32_t state_cap = 60000);
 
+// Exact matcher tables for a regex whose DFA exceeds the state cap: the
+// Thompson NFA's class positions as bitsets (bit n_pos = match).
+//   cm[c * words ..]                positions whose class holds rune class c
+//   follow[(p * 16 + combo) * words] positions reachable after position p
+//                                    (row n_pos: from the start) through epsilon
+//                                    moves whose assertions hold for combo =
+//                                    prev * 4 + next, prev / next in {0 none,
+//                                    1 '\n', 2 word char, 3 other}
+struct NfaTables {
+  uint32_t n_classes = 0, n_pos = 0, words = 0;
+  std::vector<uint8_t> amap;        // 128
+  std::vector<uint32_t> nranges;    // (lo, hi, cls) for runes >= 0x80
+  std::vector<uint8_t> cls_combo;   // bit0 '\n', bit1 word char
+  std::vector<uint64_t> cm;
+  std::vector<uint64_t> follow;
+};
+bool build_nfa_tables(const Regex& re, NfaTables* out, std::string* err, uint32_t max_pos = 4096);
+bool nfa_host_match(const NfaTables& t, const uint8_t* s, size_t n);
+
+// Superset relaxation (level 1..3) for phase-A prefilter automata; see dfa.cpp.
+void relax_regex(Regex* re, int level);
+
 // Host-side walk of a built DFA (compiler self-test only; never used by the
 // inspection path).
 bool dfa_host_match(const Dfa& d, const uint8_t* s, size_t n);

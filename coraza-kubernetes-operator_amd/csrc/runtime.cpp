@@ -81,6 +81,8 @@ struct gi_ctx {
   std::vector<DevBuf> pbufs;
   // batch buffers
   DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, tally_ext, hits, joblist, txslots;
+  DevBuf tally_idbuf;                  // distinct rule ids, ascending (k_tally bins)
+  std::vector<uint32_t> tally_ids;
   // phase A
   DevBuf bcounts, boffs, items, lscratch, pool, qblk, ctr, slow, slow_bytes;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0;
@@ -245,7 +247,7 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   hipError_t e = hipSuccess;
   const Program& P = rs->prog;
   if (P.streams.size() > GI_MAX_STREAMS) return fail(c, GI_EINVAL, "ruleset has more phase-A streams than supported");
-  std::vector<DevBuf> nbufs(32);
+  std::vector<DevBuf> nbufs(40);
   DevBuf njoblist;
   DProgram np{};
   ScanLaunch nscan{};
@@ -287,6 +289,7 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   UP(tmpls, P.tmpls, DTmpl)
   UP(tchains, P.tchains, uint8_t)
   UP(dfas, P.dfas, DDfa)
+  UP(nfas, P.nfas, DNfa)
   UP(trans, P.trans, uint16_t)
   UP(u8pool, P.u8pool, uint8_t)
   UP(nranges, P.nranges, uint32_t)
@@ -345,8 +348,17 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   std::vector<uint32_t> all(jl[0]);
   all.insert(all.end(), jl[1].begin(), jl[1].end());
   all.insert(all.end(), jl[2].begin(), jl[2].end());
-  if (upload(&njoblist, all, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+  std::vector<uint32_t> ids;
+  for (const DRule& r : P.rules)
+    if (r.id > 0 && !(r.flags & RF_CHILD)) ids.push_back((uint32_t)r.id);
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  DevBuf nidbuf;
+  if (upload(&njoblist, all, s) != hipSuccess || upload(&nidbuf, ids, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    nidbuf.release();
     return discard(GI_ENOMEM, "scan plan upload failed");
+  }
   for (int b = 0; b < 2; b++) {
     nscan.jobs[b] = (const uint32_t*)njoblist.p + (b ? jl[0].size() : 0);
     nscan.n_jobs[b] = (uint32_t)jl[b].size();
@@ -362,8 +374,11 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   // commit: the context now runs the new program; the old buffers go
   for (auto& b : c->pbufs) b.release();
   c->joblist.release();
+  c->tally_idbuf.release();
   c->pbufs.swap(nbufs);
   c->joblist = njoblist;
+  c->tally_idbuf = nidbuf;
+  c->tally_ids.swap(ids);
   c->prog = np;
   c->scan = nscan;
   c->rs = rs;
@@ -424,7 +439,7 @@ void gi_ctx_free(gi_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& b : c->pbufs) b.release();
   c->prof.release();
-  for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext,
+  for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes})
     b->release();
@@ -544,7 +559,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if ((e = c->matched.ensure(std::max<size_t>((size_t)n * c->mcap * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc matched");
   if ((e = c->tally.ensure(sizeof(gi_tally))) != hipSuccess) return hip_fail(c, e, "alloc tally");
-  if ((e = c->tally_ext.ensure(4ull * (GI_SCORE_BINS + PG.top.size()))) != hipSuccess)
+  if ((e = c->tally_ext.ensure(4ull * (GI_SCORE_BINS + c->tally_ids.size()))) != hipSuccess)
     return hip_fail(c, e, "alloc detail tally");
   if ((e = c->txslots.ensure(std::max<uint64_t>(24ull * PG.n_slots * n, 64))) != hipSuccess)
     return hip_fail(c, e, "alloc tx slots");
@@ -606,7 +621,7 @@ int gi_run_staged(gi_ctx* c) {
   (void)hipSetDevice(c->device);
   hipError_t e = hipMemsetAsync(c->tally.p, 0, sizeof(gi_tally), c->stream);
   if (e == hipSuccess)
-    e = hipMemsetAsync(c->tally_ext.p, 0, 4ull * (GI_SCORE_BINS + c->rs->prog.top.size()), c->stream);
+    e = hipMemsetAsync(c->tally_ext.p, 0, 4ull * (GI_SCORE_BINS + c->tally_ids.size()), c->stream);
   if (e != hipSuccess) return hip_fail(c, e, "memset tally");
   DBatch B;
   B.data = (const uint8_t*)c->data.p;
@@ -665,7 +680,8 @@ int gi_run_staged(gi_ctx* c) {
     e = hipMemsetAsync(c->hits.p, 0, (size_t)c->hit_words * c->n_req * 4, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "memset hits");
   }
-  launch_pipeline(c->prog, B, c->scan, c->stream, c->evs, c->stop_after, &c->log);
+  launch_pipeline(c->prog, B, c->scan, c->stream, c->evs, c->stop_after, &c->log,
+                  (const uint32_t*)c->tally_idbuf.p, (uint32_t)c->tally_ids.size());
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(c, e, "launch pipeline");
   (void)hipEventRecord(c->ev1, c->stream);
@@ -802,10 +818,10 @@ int gi_tally_get(gi_ctx* c, gi_tally* out) {
 int gi_tally_detail_get(gi_ctx* c, uint64_t* score_hist, uint32_t* rule_ids, uint64_t* rule_hits, uint32_t cap,
                         uint32_t* n_rules) {
   if (!c) return GI_EINVAL;
-  if (!c->ran) return fail(c, GI_ESTATE, "no batch has run");
-  const Program& P = c->rs->prog;
-  const uint32_t nt = (uint32_t)P.top.size();
+  const uint32_t nt = (uint32_t)c->tally_ids.size();
   if (n_rules) *n_rules = nt;
+  if (!score_hist && !rule_ids && !rule_hits) return GI_OK;  // size query
+  if (!c->ran) return fail(c, GI_ESTATE, "no batch has run");
   if ((rule_ids || rule_hits) && cap < nt) return fail(c, GI_ETRUNC, "rule tally capacity too small");
   int rc = gi_sync(c);
   if (rc != GI_OK) return rc;
@@ -815,7 +831,7 @@ int gi_tally_detail_get(gi_ctx* c, uint64_t* score_hist, uint32_t* rule_ids, uin
   if (score_hist)
     for (int b = 0; b < GI_SCORE_BINS; b++) score_hist[b] = h[b];
   for (uint32_t k = 0; k < nt; k++) {
-    if (rule_ids) rule_ids[k] = (uint32_t)P.rules[P.top[k]].id;
+    if (rule_ids) rule_ids[k] = c->tally_ids[k];
     if (rule_hits) rule_hits[k] = h[GI_SCORE_BINS + k];
   }
   return GI_OK;
@@ -835,12 +851,36 @@ int gi_inspect_batch(gi_ctx* c, const gi_batch* in, gi_results* out) {
   return gi_fetch_results(c, out);
 }
 
+int gi_selftest_regex_many(const char* pattern, size_t plen, const uint8_t* data, const uint64_t* offs, uint32_t n,
+                           uint8_t* out, uint32_t* n_states) {
+  if (!pattern || (n && (!data || !offs || !out))) return GI_EINVAL;
+  Regex re;
+  std::string err;
+  if (!re_parse(std::string(pattern, plen), &re, &err)) return GI_EPARSE;
+  Dfa d;
+  NfaTables t;
+  const bool dfa = build_regex_dfa(re, &d, &err);
+  if (!dfa && !build_nfa_tables(re, &t, &err)) return GI_EUNSUPPORTED;
+  if (n_states) *n_states = dfa ? d.n_states : 0;
+  for (uint32_t k = 0; k < n; k++) {
+    const uint8_t* s = data + offs[k];
+    const size_t len = offs[k + 1] - offs[k];
+    out[k] = (dfa ? dfa_host_match(d, s, len) : nfa_host_match(t, s, len)) ? 1 : 0;
+  }
+  return GI_OK;
+}
+
 int gi_selftest_regex(const char* pattern, size_t plen, const uint8_t* s, size_t n, uint32_t* n_states) {
   Regex re;
   std::string err;
   if (!re_parse(std::string(pattern, plen), &re, &err)) return GI_EPARSE;
   Dfa d;
-  if (!build_regex_dfa(re, &d, &err)) return GI_EUNSUPPORTED;
+  if (!build_regex_dfa(re, &d, &err)) {  // the compiler's fallback: exact NFA tables
+    NfaTables t;
+    if (!build_nfa_tables(re, &t, &err)) return GI_EUNSUPPORTED;
+    if (n_states) *n_states = 0;
+    return nfa_host_match(t, s, n) ? 1 : 0;
+  }
   if (n_states) *n_states = d.n_states;
   return dfa_host_match(d, s, n) ? 1 : 0;
 }

@@ -64,7 +64,7 @@ EXPORTED_SYMBOLS = (
     "gi_ctx_create", "gi_ctx_free", "gi_last_error", "gi_inspect_batch", "gi_stage_batch",
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
     "gi_ctx_stream", "gi_selftest_regex", "gi_selftest_plan", "gi_selftest_triggers",
-    "gi_ruleset_save", "gi_ruleset_load", "gi_ctx_swap_ruleset", "gi_compiler_rev", "gi_tally_detail_get",
+    "gi_ruleset_save", "gi_ruleset_load", "gi_ctx_swap_ruleset", "gi_compiler_rev", "gi_tally_detail_get", "gi_selftest_regex_many",
 )
 SCORE_BINS = 64  # GI_SCORE_BINS
 
@@ -166,6 +166,8 @@ def load_library(path: str = LIB_PATH):
     lib.gi_ctx_stream.restype = vp
     lib.gi_selftest_regex.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(u32)]
     lib.gi_selftest_plan.argtypes = [vp, ctypes.c_char_p, sz]
+    lib.gi_selftest_regex_many.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.POINTER(u64), u32,
+                                           ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(u32)]
     lib.gi_selftest_triggers.argtypes = [ctypes.POINTER(u32), u32, ctypes.POINTER(u32)]
     _LIB = lib
     return lib
@@ -475,9 +477,15 @@ class Engine:
         self._check(self._lib.gi_tally_get(self._h, ctypes.byref(t)), "gi_tally_get")
         return {k: getattr(t, k) for k, _ in _Tally._fields_}
 
+    def tally_rule_count(self) -> int:
+        """Distinct rule ids of the ruleset (width of the per-rule tally)."""
+        n = ctypes.c_uint32(0)
+        self._check(self._lib.gi_tally_detail_get(self._h, None, None, None, 0, ctypes.byref(n)), "gi_tally_detail_get")
+        return n.value
+
     def tally_detail(self) -> dict:
-        """Score histogram (first export, clamped to [0, 63]) and per top-level
-        rule match counts of the last batch (gi_tally_detail_get)."""
+        """Score histogram (first export, clamped to [0, 63]) and the match
+        count of every distinct rule id of the last batch (gi_tally_detail_get)."""
         n = ctypes.c_uint32(0)
         self._check(self._lib.gi_tally_detail_get(self._h, None, None, None, 0, ctypes.byref(n)), "gi_tally_detail_get")
         hist = (ctypes.c_uint64 * SCORE_BINS)()
@@ -525,3 +533,24 @@ def selftest_regex(pattern: str, data: bytes):
     n = ctypes.c_uint32(0)
     rc = lib.gi_selftest_regex(pb, len(pb), data, len(data), ctypes.byref(n))
     return rc, n.value
+
+
+def selftest_regex_many(pattern: str, strings):
+    """Host walk of the compiled @rx automaton over many strings (one build):
+    ([0/1 per string], DFA states or 0 when the NFA tables answered)."""
+    lib = load_library()
+    pb = pattern.encode()
+    data = b"".join(strings)
+    offs = (ctypes.c_uint64 * (len(strings) + 1))()
+    o = 0
+    for k, x in enumerate(strings):
+        offs[k] = o
+        o += len(x)
+    offs[len(strings)] = o
+    out = (ctypes.c_uint8 * max(len(strings), 1))()
+    n = ctypes.c_uint32(0)
+    rc = lib.gi_selftest_regex_many(pb, len(pb), data, offs, len(strings), out, ctypes.byref(n))
+    if rc != GI_OK:
+        raise SecLangError(rc, "selftest_regex_many failed")
+    return [int(out[k]) for k in range(len(strings))], n.value
+

@@ -164,8 +164,8 @@ typedef struct {
 /* Detail tallies of the last batch (what the multi-GPU tally
  * all-gathers besides gi_tally): a histogram of the first exported TX value
  * (default: blocking_inbound_anomaly_score) clamped to [0, GI_SCORE_BINS-1],
- * and per top-level rule (file order, ids as in MatchedRules) the number of
- * requests whose matched-rule list holds it. */
+ * and per distinct rule id (ascending) the number of times it appears in the
+ * matched-rule lists (MatchedRules) of the batch. */
 #define GI_SCORE_BINS 64
 
 typedef struct {
@@ -244,8 +244,9 @@ int gi_sync(gi_ctx* ctx);
 int gi_fetch_results(gi_ctx* ctx, gi_results* out);
 int gi_tally_get(gi_ctx* ctx, gi_tally* out);
 /* score_hist: GI_SCORE_BINS entries (may be NULL).  rule_ids / rule_hits:
- * cap entries each (may be NULL); *n_rules = the ruleset's top-level rules
- * (GI_ETRUNC when cap is smaller and the arrays are given). */
+ * cap entries each (may be NULL); *n_rules = the ruleset's distinct rule ids
+ * (GI_ETRUNC when cap is smaller and the arrays are given).  With every
+ * array NULL it only reports *n_rules (no batch needed). */
 int gi_tally_detail_get(gi_ctx* ctx, uint64_t* score_hist, uint32_t* rule_ids, uint64_t* rule_hits, uint32_t cap,
                         uint32_t* n_rules);
 int gi_stats_get(gi_ctx* ctx, gi_stats* out);
@@ -256,6 +257,11 @@ void* gi_ctx_stream(gi_ctx* ctx);
  * Compiler self-tests only: run a host-built automaton on the host.  These
  * never take part in gi_inspect_* (which only runs on the GPU). */
 int gi_selftest_regex(const char* pattern, size_t plen, const uint8_t* s, size_t n, uint32_t* n_states);
+/* The same over n strings (data + offs[k] .. offs[k + 1]), one build:
+ * out[k] = 1 on a match.  *n_states = 0 when the DFA exceeds the state cap
+ * and the NFA tables (the compiler's fallback for @rx) answered. */
+int gi_selftest_regex_many(const char* pattern, size_t plen, const uint8_t* data, const uint64_t* offs, uint32_t n,
+                           uint8_t* out, uint32_t* n_states);
 /* Host emulation of the phase-A scan over every job image of a compiled
  * ruleset (bounds + image walk vs the global tables).  0 = consistent. */
 int gi_selftest_plan(const gi_ruleset* rs, char* err, size_t errcap);

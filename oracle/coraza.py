@@ -982,6 +982,207 @@ def t_utf8tounicode(d: bytes) -> bytes:
     return bytes(out)
 
 
+_B64 = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"
+_B64_REV = {c: i for i, c in enumerate(_B64)}
+
+
+def t_base64decode(d: bytes) -> bytes:
+    """[upstream base64decode.go] forgiving decode: CR/LF skipped; stops at
+    '=', ' ', a byte > 127 or any other byte outside the alphabet; a trailing
+    2 / 3 symbol group yields 1 / 2 bytes, a lone symbol nothing."""
+    out = bytearray()
+    x = n = 0
+    for c in d:
+        if c in (0x0D, 0x0A):
+            continue
+        v = _B64_REV.get(c)
+        if v is None:
+            break
+        x = (x << 6) | v
+        n += 1
+        if n == 4:
+            out += bytes([(x >> 16) & 0xFF, (x >> 8) & 0xFF, x & 0xFF])
+            x = n = 0
+    if n == 2:
+        out.append((x << 12 >> 16) & 0xFF)
+    elif n == 3:
+        x <<= 6
+        out += bytes([(x >> 16) & 0xFF, (x >> 8) & 0xFF])
+    return bytes(out)
+
+
+def t_base64decodeext(d: bytes) -> bytes:
+    """ModSecurity decode_base64_ext restated [upstream base64decodeext.go]:
+    bytes outside the alphabet (padding included) are skipped, every other
+    symbol decoded; a partial trailing byte is dropped."""
+    out = bytearray()
+    x = n = 0
+    for c in d:
+        v = _B64_REV.get(c)
+        if v is None:
+            continue
+        x = (x << 6) | v
+        n += 1
+        if n == 4:
+            out += bytes([(x >> 16) & 0xFF, (x >> 8) & 0xFF, x & 0xFF])
+            x = n = 0
+    if n == 2:
+        out.append((x << 12 >> 16) & 0xFF)
+    elif n == 3:
+        x <<= 6
+        out += bytes([(x >> 16) & 0xFF, (x >> 8) & 0xFF])
+    return bytes(out)
+
+
+def t_base64encode(d: bytes) -> bytes:
+    """Go base64.StdEncoding.EncodeToString."""
+    import base64
+    return base64.b64encode(d)
+
+
+def t_hexdecode(d: bytes) -> bytes:
+    """Go hex.DecodeString; on an error (odd length, a non-hex byte) the
+    transformation fails and rule.go executeTransformations keeps the value."""
+    if len(d) % 2 or not all(_ishex(c) for c in d):
+        return d
+    return bytes.fromhex(d.decode())
+
+
+def t_hexencode(d: bytes) -> bytes:
+    return d.hex().encode()
+
+
+def t_sha1(d: bytes) -> bytes:
+    import hashlib
+    return hashlib.sha1(d).digest()
+
+
+def t_md5(d: bytes) -> bytes:
+    import hashlib
+    return hashlib.md5(d).digest()
+
+
+def t_urlencode(d: bytes) -> bytes:
+    """ModSecurity url_encode [upstream urlencode.go]: ' ' -> '+'; '*', digits
+    and letters kept; every other byte %xx (lowercase hex)."""
+    out = bytearray()
+    for c in d:
+        if c == 0x20:
+            out.append(0x2B)
+        elif c == 0x2A or 48 <= c <= 57 or 65 <= c <= 90 or 97 <= c <= 122:
+            out.append(c)
+        else:
+            out += b"%%%02x" % c
+    return bytes(out)
+
+
+def _cisspace(c: int) -> bool:
+    return c == 0x20 or 9 <= c <= 13
+
+
+def t_cssdecode(d: bytes) -> bytes:
+    """ModSecurity css_decode_inplace [upstream cssdecode.go]: a backslash and
+    1-6 hex digits -> one byte (the last two digits; full-width ff01-ff5e +0x20
+    for 4 digits, for 5 / 6 digits only with leading zeros), one whitespace
+    after the escape eaten; backslash-newline removed; any other escaped byte
+    kept; a trailing backslash dropped."""
+    out = bytearray()
+    i, n = 0, len(d)
+    while i < n:
+        if d[i] != 0x5C:
+            out.append(d[i])
+            i += 1
+            continue
+        if i + 1 >= n:
+            i += 1
+            continue
+        i += 1
+        j = 0
+        while j < 6 and i + j < n and _ishex(d[i + j]):
+            j += 1
+        if j == 0:
+            if d[i] == 0x0A:
+                i += 1
+            else:
+                out.append(d[i])
+                i += 1
+            continue
+        if j == 1:
+            out.append(int(d[i:i + 1], 16))
+        else:
+            v = _x2c(d[i + j - 2], d[i + j - 1])
+            full = j == 4 or (j == 5 and d[i] == 0x30) or (j == 6 and d[i] == 0x30 and d[i + 1] == 0x30)
+            if full and 0 < v < 0x5F and d[i + j - 3] in (0x66, 0x46) and d[i + j - 4] in (0x66, 0x46):
+                v += 0x20
+            out.append(v)
+        if i + j < n and _cisspace(d[i + j]):
+            j += 1
+        i += j
+    return bytes(out)
+
+
+_ESC_SIMPLE = {0x61: 7, 0x62: 8, 0x66: 12, 0x6E: 10, 0x72: 13, 0x74: 9, 0x76: 11, 0x5C: 0x5C, 0x3F: 0x3F,
+               0x27: 0x27, 0x22: 0x22}
+
+
+def t_escapeseqdecode(d: bytes) -> bytes:
+    """ModSecurity ansi_c_sequences_decode_inplace [upstream escapeseqdecode.go]:
+    \\a \\b \\f \\n \\r \\t \\v \\\\ \\? \\' \\"; \\xHH (two hex digits);
+    \\ooo (1-3 octal digits, value & 0xFF); an unrecognised escape keeps only
+    the escaped byte; a trailing backslash is kept."""
+    out = bytearray()
+    i, n = 0, len(d)
+    while i < n:
+        if d[i] != 0x5C or i + 1 >= n:
+            out.append(d[i])
+            i += 1
+            continue
+        e = d[i + 1]
+        if e in _ESC_SIMPLE:
+            out.append(_ESC_SIMPLE[e])
+            i += 2
+            continue
+        if e in (0x78, 0x58):
+            if i + 3 < n and _ishex(d[i + 2]) and _ishex(d[i + 3]):
+                out.append(_x2c(d[i + 2], d[i + 3]))
+                i += 4
+                continue
+        elif _isodigit(e):
+            j = 0
+            while i + 1 + j < n and j < 3:
+                j += 1
+                if not (i + 1 + j < n and _isodigit(d[i + 1 + j])):
+                    break
+            out.append(int(d[i + 1:i + 1 + j], 8) & 0xFF)
+            i += 1 + j
+            continue
+        out.append(e)
+        i += 2
+    return bytes(out)
+
+
+def t_removecommentschar(d: bytes) -> bytes:
+    """ModSecurity remove_comments_char [upstream removecommentschar.go]: drops
+    the comment markers /* */ <!-- --> -- and #."""
+    out = bytearray()
+    i, n = 0, len(d)
+    while i < n:
+        if d.startswith(b"/*", i) or d.startswith(b"*/", i):
+            i += 2
+        elif d.startswith(b"<!--", i):
+            i += 4
+        elif d.startswith(b"-->", i):
+            i += 3
+        elif d.startswith(b"--", i):
+            i += 2
+        elif d[i] == 0x23:
+            i += 1
+        else:
+            out.append(d[i])
+            i += 1
+    return bytes(out)
+
+
 TRANSFORM_FNS = {
     "utf8tounicode": t_utf8tounicode,
     "lowercase": t_lowercase,
@@ -1003,6 +1204,17 @@ TRANSFORM_FNS = {
     "normalizepathwin": lambda d: t_normalizepath(d, True),
     "normalisepathwin": lambda d: t_normalizepath(d, True),
     "jsdecode": t_jsdecode,
+    "base64decode": t_base64decode,
+    "base64decodeext": t_base64decodeext,
+    "base64encode": t_base64encode,
+    "hexdecode": t_hexdecode,
+    "hexencode": t_hexencode,
+    "sha1": t_sha1,
+    "md5": t_md5,
+    "urlencode": t_urlencode,
+    "cssdecode": t_cssdecode,
+    "escapeseqdecode": t_escapeseqdecode,
+    "removecommentschar": t_removecommentschar,
 }
 
 

@@ -246,16 +246,14 @@ def test_gpu_tally_detail():
     eng = gpuinspect.Engine(rs, matched_cap=128)
     res = eng.inspect(batch)
     d = eng.tally_detail()
-    assert len(d["rule_ids"]) == rs.info["n_rules"] == len(d["rule_hits"])
+    assert len(d["rule_ids"]) == len(d["rule_hits"]) == eng.tally_rule_count()
+    assert d["rule_ids"] == sorted(set(d["rule_ids"]))
     want = {}
     for i in range(batch.n_req):
-        for rid in set(res.matched_rules(i)):
-            want[rid] = want.get(rid, 0) + res.matched_rules(i).count(rid)
-    got = {}
-    for rid, h in zip(d["rule_ids"], d["rule_hits"]):
-        if rid:
-            got[rid] = got.get(rid, 0) + h
-    assert {k: v for k, v in got.items() if v} == want
+        for rid in res.matched_rules(i):
+            want[rid] = want.get(rid, 0) + 1
+    got = {rid: h for rid, h in zip(d["rule_ids"], d["rule_hits"]) if h}
+    assert got == want
     import numpy as np
     b = np.clip(res.verdicts["tx_export"][:, 0], 0, 63)
     assert d["score_hist"] == [int((b == k).sum()) for k in range(64)]

@@ -157,3 +157,67 @@ def test_multimatch_links_are_interpreter_only():
     coraza.parse_seclang(text)
     rs = gpuinspect.Ruleset(text)
     assert rs.info["n_rules"] == 2 and rs.info["n_hit_slots"] == 1  # only rule 2 is phase-A scanned
+
+
+# Flag groups persist across '|' to the end of the enclosing group (Go
+# regexp/syntax); CRS 941xxx relies on it: "(?i)<(?:script..)\b|\bon[a-z]{3,25}=".
+FLAG_SCOPE = [r"a(?i)b|c", r"(?:(?i)a)|b", r"x|(?i)y|z", r"(?i)<script\b|\bon[a-z]{3,25}[\s\x0b]*=|javascript:",
+              r"(?:a(?i)b|c)d", r"(?s-i:A)|(?i)b"]
+
+
+@pytest.mark.parametrize("pat", FLAG_SCOPE)
+def test_regex_flag_scope_matches_oracle(pat):
+    rnd = random.Random(len(pat))
+    alpha = b"abcdABCDxyzXYZ <scriptSCRIPT onON=:\xc5\xbf\xe2\x84\xaa"
+    g = goregex.compile_go("(?sm)" + pat)
+    strs = [b"C", b"aB", b"B", b"Z", b".oNuvw=", b"a.ONUVW=", b"Cd", b"A", b"a"] + [
+        bytes(rnd.choice(alpha) for _ in range(rnd.randint(0, 16))) for _ in range(400)]
+    got, _ = gpuinspect.selftest_regex_many("(?sm)" + pat, strs)
+    for s, rc in zip(strs, got):
+        assert rc == int(g.match_string(s)), (pat, s)
+
+
+# Patterns whose search DFA exceeds the state cap: the exact matcher is the
+# NFA position tables (host walk == the device's nfa_match), the phase-A
+# automaton a superset relaxation.
+EXPLODING = [r"(?i)<(?:script|iframe|object|svg|style|link)\b|\bon[a-z]{3,25}[\s\x0b]*=|javascript[\s\x0b]*:",
+             r"(?i)on[a-z]{3,25}=", r"[ab]*a[ab]{16}c", r"(?:x|\bq)[a-z]{2,30}\b!(?i)on[a-z]{3,25}"]
+
+
+@pytest.mark.parametrize("pat", EXPLODING)
+def test_nfa_fallback_matches_oracle(pat):
+    rnd = random.Random(len(pat) * 7)
+    alpha = b"abcnoqxONQ=!c \t.\xc5\xbf\xe2\x84\xaa\xff"
+    g = goregex.compile_go("(?sm)" + pat)
+    strs = [b".oNuvw=", b"onabc=", b"\xc5\xbfonabc=", b"a" * 18 + b"c", b"x" + b"a" * 40 + b"!onabc"] + [
+        bytes(rnd.choice(alpha) for _ in range(rnd.randint(0, 40))) for _ in range(800)]
+    got, n_states = gpuinspect.selftest_regex_many("(?sm)" + pat, strs)
+    assert n_states == 0  # took the NFA path
+    for s, rc in zip(strs, got):
+        assert rc == int(g.match_string(s)), (pat, s)
+
+
+def _crs_rx_patterns():
+    import re as _re
+    text = open(os.path.join(ROOT, "rulesets", "crs_pl1.conf")).read()
+    return sorted(set(_re.findall(r'"@rx ((?:[^"\\]|\\.)*)"', text)))
+
+
+def test_crs_rx_patterns_match_oracle():
+    """Every @rx of the CRS-shaped ruleset: host automaton (DFA, or the NFA
+    tables where the DFA exceeds the cap) vs the oracle's Go-regexp
+    restatement, on attack payloads, case variants and random strings."""
+    import traffic
+    pats = _crs_rx_patterns()
+    assert len(pats) > 50
+    rnd = random.Random(5)
+    corpus = list(traffic.ATTACKS) + [a.upper() for a in traffic.ATTACKS] + [
+        b".oNuvw=", b"x OnLoad =", b"JaVaScRiPt:", b"../../etc/passwd", b"\xc5\xbfonabc=", b"\xe2\x84\xaaey"]
+    alpha = b"abcdefghijklmnopqrstuvwxyz ABCXYZ0123456789<>/\\'\";:=()[]{}.,-_|&$%*+!?#@\n\t\xc3\xa9"
+    corpus += [bytes(rnd.choice(alpha) for _ in range(rnd.randint(0, 48))) for _ in range(60)]
+    for pat in pats:
+        p = pat.replace('\\"', '"')
+        g = goregex.compile_go("(?sm)" + p)
+        got, _ = gpuinspect.selftest_regex_many("(?sm)" + p, corpus)
+        for s, rc in zip(corpus, got):
+            assert rc == int(g.match_string(s)), (p, s)
