@@ -28,7 +28,7 @@ const char kMagic[8] = {'G', 'I', 'A', 'R', 'T', 'F', 'C', 'T'};
 struct Scalars {
   uint8_t item_sides[8];
   uint32_t item_singles, n_hit_slots, n_union_dfas, max_img_bytes, max_big_img_bytes, n_slots, n_markers;
-  uint8_t rule_engine, body_access, _pad[6];
+  uint8_t rule_engine, body_access, mv_used, _pad[5];
   uint64_t body_limit, source_digest;
   uint64_t compiler_rev;  // fnv64 of kCompilerRev
 };
@@ -91,6 +91,7 @@ std::vector<uint8_t> serialize_program(const Program& P) {
   s.n_markers = P.n_markers;
   s.rule_engine = P.rule_engine;
   s.body_access = P.body_access;
+  s.mv_used = P.mv_used;
   s.body_limit = P.body_limit;
   s.source_digest = P.source_digest;
   s.compiler_rev = compiler_rev_hash();
@@ -173,6 +174,7 @@ bool deserialize_program(const uint8_t* buf, size_t n, Program* P, std::string* 
         out.n_markers = s.n_markers;
         out.rule_engine = s.rule_engine;
         out.body_access = s.body_access;
+        out.mv_used = s.mv_used;
         out.body_limit = s.body_limit;
         out.source_digest = s.source_digest;
         seen_scalars = true;
@@ -271,6 +273,7 @@ bool validate_program(const Program& P, std::string* err) {
     if (p.kind == TP_TX && (p.slot < 0 || (uint32_t)p.slot >= nslot)) return bad("template TX slot");
     if (p.kind == TP_SINGLE && p.single >= S_COUNT) return bad("template variable");
     if ((p.kind == TP_LIT || p.kind == TP_HEADER) && !in(p.off, p.len, nstr)) return bad("template string");
+    if ((p.kind == TP_MV || p.kind == TP_MVNAME) && !P.mv_used) return bad("template matched-var without state");
   }
   // rule records
   for (uint32_t t : P.top)

@@ -224,14 +224,14 @@ const std::map<std::string, int>& collection_ids() {
       {"TX", V_TX}, {"ARGS_GET_NAMES", V_ARGS_GET_NAMES}, {"ARGS_POST_NAMES", V_ARGS_POST_NAMES},
       {"ARGS_NAMES", V_ARGS_NAMES}, {"REQUEST_HEADERS_NAMES", V_REQUEST_HEADERS_NAMES},
       {"REQUEST_COOKIES_NAMES", V_REQUEST_COOKIES_NAMES}, {"XML", V_XML}, {"FILES", V_FILES},
-      {"FILES_NAMES", V_FILES_NAMES}};
+      {"FILES_NAMES", V_FILES_NAMES}, {"MATCHED_VAR", V_MATCHED_VAR}, {"MATCHED_VAR_NAME", V_MATCHED_VAR_NAME},
+      {"MATCHED_VARS", V_MATCHED_VARS}, {"MATCHED_VARS_NAMES", V_MATCHED_VARS_NAMES}};
   return m;
 }
 // variables the oracle knows but this engine does not evaluate yet
 bool known_unsupported_var(const std::string& n) {
-  static const char* u[] = {"ARGS_COMBINED_SIZE", "FULL_REQUEST_LENGTH", "MATCHED_VAR",
-                            "MATCHED_VAR_NAME", "MATCHED_VARS", "MATCHED_VARS_NAMES",
-                            "REMOTE_ADDR", "REMOTE_PORT", "SERVER_NAME", "URLENCODED_ERROR"};
+  static const char* u[] = {"ARGS_COMBINED_SIZE", "FULL_REQUEST_LENGTH", "REMOTE_ADDR", "REMOTE_PORT",
+                            "SERVER_NAME", "URLENCODED_ERROR"};
   for (auto* s : u)
     if (n == s) return true;
   return false;
@@ -776,6 +776,12 @@ struct Lower {
         p.kind = TP_HEADER;
         p.off = str(key);
         p.len = (uint32_t)key.size();
+      } else if (name == "MATCHED_VAR" && key.empty()) {
+        p.kind = TP_MV;
+        P->mv_used = 1;
+      } else if (name == "MATCHED_VAR_NAME" && key.empty()) {
+        p.kind = TP_MVNAME;
+        P->mv_used = 1;
       } else {
         unsup("unsupported macro %{" + ref + "}");
       }
@@ -888,7 +894,9 @@ struct Lower {
         vr.var = (uint8_t)sid;
       } else {
         vr.var = (uint8_t)collection_ids().at(v.name);
-        vr.ci = (vr.var == V_REQUEST_HEADERS || vr.var == V_REQUEST_HEADERS_NAMES || vr.var == V_TX) ? 1 : 0;
+        if (vr.var >= V_MATCHED_VAR) P->mv_used = 1;
+        vr.ci = (vr.var == V_REQUEST_HEADERS || vr.var == V_REQUEST_HEADERS_NAMES || vr.var == V_TX ||
+                 vr.var == V_MATCHED_VARS || vr.var == V_MATCHED_VARS_NAMES) ? 1 : 0;
         if (v.key_rx) {
           vr.key_mode = 2;
           vr.key_dfa = regex_dfa(v.key);
@@ -1063,6 +1071,7 @@ struct Lower {
       int sid = single_id(v.name);
       if (sid >= 0 && !immutable_single(sid)) residual = true;  // tested by k_eval on a clear bit
       if (sid < 0 && v.name == "TX") return -1;
+      if (v.name.rfind("MATCHED_VAR", 0) == 0) return -1;  // transaction state, not a request variable
       if (v.name == "ARGS" || v.name == "ARGS_POST" || v.name == "ARGS_NAMES" || v.name == "ARGS_POST_NAMES")
         bodydep = true;
     }

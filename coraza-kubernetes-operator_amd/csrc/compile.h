@@ -16,7 +16,7 @@ namespace gi {
 // even when the record layout stays the same.  gi_compile folds it into the
 // source digest and the artifact stores it, so an artifact written by another
 // compiler revision is rejected (and recompiled from the rules text).
-constexpr const char* kCompilerRev = "gi-seclang-compiler/4";
+constexpr const char* kCompilerRev = "gi-seclang-compiler/5";
 
 struct Program {
   std::vector<DRule> rules;
@@ -57,6 +57,7 @@ struct Program {
   std::vector<std::string> export_names;
   uint32_t n_slots = 0, n_markers = 0;
   uint8_t rule_engine = 1, body_access = 0;
+  uint8_t mv_used = 0;  // some target / macro reads the matched-variable state
   uint64_t body_limit = 134217728;
   uint64_t source_digest = 0;  // FNV-1a 64 of the SecLang text and the export list (artifact identity)
 };

@@ -73,6 +73,13 @@ enum VarId : uint8_t {
   V_XML,  // XML body processor output: never populated (XML bodies are flagged unsupported)
   V_FILES,        // multipart output: never populated (multipart bodies are flagged unsupported)
   V_FILES_NAMES,
+  // matched-variable state of the transaction (coraza tx.matchVariable):
+  // MATCHED_VAR / MATCHED_VAR_NAME persist across rules, MATCHED_VARS(_NAMES)
+  // are reset before every top-level rule (RuleGroup.Eval)
+  V_MATCHED_VAR,
+  V_MATCHED_VAR_NAME,
+  V_MATCHED_VARS,
+  V_MATCHED_VARS_NAMES,
 };
 
 // Collection field kinds emitted by the collect stage.
@@ -169,7 +176,7 @@ enum SetvarForm : int64_t {
 enum EngineMode : uint8_t { ENGINE_OFF = 0, ENGINE_ON = 1, ENGINE_DETECTION_ONLY = 2 };
 enum BodyProc : uint8_t { BP_NONE = 0, BP_URLENCODED = 1, BP_JSON = 2, BP_XML = 3, BP_MULTIPART = 4 };
 
-enum TPartKind : uint8_t { TP_LIT = 1, TP_TX, TP_SINGLE, TP_HEADER };
+enum TPartKind : uint8_t { TP_LIT = 1, TP_TX, TP_SINGLE, TP_HEADER, TP_MV, TP_MVNAME };
 
 // ---------------------------------------------------------------- records
 struct DRule {
@@ -480,7 +487,8 @@ struct DProgram {
   uint32_t n_exports;
   uint8_t rule_engine;          // EngineMode
   uint8_t body_access;
-  uint8_t _pad[2];
+  uint8_t mv_used;              // some target / macro reads MATCHED_VAR(S)(_NAME(S)): k_eval records matches
+  uint8_t _pad;
   uint64_t body_limit;
 };
 

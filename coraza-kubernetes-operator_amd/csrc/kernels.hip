@@ -70,6 +70,11 @@ __device__ bool eq_bytes(const uint8_t* a, uint32_t an, const uint8_t* b, uint32
     if (a[i] != b[i]) return false;
   return true;
 }
+__device__ bool eq_ascii_ci_both(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    if (alower(a[i]) != alower(b[i])) return false;
+  return true;
+}
 __device__ bool eq_ascii_ci(const uint8_t* a, uint32_t an, const uint8_t* lowered, uint32_t bn) {
   if (an != bn) return false;
   for (uint32_t i = 0; i < an; i++)
@@ -1119,6 +1124,120 @@ __device__ __forceinline__ uint32_t value_summary_lut(const uint16_t* lut, const
   for (uint32_t i = 0; i < n; i++) m |= lut[s[i]];
   return m;
 }
+// ------------------------------------------------ matched-variable state
+// coraza tx.matchVariable on every operator match: MATCHED_VAR /
+// MATCHED_VAR_NAME = the matched (transformed) value and "VAR[:key]";
+// MATCHED_VARS(_NAMES) += (name -> value), an existing name (compared ASCII
+// case-insensitively, the collection's key rule) keeping its position with
+// the new value.  Only kept when the program reads it (DProgram.mv_used); all
+// strings are copied (the matched value may sit in a transformation buffer).
+// Area layout: [MvState 64 B][MvEnt x cap_e][arena cap_a][MATCHED_VAR cap_v][MATCHED_VAR_NAME cap_n]
+struct MvEnt {
+  const uint8_t* name;
+  const uint8_t* v;
+  uint32_t nn, vn;
+  uint64_t _pad;
+};
+struct MvState {
+  uint32_t n, cap_e;       // MATCHED_VARS entries of the current top-level rule
+  uint32_t nb, cap_a;      // arena bytes used (reset with the entries)
+  uint32_t cap_v, cap_n;
+  uint32_t cur_vn, cur_nn; // MATCHED_VAR / MATCHED_VAR_NAME lengths (persist across rules)
+  uint32_t _pad[8];
+};
+static_assert(sizeof(MvState) == 64 && sizeof(MvEnt) == 32, "MvState layout");
+
+__device__ inline MvEnt* mv_ents(MvState* m) { return (MvEnt*)(m + 1); }
+__device__ inline uint8_t* mv_arena(MvState* m) { return (uint8_t*)(mv_ents(m) + m->cap_e); }
+__device__ inline uint8_t* mv_curval(MvState* m) { return mv_arena(m) + ((m->cap_a + 15) & ~15u); }
+__device__ inline uint8_t* mv_curname(MvState* m) { return mv_curval(m) + ((m->cap_v + 15) & ~15u); }
+
+// The variable's name as a rule writes it (coraza RuleVariable.Name()).
+__device__ const char* var_name(uint32_t var) {
+  switch (var) {
+    case S_REQUEST_METHOD: return "REQUEST_METHOD";
+    case S_REQUEST_PROTOCOL: return "REQUEST_PROTOCOL";
+    case S_REQUEST_URI: return "REQUEST_URI";
+    case S_REQUEST_URI_RAW: return "REQUEST_URI_RAW";
+    case S_REQUEST_LINE: return "REQUEST_LINE";
+    case S_REQUEST_FILENAME: return "REQUEST_FILENAME";
+    case S_REQUEST_BASENAME: return "REQUEST_BASENAME";
+    case S_QUERY_STRING: return "QUERY_STRING";
+    case S_REQUEST_BODY: return "REQUEST_BODY";
+    case S_REQUEST_BODY_LENGTH: return "REQUEST_BODY_LENGTH";
+    case S_REQBODY_ERROR: return "REQBODY_ERROR";
+    case S_REQBODY_ERROR_MSG: return "REQBODY_ERROR_MSG";
+    case S_REQBODY_PROCESSOR: return "REQBODY_PROCESSOR";
+    case S_MULTIPART_STRICT_ERROR: return "MULTIPART_STRICT_ERROR";
+    case V_ARGS_GET: return "ARGS_GET";
+    case V_ARGS_POST: return "ARGS_POST";
+    case V_ARGS: return "ARGS";
+    case V_REQUEST_HEADERS: return "REQUEST_HEADERS";
+    case V_REQUEST_COOKIES: return "REQUEST_COOKIES";
+    case V_TX: return "TX";
+    case V_ARGS_GET_NAMES: return "ARGS_GET_NAMES";
+    case V_ARGS_POST_NAMES: return "ARGS_POST_NAMES";
+    case V_ARGS_NAMES: return "ARGS_NAMES";
+    case V_REQUEST_HEADERS_NAMES: return "REQUEST_HEADERS_NAMES";
+    case V_REQUEST_COOKIES_NAMES: return "REQUEST_COOKIES_NAMES";
+    case V_XML: return "XML";
+    case V_FILES: return "FILES";
+    case V_FILES_NAMES: return "FILES_NAMES";
+    case V_MATCHED_VAR: return "MATCHED_VAR";
+    case V_MATCHED_VAR_NAME: return "MATCHED_VAR_NAME";
+    case V_MATCHED_VARS: return "MATCHED_VARS";
+    case V_MATCHED_VARS_NAMES: return "MATCHED_VARS_NAMES";
+  }
+  return "";
+}
+
+// tx.matchVariable; false when a capacity is exceeded (the request is flagged).
+__device__ __noinline__ bool mv_record(MvState* m, uint32_t var, const uint8_t* k, uint32_t kn, const uint8_t* v,
+                                       uint32_t vn) {
+  const char* vnm = var_name(var);
+  uint32_t vl = 0;
+  while (vnm[vl]) vl++;
+  const uint32_t nn = vl + (kn ? 1 + kn : 0);
+  if (vn > m->cap_v || nn > m->cap_n) return false;
+  // MATCHED_VAR_NAME / MATCHED_VAR
+  uint8_t* cn = mv_curname(m);
+  for (uint32_t i = 0; i < vl; i++) cn[i] = (uint8_t)vnm[i];
+  if (kn) {
+    cn[vl] = ':';
+    for (uint32_t i = 0; i < kn; i++) cn[vl + 1 + i] = k[i];
+  }
+  m->cur_nn = nn;
+  uint8_t* cv = mv_curval(m);
+  for (uint32_t i = 0; i < vn; i++) cv[i] = v[i];
+  m->cur_vn = vn;
+  // MATCHED_VARS SetIndex(name, 0, value)
+  MvEnt* e = mv_ents(m);
+  uint32_t at = m->n;
+  for (uint32_t j = 0; j < m->n; j++)
+    if (e[j].nn == nn && eq_ascii_ci_both(e[j].name, cn, nn)) {
+      at = j;
+      break;
+    }
+  const uint32_t need = vn + (at == m->n ? nn : 0);
+  if (m->nb + need > m->cap_a || (at == m->n && m->n >= m->cap_e)) return false;
+  uint8_t* a = mv_arena(m) + m->nb;
+  for (uint32_t i = 0; i < vn; i++) a[i] = v[i];
+  e[at].v = a;
+  e[at].vn = vn;
+  if (at == m->n) {
+    uint8_t* nm = a + vn;
+    for (uint32_t i = 0; i < nn; i++) nm[i] = cn[i];
+    e[at].name = nm;
+    e[at].nn = nn;
+    m->n++;
+  } else {  // the key as last written (a case-insensitive equal name has the same length)
+    uint8_t* nm = (uint8_t*)e[at].name;
+    for (uint32_t i = 0; i < nn; i++) nm[i] = cn[i];
+  }
+  m->nb += need;
+  return true;
+}
+
 // ------------------------------------------------------------ transaction
 struct Tx {
   const DProgram* P;
@@ -1154,6 +1273,7 @@ struct Tx {
   uint32_t nmatched;
   uint32_t* mout;
   uint32_t mcap;
+  MvState* mv;               // matched-variable state (nullptr unless DProgram.mv_used)
   bool profon;               // GI_PROF counters (diagnostics)
   uint32_t prof_visits, prof_evals, prof_rules;
   uint64_t prof_eval_cyc, prof_act_cyc;
@@ -1790,6 +1910,10 @@ __device__ __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
       s = slot_str(t, TXS(t, p.slot), nb);
     } else if (p.kind == TP_SINGLE) {
       s = t.single[p.single];
+    } else if (p.kind == TP_MV) {
+      s = {mv_curval(t.mv), t.mv->cur_vn};
+    } else if (p.kind == TP_MVNAME) {
+      s = {mv_curname(t.mv), t.mv->cur_nn};
     } else if (p.kind == TP_HEADER) {
       for (uint32_t f = 0; f < t.nf; f++)
         if (t.fields[f].kind == FK_HEADER && eq_ascii_ci(t.fields[f].k, t.fields[f].kn, P.strpool + p.off, p.len)) {
@@ -2088,7 +2212,9 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
 // transformation of the chain that changed the value (an unchanged step adds
 // no candidate); every match counts and runs the actions.  One eval_op /
 // run_actions site serves both forms (the Tx stays in registers).
-__device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn) {
+// var / k / kn name the value for the matched-variable state (MATCHED_VAR_NAME = VAR[:key]).
+__device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn,
+                                               uint32_t var, const uint8_t* key, uint32_t kn) {
   uint32_t nm = 0;
   const uint8_t* cp = v;  // current candidate
   uint32_t cn = vn;
@@ -2108,6 +2234,7 @@ __device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp&
   for (bool fresh = true;; k++) {
     if (fresh) {
       if (eval_op(t, o, cp, cn)) {
+        if (t.mv && !mv_record(t.mv, var, key, kn, cp, cn)) t.flags |= GI_REQ_OVERFLOW;
         run_actions(t, R);
         nm++;
       }
@@ -2170,10 +2297,10 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
     if (vr.var < S_COUNT) {
       if (vr.count) {
         uint8_t one = '1';
-        nmatch += test_value(t, R, o, &one, 1);
+        nmatch += test_value(t, R, o, &one, 1, vr.var, nullptr, 0);
       } else {
         Str s = t.single[vr.var];
-        nmatch += test_value(t, R, o, s.p, s.n);
+        nmatch += test_value(t, R, o, s.p, s.n, vr.var, nullptr, 0);
       }
       continue;
     }
@@ -2211,12 +2338,46 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         }
         uint8_t nb[24];
         Str s = slot_str(t, sl, nb);
-        nmatch += test_value(t, R, o, s.p, s.n);
+        nmatch += test_value(t, R, o, s.p, s.n, V_TX, nm, nn);
       }
       if (vr.count) {
         uint8_t buf[24];
         uint32_t k = go_itoa(cnt, buf);
-        nmatch += test_value(t, R, o, buf, k);
+        nmatch += test_value(t, R, o, buf, k, V_TX, nullptr, 0);
+      }
+      continue;
+    }
+    if (vr.var >= V_MATCHED_VAR) {  // the matched-variable state (t.mv is set: mv_used)
+      MvState* m = t.mv;
+      if (vr.var == V_MATCHED_VAR || vr.var == V_MATCHED_VAR_NAME) {
+        uint8_t one = '1';
+        Str s = vr.count ? Str{&one, 1u}
+                         : vr.var == V_MATCHED_VAR ? Str{mv_curval(m), m->cur_vn} : Str{mv_curname(m), m->cur_nn};
+        nmatch += test_value(t, R, o, s.p, s.n, vr.var, nullptr, 0);
+        continue;
+      }
+      // MATCHED_VARS(_NAMES): the entries as they stood when the link started
+      const uint32_t n0 = m->n;
+      uint32_t cnt = 0;
+      for (uint32_t j = 0; j < n0; j++) {
+        const MvEnt e = mv_ents(m)[j];
+        if (vr.key_mode == 1) {
+          if (!eq_ascii_ci(e.name, e.nn, P.strpool + vr.key_off, vr.key_len)) continue;
+        } else if (vr.key_mode == 2) {
+          if (!dfa_match(P, vr.key_dfa, e.name, e.nn, true)) continue;
+        }
+        if (vr.exc_count && key_excluded(t, vr, e.name, e.nn)) continue;
+        if (vr.count) {
+          cnt++;
+          continue;
+        }
+        if (vr.var == V_MATCHED_VARS_NAMES) nmatch += test_value(t, R, o, e.name, e.nn, vr.var, e.name, e.nn);
+        else nmatch += test_value(t, R, o, e.v, e.vn, vr.var, e.name, e.nn);
+      }
+      if (vr.count) {
+        uint8_t buf[24];
+        uint32_t k = go_itoa(cnt, buf);
+        nmatch += test_value(t, R, o, buf, k, vr.var, nullptr, 0);
       }
       continue;
     }
@@ -2238,14 +2399,14 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         continue;
       }
       if (names)
-        nmatch += test_value(t, R, o, fl.k, fl.kn);
+        nmatch += test_value(t, R, o, fl.k, fl.kn, vr.var, fl.k, fl.kn);
       else
-        nmatch += test_value(t, R, o, fl.v, fl.vn);
+        nmatch += test_value(t, R, o, fl.v, fl.vn, vr.var, fl.k, fl.kn);
     }
     if (vr.count) {
       uint8_t buf[24];
       uint32_t k = go_itoa(cnt, buf);
-      nmatch += test_value(t, R, o, buf, k);
+      nmatch += test_value(t, R, o, buf, k, vr.var, nullptr, 0);
     }
   }
   return nmatch;
@@ -2313,6 +2474,10 @@ __device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
       continue;
     }
     if (R.flags & RF_MARKER) continue;
+    if (t.mv) {  // RuleGroup.Eval resets MATCHED_VARS(_NAMES) before each rule
+      t.mv->n = 0;
+      t.mv->nb = 0;
+    }
     if (R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.n_req + t.req] >> (R.hit_slot & 31)) & 1u))
       continue;  // phase A proved the first link matches nothing
@@ -2342,6 +2507,7 @@ struct Region {
   Slot* slots;
   uint8_t *bytes, *t0, *t1, *mt, *txa;
   int64_t (*rm)[2];
+  MvState* mv;
   uint32_t cap_f, cap_b, cap_t, cap_mt;
 };
 
@@ -2366,6 +2532,8 @@ __device__ inline Region region_of(const DProgram& P, const DBatch& B, uint32_t 
   g.mt = base + off;
   off += (L.cap_mt + 15) & ~15u;
   g.txa = base + off;
+  off += (L.cap_mt + 15) & ~15u;
+  g.mv = P.mv_used ? (MvState*)(base + off) : nullptr;
   g.cap_f = L.cap_f;
   g.cap_b = L.cap_b;
   g.cap_t = L.cap_t;
@@ -2389,6 +2557,7 @@ __device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
   t.removed = g.rm;
   t.cap_tx = g.cap_mt;
   t.single = g.hdr->single;
+  t.mv = g.mv;
 }
 
 __device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
@@ -3430,6 +3599,14 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
     t.mout = B.matched + (uint64_t)r * B.mcap;
     t.mcap = B.mcap;
     for (uint32_t s = 0; s < P.n_slots; s++) TXS(t, s).state = 0;
+    if (t.mv) {
+      t.mv->n = t.mv->nb = 0;
+      t.mv->cap_e = g.cap_f + 16;
+      t.mv->cap_a = g.cap_b + g.cap_mt;
+      t.mv->cap_v = g.cap_t;
+      t.mv->cap_n = g.cap_mt;
+      t.mv->cur_vn = t.mv->cur_nn = 0;
+    }
     const uint8_t* D = B.data;
     uint64_t scanned = (uint64_t)rq.method.len + rq.uri.len + rq.proto.len + rq.body.len;
     for (uint32_t h = 0; h < rq.hdr_count; h++) {

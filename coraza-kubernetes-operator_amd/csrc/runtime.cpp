@@ -325,6 +325,7 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   for (int i = 0; i < 8; i++) np.exports[i] = i < (int)P.exports.size() ? P.exports[i] : -1;
   np.rule_engine = P.rule_engine;
   np.body_access = P.body_access;
+  np.mv_used = P.mv_used;
   np.body_limit = P.body_limit;
   np.n_jobs = (uint32_t)P.jobs.size();
   np.max_img_bytes = P.max_img_bytes;
@@ -543,6 +544,10 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     L.cap_mt = (uint32_t)cap_mt;
     uint64_t sz = 256 + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + 128 + (cap_b + 15) / 16 * 16 +
                   2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
+    // matched-variable state (kernels.hip MvState): header, entries, value
+    // arena, MATCHED_VAR copy, name buffer
+    if (PG.mv_used)
+      sz += 64 + (cap_f + 16) * 32 + (cap_b + cap_mt + 15) / 16 * 16 + (cap_t + 15) / 16 * 16 + (cap_mt + 15) / 16 * 16;
     off += (sz + 63) / 64 * 64;
   }
   hipError_t e = hipSuccess;

@@ -426,7 +426,8 @@ TRANSFORMS_SUPPORTED = {
     "removenulls", "replacenulls", "removewhitespace", "compresswhitespace",
     "replacecomments", "cmdline", "length", "trim", "trimleft", "trimright",
     "normalizepath", "normalisepath", "normalizepathwin", "normalisepathwin",
-    "jsdecode", "utf8tounicode",
+    "jsdecode", "utf8tounicode", "base64decode", "base64decodeext", "base64encode", "hexdecode",
+    "hexencode", "sha1", "md5", "urlencode", "cssdecode", "escapeseqdecode", "removecommentschar",
 }
 
 
@@ -1904,6 +1905,21 @@ class Transaction:
             value = TRANSFORM_FNS[t](value)
         return value
 
+    def match_variable(self, var: str, key: bytes, value: bytes):
+        """[upstream transaction.go matchVariable]: MATCHED_VAR(_NAME) = the
+        value and "VAR[:key]"; MATCHED_VARS(_NAMES) SetIndex(name, 0, value) --
+        a name already there (case-insensitive keys) keeps its position."""
+        name = var.encode() + (b":" + key if key else b"")
+        self.single["MATCHED_VAR"] = value
+        self.single["MATCHED_VAR_NAME"] = name
+        mv = self.maps["MATCHED_VARS"]
+        for j, (k, _) in enumerate(mv):
+            if k.lower() == name.lower():
+                mv[j] = (name, value)
+                break
+        else:
+            mv.append((name, value))
+
     def do_evaluate(self, rule: Rule) -> int:
         """Rule.doEvaluate -> number of matched values (0 = no match)."""
         nmatch = 0
@@ -1928,8 +1944,7 @@ class Transaction:
                     for tv in cands:
                         if self.eval_op(rule, tv):
                             nmatch += 1
-                            self.single["MATCHED_VAR"] = tv
-                            self.single["MATCHED_VAR_NAME"] = (rv.name + (":" if k else "")).encode() + k
+                            self.match_variable(rv.name, k, tv)
                             self.run_nondisruptive(rule)
         if nmatch == 0:
             return 0
@@ -1971,8 +1986,9 @@ class Transaction:
                 continue
             if r.secmark:
                 continue
-            self.single["MATCHED_VAR"] = b""
-            self.single["MATCHED_VAR_NAME"] = b""
+            # rulegroup.go: MATCHED_VARS(_NAMES) reset before each rule;
+            # MATCHED_VAR(_NAME) keep the last match of the transaction
+            self.maps["MATCHED_VARS"] = []
             self.do_evaluate(r)
 
     def process_request_body(self):

@@ -258,3 +258,41 @@ def test_gpu_tally_detail():
     b = np.clip(res.verdicts["tx_export"][:, 0], 0, 63)
     assert d["score_hist"] == [int((b == k).sum()) for k in range(64)]
     assert sum(want.values()) == int(eng.tally()["matched_total"])
+
+
+MATCHED = """SecRuleEngine On
+SecRule ARGS "@rx (?i)select" "id:1,phase:2,pass,chain,t:none,t:urlDecodeUni"
+    SecRule MATCHED_VARS "@rx (?i)from" "setvar:tx.anomaly_score=+5"
+SecRule ARGS_NAMES "@rx ^q" "id:2,phase:2,pass,chain"
+    SecRule MATCHED_VAR "@contains x" "chain"
+    SecRule MATCHED_VAR_NAME "@streq ARGS_NAMES:qx" "setvar:tx.anomaly_score=+100"
+SecRule REQUEST_HEADERS:User-Agent|ARGS "@rx bot" "id:3,phase:2,pass,t:lowercase,setvar:'tx.ua=%{MATCHED_VAR}',setvar:'tx.uan=%{MATCHED_VAR_NAME}'"
+SecRule TX:UA "@rx crawler" "id:4,phase:2,pass,setvar:tx.anomaly_score=+10"
+SecRule MATCHED_VARS_NAMES "@rx ua" "id:5,phase:2,pass,setvar:tx.anomaly_score=+1000"
+SecRule MATCHED_VAR_NAME "@rx ^TX:ua$" "id:6,phase:2,pass,setvar:tx.anomaly_score=+20000"
+SecRule &MATCHED_VARS "@eq 0" "id:7,phase:2,pass,setvar:tx.anomaly_score=+300000"
+SecRule ARGS "@rx a" "id:8,phase:2,pass,chain"
+    SecRule &MATCHED_VARS "@gt 1" "setvar:tx.anomaly_score=+4000000"
+SecRule TX:UAN "@streq REQUEST_HEADERS:User-Agent" "id:10,phase:2,pass,setvar:tx.anomaly_score=+50000000"
+SecRule TX:ANOMALY_SCORE "@ge 50000000" "id:9,phase:2,deny,status:403"
+"""
+
+
+def test_gpu_parity_matched_vars():
+    """MATCHED_VAR / MATCHED_VAR_NAME / MATCHED_VARS / MATCHED_VARS_NAMES as
+    targets (chains, counts) and macros (coraza transaction.go matchVariable;
+    MATCHED_VARS reset before every rule): GPU vs oracle, the score pins the
+    rule-by-rule outcome."""
+    txs = []
+    for q, ua in ((b"q=1+SELECT+x+FROM+t", b"Mozilla"), (b"qx=axb&b=select+1", b"GoodBot Crawler"),
+                  (b"a=aa&b=ab", b"curl"), (b"qy=1&z=xyz", b"bot"), (b"x=Bot&q=select%20from", b"Mozilla")):
+        t = gpuinspect.Transaction(method=b"GET", uri=b"/?" + q)
+        t.add_request_header("Host", "x")
+        t.add_request_header("User-Agent", ua)
+        txs.append(t)
+    res = _parity(MATCHED, gpuinspect.pack(txs))
+    ai = list(gpuinspect.DEFAULT_EXPORTS).index("anomaly_score")
+    scores = [int(v["tx_export"][ai]) for v in res.verdicts]
+    assert scores[0] % 10 == 5 and scores[1] // 50000000 == 1  # MATCHED_VARS chain; User-Agent name macro
+    batch = traffic.TrafficGen(traffic.SEED + 13).batch(600, attack_rate=0.3)
+    _parity(MATCHED, batch)

@@ -79,6 +79,7 @@ def test_compile_new_transforms():
     text, expect = _rules()
     assert len(expect) > 100
     gpuinspect.Ruleset(text)  # every name compiles
+    coraza.parse_seclang(text)  # and the oracle accepts them
 
 
 @pytest.mark.gpu
