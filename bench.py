@@ -59,7 +59,7 @@ CONFIGS = {
 
 def _oracle_worker(args):
     text, blob, idx, exports = args
-    from oracle import coraza
+    from oracle import compare, coraza
     cfg = coraza.parse_seclang(text)
     data, reqs, headers = blob
     b = gpuinspect.PackedBatch(data, reqs, headers)
@@ -67,7 +67,7 @@ def _oracle_worker(args):
     t0 = time.perf_counter()
     for i in idx:
         t = b.request(i)
-        out[i] = coraza.inspect(cfg, coraza.Request(t.method, t.uri, t.proto, list(t.headers), t.body), exports)
+        out[i] = coraza.inspect(cfg, compare.oracle_request(t), exports)
     return time.perf_counter() - t0, out
 
 

@@ -214,7 +214,7 @@ const std::vector<std::string>& single_names() {
       "REQUEST_METHOD", "REQUEST_PROTOCOL", "REQUEST_URI", "REQUEST_URI_RAW", "REQUEST_LINE",
       "REQUEST_FILENAME", "REQUEST_BASENAME", "QUERY_STRING", "REQUEST_BODY",
       "REQUEST_BODY_LENGTH", "REQBODY_ERROR", "REQBODY_ERROR_MSG", "REQBODY_PROCESSOR",
-      "MULTIPART_STRICT_ERROR"};
+      "MULTIPART_STRICT_ERROR", "REMOTE_ADDR", "REMOTE_PORT"};
   return v;
 }
 const std::map<std::string, int>& collection_ids() {
@@ -230,8 +230,7 @@ const std::map<std::string, int>& collection_ids() {
 }
 // variables the oracle knows but this engine does not evaluate yet
 bool known_unsupported_var(const std::string& n) {
-  static const char* u[] = {"ARGS_COMBINED_SIZE", "FULL_REQUEST_LENGTH", "REMOTE_ADDR", "REMOTE_PORT",
-                            "SERVER_NAME", "URLENCODED_ERROR"};
+  static const char* u[] = {"ARGS_COMBINED_SIZE", "FULL_REQUEST_LENGTH", "SERVER_NAME", "URLENCODED_ERROR"};
   for (auto* s : u)
     if (n == s) return true;
   return false;
@@ -323,7 +322,7 @@ thread_local const std::map<std::string, std::string>* g_data_files = nullptr;
 // trailing '\r' dropped), strings.TrimSpace, empty lines and '#' comments
 // skipped, strings.ToLower; then the same ASCII case-insensitive
 // aho-corasick matcher as @pm.
-std::vector<std::string> pm_file_phrases(const std::string& data) {
+std::vector<std::string> pm_file_phrases(const std::string& data, bool lowered = true) {
   std::vector<std::string> out;
   size_t pos = 0;
   while (pos < data.size()) {
@@ -334,7 +333,142 @@ std::vector<std::string> pm_file_phrases(const std::string& data) {
     if (!l.empty() && l.back() == '\r') l.pop_back();
     l = trim(l);
     if (l.empty() || l[0] == '#') continue;
-    out.push_back(lower(l));
+    out.push_back(lowered ? lower(l) : l);
+  }
+  return out;
+}
+
+// Go net.ParseIP (no zone; IPv4 fields without leading zeros): 4 or 16 bytes
+// in `out` (n = 4 for IPv4, 16 for IPv6).  [Go net/netip parse rules]
+bool go_parse_ipv4(const std::string& s, uint8_t out[4]) {
+  size_t i = 0;
+  for (int f = 0; f < 4; f++) {
+    if (f) {
+      if (i >= s.size() || s[i] != '.') return false;
+      i++;
+    }
+    size_t j = i;
+    int v = 0;
+    while (j < s.size() && j - i < 3 && s[j] >= '0' && s[j] <= '9') v = v * 10 + (s[j++] - '0');
+    if (j == i || v > 255 || (j - i > 1 && s[i] == '0')) return false;
+    out[f] = (uint8_t)v;
+    i = j;
+  }
+  return i == s.size();
+}
+bool go_parse_ip(const std::string& s, uint8_t out[16], int* n) {
+  if (s.find(':') == std::string::npos) {
+    *n = 4;
+    return go_parse_ipv4(s, out);
+  }
+  if (s.find('%') != std::string::npos) return false;
+  *n = 16;
+  uint16_t g[8] = {0};
+  int ng = 0, gap = -1;
+  size_t i = 0;
+  if (s.compare(0, 2, "::") == 0) {
+    gap = 0;
+    i = 2;
+    if (i == s.size()) {
+      memset(out, 0, 16);
+      return true;
+    }
+  }
+  while (i < s.size()) {
+    if (ng == 8) return false;
+    size_t j = i;
+    uint32_t v = 0;
+    while (j < s.size() && j - i < 4 && isxdigit((unsigned char)s[j])) {
+      const char c = (char)tolower((unsigned char)s[j]);
+      v = v * 16 + (c <= '9' ? c - '0' : c - 'a' + 10);
+      j++;
+    }
+    if (j < s.size() && s[j] == '.') {  // embedded IPv4 in the last 32 bits
+      uint8_t v4[4];
+      if (ng > 6 || !go_parse_ipv4(s.substr(i), v4)) return false;
+      g[ng++] = (uint16_t)(v4[0] << 8 | v4[1]);
+      g[ng++] = (uint16_t)(v4[2] << 8 | v4[3]);
+      i = s.size();
+      break;
+    }
+    if (j == i) return false;
+    g[ng++] = (uint16_t)v;
+    i = j;
+    if (i == s.size()) break;
+    if (s[i] != ':') return false;
+    i++;
+    if (i < s.size() && s[i] == ':') {
+      if (gap >= 0) return false;
+      gap = ng;
+      i++;
+      if (i == s.size()) break;
+    } else if (i == s.size()) {
+      return false;
+    }
+  }
+  if (gap < 0 && ng != 8) return false;
+  if (gap >= 0 && ng > 7) return false;
+  uint16_t full[8] = {0};
+  if (gap < 0) {
+    memcpy(full, g, sizeof(full));
+  } else {
+    for (int k = 0; k < gap; k++) full[k] = g[k];
+    const int tail = ng - gap;
+    for (int k = 0; k < tail; k++) full[8 - tail + k] = g[gap + k];
+  }
+  for (int k = 0; k < 8; k++) {
+    out[2 * k] = (uint8_t)(full[k] >> 8);
+    out[2 * k + 1] = (uint8_t)full[k];
+  }
+  return true;
+}
+
+// coraza ipmatch.go: comma-separated networks; a bare address is /32 or /128;
+// net.ParseCIDR (the address is masked to the prefix); entries that do not
+// parse are skipped.  Records: GI_IPNET_BYTES each.
+std::string ipmatch_records(const std::string& arg, size_t* count) {
+  std::string out;
+  *count = 0;
+  size_t pos = 0;
+  while (pos <= arg.size()) {
+    size_t c = arg.find(',', pos);
+    if (c == std::string::npos) c = arg.size();
+    std::string e = trim(arg.substr(pos, c - pos));
+    pos = c + 1;
+    if (e.empty()) continue;
+    std::string addr = e;
+    int bits = -1;
+    size_t sl = e.find('/');
+    if (sl != std::string::npos) {
+      addr = e.substr(0, sl);
+      const std::string b = e.substr(sl + 1);
+      // net.ParseCIDR reads the prefix with dtoi (decimal digits, leading zeros allowed)
+      if (b.empty() || b.size() > 8 || b.find_first_not_of("0123456789") != std::string::npos) continue;
+      bits = atoi(b.c_str());
+    }
+    uint8_t ip[16];
+    int n = 0;
+    if (!go_parse_ip(addr, ip, &n)) continue;
+    if (bits < 0) bits = n == 4 ? 32 : 128;
+    if (bits > 8 * n) continue;
+    for (int k = 0; k < n; k++) {
+      const int keep = std::min(8, std::max(0, bits - 8 * k));
+      ip[k] &= (uint8_t)(keep == 8 ? 0xFF : (0xFF00 >> keep) & 0xFF);
+    }
+    // IPNet.Contains works on To4() of the network number: a (masked)
+    // IPv4-mapped IPv6 network is an IPv4 network with the mask's low 32 bits
+    if (n == 16 && ip[10] == 0xFF && ip[11] == 0xFF && !ip[0] && !ip[1] && !ip[2] && !ip[3] && !ip[4] && !ip[5] &&
+        !ip[6] && !ip[7] && !ip[8] && !ip[9]) {
+      memmove(ip, ip + 12, 4);
+      n = 4;
+      bits = std::max(0, bits - 96);
+    }
+    std::string rec(GI_IPNET_BYTES, '\0');
+    rec[0] = (char)n;
+    rec[1] = (char)bits;
+    for (int k = 0; k < n; k++) rec[2 + k] = (char)ip[k];
+    out += rec;
+    (*count)++;
   }
   return out;
 }
@@ -366,7 +500,8 @@ void parse_operator(std::string opstr, IrRule* rule) {
   static const char* known[] = {"rx", "pm", "contains", "containsword", "streq", "beginswith",
                                 "endswith", "within", "eq", "ge", "gt", "le", "lt",
                                 "unconditionalmatch", "nomatch", "validatebyterange",
-                                "validateurlencoding", "validateutf8encoding", "pmfromfile"};
+                                "validateurlencoding", "validateutf8encoding", "pmfromfile", "ipmatch",
+                                "ipmatchfromfile", "ipmatchf"};
   bool ok = false;
   for (auto* k : known)
     if (rule->op_name == k) ok = true;
@@ -374,6 +509,14 @@ void parse_operator(std::string opstr, IrRule* rule) {
   if (rule->op_name == "pmfromfile") {
     if (!g_data_files || !g_data_files->count(data)) perr("open " + data + ": no such file or directory");
     rule->phrases = pm_file_phrases(g_data_files->at(data));
+  }
+  if (rule->op_name == "ipmatchfromfile" || rule->op_name == "ipmatchf") {
+    // ipmatchfromfile.go: one network per line (comments and blank lines skipped)
+    if (!g_data_files || !g_data_files->count(data)) perr("open " + data + ": no such file or directory");
+    std::string list;
+    for (const auto& p : pm_file_phrases(g_data_files->at(data), false)) list.append(p).push_back(',');
+    rule->op_name = "ipmatch";
+    rule->op_arg = list;
   }
   if (rule->op_name == "rx") {
     Regex re;
@@ -811,7 +954,14 @@ struct Lower {
     o.tmpl = -1;
     const std::string& n = r.op_name;
     const std::string& a = r.op_arg;
-    if (n == "rx") {
+    if (n == "ipmatch") {
+      o.kind = OP_IPMATCH;
+      size_t cnt = 0;
+      const std::string recs = ipmatch_records(a, &cnt);
+      o.arg_is_lit = 1;
+      o.lit_off = str(recs);
+      o.lit_len = (uint32_t)recs.size();
+    } else if (n == "rx") {
       o.kind = OP_RX;
       o.dfa = regex_dfa("(?sm)" + a, &o.nfa);
     } else if (n == "pm") {
@@ -861,6 +1011,7 @@ struct Lower {
     } else {
       static const std::map<std::string, uint8_t> m = {
           {"contains", OP_CONTAINS}, {"containsword", OP_CONTAINSWORD}, {"streq", OP_STREQ},
+          {"ipmatch", OP_IPMATCH},
           {"beginswith", OP_BEGINSWITH}, {"endswith", OP_ENDSWITH}, {"within", OP_WITHIN},
           {"eq", OP_EQ}, {"ge", OP_GE}, {"gt", OP_GT}, {"le", OP_LE}, {"lt", OP_LT}};
       o.kind = m.at(n);
@@ -1048,7 +1199,7 @@ struct Lower {
   static bool immutable_single(int sid) {
     return sid == S_REQUEST_METHOD || sid == S_REQUEST_PROTOCOL || sid == S_REQUEST_URI ||
            sid == S_REQUEST_URI_RAW || sid == S_REQUEST_LINE || sid == S_REQUEST_FILENAME ||
-           sid == S_REQUEST_BASENAME || sid == S_QUERY_STRING;
+           sid == S_REQUEST_BASENAME || sid == S_QUERY_STRING || sid == S_REMOTE_ADDR || sid == S_REMOTE_PORT;
   }
 
   // Assigns a hit slot and registers the link's patterns, or returns -1 when

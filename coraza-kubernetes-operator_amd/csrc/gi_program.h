@@ -54,8 +54,11 @@ enum SingleId : uint8_t {
   S_REQBODY_ERROR_MSG,
   S_REQBODY_PROCESSOR,
   S_MULTIPART_STRICT_ERROR,
+  S_REMOTE_ADDR,   // ProcessConnection
+  S_REMOTE_PORT,
   S_COUNT
 };
+#define GI_REQHDR_BYTES 320  // per-request header slot (ReqHdr, kernels.hip) at the start of its scratch region
 
 // Variable ids used by rule targets.  [0, S_COUNT) are singles.
 enum VarId : uint8_t {
@@ -105,7 +108,11 @@ enum OpKind : uint8_t {
   OP_VALIDATE_BYTE_RANGE,
   OP_VALIDATE_URL_ENCODING,
   OP_VALIDATE_UTF8,
+  OP_IPMATCH,  // @ipMatch / @ipMatchFromFile: DOp.lit_off/lit_len = GI_IPNET_BYTES records in strpool
 };
+// @ipMatch network record (strpool, byte-addressed): [0] 4 = IPv4, 16 = IPv6;
+// [1] prefix bits; [2..18) network address (IPv4 in bytes 2..6)
+#define GI_IPNET_BYTES 18
 
 // --------------------------------------------------------- transformations
 enum TCode : uint8_t {
@@ -307,6 +314,15 @@ __host__ __device__ inline uint32_t transform_triggers(uint8_t code) {
     case T_UTF8TOUNICODE: return BS_HIGH;
     default: return BS_ALL;  // t:length and anything new: always run
   }
+}
+
+// Transformation `code` leaves a value with byte summary `summ` unchanged: its
+// trigger set misses the summary.  BS_ALL marks transformations that must
+// always run (t:length, encoders, digests): never an identity, even on a value
+// whose summary is empty.
+__host__ __device__ inline bool transform_identity(uint32_t summ, uint8_t code) {
+  const uint32_t tr = transform_triggers(code);
+  return tr != BS_ALL && !(summ & tr);
 }
 
 // Image of an LDS job (byte offsets inside the job's image):

@@ -1169,6 +1169,8 @@ __device__ const char* var_name(uint32_t var) {
     case S_REQBODY_ERROR_MSG: return "REQBODY_ERROR_MSG";
     case S_REQBODY_PROCESSOR: return "REQBODY_PROCESSOR";
     case S_MULTIPART_STRICT_ERROR: return "MULTIPART_STRICT_ERROR";
+    case S_REMOTE_ADDR: return "REMOTE_ADDR";
+    case S_REMOTE_PORT: return "REMOTE_PORT";
     case V_ARGS_GET: return "ARGS_GET";
     case V_ARGS_POST: return "ARGS_POST";
     case V_ARGS: return "ARGS";
@@ -2060,6 +2062,111 @@ __device__ __forceinline__ void run_actions(Tx& t, const DRule& R) {
 }
 
 // ------------------------------------------------------------- operators
+// Go net.ParseIP (compile.cpp go_parse_ip) + IP.To4: *n = 4 (IPv4, or an
+// IPv4-mapped IPv6 address) or 16.
+__device__ bool dev_parse_ipv4(const uint8_t* s, uint32_t len, uint8_t* out) {
+  uint32_t i = 0;
+  for (int f = 0; f < 4; f++) {
+    if (f) {
+      if (i >= len || s[i] != '.') return false;
+      i++;
+    }
+    uint32_t j = i, v = 0;
+    while (j < len && j - i < 3 && s[j] >= '0' && s[j] <= '9') v = v * 10 + (s[j++] - '0');
+    if (j == i || v > 255 || (j - i > 1 && s[i] == '0')) return false;
+    out[f] = (uint8_t)v;
+    i = j;
+  }
+  return i == len;
+}
+__device__ bool dev_parse_ip(const uint8_t* s, uint32_t len, uint8_t* out, uint32_t* n) {
+  bool colon = false;
+  for (uint32_t i = 0; i < len; i++) {
+    if (s[i] == ':') colon = true;
+    if (s[i] == '%') return false;
+  }
+  if (!colon) {
+    *n = 4;
+    return dev_parse_ipv4(s, len, out);
+  }
+  uint16_t g[8];
+  int ng = 0, gap = -1;
+  uint32_t i = 0;
+  if (len >= 2 && s[0] == ':' && s[1] == ':') {
+    gap = 0;
+    i = 2;
+  }
+  while (i < len) {
+    if (ng == 8) return false;
+    uint32_t j = i, v = 0;
+    while (j < len && j - i < 4 && ishex(s[j])) v = v * 16 + hexv(s[j++]);
+    if (j < len && s[j] == '.') {
+      uint8_t v4[4];
+      if (ng > 6 || !dev_parse_ipv4(s + i, len - i, v4)) return false;
+      g[ng++] = (uint16_t)(v4[0] << 8 | v4[1]);
+      g[ng++] = (uint16_t)(v4[2] << 8 | v4[3]);
+      i = len;
+      break;
+    }
+    if (j == i) return false;
+    g[ng++] = (uint16_t)v;
+    i = j;
+    if (i == len) break;
+    if (s[i] != ':') return false;
+    i++;
+    if (i < len && s[i] == ':') {
+      if (gap >= 0) return false;
+      gap = ng;
+      i++;
+      if (i == len) break;
+    } else if (i == len) {
+      return false;
+    }
+  }
+  if ((gap < 0 && ng != 8) || (gap >= 0 && ng > 7)) return false;
+  uint16_t full[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (gap < 0) {
+    for (int k = 0; k < 8; k++) full[k] = g[k];
+  } else {
+    for (int k = 0; k < gap; k++) full[k] = g[k];
+    for (int k = 0; k < ng - gap; k++) full[8 - (ng - gap) + k] = g[gap + k];
+  }
+  const bool mapped = !full[0] && !full[1] && !full[2] && !full[3] && !full[4] && full[5] == 0xFFFF;
+  if (mapped) {  // IP.To4
+    out[0] = (uint8_t)(full[6] >> 8); out[1] = (uint8_t)full[6];
+    out[2] = (uint8_t)(full[7] >> 8); out[3] = (uint8_t)full[7];
+    *n = 4;
+    return true;
+  }
+  for (int k = 0; k < 8; k++) {
+    out[2 * k] = (uint8_t)(full[k] >> 8);
+    out[2 * k + 1] = (uint8_t)full[k];
+  }
+  *n = 16;
+  return true;
+}
+
+// coraza ipmatch.go Evaluate: net.ParseIP(value), then IPNet.Contains per network.
+__device__ bool ip_match(const uint8_t* recs, uint32_t rlen, const uint8_t* s, uint32_t n) {
+  uint8_t ip[16];
+  uint32_t fam;
+  if (!dev_parse_ip(s, n, ip, &fam)) return false;
+  for (uint32_t r = 0; r + GI_IPNET_BYTES <= rlen; r += GI_IPNET_BYTES) {
+    const uint8_t* rec = recs + r;
+    if (rec[0] != fam) continue;
+    uint32_t bits = rec[1];
+    bool ok = true;
+    for (uint32_t k = 0; k < fam && bits && ok; k++) {
+      const uint32_t keep = bits >= 8 ? 8u : bits;
+      const uint8_t m = (uint8_t)(0xFF00u >> keep);
+      ok = (ip[k] & m) == rec[2 + k];
+      bits -= keep;
+    }
+    if (ok) return true;
+  }
+  return false;
+}
+
 __device__ bool contains_word(const uint8_t* v, uint32_t vn, const uint8_t* w, uint32_t wn) {
   if (wn == 0) return true;
   for (uint32_t i = 0; i + wn <= vn; i++) {
@@ -2084,6 +2191,9 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
       break;
     case OP_UNCONDITIONAL:
       res = true;
+      break;
+    case OP_IPMATCH:
+      res = ip_match(P.strpool + o.lit_off, o.lit_len, s, n);
       break;
     case OP_NOMATCH:
       res = false;
@@ -2162,7 +2272,7 @@ __device__ __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v
   uint32_t summ = kn ? value_summary(v, vn) : 0u;
   for (uint32_t k = 0; k < kn; k++) {
     const uint8_t code = P.tchains[R.tchain_off + k];
-    if (!(summ & transform_triggers(code))) continue;  // identity on this value
+    if (transform_identity(summ, code)) continue;  // identity on this value
     uint8_t* dst = (cur.p == t.t0) ? t.t1 : t.t0;
     int64_t m = apply_transform(P, code, cur.p, cur.n, dst, t.cap_t);
     if (m < 0) {
@@ -2242,7 +2352,7 @@ __device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp&
     if (k >= R.tchain_len) break;
     const uint8_t code = t.P->tchains[R.tchain_off + k];
     bool changed = false;
-    if (value_summary(cp, cn) & transform_triggers(code)) {  // else an identity on cp
+    if (!transform_identity(value_summary(cp, cn), code)) {  // else an identity on cp
       uint8_t* dst = (cp == t.t0) ? t.t1 : t.t0;
       const int64_t m = apply_transform(*t.P, code, cp, cn, dst, t.cap_t);
       if (m < 0) {
@@ -2499,7 +2609,7 @@ struct ReqHdr {
   uint32_t n_post;      // its ARG_POST fields, after the phase-1 fields (phase-A items)
   Str single[S_COUNT];
 };
-static_assert(sizeof(ReqHdr) <= 256, "ReqHdr must fit its 256-byte slot");
+static_assert(sizeof(ReqHdr) <= GI_REQHDR_BYTES, "ReqHdr must fit its slot");
 
 struct Region {
   ReqHdr* hdr;
@@ -2516,7 +2626,7 @@ __device__ inline Region region_of(const DProgram& P, const DBatch& B, uint32_t 
   uint8_t* base = B.scratch + L.base;
   Region g;
   g.hdr = (ReqHdr*)base;
-  uint64_t off = 256;
+  uint64_t off = GI_REQHDR_BYTES;
   g.fields = (Field*)(base + off);
   off += (uint64_t)L.cap_f * sizeof(Field);
   g.slots = (Slot*)(base + off);
@@ -2676,6 +2786,15 @@ __device__ void collect_request(const DProgram& P, const DBatch& B, uint32_t r) 
   Str proto{D + rq.proto.off, rq.proto.len};
   t.single[S_REQUEST_METHOD] = method;
   t.single[S_REQUEST_PROTOCOL] = proto;
+  t.single[S_REMOTE_ADDR] = {D + rq.remote_addr.off, rq.remote_addr.len};
+  {  // REMOTE_PORT: strconv.Itoa(port)
+    uint8_t* pb = tx_alloc(t, 12);
+    if (pb) {
+      const uint32_t pn = go_itoa((int64_t)rq.remote_port, pb);
+      t.nb -= 12 - pn;
+      t.single[S_REMOTE_PORT] = {pb, pn};
+    }
+  }
   uint8_t* ln = tx_alloc(t, method.n + uri.n + proto.n + 2);
   if (ln) {
     uint32_t k = 0;
@@ -2775,7 +2894,7 @@ __global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
       const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
       if (!(H->flags & GI_REQ_ERROR_MASK)) {
         uint32_t c[GI_NB] = {0, 0, 0, 0, 0};
-        for_each_item(P, H, (const Field*)(B.scratch + L.base + 256),
+        for_each_item(P, H, (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES),
                       [&](uint8_t, uint8_t, uint32_t, uint32_t, uint32_t n) { c[item_bucket(n)]++; });
         for (uint32_t b = 0; b < GI_NB; b++)
           if (c[b]) atomicAdd(&hist[b], c[b]);
@@ -2879,7 +2998,7 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
     const ReqLayout L = B.layout[r];
     const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
     if (!(H->flags & GI_REQ_ERROR_MASK)) {
-      const Field* Fd = (const Field*)(B.scratch + L.base + 256);
+      const Field* Fd = (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES);
       const uint32_t* boff = B.boffs + blockIdx.x * GI_NB;
       for_each_item(P, H, Fd, [&](uint8_t kind, uint8_t sg, uint32_t side, uint32_t fi, uint32_t n) {
         const uint32_t b = item_bucket(n);
@@ -2964,7 +3083,7 @@ __device__ __forceinline__ int64_t run_chain(const DProgram& P, const DStream& S
   uint32_t cn = vn;
   for (uint32_t k = 0; k < S.tchain_len; k++) {
     const uint8_t code = (uint8_t)GI_CONST(uint32_t, P.tchains32)[S.tchain_off + k];
-    if (!(summ & transform_triggers(code))) continue;
+    if (transform_identity(summ, code)) continue;
     uint8_t* dst = (cur == b0) ? b1 : b0;
     const int64_t m = INL ? apply_transform_inl(P, code, cur, cn, dst, cap) : apply_transform(P, code, cur, cn, dst, cap);
     if (m < 0) return -1;

@@ -473,7 +473,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   const uint32_t n_single_items = (uint32_t)__builtin_popcount(PG.item_singles);
   for (uint32_t r = 0; r < n; r++) {
     const gi_request& q = in->reqs[r];
-    const gi_span* sp[4] = {&q.method, &q.uri, &q.proto, &q.body};
+    const gi_span* sp[5] = {&q.method, &q.uri, &q.proto, &q.body, &q.remote_addr};
     for (auto* s : sp)
       if (s->off + s->len > in->data_len) return fail(c, GI_EINVAL, "request span out of range");
     if ((uint64_t)q.hdr_begin + q.hdr_count > in->n_headers) return fail(c, GI_EINVAL, "header range out of range");
@@ -512,7 +512,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       post_fields = std::min<uint64_t>(seps + 2, q.body.len / 2 + 2);
     }
     uint64_t cap_f = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie) + post_fields;
-    uint64_t cap_b = 4ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96;
+    uint64_t cap_b = 4ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96 + 16;  // + REMOTE_PORT
     {  // a JSON-looking body: room for the flattened "json.a.b" keys + parser stack
       const uint8_t* bd = in->data + q.body.off;
       uint32_t k = 0;
@@ -542,7 +542,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     L.cap_b = (uint32_t)cap_b;
     L.cap_t = (uint32_t)cap_t;
     L.cap_mt = (uint32_t)cap_mt;
-    uint64_t sz = 256 + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + 128 + (cap_b + 15) / 16 * 16 +
+    uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + 128 + (cap_b + 15) / 16 * 16 +
                   2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
     // matched-variable state (kernels.hip MvState): header, entries, value
     // arena, MATCHED_VAR copy, name buffer
@@ -724,7 +724,7 @@ int gi_sync(gi_ctx* c) {
       const std::string nm = c->log.name[k];
       snprintf(c->stats.launch_name[k], sizeof(c->stats.launch_name[k]), "%s", nm.c_str());
       uint64_t ab = 0;
-      if (nm == "k_collect") ab = c->raw_nobody + 256ull * c->n_req;  // request bytes in, ReqHdr out
+      if (nm == "k_collect") ab = c->raw_nobody + (uint64_t)GI_REQHDR_BYTES * c->n_req;  // request bytes in, ReqHdr out
       else if (nm == "k_items") ab = 32ull * (ibk[1] + ibk[3] + ibk[5] + ibk[7] + ibk[9]);  // item records out
       else if (nm == "k_ioffsets") ab = 8ull * 5 * ((c->n_req + 255) / 256);             // block counts in, offsets out
       else if (nm.rfind("k_stream", 0) == 0) {

@@ -53,11 +53,12 @@ MAX_EXPORTS = 8
 
 SPAN_DT = np.dtype([("off", "<u8"), ("len", "<u4"), ("_pad", "<u4")])
 REQUEST_DT = np.dtype([("method", SPAN_DT), ("uri", SPAN_DT), ("proto", SPAN_DT), ("body", SPAN_DT),
-                       ("hdr_begin", "<u4"), ("hdr_count", "<u4")])
+                       ("hdr_begin", "<u4"), ("hdr_count", "<u4"), ("remote_addr", SPAN_DT),
+                       ("remote_port", "<u4"), ("_pad", "<u4")])
 HEADER_DT = np.dtype([("name", SPAN_DT), ("value", SPAN_DT)])
 VERDICT_DT = np.dtype([("rule_id", "<i4"), ("status", "<i4"), ("action", "u1"), ("phase", "u1"),
                        ("flags", "<u2"), ("match_cnt", "<u4"), ("tx_export", "<i8", (MAX_EXPORTS,))])
-assert REQUEST_DT.itemsize == 72 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 80
+assert REQUEST_DT.itemsize == 96 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 80
 
 EXPORTED_SYMBOLS = (
     "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name", "gi_ruleset_describe",
@@ -286,6 +287,13 @@ class Transaction:
     proto: bytes = b"HTTP/1.1"
     headers: List[Tuple[bytes, bytes]] = field(default_factory=list)
     body: bytes = b""
+    remote_addr: bytes = b""
+    remote_port: int = 0
+
+    def process_connection(self, client, cport, server=b"", sport=0):
+        """ProcessConnection: REMOTE_ADDR / REMOTE_PORT (the server side is not
+        a variable this engine evaluates)."""
+        self.remote_addr, self.remote_port = _b(client), int(cport)
 
     def process_uri(self, uri, method, proto):
         self.uri, self.method, self.proto = _b(uri), _b(method), _b(proto)
@@ -343,27 +351,35 @@ class PackedBatch:
             return bytes(d[int(s["off"]):int(s["off"]) + int(s["len"])])
         hs = [(sp(h["name"]), sp(h["value"])) for h in
               self.headers[int(q["hdr_begin"]):int(q["hdr_begin"]) + int(q["hdr_count"])]]
-        return Transaction(sp(q["method"]), sp(q["uri"]), sp(q["proto"]), hs, sp(q["body"]))
+        return Transaction(sp(q["method"]), sp(q["uri"]), sp(q["proto"]), hs, sp(q["body"]),
+                           sp(q["remote_addr"]), int(q["remote_port"]))
 
 
 def pack(txs: Sequence) -> PackedBatch:
-    """Pack transactions (objects with method/uri/proto/headers/body) into the
-    gi_batch arena: per request [method, uri, proto, body, h0.name, h0.value, ...]."""
+    """Pack transactions (objects with method/uri/proto/headers/body and
+    optionally remote_addr/remote_port) into the gi_batch arena: per request
+    [method, uri, proto, body, remote_addr, h0.name, h0.value, ...]."""
     parts = []
     nh = np.empty(len(txs), np.int64)
+    ports = np.zeros(len(txs), np.int64)
     for i, t in enumerate(txs):
         parts.append(t.method)
         parts.append(t.uri)
         parts.append(t.proto)
         parts.append(t.body)
+        parts.append(getattr(t, "remote_addr", b""))
+        ports[i] = getattr(t, "remote_port", 0)
         for k, v in t.headers:
             parts.append(k)
             parts.append(v)
         nh[i] = len(t.headers)
-    return pack_parts(parts, nh)
+    return pack_parts(parts, nh, ports)
 
 
-def pack_parts(parts: List[bytes], nh: np.ndarray) -> PackedBatch:
+NFIXED = 5  # fixed parts per request in pack_parts: method, uri, proto, body, remote_addr
+
+
+def pack_parts(parts: List[bytes], nh: np.ndarray, ports=None) -> PackedBatch:
     lens = np.fromiter(map(len, parts), dtype=np.int64, count=len(parts))
     offs = np.zeros(len(parts), np.int64)
     if len(parts):
@@ -372,14 +388,16 @@ def pack_parts(parts: List[bytes], nh: np.ndarray) -> PackedBatch:
     if len(data) == 0:
         data = np.zeros(1, np.uint8)
     n = len(nh)
-    per = 4 + 2 * nh
+    per = NFIXED + 2 * nh
     start = np.zeros(n, np.int64)
     if n:
         np.cumsum(per[:-1], out=start[1:])
     reqs = np.zeros(n, REQUEST_DT)
-    for j, name in enumerate(("method", "uri", "proto", "body")):
+    for j, name in enumerate(("method", "uri", "proto", "body", "remote_addr")):
         reqs[name]["off"] = offs[start + j]
         reqs[name]["len"] = lens[start + j]
+    if ports is not None:
+        reqs["remote_port"] = ports
     hb = np.zeros(n, np.int64)
     if n:
         np.cumsum(nh[:-1], out=hb[1:])
@@ -391,7 +409,7 @@ def pack_parts(parts: List[bytes], nh: np.ndarray) -> PackedBatch:
         # index of each header's name part
         req_of_h = np.repeat(np.arange(n), nh)
         k_in_req = np.arange(H) - hb[req_of_h]
-        name_idx = start[req_of_h] + 4 + 2 * k_in_req
+        name_idx = start[req_of_h] + NFIXED + 2 * k_in_req
         headers["name"]["off"] = offs[name_idx]
         headers["name"]["len"] = lens[name_idx]
         headers["value"]["off"] = offs[name_idx + 1]

@@ -220,6 +220,7 @@ class TrafficGen:
         rng = self.rng
         parts = []
         nh = np.empty(n, np.int64)
+        ports = np.empty(n, np.int64)
         n_args = rng.integers(0, 7, n)
         attack = rng.random(n) < attack_rate
         post = rng.random(n) < post_frac
@@ -237,15 +238,24 @@ class TrafficGen:
                 body_attack = bool(attack[i]) and rng.random() < 0.5
                 is_json = rng.random() < json_frac
                 body = self._json_body(body_attack) if is_json else self._urlencoded_body(body_attack)
-                parts += [b"POST", uri, b"HTTP/1.1", body]
+                parts += [b"POST", uri, b"HTTP/1.1", body, self._client(i, ports)]
                 k = self._headers(parts, path)
                 ctype = b"application/json" if is_json else b"application/x-www-form-urlencoded"
                 parts += [b"Content-Type", ctype, b"Content-Length", str(len(body)).encode()]
                 nh[i] = k + 2
             else:
-                parts += [b"GET", uri, b"HTTP/1.1", b""]
+                parts += [b"GET", uri, b"HTTP/1.1", b"", self._client(i, ports)]
                 nh[i] = self._headers(parts, path)
-        return parts, nh
+        return parts, nh, ports
+
+    def _client(self, i, ports):
+        """ProcessConnection client (REMOTE_ADDR / REMOTE_PORT): derived from the
+        request index, so the draws of the other fields stay as they were."""
+        h = (i * 2654435761 + 12345) & 0xFFFFFFFF
+        ports[i] = 1024 + h % 60000
+        if h % 16 == 0:  # some IPv6 clients
+            return b"2001:db8:%x::%x" % ((h >> 8) & 0xFFFF, h & 0xFFF)
+        return b"10.%d.%d.%d" % ((h >> 24) & 255, (h >> 16) & 255, (h >> 8) & 255)
 
     def _urlencoded_body(self, attack: bool):
         rng = self.rng
@@ -265,8 +275,8 @@ class TrafficGen:
 
     def batch(self, n: int, post_frac: float = 0.0, attack_rate: float = 0.05,
               json_frac: float = 0.4) -> "gpuinspect.PackedBatch":
-        parts, nh = self.gen(n, post_frac, attack_rate, json_frac)
-        return gpuinspect.pack_parts(parts, nh)
+        parts, nh, ports = self.gen(n, post_frac, attack_rate, json_frac)
+        return gpuinspect.pack_parts(parts, nh, ports)
 
 
 def c1_batch(n: int = 10000, seed: int = SEED):

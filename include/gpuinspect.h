@@ -108,8 +108,9 @@ typedef struct {
   uint32_t _pad;
 } gi_span;
 
-/* One HTTP request: what ProcessURI(uri, method, proto),
- * AddRequestHeader(k, v) x hdr_count and WriteRequestBody(body) receive. */
+/* One HTTP request: what ProcessConnection(client, cport, ...),
+ * ProcessURI(uri, method, proto), AddRequestHeader(k, v) x hdr_count and
+ * WriteRequestBody(body) receive. */
 typedef struct {
   gi_span method;
   gi_span uri;
@@ -117,6 +118,9 @@ typedef struct {
   gi_span body;
   uint32_t hdr_begin; /* index into gi_batch.headers */
   uint32_t hdr_count;
+  gi_span remote_addr;  /* ProcessConnection client address -> REMOTE_ADDR (may be empty) */
+  uint32_t remote_port; /* -> REMOTE_PORT */
+  uint32_t _pad;
 } gi_request;
 
 typedef struct {

@@ -15,12 +15,18 @@ from . import coraza
 ACTION_CODES = {"": 0, "deny": 1, "drop": 2, "redirect": 3}
 
 
+def oracle_request(t):
+    """gpuinspect.Transaction -> the oracle's Request (the same inputs)."""
+    return coraza.Request(t.method, t.uri, t.proto, list(t.headers), t.body,
+                          getattr(t, "remote_addr", b""), int(getattr(t, "remote_port", 0)))
+
+
 def oracle_verdicts(cfg, batch, exports, idx=None):
     idx = range(batch.n_req) if idx is None else idx
     out = {}
     for i in idx:
         t = batch.request(i)
-        req = coraza.Request(t.method, t.uri, t.proto, list(t.headers), t.body)
+        req = oracle_request(t)
         out[i] = coraza.inspect(cfg, req, exports)
     return out
 

@@ -106,6 +106,7 @@ class Operator:
     phrases: Optional[List[bytes]] = None
     byte_ok: Optional[List[bool]] = None
     macro: Optional[list] = None
+    nets: Optional[list] = None  # @ipMatch networks (ipmatch_networks)
 
 
 @dataclass
@@ -416,6 +417,19 @@ def _parse_operator(opstr: str, data_files=None) -> Operator:
     elif name_l in ("unconditionalmatch", "nomatch", "validateurlencoding",
                     "validateutf8encoding"):
         pass
+    elif name_l == "ipmatch":
+        op.nets = ipmatch_networks(data)
+    elif name_l in ("ipmatchfromfile", "ipmatchf"):
+        # ipmatchfromfile.go: one network per line, '#' comments and blanks skipped
+        if data_files is None or data not in data_files:
+            raise SecLangError("open %s: no such file or directory" % data)
+        lines = []
+        for line in data_files[data].split(b"\n"):
+            line = line.rstrip(b"\r").strip()
+            if line and line[:1] != b"#":
+                lines.append(line.decode("latin-1"))
+        op.name = "ipmatch"
+        op.nets = ipmatch_networks(",".join(lines))
     else:
         raise SecLangError("unsupported operator @%s" % name)
     return op
@@ -1232,6 +1246,8 @@ class Request:
     proto: bytes = b"HTTP/1.1"
     headers: List[Tuple[bytes, bytes]] = field(default_factory=list)
     body: bytes = b""
+    remote_addr: bytes = b""   # ProcessConnection client -> REMOTE_ADDR
+    remote_port: int = 0       # -> REMOTE_PORT (strconv.Itoa)
 
 
 class UnsupportedInput(ValueError):
@@ -1690,6 +1706,8 @@ class Transaction:
         self.single["REQUEST_METHOD"] = req.method
         self.single["REQUEST_PROTOCOL"] = req.proto
         self.single["REQUEST_LINE"] = req.method + b" " + req.uri + b" " + req.proto
+        self.single["REMOTE_ADDR"] = req.remote_addr
+        self.single["REMOTE_PORT"] = str(req.remote_port).encode()
         self.maps["ARGS_GET"] = list(args)
         for k, val in req.headers:
             if k == b"":
@@ -1841,6 +1859,8 @@ class Transaction:
             res = any(not op.byte_ok[c] for c in value)
         elif n == "validateurlencoding":
             res = _invalid_url_encoding(value)
+        elif n == "ipmatch":
+            res = ipmatch(op.nets, value)
         elif n == "validateutf8encoding":
             try:
                 value.decode("utf-8")
@@ -2052,6 +2072,76 @@ def _pm_find_all(phrases, low: bytes, orig: bytes):
         else:
             i += 1
     return out
+
+
+def _go_parse_ip(v: bytes):
+    """Go net.ParseIP + IP.To4 via Python's ipaddress (an independent parser):
+    (4, bytes) for IPv4 or an IPv4-mapped IPv6 address, (16, bytes), or None.
+    Zones are rejected (ParseIP); IPv4 fields with leading zeros are rejected
+    by both (netip)."""
+    import ipaddress
+    try:
+        s = v.decode("ascii")
+    except UnicodeDecodeError:
+        return None
+    if "%" in s or s.strip() != s or not s:
+        return None
+    try:
+        a = ipaddress.ip_address(s)
+    except ValueError:
+        return None
+    if a.version == 6 and a.ipv4_mapped is not None:
+        return 4, a.ipv4_mapped.packed
+    return (4 if a.version == 4 else 16), a.packed
+
+
+def ipmatch_networks(arg: str):
+    """[upstream coraza internal/operators/ipmatch.go]: comma-separated
+    networks, a bare address gets /32 or /128, net.ParseCIDR (host bits
+    masked off), invalid entries skipped.  IPNet.Contains compares To4() of
+    the network number: a masked IPv4-mapped network is IPv4 with prefix-96."""
+    import ipaddress
+    nets = []
+    for e in arg.split(","):
+        e = e.strip()
+        if not e:
+            continue
+        addr, _, bits = e.partition("/")
+        got = _go_parse_ip(addr.encode())
+        if got is None:
+            continue
+        fam = 4 if (":" not in addr) else 16
+        if bits:
+            if not bits.isdigit():
+                continue
+            nb = int(bits)
+        else:
+            nb = 32 if fam == 4 else 128
+        if nb > 8 * fam:
+            continue
+        raw = ipaddress.ip_address(addr).packed
+        netw = ipaddress.ip_network((raw, nb), strict=False)
+        packed = netw.network_address.packed
+        if fam == 16 and packed[:10] == b"\0" * 10 and packed[10:12] == b"\xff\xff":
+            nets.append((4, packed[12:], max(0, nb - 96)))
+        else:
+            nets.append((fam, packed, nb))
+    return nets
+
+
+def ipmatch(nets, value: bytes) -> bool:
+    got = _go_parse_ip(value)
+    if got is None:
+        return False
+    fam, ip = got
+    iv = int.from_bytes(ip, "big")
+    for f, net, nb in nets:
+        if f != fam:
+            continue
+        sh = 8 * f - nb
+        if (iv >> sh) == (int.from_bytes(net, "big") >> sh):
+            return True
+    return False
 
 
 def _contains_word(value: bytes, w: bytes) -> bool:
