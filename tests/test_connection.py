@@ -28,7 +28,7 @@ SecRule REMOTE_ADDR "@ipMatch %s" "id:1,phase:1,pass,setvar:tx.anomaly_score=+1"
 SecRule REMOTE_ADDR "@ipMatchFromFile allow.txt" "id:2,phase:1,pass,setvar:tx.anomaly_score=+10"
 SecRule ARGS:ip "@ipMatch %s" "id:3,phase:1,pass,setvar:tx.anomaly_score=+100"
 SecRule REMOTE_PORT "@rx ^4[0-9]{3}$" "id:4,phase:1,pass,setvar:tx.anomaly_score=+1000"
-SecRule REMOTE_ADDR "@rx ^10\\\\." "id:5,phase:1,pass,setvar:tx.anomaly_score=+10000"
+SecRule REMOTE_ADDR "@rx ^10[.]" "id:5,phase:1,pass,setvar:tx.anomaly_score=+10000"
 """ % (IPM, IPM)
 FILES = {"allow.txt": b"# office\\n10.0.0.0/8\\r\\n\\n2001:db8::/32\\n"}
 
