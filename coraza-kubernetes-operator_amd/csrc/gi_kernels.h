@@ -19,8 +19,8 @@ struct ReqLayout {
   uint32_t cap_b;  // decoded-bytes arena
   uint32_t cap_t;  // each of the two transformation buffers
   uint32_t cap_mt; // macro expansion scratch == TX string arena size
-  uint64_t pa_base;  // byte offset of the request's phase-A arena in DBatch.pa
-  uint32_t pa_cap;   // its capacity (overflow voids the request's phase-A bits)
+  uint64_t vmap_bit;   // first bit of the request's value map in DBatch.vmap (a multiple of 32)
+  uint32_t vmap_bits;  // 2 x cap_f: bit 2f = value of field f hit, bit 2f+1 = its key
   uint32_t _pad;
 };
 
@@ -37,6 +37,9 @@ struct DBatch {
   unsigned long long* tally;  // gi_tally counters
   uint32_t* tally_ext;        // [GI_SCORE_BINS] score histogram, then per distinct rule id match counts
   uint32_t* hits;             // phase-A hit words [ceil(n_hit_slots/32)][n_req]
+  uint32_t* vmap;             // phase-A value map: a bit per scanned (field, side) that set some hit bit
+  const uint32_t* body_list;  // requests with a body, longest first (k_body: one wave each)
+  uint32_t n_body;
   Slot* txslots;       // TX variables [n_slots][n_req] (k_eval)
   // phase A (see kernels.hip "phase A")
   uint32_t* bcounts;          // [k_collect blocks][GI_NB] item counts
@@ -90,7 +93,7 @@ void scan_allow_lds(uint32_t lds_bytes);
 // ev (optional) = 3 events recorded after k_collect, k_stream and k_scan.
 // Per-launch HIP events of one pipeline run (ev[0] before the first launch,
 // ev[k + 1] after launch k).
-#define GI_MAX_LAUNCHES 16
+#define GI_MAX_LAUNCHES GI_STATS_LAUNCHES
 struct LaunchLog {
   hipEvent_t ev[GI_MAX_LAUNCHES + 1];
   const char* name[GI_MAX_LAUNCHES];

@@ -1258,6 +1258,8 @@ struct Tx {
   uint32_t ntx, cap_tx;
   Str* single;               // ReqHdr::single (per-request, in HBM scratch)
   const uint32_t* hits;      // phase-A hit words [slot/32][n_req]
+  const uint32_t* vmap;      // the request's phase-A value map (bit 2f + side)
+  uint32_t nf_pa;            // fields [0, nf_pa) went through phase A (value map valid)
   uint32_t n_req, req;
   bool has_post;             // ARGS_POST fields phase A did not see (phase-A bits of RF_BODYDEP links void)
   bool body_spec;            // the body went through k_collect's processor: k_body tested REQUEST_BODY
@@ -2370,6 +2372,14 @@ __device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp&
   return nm;
 }
 
+// Hit slot s is set only by per-value phase-A evaluation (each such hit also
+// marks its value in the value map): not an always-slot.
+__device__ __forceinline__ bool slot_vexact(const DProgram& P, uint32_t s) {
+  for (uint32_t k = 0; k < P.n_always; k++)
+    if (P.always_slots[k] == s) return false;
+  return true;
+}
+
 // Rule.doEvaluate for one link -> number of matched values.
 __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   const DProgram& P = *t.P;
@@ -2491,11 +2501,20 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
       }
       continue;
     }
+    // phase A tested every value of fields [0, nf_pa) this link reads: one
+    // whose value-map bit is clear set no hit bit at all, so it cannot match
+    // here (value-exact slots only: an always-slot is set without a value)
+    const bool vskip = R.hit_slot >= 0 && !vr.count && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
+                       slot_vexact(P, (uint32_t)R.hit_slot);
     uint32_t cnt = 0;
     for (uint32_t f = 0; f < t.nf; f++) {
       const Field fl = t.fields[f];
       bool names;
       if (!field_in(vr.var, fl.kind, &names)) continue;
+      if (vskip && f < t.nf_pa) {
+        const uint32_t vb = 2 * f + (names ? 1u : 0u);
+        if (!((t.vmap[vb >> 5] >> (vb & 31)) & 1u)) continue;
+      }
       if (vr.key_mode == 1) {
         if (vr.ci ? !eq_ascii_ci(fl.k, fl.kn, P.strpool + vr.key_off, vr.key_len)
                   : !eq_bytes(fl.k, fl.kn, P.strpool + vr.key_off, vr.key_len))
@@ -2726,6 +2745,11 @@ __device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
   atomicOr(&B.hits[(uint64_t)(slot >> 5) * B.n_req + r], 1u << (slot & 31));
 }
 
+__device__ __forceinline__ void void_request(const DBatch& B, uint32_t r) {
+  ReqHdr* H = (ReqHdr*)(B.scratch + B.layout[r].base);
+  H->pa_void = 1;
+}
+
 #define GI_NB 5  // item length buckets: <=16, <=32, <=64, <=128, >128 bytes
 // qblk entry {pool word offset, nv | nw << 8 | shared}: shared = the block was
 // written for an earlier stream of the same item-wave (raw item bytes)
@@ -2740,6 +2764,17 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 // rank of this lane among the lanes of mask below it
 __device__ __forceinline__ uint32_t mask_rank(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t* total) {
+  const uint32_t L = lane_id();
+  uint32_t inc = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (L >= (uint32_t)o) inc += y;
+  }
+  *total = __shfl(inc, 63, 64);
+  return inc - x;
 }
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
@@ -2859,24 +2894,148 @@ __device__ void collect_request(const DProgram& P, const DBatch& B, uint32_t r) 
           sp = BP_JSON;
       }
     }
-    if (sp == BP_URLENCODED || sp == BP_JSON) {
-      const uint32_t nf0 = t.nf, nb0 = t.nb;
-      const uint16_t fl0 = t.flags;
-      if (sp == BP_URLENCODED) parse_query(t, D + rq.body.off, bn, FK_ARG_POST);
-      else parse_json_body(t, D + rq.body.off, bn);
-      if (t.flags != fl0) {  // not parsable as guessed: k_eval decides
-        t.nf = nf0;
-        t.nb = nb0;
-        t.flags = fl0;
-        sp = BP_NONE;
+    if (sp != BP_URLENCODED && sp != BP_JSON) sp = BP_NONE;
+  }
+  H->spec_proc = sp;  // k_bparse parses the body (or resets this to BP_NONE)
+  H->n_post = 0;
+  H->nb = t.nb;
+}
+
+// Speculative ProcessRequestBody (k_collect picked the processor): one wave
+// per body.  urlencoded bodies are split over the lanes: a field is a
+// non-empty '&'-separated segment, so lane L takes the segments that start in
+// its 1/64 of the body (a wave prefix sum numbers them in body order) and
+// decodes each key / value into the arena at the segment's own offset (a
+// decoding is never longer than its input, so segments cannot collide).  JSON
+// bodies run the sequential parser on lane 0.  A body that does not parse as
+// guessed (or overflows a capacity) leaves no fields: k_eval decides.  The
+// wave then adds the body fields' phase-A item counts to its k_collect
+// block's bucket counts.
+__device__ __forceinline__ void urlenc_segment(const uint8_t* q, uint32_t n, uint32_t p, uint32_t* j_out,
+                                               uint32_t* e_out, bool* kesc, bool* vesc) {
+  uint32_t j = p, e = 0xFFFFFFFFu;
+  bool ke = false, ve = false;
+  for (; j < n; j++) {
+    const uint8_t c = q[j];
+    if (c == '&') break;
+    if (c == '=' && e == 0xFFFFFFFFu) e = j;
+    else if (c == '%' || c == '+') (e == 0xFFFFFFFFu ? ke : ve) = true;
+  }
+  *j_out = j;
+  *e_out = e == 0xFFFFFFFFu ? j : e;
+  *kesc = ke;
+  *vesc = ve;
+}
+
+__global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
+  const uint32_t L = threadIdx.x;
+  for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
+    const uint32_t r = B.body_list[bi];
+    GI_BOUND(r < B.n_req, r, bi);
+    Region g = region_of(P, B, r);
+    ReqHdr* H = g.hdr;
+    const uint8_t sp = H->spec_proc;
+    if ((sp != BP_URLENCODED && sp != BP_JSON) || (H->flags & GI_REQ_ERROR_MASK)) continue;
+    const gi_span bs = B.reqs[r].body;
+    const uint8_t* q = B.data + bs.off;
+    const uint32_t n = bs.len;
+    const uint32_t nf0 = H->nf, nb0 = H->nb;
+    uint32_t n_post = 0, nb = nb0;
+    bool ok = true;
+    if (sp == BP_URLENCODED && (uint64_t)nb0 + n <= g.cap_b) {
+      const uint32_t a0 = (uint32_t)((uint64_t)n * L / 64), a1 = (uint32_t)((uint64_t)n * (L + 1) / 64);
+      uint32_t c = 0;
+      for (uint32_t p = a0; p < a1; p++) c += (q[p] != '&' && (p == 0 || q[p - 1] == '&')) ? 1u : 0u;
+      uint32_t tot;
+      uint32_t idx = nf0 + wave_excl_sum(c, &tot);
+      n_post = tot;
+      if ((uint64_t)nf0 + tot > g.cap_f) {
+        ok = false;  // add_field would overflow
+      } else {
+        uint32_t used = 0;  // arena bytes [nb0, nb0 + used) this lane's decodings reach
+        for (uint32_t p = a0; p < a1; p++) {
+          if (q[p] == '&' || (p > 0 && q[p - 1] != '&')) continue;
+          uint32_t j, e;
+          bool kesc, vesc;
+          urlenc_segment(q, n, p, &j, &e, &kesc, &vesc);
+          const uint8_t* k = q + p;
+          uint32_t kn = e - p;
+          const uint8_t* v = q + (e < j ? e + 1 : j);
+          uint32_t vn = e < j ? j - e - 1 : 0;
+          if (kesc) {
+            uint8_t* d = g.bytes + nb0 + p;
+            kn = query_unescape(k, kn, d);
+            k = d;
+            used = max(used, p + kn);
+          }
+          if (vesc) {
+            const uint32_t vo = (uint32_t)(v - q);
+            uint8_t* d = g.bytes + nb0 + vo;
+            vn = query_unescape(v, vn, d);
+            v = d;
+            used = max(used, vo + vn);
+          }
+          Field& f = g.fields[idx++];
+          f.k = k;
+          f.v = v;
+          f.kn = kn;
+          f.vn = vn;
+          f.kind = FK_ARG_POST;
+          f._pad = 0;
+        }
+        nb = nb0 + wave_max(used);
       }
-    } else {
-      sp = BP_NONE;
+    } else {  // JSON (or an urlencoded body the arena bound does not cover): lane 0, sequential
+      uint32_t res[3] = {0, 0, 0};
+      if (L == 0) {
+        if (sp == BP_URLENCODED) {
+          Tx t;
+          tx_bind(t, P, g);
+          t.nf = nf0;
+          t.nb = nb0;
+          t.flags = 0;
+          parse_query(t, q, n, FK_ARG_POST);
+          res[0] = t.nf - nf0;
+          res[1] = t.nb;
+          res[2] = t.flags;
+        } else {
+          JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
+          parse_json_body(jc, q, n);
+          res[0] = jc.nf - nf0;
+          res[1] = jc.nb;
+          res[2] = jc.flags;
+        }
+      }
+      n_post = __shfl(res[0], 0, 64);
+      nb = __shfl(res[1], 0, 64);
+      ok = __shfl(res[2], 0, 64) == 0;
+    }
+    if (!ok) {  // not parsable as guessed: k_eval decides
+      n_post = 0;
+      nb = nb0;
+    }
+    __syncthreads();
+    if (L == 0) {
+      H->n_post = n_post;
+      H->nb = nb;
+      if (!ok) H->spec_proc = BP_NONE;
+    }
+    // phase-A item counts of the body fields (ARGS_POST sides some filter reads)
+    const uint32_t sides = P.n_streams ? P.item_sides[FK_ARG_POST] : 0u;
+    if (sides) {
+      uint32_t cnt[GI_NB] = {0, 0, 0, 0, 0};
+      for (uint32_t i = L; i < n_post; i += 64) {
+        const Field fl = g.fields[nf0 + i];
+        if (sides & 1) cnt[item_bucket(fl.vn)]++;
+        if (sides & 2) cnt[item_bucket(fl.kn)]++;
+      }
+      for (uint32_t b = 0; b < GI_NB; b++) {
+        uint32_t x = cnt[b];
+        for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, 64);
+        if (L == 0 && x) atomicAdd(&B.bcounts[(r / 256) * GI_NB + b], x);
+      }
     }
   }
-  H->spec_proc = sp;
-  H->n_post = t.nf - H->nf;
-  H->nb = t.nb;
 }
 
 // ProcessURI + AddRequestHeader* for one request per thread, then the
@@ -2935,12 +3094,37 @@ struct Item {  // 32 B
   const uint8_t* vp;  // scanned bytes: value side, key side or single
   uint32_t kn, vn;
   uint32_t req;
-  uint8_t kind;       // FieldKind, 0 = single
-  uint8_t single;     // SingleId (kind 0)
-  uint8_t side;       // 1: key side (the *_NAMES collections)
-  uint8_t _pad;
+  uint32_t meta;      // bits 0-2 FieldKind (0 = single); fields: bit 3 key side (the *_NAMES
+                      // collections), bits 4-31 field index; singles: bits 8-15 SingleId
 };
 static_assert(sizeof(Item) == 32, "Item layout");
+#define GI_MAX_ITEM_FIELD 0x0FFFFFFFu
+__device__ __forceinline__ uint32_t item_kind(const Item& it) { return it.meta & 7u; }
+__device__ __forceinline__ uint32_t item_side(const Item& it) { return (it.meta >> 3) & 1u; }
+__device__ __forceinline__ uint32_t item_single(const Item& it) { return (it.meta >> 8) & 0xFFu; }
+// value-map index of the item (2 x field + side); GI_NO_VIX for singles
+#define GI_NO_VIX 0xFFFFFFFFu
+__device__ __forceinline__ uint32_t meta_vix(uint32_t meta) {
+  return (meta & 7u) ? 2u * (meta >> 4) + ((meta >> 3) & 1u) : GI_NO_VIX;
+}
+
+// A scanned value set hit bit `slot` of request r: the bit, and the value's
+// bit in the request's value map (k_eval tests only mapped values of the
+// links whose slot is value-exact, see eval_rule).
+__device__ __forceinline__ void hit_value(const DBatch& B, uint32_t slot, uint32_t r, uint32_t vix) {
+  set_hit(B, slot, r);
+  if (vix != GI_NO_VIX) {
+    const ReqLayout L = B.layout[r];
+    GI_BOUND(vix < L.vmap_bits, vix, L.vmap_bits);
+    atomicOr(&B.vmap[(L.vmap_bit + vix) >> 5], 1u << (vix & 31));
+  }
+}
+// the same for the item at global index idx (k_scan's queue lanes carry it)
+__device__ __forceinline__ void hit_item(const DBatch& B, uint32_t slot, uint32_t idx) {
+  GI_BOUND(idx < B.items_cap, idx, B.items_cap);
+  const uint2 rm = *(const uint2*)((const uint8_t*)B.items + 32ull * idx + 24);  // (req, meta)
+  hit_value(B, slot, rm.x, meta_vix(rm.y));
+}
 
 __global__ void __launch_bounds__(1024) k_ioffsets(DBatch B, uint32_t n_blocks) {
   // bcounts[blk * GI_NB + b] -> boffs (exclusive, bucket-major global order);
@@ -3017,10 +3201,8 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
         }
         it.vn = n;
         it.req = r;
-        it.kind = kind;
-        it.single = sg;
-        it.side = (uint8_t)side;
-        it._pad = 0;
+        it.meta = kind ? (uint32_t)kind | (side << 3) | (min(fi, GI_MAX_ITEM_FIELD) << 4) : (uint32_t)sg << 8;
+        if (kind && fi > GI_MAX_ITEM_FIELD) void_request(B, r);  // no value-map index: no phase-A bit trusted
         ((Item*)B.items)[at] = it;
         atomicAdd(&ibytes[b], (unsigned long long)n);
       });
@@ -3035,15 +3217,16 @@ __device__ uint64_t item_gmask(const DProgram& P, const Item& it) {
   uint64_t m = 0;
   // key hashes (read the key once): literal selectors / exceptions compare
   // bytes only on a hash hit
-  const uint32_t hci = it.kind ? gi_fnv1a(it.kp, it.kn, true) : 0u;
-  const uint32_t hcs = it.kind ? gi_fnv1a(it.kp, it.kn, false) : 0u;
+  const uint32_t kind = item_kind(it);
+  const uint32_t hci = kind ? gi_fnv1a(it.kp, it.kn, true) : 0u;
+  const uint32_t hcs = kind ? gi_fnv1a(it.kp, it.kn, false) : 0u;
   for (uint32_t g = 0; g < P.n_gfilters; g++) {
     const DFilter F = gi_cload(P.filters, g);
-    if (it.kind == 0) {
-      if (F.single == it.single) m |= 1ull << g;
+    if (kind == 0) {
+      if (F.single == item_single(it)) m |= 1ull << g;
       continue;
     }
-    if (F.single != GI_NO_SINGLE || !((F.kind_mask >> it.kind) & 1) || F.names != it.side) continue;
+    if (F.single != GI_NO_SINGLE || !((F.kind_mask >> kind) & 1) || F.names != item_side(it)) continue;
     if (F.key_mode == 1) {
       if ((F.ci ? hci : hcs) != F.key_hash) continue;
       if (F.ci ? !eq_ascii_ci(it.kp, it.kn, P.strpool + F.key_off, F.key_len)
@@ -3064,12 +3247,12 @@ __device__ uint64_t item_gmask(const DProgram& P, const Item& it) {
 }
 
 // The stream's validate operators (@validateByteRange / UrlEncoding / Utf8Encoding).
-__device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, const DStream& S, uint64_t fm, bool maybe,
-                            const uint8_t* v, uint32_t n) {
+__device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, uint32_t vix, const DStream& S, uint64_t fm,
+                            bool maybe, const uint8_t* v, uint32_t n) {
   for (uint32_t q = 0; q < S.val_count; q++) {
     const DScanVal& sv = P.svals[S.val_begin + q];
     if (!(fm & sv.fmask)) continue;
-    if (maybe || (validate_op(sv.kind, sv.bits, v, n) != (sv.negate != 0))) set_hit(B, sv.slot, r);
+    if (maybe || (validate_op(sv.kind, sv.bits, v, n) != (sv.negate != 0))) hit_value(B, sv.slot, r, vix);
   }
 }
 
@@ -3095,14 +3278,11 @@ __device__ __forceinline__ int64_t run_chain(const DProgram& P, const DStream& S
   return cn;
 }
 
-__device__ __forceinline__ void void_request(const DBatch& B, uint32_t r) {
-  ReqHdr* H = (ReqHdr*)(B.scratch + B.layout[r].base);
-  H->pa_void = 1;
-}
 
 // Slow-list entry: the transformed bytes are copied into the slow arena.
 struct SlowEnt {
   uint32_t req, stream, flags, len;  // flags: bit0 maybe
+  uint32_t vix, _pad;                // value-map index (GI_NO_VIX: a single)
   uint64_t off;                      // byte offset in B.slow_bytes
   uint64_t fm;                       // admitting filters (global ids)
 };
@@ -3207,7 +3387,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
           cur = src;
           cn = 0;
         }
-        if (S.val_count) stream_vals(P, B, it.req, S, fm, maybe, cur, (uint32_t)cn);
+        if (S.val_count) stream_vals(P, B, it.req, meta_vix(it.meta), S, fm, maybe, cur, (uint32_t)cn);
       }
       const uint64_t c_s1 = B.prof ? clock64() : 0;
       pc_chain += c_s1 - c_s0;
@@ -3239,6 +3419,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
           e.stream = s;
           e.fm = fm;
           e.flags = maybe ? 1u : 0u;
+          e.vix = meta_vix(it.meta);
+          e._pad = 0;
           e.off = off;
           e.len = (uint32_t)cn;
           ((SlowEnt*)B.slow)[k] = e;
@@ -3288,7 +3470,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
       if (out) {
         const uint32_t i = mask_rank(om);
         uint32_t* q = B.pool + woff;
-        q[i] = it.req;
+        q[i] = base + ii;  // global item index: k_scan reaches (req, value-map index) through it on a hit
         q[nv + i] = (uint32_t)gm;
         q[2 * nv + i] = (uint32_t)(gm >> 32);
         q[3 * nv + i] = (uint32_t)cn;
@@ -3376,8 +3558,8 @@ __device__ uint64_t scan_full(const DProgram& P, const DDfa& d, const uint8_t* s
 }
 
 // Per-value path on global tables: every automaton of job J over one value.
-__device__ void scan_value_global(const DProgram& P, const DBatch& B, uint32_t r, const DJob& J, uint64_t fm,
-                                  bool maybe, const uint8_t* v, uint32_t n) {
+__device__ void scan_value_global(const DProgram& P, const DBatch& B, uint32_t r, uint32_t vix, const DJob& J,
+                                  uint64_t fm, bool maybe, const uint8_t* v, uint32_t n) {
   for (uint32_t q = 0; q < J.jdfa_count; q++) {
     const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
     uint64_t al = 0;
@@ -3388,7 +3570,7 @@ __device__ void scan_value_global(const DProgram& P, const DBatch& B, uint32_t r
     while (x) {
       const int k = __ffsll((unsigned long long)x) - 1;
       x &= x - 1;
-      set_hit(B, P.pats[jd.pat_begin + k].slot, r);
+      hit_value(B, P.pats[jd.pat_begin + k].slot, r, vix);
     }
   }
 }
@@ -3402,12 +3584,13 @@ __device__ __forceinline__ uint64_t img_allowed(const uint8_t* img, uint32_t fma
   return a;
 }
 
+// r: the queue lane's global item index
 __device__ __forceinline__ void emit_img(const DBatch& B, uint32_t r, const uint8_t* img, uint32_t slots_off,
                                          uint64_t x) {
   while (x) {
     const int k = __ffsll((unsigned long long)x) - 1;
     x &= x - 1;
-    set_hit(B, *(const uint32_t*)(img + slots_off + 4 * k), r);
+    hit_item(B, *(const uint32_t*)(img + slots_off + 4 * k), r);
   }
 }
 
@@ -3464,7 +3647,7 @@ __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B,
       req[j] = q[lane];
       fm[j] = (uint64_t)q[nv + lane] | ((uint64_t)q[2 * nv + lane] << 32);
       len[j] = q[3 * nv + lane];
-      GI_BOUND(req[j] < B.n_req && len[j] <= 4 * nw, req[j], len[j]);
+      GI_BOUND(req[j] < B.items_cap && len[j] <= 4 * nw, req[j], len[j]);  // req: global item index
       uint64_t any = 0;
       for (uint32_t k = 0; k < K; k++) any |= img_allowed(img, J.lds_fmask, nf, k, fm[j]);
       act = any != 0;
@@ -3611,48 +3794,276 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)
 }
 
 // REQUEST_BODY targets of phase-2 links (residual: the variable only exists
-// after ProcessRequestBody), tested on the speculative body of k_collect: one
-// thread per (request, link), side-effect free (transformation chain +
-// operator), a match or a chain overflow sets the link's hit bit.  k_eval
-// relies on these bits only when phase 1 ended with k_collect's processor
-// (REQUEST_BODY is then exactly the body).
-__global__ void __launch_bounds__(256) k_body(DProgram P, DBatch B) {
-  // request-major (the body stays in cache across links; the lanes of a wave
-  // walk the same link list); a link whose chain equals the previous one's
-  // reuses its output (compile.cpp orders body_links by chain)
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= B.n_req) return;
-  const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
-  if (H->spec_proc == BP_NONE || (H->flags & GI_REQ_ERROR_MASK)) return;
-  const Region g = region_of(P, B, r);
-  Tx t;
-  t.P = &P;
-  t.t0 = g.t0;
-  t.t1 = g.t1;
-  t.cap_t = g.cap_t;
-  const gi_span bs = B.reqs[r].body;
-  Str tv{nullptr, 0};
-  bool ok = true;
-  uint32_t prev_off = 0xFFFFFFFFu, prev_len = 0;
-  for (uint32_t k = 0; k < P.n_body_links; k++) {
-    const DRule R = gi_cload(P.rules, (uint64_t)P.body_links[k]);
-    const DOp o = gi_cload(P.ops, (uint64_t)R.op);
-    const uint64_t c0 = B.prof ? clock64() : 0;
-    bool same = R.tchain_len == prev_len;
-    for (uint32_t q = 0; same && q < R.tchain_len; q++)
-      same = P.tchains[R.tchain_off + q] == P.tchains[prev_off + q];
-    if (!same) {
-      t.flags = 0;
-      tv = transform(t, R, B.data + bs.off, bs.len, &ok);
-      prev_off = R.tchain_off;
-      prev_len = R.tchain_len;
+// after ProcessRequestBody), tested on the speculative body of k_collect.
+// k_eval relies on these bits only when phase 1 ended with k_collect's
+// processor (REQUEST_BODY is then exactly the body).
+//
+// One wave per body (the batch's body list, longest first).  The links come
+// ordered by transformation chain (compile.cpp); each chain runs once per body
+// and every link's operator is evaluated on its output, both split over the 64
+// lanes at "sync points" -- positions where the sequential algorithm is
+// provably in its initial state whatever came before:
+//   * a transformation stage: lane L runs the unchanged sequential
+//     transformation over [s_L, s_L+1) (s_L = the first sync point at or after
+//     L/64 of the input), writing to a 3x-scaled slot of the other buffer; a
+//     wave prefix sum of the output lengths then packs the chunks.  The
+//     concatenation equals the whole-input result because no escape sequence
+//     straddles a sync point and each chunk starts in the initial state;
+//   * an automaton: lane L steps its chunk from the state reached after a
+//     64-byte warm-up ending at s_L (started in the start state); lane L's
+//     result is exact iff its warm state equals lane L-1's exact final state
+//     (a DFA state fixes the whole future), which the wave checks lane by lane,
+//     rescanning a chunk from the exact state where it is not (rare: a pattern
+//     that remembers more than 64 bytes, e.g. "a.*b");
+//   * @validate*: each chunk evaluated independently (byte-local checks).
+// Transformations without sync points (trim, normalizePath, base64Decode,
+// digests, ...) and operators without an automaton run on lane 0 alone.
+// A chain overflow sets the chain's link bits ("maybe": k_eval evaluates).
+
+// true: transformation `code` can be split at sync points (t_sync)
+__device__ __forceinline__ bool t_chunkable(uint8_t code) {
+  switch (code) {
+    case T_LOWERCASE: case T_UTF8TOUNICODE: case T_REMOVENULLS: case T_REPLACENULLS: case T_REMOVEWHITESPACE:
+    case T_URLENCODE: case T_HEXENCODE: case T_BASE64ENCODE: case T_COMPRESSWHITESPACE: case T_CMDLINE:
+    case T_URLDECODE: case T_URLDECODEUNI: case T_JSDECODE: case T_CSSDECODE: case T_HTMLENTITYDECODE:
+      return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool no_byte_before(const uint8_t* s, uint32_t p, uint32_t w, uint8_t c) {
+  for (uint32_t k = 1; k <= w && k <= p; k++)
+    if (s[p - k] == c) return false;
+  return true;
+}
+
+// Is position p (0 < p < n) of s a sync point of transformation `code`?
+// (the sequential state at p is initial, and no escape sequence starting
+// before p reads s[p]: see the transformation's code above)
+__device__ bool t_sync(uint8_t code, const uint8_t* s, uint32_t p) {
+  const uint8_t c = s[p - 1];
+  switch (code) {
+    case T_LOWERCASE: case T_UTF8TOUNICODE: return s[p] < 0x80;  // a rune start (ASCII never continues one)
+    case T_REMOVENULLS: case T_REPLACENULLS: case T_REMOVEWHITESPACE: case T_URLENCODE: case T_HEXENCODE:
+      return true;
+    case T_BASE64ENCODE: return p % 3 == 0;
+    case T_COMPRESSWHITESPACE: return !ws_or_nbsp(c);
+    case T_CMDLINE:  // a kept character resets the pending-space state
+      return !(c == '"' || c == '\'' || c == '\\' || c == '^' || c == ' ' || c == ',' || c == ';' || c == '\t' ||
+               c == '\r' || c == '\n');
+    case T_URLDECODE: return no_byte_before(s, p, 2, '%');
+    case T_URLDECODEUNI: return no_byte_before(s, p, 5, '%');   // %uXXXX
+    case T_JSDECODE: return no_byte_before(s, p, 5, '\\');      // \uXXXX
+    case T_CSSDECODE: return no_byte_before(s, p, 7, '\\');     // \ + 6 hex + 1 space
+    case T_HTMLENTITYDECODE:  // an entity never contains '&', and ends at the first byte outside [#0-9A-Za-z]
+      return s[p] == '&' || !(isalnum_(c) || c == '#' || c == '&');
+  }
+  return false;
+}
+
+// lane's chunk [*a, *e) of s[0, n): sync points found per lane from L/64 of
+// the input (sync(p) decides); a lane without one inside its nominal range
+// gets an empty chunk and the previous lane runs through.
+template <class F>
+__device__ __forceinline__ void wave_chunks(uint32_t n, F&& sync, uint32_t* a, uint32_t* e) {
+  const uint32_t L = lane_id();
+  const uint32_t a0 = (uint32_t)((uint64_t)n * L / 64), a1 = (uint32_t)((uint64_t)n * (L + 1) / 64);
+  uint32_t sp = L == 0 ? 0u : 0xFFFFFFFFu;
+  for (uint32_t p = max(a0, 1u); L > 0 && p < a1 && sp == 0xFFFFFFFFu; p++)
+    if (sync(p)) sp = p;
+  const uint64_t valid = __ballot(sp != 0xFFFFFFFFu);
+  const uint64_t after = L == 63 ? 0ull : valid & (~0ull << (L + 1));
+  const uint32_t nxt = after ? (uint32_t)(__ffsll((unsigned long long)after) - 1) : 64u;
+  const uint32_t ne = __shfl(sp, nxt == 64 ? 0 : (int)nxt, 64);
+  *a = sp;
+  *e = sp == 0xFFFFFFFFu ? sp : (nxt == 64 ? n : ne);
+}
+
+
+// single (sticky) automaton d over s[from, to) of s[0, n) from state st;
+// returns the state (d.accept once a match completed)
+__device__ uint32_t dfa_steps(const DProgram& P, const DDfa& d, const uint8_t* s, uint32_t n, uint32_t from,
+                              uint32_t to, uint32_t st) {
+  const uint16_t* __restrict__ tr = P.trans + d.trans_off;
+  const uint8_t* __restrict__ amap = P.u8pool + d.amap_off;
+  const uint32_t ncls = d.n_classes;
+  uint32_t i = from;
+  while (i < to && st != d.accept) {
+    const uint8_t c = s[i];
+    uint32_t cls;
+    if (d.byte_mode || c < 0x80) {
+      cls = amap[c];
+      i++;
+    } else {
+      uint32_t w;
+      const uint32_t r = decode_rune(s, n, i, &w);
+      i += w;
+      cls = rune_class(P, d, r);
     }
-    const uint64_t c1 = B.prof ? clock64() : 0;
-    const bool hit = !ok || eval_op(t, o, tv.p, tv.n);
-    if (hit) set_hit(B, (uint32_t)R.hit_slot, r);
-    if (B.prof && k < 16) {  // GI_PROF: cycles per link (transform, operator)
-      atomicAdd(&B.prof[96 + 2 * k], (unsigned long long)(c1 - c0));
-      atomicAdd(&B.prof[97 + 2 * k], (unsigned long long)(clock64() - c1));
+    st = tr[st * ncls + cls];
+  }
+  return st;
+}
+
+// Exact "d matches somewhere in s[0, n)" by the whole wave (see above).
+__device__ bool wave_dfa_match(const DProgram& P, const DDfa& d, const uint8_t* s, uint32_t n) {
+  const uint32_t L = lane_id();
+  uint32_t a, e;
+  if (d.byte_mode) wave_chunks(n, [&](uint32_t) { return true; }, &a, &e);
+  else wave_chunks(n, [&](uint32_t p) { return s[p] < 0x80; }, &a, &e);
+  const bool act = a != 0xFFFFFFFFu;
+  uint32_t warm = d.start, fin = d.start;
+  if (act && a > 0) {
+    uint32_t w = a > 64 ? a - 64 : 0u;
+    if (!d.byte_mode)
+      while (w < a && s[w] >= 0x80) w++;  // a rune start (s[a] is ASCII)
+    warm = dfa_steps(P, d, s, n, w, a, d.start);
+    if (warm == d.accept) warm = 0xFFFFFFFFu;  // a warm-up match proves nothing: no guess
+  }
+  if (act && warm != 0xFFFFFFFFu) fin = dfa_steps(P, d, s, n, a, e, warm);
+  const uint64_t actm = __ballot(act);
+  // lane by lane: exact state entering each chunk
+  uint32_t ex = d.start;
+  for (uint64_t m = actm; m; m &= m - 1) {
+    const int k = __ffsll((unsigned long long)m) - 1;
+    const uint32_t gk = __shfl(warm, k, 64), fk = __shfl(fin, k, 64);
+    const uint32_t ak = __shfl(a, k, 64), ek = __shfl(e, k, 64);
+    if (gk == ex) {
+      ex = fk;
+    } else {  // mispredicted: rescan the chunk from the exact state (lane 0)
+      uint32_t x = 0;
+      if (L == 0) x = dfa_steps(P, d, s, n, ak, ek, ex);
+      ex = __shfl(x, 0, 64);
+    }
+    if (ex == d.accept) return true;
+  }
+  return P.u8pool[d.endacc_off + ex] != 0;
+}
+
+// @validate* over s[0, n) by the whole wave: chunk results OR-ed
+__device__ bool wave_validate(const DOp& o, const uint8_t* s, uint32_t n) {
+  uint32_t a, e;
+  if (o.kind == OP_VALIDATE_BYTE_RANGE) wave_chunks(n, [&](uint32_t) { return true; }, &a, &e);
+  else if (o.kind == OP_VALIDATE_URL_ENCODING) wave_chunks(n, [&](uint32_t p) { return no_byte_before(s, p, 2, '%'); }, &a, &e);
+  else wave_chunks(n, [&](uint32_t p) { return s[p] < 0x80; }, &a, &e);
+  bool r = false;
+  if (a != 0xFFFFFFFFu && e > a) r = validate_op(o.kind, o.bits, s + a, e - a);
+  return __ballot(r) != 0;
+}
+
+__global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
+  const uint32_t L = threadIdx.x;
+  for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
+    const uint32_t r = B.body_list[bi];
+    GI_BOUND(r < B.n_req, r, bi);
+    const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
+    if (H->spec_proc == BP_NONE || (H->flags & GI_REQ_ERROR_MASK)) continue;
+    const Region g = region_of(P, B, r);
+    const gi_span bs = B.reqs[r].body;
+    const uint8_t* body = B.data + bs.off;
+    const uint8_t* cur = body;
+    uint32_t cn = bs.len;
+    bool ok = true;
+    uint32_t prev_off = 0xFFFFFFFFu, prev_len = 0;
+    for (uint32_t k = 0; k < P.n_body_links; k++) {
+      const DRule R = gi_cload(P.rules, (uint64_t)P.body_links[k]);
+      const DOp o = gi_cload(P.ops, (uint64_t)R.op);
+      const uint64_t c0 = B.prof ? clock64() : 0;
+      bool same = R.tchain_len == prev_len;
+      for (uint32_t q = 0; same && q < R.tchain_len; q++)
+        same = P.tchains[R.tchain_off + q] == P.tchains[prev_off + q];
+      if (!same) {  // run this link's chain over the body
+        prev_off = R.tchain_off;
+        prev_len = R.tchain_len;
+        cur = body;
+        cn = bs.len;
+        ok = true;
+        uint32_t summ = 0;
+        {
+          uint32_t a, e;
+          wave_chunks(cn, [&](uint32_t) { return true; }, &a, &e);
+          uint32_t m = (a != 0xFFFFFFFFu && e > a) ? value_summary(cur + a, e - a) : 0u;
+          for (int q = 32; q > 0; q >>= 1) m |= (uint32_t)__shfl_xor((int)m, q, 64);
+          summ = m;
+        }
+        for (uint32_t q = 0; q < R.tchain_len && ok; q++) {
+          const uint8_t code = (uint8_t)P.tchains[R.tchain_off + q];
+          if (transform_identity(summ, code)) continue;
+          // buffers: tmp / dst are the two transformation buffers other than cur
+          uint8_t* tmp = cur == g.t1 ? g.t0 : g.t1;
+          uint8_t* dst = cur == body ? g.t0 : (uint8_t*)cur;
+          if (dst == tmp) dst = tmp == g.t0 ? g.t1 : g.t0;
+          int64_t outn = -1;
+          if (t_chunkable(code) && 3ull * cn + 8 * 64 <= g.cap_t) {
+            const uint8_t* src = cur;
+            uint32_t a, e;
+            wave_chunks(cn, [&](uint32_t p) { return t_sync(code, src, p); }, &a, &e);
+            const bool act = a != 0xFFFFFFFFu && e > a;
+            uint8_t* lt = tmp + 3ull * (act ? a : 0u) + 8u * L;
+            int64_t m = act ? apply_transform(P, code, src + a, e - a, lt, 3 * (e - a) + 8) : 0;
+            uint32_t tot = 0, o0 = 0;
+            if (__ballot(m < 0) == 0) o0 = wave_excl_sum((uint32_t)m, &tot);
+            const bool bad = __ballot(m < 0) != 0 || tot > g.cap_t;
+            if (!bad) {
+              __syncthreads();  // tmp written; dst (possibly the source) is free
+              uint32_t sm = 0;
+              for (uint32_t i = 0; i < (uint32_t)m; i++) {
+                dst[o0 + i] = lt[i];
+                sm |= byte_summary(lt[i]);
+              }
+              for (int x = 32; x > 0; x >>= 1) sm |= (uint32_t)__shfl_xor((int)sm, x, 64);
+              summ = sm;
+              __syncthreads();
+              outn = tot;
+              cur = dst;
+            }
+          } else {  // sequential on lane 0
+            int m = 0;
+            if (L == 0) m = (int)max(apply_transform(P, code, cur, cn, tmp, g.cap_t), (int64_t)-1);
+            m = __shfl(m, 0, 64);
+            __syncthreads();
+            if (m >= 0) {
+              outn = m;
+              cur = tmp;
+              uint32_t a, e;
+              wave_chunks((uint32_t)m, [&](uint32_t) { return true; }, &a, &e);
+              uint32_t sm = (a != 0xFFFFFFFFu && e > a) ? value_summary(cur + a, e - a) : 0u;
+              for (int x = 32; x > 0; x >>= 1) sm |= (uint32_t)__shfl_xor((int)sm, x, 64);
+              summ = sm;
+            }
+          }
+          if (outn < 0) ok = false;
+          else cn = (uint32_t)outn;
+        }
+      }
+      const uint64_t c1 = B.prof ? clock64() : 0;
+      bool hit;
+      if (!ok) {
+        hit = true;  // chain overflow: maybe
+      } else if ((o.kind == OP_RX || o.kind == OP_PM || (o.kind == OP_CONTAINS && o.arg_is_lit)) && o.nfa < 0 &&
+                 o.dfa >= 0 && !P.dfas[o.dfa].multi) {
+        const DDfa d = P.dfas[o.dfa];
+        hit = wave_dfa_match(P, d, cur, cn) != (o.negate != 0);
+      } else if (o.kind == OP_VALIDATE_BYTE_RANGE || o.kind == OP_VALIDATE_URL_ENCODING || o.kind == OP_VALIDATE_UTF8) {
+        hit = wave_validate(o, cur, cn) != (o.negate != 0);
+      } else {  // any other operator: lane 0, side-effect free
+        bool h = false;
+        if (L == 0) {
+          Tx t;
+          t.P = &P;
+          t.t0 = g.t0;
+          t.t1 = g.t1;
+          t.cap_t = g.cap_t;
+          t.flags = 0;
+          h = eval_op(t, o, cur, cn);
+        }
+        hit = __shfl((int)h, 0, 64) != 0;
+      }
+      if (hit && L == 0) set_hit(B, (uint32_t)R.hit_slot, r);
+      if (B.prof && k < 16 && L == 0) {  // GI_PROF: cycles per link (transform, operator), per body
+        atomicAdd(&B.prof[96 + 2 * k], (unsigned long long)(c1 - c0));
+        atomicAdd(&B.prof[97 + 2 * k], (unsigned long long)(clock64() - c1));
+      }
     }
   }
 }
@@ -3666,7 +4077,7 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
     GI_BOUND(x.req < B.n_req && x.stream < P.n_streams && x.off + x.len <= B.slow_bytes_cap, x.req, x.stream);
     const DStream S = P.streams[x.stream];
     for (uint32_t j = S.job_begin; j < S.job_begin + S.job_count; j++)
-      scan_value_global(P, B, x.req, P.jobs[j], x.fm, (x.flags & 1) != 0, B.slow_bytes + x.off, x.len);
+      scan_value_global(P, B, x.req, x.vix, P.jobs[j], x.fm, (x.flags & 1) != 0, B.slow_bytes + x.off, x.len);
   }
 }
 
@@ -3691,6 +4102,8 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
     t.prof_rule_cyc = B.prof ? B.prof + 128 : nullptr;
     tx_bind(t, P, g);
     t.hits = B.hits;
+    t.vmap = B.vmap + (B.layout[r].vmap_bit >> 5);
+    t.nf_pa = H->nf;
     t.n_req = B.n_req;
     t.req = r;
     t.slots = B.txslots + r;
@@ -3752,6 +4165,7 @@ __global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
               t.single[S_REQUEST_BODY] = {D + rq.body.off, bn};
               if (t.body_proc == H->spec_proc) {
                 t.nf += H->n_post;  // k_collect's fields, already in phase A
+                t.nf_pa = t.nf;
                 t.body_spec = true;
               } else {
                 const uint32_t nf0 = t.nf;
@@ -3939,6 +4353,8 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
   }
   const uint32_t cb = (B.n_req + 255) / 256;
   GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
+  if (B.n_body && P.body_access)
+    GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (P.n_streams) {
     GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(1), dim3(1024), 0, stream, B, cb);
@@ -3963,9 +4379,9 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
       GI_LAUNCH("k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
                 S.n_global, S.mode, 2u);
     GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
-    // one wave per workgroup: a body batch (C3: 25k POSTs of 50k) has too few
-    // requests to fill 256 CUs with 4-wave workgroups
-    if (P.n_body_links) GI_LAUNCH("k_body", k_body, dim3((B.n_req + 63) / 64), dim3(64), 0, stream, P, B);
+    // one wave (workgroup) per body
+    if (P.n_body_links && B.n_body)
+      GI_LAUNCH("k_body", k_body, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
   } else if (ev) {
     (void)hipEventRecord(ev[1], stream);
   }

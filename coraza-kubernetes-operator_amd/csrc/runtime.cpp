@@ -80,7 +80,7 @@ struct gi_ctx {
   DProgram prog{};
   std::vector<DevBuf> pbufs;
   // batch buffers
-  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, tally_ext, hits, joblist, txslots;
+  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, tally_ext, hits, vmap, blist, joblist, txslots;
   DevBuf tally_idbuf;                  // distinct rule ids, ascending (k_tally bins)
   std::vector<uint32_t> tally_ids;
   // phase A
@@ -92,6 +92,8 @@ struct gi_ctx {
   int stop_after = 0;  // debugging: launch only the first N pipeline kernels, synchronising after each
   ScanLaunch scan{};
   uint32_t hit_words = 0;
+  uint64_t vmap_words = 0;  // value map (DBatch.vmap)
+  uint32_t n_body = 0;      // requests with a body (DBatch.body_list)
   hipEvent_t evs[3] = {nullptr, nullptr, nullptr};
   LaunchLog log{};
   uint64_t raw_nobody = 0, raw_all = 0;  // batch bytes (algorithmic-byte accounting)
@@ -121,6 +123,7 @@ static void fill_info(gi_ruleset* rs) {
   rs->info.n_scan_streams = (uint32_t)P.streams.size();
   rs->info.n_hit_slots = P.n_hit_slots;
   rs->info.n_union_dfas = P.n_union_dfas;
+  rs->info.n_nfas = (uint32_t)P.nfas.size();
   rs->info.program_bytes = P.rules.size() * sizeof(DRule) + P.vars.size() * sizeof(DVarRef) +
                            P.ops.size() * sizeof(DOp) + P.acts.size() * sizeof(DAction) +
                            P.trans.size() * 2 + P.u8pool.size() + P.nranges.size() * 4 + P.strpool.size() +
@@ -441,7 +444,7 @@ void gi_ctx_free(gi_ctx* c) {
   for (auto& b : c->pbufs) b.release();
   c->prof.release();
   for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
-                    &c->hits, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->lscratch, &c->pool, &c->qblk,
+                    &c->hits, &c->vmap, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes})
     b->release();
   for (auto& ev : c->evs)
@@ -466,7 +469,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   const uint32_t n = in->n_req;
   // validate spans and lay out per-request scratch (lengths only)
   std::vector<ReqLayout> lay(n);
-  uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0;
+  uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0, vmap_bits = 0;
   uint32_t max_cap_t = 64;
   const uint32_t nslots = c->rs->prog.n_slots;
   const Program& PG = c->rs->prog;
@@ -521,7 +524,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       // transient allocation <= that again + n, parser stack 1048 B
       if (k < q.body.len && (bd[k] == '{' || bd[k] == '[')) cap_b += 8ull * q.body.len + 4200;
     }
-    uint64_t cap_t = 3 * maxv + 64;
+    uint64_t cap_t = 3 * maxv + 64 + (q.body.len ? 8 * 64 : 0);  // k_body: 64 lane slots of 3x + 8 B
     uint64_t cap_mt = 2 * maxv + 512;
     if (cap_f > 0xFFFFFFFFull || cap_b > 0xFFFFFFFFull || cap_t > 0xFFFFFFFFull || cap_mt > 0xFFFFFFFFull)
       return fail(c, GI_EINVAL, "request too large");
@@ -534,8 +537,9 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     raw_body += q.body.len;
     max_cap_t = (uint32_t)std::max<uint64_t>(max_cap_t, cap_t);
     ReqLayout& L = lay[r];
-    L.pa_base = 0;
-    L.pa_cap = 0;
+    L.vmap_bit = vmap_bits;
+    L.vmap_bits = (uint32_t)(2 * cap_f);
+    vmap_bits += (2 * cap_f + 31) & ~31ull;
     L._pad = 0;
     L.base = off;
     L.cap_f = (uint32_t)cap_f;
@@ -569,6 +573,16 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if ((e = c->txslots.ensure(std::max<uint64_t>(24ull * PG.n_slots * n, 64))) != hipSuccess)
     return hip_fail(c, e, "alloc tx slots");
   c->hit_words = (PG.n_hit_slots + 31) / 32;
+  c->vmap_words = vmap_bits / 32;
+  // k_body's work list: requests with a body, longest first (one wave each)
+  std::vector<uint32_t> blist;
+  for (uint32_t r = 0; r < n; r++)
+    if (in->reqs[r].body.len) blist.push_back(r);
+  std::stable_sort(blist.begin(), blist.end(),
+                   [&](uint32_t x, uint32_t y) { return in->reqs[x].body.len > in->reqs[y].body.len; });
+  c->n_body = (uint32_t)blist.size();
+  if ((e = upload(&c->blist, blist, s)) != hipSuccess) return hip_fail(c, e, "alloc body list");
+  if ((e = c->vmap.ensure(std::max<uint64_t>(4 * c->vmap_words, 16))) != hipSuccess) return hip_fail(c, e, "alloc value map");
   if ((e = c->hits.ensure(std::max<size_t>((size_t)c->hit_words * n * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc hits");
   if (!PG.streams.empty()) {
@@ -598,7 +612,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if ((e = c->qblk.ensure(8ull * ns * c->qcap)) != hipSuccess) return hip_fail(c, e, "alloc queue blocks");
     if ((e = c->ctr.ensure(160 + 8 * 16)) != hipSuccess) return hip_fail(c, e, "alloc counters");
     (void)ns;
-    if ((e = c->slow.ensure(32ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
+    if ((e = c->slow.ensure(40ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
   }
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
@@ -641,6 +655,9 @@ int gi_run_staged(gi_ctx* c) {
   B.tally = (unsigned long long*)c->tally.p;
   B.tally_ext = (uint32_t*)c->tally_ext.p;
   B.hits = (uint32_t*)c->hits.p;
+  B.vmap = (uint32_t*)c->vmap.p;
+  B.body_list = (const uint32_t*)c->blist.p;
+  B.n_body = c->n_body;
   B.txslots = (Slot*)c->txslots.p;
   {
     // counters (bytes): [0] pool words used, [8] slow bytes used, [16] slow
@@ -684,6 +701,10 @@ int gi_run_staged(gi_ctx* c) {
   if (c->hit_words) {
     e = hipMemsetAsync(c->hits.p, 0, (size_t)c->hit_words * c->n_req * 4, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "memset hits");
+  }
+  if (c->vmap_words) {
+    e = hipMemsetAsync(c->vmap.p, 0, 4 * c->vmap_words, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "memset value map");
   }
   launch_pipeline(c->prog, B, c->scan, c->stream, c->evs, c->stop_after, &c->log,
                   (const uint32_t*)c->tally_idbuf.p, (uint32_t)c->tally_ids.size());
@@ -735,6 +756,7 @@ int gi_sync(gi_ctx* c) {
       else if (nm == "k_scan_hbm") ab = 4ull * acct[12];
       else if (nm == "k_scan_slow") ab = slow_bytes;
       else if (nm == "k_body") ab = c->raw_all - c->raw_nobody;  // request bodies
+      else if (nm == "k_bparse") ab = c->raw_all - c->raw_nobody;
       else if (nm == "k_eval") ab = c->raw_all + (uint64_t)sizeof(gi_verdict) * c->n_req + 4ull * tl.matched_total;
       c->stats.launch_alg_bytes[k] = ab;
       c->stats.launch_steps[k] = nm == "k_scan" ? acct[13] : nm == "k_scan_big" ? acct[14] : nm == "k_scan_hbm" ? acct[15] : 0;

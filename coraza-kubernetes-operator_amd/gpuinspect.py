@@ -92,7 +92,7 @@ class _Info(ctypes.Structure):
     _fields_ = [("n_rules", ctypes.c_uint32), ("n_links", ctypes.c_uint32), ("n_dfas", ctypes.c_uint32),
                 ("n_tx_slots", ctypes.c_uint32), ("program_bytes", ctypes.c_uint64),
                 ("n_scan_jobs", ctypes.c_uint32), ("n_hit_slots", ctypes.c_uint32),
-                ("n_union_dfas", ctypes.c_uint32), ("n_scan_streams", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
+                ("n_union_dfas", ctypes.c_uint32), ("n_scan_streams", ctypes.c_uint32), ("n_nfas", ctypes.c_uint32),
                 ("source_digest", ctypes.c_uint64)]
 
 
@@ -119,8 +119,8 @@ class _Stats(ctypes.Structure):
                 ("last_eval_ms", ctypes.c_double), ("last_stream_ms", ctypes.c_double),
                 ("last_pa_bytes", ctypes.c_uint64), ("diag", ctypes.c_uint64 * 8),
                 ("n_launches", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
-                ("launch_ms", ctypes.c_double * 16), ("launch_alg_bytes", ctypes.c_uint64 * 16),
-                ("launch_name", (ctypes.c_char * 16) * 16), ("launch_steps", ctypes.c_uint64 * 16)]
+                ("launch_ms", ctypes.c_double * 24), ("launch_alg_bytes", ctypes.c_uint64 * 24),
+                ("launch_name", (ctypes.c_char * 16) * 24), ("launch_steps", ctypes.c_uint64 * 24)]
 
 
 _LIB = None

@@ -44,6 +44,7 @@ extern "C" {
 #define GI_EPARSE -1       /* SecLang syntax error (coraza.NewWAF error) */
 #define GI_EUNSUPPORTED -2 /* valid SecLang this engine does not implement */
 #define GI_EINVAL -3
+#define GI_STATS_LAUNCHES 24 /* gi_stats per-launch records */
 #define GI_ENODEV -4       /* no HIP device / kernel launch failure */
 #define GI_ENOMEM -5
 #define GI_ETRUNC -6       /* caller-provided result capacity too small */
@@ -97,7 +98,7 @@ typedef struct {
   uint32_t n_hit_slots;   /* rule links evaluated data-parallel in phase A */
   uint32_t n_union_dfas;  /* multi-pattern automata among n_dfas */
   uint32_t n_scan_streams; /* phase-A streams (value source x transformation chain) */
-  uint32_t _pad;
+  uint32_t n_nfas;        /* @rx operators matched by NFA position tables (DFA over the state cap) */
   uint64_t source_digest;  /* FNV-1a 64 of the SecLang text + export list the ruleset was compiled from */
 } gi_ruleset_info;
 
@@ -185,10 +186,10 @@ typedef struct {
   uint64_t diag[8];        /* diagnostic counters of the last batch (GI_DIAG=1) */
   uint32_t n_launches;     /* kernel launches of the last pipeline run */
   uint32_t _pad;
-  double launch_ms[16];    /* HIP-event time of each launch */
-  uint64_t launch_alg_bytes[16]; /* algorithmic bytes each launch must move */
-  char launch_name[16][16];
-  uint64_t launch_steps[16];     /* automaton byte-steps of each k_scan launch (secondary bound) */
+  double launch_ms[GI_STATS_LAUNCHES];    /* HIP-event time of each launch */
+  uint64_t launch_alg_bytes[GI_STATS_LAUNCHES]; /* algorithmic bytes each launch must move */
+  char launch_name[GI_STATS_LAUNCHES][16];
+  uint64_t launch_steps[GI_STATS_LAUNCHES];     /* automaton byte-steps of each k_scan launch (secondary bound) */
 } gi_stats;
 
 /* ------------------------------------------------------------ compile */
