@@ -124,10 +124,11 @@ struct NfaBuilder {
         int sub = n.kids[0];
         if (n.max == -1) {
           if (n.min == 0) return star(compile(sub));
-          Frag f = compile(sub);
-          for (int k = 1; k < n.min; k++) f = cat(std::move(f), compile(sub));
+          // x{m,} = x{m-1} x+
           Frag last = plus(compile(sub));
           if (n.min == 1) return last;
+          Frag f = compile(sub);
+          for (int k = 1; k < n.min - 1; k++) f = cat(std::move(f), compile(sub));
           return cat(std::move(f), std::move(last));
         }
         if (n.max == 0) return nop();

@@ -46,6 +46,7 @@ struct DBatch {
   uint32_t* boffs;            // [k_collect blocks][GI_NB] item offsets
   uint32_t* ibk;              // [GI_NB] (base, count), [GI_NB] item-wave base, total item waves
   void* items;                // Item[items_cap]
+  uint64_t* igm;              // [items_cap] global filters admitting each item (k_stream -> k_scan)
   uint8_t* lscratch;          // per-lane HBM transformation buffers (2 x lcap per k_stream lane)
   uint32_t lcap;
   uint32_t* pool;             // queue-block words

@@ -2754,6 +2754,7 @@ __device__ __forceinline__ void void_request(const DBatch& B, uint32_t r) {
 // qblk entry {pool word offset, nv | nw << 8 | shared}: shared = the block was
 // written for an earlier stream of the same item-wave (raw item bytes)
 #define GI_QB_SHARED 0x80000000u
+#define GI_QB_HDR 2  // lane header words of a queue block: global item index, value length
 #define GI_QB_NW_MASK 0x7FFFFFu
 __device__ __forceinline__ uint32_t item_bucket(uint32_t n) {
   return n <= 16 ? 0u : n <= 32 ? 1u : n <= 64 ? 2u : n <= 128 ? 3u : 4u;
@@ -3344,6 +3345,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
       it = ((const Item*)B.items)[base + ii];
       GI_BOUND(it.req < B.n_req, it.req, ii);
       gm = item_gmask(P, it);
+      B.igm[base + ii] = gm;  // k_scan's per-lane filter mask (the queue lanes carry the item index)
       src = it.vp;
       if (IN) {  // stage the scanned bytes once for all streams (bucket: vn <= IN), a word at a time
         const uint32_t n = min(it.vn, IN);
@@ -3443,9 +3445,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
         continue;
       }
       // blocks start on 16-byte cells: qblk holds the cell index (64 GB of pool)
-      const uint64_t words = ((uint64_t)nv * (4 + nw) + 3) & ~3ull;
+      const uint64_t words = ((uint64_t)nv * (GI_QB_HDR + nw) + 3) & ~3ull;
       unsigned long long woff = 0;
-      wwords += (uint64_t)nv * (4 + nw);
+      wwords += (uint64_t)nv * (GI_QB_HDR + nw);
       if (lane == 0) {
         if (pnext + words > pend) {
           const unsigned long long sz = words > GI_PCHUNK ? words : (unsigned long long)GI_PCHUNK;
@@ -3470,16 +3472,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
       if (out) {
         const uint32_t i = mask_rank(om);
         uint32_t* q = B.pool + woff;
-        q[i] = base + ii;  // global item index: k_scan reaches (req, value-map index) through it on a hit
-        q[nv + i] = (uint32_t)gm;
-        q[2 * nv + i] = (uint32_t)(gm >> 32);
-        q[3 * nv + i] = (uint32_t)cn;
+        q[i] = base + ii;  // global item index: k_scan reaches the filter mask (B.igm) and, on a hit,
+                           // (req, value-map index) through it
+        q[nv + i] = (uint32_t)cn;
         const uint32_t nwi = ((uint32_t)cn + 3) / 4;
         if (IN && !glob) {  // cur is a lane buffer in LDS (dword-aligned): a word per read
           for (uint32_t w = 0; w < nwi; w++) {
             uint32_t x = ((const uint32_t*)cur)[w];
             if (4 * w + 4 > (uint32_t)cn) x &= (1u << (8 * ((uint32_t)cn - 4 * w))) - 1u;
-            q[4 * nv + (uint64_t)w * nv + i] = x;
+            q[GI_QB_HDR * nv + (uint64_t)w * nv + i] = x;
           }
         } else {
           for (uint32_t w = 0; w < nwi; w++) {
@@ -3488,7 +3489,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
               const uint32_t at = 4 * w + b;
               x |= (at < (uint32_t)cn ? (uint32_t)cur[at] : 0u) << (8 * b);
             }
-            q[4 * nv + (uint64_t)w * nv + i] = x;
+            q[GI_QB_HDR * nv + (uint64_t)w * nv + i] = x;
           }
         }
       }
@@ -3637,7 +3638,7 @@ __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B,
   for (uint32_t j = 0; j < NB; j++) {
     const uint64_t woff = (uint64_t)d[j].x << 2;
     const uint32_t nv = d[j].y & 0xFFu, nw = (d[j].y >> 8) & GI_QB_NW_MASK;
-    GI_BOUND(nv <= 64 && woff + (uint64_t)(4 + nw) * nv <= B.pool_cap, d[j].x, d[j].y);
+    GI_BOUND(nv <= 64 && woff + (uint64_t)(GI_QB_HDR + nw) * nv <= B.pool_cap, d[j].x, d[j].y);
     const uint32_t* q = B.pool + woff;
     req[j] = 0;
     len[j] = 0;
@@ -3645,8 +3646,9 @@ __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B,
     bool act = false;
     if (lane < nv) {
       req[j] = q[lane];
-      fm[j] = (uint64_t)q[nv + lane] | ((uint64_t)q[2 * nv + lane] << 32);
-      len[j] = q[3 * nv + lane];
+      GI_BOUND(req[j] < B.items_cap, req[j], 0u);
+      fm[j] = B.igm[req[j]];
+      len[j] = q[nv + lane];
       GI_BOUND(req[j] < B.items_cap && len[j] <= 4 * nw, req[j], len[j]);  // req: global item index
       uint64_t any = 0;
       for (uint32_t k = 0; k < K; k++) any |= img_allowed(img, J.lds_fmask, nf, k, fm[j]);
@@ -3656,7 +3658,7 @@ __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B,
     nwl[j] = (act && !(mode & 4)) ? (len[j] + 3) / 4 : 0u;
     if (!act) len[j] = 0xFFFFFFFFu;  // marks an idle lane (no value_end)
     nwmax = max(nwmax, nw);
-    wp[j] = q + 4 * nv + lane;
+    wp[j] = q + GI_QB_HDR * nv + lane;
     // this lane's words, loaded two ahead of the automaton steps
     p0[j] = nwl[j] > 0 ? wp[j][0] : 0u;
     p1[j] = nwl[j] > 1 ? wp[j][nv] : 0u;
@@ -3781,7 +3783,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)
 #pragma unroll
       for (uint32_t j = 0; j < 2; j++) {
         const uint32_t dnw = (d[j].y >> 8) & GI_QB_NW_MASK;
-        const uint64_t w = (uint64_t)(d[j].y & 0xFFu) * (4 + dnw);
+        const uint64_t w = (uint64_t)(d[j].y & 0xFFu) * (GI_QB_HDR + dnw);
         rwords += (first && !(d[j].y & GI_QB_SHARED)) ? w : 0;  // a shared block is counted at its writer
         rsteps += (uint64_t)(d[j].y & 0xFFu) * dnw * 4 * K;
       }
@@ -3881,15 +3883,22 @@ __device__ __forceinline__ void wave_chunks(uint32_t n, F&& sync, uint32_t* a, u
 
 
 // single (sticky) automaton d over s[from, to) of s[0, n) from state st;
-// returns the state (d.accept once a match completed)
-__device__ uint32_t dfa_steps(const DProgram& P, const DDfa& d, const uint8_t* s, uint32_t n, uint32_t from,
-                              uint32_t to, uint32_t st) {
-  const uint16_t* __restrict__ tr = P.trans + d.trans_off;
-  const uint8_t* __restrict__ amap = P.u8pool + d.amap_off;
+// returns the state (d.accept once a match completed).  tr / amap: the
+// transition table and ASCII class map (LDS copies when they fit); the text
+// is read a word at a time.
+__device__ __forceinline__ uint32_t dfa_steps(const DProgram& P, const DDfa& d, const uint16_t* __restrict__ tr,
+                                              const uint8_t* __restrict__ amap, const uint8_t* s, uint32_t n,
+                                              uint32_t from, uint32_t to, uint32_t st) {
   const uint32_t ncls = d.n_classes;
   uint32_t i = from;
+  uint32_t win = 0, wbeg = 0, wend = 0;
   while (i < to && st != d.accept) {
-    const uint8_t c = s[i];
+    if (i >= wend) {
+      win = load_u32u(s + i);
+      wbeg = i;
+      wend = i + 4;
+    }
+    const uint8_t c = (uint8_t)(win >> (8 * (i - wbeg)));
     uint32_t cls;
     if (d.byte_mode || c < 0x80) {
       cls = amap[c];
@@ -3905,9 +3914,24 @@ __device__ uint32_t dfa_steps(const DProgram& P, const DDfa& d, const uint8_t* s
   return st;
 }
 
+#define GI_BODY_LDS 16384  // k_body's LDS automaton slot (bytes): 8 one-wave workgroups per CU
+
 // Exact "d matches somewhere in s[0, n)" by the whole wave (see above).
-__device__ bool wave_dfa_match(const DProgram& P, const DDfa& d, const uint8_t* s, uint32_t n) {
+// lds: GI_BODY_LDS bytes of the workgroup's LDS for the automaton tables.
+__device__ bool wave_dfa_match(const DProgram& P, const DDfa& d, const uint8_t* s, uint32_t n, uint8_t* lds) {
   const uint32_t L = lane_id();
+  const uint32_t tb = d.n_states * d.n_classes * 2, ab = d.byte_mode ? 256u : 128u;
+  const bool in_lds = tb + ab <= GI_BODY_LDS;
+  const uint16_t* tr = P.trans + d.trans_off;
+  const uint8_t* amap = P.u8pool + d.amap_off;
+  if (in_lds) {
+    __syncthreads();  // the previous link's tables are no longer read
+    for (uint32_t k = L; k < tb / 2; k += 64) ((uint16_t*)lds)[k] = tr[k];
+    for (uint32_t k = L; k < ab; k += 64) lds[tb + k] = amap[k];
+    __syncthreads();
+    tr = (const uint16_t*)lds;
+    amap = lds + tb;
+  }
   uint32_t a, e;
   if (d.byte_mode) wave_chunks(n, [&](uint32_t) { return true; }, &a, &e);
   else wave_chunks(n, [&](uint32_t p) { return s[p] < 0x80; }, &a, &e);
@@ -3917,10 +3941,10 @@ __device__ bool wave_dfa_match(const DProgram& P, const DDfa& d, const uint8_t* 
     uint32_t w = a > 64 ? a - 64 : 0u;
     if (!d.byte_mode)
       while (w < a && s[w] >= 0x80) w++;  // a rune start (s[a] is ASCII)
-    warm = dfa_steps(P, d, s, n, w, a, d.start);
+    warm = dfa_steps(P, d, tr, amap, s, n, w, a, d.start);
     if (warm == d.accept) warm = 0xFFFFFFFFu;  // a warm-up match proves nothing: no guess
   }
-  if (act && warm != 0xFFFFFFFFu) fin = dfa_steps(P, d, s, n, a, e, warm);
+  if (act && warm != 0xFFFFFFFFu) fin = dfa_steps(P, d, tr, amap, s, n, a, e, warm);
   const uint64_t actm = __ballot(act);
   // lane by lane: exact state entering each chunk
   uint32_t ex = d.start;
@@ -3932,7 +3956,7 @@ __device__ bool wave_dfa_match(const DProgram& P, const DDfa& d, const uint8_t* 
       ex = fk;
     } else {  // mispredicted: rescan the chunk from the exact state (lane 0)
       uint32_t x = 0;
-      if (L == 0) x = dfa_steps(P, d, s, n, ak, ek, ex);
+      if (L == 0) x = dfa_steps(P, d, tr, amap, s, n, ak, ek, ex);
       ex = __shfl(x, 0, 64);
     }
     if (ex == d.accept) return true;
@@ -3952,6 +3976,7 @@ __device__ bool wave_validate(const DOp& o, const uint8_t* s, uint32_t n) {
 }
 
 __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
+  __shared__ __attribute__((aligned(16))) uint8_t kb_lds[GI_BODY_LDS];
   const uint32_t L = threadIdx.x;
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
     const uint32_t r = B.body_list[bi];
@@ -4000,17 +4025,14 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
             wave_chunks(cn, [&](uint32_t p) { return t_sync(code, src, p); }, &a, &e);
             const bool act = a != 0xFFFFFFFFu && e > a;
             uint8_t* lt = tmp + 3ull * (act ? a : 0u) + 8u * L;
-            int64_t m = act ? apply_transform(P, code, src + a, e - a, lt, 3 * (e - a) + 8) : 0;
+            int64_t m = act ? apply_transform_inl(P, code, src + a, e - a, lt, 3 * (e - a) + 8) : 0;
             uint32_t tot = 0, o0 = 0;
             if (__ballot(m < 0) == 0) o0 = wave_excl_sum((uint32_t)m, &tot);
             const bool bad = __ballot(m < 0) != 0 || tot > g.cap_t;
             if (!bad) {
               __syncthreads();  // tmp written; dst (possibly the source) is free
-              uint32_t sm = 0;
-              for (uint32_t i = 0; i < (uint32_t)m; i++) {
-                dst[o0 + i] = lt[i];
-                sm |= byte_summary(lt[i]);
-              }
+              uint32_t sm = m > 0 ? value_summary(lt, (uint32_t)m) : 0u;
+              for (uint32_t i = 0; i < (uint32_t)m; i++) dst[o0 + i] = lt[i];
               for (int x = 32; x > 0; x >>= 1) sm |= (uint32_t)__shfl_xor((int)sm, x, 64);
               summ = sm;
               __syncthreads();
@@ -4043,7 +4065,7 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
       } else if ((o.kind == OP_RX || o.kind == OP_PM || (o.kind == OP_CONTAINS && o.arg_is_lit)) && o.nfa < 0 &&
                  o.dfa >= 0 && !P.dfas[o.dfa].multi) {
         const DDfa d = P.dfas[o.dfa];
-        hit = wave_dfa_match(P, d, cur, cn) != (o.negate != 0);
+        hit = wave_dfa_match(P, d, cur, cn, kb_lds) != (o.negate != 0);
       } else if (o.kind == OP_VALIDATE_BYTE_RANGE || o.kind == OP_VALIDATE_URL_ENCODING || o.kind == OP_VALIDATE_UTF8) {
         hit = wave_validate(o, cur, cn) != (o.negate != 0);
       } else {  // any other operator: lane 0, side-effect free
@@ -4084,7 +4106,10 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
 // ------------------------------------------------ stage 3: k_eval (phase B)
 // RuleGroup.Eval(1) -> ProcessRequestBody -> RuleGroup.Eval(2) per request,
 // skipping every phase-A rule whose hit bit is clear.
-__global__ void __launch_bounds__(128) k_eval(DProgram P, DBatch B) {
+#ifndef GI_EVAL_WPE
+#define GI_EVAL_WPE 2  // minimum waves per SIMD k_eval is compiled for (register budget; A/B: 2 beats 1 and 4)
+#endif
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVAL_WPE, 8))) k_eval(DProgram P, DBatch B) {
   __shared__ unsigned long long red[7];
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (threadIdx.x < 7) red[threadIdx.x] = 0;
@@ -4379,12 +4404,13 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
       GI_LAUNCH("k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
                 S.n_global, S.mode, 2u);
     GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
-    // one wave (workgroup) per body
-    if (P.n_body_links && B.n_body)
-      GI_LAUNCH("k_body", k_body, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
   } else if (ev) {
     (void)hipEventRecord(ev[1], stream);
   }
+  // REQUEST_BODY links (a ruleset may have them without any phase-A stream):
+  // one wave (workgroup) per body
+  if (P.n_body_links && B.n_body)
+    GI_LAUNCH("k_body", k_body, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[2], stream);
   {  // small batches (fewer than 4 workgroups of 128 per CU): one wave per workgroup to spread over all CUs
     const uint32_t ev_bs = (B.n_req + 127) / 128 < 1024 ? 64u : 128u;

@@ -84,7 +84,7 @@ struct gi_ctx {
   DevBuf tally_idbuf;                  // distinct rule ids, ascending (k_tally bins)
   std::vector<uint32_t> tally_ids;
   // phase A
-  DevBuf bcounts, boffs, items, lscratch, pool, qblk, ctr, slow, slow_bytes;
+  DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0;
   uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0;
   bool diag_on = false, prof_on = false;
@@ -133,6 +133,24 @@ static void fill_info(gi_ruleset* rs) {
                            P.jdfas.size() * sizeof(DJobDfa) + P.pats.size() * sizeof(DPat) +
                            P.svals.size() * sizeof(DScanVal) + P.images.size();
   rs->info.source_digest = P.source_digest;
+  if (getenv("GI_PLAN")) {  // diagnostics: the phase-A plan (streams -> jobs -> images)
+    for (const DRule& R : P.rules)
+      if (R.op >= 0 && P.ops[R.op].nfa >= 0) {
+        const DNfa& N = P.nfas[P.ops[R.op].nfa];
+        fprintf(stderr, "rule %d: NFA tables %d (dfa %d) pos %u words %u classes %u nr %u\n", R.id, P.ops[R.op].nfa,
+                P.ops[R.op].dfa, N.n_pos, N.words, N.n_classes, N.nr_cnt);
+      }
+    for (size_t k = 0; k < P.streams.size(); k++) {
+      const DStream& S = P.streams[k];
+      fprintf(stderr, "stream %zu chain", k);
+      for (uint32_t q = 0; q < S.tchain_len; q++) fprintf(stderr, " %u", (unsigned)P.tchains[S.tchain_off + q]);
+      fprintf(stderr, " | filters %u vals %u kinds %x:", S.filt_count, S.val_count, S.kind_mask);
+      for (uint32_t j = S.job_begin; j < S.job_begin + S.job_count; j++)
+        fprintf(stderr, " job%u(%u dfa, %u B%s%s)", j, P.jobs[j].jdfa_count, P.jobs[j].img_bytes, P.jobs[j].lds ? "" : " hbm",
+                P.jobs[j].big ? " big" : "");
+      fprintf(stderr, "\n");
+    }
+  }
 }
 
 int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ruleset** out, char* err,
@@ -444,7 +462,7 @@ void gi_ctx_free(gi_ctx* c) {
   for (auto& b : c->pbufs) b.release();
   c->prof.release();
   for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
-                    &c->hits, &c->vmap, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->lscratch, &c->pool, &c->qblk,
+                    &c->hits, &c->vmap, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes})
     b->release();
   for (auto& ev : c->evs)
@@ -606,6 +624,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if ((e = c->bcounts.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc bcounts");
     if ((e = c->boffs.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc boffs");
     if ((e = c->items.ensure(32ull * c->items_cap)) != hipSuccess) return hip_fail(c, e, "alloc items");
+    if ((e = c->igm.ensure(8ull * c->items_cap)) != hipSuccess) return hip_fail(c, e, "alloc item filter masks");
     if ((e = c->lscratch.ensure((uint64_t)GI_STREAM_GRID * 64 * 2 * c->lcap + 64)) != hipSuccess)
       return hip_fail(c, e, "alloc lane scratch");
     if ((e = c->pool.ensure(4ull * c->pool_cap)) != hipSuccess) return hip_fail(c, e, "alloc queue pool");
@@ -669,6 +688,7 @@ int gi_run_staged(gi_ctx* c) {
     B.boffs = (uint32_t*)c->boffs.p;
     B.ibk = (uint32_t*)(cp + 64);
     B.items = c->items.p;
+    B.igm = (uint64_t*)c->igm.p;
     B.lscratch = (uint8_t*)c->lscratch.p;
     B.lcap = c->lcap;
     B.pool = (uint32_t*)c->pool.p;

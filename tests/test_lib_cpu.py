@@ -177,6 +177,24 @@ def test_regex_flag_scope_matches_oracle(pat):
         assert rc == int(g.match_string(s)), (pat, s)
 
 
+# Unbounded counted repetition x{m,} (= x{m-1} x+): found by the bench's
+# parity sample (CRS 941101's relaxed phase-A automaton required m+1 copies).
+UNBOUNDED = [r"a{2,}", r"^a{3,}$", r"x(?:ab){2,}y", r"[a-c]{4,}", r"a{1,}", r"a{0,}b", r"(?i)\bon[a-z]{3,}[\s\x0b]*="]
+
+
+@pytest.mark.parametrize("pat", UNBOUNDED)
+def test_unbounded_repeat_matches_oracle(pat):
+    rnd = random.Random(len(pat) * 3)
+    alpha = b"abcxyON= "
+    g = goregex.compile_go("(?sm)" + pat)
+    strs = [b"aa", b"aaa", b"aaaa", b"xababy", b"xaby", b"abca", b"abc", b".oNuvw=", b"onab="] + [
+        bytes(rnd.choice(alpha) for _ in range(rnd.randint(0, 12))) for _ in range(600)]
+    got, n_states = gpuinspect.selftest_regex_many("(?sm)" + pat, strs)
+    assert n_states > 0  # the DFA path
+    for s, rc in zip(strs, got):
+        assert rc == int(g.match_string(s)), (pat, s)
+
+
 # Patterns whose search DFA exceeds the state cap: the exact matcher is the
 # NFA position tables (host walk == the device's nfa_match), the phase-A
 # automaton a superset relaxation.
