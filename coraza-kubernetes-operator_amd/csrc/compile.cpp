@@ -214,7 +214,7 @@ const std::vector<std::string>& single_names() {
       "REQUEST_METHOD", "REQUEST_PROTOCOL", "REQUEST_URI", "REQUEST_URI_RAW", "REQUEST_LINE",
       "REQUEST_FILENAME", "REQUEST_BASENAME", "QUERY_STRING", "REQUEST_BODY",
       "REQUEST_BODY_LENGTH", "REQBODY_ERROR", "REQBODY_ERROR_MSG", "REQBODY_PROCESSOR",
-      "MULTIPART_STRICT_ERROR", "REMOTE_ADDR", "REMOTE_PORT"};
+      "MULTIPART_STRICT_ERROR", "REMOTE_ADDR", "REMOTE_PORT", "FILES_COMBINED_SIZE"};
   return v;
 }
 const std::map<std::string, int>& collection_ids() {
@@ -224,7 +224,9 @@ const std::map<std::string, int>& collection_ids() {
       {"TX", V_TX}, {"ARGS_GET_NAMES", V_ARGS_GET_NAMES}, {"ARGS_POST_NAMES", V_ARGS_POST_NAMES},
       {"ARGS_NAMES", V_ARGS_NAMES}, {"REQUEST_HEADERS_NAMES", V_REQUEST_HEADERS_NAMES},
       {"REQUEST_COOKIES_NAMES", V_REQUEST_COOKIES_NAMES}, {"XML", V_XML}, {"FILES", V_FILES},
-      {"FILES_NAMES", V_FILES_NAMES}, {"MATCHED_VAR", V_MATCHED_VAR}, {"MATCHED_VAR_NAME", V_MATCHED_VAR_NAME},
+      {"FILES_NAMES", V_FILES_NAMES}, {"FILES_SIZES", V_FILES_SIZES}, {"FILES_TMPNAMES", V_FILES_TMPNAMES},
+      {"MULTIPART_PART_HEADERS", V_MULTIPART_PART_HEADERS},
+      {"MATCHED_VAR", V_MATCHED_VAR}, {"MATCHED_VAR_NAME", V_MATCHED_VAR_NAME},
       {"MATCHED_VARS", V_MATCHED_VARS}, {"MATCHED_VARS_NAMES", V_MATCHED_VARS_NAMES}};
   return m;
 }
@@ -1047,7 +1049,9 @@ struct Lower {
         vr.var = (uint8_t)collection_ids().at(v.name);
         if (vr.var >= V_MATCHED_VAR) P->mv_used = 1;
         vr.ci = (vr.var == V_REQUEST_HEADERS || vr.var == V_REQUEST_HEADERS_NAMES || vr.var == V_TX ||
-                 vr.var == V_MATCHED_VARS || vr.var == V_MATCHED_VARS_NAMES) ? 1 : 0;
+                 vr.var == V_MATCHED_VARS || vr.var == V_MATCHED_VARS_NAMES || vr.var == V_FILES ||
+                 vr.var == V_FILES_NAMES || vr.var == V_FILES_SIZES || vr.var == V_FILES_TMPNAMES ||
+                 vr.var == V_MULTIPART_PART_HEADERS) ? 1 : 0;  // coraza collections.NewMap
         if (v.key_rx) {
           vr.key_mode = 2;
           vr.key_dfa = regex_dfa(v.key);
@@ -1196,6 +1200,10 @@ struct Lower {
   std::vector<StreamBuild> sbuild;
   std::map<std::string, size_t> sindex;
 
+  static bool residual_collection(const std::string& n) {
+    return n == "XML" || n == "FILES" || n == "FILES_NAMES" || n == "FILES_SIZES" || n == "FILES_TMPNAMES" ||
+           n == "MULTIPART_PART_HEADERS";
+  }
   static bool immutable_single(int sid) {
     return sid == S_REQUEST_METHOD || sid == S_REQUEST_PROTOCOL || sid == S_REQUEST_URI ||
            sid == S_REQUEST_URI_RAW || sid == S_REQUEST_LINE || sid == S_REQUEST_FILENAME ||
@@ -1223,6 +1231,7 @@ struct Lower {
       if (sid >= 0 && !immutable_single(sid)) residual = true;  // tested by k_eval on a clear bit
       if (sid < 0 && v.name == "TX") return -1;
       if (v.name.rfind("MATCHED_VAR", 0) == 0) return -1;  // transaction state, not a request variable
+      if (residual_collection(v.name)) residual = true;  // body collections phase A does not scan
       if (v.name == "ARGS" || v.name == "ARGS_POST" || v.name == "ARGS_NAMES" || v.name == "ARGS_POST_NAMES")
         bodydep = true;
     }
@@ -1233,7 +1242,9 @@ struct Lower {
     DVarRef* vrs = &P->vars[d.var_begin];
     for (uint32_t vi = 0; vi < d.var_count; vi++) {
       DVarRef& vr = vrs[vi];
-      if (vr.var < S_COUNT && !immutable_single(vr.var)) {
+      if ((vr.var < S_COUNT && !immutable_single(vr.var)) || vr.var == V_XML || vr.var == V_FILES ||
+          vr.var == V_FILES_NAMES || vr.var == V_FILES_SIZES || vr.var == V_FILES_TMPNAMES ||
+          vr.var == V_MULTIPART_PART_HEADERS) {
         vr.residual = 1;
         continue;
       }

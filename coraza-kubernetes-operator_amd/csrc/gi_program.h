@@ -56,6 +56,7 @@ enum SingleId : uint8_t {
   S_MULTIPART_STRICT_ERROR,
   S_REMOTE_ADDR,   // ProcessConnection
   S_REMOTE_PORT,
+  S_FILES_COMBINED_SIZE,  // multipart: total part bytes
   S_COUNT
 };
 #define GI_REQHDR_BYTES 320  // per-request header slot (ReqHdr, kernels.hip) at the start of its scratch region
@@ -74,8 +75,12 @@ enum VarId : uint8_t {
   V_REQUEST_HEADERS_NAMES,
   V_REQUEST_COOKIES_NAMES,
   V_XML,  // XML body processor output: never populated (XML bodies are flagged unsupported)
-  V_FILES,        // multipart output: never populated (multipart bodies are flagged unsupported)
-  V_FILES_NAMES,
+  // MULTIPART body processor output (kernels.hip parse_multipart)
+  V_FILES,                   // ("", file name) per file part
+  V_FILES_NAMES,             // ("", part name) per file part
+  V_FILES_SIZES,             // (file name, size) -- SetIndex per file name
+  V_FILES_TMPNAMES,          // never populated (no upload storage, as coraza without a filesystem)
+  V_MULTIPART_PART_HEADERS,  // (part name, "Key: value") per part header
   // matched-variable state of the transaction (coraza tx.matchVariable):
   // MATCHED_VAR / MATCHED_VAR_NAME persist across rules, MATCHED_VARS(_NAMES)
   // are reset before every top-level rule (RuleGroup.Eval)
@@ -86,7 +91,12 @@ enum VarId : uint8_t {
 };
 
 // Collection field kinds emitted by the collect stage.
-enum FieldKind : uint8_t { FK_ARG_GET = 1, FK_ARG_POST = 2, FK_HEADER = 3, FK_COOKIE = 4 };
+enum FieldKind : uint8_t {
+  FK_ARG_GET = 1, FK_ARG_POST = 2, FK_HEADER = 3, FK_COOKIE = 4,
+  // multipart collections (after the phase-1 fields, among the ARGS_POST ones;
+  // never phase-A items)
+  FK_FILE = 5, FK_FILE_NAME = 6, FK_FILE_SIZE = 7, FK_PART_HEADER = 8
+};
 
 // ------------------------------------------------------------- operators
 enum OpKind : uint8_t {

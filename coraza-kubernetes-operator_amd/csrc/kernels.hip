@@ -1185,6 +1185,9 @@ __device__ const char* var_name(uint32_t var) {
     case V_XML: return "XML";
     case V_FILES: return "FILES";
     case V_FILES_NAMES: return "FILES_NAMES";
+    case V_FILES_SIZES: return "FILES_SIZES";
+    case V_FILES_TMPNAMES: return "FILES_TMPNAMES";
+    case V_MULTIPART_PART_HEADERS: return "MULTIPART_PART_HEADERS";
     case V_MATCHED_VAR: return "MATCHED_VAR";
     case V_MATCHED_VAR_NAME: return "MATCHED_VAR_NAME";
     case V_MATCHED_VARS: return "MATCHED_VARS";
@@ -1695,6 +1698,448 @@ struct JsonCtx {
 
 __device__ __noinline__ void parse_json_body_ool(JsonCtx* c, const uint8_t* s, uint32_t n) {
   parse_json_body(*c, s, n);
+}
+
+// ------------------------------------------------------------ multipart body
+// [upstream coraza internal/bodyprocessors/multipart.go ProcessRequest over
+// Go's mime.ParseMediaType, mime/multipart.Reader.NextPart and
+// textproto.ReadMIMEHeader], one sequential pass; oracle/multipart.py states
+// the same semantics, their limits and the error classes.  Output fields:
+// per part, its headers (FK_PART_HEADER: part name, "Key: value", sorted by
+// key), then either the file entries (FK_FILE "", file name; FK_FILE_SIZE
+// file name, size, SetIndex per name; FK_FILE_NAME "", part name) or the
+// field (FK_ARG_POST part name, data -> points into the body).
+enum MpErr : uint8_t {
+  MP_OK = 0, MP_E_MEDIA, MP_E_NOTMP, MP_E_EMPTYB, MP_E_EOF, MP_E_BUFFULL, MP_E_EXPECT, MP_E_UNEXP, MP_E_HDR,
+  MP_E_DATA, MP_E_COUNT
+};
+// REQBODY_ERROR_MSG per error class ("<processor>: <error>", generateRequestBodyError)
+__device__ __constant__ char kMpErrMsg[MP_E_COUNT][56] = {
+    "", "MULTIPART: mime: invalid media type", "MULTIPART: not a multipart body",
+    "MULTIPART: multipart: boundary is empty", "MULTIPART: multipart: NextPart: EOF",
+    "MULTIPART: multipart: NextPart: bufio: buffer full", "MULTIPART: multipart: expecting a new Part",
+    "MULTIPART: multipart: unexpected line in Next()", "MULTIPART: multipart: NextPart: malformed MIME header",
+    "MULTIPART: unexpected EOF"};
+
+__device__ inline bool mp_tspecial(uint8_t c) {
+  switch (c) {
+    case '(': case ')': case '<': case '>': case '@': case ',': case ';': case ':': case '\\': case '"':
+    case '/': case '[': case ']': case '?': case '=':
+      return true;
+  }
+  return false;
+}
+__device__ inline bool mp_token(uint8_t c) { return c > 0x20 && c < 0x7F && !mp_tspecial(c); }
+__device__ inline bool mp_lws(uint8_t c) { return c == ' ' || c == '\t'; }
+
+// Next ";key=value" of a media type at v[*i]: 0 ok, 1 no more, -1 syntax error.
+__device__ int mp_next_param(const uint8_t* v, uint32_t n, uint32_t* i, uint32_t* ks, uint32_t* ke, uint32_t* vs,
+                             uint32_t* ve, bool* quoted) {
+  uint32_t p = *i;
+  while (p < n && mp_lws(v[p])) p++;
+  if (p >= n) return 1;
+  if (v[p] != ';') return -1;
+  p++;
+  while (p < n && mp_lws(v[p])) p++;
+  if (p >= n) return 1;  // trailing ';'
+  const uint32_t k0 = p;
+  while (p < n && mp_token(v[p])) p++;
+  if (p == k0) return -1;
+  *ks = k0;
+  *ke = p;
+  while (p < n && mp_lws(v[p])) p++;
+  if (p >= n || v[p] != '=') return -1;
+  p++;
+  while (p < n && mp_lws(v[p])) p++;
+  if (p < n && v[p] == '"') {
+    uint32_t q = p + 1;
+    while (q < n && v[q] != '"') {
+      if (v[q] == '\r' || v[q] == '\n') return -1;
+      if (v[q] == '\\' && q + 1 < n && mp_tspecial(v[q + 1])) q++;
+      q++;
+    }
+    if (q >= n) return -1;
+    *vs = p + 1;
+    *ve = q;
+    *quoted = true;
+    p = q + 1;
+  } else {
+    uint32_t q = p;
+    while (q < n && mp_token(v[q])) q++;
+    if (q == p) return -1;
+    *vs = p;
+    *ve = q;
+    *quoted = false;
+    p = q;
+  }
+  *i = p;
+  return 0;
+}
+
+// mime.ParseMediaType(v) restricted to what the processor reads: the media
+// type [*ts, *te) (not lowercased) and up to two wanted parameters (keys
+// lowercase literals; values unescaped into the arena when quoted with
+// escapes).  Returns 0 ok, 1 error, 2 unsupported (RFC 2231 parameter).
+template <class C>
+__device__ int mp_media(C& t, const uint8_t* v, uint32_t n, uint32_t* ts, uint32_t* te, const char* w0, Str* o0,
+                        const char* w1, Str* o1) {
+  o0->p = CS_ZERO;
+  o0->n = 0;
+  if (o1) {
+    o1->p = CS_ZERO;
+    o1->n = 0;
+  }
+  uint32_t semi = 0;
+  while (semi < n && v[semi] != ';') semi++;
+  uint32_t a = 0, b = semi;
+  while (a < b && mp_lws(v[a])) a++;
+  while (b > a && mp_lws(v[b - 1])) b--;
+  if (a == b) return 1;
+  uint32_t sl = a;
+  while (sl < b && v[sl] != '/') sl++;
+  for (uint32_t k = a; k < sl; k++)
+    if (!mp_token(v[k])) return 1;
+  if (sl < b) {
+    if (sl + 1 == b) return 1;
+    for (uint32_t k = sl + 1; k < b; k++)
+      if (!mp_token(v[k])) return 1;
+  }
+  if (sl == a) return 1;
+  *ts = a;
+  *te = b;
+  uint32_t i = semi;
+  for (;;) {
+    uint32_t ks, ke, vs, ve;
+    bool q;
+    const int r = mp_next_param(v, n, &i, &ks, &ke, &vs, &ve, &q);
+    if (r == 1) break;
+    if (r < 0) return 1;
+    for (uint32_t k = ks; k < ke; k++)
+      if (v[k] == '*') return 2;
+    // duplicate name: compare with the parameters before this one
+    uint32_t j = semi;
+    for (;;) {
+      uint32_t ks2, ke2, vs2, ve2;
+      bool q2;
+      if (mp_next_param(v, n, &j, &ks2, &ke2, &vs2, &ve2, &q2) != 0 || ks2 >= ks) break;
+      if (ke2 - ks2 == ke - ks && eq_ascii_ci_both(v + ks2, v + ks, ke - ks)) return 1;
+    }
+    Str* out = nullptr;
+    uint32_t wn0 = 0, wn1 = 0;
+    while (w0[wn0]) wn0++;
+    if (w1)
+      while (w1[wn1]) wn1++;
+    if (ke - ks == wn0 && eq_ascii_ci(v + ks, ke - ks, (const uint8_t*)w0, wn0)) out = o0;
+    else if (w1 && ke - ks == wn1 && eq_ascii_ci(v + ks, ke - ks, (const uint8_t*)w1, wn1)) out = o1;
+    if (out) {
+      bool esc = false;
+      for (uint32_t k = vs; q && k < ve; k++)
+        if (v[k] == '\\' && k + 1 < ve && mp_tspecial(v[k + 1])) esc = true;
+      if (!esc) {
+        *out = {v + vs, ve - vs};
+      } else {
+        uint8_t* d = tx_alloc(t, ve - vs);
+        if (!d) return 1;
+        uint32_t o = 0;
+        for (uint32_t k = vs; k < ve; k++) {
+          if (v[k] == '\\' && k + 1 < ve && mp_tspecial(v[k + 1])) k++;
+          d[o++] = v[k];
+        }
+        t.nb -= (ve - vs) - o;
+        *out = {d, o};
+      }
+    }
+  }
+  return 0;
+}
+
+// line [*ls, *le) at s[i] without its "\r\n" / "\n"; *nx = the next line
+__device__ inline bool mp_line(const uint8_t* s, uint32_t n, uint32_t i, uint32_t* ls, uint32_t* le, uint32_t* nx) {
+  if (i >= n) return false;
+  uint32_t j = i;
+  while (j < n && s[j] != '\n') j++;
+  *ls = i;
+  *nx = j < n ? j + 1 : n;
+  if (j < n && j > i && s[j - 1] == '\r') j--;
+  *le = j;
+  return true;
+}
+
+// textproto.CanonicalMIMEHeaderKey with its validity check
+__device__ inline bool mp_canonical(const uint8_t* k, uint32_t kn, bool* already) {
+  if (kn == 0) return false;
+  bool up = true, same = true;
+  for (uint32_t i = 0; i < kn; i++) {
+    const uint8_t c = k[i];
+    if (!mp_token(c)) return false;
+    const uint8_t x = (up && c >= 'a' && c <= 'z') ? c - 32 : (!up && c >= 'A' && c <= 'Z') ? c + 32 : c;
+    same &= x == c;
+    up = x == '-';
+  }
+  *already = same;
+  return true;
+}
+
+__device__ inline bool mp_is_final(const uint8_t* s, uint32_t ls, uint32_t le_nl, const uint8_t* bd, uint32_t bn,
+                                   bool lf) {
+  // line s[ls, le_nl) including its NL: ^--boundary--[ \t]*(NL)?$
+  const uint32_t n = le_nl - ls;
+  if (n < bn + 4 || s[ls] != '-' || s[ls + 1] != '-' || !bytes_equal(s + ls + 2, bd, bn) || s[ls + 2 + bn] != '-' ||
+      s[ls + 3 + bn] != '-')
+    return false;
+  uint32_t r = ls + 4 + bn;
+  while (r < le_nl && mp_lws(s[r])) r++;
+  const uint32_t rest = le_nl - r;
+  return rest == 0 || (lf ? (rest == 1 && s[r] == '\n') : (rest == 2 && s[r] == '\r' && s[r + 1] == '\n'));
+}
+
+// matchAfterPrefix == +1 at s[k]
+__device__ inline bool mp_after_ok(const uint8_t* s, uint32_t n, uint32_t k) {
+  if (k >= n) return true;
+  const uint8_t c = s[k];
+  if (c == ' ' || c == '\t' || c == '\r' || c == '\n') return true;
+  return c == '-' && k + 1 < n && s[k + 1] == '-';
+}
+
+// Returns an MpErr (the body-error class) or MP_OK; GI_REQ_UNSUPPORTED_BODY
+// in t.flags for input outside the engine (quoted-printable parts, RFC 2231
+// parameters).  *combined / *combined_set: FILES_COMBINED_SIZE.
+template <class C>
+__device__ __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, const uint8_t* ct, uint32_t ctn,
+                                                uint64_t* combined, bool* combined_set) {
+  *combined = 0;
+  *combined_set = false;
+  uint32_t ts, te;
+  Str bstr;
+  const int mr = mp_media(t, ct, ctn, &ts, &te, "boundary", &bstr, nullptr, nullptr);
+  if (mr == 2) {
+    t.flags |= GI_REQ_UNSUPPORTED_BODY;
+    return MP_OK;
+  }
+  if (mr != 0) return MP_E_MEDIA;
+  if (te - ts < 10 || !eq_ascii_ci(ct + ts, 10, (const uint8_t*)"multipart/", 10)) return MP_E_NOTMP;
+  if (bstr.n == 0) return MP_E_EMPTYB;
+  const uint8_t* bd = bstr.p;
+  const uint32_t bn = bstr.n;
+  bool lf = false;
+  uint32_t parts = 0, i = 0;
+  uint64_t total = 0;
+  for (;;) {
+    // Reader.nextPart: lines until a delimiter line
+    bool expect_new = false;
+    for (;;) {
+      uint32_t j = i;
+      while (j < n && s[j] != '\n' && j - i < 4095) j++;  // bufio.Reader of 4096 bytes: ReadSlice('\n')
+      if (j >= n || s[j] != '\n') {
+        if (j >= n) {
+          if (mp_is_final(s, i, n, bd, bn, lf)) return MP_OK;
+          return MP_E_EOF;
+        }
+        return MP_E_BUFFULL;
+      }
+      const uint32_t ls = i, le = j + 1;  // the line with its '\n'
+      i = j + 1;
+      if (le - ls >= 2 + bn && s[ls] == '-' && s[ls + 1] == '-' && bytes_equal(s + ls + 2, bd, bn)) {
+        uint32_t r = ls + 2 + bn;
+        while (r < le && mp_lws(s[r])) r++;
+        if (parts == 0 && le - r == 1) lf = true;  // first delimiter line ends in a bare LF: LF mode
+        if (lf ? (le - r == 1) : (le - r == 2 && s[r] == '\r')) break;
+      }
+      if (mp_is_final(s, ls, le, bd, bn, lf)) return MP_OK;
+      if (expect_new) return MP_E_EXPECT;
+      if (parts == 0) continue;
+      if (lf ? (le - ls == 1) : (le - ls == 2 && s[ls] == '\r')) {
+        expect_new = true;
+        continue;
+      }
+      return MP_E_UNEXP;
+    }
+    parts++;
+    // textproto.ReadMIMEHeader: FK_PART_HEADER fields (key, value) for now
+    const uint32_t h0 = t.nf;
+    uint8_t herr = MP_OK;
+    for (bool first = true; herr == MP_OK; first = false) {
+      uint32_t ls, le, nx;
+      if (!mp_line(s, n, i, &ls, &le, &nx) || (first && le > ls && mp_lws(s[ls]))) {
+        herr = MP_E_HDR;
+        break;
+      }
+      i = nx;
+      if (le == ls) break;
+      uint32_t a = ls, b = le;
+      while (a < b && mp_lws(s[a])) a++;
+      while (b > a && mp_lws(s[b - 1])) b--;
+      const uint8_t* kv = s + a;
+      uint32_t kvn = b - a;
+      if (i < n && mp_lws(s[i])) {  // continuation lines: joined with one space
+        uint32_t cap = kvn, p = i;
+        for (;;) {
+          uint32_t l2, e2, x2;
+          if (!(p < n && mp_lws(s[p])) || !mp_line(s, n, p, &l2, &e2, &x2)) break;
+          cap += 1 + (e2 - l2);
+          p = x2;
+        }
+        uint8_t* d = tx_alloc(t, cap);
+        if (!d) return MP_OK;  // arena overflow (flagged)
+        for (uint32_t k = 0; k < kvn; k++) d[k] = kv[k];
+        uint32_t o = kvn;
+        while (i < n && mp_lws(s[i])) {
+          uint32_t l2, e2, x2;
+          mp_line(s, n, i, &l2, &e2, &x2);
+          i = x2;
+          while (l2 < e2 && mp_lws(s[l2])) l2++;
+          while (e2 > l2 && mp_lws(s[e2 - 1])) e2--;
+          d[o++] = ' ';
+          for (uint32_t k = l2; k < e2; k++) d[o++] = s[k];
+        }
+        t.nb -= cap - o;
+        kv = d;
+        kvn = o;
+      }
+      uint32_t c = 0;
+      while (c < kvn && kv[c] != ':') c++;
+      bool canon = false;
+      if (c == kvn || !mp_canonical(kv, c, &canon)) herr = MP_E_HDR;
+      for (uint32_t k = c + 1; k < kvn && herr == MP_OK; k++) {
+        const uint8_t x = kv[k];
+        if (!(x >= 0x20 || x == '\t') || x == 0x7F) herr = MP_E_HDR;
+      }
+      if (herr) break;
+      const uint8_t* key = kv;
+      if (!canon) {
+        uint8_t* d = tx_alloc(t, c);
+        if (!d) return MP_OK;
+        bool up = true;
+        for (uint32_t k = 0; k < c; k++) {
+          const uint8_t x = kv[k];
+          d[k] = (up && x >= 'a' && x <= 'z') ? x - 32 : (!up && x >= 'A' && x <= 'Z') ? x + 32 : x;
+          up = d[k] == '-';
+        }
+        key = d;
+      }
+      uint32_t vs = c + 1;
+      while (vs < kvn && mp_lws(kv[vs])) vs++;
+      add_field(t, FK_PART_HEADER, key, c, kv + vs, kvn - vs);
+    }
+    if (herr) {  // NextPart's error: this part added nothing
+      t.nf = h0;
+      return herr;
+    }
+    if (t.flags & GI_REQ_ERROR_MASK) return MP_OK;
+    const uint32_t h1 = t.nf;
+    // first Content-Disposition / Content-Transfer-Encoding
+    Str cd{CS_ZERO, 0};
+    bool have_cd = false;
+    for (uint32_t f = h0; f < h1; f++) {
+      const Field& F = t.fields[f];
+      if (!have_cd && F.kn == 19 && bytes_equal(F.k, (const uint8_t*)"Content-Disposition", 19)) {
+        cd = {F.v, F.vn};
+        have_cd = true;
+      }
+      if (F.kn == 25 && bytes_equal(F.k, (const uint8_t*)"Content-Transfer-Encoding", 25)) {
+        if (F.vn == 16 && eq_ascii_ci(F.v, 16, (const uint8_t*)"quoted-printable", 16)) {
+          t.flags |= GI_REQ_UNSUPPORTED_BODY;
+          return MP_OK;
+        }
+        break;  // Header.Get: the first value decides
+      }
+    }
+    // the part's data: up to the first NL + "--" + boundary + terminator
+    uint32_t end = 0xFFFFFFFFu;
+    if (n - i >= 2 + bn && s[i] == '-' && s[i + 1] == '-' && bytes_equal(s + i + 2, bd, bn) &&
+        mp_after_ok(s, n, i + 2 + bn)) {
+      end = i;
+    } else {
+      const uint32_t pl = (lf ? 1u : 2u) + 2 + bn;
+      for (uint32_t k = i; k + pl <= n; k++) {
+        if (s[k] != (lf ? '\n' : '\r')) continue;
+        if (!lf && s[k + 1] != '\n') continue;
+        const uint32_t d0 = k + (lf ? 1 : 2);
+        if (s[d0] == '-' && s[d0 + 1] == '-' && bytes_equal(s + d0 + 2, bd, bn) && mp_after_ok(s, n, d0 + 2 + bn)) {
+          end = k;
+          break;
+        }
+      }
+    }
+    if (end == 0xFFFFFFFFu) {  // the part's reader hits EOF: io.ReadAll / io.Copy fails before any Add
+      t.nf = h0;
+      return MP_E_DATA;
+    }
+    const uint8_t* data = s + i;
+    const uint32_t dn = end - i;
+    i = end;
+    // disposition: FormName (form-data only) and the filename parameter
+    Str name{CS_ZERO, 0}, fname{CS_ZERO, 0};
+    if (have_cd) {
+      uint32_t dts, dte;
+      Str nm, fn;
+      const int dr = mp_media(t, cd.p, cd.n, &dts, &dte, "name", &nm, "filename", &fn);
+      if (dr == 2) {
+        t.flags |= GI_REQ_UNSUPPORTED_BODY;
+        return MP_OK;
+      }
+      if (dr == 0) {
+        fname = fn;
+        if (dte - dts == 9 && eq_ascii_ci(cd.p + dts, 9, (const uint8_t*)"form-data", 9)) name = nm;
+      }
+    }
+    // MULTIPART_PART_HEADERS: (name, "Key: value"), keys sorted (stable)
+    for (uint32_t f = h0; f < h1; f++) {
+      Field& F = t.fields[f];
+      uint8_t* d = tx_alloc(t, F.kn + 2 + F.vn);
+      if (!d) return MP_OK;
+      for (uint32_t k = 0; k < F.kn; k++) d[k] = F.k[k];
+      d[F.kn] = ':';
+      d[F.kn + 1] = ' ';
+      for (uint32_t k = 0; k < F.vn; k++) d[F.kn + 2 + k] = F.v[k];
+      F.v = d;
+      F.vn = F.kn + 2 + F.vn;  // F.k still the key: the sort below reads it
+    }
+    for (uint32_t f = h0 + 1; f < h1; f++) {
+      const Field x = t.fields[f];
+      uint32_t g = f;
+      while (g > h0) {
+        const Field& y = t.fields[g - 1];
+        // y.k > x.k (bytewise)?
+        const uint32_t m = min(y.kn, x.kn);
+        int cmp = 0;
+        for (uint32_t k = 0; k < m && !cmp; k++) cmp = (int)y.k[k] - (int)x.k[k];
+        if (!cmp) cmp = (int)y.kn - (int)x.kn;
+        if (cmp <= 0) break;
+        t.fields[g] = y;
+        g--;
+      }
+      t.fields[g] = x;
+    }
+    for (uint32_t f = h0; f < h1; f++) {
+      t.fields[f].k = name.p;
+      t.fields[f].kn = name.n;
+    }
+    total += dn;
+    if (fname.n) {
+      add_field(t, FK_FILE, CS_ZERO, 0, fname.p, fname.n);
+      uint8_t* sz = tx_alloc(t, 24);
+      if (!sz) return MP_OK;
+      const uint32_t szn = go_itoa((int64_t)dn, sz);
+      t.nb -= 24 - szn;
+      bool set = false;
+      for (uint32_t f = 0; f < t.nf && !set; f++) {  // FILES_SIZES.SetIndex(file name, 0, size)
+        Field& F = t.fields[f];
+        if (F.kind == FK_FILE_SIZE && F.kn == fname.n && eq_ascii_ci_both(F.k, fname.p, fname.n)) {
+          F.v = sz;
+          F.vn = szn;
+          set = true;
+        }
+      }
+      if (!set) add_field(t, FK_FILE_SIZE, fname.p, fname.n, sz, szn);
+      add_field(t, FK_FILE_NAME, CS_ZERO, 0, name.p, name.n);
+    } else {
+      add_field(t, FK_ARG_POST, name.p, name.n, data, dn);
+    }
+    if (t.flags & GI_REQ_ERROR_MASK) return MP_OK;
+    *combined = total;
+    *combined_set = true;
+  }
 }
 
 // net/url shouldEscape(c, encodePath)
@@ -2314,6 +2759,10 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
     case V_ARGS_NAMES: *names = true; return kind == FK_ARG_GET || kind == FK_ARG_POST;
     case V_REQUEST_HEADERS_NAMES: *names = true; return kind == FK_HEADER;
     case V_REQUEST_COOKIES_NAMES: *names = true; return kind == FK_COOKIE;
+    case V_FILES: return kind == FK_FILE;
+    case V_FILES_NAMES: return kind == FK_FILE_NAME;
+    case V_FILES_SIZES: return kind == FK_FILE_SIZE;
+    case V_MULTIPART_PART_HEADERS: return kind == FK_PART_HEADER;
   }
   return false;
 }
@@ -2398,6 +2847,13 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         const DVarRef vr = gi_cload(P.vars, R.var_begin + vi);
         if (!vr.residual) continue;
         if (vr.var == S_REQUEST_BODY && t.body_spec && R.phase >= 2) continue;  // k_body's bit
+        if (vr.var >= S_COUNT) {  // a body collection phase A never scans (multipart): any value -> "maybe"
+          for (uint32_t f = 0; f < t.nf && !any; f++) {
+            bool nm;
+            any = field_in(vr.var, t.fields[f].kind, &nm);
+          }
+          continue;
+        }
         bool ok;
         const Str sv = t.single[vr.var];
         const Str tv = transform(t, R, sv.p, sv.n, &ok);
@@ -2511,7 +2967,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
       const Field fl = t.fields[f];
       bool names;
       if (!field_in(vr.var, fl.kind, &names)) continue;
-      if (vskip && f < t.nf_pa) {
+      if (vskip && f < t.nf_pa && fl.kind <= FK_COOKIE) {  // phase-A item kinds only
         const uint32_t vb = 2 * f + (names ? 1u : 0u);
         if (!((t.vmap[vb >> 5] >> (vb & 31)) & 1u)) continue;
       }
@@ -2623,9 +3079,9 @@ struct ReqHdr {
   uint16_t n_get, n_hdr, n_ck, flags;
   uint8_t body_proc;
   uint8_t pa_void;      // phase-A arena overflowed: k_eval ignores the hit bits
-  uint8_t spec_proc;    // body processor k_collect parsed the body with (BP_NONE: none)
-  uint8_t _pad;
-  uint32_t n_post;      // its ARG_POST fields, after the phase-1 fields (phase-A items)
+  uint8_t spec_proc;    // body processor k_bparse parsed the body with (BP_NONE: none)
+  uint8_t spec_err;     // its body-error class (multipart MpErr; 0 none)
+  uint32_t n_post;      // its fields (ARGS_POST, multipart collections), after the phase-1 fields
   Str single[S_COUNT];
 };
 static_assert(sizeof(ReqHdr) <= GI_REQHDR_BYTES, "ReqHdr must fit its slot");
@@ -2793,9 +3249,11 @@ __device__ __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H
   }
   const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck, n_pre = n_get + n_hdr + n_ck;
   for (uint32_t i = 0; i < n_pre + H->n_post; i++) {
-    const uint8_t kind = i < n_get ? FK_ARG_GET : i < n_get + n_hdr ? FK_HEADER : i < n_pre ? FK_COOKIE : FK_ARG_POST;
-    const uint8_t sides = P.item_sides[kind];
     const Field fl = Fd[i];
+    // the body range may hold multipart collections: never phase-A items
+    const uint8_t kind = i < n_get ? FK_ARG_GET : i < n_get + n_hdr ? FK_HEADER : i < n_pre ? FK_COOKIE : (uint8_t)fl.kind;
+    if (kind != FK_ARG_GET && kind != FK_HEADER && kind != FK_COOKIE && kind != FK_ARG_POST) continue;
+    const uint8_t sides = P.item_sides[kind];
     if (sides & 1) f(kind, (uint8_t)0, 0u, i, fl.vn);
     if (sides & 2) f(kind, (uint8_t)0, 1u, i, fl.kn);
   }
@@ -2895,11 +3353,29 @@ __device__ void collect_request(const DProgram& P, const DBatch& B, uint32_t r) 
           sp = BP_JSON;
       }
     }
-    if (sp != BP_URLENCODED && sp != BP_JSON) sp = BP_NONE;
+    if (sp != BP_URLENCODED && sp != BP_JSON && sp != BP_MULTIPART) sp = BP_NONE;
   }
   H->spec_proc = sp;  // k_bparse parses the body (or resets this to BP_NONE)
+  H->spec_err = 0;
   H->n_post = 0;
   H->nb = t.nb;
+}
+
+// The first Content-Type request header's value (coraza ProcessRequestBody's mime)
+__device__ inline Str first_content_type(const DBatch& B, const gi_request& rq) {
+  for (uint32_t h = 0; h < rq.hdr_count; h++) {
+    const gi_header hd = B.headers[rq.hdr_begin + h];
+    if (hd.name.len == 12 && eq_ascii_ci(B.data + hd.name.off, 12, (const uint8_t*)"content-type", 12))
+      return {B.data + hd.value.off, hd.value.len};
+  }
+  return {CS_ZERO, 0};
+}
+
+__device__ inline Str mp_err_msg(uint8_t e) {
+  const uint8_t* m = (const uint8_t*)kMpErrMsg[e];
+  uint32_t k = 0;
+  while (m[k]) k++;
+  return {m, k};
 }
 
 // Speculative ProcessRequestBody (k_collect picked the processor): one wave
@@ -2936,7 +3412,7 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
     Region g = region_of(P, B, r);
     ReqHdr* H = g.hdr;
     const uint8_t sp = H->spec_proc;
-    if ((sp != BP_URLENCODED && sp != BP_JSON) || (H->flags & GI_REQ_ERROR_MASK)) continue;
+    if ((sp != BP_URLENCODED && sp != BP_JSON && sp != BP_MULTIPART) || (H->flags & GI_REQ_ERROR_MASK)) continue;
     const gi_span bs = B.reqs[r].body;
     const uint8_t* q = B.data + bs.off;
     const uint32_t n = bs.len;
@@ -2986,10 +3462,28 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
         }
         nb = nb0 + wave_max(used);
       }
-    } else {  // JSON (or an urlencoded body the arena bound does not cover): lane 0, sequential
+    } else {  // JSON / multipart (or an urlencoded body the arena bound does not cover): lane 0, sequential
       uint32_t res[3] = {0, 0, 0};
       if (L == 0) {
-        if (sp == BP_URLENCODED) {
+        if (sp == BP_MULTIPART) {
+          JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
+          const Str ct = first_content_type(B, B.reqs[r]);
+          uint64_t comb;
+          bool comb_set;
+          const uint8_t err = parse_multipart(jc, q, n, ct.p, ct.n, &comb, &comb_set);
+          if (comb_set && !jc.flags) {
+            uint8_t* cb = tx_alloc(jc, 24);
+            if (cb) {
+              const uint32_t cn2 = go_itoa((int64_t)comb, cb);
+              jc.nb -= 24 - cn2;
+              H->single[S_FILES_COMBINED_SIZE] = {cb, cn2};
+            }
+          }
+          H->spec_err = err;
+          res[0] = jc.nf - nf0;
+          res[1] = jc.nb;
+          res[2] = jc.flags;
+        } else if (sp == BP_URLENCODED) {
           Tx t;
           tx_bind(t, P, g);
           t.nf = nf0;
@@ -3019,7 +3513,11 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
     if (L == 0) {
       H->n_post = n_post;
       H->nb = nb;
-      if (!ok) H->spec_proc = BP_NONE;
+      if (!ok) {
+        H->spec_proc = BP_NONE;
+        H->spec_err = 0;
+        H->single[S_FILES_COMBINED_SIZE] = {CS_ZERO, 0};
+      }
     }
     // phase-A item counts of the body fields (ARGS_POST sides some filter reads)
     const uint32_t sides = P.n_streams ? P.item_sides[FK_ARG_POST] : 0u;
@@ -3027,6 +3525,7 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
       uint32_t cnt[GI_NB] = {0, 0, 0, 0, 0};
       for (uint32_t i = L; i < n_post; i += 64) {
         const Field fl = g.fields[nf0 + i];
+        if (fl.kind != FK_ARG_POST) continue;  // multipart collections are not phase-A items
         if (sides & 1) cnt[item_bucket(fl.vn)]++;
         if (sides & 2) cnt[item_bucket(fl.kn)]++;
       }
@@ -3984,7 +4483,8 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
     const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
     if (H->spec_proc == BP_NONE || (H->flags & GI_REQ_ERROR_MASK)) continue;
     const Region g = region_of(P, B, r);
-    const gi_span bs = B.reqs[r].body;
+    gi_span bs = B.reqs[r].body;
+    if (H->spec_proc == BP_MULTIPART) bs.len = 0;  // coraza's multipart processor sets no REQUEST_BODY
     const uint8_t* body = B.data + bs.off;
     const uint8_t* cur = body;
     uint32_t cn = bs.len;
@@ -4212,6 +4712,37 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
                   }
                 }
                 t.has_post = t.nf > nf0;
+              }
+            } else if (t.body_proc == BP_MULTIPART) {
+              // [upstream multipart.go]: collections, no REQUEST_BODY; an error
+              // -> MULTIPART_STRICT_ERROR + generateRequestBodyError (rules
+              // 200002 / 200003 deny with 400)
+              uint8_t err;
+              if (H->spec_proc == BP_MULTIPART) {
+                t.nf += H->n_post;  // k_bparse's fields (ARGS_POST already in phase A)
+                t.nf_pa = t.nf;
+                t.body_spec = true;
+                err = H->spec_err;
+              } else {
+                const uint32_t nf0 = t.nf;
+                JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
+                const Str ct = first_content_type(B, rq);
+                uint64_t comb;
+                bool comb_set;
+                err = parse_multipart(jc, D + rq.body.off, bn, ct.p, ct.n, &comb, &comb_set);
+                t.nf = jc.nf;
+                t.nb = jc.nb;
+                t.flags = jc.flags;
+                if (comb_set && !(t.flags & GI_REQ_ERROR_MASK)) {
+                  uint8_t* cb = tx_alloc(t, 24);
+                  if (cb) t.single[S_FILES_COMBINED_SIZE] = {cb, go_itoa((int64_t)comb, cb)};
+                }
+                t.has_post = t.nf > nf0;
+              }
+              if (err) {
+                t.single[S_MULTIPART_STRICT_ERROR] = {CS_ONE, 1};
+                t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
+                t.single[S_REQBODY_ERROR_MSG] = mp_err_msg(err);
               }
             } else if (t.body_proc != BP_NONE) {
               t.flags |= GI_REQ_UNSUPPORTED_BODY;

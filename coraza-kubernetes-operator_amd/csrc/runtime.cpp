@@ -501,12 +501,18 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     uint64_t maxv = std::max<uint64_t>({(uint64_t)q.uri.len * 3 + 2, (uint64_t)q.method.len + q.uri.len + q.proto.len + 2,
                                         (uint64_t)q.body.len, 64});
     uint64_t cookie = 0, ncookie = 0, hdr_bytes = 0;
+    bool multipart = false;
     for (uint32_t h = 0; h < q.hdr_count; h++) {
       const gi_header& hd = in->headers[q.hdr_begin + h];
       if (hd.name.off + hd.name.len > in->data_len || hd.value.off + hd.value.len > in->data_len)
         return fail(c, GI_EINVAL, "header span out of range");
       maxv = std::max<uint64_t>(maxv, std::max(hd.name.len, hd.value.len));
       hdr_bytes += hd.name.len + hd.value.len;
+      if (hd.name.len == 12 && strncasecmp((const char*)in->data + hd.name.off, "content-type", 12) == 0) {
+        const char* hv = (const char*)in->data + hd.value.off;
+        for (uint32_t k = 0; k + 9 <= hd.value.len && !multipart; k++)
+          multipart = strncasecmp(hv + k, "multipart", 9) == 0;
+      }
       if (hd.name.len == 6) {
         const uint8_t* nm = in->data + hd.name.off;
         bool ck = true;
@@ -525,15 +531,23 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     uint64_t post_fields = 0;
     if (q.body.len) {
       const uint8_t* bd = in->data + q.body.off;
-      uint64_t seps = 0;
+      uint64_t seps = 0, nls = 0;
       for (uint32_t k = 0; k < q.body.len; k++) {
         const uint8_t ch = bd[k];
         seps += (ch == '&') + (ch == ',') + 2 * (ch == '[') + (ch == '{');
+        nls += ch == '\n';
       }
       post_fields = std::min<uint64_t>(seps + 2, q.body.len / 2 + 2);
+      // multipart (kernels.hip parse_multipart): a part spends >= 2 lines on
+      // its delimiter and header end and yields <= 3 entries + 1 per header line
+      if (multipart) post_fields += nls + 8;
     }
     uint64_t cap_f = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie) + post_fields;
     uint64_t cap_b = 4ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96 + 16;  // + REMOTE_PORT
+    // multipart: canonical keys, joined continuation lines, "Key: value"
+    // strings and unescaped parameters are each at most the part header
+    // bytes; sizes 24 B per part
+    if (multipart) cap_b += 4ull * q.body.len + 1024;
     {  // a JSON-looking body: room for the flattened "json.a.b" keys + parser stack
       const uint8_t* bd = in->data + q.body.off;
       uint32_t k = 0;

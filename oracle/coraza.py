@@ -36,7 +36,7 @@ import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
-from . import goregex
+from . import goregex, multipart
 
 # ---------------------------------------------------------------------------
 # Errors
@@ -59,6 +59,7 @@ SINGLE_VARS = {
     "REQBODY_PROCESSOR", "MULTIPART_STRICT_ERROR", "ARGS_COMBINED_SIZE",
     "FULL_REQUEST_LENGTH", "MATCHED_VAR", "MATCHED_VAR_NAME",
     "REMOTE_ADDR", "REMOTE_PORT", "SERVER_NAME", "URLENCODED_ERROR",
+    "FILES_COMBINED_SIZE",
 }
 MAP_VARS = {
     # name: (source collection(s), case_insensitive_keys)
@@ -72,9 +73,14 @@ MAP_VARS = {
     # populated only by the XML body processor (not implemented: such
     # requests are flagged unsupported), so always empty here
     "XML": (("XML",), False),
-    # multipart file collections: populated only by the MULTIPART processor
-    # (not implemented: such requests are flagged unsupported)
-    "FILES": (("FILES",), False),
+    # multipart collections (oracle/multipart.py); keys: "" for FILES /
+    # FILES_NAMES, the file name for FILES_SIZES, the part name for
+    # MULTIPART_PART_HEADERS (coraza collections.NewMap: case-insensitive)
+    "FILES": (("FILES",), True),
+    "FILES_NAMES": (("FILES_NAMES",), True),
+    "FILES_SIZES": (("FILES_SIZES",), True),
+    "FILES_TMPNAMES": (("FILES_TMPNAMES",), True),
+    "MULTIPART_PART_HEADERS": (("MULTIPART_PART_HEADERS",), True),
 }
 NAMES_VARS = {
     "ARGS_GET_NAMES": (("ARGS_GET",), False),
@@ -83,7 +89,6 @@ NAMES_VARS = {
     "REQUEST_HEADERS_NAMES": (("REQUEST_HEADERS",), True),
     "REQUEST_COOKIES_NAMES": (("REQUEST_COOKIES",), False),
     "MATCHED_VARS_NAMES": (("MATCHED_VARS",), True),
-    "FILES_NAMES": (("FILES",), False),
 }
 ALL_VARS = SINGLE_VARS | set(MAP_VARS) | set(NAMES_VARS)
 
@@ -1694,7 +1699,8 @@ class Transaction:
         self.single["MULTIPART_STRICT_ERROR"] = b"0"
         self.maps: Dict[str, List[Tuple[bytes, bytes]]] = {
             "ARGS_GET": [], "ARGS_POST": [], "REQUEST_HEADERS": [],
-            "REQUEST_COOKIES": [], "MATCHED_VARS": [], "XML": [], "FILES": []}
+            "REQUEST_COOKIES": [], "MATCHED_VARS": [], "XML": [], "FILES": [], "FILES_NAMES": [],
+            "FILES_SIZES": [], "FILES_TMPNAMES": [], "MULTIPART_PART_HEADERS": []}
         self.force_body = False
         self.body = b""
         self.phase = 0
@@ -2048,6 +2054,30 @@ class Transaction:
                         raise UnsupportedInput("JSON body beyond the engine's limits")
                     self.single["REQUEST_BODY"] = self.body
                 self.maps["ARGS_POST"] = args
+            elif rbp == b"MULTIPART":
+                # [upstream multipart.go ProcessRequest] (oracle/multipart.py);
+                # an error -> MULTIPART_STRICT_ERROR and generateRequestBodyError,
+                # the collections keep the parts before it; no REQUEST_BODY
+                ct = b""
+                for k, val in self.maps["REQUEST_HEADERS"]:
+                    if k.lower() == b"content-type":
+                        ct = val
+                        break
+                try:
+                    res = multipart.process(self.body, ct)
+                except multipart.MultipartUnsupported as e:
+                    raise UnsupportedInput("multipart: %s" % e)
+                self.maps["ARGS_POST"] = res["args_post"]
+                self.maps["FILES"] = res["files"]
+                self.maps["FILES_NAMES"] = res["files_names"]
+                self.maps["FILES_SIZES"] = res["files_sizes"]
+                self.maps["MULTIPART_PART_HEADERS"] = res["part_headers"]
+                if res["combined_size"] is not None:
+                    self.single["FILES_COMBINED_SIZE"] = res["combined_size"]
+                if res["error"] is not None:
+                    self.single["MULTIPART_STRICT_ERROR"] = b"1"
+                    self.single["REQBODY_ERROR"] = b"1"
+                    self.single["REQBODY_ERROR_MSG"] = b"MULTIPART: " + res["error"].encode()
             elif rbp == b"":
                 pass
             else:
