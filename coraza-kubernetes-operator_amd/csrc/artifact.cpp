@@ -310,6 +310,8 @@ bool validate_program(const Program& P, std::string* err) {
       if (a.tmpl >= 0 && (size_t)a.tmpl >= ntm) return bad("setvar template");
       if ((a.a == SV_ADD_SLOT || a.a == SV_SUB_SLOT) && (a.b < 0 || (uint64_t)a.b >= nslot)) return bad("setvar source");
     }
+    if (a.kind == A_CTL_RULE_REMOVE_TARGET && (a.tmpl < 0 || a._pad2 < 0 || !in((uint32_t)a.tmpl, (uint32_t)a._pad2, nstr)))
+      return bad("ctl target key");
   }
   // phase-A scan plan
   if (P.streams.size() > GI_MAX_STREAMS || P.filters.size() > GI_MAX_GFILTERS) return bad("scan plan size");

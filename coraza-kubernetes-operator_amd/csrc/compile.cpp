@@ -613,7 +613,7 @@ void apply_actions(IrRule* rule, const Actions& acts) {
       size_t eq = v.find('=');
       nd.ctl_name = lower(trim(eq == std::string::npos ? v : v.substr(0, eq)));
       nd.ctl_value = trim(eq == std::string::npos ? "" : v.substr(eq + 1));
-      if (nd.ctl_name != "ruleremovebyid" && nd.ctl_name != "ruleengine" &&
+      if (nd.ctl_name != "ruleremovebyid" && nd.ctl_name != "ruleremovetargetbyid" && nd.ctl_name != "ruleengine" &&
           nd.ctl_name != "requestbodyprocessor" && nd.ctl_name != "requestbodyaccess" &&
           nd.ctl_name != "forcerequestbodyvariable")
         unsup("unsupported ctl " + nd.ctl_name);
@@ -1147,6 +1147,37 @@ struct Lower {
           a.b = hi;
           P->acts.push_back(a);
         }
+      } else if (nd.ctl_name == "ruleremovetargetbyid") {
+        // "ID[-ID];VARIABLE[:key]" [upstream internal/actions/ctl.go]
+        const size_t semi = nd.ctl_value.find(';');
+        if (semi == std::string::npos) perr("invalid ctl:ruleRemoveTargetById " + nd.ctl_value);
+        const std::string ids = trim(nd.ctl_value.substr(0, semi)), tgt = trim(nd.ctl_value.substr(semi + 1));
+        int64_t lo, hi;
+        const size_t dash = ids.find('-');
+        if (dash != std::string::npos && dash > 0) {
+          if (!go_atoi(ids.substr(0, dash), &lo) || !go_atoi(ids.substr(dash + 1), &hi))
+            perr("invalid ctl:ruleRemoveTargetById " + nd.ctl_value);
+        } else {
+          if (!go_atoi(ids, &lo)) perr("invalid ctl:ruleRemoveTargetById " + nd.ctl_value);
+          hi = lo;
+        }
+        const size_t colon = tgt.find(':');
+        const std::string vname = upper(trim(tgt.substr(0, colon)));
+        const std::string key = colon == std::string::npos ? "" : lower(tgt.substr(colon + 1));
+        int vid = single_id(vname);
+        if (vid < 0) {
+          auto it = collection_ids().find(vname);
+          if (it == collection_ids().end()) unsup("ctl:ruleRemoveTargetById variable " + vname);
+          vid = it->second;
+        }
+        DAction a{};
+        a.kind = A_CTL_RULE_REMOVE_TARGET;
+        a.a = lo;
+        a.b = hi;
+        a.slot = vid;
+        a.tmpl = (int32_t)str(key);
+        a._pad2 = (int32_t)key.size();
+        P->acts.push_back(a);
       } else if (nd.ctl_name == "ruleengine") {
         DAction a{};
         a.kind = A_CTL_RULE_ENGINE;
@@ -1200,8 +1231,9 @@ struct Lower {
   std::vector<StreamBuild> sbuild;
   std::map<std::string, size_t> sindex;
 
+  // body collections phase A does not scan (XML stays empty: its processor is not implemented)
   static bool residual_collection(const std::string& n) {
-    return n == "XML" || n == "FILES" || n == "FILES_NAMES" || n == "FILES_SIZES" || n == "FILES_TMPNAMES" ||
+    return n == "FILES" || n == "FILES_NAMES" || n == "FILES_SIZES" || n == "FILES_TMPNAMES" ||
            n == "MULTIPART_PART_HEADERS";
   }
   static bool immutable_single(int sid) {
@@ -1242,7 +1274,7 @@ struct Lower {
     DVarRef* vrs = &P->vars[d.var_begin];
     for (uint32_t vi = 0; vi < d.var_count; vi++) {
       DVarRef& vr = vrs[vi];
-      if ((vr.var < S_COUNT && !immutable_single(vr.var)) || vr.var == V_XML || vr.var == V_FILES ||
+      if ((vr.var < S_COUNT && !immutable_single(vr.var)) || vr.var == V_FILES ||
           vr.var == V_FILES_NAMES || vr.var == V_FILES_SIZES || vr.var == V_FILES_TMPNAMES ||
           vr.var == V_MULTIPART_PART_HEADERS) {
         vr.residual = 1;

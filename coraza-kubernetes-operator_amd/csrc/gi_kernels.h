@@ -40,6 +40,7 @@ struct DBatch {
   uint32_t* vmap;             // phase-A value map: a bit per scanned (field, side) that set some hit bit
   const uint32_t* body_list;  // requests with a body, longest first (k_body: one wave each)
   uint32_t n_body;
+  uint32_t n_mp_body;         // of which multipart (k_mpparse)
   Slot* txslots;       // TX variables [n_slots][n_req] (k_eval)
   // phase A (see kernels.hip "phase A")
   uint32_t* bcounts;          // [k_collect blocks][GI_NB] item counts

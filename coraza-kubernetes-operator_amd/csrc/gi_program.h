@@ -59,7 +59,8 @@ enum SingleId : uint8_t {
   S_FILES_COMBINED_SIZE,  // multipart: total part bytes
   S_COUNT
 };
-#define GI_REQHDR_BYTES 320  // per-request header slot (ReqHdr, kernels.hip) at the start of its scratch region
+#define GI_REQHDR_BYTES 320
+#define GI_RM_BYTES 384  // per request: 8 ctl:ruleRemoveById ranges (128 B) + 8 ctl:ruleRemoveTargetById entries (32 B)  // per-request header slot (ReqHdr, kernels.hip) at the start of its scratch region
 
 // Variable ids used by rule targets.  [0, S_COUNT) are singles.
 enum VarId : uint8_t {
@@ -178,6 +179,7 @@ enum ActKind : uint8_t {
   A_CTL_BODY_PROCESSOR,
   A_CTL_BODY_ACCESS,
   A_CTL_FORCE_BODY,
+  A_CTL_RULE_REMOVE_TARGET,  // ctl:ruleRemoveTargetById: a..b ids, slot = VarId, tmpl/_pad2 = key (strpool, lowercase)
 };
 
 // setvar fast forms (DAction.a for A_SETVAR)

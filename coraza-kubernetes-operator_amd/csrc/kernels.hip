@@ -1268,6 +1268,12 @@ struct Tx {
   bool body_spec;            // the body went through k_collect's processor: k_body tested REQUEST_BODY
   bool pa_void;              // phase-A arena overflowed: no phase-A bit is trusted
   int64_t (*removed)[2];     // ctl:ruleRemoveById ranges (8, in the request's scratch region)
+  struct RmTarget {          // ctl:ruleRemoveTargetById entries (8, after the ranges)
+    int64_t lo, hi;
+    uint32_t var, koff, klen, _pad;
+  }* rtgt;
+  uint32_t nrtgt;
+  uint32_t n_mp;             // multipart collection entries (FILES*, MULTIPART_PART_HEADERS)
   uint32_t nremoved;
   uint8_t engine, body_access, body_proc, phase;
   uint8_t force_body;
@@ -2487,6 +2493,14 @@ __device__ __forceinline__ void run_actions(Tx& t, const DRule& R) {
           t.flags |= GI_REQ_OVERFLOW;
         }
         break;
+      case A_CTL_RULE_REMOVE_TARGET:
+        if (t.nrtgt < 8) {
+          t.rtgt[t.nrtgt] = {a.a, a.b, (uint32_t)a.slot, (uint32_t)a.tmpl, (uint32_t)a._pad2, 0u};
+          t.nrtgt++;
+        } else {
+          t.flags |= GI_REQ_OVERFLOW;
+        }
+        break;
       case A_CTL_RULE_ENGINE:
         t.engine = (uint8_t)a.a;
         break;
@@ -2733,6 +2747,19 @@ __device__ __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v
   return cur;
 }
 
+// ctl:ruleRemoveTargetById: the link's rule id removed variable `var`
+// entries with key k (coraza rule.go doEvaluate adds them to the variable's
+// exceptions: compared with the lowercased key; a single's key is "")
+__device__ __noinline__ bool target_removed_in(const Tx::RmTarget* rt, uint32_t n, const uint8_t* strpool, int32_t id,
+                                               uint32_t var, const uint8_t* k, uint32_t kn) {
+  for (uint32_t e = 0; e < n; e++) {
+    const Tx::RmTarget x = rt[e];
+    if (x.var == var && x.lo <= id && id <= x.hi && eq_ascii_ci(k, kn, strpool + x.koff, x.klen)) return true;
+  }
+  return false;
+}
+#define target_removed(t, id, var, k, kn) target_removed_in((t).rtgt, (t).nrtgt, (t).P->strpool, (id), (var), (k), (kn))
+
 __device__ __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
   const DProgram& P = *t.P;
   for (uint32_t e = 0; e < vr.exc_count; e++) {
@@ -2847,11 +2874,8 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         const DVarRef vr = gi_cload(P.vars, R.var_begin + vi);
         if (!vr.residual) continue;
         if (vr.var == S_REQUEST_BODY && t.body_spec && R.phase >= 2) continue;  // k_body's bit
-        if (vr.var >= S_COUNT) {  // a body collection phase A never scans (multipart): any value -> "maybe"
-          for (uint32_t f = 0; f < t.nf && !any; f++) {
-            bool nm;
-            any = field_in(vr.var, t.fields[f].kind, &nm);
-          }
+        if (vr.var >= S_COUNT) {  // a body collection phase A never scans (multipart): any entry -> "maybe"
+          any = t.n_mp != 0;
           continue;
         }
         bool ok;
@@ -2871,6 +2895,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   for (uint32_t vi = 0; vi < R.var_count; vi++) {
     const DVarRef vr = gi_cload(P.vars, R.var_begin + vi);
     if (vr.var < S_COUNT) {
+      if (t.nrtgt && R.id != 0 && target_removed(t, R.id, vr.var, nullptr, 0)) continue;
       if (vr.count) {
         uint8_t one = '1';
         nmatch += test_value(t, R, o, &one, 1, vr.var, nullptr, 0);
@@ -2894,6 +2919,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         uint32_t nn = P.slot_names[sid * 2 + 1];
         if (vr.key_mode == 2 && !dfa_match(P, vr.key_dfa, nm, nn, false)) continue;
         if (key_excluded(t, vr, nm, nn)) continue;
+        if (t.nrtgt && R.id != 0 && target_removed(t, R.id, V_TX, nm, nn)) continue;
         if (vr.count) {
           cnt++;
           continue;
@@ -2979,6 +3005,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         if (!dfa_match(P, vr.key_dfa, fl.k, fl.kn, vr.ci != 0)) continue;
       }
       if (vr.exc_count && key_excluded(t, vr, fl.k, fl.kn)) continue;
+      if (t.nrtgt && R.id != 0 && target_removed(t, R.id, vr.var, fl.k, fl.kn)) continue;
       if (vr.count) {
         cnt++;
         continue;
@@ -3107,7 +3134,7 @@ __device__ inline Region region_of(const DProgram& P, const DBatch& B, uint32_t 
   g.slots = (Slot*)(base + off);
   off += ((uint64_t)P.n_slots * sizeof(Slot) + 15) & ~15ull;
   g.rm = (int64_t(*)[2])(base + off);
-  off += 128;
+  off += GI_RM_BYTES;
   g.bytes = base + off;
   off += (L.cap_b + 15) & ~15u;
   g.t0 = base + off;
@@ -3140,6 +3167,7 @@ __device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
   t.cap_mt = g.cap_mt;
   t.txa = g.txa;
   t.removed = g.rm;
+  t.rtgt = (Tx::RmTarget*)(g.rm + 8);
   t.cap_tx = g.cap_mt;
   t.single = g.hdr->single;
   t.mv = g.mv;
@@ -3412,7 +3440,7 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
     Region g = region_of(P, B, r);
     ReqHdr* H = g.hdr;
     const uint8_t sp = H->spec_proc;
-    if ((sp != BP_URLENCODED && sp != BP_JSON && sp != BP_MULTIPART) || (H->flags & GI_REQ_ERROR_MASK)) continue;
+    if ((sp != BP_URLENCODED && sp != BP_JSON) || (H->flags & GI_REQ_ERROR_MASK)) continue;  // multipart: k_mpparse
     const gi_span bs = B.reqs[r].body;
     const uint8_t* q = B.data + bs.off;
     const uint32_t n = bs.len;
@@ -3462,28 +3490,10 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
         }
         nb = nb0 + wave_max(used);
       }
-    } else {  // JSON / multipart (or an urlencoded body the arena bound does not cover): lane 0, sequential
+    } else {  // JSON (or an urlencoded body the arena bound does not cover): lane 0, sequential
       uint32_t res[3] = {0, 0, 0};
       if (L == 0) {
-        if (sp == BP_MULTIPART) {
-          JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
-          const Str ct = first_content_type(B, B.reqs[r]);
-          uint64_t comb;
-          bool comb_set;
-          const uint8_t err = parse_multipart(jc, q, n, ct.p, ct.n, &comb, &comb_set);
-          if (comb_set && !jc.flags) {
-            uint8_t* cb = tx_alloc(jc, 24);
-            if (cb) {
-              const uint32_t cn2 = go_itoa((int64_t)comb, cb);
-              jc.nb -= 24 - cn2;
-              H->single[S_FILES_COMBINED_SIZE] = {cb, cn2};
-            }
-          }
-          H->spec_err = err;
-          res[0] = jc.nf - nf0;
-          res[1] = jc.nb;
-          res[2] = jc.flags;
-        } else if (sp == BP_URLENCODED) {
+        if (sp == BP_URLENCODED) {
           Tx t;
           tx_bind(t, P, g);
           t.nf = nf0;
@@ -3535,6 +3545,56 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
         if (L == 0 && x) atomicAdd(&B.bcounts[(r / 256) * GI_NB + b], x);
       }
     }
+  }
+}
+
+// Speculative multipart ProcessRequestBody: one thread per body-list entry
+// (its own kernel: the sequential parser's registers stay out of k_bparse).
+// On failure the request keeps no fields (k_eval parses it again).
+__global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
+  const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= B.n_body) return;
+  const uint32_t r = B.body_list[bi];
+  GI_BOUND(r < B.n_req, r, bi);
+  Region g = region_of(P, B, r);
+  ReqHdr* H = g.hdr;
+  if (H->spec_proc != BP_MULTIPART || (H->flags & GI_REQ_ERROR_MASK)) return;
+  const gi_span bs = B.reqs[r].body;
+  const uint32_t nf0 = H->nf, nb0 = H->nb;
+  JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
+  const Str ct = first_content_type(B, B.reqs[r]);
+  uint64_t comb;
+  bool comb_set;
+  const uint8_t err = parse_multipart(jc, B.data + bs.off, bs.len, ct.p, ct.n, &comb, &comb_set);
+  if (jc.flags) {  // an engine limit / unsupported input: k_eval decides
+    H->spec_proc = BP_NONE;
+    return;
+  }
+  if (comb_set) {
+    uint8_t* cb = tx_alloc(jc, 24);
+    if (!cb) {
+      H->spec_proc = BP_NONE;
+      return;
+    }
+    const uint32_t cn2 = go_itoa((int64_t)comb, cb);
+    jc.nb -= 24 - cn2;
+    H->single[S_FILES_COMBINED_SIZE] = {cb, cn2};
+  }
+  H->spec_err = err;
+  H->n_post = jc.nf - nf0;
+  H->nb = jc.nb;
+  // phase-A item counts of its ARGS_POST fields
+  const uint32_t sides = P.n_streams ? P.item_sides[FK_ARG_POST] : 0u;
+  if (sides) {
+    uint32_t cnt[GI_NB] = {0, 0, 0, 0, 0};
+    for (uint32_t i = nf0; i < jc.nf; i++) {
+      const Field fl = g.fields[i];
+      if (fl.kind != FK_ARG_POST) continue;
+      if (sides & 1) cnt[item_bucket(fl.vn)]++;
+      if (sides & 2) cnt[item_bucket(fl.kn)]++;
+    }
+    for (uint32_t b = 0; b < GI_NB; b++)
+      if (cnt[b]) atomicAdd(&B.bcounts[(r / 256) * GI_NB + b], cnt[b]);
   }
 }
 
@@ -4641,6 +4701,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
     t.body_proc = H->body_proc;
     t.ntx = 0;
     t.nremoved = 0;
+    t.nrtgt = 0;
+    t.n_mp = 0;
     t.engine = P.rule_engine;
     t.body_access = P.body_access;
     t.force_body = 0;
@@ -4739,6 +4801,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
                 }
                 t.has_post = t.nf > nf0;
               }
+              for (uint32_t f = H->nf; f < t.nf; f++) t.n_mp += t.fields[f].kind >= FK_FILE ? 1u : 0u;
               if (err) {
                 t.single[S_MULTIPART_STRICT_ERROR] = {CS_ONE, 1};
                 t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
@@ -4909,8 +4972,10 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
   }
   const uint32_t cb = (B.n_req + 255) / 256;
   GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
-  if (B.n_body && P.body_access)
+  if (B.n_body && P.body_access) {
     GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
+    if (B.n_mp_body) GI_LAUNCH("k_mpparse", k_mpparse, dim3((B.n_body + 63) / 64), dim3(64), 0, stream, P, B);
+  }
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (P.n_streams) {
     GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(1), dim3(1024), 0, stream, B, cb);

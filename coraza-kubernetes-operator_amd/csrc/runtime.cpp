@@ -94,6 +94,7 @@ struct gi_ctx {
   uint32_t hit_words = 0;
   uint64_t vmap_words = 0;  // value map (DBatch.vmap)
   uint32_t n_body = 0;      // requests with a body (DBatch.body_list)
+  uint32_t n_mp_body = 0;   // of which multipart
   hipEvent_t evs[3] = {nullptr, nullptr, nullptr};
   LaunchLog log{};
   uint64_t raw_nobody = 0, raw_all = 0;  // batch bytes (algorithmic-byte accounting)
@@ -488,6 +489,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   // validate spans and lay out per-request scratch (lengths only)
   std::vector<ReqLayout> lay(n);
   uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0, vmap_bits = 0;
+  uint32_t n_mp_body = 0;
   uint32_t max_cap_t = 64;
   const uint32_t nslots = c->rs->prog.n_slots;
   const Program& PG = c->rs->prog;
@@ -541,6 +543,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       // multipart (kernels.hip parse_multipart): a part spends >= 2 lines on
       // its delimiter and header end and yields <= 3 entries + 1 per header line
       if (multipart) post_fields += nls + 8;
+      n_mp_body += multipart ? 1 : 0;
     }
     uint64_t cap_f = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie) + post_fields;
     uint64_t cap_b = 4ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96 + 16;  // + REMOTE_PORT
@@ -578,7 +581,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     L.cap_b = (uint32_t)cap_b;
     L.cap_t = (uint32_t)cap_t;
     L.cap_mt = (uint32_t)cap_mt;
-    uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + 128 + (cap_b + 15) / 16 * 16 +
+    uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + GI_RM_BYTES + (cap_b + 15) / 16 * 16 +
                   2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
     // matched-variable state (kernels.hip MvState): header, entries, value
     // arena, MATCHED_VAR copy, name buffer
@@ -613,6 +616,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   std::stable_sort(blist.begin(), blist.end(),
                    [&](uint32_t x, uint32_t y) { return in->reqs[x].body.len > in->reqs[y].body.len; });
   c->n_body = (uint32_t)blist.size();
+  c->n_mp_body = n_mp_body;
   if ((e = upload(&c->blist, blist, s)) != hipSuccess) return hip_fail(c, e, "alloc body list");
   if ((e = c->vmap.ensure(std::max<uint64_t>(4 * c->vmap_words, 16))) != hipSuccess) return hip_fail(c, e, "alloc value map");
   if ((e = c->hits.ensure(std::max<size_t>((size_t)c->hit_words * n * 4, 16))) != hipSuccess)
@@ -691,6 +695,7 @@ int gi_run_staged(gi_ctx* c) {
   B.vmap = (uint32_t*)c->vmap.p;
   B.body_list = (const uint32_t*)c->blist.p;
   B.n_body = c->n_body;
+  B.n_mp_body = c->n_mp_body;
   B.txslots = (Slot*)c->txslots.p;
   {
     // counters (bytes): [0] pool words used, [8] slow bytes used, [16] slow
@@ -790,7 +795,7 @@ int gi_sync(gi_ctx* c) {
       else if (nm == "k_scan_hbm") ab = 4ull * acct[12];
       else if (nm == "k_scan_slow") ab = slow_bytes;
       else if (nm == "k_body") ab = c->raw_all - c->raw_nobody;  // request bodies
-      else if (nm == "k_bparse") ab = c->raw_all - c->raw_nobody;
+      else if (nm == "k_bparse" || nm == "k_mpparse") ab = c->raw_all - c->raw_nobody;
       else if (nm == "k_eval") ab = c->raw_all + (uint64_t)sizeof(gi_verdict) * c->n_req + 4ull * tl.matched_total;
       c->stats.launch_alg_bytes[k] = ab;
       c->stats.launch_steps[k] = nm == "k_scan" ? acct[13] : nm == "k_scan_big" ? acct[14] : nm == "k_scan_hbm" ? acct[15] : 0;

@@ -491,7 +491,7 @@ def _apply_actions(rule: Rule, actions, is_child: bool):
             name, _, val = v.partition("=")
             name = name.strip()
             cl = (name.lower(), val.strip())
-            if cl[0] not in ("ruleremovebyid", "ruleengine", "requestbodyprocessor",
+            if cl[0] not in ("ruleremovebyid", "ruleremovetargetbyid", "ruleengine", "requestbodyprocessor",
                              "requestbodyaccess", "forcerequestbodyvariable"):
                 raise SecLangError("unsupported ctl %s" % name)
             rule.ctls.append(cl)
@@ -1694,6 +1694,7 @@ class Transaction:
         self.skip_after = ""
         self.skip = 0
         self.removed: List[Tuple[int, int]] = []
+        self.removed_targets: List[Tuple[int, int, str, str]] = []
         self.single: Dict[str, bytes] = {k: b"" for k in SINGLE_VARS}
         self.single["REQBODY_ERROR"] = b"0"
         self.single["MULTIPART_STRICT_ERROR"] = b"0"
@@ -1910,6 +1911,19 @@ class Transaction:
                     self.removed.append((int(a), int(b)))
                 else:
                     self.removed.append((int(part), int(part)))
+        elif name == "ruleremovetargetbyid":
+            # [upstream internal/actions/ctl.go]: "ID[-ID];VARIABLE[:key]" ->
+            # tx.RemoveRuleTargetByID: rule.go doEvaluate adds (key) to the
+            # variable's exceptions for rules with that id
+            ids, _, tgt = val.partition(";")
+            ids = ids.strip()
+            if "-" in ids[1:]:
+                a, b = ids.split("-", 1)
+                lo, hi = int(a), int(b)
+            else:
+                lo = hi = int(ids)
+            var, _, key = tgt.strip().partition(":")
+            self.removed_targets.append((lo, hi, var.strip().upper(), key.lower()))
         elif name == "ruleengine":
             self.rule_engine = {"on": "On", "off": "Off", "detectiononly": "DetectionOnly"}[val.lower()]
         elif name == "requestbodyprocessor":
@@ -1954,6 +1968,11 @@ class Transaction:
             self.run_nondisruptive(rule)
         else:
             for rv in rule.variables:
+                dyn = [key for lo, hi, var, key in self.removed_targets
+                       if rule.id and lo <= rule.id <= hi and var == rv.name]
+                if dyn:
+                    rv = RuleVariable(rv.name, rv.key, rv.key_rx, rv.count,
+                                      rv.exceptions + [(key, None) for key in dyn])
                 for k, v in self.get_field(rv):
                     if rule.multimatch:
                         # rule.go executeTransformationsMultimatch: the value,
