@@ -54,13 +54,16 @@ CONFIGS = {
            "config/samples RuleSet x 10k synthetic GET"),
     "c3": ("rulesets/crs_pl1.conf", 50_000, 0.5,
            "CRS-shaped v4 PL1 x mixed GET/POST (50% POST, 4-64 KB bodies: 60% urlencoded, 40% JSON)"),
+    "c5": (None, 256, 1.0,
+           "generated 10k @rx rules + 100k-phrase @pmFromFile (traffic.c5_ruleset) x ~1 MB multipart bodies "
+           "(traffic.c5_batch)"),
 }
 
 
 def _oracle_worker(args):
-    text, blob, idx, exports = args
+    text, blob, idx, exports, files = args
     from oracle import compare, coraza
-    cfg = coraza.parse_seclang(text)
+    cfg = coraza.parse_seclang(text, files)
     data, reqs, headers = blob
     b = gpuinspect.PackedBatch(data, reqs, headers)
     out = {}
@@ -71,19 +74,20 @@ def _oracle_worker(args):
     return time.perf_counter() - t0, out
 
 
-def oracle_sample(text, batch, exports, budget_s=15.0, procs=16, n_max=4000):
+def oracle_sample(text, batch, exports, budget_s=15.0, procs=16, n_max=4000, files=None, calib=100):
     """The CPU oracle over a bounded sample of the batch: (verdicts by request
-    index, wall seconds, processes).  Sized from a 100-request calibration to
-    about budget_s of wall time."""
+    index, wall seconds, processes).  Sized from a `calib`-request calibration
+    to about budget_s of wall time."""
     blob = (batch.data, batch.reqs, batch.headers)
-    dt, _ = _oracle_worker((text, blob, range(100), exports))
-    per = dt / 100
+    calib = min(calib, batch.n_req)
+    dt, _ = _oracle_worker((text, blob, range(calib), exports, files))
+    per = dt / calib
     procs = max(1, min(procs, os.cpu_count() or 1))
-    n_sample = int(min(n_max * procs, max(200, budget_s * procs / max(per, 1e-6)), batch.n_req))
+    n_sample = int(min(n_max * procs, max(min(200, 2 * procs), budget_s * procs / max(per, 1e-6)), batch.n_req))
     chunks = [range(k, n_sample, procs) for k in range(procs)]
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(procs) as pool:
-        outs = pool.map(_oracle_worker, [(text, blob, c, exports) for c in chunks])
+        outs = pool.map(_oracle_worker, [(text, blob, c, exports, files) for c in chunks])
     wall = time.perf_counter() - t0
     verdicts = {}
     for _, o in outs:
@@ -122,12 +126,21 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     rs_file, n_default, post_frac, desc = CONFIGS[args.config]
-    text = open(os.path.join(ROOT, rs_file)).read()
+    files = None
+    if rs_file is None:  # c5: generated ruleset + phrase file
+        text, files = traffic.c5_ruleset()
+    else:
+        text = open(os.path.join(ROOT, rs_file)).read()
     n_req = args.n_req or n_default
-    rs = gpuinspect.Ruleset(text)
+    t_compile = time.perf_counter()
+    rs = gpuinspect.Ruleset(text, data_files=files)
+    t_compile = time.perf_counter() - t_compile
     eng = gpuinspect.Engine(rs, device=local, matched_cap=args.matched_cap)
     t_gen = time.perf_counter()
-    batch = traffic.TrafficGen(shard.shard_seed(traffic.SEED, rank)).batch(n_req, post_frac=post_frac)
+    if args.config == "c5":
+        batch = traffic.c5_batch(n_req, seed=shard.shard_seed(traffic.SEED, rank))
+    else:
+        batch = traffic.TrafficGen(shard.shard_seed(traffic.SEED, rank)).batch(n_req, post_frac=post_frac)
     t_gen = time.perf_counter() - t_gen
     raw = batch.raw_bytes()
     eng.stage(batch)
@@ -194,7 +207,7 @@ def main():
             hbm_traffic = tj["hbm_bytes_per_launch"]
     steps_s = launch_steps.get(dom, 0) / (avg_launch[dom] * 1e-3)
     out = {
-        "metric": "requests inspected/sec (node), CRS v4 PL1",
+        "metric": "requests inspected/sec (node), " + ("generated 10k-rule set" if args.config == "c5" else "CRS v4 PL1"),
         "value": round(value, 1),
         "unit": "requests/s",
         "n_gpus": world,
@@ -237,6 +250,7 @@ def main():
                   "top_rules": sorted(([int(i), int(h)] for i, h in zip(detail["rule_ids"], node_tally["rule_hits"]) if h),
                                       key=lambda x: -x[1])[:8]},
         "gen_s": round(t_gen, 1),
+        "compile_s": round(t_compile, 1),
     }
     # Host-inclusive pass: stage (layout + H2D of pageable numpy buffers) +
     # pipeline + D2H of verdicts and matched ids.  Never `value`.
@@ -254,7 +268,9 @@ def main():
                   "GB/s": round(raw / (t4 - t1) / 1e9, 3),
                   "def": "one pass incl. gi_stage_batch (host layout + H2D, pageable) and gi_fetch_results (D2H), per GPU"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        verdicts, wall, procs = oracle_sample(text, batch, rs.exports)
+        verdicts, wall, procs = oracle_sample(text, batch, rs.exports, files=files,
+                                              calib=2 if args.config == "c5" else 100,
+                                              budget_s=30.0 if args.config == "c5" else 15.0)
         out["cpu_baseline"] = {
             "value": round(len(verdicts) / wall, 1), "unit": "requests/s", "cores": procs, "kind": "port",
             "sample": "%d requests of the benchmark batch, oracle/coraza.py (pure-Python Coraza restatement, "
@@ -263,8 +279,8 @@ def main():
     elif world > 1:
         # every rank checks a small sample of its own batch against the oracle
         from oracle import compare, coraza
-        cfg = coraza.parse_seclang(text)
-        idx = range(0, batch.n_req, max(1, batch.n_req // 128))
+        cfg = coraza.parse_seclang(text, files)
+        idx = range(0, batch.n_req, max(1, batch.n_req // (8 if args.config == "c5" else 128)))
         ps = parity(res, compare.oracle_verdicts(cfg, batch, rs.exports, idx))
         import torch
         t = torch.tensor([ps["n"], ps["mismatches"]], dtype=torch.int64, device="cuda")

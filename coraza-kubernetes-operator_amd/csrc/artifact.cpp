@@ -300,6 +300,9 @@ bool validate_program(const Program& P, std::string* err) {
   for (const DOp& o : P.ops) {
     if ((o.kind == OP_RX || o.kind == OP_PM) && !single_dfa(o.dfa) && o.nfa < 0) return bad("operator automaton");
     if (o.dfa >= 0 && !single_dfa(o.dfa)) return bad("operator automaton index");
+    if (o.ngroups && (o.dfa < 0 || (uint64_t)o.dfa + o.ngroups > P.dfas.size())) return bad("phrase groups");
+    for (uint32_t g = 1; g < o.ngroups; g++)
+      if (!single_dfa(o.dfa + (int32_t)g)) return bad("phrase group automaton");
     if (o.nfa >= 0 && (size_t)o.nfa >= P.nfas.size()) return bad("operator nfa index");
     if (o.tmpl >= 0 && (size_t)o.tmpl >= ntm) return bad("operator template");
     if (o.arg_is_lit && !in(o.lit_off, o.lit_len, nstr)) return bad("operator literal");

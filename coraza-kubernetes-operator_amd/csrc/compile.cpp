@@ -874,6 +874,42 @@ struct Lower {
     P->nfas.push_back(h);
     return (int)P->nfas.size() - 1;
   }
+  // Large phrase sets split into groups whose Aho-Corasick automata stay
+  // below the state cap (a trie has at most 1 + total phrase bytes nodes).
+  static constexpr size_t kPhraseGroupBytes = 40000;
+  static std::vector<std::vector<std::string>> phrase_groups(const std::vector<std::string>& phrases) {
+    std::vector<std::vector<std::string>> g(1);
+    size_t bytes = 0;
+    for (auto& p : phrases) {
+      if (bytes + p.size() > kPhraseGroupBytes && !g.back().empty()) {
+        g.emplace_back();
+        bytes = 0;
+      }
+      g.back().push_back(p);
+      bytes += p.size();
+    }
+    return g;
+  }
+  // the phrase automata of an operator: first DFA id, *ngroups = 0 (one
+  // automaton) or the number of consecutive group automata
+  int phrase_dfas(const std::vector<std::string>& phrases, bool fold, const std::string& key, uint32_t* ngroups) {
+    size_t total = 0;
+    for (auto& p : phrases) total += p.size();
+    *ngroups = 0;
+    if (total <= kPhraseGroupBytes) return phrase_dfa(phrases, fold, key);
+    auto groups = phrase_groups(phrases);
+    std::vector<Dfa> ds(groups.size());
+    std::string err;
+    for (size_t k = 0; k < groups.size(); k++)
+      if (!build_phrase_dfa(groups[k], fold, &ds[k], &err, cap)) unsup(err);
+    int first = -1;
+    for (auto& d : ds) {
+      const int id = add_dfa(d);
+      if (first < 0) first = id;
+    }
+    *ngroups = (uint32_t)groups.size();
+    return first;
+  }
   int phrase_dfa(const std::vector<std::string>& phrases, bool fold, const std::string& key) {
     auto it = dfa_cache.find(key);
     if (it != dfa_cache.end()) return it->second;
@@ -977,12 +1013,12 @@ struct Lower {
         if (sp > pos) phrases.push_back(la.substr(pos, sp - pos));
         pos = sp + 1;
       }
-      o.dfa = phrase_dfa(phrases, true, "pm:" + la);
+      o.dfa = phrase_dfas(phrases, true, "pm:" + la, &o.ngroups);
     } else if (n == "pmfromfile") {
       o.kind = OP_PM;
       std::string key = "pmf:";
       for (auto& p : r.phrases) key.append(p).push_back('\n');
-      o.dfa = phrase_dfa(r.phrases, true, key);
+      o.dfa = phrase_dfas(r.phrases, true, key, &o.ngroups);
     } else if (n == "unconditionalmatch") {
       o.kind = OP_UNCONDITIONAL;
     } else if (n == "nomatch") {
@@ -1479,6 +1515,20 @@ struct Lower {
       for (auto& pe : sb.pats) {
         auto re = std::make_unique<Regex>();
         bool ok;
+        size_t pbytes = 0;
+        for (auto& p : pe.phrases) pbytes += p.size();
+        if (pe.kind != 0 && pbytes > kPhraseGroupBytes) {  // a large phrase set: its group automata
+          if (pe.negate) {  // "no group matches" is not a per-automaton bit: always "maybe"
+            P->always_slots.push_back(pe.slot);
+            continue;
+          }
+          for (auto& g : phrase_groups(pe.phrases)) {
+            Dfa d;
+            if (!build_phrase_dfa(g, pe.kind == 1, &d, &err, cap)) unsup(err);
+            autos.push_back({std::move(d), {&pe}});
+          }
+          continue;
+        }
         if (pe.kind == 0) {
           ok = re_parse(pe.rx, re.get(), &err);
           if (!ok) perr("invalid regex " + pe.rx + ": " + err);

@@ -412,7 +412,8 @@ struct DOp {
   int32_t nfa;         // @rx whose DFA exceeds the state cap: exact NFA tables (DNfa), else -1
   int32_t tmpl;
   uint32_t lit_off, lit_len;
-  uint32_t _pad;
+  uint32_t ngroups;    // @pm / @pmFromFile over a large phrase set: automata dfa .. dfa + ngroups - 1
+                       // (phrase groups, any match), else 0
   int64_t num;
   uint32_t bits[8];    // @validateByteRange allowed-byte bitmap
 };

@@ -2649,6 +2649,7 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
     case OP_RX:
     case OP_PM:
       res = o.nfa >= 0 ? nfa_match(P, o.nfa, s, n) : dfa_match(P, o.dfa, s, n, false);
+      for (uint32_t g = 1; g < o.ngroups && !res; g++) res = dfa_match(P, o.dfa + (int32_t)g, s, n, false);
       break;
     case OP_UNCONDITIONAL:
       res = true;
@@ -4624,8 +4625,9 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
         hit = true;  // chain overflow: maybe
       } else if ((o.kind == OP_RX || o.kind == OP_PM || (o.kind == OP_CONTAINS && o.arg_is_lit)) && o.nfa < 0 &&
                  o.dfa >= 0 && !P.dfas[o.dfa].multi) {
-        const DDfa d = P.dfas[o.dfa];
-        hit = wave_dfa_match(P, d, cur, cn, kb_lds) != (o.negate != 0);
+        bool m = false;
+        for (uint32_t g = 0; g < max(o.ngroups, 1u) && !m; g++) m = wave_dfa_match(P, P.dfas[o.dfa + (int32_t)g], cur, cn, kb_lds);
+        hit = m != (o.negate != 0);
       } else if (o.kind == OP_VALIDATE_BYTE_RANGE || o.kind == OP_VALIDATE_URL_ENCODING || o.kind == OP_VALIDATE_UTF8) {
         hit = wave_validate(o, cur, cn) != (o.negate != 0);
       } else {  // any other operator: lane 0, side-effect free

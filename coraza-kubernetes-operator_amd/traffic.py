@@ -289,3 +289,113 @@ def c2_batch(n: int = 1_000_000, seed: int = SEED):
 
 def c3_batch(n: int = 100_000, seed: int = SEED):
     return TrafficGen(seed).batch(n, post_frac=0.5)
+
+
+# ------------------------------------------------------------------- C5
+# BASELINE.json configs[4]: a large custom ruleset (10k generated @rx rules +
+# a 100k-phrase @pmFromFile list) over ~1 MB multipart bodies.  Seeded; the
+# rule text, the phrase file and the bodies are pure functions of the seed.
+C5_ALPHA = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
+
+
+def _c5_words(rng, n, lo=4, hi=9):
+    lens = rng.integers(lo, hi, n)
+    chars = C5_ALPHA[rng.integers(0, 26, int(lens.sum()))].tobytes()
+    out, o = [], 0
+    for ln in lens:
+        out.append(chars[o:o + ln])
+        o += ln
+    return out
+
+
+def _c5_material(seed: int, n_rx: int, n_phrases: int):
+    """The seeded rule material shared by the ruleset and the traffic: the
+    rule vocabulary, per rule (kind, words), and the phrase list."""
+    rng = np.random.Generator(np.random.PCG64(seed + 5))
+    vocab = [w.decode() for w in _c5_words(rng, 4096)]
+    rules = []
+    for _ in range(n_rx):
+        w = [vocab[int(k)] for k in rng.integers(0, len(vocab), 3)]
+        rules.append((int(rng.integers(0, 5)), w))
+    phrases = sorted(set(w.decode() for w in _c5_words(rng, n_phrases, 6, 12)))
+    return vocab, rules, phrases
+
+
+def c5_ruleset(n_rx: int = 10_000, n_phrases: int = 100_000, seed: int = SEED):
+    """(SecLang text, {file name: bytes}): n_rx @rx rules over ARGS /
+    ARGS_NAMES / FILES_NAMES (t:lowercase), one @pmFromFile rule over ARGS
+    with n_phrases phrases, anomaly-scored, blocking at score >= 5."""
+    vocab, rules, phrases = _c5_material(seed, n_rx, n_phrases)
+    lines = ["SecRuleEngine On", "SecRequestBodyAccess On", "SecRequestBodyLimit 4194304",
+             'SecAction "id:1,phase:1,pass,nolog,setvar:tx.anomaly_score=0"']
+    for i, (kind, w) in enumerate(rules):
+        if kind == 0:
+            pat = "%s[-_.]?%s" % (w[0], w[1])
+        elif kind == 1:
+            pat = "(?:%s|%s)\\d{2,4}" % (w[0], w[1])
+        elif kind == 2:
+            pat = "\\b%s\\s*=\\s*%s" % (w[0], w[1])
+        elif kind == 3:
+            pat = "%s[a-z]{0,3}%s" % (w[0][:4], w[1][:4])
+        else:
+            pat = "^%s|%s$" % (w[0], w[2])
+        lines.append('SecRule ARGS|ARGS_NAMES|FILES_NAMES "@rx %s" "id:%d,phase:2,pass,t:none,t:lowercase,'
+                     'setvar:tx.anomaly_score=+1"' % (pat, 100000 + i))
+    lines.append('SecRule ARGS "@pmFromFile c5_phrases.txt" "id:99000,phase:2,pass,t:none,t:lowercase,'
+                 'setvar:tx.anomaly_score=+2"')
+    lines.append('SecRule TX:ANOMALY_SCORE "@ge 5" "id:99100,phase:2,deny,status:403"')
+    files = {"c5_phrases.txt": ("\n".join(["# generated"] + phrases) + "\n").encode()}
+    return "\n".join(lines) + "\n", files
+
+
+def _c5_snippet(rng, rules, phrases) -> bytes:
+    """A string some rule (or the phrase list) matches."""
+    if rng.random() < 0.5:
+        return phrases[int(rng.integers(0, len(phrases)))].upper().encode()
+    kind, w = rules[int(rng.integers(0, len(rules)))]
+    return {0: "%s-%s" % (w[0], w[1]), 1: "%s%d" % (w[0], 100 + int(rng.integers(0, 899))),
+            2: "%s = %s" % (w[0], w[1]), 3: "%sxy%s" % (w[0][:4], w[1][:4]), 4: "%s" % w[2]}[kind].encode()
+
+
+def c5_body(rng, body_bytes: int, vocab, boundary: bytes, rules=None, phrases=None, hit_rate: float = 0.01):
+    """~body_bytes of multipart/form-data: a few file parts (their content is
+    only sized by coraza) and ~1 KB form fields of vocabulary text, a
+    hit_rate fraction of them carrying a rule-matching snippet."""
+    parts, size = [], 0
+    k = 0
+    while size < body_bytes:
+        if k % 64 == 7:
+            fn = b"%s.%s" % (vocab[int(rng.integers(0, len(vocab)))], [b"txt", b"jpg", b"php"][k % 3])
+            data = C5_ALPHA[rng.integers(0, 26, int(rng.integers(16384, 65536)))].tobytes()
+            p = (b'Content-Disposition: form-data; name="up%d"; filename="%s"\r\nContent-Type: '
+                 b"application/octet-stream\r\n\r\n" % (k, fn) + data)
+        else:
+            words = [vocab[int(x)] for x in rng.integers(0, len(vocab), int(rng.integers(60, 200)))]
+            if rules and rng.random() < hit_rate:
+                words.insert(int(rng.integers(0, len(words) + 1)), _c5_snippet(rng, rules, phrases))
+            data = b" ".join(words)
+            p = b'Content-Disposition: form-data; name="f%d"\r\n\r\n' % k + data
+        parts.append(b"--" + boundary + b"\r\n" + p + b"\r\n")
+        size += len(parts[-1])
+        k += 1
+    return b"".join(parts) + b"--" + boundary + b"--\r\n"
+
+
+def c5_batch(n: int, body_bytes: int = 1 << 20, seed: int = SEED, n_rx: int = 10_000,
+             n_phrases: int = 100_000, hit_rate: float = 0.01) -> "gpuinspect.PackedBatch":
+    """n multipart requests for c5_ruleset(n_rx, n_phrases, seed)."""
+    vocab_s, rules, phrases = _c5_material(seed, n_rx, n_phrases)
+    rng = np.random.Generator(np.random.PCG64(seed + 55))
+    vocab = [w.encode() for w in vocab_s] + _c5_words(rng, 4096)  # the rules' vocabulary and unrelated words
+    parts, nh = [], np.empty(n, np.int64)
+    ports = np.empty(n, np.int64)
+    for i in range(n):
+        b = b"c5b%08x" % int(rng.integers(0, 1 << 31))
+        body = c5_body(rng, body_bytes, vocab, b, rules, phrases, hit_rate)
+        parts += [b"POST", b"/upload?id=%d" % i, b"HTTP/1.1", body, TrafficGen._client(None, i, ports)]
+        hs = [(b"Host", b"files.example.com"), (b"User-Agent", USER_AGENTS[i % len(USER_AGENTS)]),
+              (b"Content-Type", b"multipart/form-data; boundary=" + b), (b"Content-Length", str(len(body)).encode())]
+        for k, v in hs:
+            parts += [k, v]
+        nh[i] = len(hs)
+    return gpuinspect.pack_parts(parts, nh, ports)

@@ -1,0 +1,68 @@
+"""Large rulesets (BASELINE.json configs[4], C5): generated @rx rules, a
+phrase file split into phrase-group automata, multipart bodies -- and the
+HBM-table scan launch (k_scan<false,false>) for automata beyond LDS.
+
+CPU: generator determinism and compile plan.  GPU: a scaled C5 mix vs the
+oracle, and the CRS mix with every job forced onto global tables
+(GI_SCAN_HBM=1), bit-exact."""
+import os
+
+import pytest
+
+import gpuinspect
+import traffic
+from oracle import compare, coraza
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def small_c5():
+    return traffic.c5_ruleset(n_rx=300, n_phrases=12000)
+
+
+def test_c5_generator_deterministic():
+    a = traffic.c5_ruleset(n_rx=50, n_phrases=500)
+    b = traffic.c5_ruleset(n_rx=50, n_phrases=500)
+    assert a == b and a[0].count("@rx ") == 50
+    x = traffic.c5_batch(2, body_bytes=20000, n_rx=50, n_phrases=500)
+    y = traffic.c5_batch(2, body_bytes=20000, n_rx=50, n_phrases=500)
+    assert bytes(x.data) == bytes(y.data) and x.raw_bytes() > 40000
+
+
+def test_c5_small_compiles_with_phrase_groups():
+    text, files = small_c5()
+    rs = gpuinspect.Ruleset(text, data_files=files)
+    # 300 exact @rx automata + phase-A unions + >= 3 phrase groups twice (operator + phase A)
+    assert rs.info["n_rules"] == 303 and rs.info["n_dfas"] >= 306
+    coraza.parse_seclang(text, files)
+
+
+@pytest.mark.gpu
+def test_gpu_c5_small_parity():
+    text, files = small_c5()
+    batch = traffic.c5_batch(8, body_bytes=65536, n_rx=300, n_phrases=12000, hit_rate=0.2)
+    rs = gpuinspect.Ruleset(text, data_files=files)
+    res = gpuinspect.Engine(rs).inspect(batch)
+    cfg = coraza.parse_seclang(text, files)
+    verdicts = compare.oracle_verdicts(cfg, batch, rs.exports)
+    bad = compare.compare(res, verdicts)
+    assert not bad, bad[:3]
+    assert any(len(v.matched) > 2 for v in verdicts.values())
+
+
+@pytest.mark.gpu
+def test_gpu_scan_hbm_forced_parity():
+    text = open(os.path.join(ROOT, "rulesets", "crs_pl1.conf")).read()
+    batch = traffic.TrafficGen(traffic.SEED + 3).batch(1500, post_frac=0.2)
+    os.environ["GI_SCAN_HBM"] = "1"
+    try:
+        rs = gpuinspect.Ruleset(text)
+        eng = gpuinspect.Engine(rs)
+        res = eng.inspect(batch)
+        names = [ln["name"] for ln in eng.stats()["launches"]]
+    finally:
+        del os.environ["GI_SCAN_HBM"]
+    assert "k_scan_hbm" in names and "k_scan" not in names, names
+    cfg = coraza.parse_seclang(text)
+    bad = compare.compare(res, compare.oracle_verdicts(cfg, batch, rs.exports))
+    assert not bad, bad[:3]
