@@ -503,7 +503,7 @@ void parse_operator(std::string opstr, IrRule* rule) {
                                 "endswith", "within", "eq", "ge", "gt", "le", "lt",
                                 "unconditionalmatch", "nomatch", "validatebyterange",
                                 "validateurlencoding", "validateutf8encoding", "pmfromfile", "ipmatch",
-                                "ipmatchfromfile", "ipmatchf"};
+                                "ipmatchfromfile", "ipmatchf", "detectsqli", "detectxss"};
   bool ok = false;
   for (auto* k : known)
     if (rule->op_name == k) ok = true;
@@ -1019,6 +1019,10 @@ struct Lower {
       std::string key = "pmf:";
       for (auto& p : r.phrases) key.append(p).push_back('\n');
       o.dfa = phrase_dfas(r.phrases, true, key, &o.ngroups);
+    } else if (n == "detectsqli") {
+      o.kind = OP_DETECT_SQLI;  // [upstream] detect_sqli.go (libinjection-go v0.2.2 IsSQLi; csrc/libinj.h)
+    } else if (n == "detectxss") {
+      o.kind = OP_DETECT_XSS;   // detect_xss.go (IsXSS)
     } else if (n == "unconditionalmatch") {
       o.kind = OP_UNCONDITIONAL;
     } else if (n == "nomatch") {
@@ -1285,12 +1289,11 @@ struct Lower {
   bool capture_seen = true;  // some rule, macro or export can read TX:0-TX:9 (capture_observable)
 
   int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
-    // multiMatch links test every intermediate value, not the one a stream
-    // produces: interpreter only
-    if (!r.has_op || no_scan || r.multimatch) return -1;
+    if (!r.has_op || no_scan) return -1;
     const std::string& n = r.op_name;
     bool scannable = n == "rx" || n == "pm" || n == "pmfromfile" || n == "validatebyterange" || n == "validateurlencoding" ||
-                     n == "validateutf8encoding" || (n == "contains" && r.op_arg.find("%{") == std::string::npos);
+                     n == "validateutf8encoding" || n == "detectsqli" || n == "detectxss" ||
+                     (n == "contains" && r.op_arg.find("%{") == std::string::npos);
     if (!scannable) return -1;
     bool bodydep = false, residual = false;
     for (auto& v : r.vars) {
@@ -1303,6 +1306,12 @@ struct Lower {
       if (v.name == "ARGS" || v.name == "ARGS_POST" || v.name == "ARGS_NAMES" || v.name == "ARGS_POST_NAMES")
         bodydep = true;
     }
+    // multiMatch (rule.go executeTransformationsMultimatch) tests the value
+    // after every prefix of the chain: its patterns go into one stream per
+    // prefix, all on the link's slot (the bit ORs the candidates: exact
+    // superset).  The residual clear-bit path and k_body test final values
+    // only, so a multiMatch link with residual targets stays interpreter-only.
+    if (r.multimatch && residual) return -1;
     const int32_t slot = (int32_t)P->n_hit_slots++;
     if (bodydep) *flags |= RF_BODYDEP;
     if (residual) *flags |= RF_RESIDUAL;
@@ -1350,7 +1359,8 @@ struct Lower {
         f.exc_begin = vr.exc_begin;
         f.exc_count = vr.exc_count;
       }
-      const std::string skey((const char*)&P->tchains[d.tchain_off], d.tchain_len);
+      for (uint32_t plen = r.multimatch ? 0 : d.tchain_len; plen <= d.tchain_len; plen++) {
+      const std::string skey((const char*)&P->tchains[d.tchain_off], plen);
       std::string fkey((const char*)&f, 5);
       if (f.key_mode == 1) fkey.append((const char*)&P->strpool[f.key_off], f.key_len);
       fkey.append("|" + std::to_string(f.key_dfa) + "|");
@@ -1370,7 +1380,7 @@ struct Lower {
           StreamBuild sb;
           sb.s = DStream{};
           sb.s.tchain_off = d.tchain_off;
-          sb.s.tchain_len = d.tchain_len;
+          sb.s.tchain_len = plen;
           sindex[k] = sbuild.size();
           sbuild.push_back(sb);
           it = sindex.find(k);
@@ -1402,7 +1412,8 @@ struct Lower {
         }
       }
       StreamBuild& sb = sbuild[si];
-      if (o.kind == OP_VALIDATE_BYTE_RANGE || o.kind == OP_VALIDATE_URL_ENCODING || o.kind == OP_VALIDATE_UTF8) {
+      if (o.kind == OP_VALIDATE_BYTE_RANGE || o.kind == OP_VALIDATE_URL_ENCODING || o.kind == OP_VALIDATE_UTF8 ||
+          o.kind == OP_DETECT_SQLI || o.kind == OP_DETECT_XSS) {
         bool merged = false;
         for (auto& sv : sb.vals)
           if (sv.slot == (uint32_t)slot) sv.fmask |= 1ull << sb.gids[fid], merged = true;
@@ -1445,6 +1456,7 @@ struct Lower {
         pe.phrases.push_back(r.op_arg);
       }
       sb.pats.push_back(pe);
+      }  // prefix streams
     }
     return slot;
   }

@@ -120,6 +120,8 @@ enum OpKind : uint8_t {
   OP_VALIDATE_URL_ENCODING,
   OP_VALIDATE_UTF8,
   OP_IPMATCH,  // @ipMatch / @ipMatchFromFile: DOp.lit_off/lit_len = GI_IPNET_BYTES records in strpool
+  OP_DETECT_SQLI,  // @detectSQLi (libinj.h; phase A: a DScanVal kind, evaluated in k_stream)
+  OP_DETECT_XSS,   // @detectXSS
 };
 // @ipMatch network record (strpool, byte-addressed): [0] 4 = IPv4, 16 = IPv6;
 // [1] prefix bits; [2..18) network address (IPv4 in bytes 2..6)
@@ -374,7 +376,7 @@ struct DPat {
   uint32_t slot;      // hit slot of the rule link
 };
 
-struct DScanVal {     // @validateByteRange / @validateUrlEncoding / @validateUtf8Encoding
+struct DScanVal {     // @validateByteRange / @validateUrlEncoding / @validateUtf8Encoding / @detectSQLi / @detectXSS
   uint8_t kind;
   uint8_t negate;
   uint8_t _pad[2];

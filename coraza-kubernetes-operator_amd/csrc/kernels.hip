@@ -17,6 +17,7 @@
 #include <cstdio>
 
 #include "gi_kernels.h"
+#include "libinj.h"
 
 namespace gi {
 
@@ -2660,6 +2661,12 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
     case OP_NOMATCH:
       res = false;
       break;
+    case OP_DETECT_SQLI:  // [upstream] detect_sqli.go: libinjection.IsSQLi (capture of the fingerprint is unobservable here)
+      res = li_detect_sqli(s, n);
+      break;
+    case OP_DETECT_XSS:  // detect_xss.go: libinjection.IsXSS
+      res = li_detect_xss(s, n);
+      break;
     case OP_VALIDATE_BYTE_RANGE:
       for (uint32_t i = 0; i < n; i++)
         if (!((o.bits[s[i] >> 5] >> (s[i] & 31)) & 1)) { res = true; break; }
@@ -3175,6 +3182,8 @@ __device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
 }
 
 __device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
+  if (kind == OP_DETECT_SQLI) return li_detect_sqli(s, n);
+  if (kind == OP_DETECT_XSS) return li_detect_xss(s, n);
   if (kind == OP_VALIDATE_BYTE_RANGE) {
     for (uint32_t i = 0; i < n; i++)
       if (!((bits[s[i] >> 5] >> (s[i] & 31)) & 1)) return true;

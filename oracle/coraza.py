@@ -36,7 +36,7 @@ import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
-from . import goregex, multipart
+from . import goregex, libinjection, multipart
 
 # ---------------------------------------------------------------------------
 # Errors
@@ -420,7 +420,7 @@ def _parse_operator(opstr: str, data_files=None) -> Operator:
                 ok[a] = True
         op.byte_ok = ok
     elif name_l in ("unconditionalmatch", "nomatch", "validateurlencoding",
-                    "validateutf8encoding"):
+                    "validateutf8encoding", "detectsqli", "detectxss"):
         pass
     elif name_l == "ipmatch":
         op.nets = ipmatch_networks(data)
@@ -1868,6 +1868,13 @@ class Transaction:
             res = _invalid_url_encoding(value)
         elif n == "ipmatch":
             res = ipmatch(op.nets, value)
+        elif n == "detectsqli":
+            # detect_sqli.go: libinjection.IsSQLi; the fingerprint is captured as TX.0
+            res, fp = libinjection.is_sqli(value)
+            if res and rule.capture:
+                self.tx[b"0"] = fp.encode()
+        elif n == "detectxss":
+            res = libinjection.is_xss(value)  # detect_xss.go
         elif n == "validateutf8encoding":
             try:
                 value.decode("utf-8")

@@ -55,7 +55,7 @@ def test_compile_rejects_like_oracle(text, kind):
 
 def test_unsupported_is_flagged_not_guessed():
     with pytest.raises(gpuinspect.SecLangError) as e:
-        gpuinspect.Ruleset('SecRule ARGS "@detectSQLi" "id:1,deny"')
+        gpuinspect.Ruleset('SecRule ARGS "@verifyCC \\d{13,16}" "id:1,deny"')
     assert e.value.code == gpuinspect.GI_EUNSUPPORTED
 
 
@@ -151,12 +151,17 @@ def test_pmfromfile_missing_file_is_a_parse_error():
     assert "allow.data" in str(e.value)
 
 
-def test_multimatch_links_are_interpreter_only():
-    text = ('SecRule ARGS "@rx ^abc$" "id:1,phase:2,pass,multiMatch,t:lowercase"\n'
-            'SecRule ARGS "@rx ^abc$" "id:2,phase:2,pass,t:lowercase"')
+def test_multimatch_links_scan_prefix_streams():
+    # multiMatch links are phase-A scanned on every prefix of their chain (one
+    # stream per prefix, one slot); with a residual target (REQUEST_BODY) they
+    # stay interpreter-only (the clear-bit path tests final values only)
+    text = ('SecRule ARGS "@rx ^abc$" "id:1,phase:2,pass,multiMatch,t:lowercase,t:trim"\n'
+            'SecRule ARGS "@rx ^abc$" "id:2,phase:2,pass,t:lowercase"\n'
+            'SecRule ARGS|REQUEST_BODY "@rx ^abc$" "id:3,phase:2,pass,multiMatch,t:lowercase"')
     coraza.parse_seclang(text)
     rs = gpuinspect.Ruleset(text)
-    assert rs.info["n_rules"] == 2 and rs.info["n_hit_slots"] == 1  # only rule 2 is phase-A scanned
+    assert rs.info["n_rules"] == 3 and rs.info["n_hit_slots"] == 2
+    assert rs.info["n_scan_streams"] >= 3  # (), (lowercase), (lowercase, trim)
 
 
 # Flag groups persist across '|' to the end of the enclosing group (Go

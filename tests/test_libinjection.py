@@ -1,0 +1,153 @@
+"""@detectSQLi / @detectXSS (libinjection-go v0.2.2 restated; /root/reference/go.mod:24).
+
+Pins:
+* the reference's own KATs (test/integration/coreruleset_test.go:121-127):
+  `1 UNION SELECT username FROM users` is SQLi (CRS 942100), the XSS payload
+  `<script>alert(1)</script>` is XSS (941100), `hello world` is neither;
+* everything else is PARITY UNPINNED against libinjection-go (its keyword /
+  fingerprint tables are absent; libinj_tables.py holds the authored ones).
+
+CPU: the device source (csrc/libinj.h) compiled for the host
+(tests/native/libinj_host.cpp) against oracle/libinjection.py on a seeded
+token-soup corpus, and the fingerprint grammar matcher against the oracle's
+regular expressions exhaustively up to 4 tokens.  GPU: rules with both
+operators (plain, negated, multiMatch prefix streams, a header target) per
+request against the oracle.
+"""
+import ctypes
+import itertools
+import os
+import random
+import subprocess
+
+import pytest
+
+import gpuinspect
+from oracle import compare, coraza
+from oracle import libinjection as L
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+FRAGMENTS = [
+    b"'", b'"', b"`", b"--", b"-- ", b"#", b"/*", b"*/", b"/*!", b"1", b"0x1f", b"0b1", b"select", b"SELECT", b"union",
+    b"UNION ALL", b"or", b"and", b"=", b"(", b")", b",", b";", b" ", b" ", b"@@version", b"@a", b"@`x`", b"$$", b"$x$",
+    b"$1.5", b"e'", b"n'", b"q'[", b"b'01'", b"x'ab'", b"\\N", b"\\", b".", b"1e", b"1.5", b"1.0d", b"sleep", b"user",
+    b"in", b"not in", b"like", b"collate", b"utf8_bin", b"{", b"}", b"[a]", b"<", b">", b"<=>", b"!=", b"::", b"int",
+    b"from", b"where", b"order by", b"group by", b"into outfile", b"exec", b"if", b"sp_password", b"\n", b"\t", b"\x00",
+    b"\xa0", b"\xff", b"u&'", b"information_schema.tables", b"abc", b"x", b"!", b"~", b"+", b"-", b"<script>", b"<img",
+    b" src=", b"onerror=", b"javascript:", b"&#x6A;", b"&#106;", b"<!--", b"-->", b"<!DOCTYPE", b"<![CDATA[", b"]]>",
+    b"<%", b"%>", b"<?", b"xmlns", b"style=", b"href=", b"<svg", b"<a ", b"/>", b"</", b"data:", b"vbscript:", b"[if",
+    b"&#x", b"&#", b"attributename=", b"import", b"ENTITY", b"<xml", b"!-", b"-!>", b"\x00\x00",
+]
+
+KNOWN = [  # (value, sqli, xss)
+    (b"1 UNION SELECT username FROM users", True, False),   # coreruleset_test.go:121 (942100)
+    (b"<script>alert(1)</script>", False, True),            # coreruleset_test.go:124 (941100)
+    (b"hello world", False, False),                          # coreruleset_test.go:127
+    (b"1' OR '1'='1", True, False),
+    (b"admin' or 1=1--", True, False),
+    (b"1 AND SLEEP(5)", True, False),
+    (b"/*!union*/ select", True, False),
+    (b"<img src=x onerror=alert(1)>", False, True),
+    (b"\" onmouseover=\"alert(1)", False, True),
+    (b"<a href=\"javascript:alert(1)\">x</a>", False, True),
+    (b"<!DOCTYPE html>", False, True),
+    (b"Mozilla/5.0 (X11; Linux x86_64) AppleWebKit/537.36 (KHTML, like Gecko)", False, False),
+    (b"", False, False),
+]
+
+
+def corpus(seed: int, n: int):
+    rng = random.Random(seed)
+    out = [v for v, _, _ in KNOWN]
+    while len(out) < n:
+        if rng.random() < 0.1:
+            out.append(bytes(rng.randrange(256) for _ in range(rng.randint(0, 12))))
+        else:
+            out.append(b"".join(rng.choice(FRAGMENTS) for _ in range(rng.randint(1, 9))))
+    return out
+
+
+@pytest.mark.parametrize("v,sqli,xss", KNOWN)
+def test_oracle_known(v, sqli, xss):
+    assert L.is_sqli(v)[0] == sqli
+    assert L.is_xss(v) == xss
+
+
+def test_oracle_fingerprints():
+    assert L.is_sqli(b"1 UNION SELECT username FROM users") == (True, "1UEnk")
+    assert L.is_sqli(b"admin' or 1=1--") == (True, "s&1c")
+    assert L.is_sqli(b"/*!union*/")[1] == "X"
+
+
+@pytest.fixture(scope="module")
+def host_lib(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("li") / "libinj_host.so")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-o", out,
+                    os.path.join(HERE, "native", "libinj_host.cpp")], check=True)
+    return ctypes.CDLL(out)
+
+
+def test_device_source_matches_oracle(host_lib):
+    bad = []
+    for v in corpus(11, 6000):
+        a, b = L.is_sqli(v)[0], bool(host_lib.li_host_sqli(v, len(v)))
+        c, d = L.is_xss(v), bool(host_lib.li_host_xss(v, len(v)))
+        if a != b or c != d:
+            bad.append((v, a, b, c, d))
+    assert not bad, bad[:10]
+
+
+def test_fingerprint_grammar_exhaustive(host_lib):
+    alpha = "1SNVKUBETFO&CA(){}.,:;?X\\"
+    bad = []
+    for n in range(1, 5):
+        for t in itertools.product(alpha, repeat=n):
+            f = "".join(t)
+            if L.fp_blacklisted(f) != bool(host_lib.li_host_fp_black(f.encode(), n)):
+                bad.append(f)
+    assert not bad, bad[:10]
+
+
+def _rules():
+    return "\n".join([
+        "SecRuleEngine On",
+        'SecRule ARGS_GET "@detectSQLi" "id:1,phase:1,pass,nolog,t:none"',
+        'SecRule ARGS_GET "@detectXSS" "id:2,phase:1,pass,nolog,t:none"',
+        'SecRule ARGS_GET|ARGS_GET_NAMES "@detectSQLi" "id:3,phase:2,pass,nolog,capture,t:none,t:urlDecodeUni,'
+        't:lowercase,multiMatch,setvar:tx.sqli=+1"',
+        'SecRule ARGS_GET "!@detectXSS" "id:4,phase:2,pass,nolog,t:none,t:htmlEntityDecode"',
+        'SecRule REQUEST_HEADERS:User-Agent "@detectXSS" "id:5,phase:1,pass,nolog,t:none,t:urlDecodeUni"',
+        'SecRule ARGS_GET "@detectXSS" "id:6,phase:2,pass,nolog,t:none,t:utf8toUnicode,t:urlDecodeUni,'
+        't:htmlEntityDecode,t:jsDecode,t:cssDecode,t:removeNulls,multiMatch,setvar:tx.xss=+1"',
+    ]) + "\n"
+
+
+def test_compile_detect_ops():
+    rs = gpuinspect.Ruleset(_rules(), tx_exports=["sqli", "xss"])
+    assert rs.info["n_hit_slots"] >= 6  # every link is phase-A scanned (multiMatch through prefix streams)
+    coraza.parse_seclang(_rules())
+
+
+def _esc(v: bytes) -> bytes:
+    return b"".join(b"%%%02X" % c for c in v)
+
+
+@pytest.mark.gpu
+def test_gpu_detect_parity():
+    text = _rules()
+    rs = gpuinspect.Ruleset(text, tx_exports=["sqli", "xss"])
+    eng = gpuinspect.Engine(rs)
+    vals = corpus(5, 3000)
+    txs = []
+    for k, v in enumerate(vals):
+        t = gpuinspect.Transaction(method=b"GET", uri=b"/p?v=" + _esc(v) + b"&" + _esc(vals[k - 1][:8]) + b"=1")
+        t.add_request_header(b"User-Agent", _esc(v[:40]))
+        txs.append(t)
+    batch = gpuinspect.pack(txs)
+    res = eng.inspect(batch)
+    orc = compare.oracle_verdicts(coraza.parse_seclang(text), batch, rs.exports)
+    bad = compare.compare(res, orc)
+    assert not bad, bad
+    hits = sum(1 for i in range(batch.n_req) if 1 in res.matched_rules(i))
+    assert hits > 50  # the corpus exercises the detector
