@@ -7,7 +7,7 @@ all-gather of the per-GPU tally (7 counters + score histogram + per-rule
 match counts).  Requests are sharded with no data-path collective: each rank
 inspects its own batch (weak scaling).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3] [--n-req R]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5] [--n-req R]
 
 N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).
 Prints ONE JSON line on rank 0.
@@ -54,6 +54,9 @@ CONFIGS = {
            "config/samples RuleSet x 10k synthetic GET"),
     "c3": ("rulesets/crs_pl1.conf", 50_000, 0.5,
            "CRS-shaped v4 PL1 x mixed GET/POST (50% POST, 4-64 KB bodies: 60% urlencoded, 40% JSON)"),
+    "c4": ("rulesets/crs_pl4.conf", 50_000, 0.5,
+           "CRS-shaped v4 PL4 (blocking paranoia 4: +35 PL2-4 rules, @detectSQLi/@detectXSS) x C3 mix "
+           "(50% POST 4-64 KB urlencoded/JSON); SURVEY C4 = 10M across 8 GPUs = this batch per GPU, repeated"),
     "c5": (None, 256, 1.0,
            "generated 10k @rx rules + 100k-phrase @pmFromFile (traffic.c5_ruleset) x ~1 MB multipart bodies "
            "(traffic.c5_batch)"),

@@ -1269,6 +1269,7 @@ struct Lower {
     std::vector<DScanVal> vals;
   };
   std::vector<StreamBuild> sbuild;
+  uint32_t n_det = 0;  // streams with detect vals (DStream.det_id)
   std::map<std::string, size_t> sindex;
 
   // body collections phase A does not scan (XML stays empty: its processor is not implemented)
@@ -1605,6 +1606,13 @@ struct Lower {
       P->svals.insert(P->svals.end(), sb.vals.begin(), sb.vals.end());
       s.job_begin = (uint32_t)P->jobs.size();
       s.collapse = 1;  // cleared below by any automaton that tells non-ASCII runes apart
+      s.det_id = 0xFF;
+      for (const DScanVal& v : sb.vals)
+        if (v.kind == OP_DETECT_SQLI || v.kind == OP_DETECT_XSS) {
+          if (n_det >= GI_MAX_DET_STREAMS) unsup("more than 32 phase-A transformation chains with @detectSQLi/@detectXSS");
+          s.det_id = (uint8_t)n_det++;
+          break;
+        }
       P->streams.push_back(s);
       if (!first_s) js << ",";
       first_s = false;

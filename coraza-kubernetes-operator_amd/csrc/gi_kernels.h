@@ -63,6 +63,12 @@ struct DBatch {
   uint8_t* slow_bytes;
   uint64_t slow_bytes_cap;
   unsigned long long* slow_used;
+  void* det;                  // DetEnt[det_cap]: @detectSQLi/@detectXSS candidates (k_stream -> k_detect)
+  uint32_t* det_count;
+  uint32_t det_cap;
+  uint8_t* det_bytes;
+  uint64_t det_bytes_cap;
+  unsigned long long* det_used;
   unsigned long long* diag;   // optional diagnostic counters (gi_stats.diag)
   uint32_t* dbg;              // debug-build bounds-violation record (-DGI_DEBUG)
   unsigned long long* prof;   // GI_PROF=1: k_eval cycle / rule counters (stderr at gi_sync)

@@ -251,8 +251,10 @@ struct DStream {
   uint8_t kind_mask;  // union of the field filters' kinds (1 << FieldKind)
   uint8_t collapse;   // every automaton maps all non-ASCII runes to one class: values are
                       // rune-collapsed (each non-ASCII rune -> GI_RUNE_MARK) instead of slow
-  uint8_t _pad[2];
+  uint8_t det_id;     // index in DProgram.det_streams if some val is @detectSQLi/@detectXSS, else 0xFF
+  uint8_t _pad;
 };
+#define GI_MAX_DET_STREAMS 32
 
 struct DFilter {
   uint8_t single;     // SingleId, or GI_NO_SINGLE for a field filter
@@ -521,6 +523,8 @@ struct DProgram {
   uint8_t mv_used;              // some target / macro reads MATCHED_VAR(S)(_NAME(S)): k_eval records matches
   uint8_t _pad;
   uint64_t body_limit;
+  uint32_t n_det_streams;       // streams with @detectSQLi/@detectXSS vals (k_detect entries carry a mask)
+  uint32_t det_streams[GI_MAX_DET_STREAMS];
 };
 
 }  // namespace gi

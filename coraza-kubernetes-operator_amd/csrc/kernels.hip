@@ -2662,7 +2662,7 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
       res = false;
       break;
     case OP_DETECT_SQLI:  // [upstream] detect_sqli.go: libinjection.IsSQLi (capture of the fingerprint is unobservable here)
-      res = li_detect_sqli(s, n);
+      res = li_detect_sqli(s, n, (LiSqli*)t.mt);  // tokenizer state in the request's macro scratch (>= 512 B)
       break;
     case OP_DETECT_XSS:  // detect_xss.go: libinjection.IsXSS
       res = li_detect_xss(s, n);
@@ -3182,8 +3182,6 @@ __device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
 }
 
 __device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
-  if (kind == OP_DETECT_SQLI) return li_detect_sqli(s, n);
-  if (kind == OP_DETECT_XSS) return li_detect_xss(s, n);
   if (kind == OP_VALIDATE_BYTE_RANGE) {
     for (uint32_t i = 0; i < n; i++)
       if (!((bits[s[i] >> 5] >> (s[i] & 31)) & 1)) return true;
@@ -3817,11 +3815,74 @@ __device__ uint64_t item_gmask(const DProgram& P, const Item& it) {
 }
 
 // The stream's validate operators (@validateByteRange / UrlEncoding / Utf8Encoding).
+// @detectSQLi / @detectXSS candidate (k_stream -> k_detect): the value bytes
+// are copied to the detect arena; `mask` = the detect streams (DStream.det_id)
+// whose vals test this value (several when chains left it unchanged).
+struct DetEnt {
+  uint32_t req, vix, mask, len;
+  uint64_t off, gm;  // arena byte offset; the item's global filter mask
+};
+
+// every detect val of the masked streams that admits the value (gm): its bit
+// becomes "maybe" (list overflow: exact, k_eval re-evaluates)
+__device__ void det_maybe(const DProgram& P, const DBatch& B, uint32_t r, uint32_t vix, uint64_t gm, uint32_t mask) {
+  for (uint32_t d = 0; d < P.n_det_streams; d++) {
+    if (!((mask >> d) & 1u)) continue;
+    const DStream S = P.streams[P.det_streams[d]];
+    const uint64_t fm = gm & S.gmask;
+    for (uint32_t q = 0; q < S.val_count; q++) {
+      const DScanVal& sv = P.svals[S.val_begin + q];
+      if ((sv.kind == OP_DETECT_SQLI || sv.kind == OP_DETECT_XSS) && (fm & sv.fmask)) hit_value(B, sv.slot, r, vix);
+    }
+  }
+}
+
+__device__ void det_push(const DProgram& P, const DBatch& B, uint32_t r, uint32_t vix, uint64_t gm, uint32_t mask,
+                         const uint8_t* v, uint32_t n) {
+  const uint32_t k = atomicAdd(B.det_count, 1u);
+  const unsigned long long off = atomicAdd(B.det_used, (unsigned long long)((n + 15) & ~15u));
+  if (k >= B.det_cap || off + n > B.det_bytes_cap) {
+    det_maybe(P, B, r, vix, gm, mask);
+    return;
+  }
+  for (uint32_t i = 0; i < n; i++) B.det_bytes[off + i] = v[i];
+  DetEnt e;
+  e.req = r;
+  e.vix = vix;
+  e.mask = mask;
+  e.len = n;
+  e.off = off;
+  e.gm = gm;
+  ((DetEnt*)B.det)[k] = e;
+}
+
+// The stream's scan values on its output v[0, n): validate operators here;
+// @detectSQLi/@detectXSS through their exact prefilters -- a value that cannot
+// match is settled (a negated val hits), a candidate goes to k_detect: once
+// per item for the unchanged (raw) value (*rawmask collects the streams),
+// else once for this stream's output (*det_append).
 __device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, uint32_t vix, const DStream& S, uint64_t fm,
-                            bool maybe, const uint8_t* v, uint32_t n) {
+                            bool maybe, const uint8_t* v, uint32_t n, bool raw, uint32_t* rawmask, bool* det_append) {
+  int cand_sq = -1, cand_xs = -1;
   for (uint32_t q = 0; q < S.val_count; q++) {
     const DScanVal& sv = P.svals[S.val_begin + q];
     if (!(fm & sv.fmask)) continue;
+    if (sv.kind == OP_DETECT_SQLI || sv.kind == OP_DETECT_XSS) {
+      if (maybe) {
+        hit_value(B, sv.slot, r, vix);
+        continue;
+      }
+      const bool sq = sv.kind == OP_DETECT_SQLI;
+      int& cand = sq ? cand_sq : cand_xs;
+      if (cand < 0) cand = li_candidate(sq, v, n) ? 1 : 0;
+      if (!cand) {
+        if (sv.negate) hit_value(B, sv.slot, r, vix);
+        continue;
+      }
+      if (raw) *rawmask |= 1u << S.det_id;
+      else *det_append = true;
+      continue;
+    }
     if (maybe || (validate_op(sv.kind, sv.bits, v, n) != (sv.negate != 0))) hit_value(B, sv.slot, r, vix);
   }
 }
@@ -3933,6 +3994,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
     // filters of other streams).
     uint64_t rom0 = 0, rom1 = 0;
     uint32_t rq0 = 0, rq1 = 0, rw0 = 0, rw1 = 0;
+    uint32_t rawmask = 0;  // detect streams whose output is the unchanged item (one k_detect entry per item)
     for (uint32_t s = 0; s < P.n_streams; s++) {
       const uint64_t c_s0 = B.prof ? clock64() : 0;
       const DStream S = gi_cload(P.streams, s);
@@ -3958,7 +4020,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
           cur = src;
           cn = 0;
         }
-        if (S.val_count) stream_vals(P, B, it.req, meta_vix(it.meta), S, fm, maybe, cur, (uint32_t)cn);
+        if (S.val_count) {
+          bool det_append = false;
+          stream_vals(P, B, it.req, meta_vix(it.meta), S, fm, maybe, cur, (uint32_t)cn, !maybe && cur == src, &rawmask,
+                      &det_append);
+          if (det_append) det_push(P, B, it.req, meta_vix(it.meta), gm, 1u << S.det_id, cur, (uint32_t)cn);
+        }
       }
       const uint64_t c_s1 = B.prof ? clock64() : 0;
       pc_chain += c_s1 - c_s0;
@@ -4064,6 +4131,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
       }
       if (B.prof) pc_out += clock64() - c_s2;
     }
+    if (rawmask) det_push(P, B, it.req, meta_vix(it.meta), gm, rawmask, src, it.vn);
     if (B.prof) pc_loop += clock64() - c_b;
   }
   if (lane == 0 && wwords) atomicAdd(&B.acct[5 + bucket], (unsigned long long)wwords);
@@ -4647,6 +4715,8 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
           t.t0 = g.t0;
           t.t1 = g.t1;
           t.cap_t = g.cap_t;
+          t.mt = g.mt;
+          t.cap_mt = g.cap_mt;
           t.flags = 0;
           h = eval_op(t, o, cur, cn);
         }
@@ -4656,6 +4726,40 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
       if (B.prof && k < 16 && L == 0) {  // GI_PROF: cycles per link (transform, operator), per body
         atomicAdd(&B.prof[96 + 2 * k], (unsigned long long)(c1 - c0));
         atomicAdd(&B.prof[97 + 2 * k], (unsigned long long)(clock64() - c1));
+      }
+    }
+  }
+}
+
+// @detectSQLi / @detectXSS candidates, one lane per entry: libinjection with
+// the tokenizer state in LDS; each detector runs at most once per entry and
+// its result serves every admitting val of the masked streams.
+__global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
+  __shared__ LiSqli st[256];
+  const uint32_t n = min(*B.det_count, B.det_cap);
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const DetEnt x = ((const DetEnt*)B.det)[e];
+    GI_BOUND(x.req < B.n_req && x.off + x.len <= B.det_bytes_cap, x.req, x.off);
+    const uint8_t* v = B.det_bytes + x.off;
+    int sq = -1, xs = -1;
+    for (uint32_t d = 0; d < P.n_det_streams; d++) {
+      if (!((x.mask >> d) & 1u)) continue;
+      const DStream S = P.streams[P.det_streams[d]];
+      const uint64_t fm = x.gm & S.gmask;
+      for (uint32_t q = 0; q < S.val_count; q++) {
+        const DScanVal sv = P.svals[S.val_begin + q];
+        if (!(fm & sv.fmask)) continue;
+        bool res;
+        if (sv.kind == OP_DETECT_SQLI) {
+          if (sq < 0) sq = li_detect_sqli(v, x.len, &st[threadIdx.x]) ? 1 : 0;
+          res = sq != 0;
+        } else if (sv.kind == OP_DETECT_XSS) {
+          if (xs < 0) xs = li_detect_xss(v, x.len) ? 1 : 0;
+          res = xs != 0;
+        } else {
+          continue;
+        }
+        if (res != (sv.negate != 0)) hit_value(B, sv.slot, x.req, x.vix);
       }
     }
   }
@@ -4996,6 +5100,7 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
     GI_LAUNCH("k_stream2", (k_stream<64, 68>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 2u);
     GI_LAUNCH("k_stream3", (k_stream<128, 132>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
     GI_LAUNCH("k_stream4", (k_stream<0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
+    if (P.n_det_streams) GI_LAUNCH("k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
     if (ev) (void)hipEventRecord(ev[1], stream);
     for (int big = 0; big < 2; big++)
       if (S.n_jobs[big])

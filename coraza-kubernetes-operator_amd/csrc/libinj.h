@@ -10,11 +10,12 @@
 // libinjection_html5.c and libinjection_xss.c; the keyword table and the
 // fingerprint grammar are authored (libinj_tables.py; PARITY UNPINNED).
 //
-// GPU shape: k_stream calls these per (item, stream) lane right after the
-// transformation chain (a wave = 64 fields in lockstep); k_eval calls them
-// when it re-evaluates a set-bit link exactly.  The state is a few hundred
-// bytes of private memory per lane; tokens point into the value (or into the
-// keyword pool after a word merge) instead of copying 32-byte values.
+// GPU shape: k_stream tests each (item, stream) value against an exact
+// character-class prefilter (li_sqli_candidate / li_xss_candidate) and lists
+// the candidates; k_detect runs these functions one lane per candidate with
+// the tokenizer state in LDS; k_eval calls them when it re-evaluates a
+// set-bit link exactly.  Tokens point into the value (or into the keyword
+// pool after a word merge) instead of copying 32-byte values.
 #pragma once
 #include <stdint.h>
 
@@ -212,7 +213,7 @@ __device__ __forceinline__ uint8_t li_parser(uint8_t c) {
   return LP_WORD;
 }
 
-__device__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos) {
+__device__ __noinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint8_t* s = S.s;
   uint32_t e = pos;
   while (e < S.slen && !li_word_stop(s[e])) e++;
@@ -278,7 +279,7 @@ __device__ uint32_t li_parse_tick(LiSqli& S, LiTok& c, uint32_t pos) {
   return np;
 }
 
-__device__ uint32_t li_parse_money(LiSqli& S, LiTok& c, uint32_t pos) {
+__device__ __noinline__ uint32_t li_parse_money(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen;
   if (pos + 1 == slen) {
@@ -332,7 +333,7 @@ __device__ uint32_t li_parse_money(LiSqli& S, LiTok& c, uint32_t pos) {
   return pos + 1 + xlen;
 }
 
-__device__ uint32_t li_parse_number(LiSqli& S, LiTok& c, uint32_t pos) {
+__device__ __noinline__ uint32_t li_parse_number(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen;
   if (s[pos] == '0' && pos + 1 < slen) {
@@ -382,7 +383,7 @@ __device__ uint32_t li_parse_number(LiSqli& S, LiTok& c, uint32_t pos) {
 }
 
 // one parser step at S.pos into token c: returns the new position
-__device__ uint32_t li_parse(LiSqli& S, LiTok& c) {
+__device__ __noinline__ uint32_t li_parse(LiSqli& S, LiTok& c) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen, pos = S.pos;
   const uint8_t ch = s[pos];
@@ -508,7 +509,7 @@ __device__ uint32_t li_parse(LiSqli& S, LiTok& c) {
 }
 
 // libinjection_sqli_tokenize into tv[S.cur]
-__device__ bool li_tokenize(LiSqli& S) {
+__device__ __noinline__ bool li_tokenize(LiSqli& S) {
   if (S.slen == 0) return false;
   LiTok& c = S.tv[S.cur];
   li_clear(c);
@@ -545,7 +546,7 @@ __device__ __forceinline__ bool li_in(uint8_t c, const char* set) {
 }
 
 // syntax_merge_words: a's value becomes the keyword pool entry of "a b"
-__device__ bool li_merge(LiTok& a, const LiTok& b) {
+__device__ __noinline__ bool li_merge(LiTok& a, const LiTok& b) {
   if (!li_in(a.type, "knoUfETt") || !li_in(b.type, "knoUfETt&")) return false;
   const uint32_t sz3 = (uint32_t)a.len + b.len + 1;
   if (sz3 >= LI_TOKEN_SIZE) return false;
@@ -592,7 +593,7 @@ __device__ __forceinline__ void li_pull(LiSqli& S, uint32_t& pos, bool& more, Li
 }
 
 // libinjection_sqli_fold -> number of fingerprint tokens
-__device__ uint32_t li_fold(LiSqli& S) {
+__device__ __noinline__ uint32_t li_fold(LiSqli& S) {
   LiTok* tv = S.tv;
   uint32_t pos = 0, left = 0;
   bool more = true;
@@ -725,7 +726,7 @@ __device__ uint32_t li_fold(LiSqli& S) {
 
 // fingerprint blacklist: the authored grammar of libinj_tables.FINGERPRINT_RULES
 // (f upper-cased, n <= 5), matched by hand
-__device__ bool li_fp_black(const uint8_t* f, uint32_t n) {
+__device__ __noinline__ bool li_fp_black(const uint8_t* f, uint32_t n) {
   if (n == 0) return false;
   auto at = [&](uint32_t i) -> uint8_t { return i < n ? f[i] : (uint8_t)0; };
   auto val1s = [&](uint8_t c) { return c == '1' || c == 'S'; };
@@ -775,7 +776,7 @@ __device__ bool li_fp_black(const uint8_t* f, uint32_t n) {
 __device__ __forceinline__ uint8_t li_fpc(const LiSqli& S, uint32_t i) { return S.tv[i].type; }
 
 // libinjection_sqli_not_whitelist (fp = the fingerprint, tlen tokens)
-__device__ bool li_not_whitelist(const LiSqli& S, const uint8_t* fp, uint32_t tlen) {
+__device__ __noinline__ bool li_not_whitelist(const LiSqli& S, const uint8_t* fp, uint32_t tlen) {
   const LiTok* tv = S.tv;
   if (tlen > 1 && fp[tlen - 1] == 'c') {
     const uint8_t* s = S.s;
@@ -820,7 +821,7 @@ __device__ bool li_not_whitelist(const LiSqli& S, const uint8_t* fp, uint32_t tl
 }
 
 // libinjection_sqli_fingerprint + the blacklist/whitelist check for one context
-__device__ bool li_sqli_ctx(LiSqli& S, uint32_t flags) {
+__device__ __noinline__ bool li_sqli_ctx(LiSqli& S, uint32_t flags) {
   S.flags = flags;
   S.pos = 0;
   S.cur = 0;
@@ -849,10 +850,12 @@ __device__ bool li_sqli_ctx(LiSqli& S, uint32_t flags) {
   return li_fp_black(up, tlen) && li_not_whitelist(S, fp, tlen);
 }
 
-// libinjection_is_sqli
-__device__ __noinline__ bool li_detect_sqli(const uint8_t* s, uint32_t n) {
+// libinjection_is_sqli.  `st` is the caller's state buffer (LDS in k_detect,
+// the request's macro scratch in k_eval): kept in memory, the tokenizer state
+// does not inflate the register budget of every kernel that can call this.
+__device__ __noinline__ bool li_detect_sqli(const uint8_t* s, uint32_t n, LiSqli* st) {
   if (n == 0) return false;
-  LiSqli S;
+  LiSqli& S = *st;
   S.s = s;
   S.slen = n;
   if (li_sqli_ctx(S, LI_FLAG_QUOTE_NONE | LI_FLAG_SQL_ANSI)) return true;
@@ -867,6 +870,28 @@ __device__ __noinline__ bool li_detect_sqli(const uint8_t* s, uint32_t n) {
     if ((S.ddx || S.hash) && li_sqli_ctx(S, LI_FLAG_QUOTE_SINGLE | LI_FLAG_SQL_MYSQL)) return true;
   }
   if (dq && li_sqli_ctx(S, LI_FLAG_QUOTE_DOUBLE | LI_FLAG_SQL_MYSQL)) return true;
+  return false;
+}
+
+// Exact prefilter: a value whose bytes are all in [A-Za-z0-9_] tokenizes to at
+// most two tokens (a number, then one word running to the end: the word stop
+// set has none of these bytes, and the quote contexts need a quote), and no
+// two-token fingerprint of that shape survives blacklist + whitelist (the only
+// blacklisted one, value + UNION, is whitelisted at two tokens) -- so it is
+// never SQLi.  tests/test_libinjection.py checks the claim on a corpus.
+__device__ __forceinline__ bool li_sqli_byte(uint8_t c) {
+  return !((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_');
+}
+// Exact prefilter: without any of  NUL \t \n \v \f \r space < > = ' " ` /
+// each of the five start states yields a single DATA_TEXT / ATTR_NAME /
+// ATTR_VALUE token with no black attribute before it -- never XSS.
+__device__ __forceinline__ bool li_xss_byte(uint8_t c) {
+  return c == 0 || (c >= 9 && c <= 13) || c == ' ' || c == '<' || c == '>' || c == '=' || c == '\'' || c == '"' ||
+         c == '`' || c == '/';
+}
+__device__ inline bool li_candidate(bool sqli, const uint8_t* s, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    if (sqli ? li_sqli_byte(s[i]) : li_xss_byte(s[i])) return true;
   return false;
 }
 
@@ -911,7 +936,7 @@ __device__ __forceinline__ int h5_skip_white(H5& h) {
 // libinjection_h5_next: one token (false at the end).  `run` is the state
 // code to execute (a C tail call jumps to another state's code without
 // changing the persistent h.state).
-__device__ bool h5_next(H5& h) {
+__device__ __noinline__ bool h5_next(H5& h) {
   uint8_t run = h.state;
   const uint8_t* s = h.s;
   for (uint32_t guard = 0; guard < 64; guard++) {
@@ -1248,7 +1273,7 @@ __device__ bool li_eq_with_null(const uint8_t* lit, uint32_t ln, const uint8_t* 
   return j == ln;
 }
 
-__device__ bool li_black_tag(const uint8_t* s, uint32_t n) {
+__device__ __noinline__ bool li_black_tag(const uint8_t* s, uint32_t n) {
   if (n < 3) return false;
   for (uint32_t k = 0; k < LI_NTAGS; k++) {
     const uint32_t e = kLiTags[k];
@@ -1259,7 +1284,7 @@ __device__ bool li_black_tag(const uint8_t* s, uint32_t n) {
   return false;
 }
 
-__device__ uint32_t li_black_attr(const uint8_t* s, uint32_t n) {
+__device__ __noinline__ uint32_t li_black_attr(const uint8_t* s, uint32_t n) {
   if (n < 2) return 0;
   if (n >= 5) {
     if ((s[0] == 'o' || s[0] == 'O') && (s[1] == 'n' || s[1] == 'N')) return 1;
@@ -1353,7 +1378,7 @@ __device__ bool li_htmlencode_startswith(const char* prefix, const uint8_t* s, u
   return !prefix[j];
 }
 
-__device__ bool li_black_url(const uint8_t* s, uint32_t n) {
+__device__ __noinline__ bool li_black_url(const uint8_t* s, uint32_t n) {
   while (n > 0 && (s[0] <= 32 || s[0] >= 127)) {
     s++;
     n--;
@@ -1363,7 +1388,7 @@ __device__ bool li_black_url(const uint8_t* s, uint32_t n) {
 }
 
 // libinjection_is_xss for one start state
-__device__ bool li_xss_ctx(const uint8_t* s, uint32_t n, uint8_t start) {
+__device__ __noinline__ bool li_xss_ctx(const uint8_t* s, uint32_t n, uint8_t start) {
   H5 h;
   h.s = s;
   h.len = n;

@@ -84,9 +84,9 @@ struct gi_ctx {
   DevBuf tally_idbuf;                  // distinct rule ids, ascending (k_tally bins)
   std::vector<uint32_t> tally_ids;
   // phase A
-  DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes;
-  uint32_t lcap = 0, qcap = 0, slow_cap = 0;
-  uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0;
+  DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes;
+  uint32_t lcap = 0, qcap = 0, slow_cap = 0, det_cap = 0;
+  uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0, det_bytes_cap = 0;
   bool diag_on = false, prof_on = false;
   DevBuf prof;
   int stop_after = 0;  // debugging: launch only the first N pipeline kernels, synchronising after each
@@ -349,6 +349,12 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   np.body_access = P.body_access;
   np.mv_used = P.mv_used;
   np.body_limit = P.body_limit;
+  np.n_det_streams = 0;
+  for (uint32_t k = 0; k < (uint32_t)P.streams.size(); k++)
+    if (P.streams[k].det_id != 0xFF && P.streams[k].det_id < GI_MAX_DET_STREAMS) {
+      np.det_streams[P.streams[k].det_id] = k;
+      np.n_det_streams = std::max(np.n_det_streams, (uint32_t)P.streams[k].det_id + 1);
+    }
   np.n_jobs = (uint32_t)P.jobs.size();
   np.max_img_bytes = P.max_img_bytes;
   np.max_big_img_bytes = P.max_big_img_bytes;
@@ -464,7 +470,7 @@ void gi_ctx_free(gi_ctx* c) {
   c->prof.release();
   for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
-                    &c->ctr, &c->slow, &c->slow_bytes})
+                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes})
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
@@ -651,6 +657,11 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     (void)ns;
     if ((e = c->slow.ensure(40ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
+    // @detectSQLi/@detectXSS candidate list (overflow: the vals' bits become "maybe", exact)
+    c->det_cap = c->prog.n_det_streams ? (uint32_t)std::min<uint64_t>(8ull * n + 4096 + post_total / 8, 0x7FFFFFFFull) : 0;
+    c->det_bytes_cap = c->prog.n_det_streams ? 2ull * (raw_total + raw_body) + 16ull * c->det_cap : 0;
+    if ((e = c->det.ensure(std::max<uint64_t>(32ull * c->det_cap, 64))) != hipSuccess) return hip_fail(c, e, "alloc detect list");
+    if ((e = c->det_bytes.ensure(c->det_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc detect bytes");
   }
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && n) e = hipMemcpyAsync(c->reqs.p, in->reqs, n * sizeof(gi_request), hipMemcpyHostToDevice, s);
@@ -722,6 +733,12 @@ int gi_run_staged(gi_ctx* c) {
     B.slow_bytes = (uint8_t*)c->slow_bytes.p;
     B.slow_bytes_cap = c->slow_bytes_cap;
     B.slow_used = (unsigned long long*)(cp + 8);
+    B.det = c->det.p;
+    B.det_count = (uint32_t*)(cp + 24);
+    B.det_cap = c->det_cap;
+    B.det_bytes = (uint8_t*)c->det_bytes.p;
+    B.det_bytes_cap = c->det_bytes_cap;
+    B.det_used = (unsigned long long*)(cp + 32);
     B.diag = nullptr;
     B.prof = nullptr;
     if (c->prof_on && c->prof.ensure(1024 + 8000) == hipSuccess) {

@@ -95,6 +95,24 @@ def test_gpu_parity_crs_pl1_mixed_post():
     _parity(text, batch)
 
 
+def test_gpu_parity_crs_pl4_c3_mix():
+    """C4's ruleset (blocking paranoia level 4, the PL2-4 rules and
+    libinjection at PL1) over the C3 request mix."""
+    text = open(os.path.join(ROOT, "rulesets", "crs_pl4.conf")).read()
+    batch = traffic.TrafficGen(traffic.SEED + 4).batch(300, post_frac=0.5, attack_rate=0.3)
+    res = _parity(text, batch)
+    assert int((res.verdicts["action"] != 0).sum()) > 30
+
+
+def test_gpu_parity_crs_ftw_detection_only():
+    """The go-ftw configuration (X-CRS-Test rule block, generate_coreruleset_configmaps.py:113-141):
+    DetectionOnly, so nothing is interrupted, but the matched ids are compared."""
+    text = open(os.path.join(ROOT, "rulesets", "crs_ftw.conf")).read()
+    batch = traffic.TrafficGen(traffic.SEED + 5).batch(300, attack_rate=0.5)
+    res = _parity(text, batch)
+    assert int((res.verdicts["action"] != 0).sum()) == 0
+
+
 def test_gpu_parity_crs_pl1_kat_payloads():
     """Every attack payload of the generator, raw and encoded, in every
     position the CRS-shaped rules look at."""

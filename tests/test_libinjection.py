@@ -151,3 +151,25 @@ def test_gpu_detect_parity():
     assert not bad, bad
     hits = sum(1 for i in range(batch.n_req) if 1 in res.matched_rules(i))
     assert hits > 50  # the corpus exercises the detector
+
+
+def test_prefilters_are_exact(host_lib):
+    """k_stream settles values the character-class prefilters reject without
+    running libinjection: such a value must never be SQLi / XSS (oracle)."""
+    rng = random.Random(23)
+    sq_frag = [b"1", b"0x", b"0b", b"1e", b"1d", b"union", b"UNION", b"select", b"or", b"and", b"sleep", b"e", b"n",
+               b"q", b"b", b"x", b"u", b"int", b"from", b"9", b"_", b"abc", b"f", b"in", b"not", b"like", b"exec", b"if"]
+    xs_frag = [b"script", b"onerror", b"javascript:", b"&#x6A;", b"&#106", b"<", b"svg", b"xss", b"style", b"href",
+               b"data:", b"vbscript", b"[if", b"!--", b"-->", b"%>", b"?", b"import", b"ENTITY", b"a", b"(", b")",
+               b";", b"&", b"#", b"\\", b"\xff", b"\xa0", b"on", b"xml"]
+    n_sq = n_xs = 0
+    for _ in range(20000):
+        v = b"".join(rng.choice(sq_frag) for _ in range(rng.randint(1, 7)))
+        if not host_lib.li_host_candidate(1, v, len(v)):
+            n_sq += 1
+            assert not L.is_sqli(v)[0], v
+        w = b"".join(rng.choice(xs_frag) for _ in range(rng.randint(1, 7)))
+        if not host_lib.li_host_candidate(0, w, len(w)):
+            n_xs += 1
+            assert not L.is_xss(w), w
+    assert n_sq > 10000 and n_xs > 1000

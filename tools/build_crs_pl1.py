@@ -92,14 +92,65 @@ SecAction \
 '''
 
 
+# hack/generate_coreruleset_configmaps.py:113-141: the X-CRS-Test rule block the
+# generator appends to the base rules with --include-test-rule (:451-452), the
+# go-ftw configuration (coraza-proxy-wasm ftw-config.conf): blocking paranoia
+# level 4, DetectionOnly, and an X-CRS-Test header that disables detection
+X_CRS_TEST_RULE = r'''SecResponseBodyMimeType text/plain text/html text/xml application/json
+SecDefaultAction "phase:3,log,auditlog,pass"
+SecDefaultAction "phase:4,log,auditlog,pass"
+SecDefaultAction "phase:5,log,auditlog,pass"
+SecDebugLogLevel 3
+SecAction \
+ "id:900005,\
+ phase:1,\
+ nolog,\
+ pass,\
+ t:none,\
+ setvar:tx.blocking_paranoia_level=4,\
+ setvar:tx.crs_validate_utf8_encoding=1,\
+ setvar:tx.arg_name_length=100,\
+ setvar:tx.arg_length=400,\
+ setvar:tx.total_arg_length=64000,\
+ setvar:tx.max_num_args=255,\
+ setvar:tx.max_file_size=64100,\
+ setvar:tx.combined_file_sizes=65535,\
+ ctl:ruleEngine=DetectionOnly,\
+ ctl:ruleRemoveById=910000"
+SecRule REQUEST_HEADERS:X-CRS-Test "@rx ^.*$" \
+ "id:999999,\
+ pass,\
+ phase:1,\
+ log,\
+ msg:'X-CRS-Test %{MATCHED_VAR}',\
+ ctl:ruleRemoveById=1-999999"
+'''
+
+# C4 (SURVEY 8(d)): blocking paranoia level 4 (crs-setup.conf's 900000 convention)
+PL4_SETUP = r'''SecAction \
+ "id:900000,\
+ phase:1,\
+ pass,\
+ t:none,\
+ nolog,\
+ tag:'OWASP_CRS',\
+ ver:'OWASP_CRS/4.23.0',\
+ setvar:tx.blocking_paranoia_level=4"
+'''
+
+
 def main():
-    parts = [BASE_RULES]
-    for p in sorted(glob.glob(os.path.join(ROOT, "rulesets", "crs", "*.conf"))):
-        parts.append(open(p).read())
-    out = os.path.join(ROOT, "rulesets", "crs_pl1.conf")
-    with open(out, "w") as f:
-        f.write("\n".join(parts))
-    print("wrote", out, sum(len(p) for p in parts), "bytes")
+    crs = [open(p).read() for p in sorted(glob.glob(os.path.join(ROOT, "rulesets", "crs", "*.conf")))]
+    outs = {
+        "crs_pl1.conf": [BASE_RULES] + crs,
+        "crs_pl4.conf": [BASE_RULES + PL4_SETUP] + crs,
+        "crs_ftw.conf": [BASE_RULES + "\n" + X_CRS_TEST_RULE] + crs,
+    }
+    for name, parts in outs.items():
+        out = os.path.join(ROOT, "rulesets", name)
+        with open(out, "w") as f:
+            f.write("\n".join(parts))
+        print("wrote", out, sum(len(p) for p in parts), "bytes")
 
 
 if __name__ == "__main__":

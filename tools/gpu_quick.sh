@@ -19,6 +19,9 @@ python -c "import json; d=json.load(open('gpurun_out/${TAG}_c2_bench.json')); pr
 step c3
 timeout -k 10 300 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3.err || { tail -20 gpurun_out/${TAG}_c3.err; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/${TAG}_c3_bench.json')); print(d['value'], d['ms_per_step'], d['gb_per_s_scanned'])"
+step c4
+timeout -k 10 300 python -u bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_c4_bench.json 2> gpurun_out/${TAG}_c4.err || { tail -20 gpurun_out/${TAG}_c4.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/${TAG}_c4_bench.json')); print(d['value'], d['ms_per_step'], d['gb_per_s_scanned'])"
 [ "${PROF:-0}" = "0" ] && exit 0
 export TMPDIR=/tmp
 step rocprof
