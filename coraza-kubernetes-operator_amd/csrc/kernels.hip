@@ -2662,7 +2662,7 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
       res = false;
       break;
     case OP_DETECT_SQLI:  // [upstream] detect_sqli.go: libinjection.IsSQLi (capture of the fingerprint is unobservable here)
-      res = li_detect_sqli(s, n, (LiSqli*)t.mt);  // tokenizer state in the request's macro scratch (>= 512 B)
+      res = li_detect_sqli(s, n, (LiSqli*)t.mt, li_tables_const());  // state in the request's macro scratch (>= 512 B)
       break;
     case OP_DETECT_XSS:  // detect_xss.go: libinjection.IsXSS
       res = li_detect_xss(s, n);
@@ -4736,6 +4736,18 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
 // its result serves every admitting val of the masked streams.
 __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
   __shared__ LiSqli st[256];
+  // the keyword tables in LDS: every word lookup is a hash probe + compare
+  __shared__ uint32_t lw[LI_NWORDS];
+  __shared__ uint16_t lh[LI_HASH_SIZE];
+  __shared__ __attribute__((aligned(16))) uint8_t lp[sizeof(kLiPool)];
+  for (uint32_t i = threadIdx.x; i < LI_NWORDS; i += blockDim.x) lw[i] = kLiWords[i];
+  for (uint32_t i = threadIdx.x; i < LI_HASH_SIZE; i += blockDim.x) lh[i] = kLiHash[i];
+  for (uint32_t i = threadIdx.x; i < sizeof(kLiPool); i += blockDim.x) lp[i] = kLiPool[i];
+  __syncthreads();
+  LiTables T;  // (member-wise: an aggregate of LDS addresses would become a static initializer)
+  T.words = lw;
+  T.pool = lp;
+  T.hash = lh;
   const uint32_t n = min(*B.det_count, B.det_cap);
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const DetEnt x = ((const DetEnt*)B.det)[e];
@@ -4751,7 +4763,7 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
         if (!(fm & sv.fmask)) continue;
         bool res;
         if (sv.kind == OP_DETECT_SQLI) {
-          if (sq < 0) sq = li_detect_sqli(v, x.len, &st[threadIdx.x]) ? 1 : 0;
+          if (sq < 0) sq = li_detect_sqli(v, x.len, &st[threadIdx.x], T) ? 1 : 0;
           res = sq != 0;
         } else if (sv.kind == OP_DETECT_XSS) {
           if (xs < 0) xs = li_detect_xss(v, x.len) ? 1 : 0;

@@ -39,12 +39,23 @@ struct LiTok {
   uint8_t _pad[3];
 };
 
+// Keyword tables the lookups read: the __constant__ arrays of libinj_words.h,
+// or k_detect's LDS copies of them (li_tables_const / k_detect).
+struct LiTables {
+  const uint32_t* words;  // kLiWords
+  const uint8_t* pool;    // kLiPool
+  const uint16_t* hash;   // kLiHash
+};
+
 struct LiSqli {
   const uint8_t* s;
   uint32_t slen, flags, pos, cur;
   uint32_t ddx, hash, ntok;
+  LiTables T;
   LiTok tv[8];
 };
+
+__device__ __forceinline__ LiTables li_tables_const() { return LiTables{kLiWords, kLiPool, kLiHash}; }
 
 __device__ __forceinline__ uint8_t li_up(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
 
@@ -55,27 +66,34 @@ __device__ __forceinline__ uint8_t li_key_at(const uint8_t* a, uint32_t an, cons
   return li_up(b[i - an - 1]);
 }
 
-// bsearch_keyword_type: type of the word (exact match of the upper-cased key), 0 if none
-__device__ __noinline__ uint8_t li_lookup2(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn, bool two) {
+// bsearch_keyword_type restated as a hash probe: the index of the word equal
+// to the upper-cased key (a, or a + ' ' + b), -1 if none.  FNV-1a over the
+// upper-cased bytes into an open-addressing table (tools/gen_libinj_tables.py).
+__device__ __noinline__ int li_find(const LiTables& T, const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn,
+                                    bool two) {
   const uint32_t kn = two ? an + 1 + bn : an;
-  if (kn == 0 || kn >= LI_TOKEN_SIZE) return 0;
-  for (uint32_t i = 0; i < kn; i++)
-    if (li_key_at(a, an, b, i) == 0) return 0;  // cstrcasecmp never equates a NUL
-  uint32_t lo = 0, hi = LI_NWORDS;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    const uint32_t e = kLiWords[mid], off = e & 0xFFFFu, n = (e >> 16) & 0xFFu;
-    const uint32_t m = n < kn ? n : kn;
-    int d = 0;
-    for (uint32_t i = 0; i < m && !d; i++) d = (int)kLiPool[off + i] - (int)li_key_at(a, an, b, i);
-    if (!d) d = (int)n - (int)kn;
-    if (d < 0) lo = mid + 1;
-    else if (d > 0) hi = mid;
-    else return (uint8_t)(e >> 24);
+  if (kn == 0 || kn >= LI_TOKEN_SIZE) return -1;
+  uint32_t h = 2166136261u;
+  for (uint32_t i = 0; i < kn; i++) {
+    const uint8_t c = li_key_at(a, an, b, i);
+    if (c == 0) return -1;  // cstrcasecmp never equates a NUL
+    h = (h ^ c) * 16777619u;
   }
-  return 0;
+  for (uint32_t slot = h & (LI_HASH_SIZE - 1);; slot = (slot + 1) & (LI_HASH_SIZE - 1)) {
+    const uint32_t idx = T.hash[slot];
+    if (!idx) return -1;
+    const uint32_t e = T.words[idx - 1];
+    if (((e >> 16) & 0xFFu) != kn) continue;
+    const uint8_t* w = T.pool + (e & 0xFFFFu);
+    bool eq = true;
+    for (uint32_t i = 0; i < kn && eq; i++) eq = w[i] == li_key_at(a, an, b, i);
+    if (eq) return (int)(idx - 1);
+  }
 }
-__device__ __forceinline__ uint8_t li_lookup(const uint8_t* a, uint32_t an) { return li_lookup2(a, an, nullptr, 0, false); }
+__device__ __forceinline__ uint8_t li_lookup(const LiTables& T, const uint8_t* a, uint32_t an) {
+  const int i = li_find(T, a, an, nullptr, 0, false);
+  return i < 0 ? (uint8_t)0 : (uint8_t)(T.words[i] >> 24);
+}
 
 // cstrcasecmp(lit, tok, tok.len) == 0 (lit upper case, no NUL)
 __device__ __forceinline__ bool li_tok_is(const LiTok& t, const char* lit) {
@@ -222,7 +240,7 @@ __device__ __noinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos
   for (uint32_t i = 0; i < c.len; i++) {
     const uint8_t d = c.p[i];
     if (d == '.' || d == '`') {
-      const uint8_t ch = li_lookup(c.p, i);
+      const uint8_t ch = li_lookup(S.T, c.p, i);
       if (ch != 0 && ch != 'n') {
         li_clear(c);
         li_assign(c, ch, s + pos, i);
@@ -231,7 +249,7 @@ __device__ __noinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos
     }
   }
   if (wlen < LI_TOKEN_SIZE) {
-    const uint8_t ch = li_lookup(c.p, wlen);
+    const uint8_t ch = li_lookup(S.T, c.p, wlen);
     c.type = ch ? ch : 'n';
   }
   return pos + wlen;
@@ -274,7 +292,7 @@ __device__ uint32_t li_parse_estring(LiSqli& S, LiTok& c, uint32_t pos) {
 
 __device__ uint32_t li_parse_tick(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint32_t np = li_string_core(S.s, S.slen, pos, c, '`', 1);
-  const uint8_t ch = li_lookup(c.p, c.len);
+  const uint8_t ch = li_lookup(S.T, c.p, c.len);
   c.type = ch == 'f' ? 'f' : 'n';
   return np;
 }
@@ -440,7 +458,7 @@ __device__ __noinline__ uint32_t li_parse(LiSqli& S, LiTok& c) {
         li_assign(c, 'o', s + pos, 3);
         return pos + 3;
       }
-      const uint8_t t = li_lookup(s + pos, 2);
+      const uint8_t t = li_lookup(S.T, s + pos, 2);
       if (t) {
         li_assign(c, t, s + pos, 2);
         return pos + 2;
@@ -546,27 +564,15 @@ __device__ __forceinline__ bool li_in(uint8_t c, const char* set) {
 }
 
 // syntax_merge_words: a's value becomes the keyword pool entry of "a b"
-__device__ __noinline__ bool li_merge(LiTok& a, const LiTok& b) {
+__device__ __noinline__ bool li_merge(const LiTables& T, LiTok& a, const LiTok& b) {
   if (!li_in(a.type, "knoUfETt") || !li_in(b.type, "knoUfETt&")) return false;
   const uint32_t sz3 = (uint32_t)a.len + b.len + 1;
   if (sz3 >= LI_TOKEN_SIZE) return false;
-  const uint8_t ch = li_lookup2(a.p, a.len, b.p, b.len, true);
-  if (!ch) return false;
-  // point at the pool copy of the merged word (same bytes up to case)
-  uint32_t lo = 0, hi = LI_NWORDS, at = 0;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    const uint32_t e = kLiWords[mid], off = e & 0xFFFFu, n = (e >> 16) & 0xFFu;
-    const uint32_t m = n < sz3 ? n : sz3;
-    int d = 0;
-    for (uint32_t i = 0; i < m && !d; i++) d = (int)kLiPool[off + i] - (int)li_key_at(a.p, a.len, b.p, i);
-    if (!d) d = (int)n - (int)sz3;
-    if (d < 0) lo = mid + 1;
-    else if (d > 0) hi = mid;
-    else { at = off; break; }
-  }
-  a.type = ch;
-  a.p = &kLiPool[at];
+  const int i = li_find(T, a.p, a.len, b.p, b.len, true);
+  if (i < 0) return false;
+  const uint32_t e = T.words[i];
+  a.type = (uint8_t)(e >> 24);
+  a.p = T.pool + (e & 0xFFFFu);  // the pool copy of the merged word (same bytes up to case)
   a.len = (uint16_t)sz3;
   return true;
 }
@@ -638,7 +644,7 @@ __device__ __noinline__ uint32_t li_fold(LiSqli& S) {
     if (a.type == ';' && b.type == ';') { pos--; continue; }
     if ((a.type == 'o' || a.type == '&') && (li_unary(b) || b.type == 't')) { pos--; left = 0; continue; }
     if (a.type == '(' && li_unary(b)) { pos--; if (left > 0) left--; continue; }
-    if (li_merge(a, b)) { pos--; if (left > 0) left--; continue; }
+    if (li_merge(S.T, a, b)) { pos--; if (left > 0) left--; continue; }
     if (a.type == ';' && b.type == 'f' && b.len >= 2 && (b.p[0] == 'I' || b.p[0] == 'i') && (b.p[1] == 'F' || b.p[1] == 'f')) {
       b.type = 'T';
       continue;
@@ -853,9 +859,10 @@ __device__ __noinline__ bool li_sqli_ctx(LiSqli& S, uint32_t flags) {
 // libinjection_is_sqli.  `st` is the caller's state buffer (LDS in k_detect,
 // the request's macro scratch in k_eval): kept in memory, the tokenizer state
 // does not inflate the register budget of every kernel that can call this.
-__device__ __noinline__ bool li_detect_sqli(const uint8_t* s, uint32_t n, LiSqli* st) {
+__device__ __noinline__ bool li_detect_sqli(const uint8_t* s, uint32_t n, LiSqli* st, const LiTables& T) {
   if (n == 0) return false;
   LiSqli& S = *st;
+  S.T = T;
   S.s = s;
   S.slen = n;
   if (li_sqli_ctx(S, LI_FLAG_QUOTE_NONE | LI_FLAG_SQL_ANSI)) return true;

@@ -658,8 +658,13 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if ((e = c->slow.ensure(40ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
     // @detectSQLi/@detectXSS candidate list (overflow: the vals' bits become "maybe", exact)
-    c->det_cap = c->prog.n_det_streams ? (uint32_t)std::min<uint64_t>(8ull * n + 4096 + post_total / 8, 0x7FFFFFFFull) : 0;
-    c->det_bytes_cap = c->prog.n_det_streams ? 2ull * (raw_total + raw_body) + 16ull * c->det_cap : 0;
+    // an item lists its unchanged value once and each differently transformed
+    // output once per detect stream: 2 entries per item covers the common case
+    c->det_cap = c->prog.n_det_streams
+                     ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(2ull * c->items_cap, 24ull * n + 2ull * post_total) + 4096,
+                                                    0x7FFFFFFFull)
+                     : 0;
+    c->det_bytes_cap = c->prog.n_det_streams ? 3ull * (raw_total + raw_body) + 16ull * c->det_cap : 0;
     if ((e = c->det.ensure(std::max<uint64_t>(32ull * c->det_cap, 64))) != hipSuccess) return hip_fail(c, e, "alloc detect list");
     if ((e = c->det_bytes.ensure(c->det_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc detect bytes");
   }
@@ -867,6 +872,10 @@ int gi_sync(gi_ctx* c) {
         c->stats.diag[1] = h[1];
         c->stats.diag[2] = h[2] & 0xFFFFFFFFull;
         for (int b = 0; b < 5; b++) c->stats.diag[3 + b] = ib[2 * b + 1];
+        if (c->det_cap)  // @detectSQLi/@detectXSS candidates listed by k_stream (k_detect entries)
+          fprintf(stderr, "GI_DIAG detect entries %llu (cap %u), bytes %llu (cap %llu)\n",
+                  (unsigned long long)(h[3] & 0xFFFFFFFFull), c->det_cap, (unsigned long long)h[4],
+                  (unsigned long long)c->det_bytes_cap);
       }
     }
   }

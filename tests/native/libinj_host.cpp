@@ -9,7 +9,7 @@
 
 extern "C" int li_host_sqli(const uint8_t* s, uint32_t n) {
   gi::LiSqli st;
-  return gi::li_detect_sqli(s, n, &st) ? 1 : 0;
+  return gi::li_detect_sqli(s, n, &st, gi::li_tables_const()) ? 1 : 0;
 }
 extern "C" int li_host_candidate(int sqli, const uint8_t* s, uint32_t n) { return gi::li_candidate(sqli != 0, s, n) ? 1 : 0; }
 extern "C" int li_host_xss(const uint8_t* s, uint32_t n) { return gi::li_detect_xss(s, n) ? 1 : 0; }
