@@ -1313,6 +1313,10 @@ struct Lower {
     // superset).  The residual clear-bit path and k_body test final values
     // only, so a multiMatch link with residual targets stays interpreter-only.
     if (r.multimatch && residual) return -1;
+    // a detect link reading REQUEST_BODY would go to k_body, which does not run libinjection: interpreter-only
+    if ((n == "detectsqli" || n == "detectxss") && residual)
+      for (auto& v : r.vars)
+        if (v.name == "REQUEST_BODY") return -1;
     const int32_t slot = (int32_t)P->n_hit_slots++;
     if (bodydep) *flags |= RF_BODYDEP;
     if (residual) *flags |= RF_RESIDUAL;

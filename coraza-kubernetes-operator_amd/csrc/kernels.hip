@@ -2643,6 +2643,10 @@ __device__ bool contains_word(const uint8_t* v, uint32_t vn, const uint8_t* w, u
   return false;
 }
 
+// DETECT = false (k_body): @detectSQLi/@detectXSS cannot reach the call (the
+// compiler keeps REQUEST_BODY detect links out of k_body), so the kernel does
+// not link libinjection and keeps its register budget.
+template <bool DETECT = true>
 __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, uint32_t n) {
   const DProgram& P = *t.P;
   bool res = false;
@@ -2662,10 +2666,10 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
       res = false;
       break;
     case OP_DETECT_SQLI:  // [upstream] detect_sqli.go: libinjection.IsSQLi (capture of the fingerprint is unobservable here)
-      res = li_detect_sqli(s, n, (LiSqli*)t.mt, li_tables_const());  // state in the request's macro scratch (>= 512 B)
+      if (DETECT) res = li_detect_sqli(s, n, (LiSqli*)t.mt, li_tables_const());  // state in the macro scratch (>= 512 B)
       break;
     case OP_DETECT_XSS:  // detect_xss.go: libinjection.IsXSS
-      res = li_detect_xss(s, n);
+      if (DETECT) res = li_detect_xss(s, n);
       break;
     case OP_VALIDATE_BYTE_RANGE:
       for (uint32_t i = 0; i < n; i++)
@@ -4718,7 +4722,7 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
           t.mt = g.mt;
           t.cap_mt = g.cap_mt;
           t.flags = 0;
-          h = eval_op(t, o, cur, cn);
+          h = eval_op<false>(t, o, cur, cn);
         }
         hit = __shfl((int)h, 0, 64) != 0;
       }
@@ -4763,10 +4767,12 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
         if (!(fm & sv.fmask)) continue;
         bool res;
         if (sv.kind == OP_DETECT_SQLI) {
-          if (sq < 0) sq = li_detect_sqli(v, x.len, &st[threadIdx.x], T) ? 1 : 0;
+          // (k_stream listed the value for some val of the masked streams: the
+          // other kind's prefilter may still settle it)
+          if (sq < 0) sq = li_candidate(true, v, x.len) && li_detect_sqli(v, x.len, &st[threadIdx.x], T) ? 1 : 0;
           res = sq != 0;
         } else if (sv.kind == OP_DETECT_XSS) {
-          if (xs < 0) xs = li_detect_xss(v, x.len) ? 1 : 0;
+          if (xs < 0) xs = li_candidate(false, v, x.len) && li_detect_xss(v, x.len) ? 1 : 0;
           res = xs != 0;
         } else {
           continue;

@@ -69,7 +69,7 @@ __device__ __forceinline__ uint8_t li_key_at(const uint8_t* a, uint32_t an, cons
 // bsearch_keyword_type restated as a hash probe: the index of the word equal
 // to the upper-cased key (a, or a + ' ' + b), -1 if none.  FNV-1a over the
 // upper-cased bytes into an open-addressing table (tools/gen_libinj_tables.py).
-__device__ __noinline__ int li_find(const LiTables& T, const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn,
+__device__ __forceinline__ int li_find(const LiTables& T, const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn,
                                     bool two) {
   const uint32_t kn = two ? an + 1 + bn : an;
   if (kn == 0 || kn >= LI_TOKEN_SIZE) return -1;
@@ -231,7 +231,7 @@ __device__ __forceinline__ uint8_t li_parser(uint8_t c) {
   return LP_WORD;
 }
 
-__device__ __noinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos) {
+__device__ __forceinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint8_t* s = S.s;
   uint32_t e = pos;
   while (e < S.slen && !li_word_stop(s[e])) e++;
@@ -297,7 +297,7 @@ __device__ uint32_t li_parse_tick(LiSqli& S, LiTok& c, uint32_t pos) {
   return np;
 }
 
-__device__ __noinline__ uint32_t li_parse_money(LiSqli& S, LiTok& c, uint32_t pos) {
+__device__ __forceinline__ uint32_t li_parse_money(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen;
   if (pos + 1 == slen) {
@@ -351,7 +351,7 @@ __device__ __noinline__ uint32_t li_parse_money(LiSqli& S, LiTok& c, uint32_t po
   return pos + 1 + xlen;
 }
 
-__device__ __noinline__ uint32_t li_parse_number(LiSqli& S, LiTok& c, uint32_t pos) {
+__device__ __forceinline__ uint32_t li_parse_number(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen;
   if (s[pos] == '0' && pos + 1 < slen) {
@@ -401,7 +401,7 @@ __device__ __noinline__ uint32_t li_parse_number(LiSqli& S, LiTok& c, uint32_t p
 }
 
 // one parser step at S.pos into token c: returns the new position
-__device__ __noinline__ uint32_t li_parse(LiSqli& S, LiTok& c) {
+__device__ __forceinline__ uint32_t li_parse(LiSqli& S, LiTok& c) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen, pos = S.pos;
   const uint8_t ch = s[pos];
@@ -527,7 +527,7 @@ __device__ __noinline__ uint32_t li_parse(LiSqli& S, LiTok& c) {
 }
 
 // libinjection_sqli_tokenize into tv[S.cur]
-__device__ __noinline__ bool li_tokenize(LiSqli& S) {
+__device__ __forceinline__ bool li_tokenize(LiSqli& S) {
   if (S.slen == 0) return false;
   LiTok& c = S.tv[S.cur];
   li_clear(c);
@@ -564,7 +564,7 @@ __device__ __forceinline__ bool li_in(uint8_t c, const char* set) {
 }
 
 // syntax_merge_words: a's value becomes the keyword pool entry of "a b"
-__device__ __noinline__ bool li_merge(const LiTables& T, LiTok& a, const LiTok& b) {
+__device__ __forceinline__ bool li_merge(const LiTables& T, LiTok& a, const LiTok& b) {
   if (!li_in(a.type, "knoUfETt") || !li_in(b.type, "knoUfETt&")) return false;
   const uint32_t sz3 = (uint32_t)a.len + b.len + 1;
   if (sz3 >= LI_TOKEN_SIZE) return false;
