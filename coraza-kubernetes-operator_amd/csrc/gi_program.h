@@ -287,6 +287,9 @@ enum : uint32_t {
   BS_PCT = 1u << 0, BS_PLUS = 1u << 1, BS_AMP = 1u << 2, BS_UPPER = 1u << 3, BS_HIGH = 1u << 4,
   BS_NUL = 1u << 5, BS_WS = 1u << 6, BS_SLASH = 1u << 7, BS_BSLASH = 1u << 8, BS_DOT = 1u << 9,
   BS_QUOTE = 1u << 10, BS_CARET = 1u << 11, BS_SEP = 1u << 12, BS_ALL = 0xFFFFFFFFu,
+  // k_stream's summary LUT only: a byte outside [A-Za-z0-9_] / a byte of the
+  // XSS trigger set (libinj.h li_sqli_byte / li_xss_byte; no transformation triggers on them)
+  BS_LI_SQLI = 1u << 13, BS_LI_XSS = 1u << 14,
 };
 __host__ __device__ inline uint32_t byte_summary(uint8_t c) {
   uint32_t m = 0;

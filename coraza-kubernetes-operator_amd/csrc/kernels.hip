@@ -3866,19 +3866,18 @@ __device__ void det_push(const DProgram& P, const DBatch& B, uint32_t r, uint32_
 // per item for the unchanged (raw) value (*rawmask collects the streams),
 // else once for this stream's output (*det_append).
 __device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, uint32_t vix, const DStream& S, uint64_t fm,
-                            bool maybe, const uint8_t* v, uint32_t n, bool raw, uint32_t* rawmask, bool* det_append) {
-  int cand_sq = -1, cand_xs = -1;
+                            bool maybe, const uint8_t* v, uint32_t n, uint32_t osum, bool raw, uint32_t* rawmask,
+                            bool* det_append) {
   for (uint32_t q = 0; q < S.val_count; q++) {
-    const DScanVal& sv = P.svals[S.val_begin + q];
+    const DScanVal sv = gi_cload(P.svals, S.val_begin + q);  // wave-uniform: scalar loads
     if (!(fm & sv.fmask)) continue;
     if (sv.kind == OP_DETECT_SQLI || sv.kind == OP_DETECT_XSS) {
       if (maybe) {
         hit_value(B, sv.slot, r, vix);
         continue;
       }
-      const bool sq = sv.kind == OP_DETECT_SQLI;
-      int& cand = sq ? cand_sq : cand_xs;
-      if (cand < 0) cand = li_candidate(sq, v, n) ? 1 : 0;
+      // the output's byte summary carries the exact prefilters (li_sqli_byte / li_xss_byte)
+      const bool cand = (osum & (sv.kind == OP_DETECT_SQLI ? BS_LI_SQLI : BS_LI_XSS)) != 0;
       if (!cand) {
         if (sv.negate) hit_value(B, sv.slot, r, vix);
         continue;
@@ -3896,7 +3895,7 @@ __device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, uint
 template <bool INL>
 __device__ __forceinline__ int64_t run_chain(const DProgram& P, const DStream& S, const uint8_t* v, uint32_t vn,
                                              uint32_t summ, uint8_t* b0, uint8_t* b1, uint32_t cap,
-                                             const uint8_t** out, const uint16_t* lut) {
+                                             const uint8_t** out, const uint16_t* lut, uint32_t* osumm) {
   const uint8_t* cur = v;
   uint32_t cn = vn;
   for (uint32_t k = 0; k < S.tchain_len; k++) {
@@ -3910,6 +3909,7 @@ __device__ __forceinline__ int64_t run_chain(const DProgram& P, const DStream& S
     summ = value_summary_lut(lut, cur, cn);
   }
   *out = cur;
+  *osumm = summ;  // byte summary of the output (k_stream's LUT adds the libinjection prefilter bits)
   return cn;
 }
 
@@ -3954,7 +3954,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
   __shared__ uint16_t sumlut[256];  // byte_summary of every byte value
   const uint32_t lane = threadIdx.x;
   if (lane == 0) pnext = pend = 0;
-  for (uint32_t b = lane; b < 256; b += 64) sumlut[b] = (uint16_t)byte_summary((uint8_t)b);
+  for (uint32_t b = lane; b < 256; b += 64)
+    sumlut[b] = (uint16_t)(byte_summary((uint8_t)b) | (li_sqli_byte((uint8_t)b) ? BS_LI_SQLI : 0u) |
+                           (li_xss_byte((uint8_t)b) ? BS_LI_XSS : 0u));
   __syncthreads();
   const uint32_t iw_base = B.ibk[2 * GI_NB + bucket];
   const uint32_t base = B.ibk[2 * bucket], cnt = B.ibk[2 * bucket + 1];
@@ -4011,12 +4013,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
       pc_fm += c_sa - c_s0;
       const uint8_t* cur = nullptr;
       int64_t cn = 0;
+      uint32_t osum = summ;  // byte summary of the chain output
       bool maybe = false, glob = !IN;
       if (fm) {
-        cn = run_chain<IN != 0>(P, S, src, it.vn, summ, b0, b1, cap, &cur, sumlut);
+        cn = run_chain<IN != 0>(P, S, src, it.vn, summ, b0, b1, cap, &cur, sumlut, &osum);
         if (B.prof) pc_run += clock64() - c_sa;
         if (cn < 0 && IN) {
-          cn = run_chain<false>(P, S, src, it.vn, summ, g0, g1, B.lcap, &cur, sumlut);
+          cn = run_chain<false>(P, S, src, it.vn, summ, g0, g1, B.lcap, &cur, sumlut, &osum);
           glob = true;
         }
         if (cn < 0) {
@@ -4026,8 +4029,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
         }
         if (S.val_count) {
           bool det_append = false;
-          stream_vals(P, B, it.req, meta_vix(it.meta), S, fm, maybe, cur, (uint32_t)cn, !maybe && cur == src, &rawmask,
-                      &det_append);
+          stream_vals(P, B, it.req, meta_vix(it.meta), S, fm, maybe, cur, (uint32_t)cn, osum, !maybe && cur == src,
+                      &rawmask, &det_append);
           if (det_append) det_push(P, B, it.req, meta_vix(it.meta), gm, 1u << S.det_id, cur, (uint32_t)cn);
         }
       }
@@ -4038,7 +4041,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8)))
       if (fm && !maybe) {
         // byte summary of the chain output (run_chain leaves it current in
         // the identity case; recompute otherwise)
-        const uint32_t osum = (cur == src) ? summ : value_summary_lut(sumlut, cur, (uint32_t)cn);
+
         if (osum & BS_HIGH) {
           if (S.collapse) {
             uint8_t* dst = glob ? (cur == g0 ? g1 : g0) : (cur == b0 ? b1 : b0);
