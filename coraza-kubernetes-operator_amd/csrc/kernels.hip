@@ -3943,8 +3943,14 @@ __device__ uint32_t collapse_runes(const uint8_t* s, uint32_t n, uint8_t* d) {
 
 // IN = per-lane LDS copy of the item's bytes (bucket maximum); WT = per-lane
 // LDS transformation buffers.  IN == 0: long items, HBM buffers throughout.
+// 2 waves/SIMD: the chains + queue writer fit without spills (at 3 the
+// compiler spilled ~128 VGPRs, and scratch traffic dominated k_stream's HBM
+// writes: PMC WRITE_SIZE 38 GB per launch against 4.6 GB of queue words)
+#ifndef GI_STREAM_WPE
+#define GI_STREAM_WPE 2
+#endif
 template <uint32_t IN, uint32_t WT>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) k_stream(DProgram P, DBatch B, uint32_t bucket) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STREAM_WPE, 8))) k_stream(DProgram P, DBatch B, uint32_t bucket) {
   constexpr uint32_t IS = IN ? IN + 4 : 0;  // lane strides = odd dword counts: conflict-free
   __shared__ __attribute__((aligned(16))) uint8_t lb[IN ? 64 * (IS + 2 * WT) : 16];
   // Queue block of (item-wave, stream) = qblk[stream][item-wave index]: no

@@ -29,6 +29,13 @@ tail -1 gpurun_out/${TAG}_traffic.log
 step occupancy
 timeout -k 10 400 python -u tools/pmc_occupancy.py --config c2 --n-req 1000000 --out gpurun_out/${TAG}_pmc_c2.json > gpurun_out/${TAG}_occ.log 2>&1 || { tail -20 gpurun_out/${TAG}_occ.log; exit 1; }
 cat gpurun_out/${TAG}_occ.log
+[ "${CONFIGS:-1}" = "0" ] && exit 0
 step c3
 timeout -k 10 400 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3.err || { tail -20 gpurun_out/${TAG}_c3.err; exit 1; }
 cat gpurun_out/${TAG}_c3_bench.json
+step c4
+timeout -k 10 400 python -u bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_c4_bench.json 2> gpurun_out/${TAG}_c4.err || { tail -20 gpurun_out/${TAG}_c4.err; exit 1; }
+cat gpurun_out/${TAG}_c4_bench.json
+step c5
+timeout -k 10 500 python -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_c5_bench.json 2> gpurun_out/${TAG}_c5.err || { tail -20 gpurun_out/${TAG}_c5.err; exit 1; }
+cat gpurun_out/${TAG}_c5_bench.json
