@@ -53,6 +53,7 @@ struct LiSqli {
   uint32_t ddx, hash, ntok;
   LiTables T;
   LiTok tv[8];
+  uint32_t _pad[2];  // 200 B = 50 dwords: k_detect's per-lane LDS states hit ~2-way, not 16-way, bank conflicts
 };
 
 __device__ __forceinline__ LiTables li_tables_const() { return LiTables{kLiWords, kLiPool, kLiHash}; }
