@@ -107,6 +107,12 @@ def parity(res, verdicts):
                    "ordered matched ids, exported TX values, unsupported flag (oracle/compare.py)"}
 
 
+def log(msg):
+    """Progress on stderr (a long compile or batch must not look hung to a watchdog)."""
+    sys.stderr.write("[bench %s] %s\n" % (time.strftime("%H:%M:%S"), msg))
+    sys.stderr.flush()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -136,8 +142,10 @@ def main():
         text = open(os.path.join(ROOT, rs_file)).read()
     n_req = args.n_req or n_default
     t_compile = time.perf_counter()
+    log("compiling %s (%d bytes of SecLang)" % (args.config, len(text)))
     rs = gpuinspect.Ruleset(text, data_files=files)
     t_compile = time.perf_counter() - t_compile
+    log("compiled in %.1f s: %s" % (t_compile, rs.info))
     eng = gpuinspect.Engine(rs, device=local, matched_cap=args.matched_cap)
     t_gen = time.perf_counter()
     if args.config == "c5":
@@ -146,6 +154,7 @@ def main():
         batch = traffic.TrafficGen(shard.shard_seed(traffic.SEED, rank)).batch(n_req, post_frac=post_frac)
     t_gen = time.perf_counter() - t_gen
     raw = batch.raw_bytes()
+    log("generated %d requests (%d bytes) in %.1f s; staging" % (batch.n_req, raw, t_gen))
     eng.stage(batch)
 
     gather = shard.TallyGather(dist, world, "cuda", n_rules=eng.tally_rule_count()) if dist is not None else None
@@ -156,8 +165,9 @@ def main():
         if gather is not None:
             gather.push(eng.tally(), eng.tally_detail())
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         step()
+        log("warmup %d done" % w)
     if dist is not None:
         dist.barrier()
         torch.cuda.synchronize()
@@ -165,8 +175,9 @@ def main():
     kern_ms = []
     launch_ms, launch_bytes, launch_steps = {}, {}, {}
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
         step()
+        log("step %d done" % k)
         st = eng.stats()
         kern_ms.append(st["last_kernel_ms"])
         for ln in st["launches"]:
@@ -271,6 +282,7 @@ def main():
                   "GB/s": round(raw / (t4 - t1) / 1e9, 3),
                   "def": "one pass incl. gi_stage_batch (host layout + H2D, pageable) and gi_fetch_results (D2H), per GPU"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline / parity sample (oracle)")
         verdicts, wall, procs = oracle_sample(text, batch, rs.exports, files=files,
                                               calib=2 if args.config == "c5" else 100,
                                               budget_s=30.0 if args.config == "c5" else 15.0)

@@ -63,6 +63,12 @@ struct DBatch {
   uint8_t* slow_bytes;
   uint64_t slow_bytes_cap;
   unsigned long long* slow_used;
+  uint2* long_list;           // (item, stream) of long values (k_stream -> k_long, one wave each)
+  uint32_t* long_count;
+  uint32_t long_cap;
+  uint32_t long_grid;         // k_long workgroups (each owns two long_bufcap buffers)
+  uint8_t* long_buf;
+  uint64_t long_bufcap;
   void* det;                  // DetEnt[det_cap]: @detectSQLi/@detectXSS candidates (k_stream -> k_detect)
   uint32_t* det_count;
   uint32_t det_cap;
@@ -91,6 +97,8 @@ struct ScanLaunch {
 #define GI_RHIST_LDS 1024     // per-rule match counts k_eval aggregates in LDS (more rules: global atomics)
 #define GI_STREAM_GRID 8192  // k_stream workgroups (64 lanes) per bucket launch (~8 waves/SIMD)
 #define GI_PCHUNK 2048       // pool words a k_stream wave reserves at a time
+#define GI_LONG_MIN 2048     // items at least this long take k_long (one wave per (item, stream)), not the queue
+#define GI_LONG_GRID 512     // k_long workgroups
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.
 uint32_t scan_resident_blocks(uint32_t lds_bytes);

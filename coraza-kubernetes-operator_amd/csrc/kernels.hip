@@ -4007,10 +4007,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
     uint64_t rom0 = 0, rom1 = 0;
     uint32_t rq0 = 0, rq1 = 0, rw0 = 0, rw1 = 0;
     uint32_t rawmask = 0;  // detect streams whose output is the unchanged item (one k_detect entry per item)
+    // a long value (>= GI_LONG_MIN bytes) takes k_long: one wave per (item, stream), no queue block
+    const bool is_long = IN == 0 && B.long_cap && ii < cnt && it.vn >= GI_LONG_MIN;
     for (uint32_t s = 0; s < P.n_streams; s++) {
       const uint64_t c_s0 = B.prof ? clock64() : 0;
       const DStream S = gi_cload(P.streams, s);
-      const uint64_t fm = gm & S.gmask;
+      const uint64_t fm0 = gm & S.gmask;
+      if (is_long && fm0) {
+        const uint32_t k = atomicAdd(B.long_count, 1u);
+        if (k < B.long_cap) B.long_list[k] = make_uint2(base + ii, s);
+        else void_request(B, it.req);  // list full: the request's phase-A bits are void (exact)
+      }
+      const uint64_t fm = is_long ? 0ull : fm0;
       if (!__ballot(fm != 0)) {
         if (lane == 0 && S.job_count && blk < B.qcap) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2(0u, 0u);
         continue;
@@ -4625,6 +4633,67 @@ __device__ bool wave_validate(const DOp& o, const uint8_t* s, uint32_t n) {
   return __ballot(r) != 0;
 }
 
+// One wave runs transformation chain (off, len) over v[0, *cn): chunk-parallel
+// for the chunkable transformations (t_sync boundaries), lane 0 otherwise.
+// t0 / t1 are the two cap-byte buffers; *cur / *cn are the input on entry
+// and the output on return; false on overflow.  summ = byte summary of v.
+__device__ bool wave_run_chain(const DProgram& P, uint32_t off, uint32_t len, const uint8_t* src0, uint8_t* t0,
+                               uint8_t* t1, uint64_t cap, uint32_t summ, const uint8_t** pcur, uint32_t* pcn) {
+  const uint32_t L = threadIdx.x;
+  const uint8_t* cur = *pcur;
+  uint32_t cn = *pcn;
+  bool ok = true;
+  for (uint32_t q = 0; q < len && ok; q++) {
+    const uint8_t code = (uint8_t)P.tchains[off + q];
+    if (transform_identity(summ, code)) continue;
+    // buffers: tmp / dst are the two transformation buffers other than cur
+    uint8_t* tmp = cur == t1 ? t0 : t1;
+    uint8_t* dst = cur == src0 ? t0 : (uint8_t*)cur;
+    if (dst == tmp) dst = tmp == t0 ? t1 : t0;
+    int64_t outn = -1;
+    if (t_chunkable(code) && 3ull * cn + 8 * 64 <= cap) {
+      const uint8_t* src = cur;
+      uint32_t a, e;
+      wave_chunks(cn, [&](uint32_t p) { return t_sync(code, src, p); }, &a, &e);
+      const bool act = a != 0xFFFFFFFFu && e > a;
+      uint8_t* lt = tmp + 3ull * (act ? a : 0u) + 8u * L;
+      int64_t m = act ? apply_transform_inl(P, code, src + a, e - a, lt, 3 * (e - a) + 8) : 0;
+      uint32_t tot = 0, o0 = 0;
+      if (__ballot(m < 0) == 0) o0 = wave_excl_sum((uint32_t)m, &tot);
+      const bool bad = __ballot(m < 0) != 0 || tot > cap;
+      if (!bad) {
+        __syncthreads();  // tmp written; dst (possibly the source) is free
+        uint32_t sm = m > 0 ? value_summary(lt, (uint32_t)m) : 0u;
+        for (uint32_t i = 0; i < (uint32_t)m; i++) dst[o0 + i] = lt[i];
+        for (int x = 32; x > 0; x >>= 1) sm |= (uint32_t)__shfl_xor((int)sm, x, 64);
+        summ = sm;
+        __syncthreads();
+        outn = tot;
+        cur = dst;
+      }
+    } else {  // sequential on lane 0
+      int m = 0;
+      if (L == 0) m = (int)max(apply_transform(P, code, cur, cn, tmp, (uint32_t)min(cap, (uint64_t)0xFFFFFFFFu)), (int64_t)-1);
+      m = __shfl(m, 0, 64);
+      __syncthreads();
+      if (m >= 0) {
+        outn = m;
+        cur = tmp;
+        uint32_t a, e;
+        wave_chunks((uint32_t)m, [&](uint32_t) { return true; }, &a, &e);
+        uint32_t sm = (a != 0xFFFFFFFFu && e > a) ? value_summary(cur + a, e - a) : 0u;
+        for (int x = 32; x > 0; x >>= 1) sm |= (uint32_t)__shfl_xor((int)sm, x, 64);
+        summ = sm;
+      }
+    }
+    if (outn < 0) ok = false;
+    else cn = (uint32_t)outn;
+  }
+  *pcur = cur;
+  *pcn = cn;
+  return ok;
+}
+
 __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
   __shared__ __attribute__((aligned(16))) uint8_t kb_lds[GI_BODY_LDS];
   const uint32_t L = threadIdx.x;
@@ -4662,52 +4731,7 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
           for (int q = 32; q > 0; q >>= 1) m |= (uint32_t)__shfl_xor((int)m, q, 64);
           summ = m;
         }
-        for (uint32_t q = 0; q < R.tchain_len && ok; q++) {
-          const uint8_t code = (uint8_t)P.tchains[R.tchain_off + q];
-          if (transform_identity(summ, code)) continue;
-          // buffers: tmp / dst are the two transformation buffers other than cur
-          uint8_t* tmp = cur == g.t1 ? g.t0 : g.t1;
-          uint8_t* dst = cur == body ? g.t0 : (uint8_t*)cur;
-          if (dst == tmp) dst = tmp == g.t0 ? g.t1 : g.t0;
-          int64_t outn = -1;
-          if (t_chunkable(code) && 3ull * cn + 8 * 64 <= g.cap_t) {
-            const uint8_t* src = cur;
-            uint32_t a, e;
-            wave_chunks(cn, [&](uint32_t p) { return t_sync(code, src, p); }, &a, &e);
-            const bool act = a != 0xFFFFFFFFu && e > a;
-            uint8_t* lt = tmp + 3ull * (act ? a : 0u) + 8u * L;
-            int64_t m = act ? apply_transform_inl(P, code, src + a, e - a, lt, 3 * (e - a) + 8) : 0;
-            uint32_t tot = 0, o0 = 0;
-            if (__ballot(m < 0) == 0) o0 = wave_excl_sum((uint32_t)m, &tot);
-            const bool bad = __ballot(m < 0) != 0 || tot > g.cap_t;
-            if (!bad) {
-              __syncthreads();  // tmp written; dst (possibly the source) is free
-              uint32_t sm = m > 0 ? value_summary(lt, (uint32_t)m) : 0u;
-              for (uint32_t i = 0; i < (uint32_t)m; i++) dst[o0 + i] = lt[i];
-              for (int x = 32; x > 0; x >>= 1) sm |= (uint32_t)__shfl_xor((int)sm, x, 64);
-              summ = sm;
-              __syncthreads();
-              outn = tot;
-              cur = dst;
-            }
-          } else {  // sequential on lane 0
-            int m = 0;
-            if (L == 0) m = (int)max(apply_transform(P, code, cur, cn, tmp, g.cap_t), (int64_t)-1);
-            m = __shfl(m, 0, 64);
-            __syncthreads();
-            if (m >= 0) {
-              outn = m;
-              cur = tmp;
-              uint32_t a, e;
-              wave_chunks((uint32_t)m, [&](uint32_t) { return true; }, &a, &e);
-              uint32_t sm = (a != 0xFFFFFFFFu && e > a) ? value_summary(cur + a, e - a) : 0u;
-              for (int x = 32; x > 0; x >>= 1) sm |= (uint32_t)__shfl_xor((int)sm, x, 64);
-              summ = sm;
-            }
-          }
-          if (outn < 0) ok = false;
-          else cn = (uint32_t)outn;
-        }
+        ok = wave_run_chain(P, R.tchain_off, R.tchain_len, body, g.t0, g.t1, g.cap_t, summ, &cur, &cn);
       }
       const uint64_t c1 = B.prof ? clock64() : 0;
       bool hit;
@@ -4739,6 +4763,101 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
       if (B.prof && k < 16 && L == 0) {  // GI_PROF: cycles per link (transform, operator), per body
         atomicAdd(&B.prof[96 + 2 * k], (unsigned long long)(c1 - c0));
         atomicAdd(&B.prof[97 + 2 * k], (unsigned long long)(clock64() - c1));
+      }
+    }
+  }
+}
+
+// Long values (>= GI_LONG_MIN bytes): one wave per (item, stream) listed by
+// k_stream.  The stream's chain runs chunk-parallel (wave_run_chain) into the
+// workgroup's two HBM buffers; each admitted pattern is decided exactly with
+// its rule's own operator automaton (wave_dfa_match: chunk-parallel with
+// speculative entry states checked lane by lane), the stream's validate /
+// detect operators likewise -> hit bits + value map.  An overflowing chain
+// sets every admitted bit ("maybe", exact).
+__global__ void __launch_bounds__(64) k_long(DProgram P, DBatch B) {
+  __shared__ __attribute__((aligned(16))) uint8_t kl_lds[GI_BODY_LDS];
+  __shared__ LiSqli lst;
+  const uint32_t L = threadIdx.x;
+  const uint32_t n = min(*B.long_count, B.long_cap);
+  uint8_t* t0 = B.long_buf + (uint64_t)blockIdx.x * 2ull * B.long_bufcap;
+  uint8_t* t1 = t0 + B.long_bufcap;
+  for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {
+    const uint2 ent = B.long_list[e];
+    GI_BOUND(ent.x < B.items_cap && ent.y < P.n_streams, ent.x, ent.y);
+    const Item it = ((const Item*)B.items)[ent.x];
+    const DStream S = P.streams[ent.y];
+    const uint64_t fm = B.igm[ent.x] & S.gmask;
+    const uint32_t r = it.req, vix = meta_vix(it.meta);
+    uint32_t summ;
+    {
+      uint32_t a, b;
+      wave_chunks(it.vn, [&](uint32_t) { return true; }, &a, &b);
+      uint32_t m = (a != 0xFFFFFFFFu && b > a) ? value_summary(it.vp + a, b - a) : 0u;
+      for (int q = 32; q > 0; q >>= 1) m |= (uint32_t)__shfl_xor((int)m, q, 64);
+      summ = m;
+    }
+    const uint8_t* cur = it.vp;
+    uint32_t cn = it.vn;
+    const bool ok = wave_run_chain(P, S.tchain_off, S.tchain_len, it.vp, t0, t1, B.long_bufcap, summ, &cur, &cn);
+    // validate / detect operators of the stream
+    for (uint32_t q = 0; q < S.val_count; q++) {
+      const DScanVal sv = P.svals[S.val_begin + q];
+      if (!(fm & sv.fmask)) continue;
+      bool hit = true;
+      if (ok) {
+        bool res;
+        if (sv.kind == OP_DETECT_SQLI || sv.kind == OP_DETECT_XSS) {
+          int x = 0;
+          if (L == 0)
+            x = sv.kind == OP_DETECT_SQLI ? li_detect_sqli(cur, cn, &lst, li_tables_const()) : li_detect_xss(cur, cn);
+          res = __shfl(x, 0, 64) != 0;
+        } else {
+          DOp vo{};
+          vo.kind = sv.kind;
+          for (int k = 0; k < 8; k++) vo.bits[k] = sv.bits[k];
+          res = wave_validate(vo, cur, cn);
+        }
+        hit = res != (sv.negate != 0);
+      }
+      if (hit && L == 0) hit_value(B, sv.slot, r, vix);
+    }
+    // automaton patterns: each through its rule's operator
+    for (uint32_t j = 0; j < S.job_count; j++) {
+      const DJob J = P.jobs[S.job_begin + j];
+      for (uint32_t q = 0; q < J.jdfa_count; q++) {
+        const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
+        uint64_t al = 0;
+        for (uint64_t f = fm; f; f &= f - 1) al |= P.u64pool[jd.fmask_off + (__ffsll((unsigned long long)f) - 1)];
+        for (uint64_t x = al; x; x &= x - 1) {
+          const int k = __ffsll((unsigned long long)x) - 1;
+          const uint32_t slot = P.pats[jd.pat_begin + k].slot;
+          const bool neg = (jd.neg_mask >> k) & 1ull;
+          bool hit = true;
+          if (ok) {
+            const DRule R = P.rules[P.slot_rules[slot]];
+            const DOp o = P.ops[R.op];
+            bool m = false;
+            if (o.nfa >= 0) {
+              int y = 0;
+              if (L == 0) y = nfa_match(P, o.nfa, cur, cn) ? 1 : 0;
+              m = __shfl(y, 0, 64) != 0;
+            } else {
+              for (uint32_t g = 0; g < max(o.ngroups, 1u) && !m; g++) {
+                const DDfa d = P.dfas[o.dfa + (int32_t)g];
+                if (d.multi) {
+                  int y = 0;
+                  if (L == 0) y = dfa_match(P, o.dfa + (int32_t)g, cur, cn, false) ? 1 : 0;
+                  m = __shfl(y, 0, 64) != 0;
+                } else {
+                  m = wave_dfa_match(P, d, cur, cn, kl_lds);
+                }
+              }
+            }
+            hit = m != neg;
+          }
+          if (hit && L == 0) hit_value(B, slot, r, vix);
+        }
       }
     }
   }
@@ -5128,6 +5247,7 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
     GI_LAUNCH("k_stream3", (k_stream<128, 132>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
     GI_LAUNCH("k_stream4", (k_stream<0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
     if (P.n_det_streams) GI_LAUNCH("k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
+    if (B.long_cap) GI_LAUNCH("k_long", k_long, dim3(B.long_grid), dim3(64), 0, stream, P, B);
     if (ev) (void)hipEventRecord(ev[1], stream);
     for (int big = 0; big < 2; big++)
       if (S.n_jobs[big])

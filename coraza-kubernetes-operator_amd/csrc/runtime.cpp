@@ -84,7 +84,9 @@ struct gi_ctx {
   DevBuf tally_idbuf;                  // distinct rule ids, ascending (k_tally bins)
   std::vector<uint32_t> tally_ids;
   // phase A
-  DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes;
+  DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf;
+  uint32_t long_cap = 0;
+  uint64_t long_bufcap = 0;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0, det_cap = 0;
   uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0, det_bytes_cap = 0;
   bool diag_on = false, prof_on = false;
@@ -332,6 +334,10 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   UP(tchains32, tch32, uint32_t)
   UP(always_slots, P.always_slots, uint32_t)
   UP(body_links, P.body_links, uint32_t)
+  std::vector<uint32_t> slot_rules(std::max<uint32_t>(P.n_hit_slots, 1), 0u);
+  for (uint32_t i = 0; i < (uint32_t)P.rules.size(); i++)
+    if (P.rules[i].hit_slot >= 0 && (uint32_t)P.rules[i].hit_slot < P.n_hit_slots) slot_rules[P.rules[i].hit_slot] = i;
+  UP(slot_rules, slot_rules, uint32_t)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return discard(e == hipErrorOutOfMemory ? GI_ENOMEM : GI_ENODEV, "ruleset upload failed");
@@ -470,7 +476,7 @@ void gi_ctx_free(gi_ctx* c) {
   c->prof.release();
   for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
-                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes})
+                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf})
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
@@ -494,7 +500,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   const uint32_t n = in->n_req;
   // validate spans and lay out per-request scratch (lengths only)
   std::vector<ReqLayout> lay(n);
-  uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0, vmap_bits = 0;
+  uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0, vmap_bits = 0, max_req_bytes = 0;
   uint32_t n_mp_body = 0;
   uint32_t max_cap_t = 64;
   const uint32_t nslots = c->rs->prog.n_slots;
@@ -576,6 +582,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     post_total += PG.body_access ? post_fields : 0;
     raw_total += (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
     raw_body += q.body.len;
+    max_req_bytes = std::max<uint64_t>(max_req_bytes, (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes + q.body.len);
     max_cap_t = (uint32_t)std::max<uint64_t>(max_cap_t, cap_t);
     ReqLayout& L = lay[r];
     L.vmap_bit = vmap_bits;
@@ -657,6 +664,13 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     (void)ns;
     if ((e = c->slow.ensure(40ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
+    // long values (>= GI_LONG_MIN bytes): one k_long wave per (item, stream), each
+    // workgroup with two buffers of 3x the longest request (overflow: "maybe", exact)
+    c->long_cap = (uint32_t)std::min<uint64_t>(((raw_total + raw_body) / GI_LONG_MIN + 16) * 2ull * ns, 0x7FFFFFFFull);
+    c->long_bufcap = (3ull * max_req_bytes + 1024 + 15) & ~15ull;
+    if ((e = c->long_list.ensure(8ull * c->long_cap)) != hipSuccess) return hip_fail(c, e, "alloc long-value list");
+    if ((e = c->long_buf.ensure((uint64_t)GI_LONG_GRID * 2 * c->long_bufcap)) != hipSuccess)
+      return hip_fail(c, e, "alloc long-value buffers");
     // @detectSQLi/@detectXSS candidate list (overflow: the vals' bits become "maybe", exact)
     // an item lists its unchanged value once and each differently transformed
     // output once per detect stream: 2 entries per item covers the common case
@@ -738,6 +752,12 @@ int gi_run_staged(gi_ctx* c) {
     B.slow_bytes = (uint8_t*)c->slow_bytes.p;
     B.slow_bytes_cap = c->slow_bytes_cap;
     B.slow_used = (unsigned long long*)(cp + 8);
+    B.long_list = (uint2*)c->long_list.p;
+    B.long_count = (uint32_t*)(cp + 40);
+    B.long_cap = c->prog.n_streams ? c->long_cap : 0;
+    B.long_grid = GI_LONG_GRID;
+    B.long_buf = (uint8_t*)c->long_buf.p;
+    B.long_bufcap = c->long_bufcap;
     B.det = c->det.p;
     B.det_count = (uint32_t*)(cp + 24);
     B.det_cap = c->det_cap;
