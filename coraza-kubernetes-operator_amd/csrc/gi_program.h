@@ -526,7 +526,6 @@ struct DProgram {
   uint8_t mv_used;              // some target / macro reads MATCHED_VAR(S)(_NAME(S)): k_eval records matches
   uint8_t _pad;
   uint64_t body_limit;
-  const uint32_t* slot_rules;   // rule (link) index of each hit slot (k_long evaluates a pattern through its op)
   uint32_t n_det_streams;       // streams with @detectSQLi/@detectXSS vals (k_detect entries carry a mask)
   uint32_t det_streams[GI_MAX_DET_STREAMS];
 };

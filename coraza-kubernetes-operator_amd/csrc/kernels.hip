@@ -2886,8 +2886,16 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         const DVarRef vr = gi_cload(P.vars, R.var_begin + vi);
         if (!vr.residual) continue;
         if (vr.var == S_REQUEST_BODY && t.body_spec && R.phase >= 2) continue;  // k_body's bit
-        if (vr.var >= S_COUNT) {  // a body collection phase A never scans (multipart): any entry -> "maybe"
-          any = t.n_mp != 0;
+        if (vr.var >= S_COUNT) {  // a body collection phase A never scans (multipart): test its entries
+          // (key filters ignored: a superset, the full evaluation below is exact)
+          for (uint32_t f = 0; f < t.nf && !any && t.n_mp; f++) {
+            const Field fl = t.fields[f];
+            bool names;
+            if (!field_in(vr.var, fl.kind, &names)) continue;
+            bool ok;
+            const Str tv = transform(t, R, names ? fl.k : fl.v, names ? fl.kn : fl.vn, &ok);
+            any = !ok || eval_op(t, o, tv.p, tv.n);
+          }
           continue;
         }
         bool ok;
@@ -4770,13 +4778,12 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
 
 // Long values (>= GI_LONG_MIN bytes): one wave per (item, stream) listed by
 // k_stream.  The stream's chain runs chunk-parallel (wave_run_chain) into the
-// workgroup's two HBM buffers; each admitted pattern is decided exactly with
-// its rule's own operator automaton (wave_dfa_match: chunk-parallel with
-// speculative entry states checked lane by lane), the stream's validate /
-// detect operators likewise -> hit bits + value map.  An overflowing chain
-// sets every admitted bit ("maybe", exact).
+// workgroup's two HBM buffers; the stream's automata are spread over the 64
+// lanes, each a sequential full scan (no speculative chunk states to
+// mispredict on 1 MB values), the validate operators run chunk-parallel and
+// the detectors on lane 0 -> hit bits + value map.  An overflowing chain sets
+// every admitted bit ("maybe", exact).
 __global__ void __launch_bounds__(64) k_long(DProgram P, DBatch B) {
-  __shared__ __attribute__((aligned(16))) uint8_t kl_lds[GI_BODY_LDS];
   __shared__ LiSqli lst;
   const uint32_t L = threadIdx.x;
   const uint32_t n = min(*B.long_count, B.long_cap);
@@ -4822,41 +4829,24 @@ __global__ void __launch_bounds__(64) k_long(DProgram P, DBatch B) {
       }
       if (hit && L == 0) hit_value(B, sv.slot, r, vix);
     }
-    // automaton patterns: each through its rule's operator
+    // automaton patterns: the stream's (job, automaton) pairs spread over the
+    // lanes, each scanned sequentially over the whole value on the global
+    // tables (scan_full: the union automaton's match mask, as k_scan_slow)
+    uint32_t pair = 0;
     for (uint32_t j = 0; j < S.job_count; j++) {
       const DJob J = P.jobs[S.job_begin + j];
-      for (uint32_t q = 0; q < J.jdfa_count; q++) {
+      for (uint32_t q = 0; q < J.jdfa_count; q++, pair++) {
+        if ((pair & 63u) != L) continue;
         const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
         uint64_t al = 0;
         for (uint64_t f = fm; f; f &= f - 1) al |= P.u64pool[jd.fmask_off + (__ffsll((unsigned long long)f) - 1)];
-        for (uint64_t x = al; x; x &= x - 1) {
+        if (!al) continue;
+        uint64_t x = al;
+        if (ok) x &= scan_full(P, P.dfas[jd.dfa], cur, cn) ^ jd.neg_mask;
+        while (x) {
           const int k = __ffsll((unsigned long long)x) - 1;
-          const uint32_t slot = P.pats[jd.pat_begin + k].slot;
-          const bool neg = (jd.neg_mask >> k) & 1ull;
-          bool hit = true;
-          if (ok) {
-            const DRule R = P.rules[P.slot_rules[slot]];
-            const DOp o = P.ops[R.op];
-            bool m = false;
-            if (o.nfa >= 0) {
-              int y = 0;
-              if (L == 0) y = nfa_match(P, o.nfa, cur, cn) ? 1 : 0;
-              m = __shfl(y, 0, 64) != 0;
-            } else {
-              for (uint32_t g = 0; g < max(o.ngroups, 1u) && !m; g++) {
-                const DDfa d = P.dfas[o.dfa + (int32_t)g];
-                if (d.multi) {
-                  int y = 0;
-                  if (L == 0) y = dfa_match(P, o.dfa + (int32_t)g, cur, cn, false) ? 1 : 0;
-                  m = __shfl(y, 0, 64) != 0;
-                } else {
-                  m = wave_dfa_match(P, d, cur, cn, kl_lds);
-                }
-              }
-            }
-            hit = m != neg;
-          }
-          if (hit && L == 0) hit_value(B, slot, r, vix);
+          x &= x - 1;
+          hit_value(B, P.pats[jd.pat_begin + k].slot, r, vix);
         }
       }
     }

@@ -334,10 +334,6 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   UP(tchains32, tch32, uint32_t)
   UP(always_slots, P.always_slots, uint32_t)
   UP(body_links, P.body_links, uint32_t)
-  std::vector<uint32_t> slot_rules(std::max<uint32_t>(P.n_hit_slots, 1), 0u);
-  for (uint32_t i = 0; i < (uint32_t)P.rules.size(); i++)
-    if (P.rules[i].hit_slot >= 0 && (uint32_t)P.rules[i].hit_slot < P.n_hit_slots) slot_rules[P.rules[i].hit_slot] = i;
-  UP(slot_rules, slot_rules, uint32_t)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return discard(e == hipErrorOutOfMemory ? GI_ENOMEM : GI_ENODEV, "ruleset upload failed");
