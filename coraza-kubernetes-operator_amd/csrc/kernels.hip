@@ -1275,6 +1275,7 @@ struct Tx {
   }* rtgt;
   uint32_t nrtgt;
   uint32_t n_mp;             // multipart collection entries (FILES*, MULTIPART_PART_HEADERS)
+  const uint32_t* mpl;       // their field indices (nullptr: not listed, scan all fields)
   uint32_t nremoved;
   uint8_t engine, body_access, body_proc, phase;
   uint8_t force_body;
@@ -2888,8 +2889,9 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         if (vr.var == S_REQUEST_BODY && t.body_spec && R.phase >= 2) continue;  // k_body's bit
         if (vr.var >= S_COUNT) {  // a body collection phase A never scans (multipart): test its entries
           // (key filters ignored: a superset, the full evaluation below is exact)
-          for (uint32_t f = 0; f < t.nf && !any && t.n_mp; f++) {
-            const Field fl = t.fields[f];
+          const uint32_t nscan = t.mpl ? t.n_mp : (t.n_mp ? t.nf : 0u);
+          for (uint32_t k = 0; k < nscan && !any; k++) {
+            const Field fl = t.fields[t.mpl ? t.mpl[k] : k];
             bool names;
             if (!field_in(vr.var, fl.kind, &names)) continue;
             bool ok;
@@ -4954,6 +4956,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
     t.nremoved = 0;
     t.nrtgt = 0;
     t.n_mp = 0;
+    t.mpl = nullptr;
     t.engine = P.rule_engine;
     t.body_access = P.body_access;
     t.force_body = 0;
@@ -5053,6 +5056,17 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
                 t.has_post = t.nf > nf0;
               }
               for (uint32_t f = H->nf; f < t.nf; f++) t.n_mp += t.fields[f].kind >= FK_FILE ? 1u : 0u;
+              {  // list them (the residual clear-bit test of FILES* targets visits only these)
+                const uint32_t pad = (4u - (uint32_t)((uintptr_t)(t.bytes + t.nb) & 3u)) & 3u;
+                if (t.n_mp && (uint64_t)t.nb + pad + 4ull * t.n_mp <= t.cap_b) {
+                  uint32_t* l = (uint32_t*)(t.bytes + t.nb + pad);
+                  uint32_t k = 0;
+                  for (uint32_t f = H->nf; f < t.nf; f++)
+                    if (t.fields[f].kind >= FK_FILE) l[k++] = f;
+                  t.nb += pad + 4 * t.n_mp;
+                  t.mpl = l;
+                }
+              }
               if (err) {
                 t.single[S_MULTIPART_STRICT_ERROR] = {CS_ONE, 1};
                 t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
