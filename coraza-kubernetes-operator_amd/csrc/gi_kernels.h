@@ -19,8 +19,8 @@ struct ReqLayout {
   uint32_t cap_b;  // decoded-bytes arena
   uint32_t cap_t;  // each of the two transformation buffers
   uint32_t cap_mt; // macro expansion scratch == TX string arena size
-  uint64_t vmap_bit;   // first bit of the request's value map in DBatch.vmap (a multiple of 32)
-  uint32_t vmap_bits;  // 2 x cap_f: bit 2f = value of field f hit, bit 2f+1 = its key
+  uint64_t vmap_bit;   // first word of the request's value signatures in DBatch.vmap
+  uint32_t vmap_bits;  // 2 x cap_f signatures: word 2f = value of field f, 2f + 1 = its key
   uint32_t _pad;
 };
 
@@ -37,7 +37,8 @@ struct DBatch {
   unsigned long long* tally;  // gi_tally counters
   uint32_t* tally_ext;        // [GI_SCORE_BINS] score histogram, then per distinct rule id match counts
   uint32_t* hits;             // phase-A hit words [ceil(n_hit_slots/32)][n_req]
-  uint32_t* vmap;             // phase-A value map: a bit per scanned (field, side) that set some hit bit
+  uint32_t* vmap;             // phase-A value map: per scanned (field, side) a u32 signature, bit (slot % 32)
+                              // of every hit slot the value set (k_eval re-tests a link only on values with its bit)
   const uint32_t* body_list;  // requests with a body, longest first (k_body: one wave each)
   uint32_t n_body;
   uint32_t n_mp_body;         // of which multipart (k_mpparse)

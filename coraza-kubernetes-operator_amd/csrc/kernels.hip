@@ -1262,7 +1262,7 @@ struct Tx {
   uint32_t ntx, cap_tx;
   Str* single;               // ReqHdr::single (per-request, in HBM scratch)
   const uint32_t* hits;      // phase-A hit words [slot/32][n_req]
-  const uint32_t* vmap;      // the request's phase-A value map (bit 2f + side)
+  const uint32_t* vmap;      // the request's phase-A value signatures (word 2f + side: bit slot % 32)
   uint32_t nf_pa;            // fields [0, nf_pa) went through phase A (value map valid)
   uint32_t n_req, req;
   bool has_post;             // ARGS_POST fields phase A did not see (phase-A bits of RF_BODYDEP links void)
@@ -3017,7 +3017,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
       if (!field_in(vr.var, fl.kind, &names)) continue;
       if (vskip && f < t.nf_pa && fl.kind <= FK_COOKIE) {  // phase-A item kinds only
         const uint32_t vb = 2 * f + (names ? 1u : 0u);
-        if (!((t.vmap[vb >> 5] >> (vb & 31)) & 1u)) continue;
+        if (!((t.vmap[vb] >> ((uint32_t)R.hit_slot & 31u)) & 1u)) continue;
       }
       if (vr.key_mode == 1) {
         if (vr.ci ? !eq_ascii_ci(fl.k, fl.kn, P.strpool + vr.key_off, vr.key_len)
@@ -3698,7 +3698,7 @@ __device__ __forceinline__ void hit_value(const DBatch& B, uint32_t slot, uint32
   if (vix != GI_NO_VIX) {
     const ReqLayout L = B.layout[r];
     GI_BOUND(vix < L.vmap_bits, vix, L.vmap_bits);
-    atomicOr(&B.vmap[(L.vmap_bit + vix) >> 5], 1u << (vix & 31));
+    atomicOr(&B.vmap[L.vmap_bit + vix], 1u << (slot & 31));  // the value's slot signature
   }
 }
 // the same for the item at global index idx (k_scan's queue lanes carry it)
@@ -4940,7 +4940,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
     t.prof_rule_cyc = B.prof ? B.prof + 128 : nullptr;
     tx_bind(t, P, g);
     t.hits = B.hits;
-    t.vmap = B.vmap + (B.layout[r].vmap_bit >> 5);
+    t.vmap = B.vmap + B.layout[r].vmap_bit;
     t.nf_pa = H->nf;
     t.n_req = B.n_req;
     t.req = r;

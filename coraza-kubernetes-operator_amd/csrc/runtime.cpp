@@ -617,7 +617,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if ((e = c->txslots.ensure(std::max<uint64_t>(24ull * PG.n_slots * n, 64))) != hipSuccess)
     return hip_fail(c, e, "alloc tx slots");
   c->hit_words = (PG.n_hit_slots + 31) / 32;
-  c->vmap_words = vmap_bits / 32;
+  c->vmap_words = vmap_bits;  // one u32 slot signature per (field, side): bit (slot % 32) of each slot it hit
   // k_body's work list: requests with a body, longest first (one wave each)
   std::vector<uint32_t> blist;
   for (uint32_t r = 0; r < n; r++)
