@@ -57,7 +57,7 @@ CONFIGS = {
     "c4": ("rulesets/crs_pl4.conf", 50_000, 0.5,
            "CRS-shaped v4 PL4 (blocking paranoia 4: +35 PL2-4 rules, @detectSQLi/@detectXSS) x C3 mix "
            "(50% POST 4-64 KB urlencoded/JSON); SURVEY C4 = 10M across 8 GPUs = this batch per GPU, repeated"),
-    "c5": (None, 256, 1.0,
+    "c5": (None, 4, 1.0,
            "generated 10k @rx rules + 100k-phrase @pmFromFile (traffic.c5_ruleset) x ~1 MB multipart bodies "
            "(traffic.c5_batch)"),
 }
