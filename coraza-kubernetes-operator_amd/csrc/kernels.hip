@@ -4864,6 +4864,9 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
   __shared__ uint32_t lw[LI_NWORDS];
   __shared__ uint16_t lh[LI_HASH_SIZE];
   __shared__ __attribute__((aligned(16))) uint8_t lp[sizeof(kLiPool)];
+  // short candidates (<= 64 B, most of them) are read from LDS: stride 68 B =
+  // 17 dwords per lane, conflict-free
+  __shared__ __attribute__((aligned(16))) uint32_t lval[256 * 17];
   for (uint32_t i = threadIdx.x; i < LI_NWORDS; i += blockDim.x) lw[i] = kLiWords[i];
   for (uint32_t i = threadIdx.x; i < LI_HASH_SIZE; i += blockDim.x) lh[i] = kLiHash[i];
   for (uint32_t i = threadIdx.x; i < sizeof(kLiPool); i += blockDim.x) lp[i] = kLiPool[i];
@@ -4877,6 +4880,18 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
     const DetEnt x = ((const DetEnt*)B.det)[e];
     GI_BOUND(x.req < B.n_req && x.off + x.len <= B.det_bytes_cap, x.req, x.off);
     const uint8_t* v = B.det_bytes + x.off;
+    if (x.len <= 64) {  // the arena offset is 16-byte aligned: four 16-byte loads
+      uint32_t* dst = lval + threadIdx.x * 17;
+      const uint4* src = (const uint4*)v;
+      for (uint32_t k = 0; k < (x.len + 15) / 16; k++) {
+        const uint4 w = src[k];
+        dst[4 * k] = w.x;
+        dst[4 * k + 1] = w.y;
+        dst[4 * k + 2] = w.z;
+        dst[4 * k + 3] = w.w;
+      }
+      v = (const uint8_t*)dst;
+    }
     int sq = -1, xs = -1;
     for (uint32_t d = 0; d < P.n_det_streams; d++) {
       if (!((x.mask >> d) & 1u)) continue;
