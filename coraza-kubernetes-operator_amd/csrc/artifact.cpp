@@ -331,6 +331,7 @@ bool validate_program(const Program& P, std::string* err) {
     if (!in(s.tchain_off, s.tchain_len, P.tchains.size()) || !in(s.filt_begin, s.filt_count, P.sfilt.size()) ||
         !in(s.job_begin, s.job_count, P.jobs.size()) || !in(s.val_begin, s.val_count, P.svals.size()))
       return bad("stream record");
+    if (s.det_id != 0xFF && s.det_id >= GI_MAX_DET_STREAMS) return bad("stream detect id");  // k_stream shifts by it
   }
   for (const DScanVal& v : P.svals)
     if (v.slot >= nhit) return bad("validate slot");

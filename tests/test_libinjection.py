@@ -173,3 +173,13 @@ def test_prefilters_are_exact(host_lib):
             n_xs += 1
             assert not L.is_xss(w), w
     assert n_sq > 10000 and n_xs > 1000
+
+
+def test_detect_ruleset_artifact_round_trip():
+    """The compiled program with detect streams survives gi_ruleset_save / load
+    (DStream.det_id is bounds-checked by the loader)."""
+    rs = gpuinspect.Ruleset(_rules(), tx_exports=["sqli", "xss"])
+    blob = rs.save()
+    rs2 = gpuinspect.Ruleset.load(blob)
+    assert rs2.info["n_hit_slots"] == rs.info["n_hit_slots"]
+    assert rs2.info["n_scan_streams"] == rs.info["n_scan_streams"]
