@@ -28,7 +28,7 @@ const char kMagic[8] = {'G', 'I', 'A', 'R', 'T', 'F', 'C', 'T'};
 struct Scalars {
   uint8_t item_sides[8];
   uint32_t item_singles, n_hit_slots, n_union_dfas, max_img_bytes, max_big_img_bytes, n_slots, n_markers;
-  uint8_t rule_engine, body_access, mv_used, _pad[5];
+  uint8_t rule_engine, body_access, mv_used, body_partial, _pad[4];
   uint64_t body_limit, source_digest;
   uint64_t compiler_rev;  // fnv64 of kCompilerRev
 };
@@ -40,7 +40,8 @@ uint64_t compiler_rev_hash() { return fnv64((const uint8_t*)kCompilerRev, strlen
   X(1, rules) X(2, top) X(3, vars) X(4, excs) X(5, ops) X(6, acts) X(7, tparts) X(8, tmpls) X(9, tchains)    \
   X(10, dfas) X(11, trans) X(12, u8pool) X(13, nranges) X(14, strpool) X(15, slot_names) X(16, u64pool)     \
   X(17, streams) X(18, filters) X(19, sfilt) X(20, body_links) X(21, always_slots) X(22, jobs) X(23, jdfas) \
-  X(24, pats) X(25, svals) X(26, images) X(27, exports) X(28, nfas)
+  X(24, pats) X(25, svals) X(26, images) X(27, exports) X(28, nfas) X(29, pikes) X(30, pike_insts)              \
+  X(31, pike_ranges)
 
 constexpr uint32_t kTagScalars = 100, kTagPlan = 101, kTagExportNames = 102;
 
@@ -48,7 +49,7 @@ uint64_t layout_signature() {
   const uint64_t sz[] = {sizeof(DRule), sizeof(DVarRef), sizeof(DExc), sizeof(DOp), sizeof(DAction),
                          sizeof(DTmplPart), sizeof(DTmpl), sizeof(DDfa), sizeof(DStream), sizeof(DFilter),
                          sizeof(DJob), sizeof(DJobDfa), sizeof(DPat), sizeof(DScanVal), sizeof(Scalars),
-                         sizeof(DNfa)};
+                         sizeof(DNfa), sizeof(DPike), sizeof(DPikeInst)};
   return fnv64((const uint8_t*)sz, sizeof(sz));
 }
 
@@ -92,6 +93,7 @@ std::vector<uint8_t> serialize_program(const Program& P) {
   s.rule_engine = P.rule_engine;
   s.body_access = P.body_access;
   s.mv_used = P.mv_used;
+  s.body_partial = P.body_partial;
   s.body_limit = P.body_limit;
   s.source_digest = P.source_digest;
   s.compiler_rev = compiler_rev_hash();
@@ -175,6 +177,7 @@ bool deserialize_program(const uint8_t* buf, size_t n, Program* P, std::string* 
         out.rule_engine = s.rule_engine;
         out.body_access = s.body_access;
         out.mv_used = s.mv_used;
+        out.body_partial = s.body_partial;
         out.body_limit = s.body_limit;
         out.source_digest = s.source_digest;
         seen_scalars = true;
@@ -306,6 +309,10 @@ bool validate_program(const Program& P, std::string* err) {
     if (o.nfa >= 0 && (size_t)o.nfa >= P.nfas.size()) return bad("operator nfa index");
     if (o.tmpl >= 0 && (size_t)o.tmpl >= ntm) return bad("operator template");
     if (o.arg_is_lit && !in(o.lit_off, o.lit_len, nstr)) return bad("operator literal");
+    if (o.pike >= 0 && ((size_t)o.pike >= P.pikes.size() || o.kind != OP_RX)) return bad("operator capture program");
+    // the @ipMatch kernel path reads lit_len bytes of network records at lit_off
+    if (o.kind == OP_IPMATCH && (!o.arg_is_lit || !in(o.lit_off, o.lit_len, nstr) || o.lit_len % GI_IPNET_BYTES))
+      return bad("ipMatch networks");
   }
   for (const DAction& a : P.acts) {
     if (a.kind == A_SETVAR || a.kind == A_SETVAR_DEL) {
@@ -315,6 +322,19 @@ bool validate_program(const Program& P, std::string* err) {
     }
     if (a.kind == A_CTL_RULE_REMOVE_TARGET && (a.tmpl < 0 || a._pad2 < 0 || !in((uint32_t)a.tmpl, (uint32_t)a._pad2, nstr)))
       return bad("ctl target key");
+  }
+  // capture programs (pike.h): every jump inside its program, rune ranges in the pool
+  for (const DPike& k : P.pikes) {
+    if (!in(k.inst_off, k.n_inst, P.pike_insts.size()) || k.n_inst == 0 || k.start >= k.n_inst ||
+        k.nslot < 2 || k.nslot > GI_PIKE_MAX_SLOTS || (k.nslot & 1))
+      return bad("capture program");
+    for (uint32_t i = 0; i < k.n_inst; i++) {
+      const DPikeInst& I = P.pike_insts[k.inst_off + i];
+      if (I.op < PK_RUNE || I.op > PK_FAIL) return bad("capture instruction");
+      if ((I.op != PK_MATCH && I.op != PK_FAIL && I.x >= k.n_inst) || (I.op == PK_SPLIT && I.y >= k.n_inst))
+        return bad("capture jump");
+      if (I.op == PK_RUNE && !in(I.roff, 2ull * I.rcnt, P.pike_ranges.size())) return bad("capture rune ranges");
+    }
   }
   // phase-A scan plan
   if (P.streams.size() > GI_MAX_STREAMS || P.filters.size() > GI_MAX_GFILTERS) return bad("scan plan size");
@@ -332,6 +352,9 @@ bool validate_program(const Program& P, std::string* err) {
         !in(s.job_begin, s.job_count, P.jobs.size()) || !in(s.val_begin, s.val_count, P.svals.size()))
       return bad("stream record");
     if (s.det_id != 0xFF && s.det_id >= GI_MAX_DET_STREAMS) return bad("stream detect id");  // k_stream shifts by it
+    if (!in(s.rmap_off, 3ull * s.rmap_cnt, P.nranges.size())) return bad("stream rune map");
+    for (uint32_t k = 0; k < s.rmap_cnt; k++)
+      if (P.nranges[s.rmap_off + 3 * k + 2] < 0x80 || P.nranges[s.rmap_off + 3 * k + 2] > 0xFF) return bad("stream rune map byte");
   }
   for (const DScanVal& v : P.svals)
     if (v.slot >= nhit) return bad("validate slot");

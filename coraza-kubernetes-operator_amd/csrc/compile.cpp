@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <sstream>
 #include <unordered_map>
@@ -109,6 +110,7 @@ struct IrWaf {
   std::string engine = "On";
   bool body_access = false;
   int64_t body_limit = 134217728;
+  bool body_partial = false;
   std::vector<IrRule> rules;
   std::map<int, Actions> defaults;
 };
@@ -214,7 +216,8 @@ const std::vector<std::string>& single_names() {
       "REQUEST_METHOD", "REQUEST_PROTOCOL", "REQUEST_URI", "REQUEST_URI_RAW", "REQUEST_LINE",
       "REQUEST_FILENAME", "REQUEST_BASENAME", "QUERY_STRING", "REQUEST_BODY",
       "REQUEST_BODY_LENGTH", "REQBODY_ERROR", "REQBODY_ERROR_MSG", "REQBODY_PROCESSOR",
-      "MULTIPART_STRICT_ERROR", "REMOTE_ADDR", "REMOTE_PORT", "FILES_COMBINED_SIZE"};
+      "MULTIPART_STRICT_ERROR", "REMOTE_ADDR", "REMOTE_PORT", "FILES_COMBINED_SIZE", "ARGS_COMBINED_SIZE",
+      "FULL_REQUEST_LENGTH", "URLENCODED_ERROR", "INBOUND_DATA_ERROR"};
   return v;
 }
 const std::map<std::string, int>& collection_ids() {
@@ -232,7 +235,7 @@ const std::map<std::string, int>& collection_ids() {
 }
 // variables the oracle knows but this engine does not evaluate yet
 bool known_unsupported_var(const std::string& n) {
-  static const char* u[] = {"ARGS_COMBINED_SIZE", "FULL_REQUEST_LENGTH", "SERVER_NAME", "URLENCODED_ERROR"};
+  static const char* u[] = {"SERVER_NAME"};
   for (auto* s : u)
     if (n == s) return true;
   return false;
@@ -692,6 +695,10 @@ IrWaf parse_seclang(const std::string& text) {
       if (!go_atoi(trim(opts), &v)) perr("invalid SecRequestBodyLimit");
       waf.body_limit = v;
     } else if (d == "secrequestbodylimitaction") {
+      const std::string o = lower(trim(opts));
+      if (o == "processpartial") waf.body_partial = true;
+      else if (o == "reject") waf.body_partial = false;
+      else perr("invalid SecRequestBodyLimitAction " + opts);
     } else if (d == "secdefaultaction") {
       Actions acts = parse_actions(opts);
       int phase = 2;
@@ -990,6 +997,7 @@ struct Lower {
     o.dfa = -1;
     o.nfa = -1;
     o.tmpl = -1;
+    o.pike = -1;
     const std::string& n = r.op_name;
     const std::string& a = r.op_arg;
     if (n == "ipmatch") {
@@ -1287,7 +1295,9 @@ struct Lower {
   // the link stays interpreter-only (TX / count targets, macro arguments,
   // operators without an automaton form, mutable singles).
   bool no_scan = false;  // the current top-level rule sits behind a paranoia gate (gated_rules)
-  bool capture_seen = true;  // some rule, macro or export can read TX:0-TX:9 (capture_observable)
+  // capture analysis (capture_analysis): every capture is observable, or only these links'
+  bool cap_global = true;
+  std::set<const IrRule*> cap_links;
 
   int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
     if (!r.has_op || no_scan) return -1;
@@ -1597,6 +1607,60 @@ struct Lower {
         owned.push_back(std::move(re));
       }
       flush();
+      // 1b. rune map: the joint partition of non-ASCII runes over the stream's
+      // image automata.  Every rune of a joint class falls in one class of
+      // each automaton, so k_stream can replace each non-ASCII rune of a value
+      // by one byte 0x80 + joint class and k_scan steps once per rune through
+      // the joint class map -- what the rune-decoding scan computes.  A stream
+      // with a byte-mode automaton or more than 127 joint classes keeps its
+      // non-ASCII values on the per-value path (k_scan_slow).
+      std::vector<uint32_t> rmap;              // (lo, hi, joint class) triples
+      std::vector<std::vector<uint8_t>> jcls;  // per joint class: the class in each automaton
+      bool mappable = true;
+      {
+        auto cls_of = [](const Dfa& d, uint32_t r) -> uint8_t {
+          const auto& nr = d.nranges;
+          size_t lo = 0, hi = nr.size() / 3;
+          while (lo < hi) {
+            const size_t mid = (lo + hi) / 2;
+            if (nr[mid * 3 + 1] < r) lo = mid + 1;
+            else hi = mid;
+          }
+          return (lo < nr.size() / 3 && nr[lo * 3] <= r) ? (uint8_t)nr[lo * 3 + 2] : (uint8_t)0;
+        };
+        std::vector<uint32_t> bnd{0x80, 0x110000};
+        for (const AutoBuild& ab : autos) {
+          if (!img_ok(ab.d)) continue;
+          if (ab.d.byte_mode) mappable = false;
+          const auto& nr = ab.d.nranges;
+          for (size_t i = 0; i + 2 < nr.size(); i += 3) {
+            bnd.push_back(std::max<uint32_t>(nr[i], 0x80));
+            bnd.push_back(std::min<uint32_t>(nr[i + 1] + 1, 0x110000));
+          }
+        }
+        std::sort(bnd.begin(), bnd.end());
+        bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+        std::map<std::vector<uint8_t>, uint32_t> ids;
+        for (size_t i = 0; mappable && i + 1 < bnd.size(); i++) {
+          if (bnd[i] >= 0x110000) break;
+          std::vector<uint8_t> tup(autos.size(), 0);
+          for (size_t k = 0; k < autos.size(); k++)
+            if (img_ok(autos[k].d) && !autos[k].d.byte_mode) tup[k] = cls_of(autos[k].d, bnd[i]);
+          auto it = ids.find(tup);
+          uint32_t jc;
+          if (it == ids.end()) {
+            jc = (uint32_t)jcls.size();
+            ids[tup] = jc;
+            jcls.push_back(tup);
+          } else {
+            jc = it->second;
+          }
+          const uint32_t lo = bnd[i], hi = bnd[i + 1] - 1;
+          if (!rmap.empty() && rmap[rmap.size() - 1] == jc && rmap[rmap.size() - 2] + 1 == lo) rmap[rmap.size() - 2] = hi;
+          else rmap.insert(rmap.end(), {lo, hi, jc});
+        }
+        if (jcls.size() > 127) mappable = false;
+      }
       // 2. stream record
       DStream s = sb.s;
       s.filt_begin = (uint32_t)P->sfilt.size();
@@ -1609,7 +1673,14 @@ struct Lower {
       s.val_count = (uint32_t)sb.vals.size();
       P->svals.insert(P->svals.end(), sb.vals.begin(), sb.vals.end());
       s.job_begin = (uint32_t)P->jobs.size();
-      s.collapse = 1;  // cleared below by any automaton that tells non-ASCII runes apart
+      s.collapse = mappable ? 1 : 0;  // values are rune-mapped (s.rmap_*) instead of going slow
+      s.rmap_off = 0;
+      s.rmap_cnt = 0;
+      if (mappable && jcls.size() > 1) {  // one class: every non-ASCII rune -> GI_RUNE_MARK
+        s.rmap_off = (uint32_t)P->nranges.size();
+        s.rmap_cnt = (uint32_t)rmap.size() / 3;
+        for (size_t i = 0; i < rmap.size(); i += 3) P->nranges.insert(P->nranges.end(), {rmap[i], rmap[i + 1], 0x80u + rmap[i + 2]});
+      }
       s.det_id = 0xFF;
       for (const DScanVal& v : sb.vals)
         if (v.kind == OP_DETECT_SQLI || v.kind == OP_DETECT_XSS) {
@@ -1695,9 +1766,8 @@ struct Lower {
               img_put(j.img_off, d.end_accept.data(), d.end_accept.size(), &jd.lds_endacc);
             }
             for (uint32_t c = 0; c < 128; c++) jam[c] |= (uint32_t)d.amap[c] << (8 * q);
-            const DDfa& dd = P->dfas[jd.dfa];
-            if (!d.byte_mode && dd.nonascii_uniform) jam[128] |= (uint32_t)dd.nonascii_cls << (8 * q);
-            else P->streams[sid].collapse = 0;
+            // rune-mapped bytes 0x80 + joint class (stage 1b)
+            for (size_t jc = 0; mappable && jc < jcls.size(); jc++) jam[0x80 + jc] |= (uint32_t)jcls[jc][pick[q]] << (8 * q);
             jd.lds_slots = (int32_t)(slots.size() * 4);  // relative; rebased below
           }
           jd.pat_begin = (uint32_t)P->pats.size();
@@ -1740,7 +1810,8 @@ struct Lower {
         P->jobs.push_back(j);
       }
       P->streams[sid].job_count = (uint32_t)P->jobs.size() - P->streams[sid].job_begin;
-      js << "],\"collapse\":" << (int)P->streams[sid].collapse << "}";
+      js << "],\"collapse\":" << (int)P->streams[sid].collapse << ",\"rune_classes\":" << (mappable ? jcls.size() : 0)
+         << "}";
     }
     js << "],\"jobs\":" << P->jobs.size() << ",\"hit_slots\":" << P->n_hit_slots
        << ",\"image_bytes\":" << P->images.size() << "}";
@@ -1759,8 +1830,11 @@ struct Lower {
     d.phase = (uint8_t)r.phase;
     d.flags = (child ? RF_CHILD : 0) | (r.secmark.empty() ? 0 : RF_MARKER);
     d.op = -1;
-    if (r.capture && capture_seen)
-      unsup("capture is not supported yet when a rule, macro or export reads TX:0-TX:9");
+    const bool cap_obs = r.capture && r.has_op && (cap_global || cap_links.count(&r));
+    if (cap_obs && r.op_name != "rx")
+      unsup("capture on @" + r.op_name + " whose TX:0-TX:8 values a rule, macro or export reads");
+    if (cap_obs && r.multimatch) unsup("observable capture with multiMatch");
+    if (cap_obs) d.flags |= RF_CAPTURE;
     if (r.multimatch) d.flags |= RF_MULTIMATCH;
     const std::string& dis = r.disruptive;
     d.disruptive = dis == "deny" ? D_DENY : dis == "drop" ? D_DROP : dis == "redirect" ? D_REDIRECT
@@ -1768,6 +1842,16 @@ struct Lower {
     if (dis == "block") d.disruptive = D_NONE;  // block without a default disruptive action
     vars(r, &d);
     if (r.has_op) d.op = op(r);
+    if (cap_obs) {  // the submatch program k_eval runs on every value the operator sees match
+      Regex re;
+      std::string err;
+      if (!re_parse("(?sm)" + r.op_arg, &re, &err)) perr("invalid regex " + r.op_arg + ": " + err);
+      DPike pk{};
+      if (!build_pike(re, &P->pike_insts, &P->pike_ranges, &pk, &err)) unsup("capture: " + err);
+      P->pikes.push_back(pk);
+      P->ops[d.op].pike = (int32_t)P->pikes.size() - 1;
+      for (int g = 0; g < 9; g++) slot(std::to_string(g));  // TX.0-TX.8 (CaptureField keys)
+    }
     d.tchain_off = (uint32_t)P->tchains.size();
     for (auto& t : r.transforms) {
       uint8_t code;
@@ -1776,7 +1860,10 @@ struct Lower {
     }
     d.tchain_len = (uint32_t)P->tchains.size() - d.tchain_off;
     actions(r, &d);
-    d.hit_slot = plan(r, d, &d.flags);
+    // a negated capturing link writes captures on values whose regex matches
+    // -- exactly those that do not make the link match -- so it is always
+    // evaluated by the interpreter (no phase-A bit)
+    d.hit_slot = (cap_obs && r.op_neg) ? -1 : plan(r, d, &d.flags);
     P->rules.push_back(d);
     const uint32_t idx = (uint32_t)P->rules.size() - 1;
     if (d.hit_slot >= 0 && (d.flags & RF_RESIDUAL) && d.phase >= 2 && d.op >= 0)
@@ -1859,52 +1946,116 @@ static std::vector<bool> gated_rules(const IrWaf& waf) {
   return out;
 }
 
-// `capture` (coraza internal/actions/capture.go; internal/operators/rx.go and
-// pm.go fill TX.0-TX.9 on a match) changes nothing but the TX.0-TX.9 values:
-// the operator's boolean result is the same with or without it.  When no
-// rule target, no macro in an operator argument / setvar / ctl, and no
-// exported name can read those keys, the action is unobservable in every
-// output this engine produces (interruption, matched ids, exported TX
-// integers) and the program drops it.  CRS uses it that way in most
-// detection rules (its only reader there is logdata, which is not an output).
-// Conservative: a whole-collection or regex-keyed TX target (counted or not) counts
-// as a reader.
-static bool capture_observable(const IrWaf& waf, const std::vector<std::string>& exports) {
-  auto lower = [](std::string x) {
+// `capture` (coraza internal/actions/capture.go; internal/operators/rx.go
+// FindStringSubmatch -> TX.0-TX.8) changes nothing but the TX.0-TX.8 values:
+// the operator's boolean result is the same with or without it.  A capture
+// matters only if something reads those keys before the next capture
+// overwrites them.  The analysis:
+//   * readers: TX targets (a digit key, the whole collection, a regex key that
+//     matches a digit key), %{tx.<digit>} macros (operator argument, setvar,
+//     ctl), exported digit keys;
+//   * a read of group k is "fed in chain" when a link of the reader's own
+//     chain that certainly ran a capture of group k comes before the read:
+//     a non-negated @rx with >= k groups (its chain successors only run when
+//     it matched, and every match writes groups 0..ncap), or @detectSQLi for
+//     k = 0.  For a target the feeder must be an earlier link; for an action
+//     macro the link itself counts (its captures precede its actions); an
+//     operator-argument macro is expanded before the link's own operator.
+//   * if every read is fed in chain, the observable captures are those links
+//     (the feeder and any capture link between it and the reader); otherwise
+//     every capture in the program is observable (cap_global).
+// CRS's capture rules are read only through logdata (not an output) except
+// the 920420 / 920480 chains, which read their own parent's TX.0 / TX.1.
+static void capture_analysis(const IrWaf& waf, const std::vector<std::string>& exports, bool* global,
+                             std::set<const IrRule*>* links) {
+  auto lowerc = [](std::string x) {
     for (auto& c : x) c = (char)tolower((unsigned char)c);
     return x;
   };
   auto digit_key = [](const std::string& k) { return k.size() == 1 && k[0] >= '0' && k[0] <= '9'; };
-  auto macro_reads = [&](const std::string& s) {
-    const std::string l = lower(s);
+  // groups read by macros in s: bit k (bit 10: an unresolvable read)
+  auto macro_groups = [&](const std::string& s) {
+    uint32_t m = 0;
+    const std::string l = lowerc(s);
     for (size_t p = l.find("%{"); p != std::string::npos; p = l.find("%{", p + 2)) {
       size_t q = p + 2;
       while (q < l.size() && (l[q] == ' ' || l[q] == '\t')) q++;
       if (l.compare(q, 2, "tx") == 0 && q + 3 < l.size() && (l[q + 2] == '.' || l[q + 2] == ':') &&
           isdigit((unsigned char)l[q + 3]))
-        return true;
+        m |= (q + 4 < l.size() && isdigit((unsigned char)l[q + 4])) ? 0u : (1u << (l[q + 3] - '0'));
     }
-    return false;
+    return m;
   };
-  auto reads = [&](const IrRule& r) {
-    for (const IrVar& v : r.vars)
-      if (lower(v.name) == "tx" && (v.key.empty() || v.key_rx || digit_key(v.key))) return true;
-    if (r.has_op && macro_reads(r.op_arg)) return true;
-    for (const IrNd& a : r.nd)
-      if (macro_reads(a.sv_key) || macro_reads(a.sv_value) || macro_reads(a.ctl_value)) return true;
-    return false;
+  auto target_groups = [&](const IrRule& r) {
+    uint32_t m = 0;
+    for (const IrVar& v : r.vars) {
+      if (lowerc(v.name) != "tx") continue;
+      if (v.key.empty()) {
+        m |= 0x3FFu;
+      } else if (v.key_rx) {
+        Regex re;
+        std::string err;
+        Dfa d;
+        if (!re_parse(v.key, &re, &err) || !build_regex_dfa(re, &d, &err)) {
+          m |= 0x3FFu;
+        } else {
+          for (int g = 0; g < 10; g++) {
+            const uint8_t c = (uint8_t)('0' + g);
+            if (dfa_host_match(d, &c, 1)) m |= 1u << g;
+          }
+        }
+      } else if (digit_key(v.key)) {
+        m |= 1u << (v.key[0] - '0');
+      }
+    }
+    return m;
   };
+  // groups link r certainly writes when it matched
+  auto writes = [&](const IrRule& r) {
+    if (!r.capture || !r.has_op || r.op_neg) return 0u;
+    if (r.op_name == "detectsqli") return 1u;
+    if (r.op_name != "rx") return 1u;  // @pm: at least TX.0 on a match
+    Regex re;
+    std::string err;
+    if (!re_parse("(?sm)" + r.op_arg, &re, &err)) return 0u;
+    return (1u << std::min(re.ncap + 1, 9)) - 1u;
+  };
+  *global = false;
+  links->clear();
   for (const std::string& e : exports) {
-    std::string k = lower(e);
+    std::string k = lowerc(e);
     if (k.rfind("tx.", 0) == 0) k = k.substr(3);
-    if (digit_key(k)) return true;
+    if (digit_key(k)) *global = true;
   }
-  for (const IrRule& r : waf.rules) {
-    if (reads(r)) return true;
-    for (const IrRule& c : r.children)
-      if (reads(c)) return true;
+  for (const IrRule& top : waf.rules) {
+    std::vector<const IrRule*> chain{&top};
+    for (const IrRule& c : top.children) chain.push_back(&c);
+    for (size_t j = 0; j < chain.size(); j++) {
+      const IrRule& r = *chain[j];
+      uint32_t before = target_groups(r) | (r.has_op ? macro_groups(r.op_arg) : 0u);  // read before r's operator
+      uint32_t after = 0;                                                              // read by r's actions
+      for (const IrNd& a : r.nd) after |= macro_groups(a.sv_key) | macro_groups(a.sv_value) | macro_groups(a.ctl_value);
+      for (int pass = 0; pass < 2; pass++) {
+        const uint32_t need = pass == 0 ? before : after;
+        const size_t last = pass == 0 ? j : j + 1;  // feeders: links [0, last)
+        for (int g = 0; g < 10; g++) {
+          if (!((need >> g) & 1u)) continue;
+          if (g == 9) {  // TX.9 is never written by a capture: nothing to feed
+            continue;
+          }
+          size_t f = last;
+          while (f > 0 && !((writes(*chain[f - 1]) >> g) & 1u)) f--;
+          if (f == 0) {
+            *global = true;
+            continue;
+          }
+          for (size_t x = f - 1; x < last; x++)
+            if (chain[x]->capture) links->insert(chain[x]);
+        }
+      }
+      if (((before | after) >> 10) & 1u) *global = true;
+    }
   }
-  return false;
 }
 
 int compile_program(const std::string& text, const std::vector<std::string>& exports, uint32_t cap,
@@ -1923,7 +2074,7 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
     // the merged list then holds "block" followed by the default action; the last
     // disruptive action wins (apply_actions), so nothing else is needed here.
     const std::vector<bool> gated = gated_rules(waf);
-    L.capture_seen = capture_observable(waf, exports);
+    capture_analysis(waf, exports, &L.cap_global, &L.cap_links);
     for (size_t ti = 0; ti < waf.rules.size(); ti++) {
       const IrRule& r = waf.rules[ti];
       L.no_scan = gated[ti];
@@ -1937,10 +2088,22 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
       }
     }
     L.finish_streams();
+    {  // top-level rules with an observable capture link (capture records, gi_capture)
+      std::string ids;
+      for (uint32_t ti : out->top)
+        for (int32_t ci = (int32_t)ti; ci >= 0; ci = out->rules[ci].chain_next)
+          if (out->rules[ci].flags & RF_CAPTURE) {
+            ids += (ids.empty() ? "" : ",") + std::to_string(out->rules[ti].id);
+            break;
+          }
+      out->plan_json.pop_back();  // the closing brace
+      out->plan_json += ",\"capture_rules\":[" + ids + "]}";
+    }
     if (out->u64pool.empty()) out->u64pool.push_back(0);
     out->rule_engine = waf.engine == "On" ? ENGINE_ON : waf.engine == "Off" ? ENGINE_OFF : ENGINE_DETECTION_ONLY;
     out->body_access = waf.body_access;
     out->body_limit = (uint64_t)waf.body_limit;
+    out->body_partial = waf.body_partial ? 1 : 0;
     out->export_names = exports;
     for (auto& e : exports) out->exports.push_back(L.slot(e));
     out->n_slots = (uint32_t)L.slots.size();

@@ -16,7 +16,7 @@ namespace gi {
 // even when the record layout stays the same.  gi_compile folds it into the
 // source digest and the artifact stores it, so an artifact written by another
 // compiler revision is rejected (and recompiled from the rules text).
-constexpr const char* kCompilerRev = "gi-seclang-compiler/8";
+constexpr const char* kCompilerRev = "gi-seclang-compiler/10";
 
 struct Program {
   std::vector<DRule> rules;
@@ -48,6 +48,9 @@ struct Program {
   std::vector<DPat> pats;
   std::vector<DScanVal> svals;
   std::vector<uint8_t> images;
+  std::vector<DPike> pikes;            // submatch programs of observable captures
+  std::vector<DPikeInst> pike_insts;
+  std::vector<uint32_t> pike_ranges;
   uint32_t n_hit_slots = 0;
   uint32_t n_union_dfas = 0;
   uint32_t max_img_bytes = 0;      // largest small-job LDS image
@@ -58,6 +61,7 @@ struct Program {
   uint32_t n_slots = 0, n_markers = 0;
   uint8_t rule_engine = 1, body_access = 0;
   uint8_t mv_used = 0;  // some target / macro reads the matched-variable state
+  uint8_t body_partial = 0;  // SecRequestBodyLimitAction ProcessPartial
   uint64_t body_limit = 134217728;
   uint64_t source_digest = 0;  // FNV-1a 64 of the SecLang text and the export list (artifact identity)
 };

@@ -21,7 +21,8 @@ struct ReqLayout {
   uint32_t cap_mt; // macro expansion scratch == TX string arena size
   uint64_t vmap_bit;   // first word of the request's value signatures in DBatch.vmap
   uint32_t vmap_bits;  // 2 x cap_f signatures: word 2f = value of field f, 2f + 1 = its key
-  uint32_t _pad;
+  uint32_t hset_mask;  // exact phase-A hit set: capacity - 1 (a power of two minus one)
+  uint64_t hset_word;  // its first word in DBatch.hset: [0] overflow flag, [1, cap] keys
 };
 
 struct DBatch {
@@ -34,11 +35,16 @@ struct DBatch {
   const ReqLayout* layout;
   gi_verdict* verdicts;
   uint32_t* matched;
+  uint32_t* caprec;           // [n_req][crcap] gi_capture records (4 words)
+  uint8_t* capbytes;          // [n_req][cbcap] capture bytes
+  uint32_t crcap, cbcap;
   unsigned long long* tally;  // gi_tally counters
   uint32_t* tally_ext;        // [GI_SCORE_BINS] score histogram, then per distinct rule id match counts
   uint32_t* hits;             // phase-A hit words [ceil(n_hit_slots/32)][n_req]
   uint32_t* vmap;             // phase-A value map: per scanned (field, side) a u32 signature, bit (slot % 32)
                               // of every hit slot the value set (k_eval re-tests a link only on values with its bit)
+  uint32_t* hset;             // exact phase-A hit sets: per request an open-addressing table of
+                              // (slot, value index, maybe) keys (kernels.hip hset_key)
   const uint32_t* body_list;  // requests with a body, longest first (k_body: one wave each)
   uint32_t n_body;
   uint32_t n_mp_body;         // of which multipart (k_mpparse)
@@ -77,6 +83,7 @@ struct DBatch {
   uint64_t det_bytes_cap;
   unsigned long long* det_used;
   unsigned long long* diag;   // optional diagnostic counters (gi_stats.diag)
+  unsigned long long* vcause; // [5] phase-A void events per cause (GI_VOID_*, kernels.hip)
   uint32_t* dbg;              // debug-build bounds-violation record (-DGI_DEBUG)
   unsigned long long* prof;   // GI_PROF=1: k_eval cycle / rule counters (stderr at gi_sync)
   uint64_t items_cap;
@@ -99,7 +106,8 @@ struct ScanLaunch {
 #define GI_STREAM_GRID 8192  // k_stream workgroups (64 lanes) per bucket launch (~8 waves/SIMD)
 #define GI_PCHUNK 2048       // pool words a k_stream wave reserves at a time
 #define GI_LONG_MIN 2048     // items at least this long take k_long (one wave per (item, stream)), not the queue
-#define GI_LONG_GRID 512     // k_long workgroups
+#define GI_LONG_GRID 512     // k_long workgroups (at most)
+#define GI_LONG_BUDGET (4ull << 30)  // bytes of k_long chain buffers (runtime.cpp gi_stage_batch)
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.
 uint32_t scan_resident_blocks(uint32_t lds_bytes);

@@ -8,6 +8,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "pike.h"
+
 #if !defined(__HIPCC__) && !defined(__host__)
 #define __host__
 #define __device__
@@ -57,9 +59,13 @@ enum SingleId : uint8_t {
   S_REMOTE_ADDR,   // ProcessConnection
   S_REMOTE_PORT,
   S_FILES_COMBINED_SIZE,  // multipart: total part bytes
+  S_ARGS_COMBINED_SIZE,   // computed when read: sum of key + value lengths of ARGS_GET and ARGS_POST
+  S_FULL_REQUEST_LENGTH,  // declared, never set by coraza v3.3.3: ""
+  S_URLENCODED_ERROR,     // declared, never set by coraza v3.3.3: ""
+  S_INBOUND_DATA_ERROR,   // "1" when the body reached SecRequestBodyLimit
   S_COUNT
 };
-#define GI_REQHDR_BYTES 320
+#define GI_REQHDR_BYTES 384
 #define GI_RM_BYTES 384  // per request: 8 ctl:ruleRemoveById ranges (128 B) + 8 ctl:ruleRemoveTargetById entries (32 B)  // per-request header slot (ReqHdr, kernels.hip) at the start of its scratch region
 
 // Variable ids used by rule targets.  [0, S_COUNT) are singles.
@@ -238,7 +244,7 @@ struct DRule {
 #define GI_JOB_LDS_BYTES 65536          // small jobs: 2 workgroups of 1024 per CU
 #define GI_BIG_LDS_BYTES (148 * 1024)   // big jobs: 1 workgroup of 1024 per CU (+ 8 KB k_scan block list)
 #define GI_JOB_MAX_DFA 4
-#define GI_JAMAP_BYTES 528              // joint class map: u32[129] (128 = collapsed non-ASCII rune), byte q = class in automaton q
+#define GI_JAMAP_BYTES 1024             // joint class map: u32[256] (>= 0x80: rune-mapped non-ASCII), byte q = class in automaton q
 #define GI_RUNE_MARK 0x80               // a non-ASCII rune in a collapsed value
 #define GI_NO_SINGLE 0xFF
 
@@ -249,10 +255,13 @@ struct DStream {
   uint32_t val_begin, val_count;    // DScanVal: validate operators, evaluated by k_stream
   uint64_t gmask;     // the stream's filters as global filter ids
   uint8_t kind_mask;  // union of the field filters' kinds (1 << FieldKind)
-  uint8_t collapse;   // every automaton maps all non-ASCII runes to one class: values are
-                      // rune-collapsed (each non-ASCII rune -> GI_RUNE_MARK) instead of slow
+  uint8_t collapse;   // values are rune-mapped for the scan instead of slow: each non-ASCII rune
+                      // becomes one byte, GI_RUNE_MARK (rmap_cnt 0: the automata agree on all of
+                      // them) or 0x80 + its joint class (rmap triples (lo, hi, byte) in nranges)
   uint8_t det_id;     // index in DProgram.det_streams if some val is @detectSQLi/@detectXSS, else 0xFF
   uint8_t _pad;
+  uint32_t rmap_off, rmap_cnt;
+  uint32_t _pad2;
 };
 #define GI_MAX_DET_STREAMS 32
 
@@ -421,6 +430,7 @@ struct DOp {
   uint32_t lit_off, lit_len;
   uint32_t ngroups;    // @pm / @pmFromFile over a large phrase set: automata dfa .. dfa + ngroups - 1
                        // (phrase groups, any match), else 0
+  int32_t pike;        // @rx of a link whose `capture` is observable: submatch program (DPike), else -1
   int64_t num;
   uint32_t bits[8];    // @validateByteRange allowed-byte bitmap
 };
@@ -504,6 +514,12 @@ struct DProgram {
   const uint32_t* sfilt;        // per stream filter: global filter id (filters[] is global)
   const uint32_t* always_slots; // hit slots without an automaton image
   const uint32_t* body_links;   // links k_body tests on the speculative REQUEST_BODY
+  const DPike* pikes;           // submatch programs of observable captures (pike.h)
+  const DPikeInst* pike_insts;
+  const uint32_t* pike_ranges;
+  uint32_t cap_ws_words;        // pike_match workspace per request (max over the programs; 0: none)
+  uint32_t cap_groups;          // capture groups written at most (TX.0 .. TX.<cap_groups - 1>)
+  int32_t cap_slots[9];         // TX slot of the keys "0".."8" (capture targets), -1 when none
   uint32_t n_body_links;
   uint32_t n_always;
   uint32_t n_gfilters;
@@ -524,7 +540,7 @@ struct DProgram {
   uint8_t rule_engine;          // EngineMode
   uint8_t body_access;
   uint8_t mv_used;              // some target / macro reads MATCHED_VAR(S)(_NAME(S)): k_eval records matches
-  uint8_t _pad;
+  uint8_t body_partial;         // SecRequestBodyLimitAction ProcessPartial (else Reject)
   uint64_t body_limit;
   uint32_t n_det_streams;       // streams with @detectSQLi/@detectXSS vals (k_detect entries carry a mask)
   uint32_t det_streams[GI_MAX_DET_STREAMS];

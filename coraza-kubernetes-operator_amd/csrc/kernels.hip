@@ -1172,6 +1172,11 @@ __device__ const char* var_name(uint32_t var) {
     case S_MULTIPART_STRICT_ERROR: return "MULTIPART_STRICT_ERROR";
     case S_REMOTE_ADDR: return "REMOTE_ADDR";
     case S_REMOTE_PORT: return "REMOTE_PORT";
+    case S_FILES_COMBINED_SIZE: return "FILES_COMBINED_SIZE";
+    case S_ARGS_COMBINED_SIZE: return "ARGS_COMBINED_SIZE";
+    case S_FULL_REQUEST_LENGTH: return "FULL_REQUEST_LENGTH";
+    case S_URLENCODED_ERROR: return "URLENCODED_ERROR";
+    case S_INBOUND_DATA_ERROR: return "INBOUND_DATA_ERROR";
     case V_ARGS_GET: return "ARGS_GET";
     case V_ARGS_POST: return "ARGS_POST";
     case V_ARGS: return "ARGS";
@@ -1263,6 +1268,8 @@ struct Tx {
   Str* single;               // ReqHdr::single (per-request, in HBM scratch)
   const uint32_t* hits;      // phase-A hit words [slot/32][n_req]
   const uint32_t* vmap;      // the request's phase-A value signatures (word 2f + side: bit slot % 32)
+  const uint32_t* hset;      // the request's exact hit set (nullptr: none, or it overflowed)
+  uint32_t hmask;
   uint32_t nf_pa;            // fields [0, nf_pa) went through phase A (value map valid)
   uint32_t n_req, req;
   bool has_post;             // ARGS_POST fields phase A did not see (phase-A bits of RF_BODYDEP links void)
@@ -1289,6 +1296,9 @@ struct Tx {
   uint32_t* mout;
   uint32_t mcap;
   MvState* mv;               // matched-variable state (nullptr unless DProgram.mv_used)
+  uint32_t* capws;           // pike_match workspace (observable captures; nullptr: none)
+  uint8_t* capbuf;           // per capture group g: cap_t bytes holding TX.g's value
+  uint32_t cur_id;           // id of the top-level rule being evaluated (capture records)
   bool profon;               // GI_PROF counters (diagnostics)
   uint32_t prof_visits, prof_evals, prof_rules;
   uint64_t prof_eval_cyc, prof_act_cyc;
@@ -1912,9 +1922,14 @@ __device__ inline bool mp_after_ok(const uint8_t* s, uint32_t n, uint32_t k) {
 // Returns an MpErr (the body-error class) or MP_OK; GI_REQ_UNSUPPORTED_BODY
 // in t.flags for input outside the engine (quoted-printable parts, RFC 2231
 // parameters).  *combined / *combined_set: FILES_COMBINED_SIZE.
+// cand (optional, k_mpparse): every position k of a '\n' followed by
+// "--" + boundary, ascending -- the delimiter search of a part's data then
+// walks this list instead of every byte of the part.
 template <class C>
 __device__ __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, const uint8_t* ct, uint32_t ctn,
-                                                uint64_t* combined, bool* combined_set) {
+                                                uint64_t* combined, bool* combined_set,
+                                                const uint32_t* cand = nullptr, uint32_t ncand = 0) {
+  uint32_t ci = 0;  // next candidate
   *combined = 0;
   *combined_set = false;
   uint32_t ts, te;
@@ -2057,6 +2072,17 @@ __device__ __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t
     if (n - i >= 2 + bn && s[i] == '-' && s[i + 1] == '-' && bytes_equal(s + i + 2, bd, bn) &&
         mp_after_ok(s, n, i + 2 + bn)) {
       end = i;
+    } else if (cand) {  // the same first match, from the candidate list
+      while (ci < ncand && cand[ci] < i + (lf ? 0u : 1u)) ci++;
+      for (uint32_t c = ci; c < ncand; c++) {
+        const uint32_t k = cand[c];  // '\n'; the delimiter starts at k (LF) or k - 1 (CRLF)
+        if (!lf && s[k - 1] != '\r') continue;
+        if (mp_after_ok(s, n, k + 3 + bn)) {
+          end = lf ? k : k - 1;
+          ci = c;
+          break;
+        }
+      }
     } else {
       const uint32_t pl = (lf ? 1u : 2u) + 2 + bn;
       for (uint32_t k = i; k + pl <= n; k++) {
@@ -2344,6 +2370,21 @@ __device__ int64_t slot_int(const Slot& s, bool* ok) {
   return 0;
 }
 
+// A single's value.  ARGS_COMBINED_SIZE is computed when read [upstream
+// internal/collections/sized.go SizeCollection over ARGS_GET + ARGS_POST:
+// the sum of len(key) + len(value) of every entry]; buf >= 24 bytes.
+__device__ __forceinline__ Str single_val(Tx& t, uint32_t sid, uint8_t* buf) {
+  if (sid == S_ARGS_COMBINED_SIZE) {
+    uint64_t n = 0;
+    for (uint32_t f = 0; f < t.nf; f++) {
+      const Field& fl = t.fields[f];
+      if (fl.kind == FK_ARG_GET || fl.kind == FK_ARG_POST) n += (uint64_t)fl.kn + fl.vn;
+    }
+    return {buf, go_itoa((int64_t)n, buf)};
+  }
+  return t.single[sid];
+}
+
 // Expand a %{..} template.  *persistent: result points into the program's
 // string pool (safe to keep in TX); otherwise into the macro scratch.
 __device__ __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
@@ -2366,7 +2407,7 @@ __device__ __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
     } else if (p.kind == TP_TX) {
       s = slot_str(t, TXS(t, p.slot), nb);
     } else if (p.kind == TP_SINGLE) {
-      s = t.single[p.single];
+      s = single_val(t, p.single, nb);
     } else if (p.kind == TP_MV) {
       s = {mv_curval(t.mv), t.mv->cur_vn};
     } else if (p.kind == TP_MVNAME) {
@@ -2735,6 +2776,113 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
   return o.negate ? !res : res;
 }
 
+// Exact hit set (k_eval's per-value phase-A results): a key per (hit slot,
+// value index) records that this value, transformed by the link's chain,
+// satisfies the link's operator (maybe = 0), or that phase A could not decide
+// it (maybe = 1: chain overflow, list overflow).  A value of a value-exact
+// slot with neither key cannot match the link.  Keys need slot < 65535 and
+// vix < 32768; a request with a key outside that range, or whose table fills,
+// gets the overflow word set and k_eval re-evaluates as without the set.
+__device__ __forceinline__ uint32_t hset_key(uint32_t slot, uint32_t vix, uint32_t maybe) {
+  return ((slot + 1u) << 16) | (vix << 1) | maybe;
+}
+__device__ __forceinline__ uint32_t hset_hash(uint32_t k) {
+  k ^= k >> 15;
+  k *= 0x2C1B3C6Du;
+  k ^= k >> 12;
+  return k;
+}
+__device__ __noinline__ void hset_insert(const DBatch& B, const ReqLayout& L, uint32_t slot, uint32_t vix, uint32_t maybe) {
+  uint32_t* tab = B.hset + L.hset_word;
+  if (slot >= 65534u || vix >= 32768u) {
+    tab[0] = 1u;
+    return;
+  }
+  const uint32_t key = hset_key(slot, vix, maybe);
+  uint32_t h = hset_hash(key) & L.hset_mask;
+  for (uint32_t probe = 0; probe <= L.hset_mask; probe++) {
+    const uint32_t prev = atomicCAS(&tab[1 + h], 0u, key);
+    if (prev == 0u || prev == key) return;
+    h = (h + 1) & L.hset_mask;
+  }
+  tab[0] = 1u;  // full
+}
+// k_eval: 0 = no key, 1 = exact match, 2 = maybe (evaluate the value)
+__device__ __forceinline__ uint32_t hset_lookup(const uint32_t* tab, uint32_t mask, uint32_t slot, uint32_t vix) {
+  uint32_t res = 0;
+  for (uint32_t m = 0; m < 2 && !res; m++) {
+    const uint32_t key = hset_key(slot, vix, m);
+    uint32_t h = hset_hash(key) & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+      const uint32_t x = tab[1 + h];
+      if (x == key) {
+        res = 1 + m;
+        break;
+      }
+      if (x == 0u) break;
+      h = (h + 1) & mask;
+    }
+  }
+  return res;
+}
+
+// ------------------------------------------------------------ captures
+// Header of the per-request capture workspace (k_eval sets it up), then the
+// pike_match workspace.
+#define GI_CAPWS_HDR 16
+struct CapHdr {
+  uint32_t nrec, nbytes;     // records / bytes written for this request
+  uint32_t* rec;             // its row of gi_capture records (4 words each)
+  uint8_t* bytes;            // its row of capture bytes
+  uint32_t rec_cap, bytes_cap;
+  uint32_t trunc;            // records or bytes did not fit
+  uint32_t _pad[7];
+};
+static_assert(sizeof(CapHdr) == 4 * GI_CAPWS_HDR, "CapHdr layout");
+
+// [upstream rx.go Evaluate, capturing]: FindStringSubmatch(value); groups
+// 0..8 -> TX.0..TX.8 (transaction.go CaptureField: TX SetIndex(strconv.Itoa(i)),
+// unset groups ""), each value copied into its group's buffer; one capture
+// record per group.  Returns GI_REQ_OVERFLOW when the value does not fit.
+__device__ __noinline__ uint32_t run_capture(const DProgram& P, uint32_t* capws, uint8_t* capbuf, uint32_t cap_t,
+                                             Slot* slots, uint32_t n_req, uint32_t rule_id, int32_t pike,
+                                             const uint8_t* v, uint32_t n) {
+  const DPike pk = P.pikes[pike];
+  int32_t caps[GI_PIKE_MAX_SLOTS];
+  CapHdr* H = (CapHdr*)capws;
+  if (!pike_match(P.pike_insts + pk.inst_off, P.pike_ranges, pk, v, n, capws + GI_CAPWS_HDR, caps)) return 0;
+  if (n > cap_t) return GI_REQ_OVERFLOW;
+  const uint32_t stride = (cap_t + 15) & ~15u;
+  for (uint32_t g = 0; 2 * g < pk.nslot && g < 9; g++) {
+    const int32_t a = caps[2 * g], b = caps[2 * g + 1];
+    const uint32_t len = (a >= 0 && b >= a) ? (uint32_t)(b - a) : 0u;
+    uint8_t* dst = capbuf + (uint64_t)g * stride;
+    for (uint32_t i = 0; i < len; i++) dst[i] = v[a + i];
+    const int32_t sl = P.cap_slots[g];
+    if (sl >= 0) {
+      Slot& x = slots[(uint64_t)sl * n_req];
+      x.state = 2;
+      x.p = dst;
+      x.n = len;
+    }
+    if (H->rec) {  // capture record {rule id, group, byte offset in the request's row, length}
+      if (H->nrec < H->rec_cap && H->nbytes + len <= H->bytes_cap) {
+        uint32_t* r = H->rec + 4ull * H->nrec;
+        r[0] = rule_id;
+        r[1] = g;
+        r[2] = H->nbytes;
+        r[3] = len;
+        for (uint32_t i = 0; i < len; i++) H->bytes[H->nbytes + i] = dst[i];
+        H->nbytes += len;
+        H->nrec++;
+      } else {
+        H->trunc = 1;
+      }
+    }
+  }
+  return 0;
+}
+
 // ------------------------------------------------------------ evaluation
 // Apply the rule's transformation chain; returns the value to test.
 __device__ __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uint32_t vn, bool* ok,
@@ -2814,18 +2962,23 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
 // no candidate); every match counts and runs the actions.  One eval_op /
 // run_actions site serves both forms (the Tx stays in registers).
 // var / k / kn name the value for the matched-variable state (MATCHED_VAR_NAME = VAR[:key]).
+// exact (non-multiMatch links): phase A proved the transformed value matches
+// (k_eval's hit set): the operator does not run again, and the chain runs
+// only when the matched-variable state needs the transformed value.
 __device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn,
-                                               uint32_t var, const uint8_t* key, uint32_t kn) {
+                                               uint32_t var, const uint8_t* key, uint32_t kn, bool exact = false) {
   uint32_t nm = 0;
   const uint8_t* cp = v;  // current candidate
   uint32_t cn = vn;
   uint32_t k = 0;         // transformations applied so far
   if (!(R.flags & RF_MULTIMATCH)) {
-    bool ok;
-    const Str tv = transform(t, R, v, vn, &ok);
-    if (!ok) return 0;
-    cp = tv.p;
-    cn = tv.n;
+    if (!exact || t.mv || (R.flags & RF_CAPTURE)) {
+      bool ok;
+      const Str tv = transform(t, R, v, vn, &ok);
+      if (!ok) return 0;
+      cp = tv.p;
+      cn = tv.n;
+    }
     k = R.tchain_len;
   }
   // `fresh` = cp is a candidate not yet tested.  The loop body has no
@@ -2834,7 +2987,12 @@ __device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp&
   // lost while other lanes of the wave took the identity path).
   for (bool fresh = true;; k++) {
     if (fresh) {
-      if (eval_op(t, o, cp, cn)) {
+      const bool hit = exact || eval_op(t, o, cp, cn);
+      // capturing @rx: a value the regex matches writes TX.0-TX.8 -- for a
+      // negated operator exactly the values that do not make the link match
+      if ((R.flags & RF_CAPTURE) && hit != (o.negate != 0))
+        t.flags |= run_capture(*t.P, t.capws, t.capbuf, t.cap_t, t.slots, t.n_req, t.cur_id, o.pike, cp, cn);
+      if (hit) {
         if (t.mv && !mv_record(t.mv, var, key, kn, cp, cn)) t.flags |= GI_REQ_OVERFLOW;
         run_actions(t, R);
         nm++;
@@ -2901,7 +3059,8 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
           continue;
         }
         bool ok;
-        const Str sv = t.single[vr.var];
+        uint8_t sb[24];
+        const Str sv = single_val(t, vr.var, sb);
         const Str tv = transform(t, R, sv.p, sv.n, &ok);
         any = ok && eval_op(t, o, tv.p, tv.n);
       }
@@ -2922,7 +3081,8 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         uint8_t one = '1';
         nmatch += test_value(t, R, o, &one, 1, vr.var, nullptr, 0);
       } else {
-        Str s = t.single[vr.var];
+        uint8_t sb[24];
+        const Str s = single_val(t, vr.var, sb);
         nmatch += test_value(t, R, o, s.p, s.n, vr.var, nullptr, 0);
       }
       continue;
@@ -3007,17 +3167,27 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
     }
     // phase A tested every value of fields [0, nf_pa) this link reads: one
     // whose value-map bit is clear set no hit bit at all, so it cannot match
-    // here (value-exact slots only: an always-slot is set without a value)
+    // here (value-exact slots only: an always-slot is set without a value).
+    // With the exact hit set, a value with a set bit is decided by its key:
+    // an exact key is a match (the operator is not run again), a maybe key
+    // is evaluated, no key is no match.  multiMatch links count candidates
+    // per value, so they always evaluate.
     const bool vskip = R.hit_slot >= 0 && !vr.count && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
                        slot_vexact(P, (uint32_t)R.hit_slot);
+    const bool vexact = vskip && t.hset && !(R.flags & RF_MULTIMATCH);
     uint32_t cnt = 0;
     for (uint32_t f = 0; f < t.nf; f++) {
       const Field fl = t.fields[f];
       bool names;
       if (!field_in(vr.var, fl.kind, &names)) continue;
+      uint32_t hres = 2;  // 2: evaluate the value
       if (vskip && f < t.nf_pa && fl.kind <= FK_COOKIE) {  // phase-A item kinds only
         const uint32_t vb = 2 * f + (names ? 1u : 0u);
         if (!((t.vmap[vb] >> ((uint32_t)R.hit_slot & 31u)) & 1u)) continue;
+        if (vexact) {
+          hres = hset_lookup(t.hset, t.hmask, (uint32_t)R.hit_slot, vb);
+          if (!hres) continue;
+        }
       }
       if (vr.key_mode == 1) {
         if (vr.ci ? !eq_ascii_ci(fl.k, fl.kn, P.strpool + vr.key_off, vr.key_len)
@@ -3033,9 +3203,9 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         continue;
       }
       if (names)
-        nmatch += test_value(t, R, o, fl.k, fl.kn, vr.var, fl.k, fl.kn);
+        nmatch += test_value(t, R, o, fl.k, fl.kn, vr.var, fl.k, fl.kn, hres == 1);
       else
-        nmatch += test_value(t, R, o, fl.v, fl.vn, vr.var, fl.k, fl.kn);
+        nmatch += test_value(t, R, o, fl.v, fl.vn, vr.var, fl.k, fl.kn, hres == 1);
     }
     if (vr.count) {
       uint8_t buf[24];
@@ -3051,6 +3221,7 @@ __device__ __forceinline__ void eval_top(Tx& t, uint32_t ri) {
   const DRule R = gi_cload(P.rules, ri);
   // the rule and its chain links; all must match (one eval_rule call site)
   t.prof_evals++;
+  t.cur_id = (uint32_t)R.id;
   for (int32_t ci = (int32_t)ri; ci >= 0;) {
     const DRule C = gi_cload(P.rules, (uint64_t)ci);
     const uint64_t c0 = t.profon ? clock64() : 0;
@@ -3141,6 +3312,8 @@ struct Region {
   Slot* slots;
   uint8_t *bytes, *t0, *t1, *mt, *txa;
   int64_t (*rm)[2];
+  uint32_t* capws;
+  uint8_t* capbuf;
   MvState* mv;
   uint32_t cap_f, cap_b, cap_t, cap_mt;
 };
@@ -3167,6 +3340,11 @@ __device__ inline Region region_of(const DProgram& P, const DBatch& B, uint32_t 
   off += (L.cap_mt + 15) & ~15u;
   g.txa = base + off;
   off += (L.cap_mt + 15) & ~15u;
+  // observable captures: the submatch workspace and one value buffer per group
+  g.capws = P.cap_ws_words ? (uint32_t*)(base + off) : nullptr;
+  off += ((uint64_t)P.cap_ws_words * 4 + 15) & ~15ull;
+  g.capbuf = P.cap_ws_words ? base + off : nullptr;
+  off += P.cap_ws_words ? (uint64_t)P.cap_groups * ((L.cap_t + 15) & ~15u) : 0ull;
   g.mv = P.mv_used ? (MvState*)(base + off) : nullptr;
   g.cap_f = L.cap_f;
   g.cap_b = L.cap_b;
@@ -3193,6 +3371,8 @@ __device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
   t.cap_tx = g.cap_mt;
   t.single = g.hdr->single;
   t.mv = g.mv;
+  t.capws = g.capws;
+  t.capbuf = g.capbuf;
 }
 
 __device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
@@ -3251,9 +3431,16 @@ __device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
   atomicOr(&B.hits[(uint64_t)(slot >> 5) * B.n_req + r], 1u << (slot & 31));
 }
 
-__device__ __forceinline__ void void_request(const DBatch& B, uint32_t r) {
+// cause (GI_VOID_*): which capacity ran out (counted in B.vcause for GI_DIAG)
+#define GI_VOID_FIELD 0
+#define GI_VOID_LONG 1
+#define GI_VOID_SLOW 2
+#define GI_VOID_QCAP 3
+#define GI_VOID_POOL 4
+__device__ __forceinline__ void void_request(const DBatch& B, uint32_t r, uint32_t cause) {
   ReqHdr* H = (ReqHdr*)(B.scratch + B.layout[r].base);
   H->pa_void = 1;
+  atomicAdd(&B.vcause[cause], 1ull);
 }
 
 #define GI_NB 5  // item length buckets: <=16, <=32, <=64, <=128, >128 bytes
@@ -3570,53 +3757,101 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
   }
 }
 
-// Speculative multipart ProcessRequestBody: one thread per body-list entry
-// (its own kernel: the sequential parser's registers stay out of k_bparse).
+// Speculative multipart ProcessRequestBody: one wave per body.  The wave
+// first lists every '\n' + "--" + boundary position of the body (lanes scan
+// 1/64 each, a prefix sum orders the lists) into the request's t0 buffer;
+// lane 0 then runs the sequential parser (Go mime/multipart restated), whose
+// part-data delimiter search walks that list instead of the part's bytes.
 // On failure the request keeps no fields (k_eval parses it again).
+#define GI_MP_MAX_BOUNDARY 256
 __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
-  const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
-  if (bi >= B.n_body) return;
-  const uint32_t r = B.body_list[bi];
-  GI_BOUND(r < B.n_req, r, bi);
-  Region g = region_of(P, B, r);
-  ReqHdr* H = g.hdr;
-  if (H->spec_proc != BP_MULTIPART || (H->flags & GI_REQ_ERROR_MASK)) return;
-  const gi_span bs = B.reqs[r].body;
-  const uint32_t nf0 = H->nf, nb0 = H->nb;
-  JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
-  const Str ct = first_content_type(B, B.reqs[r]);
-  uint64_t comb;
-  bool comb_set;
-  const uint8_t err = parse_multipart(jc, B.data + bs.off, bs.len, ct.p, ct.n, &comb, &comb_set);
-  if (jc.flags) {  // an engine limit / unsupported input: k_eval decides
-    H->spec_proc = BP_NONE;
-    return;
-  }
-  if (comb_set) {
-    uint8_t* cb = tx_alloc(jc, 24);
-    if (!cb) {
-      H->spec_proc = BP_NONE;
-      return;
+  __shared__ uint8_t sbd[GI_MP_MAX_BOUNDARY];
+  __shared__ uint32_t sbn;
+  const uint32_t L = threadIdx.x;
+  for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
+    const uint32_t r = B.body_list[bi];
+    GI_BOUND(r < B.n_req, r, bi);
+    Region g = region_of(P, B, r);
+    ReqHdr* H = g.hdr;
+    if (H->spec_proc != BP_MULTIPART || (H->flags & GI_REQ_ERROR_MASK)) continue;  // wave-uniform
+    const gi_span bs = B.reqs[r].body;
+    const uint8_t* s = B.data + bs.off;
+    const uint32_t n = bs.len;
+    const uint32_t nf0 = H->nf, nb0 = H->nb;
+    const Str ct = first_content_type(B, B.reqs[r]);
+    if (L == 0) {  // the boundary (a throw-away arena copy: parse_multipart parses the media type again)
+      JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
+      uint32_t ts, te;
+      Str bstr;
+      sbn = 0;
+      if (mp_media(jc, ct.p, ct.n, &ts, &te, "boundary", &bstr, nullptr, nullptr) == 0 && bstr.n > 0 &&
+          bstr.n <= GI_MP_MAX_BOUNDARY) {
+        for (uint32_t k = 0; k < bstr.n; k++) sbd[k] = bstr.p[k];
+        sbn = bstr.n;
+      }
     }
-    const uint32_t cn2 = go_itoa((int64_t)comb, cb);
-    jc.nb -= 24 - cn2;
-    H->single[S_FILES_COMBINED_SIZE] = {cb, cn2};
-  }
-  H->spec_err = err;
-  H->n_post = jc.nf - nf0;
-  H->nb = jc.nb;
-  // phase-A item counts of its ARGS_POST fields
-  const uint32_t sides = P.n_streams ? P.item_sides[FK_ARG_POST] : 0u;
-  if (sides) {
-    uint32_t cnt[GI_NB] = {0, 0, 0, 0, 0};
-    for (uint32_t i = nf0; i < jc.nf; i++) {
-      const Field fl = g.fields[i];
-      if (fl.kind != FK_ARG_POST) continue;
-      if (sides & 1) cnt[item_bucket(fl.vn)]++;
-      if (sides & 2) cnt[item_bucket(fl.kn)]++;
+    __syncthreads();
+    const uint32_t bn = sbn;
+    uint32_t* cand = (uint32_t*)g.t0;
+    uint32_t ncand = 0;
+    bool use = false;
+    if (bn) {
+      const uint32_t a0 = (uint32_t)((uint64_t)n * L / 64), a1 = (uint32_t)((uint64_t)n * (L + 1) / 64);
+      auto hit = [&](uint32_t k) {
+        if (s[k] != '\n' || k + 3 + bn > n || s[k + 1] != '-' || s[k + 2] != '-') return false;
+        for (uint32_t q = 0; q < bn; q++)
+          if (s[k + 3 + q] != sbd[q]) return false;
+        return true;
+      };
+      uint32_t c = 0;
+      for (uint32_t k = a0; k < a1; k++) c += hit(k) ? 1u : 0u;
+      uint32_t tot;
+      uint32_t at = wave_excl_sum(c, &tot);
+      use = 4ull * tot <= g.cap_t;
+      if (use)
+        for (uint32_t k = a0; k < a1; k++)
+          if (hit(k)) cand[at++] = k;
+      ncand = tot;
     }
-    for (uint32_t b = 0; b < GI_NB; b++)
-      if (cnt[b]) atomicAdd(&B.bcounts[(r / 256) * GI_NB + b], cnt[b]);
+    __syncthreads();
+    if (L == 0) {
+      JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
+      uint64_t comb;
+      bool comb_set;
+      const uint8_t err = parse_multipart(jc, s, n, ct.p, ct.n, &comb, &comb_set, use ? cand : nullptr, use ? ncand : 0u);
+      bool ok = !jc.flags;
+      if (ok && comb_set) {
+        uint8_t* cb = tx_alloc(jc, 24);
+        if (!cb) {
+          ok = false;
+        } else {
+          const uint32_t cn2 = go_itoa((int64_t)comb, cb);
+          jc.nb -= 24 - cn2;
+          H->single[S_FILES_COMBINED_SIZE] = {cb, cn2};
+        }
+      }
+      if (!ok) {  // an engine limit / unsupported input: k_eval decides
+        H->spec_proc = BP_NONE;
+      } else {
+        H->spec_err = err;
+        H->n_post = jc.nf - nf0;
+        H->nb = jc.nb;
+        // phase-A item counts of its ARGS_POST fields
+        const uint32_t sides = P.n_streams ? P.item_sides[FK_ARG_POST] : 0u;
+        if (sides) {
+          uint32_t cnt[GI_NB] = {0, 0, 0, 0, 0};
+          for (uint32_t f = nf0; f < jc.nf; f++) {
+            const Field fl = g.fields[f];
+            if (fl.kind != FK_ARG_POST) continue;
+            if (sides & 1) cnt[item_bucket(fl.vn)]++;
+            if (sides & 2) cnt[item_bucket(fl.kn)]++;
+          }
+          for (uint32_t b = 0; b < GI_NB; b++)
+            if (cnt[b]) atomicAdd(&B.bcounts[(r / 256) * GI_NB + b], cnt[b]);
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -3693,12 +3928,13 @@ __device__ __forceinline__ uint32_t meta_vix(uint32_t meta) {
 // A scanned value set hit bit `slot` of request r: the bit, and the value's
 // bit in the request's value map (k_eval tests only mapped values of the
 // links whose slot is value-exact, see eval_rule).
-__device__ __forceinline__ void hit_value(const DBatch& B, uint32_t slot, uint32_t r, uint32_t vix) {
+__device__ __forceinline__ void hit_value(const DBatch& B, uint32_t slot, uint32_t r, uint32_t vix, uint32_t maybe = 0) {
   set_hit(B, slot, r);
   if (vix != GI_NO_VIX) {
     const ReqLayout L = B.layout[r];
     GI_BOUND(vix < L.vmap_bits, vix, L.vmap_bits);
     atomicOr(&B.vmap[L.vmap_bit + vix], 1u << (slot & 31));  // the value's slot signature
+    if (L.hset_mask) hset_insert(B, L, slot, vix, maybe);
   }
 }
 // the same for the item at global index idx (k_scan's queue lanes carry it)
@@ -3784,7 +4020,7 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
         it.vn = n;
         it.req = r;
         it.meta = kind ? (uint32_t)kind | (side << 3) | (min(fi, GI_MAX_ITEM_FIELD) << 4) : (uint32_t)sg << 8;
-        if (kind && fi > GI_MAX_ITEM_FIELD) void_request(B, r);  // no value-map index: no phase-A bit trusted
+        if (kind && fi > GI_MAX_ITEM_FIELD) void_request(B, r, GI_VOID_FIELD);  // no value-map index: no phase-A bit trusted
         ((Item*)B.items)[at] = it;
         atomicAdd(&ibytes[b], (unsigned long long)n);
       });
@@ -3846,7 +4082,7 @@ __device__ void det_maybe(const DProgram& P, const DBatch& B, uint32_t r, uint32
     const uint64_t fm = gm & S.gmask;
     for (uint32_t q = 0; q < S.val_count; q++) {
       const DScanVal& sv = P.svals[S.val_begin + q];
-      if ((sv.kind == OP_DETECT_SQLI || sv.kind == OP_DETECT_XSS) && (fm & sv.fmask)) hit_value(B, sv.slot, r, vix);
+      if ((sv.kind == OP_DETECT_SQLI || sv.kind == OP_DETECT_XSS) && (fm & sv.fmask)) hit_value(B, sv.slot, r, vix, 1u);
     }
   }
 }
@@ -3883,7 +4119,7 @@ __device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, uint
     if (!(fm & sv.fmask)) continue;
     if (sv.kind == OP_DETECT_SQLI || sv.kind == OP_DETECT_XSS) {
       if (maybe) {
-        hit_value(B, sv.slot, r, vix);
+        hit_value(B, sv.slot, r, vix, 1u);
         continue;
       }
       // the output's byte summary carries the exact prefilters (li_sqli_byte / li_xss_byte)
@@ -3896,7 +4132,8 @@ __device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, uint
       else *det_append = true;
       continue;
     }
-    if (maybe || (validate_op(sv.kind, sv.bits, v, n) != (sv.negate != 0))) hit_value(B, sv.slot, r, vix);
+    if (maybe) hit_value(B, sv.slot, r, vix, 1u);
+    else if (validate_op(sv.kind, sv.bits, v, n) != (sv.negate != 0)) hit_value(B, sv.slot, r, vix);
   }
 }
 
@@ -3936,16 +4173,28 @@ struct SlowEnt {
 // class: each rune >= 0x80 (a valid UTF-8 sequence, or one invalid byte that
 // utf8.DecodeRune reads as U+FFFD) becomes one GI_RUNE_MARK byte, so the
 // lockstep scan steps exactly once per rune, as the rune-decoding scan does.
-__device__ uint32_t collapse_runes(const uint8_t* s, uint32_t n, uint8_t* d) {
+// With a rune map (DStream.rmap_cnt > 0: the automata tell some non-ASCII
+// runes apart) each rune becomes 0x80 + its joint class instead.
+__device__ uint32_t collapse_runes(const uint8_t* s, uint32_t n, uint8_t* d, const uint32_t* rmap, uint32_t rcnt) {
   uint32_t o = 0;
   for (uint32_t i = 0; i < n;) {
     if (s[i] < 0x80) {
       d[o++] = s[i++];
     } else {
       uint32_t w;
-      (void)decode_rune(s, n, i, &w);
+      const uint32_t r = decode_rune(s, n, i, &w);
       i += w;
-      d[o++] = GI_RUNE_MARK;
+      uint8_t b = GI_RUNE_MARK;
+      if (rcnt) {
+        uint32_t lo = 0, hi = rcnt;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (rmap[mid * 3 + 1] < r) lo = mid + 1;
+          else hi = mid;
+        }
+        if (lo < rcnt && rmap[lo * 3] <= r) b = (uint8_t)rmap[lo * 3 + 2];
+      }
+      d[o++] = b;
     }
   }
   return o;
@@ -4026,7 +4275,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
       if (is_long && fm0) {
         const uint32_t k = atomicAdd(B.long_count, 1u);
         if (k < B.long_cap) B.long_list[k] = make_uint2(base + ii, s);
-        else void_request(B, it.req);  // list full: the request's phase-A bits are void (exact)
+        else void_request(B, it.req, GI_VOID_LONG);  // list full: the request's phase-A bits are void (exact)
       }
       const uint64_t fm = is_long ? 0ull : fm0;
       if (!__ballot(fm != 0)) {
@@ -4069,7 +4318,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
         if (osum & BS_HIGH) {
           if (S.collapse) {
             uint8_t* dst = glob ? (cur == g0 ? g1 : g0) : (cur == b0 ? b1 : b0);
-            cn = collapse_runes(cur, (uint32_t)cn, dst);
+            cn = collapse_runes(cur, (uint32_t)cn, dst, P.nranges + S.rmap_off, S.rmap_cnt);
             cur = dst;
           } else {
             slow = true;
@@ -4080,7 +4329,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
         const uint32_t k = atomicAdd(B.slow_count, 1u);
         const unsigned long long off = atomicAdd(B.slow_used, (unsigned long long)((cn + 15) & ~15ll));
         if (k >= B.slow_cap || off + (uint64_t)cn > B.slow_bytes_cap) {
-          void_request(B, it.req);
+          void_request(B, it.req, GI_VOID_SLOW);
         } else {
           for (uint32_t i = 0; i < (uint32_t)cn; i++) B.slow_bytes[off + i] = cur[i];
           SlowEnt e;
@@ -4127,7 +4376,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
       }
       woff = __shfl(woff, 0, 64);
       if (blk >= B.qcap || woff + words > B.pool_cap) {  // out of queue space: exact fallback
-        if (out) void_request(B, it.req);
+        if (out) void_request(B, it.req, blk >= B.qcap ? GI_VOID_QCAP : GI_VOID_POOL);
         if (lane == 0 && blk < B.qcap) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2(0u, 0u);
         continue;
       }
@@ -4239,7 +4488,7 @@ __device__ void scan_value_global(const DProgram& P, const DBatch& B, uint32_t r
     while (x) {
       const int k = __ffsll((unsigned long long)x) - 1;
       x &= x - 1;
-      hit_value(B, P.pats[jd.pat_begin + k].slot, r, vix);
+      hit_value(B, P.pats[jd.pat_begin + k].slot, r, vix, maybe ? 1u : 0u);
     }
   }
 }
@@ -4829,7 +5078,7 @@ __global__ void __launch_bounds__(64) k_long(DProgram P, DBatch B) {
         }
         hit = res != (sv.negate != 0);
       }
-      if (hit && L == 0) hit_value(B, sv.slot, r, vix);
+      if (hit && L == 0) hit_value(B, sv.slot, r, vix, ok ? 0u : 1u);
     }
     // automaton patterns: the stream's (job, automaton) pairs spread over the
     // lanes, each scanned sequentially over the whole value on the global
@@ -4848,7 +5097,7 @@ __global__ void __launch_bounds__(64) k_long(DProgram P, DBatch B) {
         while (x) {
           const int k = __ffsll((unsigned long long)x) - 1;
           x &= x - 1;
-          hit_value(B, P.pats[jd.pat_begin + k].slot, r, vix);
+          hit_value(B, P.pats[jd.pat_begin + k].slot, r, vix, ok ? 0u : 1u);
         }
       }
     }
@@ -4956,6 +5205,12 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
     tx_bind(t, P, g);
     t.hits = B.hits;
     t.vmap = B.vmap + B.layout[r].vmap_bit;
+    {
+      const ReqLayout Lr = B.layout[r];
+      const uint32_t* tab = B.hset + Lr.hset_word;
+      t.hset = (Lr.hset_mask && tab[0] == 0u) ? tab : nullptr;
+      t.hmask = Lr.hset_mask;
+    }
     t.nf_pa = H->nf;
     t.n_req = B.n_req;
     t.req = r;
@@ -4985,6 +5240,16 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
     t.int_phase = 0;
     t.nmatched = 0;
     t.mout = B.matched + (uint64_t)r * B.mcap;
+    t.cur_id = 0;
+    if (t.capws) {
+      CapHdr* CH = (CapHdr*)t.capws;
+      CH->nrec = CH->nbytes = 0;
+      CH->rec = B.caprec ? B.caprec + 4ull * B.crcap * r : nullptr;
+      CH->bytes = B.capbytes ? B.capbytes + (uint64_t)B.cbcap * r : nullptr;
+      CH->rec_cap = B.crcap;
+      CH->bytes_cap = B.cbcap;
+      CH->trunc = 0;
+    }
     t.mcap = B.mcap;
     for (uint32_t s = 0; s < P.n_slots; s++) TXS(t, s).state = 0;
     if (t.mv) {
@@ -5006,11 +5271,38 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
     for (uint8_t ph = 1; ph <= 2 && !(t.flags & GI_REQ_ERROR_MASK); ph++) {
       if (ph == 2) {
         if (t.interrupted || t.engine == ENGINE_OFF) break;
-        const uint32_t bn = rq.body.len;
+        uint32_t bn = rq.body.len;
+        bool run2 = true;
         if (t.body_access && bn > 0) {
+          // [upstream transaction.go WriteRequestBody]: over SecRequestBodyLimit
+          // -> INBOUND_DATA_ERROR; Reject: interruption 413 (no rule id) and no
+          // ProcessRequestBody; ProcessPartial: the first limit bytes.
+          // ProcessRequestBody: a buffer of exactly the limit sets it too and,
+          // with Reject, returns before phase 2.  (DetectionOnly + Reject:
+          // nothing buffered.)
           if (bn > P.body_limit) {
-            t.flags |= GI_REQ_BODY_LIMIT;
-          } else {
+            t.single[S_INBOUND_DATA_ERROR] = {CS_ONE, 1};
+            if (!P.body_partial) {
+              if (t.engine == ENGINE_ON) {
+                t.interrupted = true;
+                t.int_rule = 0;
+                t.int_status = 413;
+                t.int_action = GI_ACTION_DENY;
+                t.int_phase = 2;
+                break;
+              }
+              bn = 0;
+            } else {
+              bn = (uint32_t)P.body_limit;
+            }
+          }
+          if (bn > 0 && bn >= P.body_limit) {
+            t.single[S_INBOUND_DATA_ERROR] = {CS_ONE, 1};
+            if (!P.body_partial) run2 = false;
+          }
+        }
+        if (t.body_access && bn > 0 && run2) {
+          {
             uint8_t* lb = tx_alloc(t, 24);
             if (lb) t.single[S_REQUEST_BODY_LENGTH] = {lb, go_itoa((int64_t)bn, lb)};
             if (t.force_body && t.body_proc == BP_NONE) {
@@ -5092,7 +5384,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
             }
           }
         }
-        if (t.flags & GI_REQ_ERROR_MASK) break;
+        if ((t.flags & GI_REQ_ERROR_MASK) || !run2) break;
       }
       const uint64_t c0 = B.prof ? clock64() : 0;
       eval_phase(t, ph);
@@ -5112,6 +5404,13 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
     v.status = t.interrupted ? t.int_status : 0;
     v.action = t.interrupted ? t.int_action : 0;
     v.phase = t.interrupted ? t.int_phase : 0;
+    v.capture_cnt = 0;
+    v._pad = 0;
+    if (t.capws) {
+      const CapHdr* CH = (const CapHdr*)t.capws;
+      v.capture_cnt = CH->nrec;
+      if (CH->trunc) t.flags |= GI_REQ_CAPTURE_TRUNC;
+    }
     v.flags = t.flags;
     v.match_cnt = t.nmatched;
     for (uint32_t e = 0; e < GI_MAX_EXPORTS; e++) {
@@ -5254,7 +5553,7 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
   GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
   if (B.n_body && P.body_access) {
     GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
-    if (B.n_mp_body) GI_LAUNCH("k_mpparse", k_mpparse, dim3((B.n_body + 63) / 64), dim3(64), 0, stream, P, B);
+    if (B.n_mp_body) GI_LAUNCH("k_mpparse", k_mpparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (P.n_streams) {

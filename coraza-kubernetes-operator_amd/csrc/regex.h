@@ -115,6 +115,13 @@ struct NfaTables {
 bool build_nfa_tables(const Regex& re, NfaTables* out, std::string* err, uint32_t max_pos = 4096);
 bool nfa_host_match(const NfaTables& t, const uint8_t* s, size_t n);
 
+// Pike VM program for submatch extraction (pike.h / pike.cpp), appended to
+// insts / pool; false if it would exceed max_inst instructions.
+struct DPikeInst;
+struct DPike;
+bool build_pike(const Regex& re, std::vector<DPikeInst>* insts, std::vector<uint32_t>* pool, DPike* out,
+                std::string* err, uint32_t max_inst = 4096);
+
 // Superset relaxation (level 1..3) for phase-A prefilter automata; see dfa.cpp.
 void relax_regex(Regex* re, int level);
 

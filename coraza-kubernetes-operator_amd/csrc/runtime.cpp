@@ -80,12 +80,16 @@ struct gi_ctx {
   DProgram prog{};
   std::vector<DevBuf> pbufs;
   // batch buffers
-  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, tally_ext, hits, vmap, blist, joblist, txslots;
+  DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, tally_ext, hits, vmap, hset, blist, joblist, txslots;
   DevBuf tally_idbuf;                  // distinct rule ids, ascending (k_tally bins)
+  DevBuf caprec, capbytes;             // capture records / bytes (observable captures)
+  uint32_t crcap = 8, cbcap = 512;     // per request (gi_ctx_set_capture_cap)
+  uint32_t staged_crcap = 8, staged_cbcap = 512;
+  bool cap_on = false;
   std::vector<uint32_t> tally_ids;
   // phase A
   DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf;
-  uint32_t long_cap = 0;
+  uint32_t long_cap = 0, long_grid = GI_LONG_GRID;
   uint64_t long_bufcap = 0;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0, det_cap = 0;
   uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0, det_bytes_cap = 0;
@@ -95,6 +99,7 @@ struct gi_ctx {
   ScanLaunch scan{};
   uint32_t hit_words = 0;
   uint64_t vmap_words = 0;  // value map (DBatch.vmap)
+  uint64_t hset_words = 0;  // exact hit sets (DBatch.hset)
   uint32_t n_body = 0;      // requests with a body (DBatch.body_list)
   uint32_t n_mp_body = 0;   // of which multipart
   hipEvent_t evs[3] = {nullptr, nullptr, nullptr};
@@ -271,7 +276,7 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   hipError_t e = hipSuccess;
   const Program& P = rs->prog;
   if (P.streams.size() > GI_MAX_STREAMS) return fail(c, GI_EINVAL, "ruleset has more phase-A streams than supported");
-  std::vector<DevBuf> nbufs(40);
+  std::vector<DevBuf> nbufs(48);
   DevBuf njoblist;
   DProgram np{};
   ScanLaunch nscan{};
@@ -334,10 +339,26 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   UP(tchains32, tch32, uint32_t)
   UP(always_slots, P.always_slots, uint32_t)
   UP(body_links, P.body_links, uint32_t)
+  UP(pikes, P.pikes, DPike)
+  UP(pike_insts, P.pike_insts, DPikeInst)
+  UP(pike_ranges, P.pike_ranges, uint32_t)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return discard(e == hipErrorOutOfMemory ? GI_ENOMEM : GI_ENODEV, "ruleset upload failed");
   np.n_lower_pairs = GI_N_LOWER_PAIRS;
+  // observable captures: per-request submatch workspace (kernels.hip CapHdr +
+  // pike_match) and the TX slots of the keys "0".."8"
+  np.cap_ws_words = 0;
+  np.cap_groups = 0;
+  for (const DPike& k : P.pikes) {
+    np.cap_ws_words = (uint32_t)std::max<uint64_t>(np.cap_ws_words, 16 + pike_ws_words(k.n_inst, k.nslot));
+    np.cap_groups = std::max<uint32_t>(np.cap_groups, k.nslot / 2);
+  }
+  for (int g = 0; g < 9; g++) {
+    np.cap_slots[g] = -1;
+    for (uint32_t sl = 0; sl < P.n_slots && !P.pikes.empty(); sl++)
+      if (P.slot_names[2 * sl + 1] == 1 && P.strpool[P.slot_names[2 * sl]] == (uint8_t)('0' + g)) np.cap_slots[g] = (int32_t)sl;
+  }
   np.n_top = (uint32_t)P.top.size();
   np.top_begin[0] = 0;
   np.top_end[0] = n_ph1;
@@ -350,6 +371,7 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   np.rule_engine = P.rule_engine;
   np.body_access = P.body_access;
   np.mv_used = P.mv_used;
+  np.body_partial = P.body_partial;
   np.body_limit = P.body_limit;
   np.n_det_streams = 0;
   for (uint32_t k = 0; k < (uint32_t)P.streams.size(); k++)
@@ -455,6 +477,13 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   return GI_OK;
 }
 
+int gi_ctx_set_capture_cap(gi_ctx* c, uint32_t records, uint32_t bytes) {
+  if (!c || records == 0 || records > (1u << 16) || bytes > (1u << 30)) return GI_EINVAL;
+  c->crcap = records;
+  c->cbcap = bytes;
+  return GI_OK;
+}
+
 int gi_ctx_swap_ruleset(gi_ctx* c, const gi_ruleset* rs) {
   if (!c || !rs) return GI_EINVAL;
   (void)hipSetDevice(c->device);
@@ -470,8 +499,8 @@ void gi_ctx_free(gi_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& b : c->pbufs) b.release();
   c->prof.release();
-  for (DevBuf* b : {&c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
-                    &c->hits, &c->vmap, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
+  for (DevBuf* b : {&c->caprec, &c->capbytes, &c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
+                    &c->hits, &c->vmap, &c->hset, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf})
     b->release();
   for (auto& ev : c->evs)
@@ -497,6 +526,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   // validate spans and lay out per-request scratch (lengths only)
   std::vector<ReqLayout> lay(n);
   uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0, vmap_bits = 0, max_req_bytes = 0;
+  uint64_t hset_words = 0;
   uint32_t n_mp_body = 0;
   uint32_t max_cap_t = 64;
   const uint32_t nslots = c->rs->prog.n_slots;
@@ -584,7 +614,19 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     L.vmap_bit = vmap_bits;
     L.vmap_bits = (uint32_t)(2 * cap_f);
     vmap_bits += (2 * cap_f + 31) & ~31ull;
-    L._pad = 0;
+    {  // exact hit set (kernels.hip hset_insert): ~one key per phase-A item; a fuller table
+       // only sends the request back to re-evaluation (exact either way)
+      uint64_t amps = 1;
+      const uint8_t* u = in->data + q.uri.off;
+      for (uint32_t k = 0; k < q.uri.len; k++) amps += u[k] == '&';
+      const uint64_t est = 2 * (amps + q.hdr_count + 2 * ncookie + cookie / 8 + (PG.body_access ? post_fields : 0)) +
+                           n_single_items;
+      uint64_t cap = 16;
+      while (cap < est && cap < (1ull << 16)) cap <<= 1;
+      L.hset_mask = PG.streams.empty() ? 0u : (uint32_t)(cap - 1);
+      L.hset_word = hset_words;
+      hset_words += PG.streams.empty() ? 0 : (cap + 1 + 3) & ~3ull;
+    }
     L.base = off;
     L.cap_f = (uint32_t)cap_f;
     L.cap_b = (uint32_t)cap_b;
@@ -592,6 +634,9 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     L.cap_mt = (uint32_t)cap_mt;
     uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + GI_RM_BYTES + (cap_b + 15) / 16 * 16 +
                   2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
+    // observable captures (kernels.hip region_of): workspace + one value buffer per group
+    sz += (4ull * c->prog.cap_ws_words + 15) / 16 * 16 +
+          (c->prog.cap_ws_words ? (uint64_t)c->prog.cap_groups * ((cap_t + 15) / 16 * 16) : 0);
     // matched-variable state (kernels.hip MvState): header, entries, value
     // arena, MATCHED_VAR copy, name buffer
     if (PG.mv_used)
@@ -611,6 +656,13 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     return hip_fail(c, e, "alloc verdicts");
   if ((e = c->matched.ensure(std::max<size_t>((size_t)n * c->mcap * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc matched");
+  c->cap_on = c->prog.cap_ws_words != 0;
+  if (c->cap_on) {
+    if ((e = c->caprec.ensure(std::max<size_t>(16ull * n * c->crcap, 16))) != hipSuccess) return hip_fail(c, e, "alloc capture records");
+    if ((e = c->capbytes.ensure(std::max<size_t>((size_t)n * c->cbcap, 16))) != hipSuccess) return hip_fail(c, e, "alloc capture bytes");
+  }
+  c->staged_crcap = c->crcap;
+  c->staged_cbcap = c->cbcap;
   if ((e = c->tally.ensure(sizeof(gi_tally))) != hipSuccess) return hip_fail(c, e, "alloc tally");
   if ((e = c->tally_ext.ensure(4ull * (GI_SCORE_BINS + c->tally_ids.size()))) != hipSuccess)
     return hip_fail(c, e, "alloc detail tally");
@@ -618,6 +670,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     return hip_fail(c, e, "alloc tx slots");
   c->hit_words = (PG.n_hit_slots + 31) / 32;
   c->vmap_words = vmap_bits;  // one u32 slot signature per (field, side): bit (slot % 32) of each slot it hit
+  c->hset_words = hset_words;
+  if ((e = c->hset.ensure(std::max<uint64_t>(4 * hset_words, 16))) != hipSuccess) return hip_fail(c, e, "alloc hit sets");
   // k_body's work list: requests with a body, longest first (one wave each)
   std::vector<uint32_t> blist;
   for (uint32_t r = 0; r < n; r++)
@@ -656,16 +710,21 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       return hip_fail(c, e, "alloc lane scratch");
     if ((e = c->pool.ensure(4ull * c->pool_cap)) != hipSuccess) return hip_fail(c, e, "alloc queue pool");
     if ((e = c->qblk.ensure(8ull * ns * c->qcap)) != hipSuccess) return hip_fail(c, e, "alloc queue blocks");
-    if ((e = c->ctr.ensure(160 + 8 * 16)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+    if ((e = c->ctr.ensure(352)) != hipSuccess) return hip_fail(c, e, "alloc counters");
     (void)ns;
     if ((e = c->slow.ensure(40ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
     // long values (>= GI_LONG_MIN bytes): one k_long wave per (item, stream), each
     // workgroup with two buffers of 3x the longest request (overflow: "maybe", exact)
     c->long_cap = (uint32_t)std::min<uint64_t>(((raw_total + raw_body) / GI_LONG_MIN + 16) * 2ull * ns, 0x7FFFFFFFull);
-    c->long_bufcap = (3ull * max_req_bytes + 1024 + 15) & ~15ull;
+    // The buffers are bounded by GI_LONG_BUDGET bytes in total: fewer k_long
+    // workgroups when the longest request is large, and a per-buffer cap past
+    // which a chain overflows ("maybe": k_eval evaluates those links, exact),
+    // so one oversized request can never fail the batch's allocation.
+    c->long_bufcap = std::min<uint64_t>((3ull * max_req_bytes + 1024 + 15) & ~15ull, GI_LONG_BUDGET / 2);
+    c->long_grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(GI_LONG_GRID, GI_LONG_BUDGET / (2 * c->long_bufcap)));
     if ((e = c->long_list.ensure(8ull * c->long_cap)) != hipSuccess) return hip_fail(c, e, "alloc long-value list");
-    if ((e = c->long_buf.ensure((uint64_t)GI_LONG_GRID * 2 * c->long_bufcap)) != hipSuccess)
+    if ((e = c->long_buf.ensure((uint64_t)c->long_grid * 2 * c->long_bufcap)) != hipSuccess)
       return hip_fail(c, e, "alloc long-value buffers");
     // @detectSQLi/@detectXSS candidate list (overflow: the vals' bits become "maybe", exact)
     // an item lists its unchanged value once and each differently transformed
@@ -715,10 +774,15 @@ int gi_run_staged(gi_ctx* c) {
   B.layout = (const ReqLayout*)c->layout.p;
   B.verdicts = (gi_verdict*)c->verdicts.p;
   B.matched = (uint32_t*)c->matched.p;
+  B.caprec = c->cap_on ? (uint32_t*)c->caprec.p : nullptr;
+  B.capbytes = c->cap_on ? (uint8_t*)c->capbytes.p : nullptr;
+  B.crcap = c->staged_crcap;
+  B.cbcap = c->staged_cbcap;
   B.tally = (unsigned long long*)c->tally.p;
   B.tally_ext = (uint32_t*)c->tally_ext.p;
   B.hits = (uint32_t*)c->hits.p;
   B.vmap = (uint32_t*)c->vmap.p;
+  B.hset = (uint32_t*)c->hset.p;
   B.body_list = (const uint32_t*)c->blist.p;
   B.n_body = c->n_body;
   B.n_mp_body = c->n_mp_body;
@@ -751,7 +815,7 @@ int gi_run_staged(gi_ctx* c) {
     B.long_list = (uint2*)c->long_list.p;
     B.long_count = (uint32_t*)(cp + 40);
     B.long_cap = c->prog.n_streams ? c->long_cap : 0;
-    B.long_grid = GI_LONG_GRID;
+    B.long_grid = c->long_grid;
     B.long_buf = (uint8_t*)c->long_buf.p;
     B.long_bufcap = c->long_bufcap;
     B.det = c->det.p;
@@ -768,6 +832,7 @@ int gi_run_staged(gi_ctx* c) {
     }
     B.items_cap = c->items_cap;
     B.n_hit_slots = c->rs->prog.n_hit_slots;
+    B.vcause = (unsigned long long*)(cp + 288);  // 5 void-cause counters
     B.dbg = (uint32_t*)(cp + 128);  // 4 words (only written by -DGI_DEBUG builds)
   }
   (void)hipEventRecord(c->ev0, c->stream);
@@ -782,6 +847,10 @@ int gi_run_staged(gi_ctx* c) {
   if (c->vmap_words) {
     e = hipMemsetAsync(c->vmap.p, 0, 4 * c->vmap_words, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "memset value map");
+  }
+  if (c->hset_words) {
+    e = hipMemsetAsync(c->hset.p, 0, 4 * c->hset_words, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "memset hit sets");
   }
   launch_pipeline(c->prog, B, c->scan, c->stream, c->evs, c->stop_after, &c->log,
                   (const uint32_t*)c->tally_idbuf.p, (uint32_t)c->tally_ids.size());
@@ -888,6 +957,14 @@ int gi_sync(gi_ctx* c) {
         c->stats.diag[1] = h[1];
         c->stats.diag[2] = h[2] & 0xFFFFFFFFull;
         for (int b = 0; b < 5; b++) c->stats.diag[3 + b] = ib[2 * b + 1];
+        uint64_t vc[5] = {0, 0, 0, 0, 0};
+        if (hipMemcpy(vc, (uint8_t*)c->ctr.p + 288, 40, hipMemcpyDeviceToHost) == hipSuccess)
+          fprintf(stderr, "GI_DIAG phase-A void events: field %llu long %llu slow %llu qcap %llu pool %llu "
+                  "(pool used %llu of %llu words, slow %llu of %u entries, %llu of %llu bytes)\n",
+                  (unsigned long long)vc[0], (unsigned long long)vc[1], (unsigned long long)vc[2],
+                  (unsigned long long)vc[3], (unsigned long long)vc[4], (unsigned long long)h[0],
+                  (unsigned long long)c->pool_cap, (unsigned long long)(h[2] & 0xFFFFFFFFull), c->slow_cap,
+                  (unsigned long long)h[1], (unsigned long long)c->slow_bytes_cap);
         if (c->det_cap)  // @detectSQLi/@detectXSS candidates listed by k_stream (k_detect entries)
           fprintf(stderr, "GI_DIAG detect entries %llu (cap %u), bytes %llu (cap %llu)\n",
                   (unsigned long long)(h[3] & 0xFFFFFFFFull), c->det_cap, (unsigned long long)h[4],
@@ -909,6 +986,18 @@ int gi_fetch_results(gi_ctx* c, gi_results* out) {
     e = hipMemcpy(out->verdicts, c->verdicts.p, (size_t)c->n_req * sizeof(gi_verdict), hipMemcpyDeviceToHost);
   if (e == hipSuccess && c->n_req && out->matched_ids)
     e = hipMemcpy(out->matched_ids, c->matched.p, (size_t)c->n_req * c->mcap * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && c->n_req && (out->captures || out->capture_bytes)) {
+    if (out->capture_cap != c->staged_crcap || out->capture_bytes_cap != c->staged_cbcap)
+      return fail(c, GI_ETRUNC, "capture caps differ from the context's");
+    if (!c->cap_on) {  // no observable capture in the ruleset: empty rows
+      if (out->captures) memset(out->captures, 0, sizeof(gi_capture) * c->n_req * c->staged_crcap);
+    } else {
+      if (out->captures)
+        e = hipMemcpy(out->captures, c->caprec.p, sizeof(gi_capture) * c->n_req * c->staged_crcap, hipMemcpyDeviceToHost);
+      if (e == hipSuccess && out->capture_bytes)
+        e = hipMemcpy(out->capture_bytes, c->capbytes.p, (size_t)c->n_req * c->staged_cbcap, hipMemcpyDeviceToHost);
+    }
+  }
   if (e != hipSuccess) return hip_fail(c, e, "fetch D2H");
   return GI_OK;
 }
@@ -976,6 +1065,21 @@ int gi_selftest_regex_many(const char* pattern, size_t plen, const uint8_t* data
     out[k] = (dfa ? dfa_host_match(d, s, len) : nfa_host_match(t, s, len)) ? 1 : 0;
   }
   return GI_OK;
+}
+
+int gi_selftest_capture(const char* pattern, size_t plen, const uint8_t* s, size_t n, int32_t* caps,
+                        uint32_t* nslot) {
+  if (!pattern || (n && !s) || !caps || !nslot) return GI_EINVAL;
+  Regex re;
+  std::string err;
+  if (!re_parse("(?sm)" + std::string(pattern, plen), &re, &err)) return GI_EPARSE;
+  std::vector<DPikeInst> insts;
+  std::vector<uint32_t> pool;
+  DPike pk{};
+  if (!build_pike(re, &insts, &pool, &pk, &err)) return GI_EUNSUPPORTED;
+  std::vector<uint32_t> ws(pike_ws_words(pk.n_inst, pk.nslot));
+  *nslot = pk.nslot;
+  return pike_match(insts.data() + pk.inst_off, pool.data(), pk, s, (uint32_t)n, ws.data(), caps) ? 1 : 0;
 }
 
 int gi_selftest_regex(const char* pattern, size_t plen, const uint8_t* s, size_t n, uint32_t* n_states) {
@@ -1067,9 +1171,26 @@ extern "C" int gi_selftest_plan(const gi_ruleset* rs, char* err, size_t errcap) 
         const uint32_t jc = (((const uint32_t*)img)[c] >> (8 * q)) & 0xFF;
         if (jc >= d.n_classes || jc != img[jd.lds_amap + c]) return bad(13, "joint class map");
       }
-      if (P.streams[J.stream].collapse &&
-          (d.byte_mode || !d.nonascii_uniform || ((((const uint32_t*)img)[128] >> (8 * q)) & 0xFF) != d.nonascii_cls))
-        return bad(20, "collapsed stream with a rune-distinguishing automaton");
+      if (P.streams[J.stream].collapse) {  // every rune-mapped byte lands in the automaton's class of its runes
+        const DStream& S = P.streams[J.stream];
+        if (d.byte_mode) return bad(20, "rune-mapped stream with a byte-mode automaton");
+        auto cls_of = [&](uint32_t r) -> uint32_t {
+          for (uint32_t k = 0; k < d.nr_cnt; k++)
+            if (P.nranges[d.nr_off + 3 * k] <= r && r <= P.nranges[d.nr_off + 3 * k + 1]) return P.nranges[d.nr_off + 3 * k + 2];
+          return 0;
+        };
+        if (S.rmap_cnt == 0) {
+          if (!d.nonascii_uniform || ((((const uint32_t*)img)[128] >> (8 * q)) & 0xFF) != d.nonascii_cls)
+            return bad(20, "collapsed stream with a rune-distinguishing automaton");
+        }
+        for (uint32_t k = 0; k < S.rmap_cnt; k++) {
+          const uint32_t lo = P.nranges[S.rmap_off + 3 * k], hi = P.nranges[S.rmap_off + 3 * k + 1];
+          const uint32_t b = P.nranges[S.rmap_off + 3 * k + 2];
+          const uint32_t jc = (((const uint32_t*)img)[b] >> (8 * q)) & 0xFF;
+          if (jc != cls_of(lo) || jc != cls_of(hi) || jc != cls_of(lo + (hi - lo) / 2))
+            return bad(22, "rune map byte in another class than its runes");
+        }
+      }
       for (uint32_t k = 0; k < jd.n_pat; k++)
         if (*(const uint32_t*)(img + jd.lds_slots + 4 * k) != P.pats[jd.pat_begin + k].slot) return bad(14, "slot table");
       // image walk == global-table walk on random ASCII strings

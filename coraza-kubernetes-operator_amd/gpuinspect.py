@@ -46,6 +46,7 @@ GI_REQ_BODY_LIMIT = 0x4
 GI_REQ_OVERFLOW = 0x8
 GI_REQ_MATCH_TRUNC = 0x10
 GI_REQ_BODY_ERROR = 0x20
+GI_REQ_CAPTURE_TRUNC = 0x40
 GI_REQ_ERROR_MASK = 0x0F
 
 ACTIONS = {0: "", 1: "deny", 2: "drop", 3: "redirect"}
@@ -57,8 +58,10 @@ REQUEST_DT = np.dtype([("method", SPAN_DT), ("uri", SPAN_DT), ("proto", SPAN_DT)
                        ("remote_port", "<u4"), ("_pad", "<u4")])
 HEADER_DT = np.dtype([("name", SPAN_DT), ("value", SPAN_DT)])
 VERDICT_DT = np.dtype([("rule_id", "<i4"), ("status", "<i4"), ("action", "u1"), ("phase", "u1"),
-                       ("flags", "<u2"), ("match_cnt", "<u4"), ("tx_export", "<i8", (MAX_EXPORTS,))])
-assert REQUEST_DT.itemsize == 96 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 80
+                       ("flags", "<u2"), ("match_cnt", "<u4"), ("tx_export", "<i8", (MAX_EXPORTS,)),
+                       ("capture_cnt", "<u4"), ("_pad", "<u4")])
+CAPTURE_DT = np.dtype([("rule_id", "<i4"), ("group", "<u4"), ("off", "<u4"), ("len", "<u4")])
+assert REQUEST_DT.itemsize == 96 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 88
 
 EXPORTED_SYMBOLS = (
     "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name", "gi_ruleset_describe",
@@ -66,6 +69,7 @@ EXPORTED_SYMBOLS = (
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
     "gi_ctx_stream", "gi_selftest_regex", "gi_selftest_plan", "gi_selftest_triggers",
     "gi_ruleset_save", "gi_ruleset_load", "gi_ctx_swap_ruleset", "gi_compiler_rev", "gi_tally_detail_get", "gi_selftest_regex_many",
+    "gi_ctx_set_capture_cap", "gi_selftest_capture",
 )
 SCORE_BINS = 64  # GI_SCORE_BINS
 
@@ -102,7 +106,9 @@ class _Batch(ctypes.Structure):
 
 
 class _Results(ctypes.Structure):
-    _fields_ = [("verdicts", ctypes.c_void_p), ("matched_ids", ctypes.c_void_p), ("matched_cap", ctypes.c_uint32)]
+    _fields_ = [("verdicts", ctypes.c_void_p), ("matched_ids", ctypes.c_void_p), ("matched_cap", ctypes.c_uint32),
+                ("captures", ctypes.c_void_p), ("capture_bytes", ctypes.c_void_p), ("capture_cap", ctypes.c_uint32),
+                ("capture_bytes_cap", ctypes.c_uint32)]
 
 
 class _Tally(ctypes.Structure):
@@ -170,6 +176,9 @@ def load_library(path: str = LIB_PATH):
     lib.gi_selftest_regex_many.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.POINTER(u64), u32,
                                            ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(u32)]
     lib.gi_selftest_triggers.argtypes = [ctypes.POINTER(u32), u32, ctypes.POINTER(u32)]
+    lib.gi_ctx_set_capture_cap.argtypes = [vp, u32, u32]
+    lib.gi_selftest_capture.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int32),
+                                        ctypes.POINTER(u32)]
     _LIB = lib
     return lib
 
@@ -225,6 +234,7 @@ class Ruleset:
         info = _Info()
         self._lib.gi_ruleset_info_get(self._h, ctypes.byref(info))
         self.info = {k: getattr(info, k) for k, _ in _Info._fields_ if not k.startswith("_")}
+        self.capture_rules = frozenset(self.describe().get("capture_rules", []))
 
     def save(self) -> bytes:
         """The GPU artifact (gi_ruleset_save): the compiled program as one blob."""
@@ -336,8 +346,29 @@ class PackedBatch:
         return per + hs[b + r["hdr_count"]] - hs[b]
 
     def take(self, lo: int, hi: int) -> "PackedBatch":
-        """Requests [lo, hi) as their own batch (a shard of this one)."""
-        return pack([self.request(i) for i in range(lo, hi)])
+        """Requests [lo, hi) as their own batch (a shard of this one): the
+        records are sliced and the byte arena is cut to the range they span."""
+        reqs = self.reqs[lo:hi].copy()
+        if hi <= lo:
+            return PackedBatch(np.zeros(1, np.uint8), reqs, np.zeros(0, HEADER_DT))
+        h0 = int(self.reqs[lo]["hdr_begin"])
+        h1 = int(self.reqs[hi - 1]["hdr_begin"] + self.reqs[hi - 1]["hdr_count"])
+        headers = self.headers[h0:h1].copy()
+        starts = [reqs[n]["off"] for n in ("method", "uri", "proto", "body", "remote_addr")]
+        ends = [reqs[n]["off"] + reqs[n]["len"] for n in ("method", "uri", "proto", "body", "remote_addr")]
+        if len(headers):
+            starts += [headers["name"]["off"], headers["value"]["off"]]
+            ends += [headers["name"]["off"] + headers["name"]["len"], headers["value"]["off"] + headers["value"]["len"]]
+        d0 = int(min(int(x.min()) for x in starts))
+        d1 = int(max(int(x.max()) for x in ends))
+        for n in ("method", "uri", "proto", "body", "remote_addr"):
+            reqs[n]["off"] -= d0
+        if len(headers):
+            headers["name"]["off"] -= d0
+            headers["value"]["off"] -= d0
+        reqs["hdr_begin"] -= h0
+        data = self.data[d0:max(d1, d0 + 1)].copy()
+        return PackedBatch(data, reqs, headers)
 
     def to_ctypes(self) -> _Batch:
         return _Batch(self.n_req, self.data.ctypes.data, len(self.data), self.reqs.ctypes.data,
@@ -353,6 +384,28 @@ class PackedBatch:
               self.headers[int(q["hdr_begin"]):int(q["hdr_begin"]) + int(q["hdr_count"])]]
         return Transaction(sp(q["method"]), sp(q["uri"]), sp(q["proto"]), hs, sp(q["body"]),
                            sp(q["remote_addr"]), int(q["remote_port"]))
+
+
+def concat(batches: Sequence[PackedBatch]) -> PackedBatch:
+    """One batch of the requests of `batches`, in order (arenas appended)."""
+    datas, reqs, hdrs = [], [], []
+    doff = hoff = 0
+    for b in batches:
+        r = b.reqs.copy()
+        h = b.headers.copy()
+        for n in ("method", "uri", "proto", "body", "remote_addr"):
+            r[n]["off"] += doff
+        h["name"]["off"] += doff
+        h["value"]["off"] += doff
+        r["hdr_begin"] += hoff
+        datas.append(b.data)
+        reqs.append(r)
+        hdrs.append(h)
+        doff += len(b.data)
+        hoff += len(b.headers)
+    if not batches:
+        return PackedBatch(np.zeros(1, np.uint8), np.zeros(0, REQUEST_DT), np.zeros(0, HEADER_DT))
+    return PackedBatch(np.concatenate(datas), np.concatenate(reqs), np.concatenate(hdrs))
 
 
 def pack(txs: Sequence) -> PackedBatch:
@@ -422,6 +475,19 @@ class Results:
     verdicts: np.ndarray     # VERDICT_DT
     matched: np.ndarray      # uint32 [n_req, matched_cap]
     exports: Tuple[str, ...]
+    capture_recs: Optional[np.ndarray] = None   # CAPTURE_DT [n_req, capture_cap]
+    capture_bytes: Optional[np.ndarray] = None  # uint8 [n_req, capture_bytes_cap]
+    capture_rules: Optional[frozenset] = None   # rule ids with observable captures (the plan's capture_rules)
+
+    def captures(self, i: int) -> List[Tuple[int, int, bytes]]:
+        """The observable captures of request i in evaluation order:
+        (top-level rule id, group, captured bytes)."""
+        if self.capture_recs is None:
+            return []
+        n = min(int(self.verdicts[i]["capture_cnt"]), self.capture_recs.shape[1])
+        row = self.capture_bytes[i]
+        return [(int(c["rule_id"]), int(c["group"]), bytes(row[int(c["off"]):int(c["off"]) + int(c["len"])]))
+                for c in self.capture_recs[i, :n]]
 
     def matched_rules(self, i: int) -> List[int]:
         n = min(int(self.verdicts[i]["match_cnt"]), self.matched.shape[1])
@@ -441,7 +507,8 @@ class Results:
 class Engine:
     """A device context (one HIP stream) evaluating batches on one GPU."""
 
-    def __init__(self, ruleset: Ruleset, device: int = 0, matched_cap: int = 64):
+    def __init__(self, ruleset: Ruleset, device: int = 0, matched_cap: int = 64, capture_cap: int = 8,
+                 capture_bytes_cap: int = 512):
         lib = load_library()
         self._lib = lib
         self.ruleset = ruleset
@@ -452,6 +519,8 @@ class Engine:
             raise EngineError("gi_ctx_create failed (%d): no usable HIP device %d" % (rc, device))
         self._h = h
         self._staged = None
+        self.capture_cap, self.capture_bytes_cap = capture_cap, capture_bytes_cap
+        self._check(lib.gi_ctx_set_capture_cap(h, capture_cap, capture_bytes_cap), "gi_ctx_set_capture_cap")
 
     def swap(self, ruleset: Ruleset):
         """Hot swap (gi_ctx_swap_ruleset): later batches run `ruleset`; a staged
@@ -479,9 +548,12 @@ class Engine:
         n = self._staged.n_req
         verd = np.zeros(n, VERDICT_DT)
         matched = np.zeros((n, self.matched_cap), np.uint32)
-        res = _Results(verd.ctypes.data, matched.ctypes.data, self.matched_cap)
+        crec = np.zeros((n, self.capture_cap), CAPTURE_DT)
+        cbytes = np.zeros((n, self.capture_bytes_cap), np.uint8)
+        res = _Results(verd.ctypes.data, matched.ctypes.data, self.matched_cap, crec.ctypes.data, cbytes.ctypes.data,
+                       self.capture_cap, self.capture_bytes_cap)
         self._check(self._lib.gi_fetch_results(self._h, ctypes.byref(res)), "gi_fetch_results")
-        return Results(verd, matched, self.ruleset.exports)
+        return Results(verd, matched, self.ruleset.exports, crec, cbytes, self.ruleset.capture_rules)
 
     def inspect(self, batch) -> Results:
         if not isinstance(batch, PackedBatch):
@@ -572,3 +644,19 @@ def selftest_regex_many(pattern: str, strings):
         raise SecLangError(rc, "selftest_regex_many failed")
     return [int(out[k]) for k in range(len(strings))], n.value
 
+
+
+def selftest_capture(pattern: str, data: bytes):
+    """The capture submatch program (pike.h, what k_eval runs) on the host:
+    None without a match, else the group spans [(start, end) or None, ...]
+    (FindStringSubmatchIndex restricted to groups 0..8)."""
+    lib = load_library()
+    pb = pattern.encode()
+    caps = (ctypes.c_int32 * 18)()
+    ns = ctypes.c_uint32(0)
+    rc = lib.gi_selftest_capture(pb, len(pb), data, len(data), caps, ctypes.byref(ns))
+    if rc < 0:
+        raise SecLangError(rc, "selftest_capture failed")
+    if rc == 0:
+        return None
+    return [(caps[2 * g], caps[2 * g + 1]) if caps[2 * g] >= 0 else None for g in range(ns.value // 2)]

@@ -44,6 +44,92 @@ def balanced_slices(sizes: Sequence[int], world: int) -> List[Tuple[int, int]]:
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
+def request_set_chunk(rank: int) -> int:
+    """The request set a multi-GPU bench inspects is one seeded set: chunk k is
+    the generator's batch for seed shard_seed(SEED, k), k = 0 .. world - 1,
+    concatenated in order.  Each rank generates only its own chunk, then
+    `rebalance` moves requests across chunk boundaries so every rank holds a
+    byte-balanced contiguous slice of the whole set."""
+    return rank
+
+
+def _gather_i64(dist, x, device):
+    import torch
+    t = torch.as_tensor(np.asarray(x, dtype=np.int64), device=device)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=device)
+    world = dist.get_world_size()
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    m = int(max(int(v.item()) for v in ns))
+    pad = torch.zeros(m, dtype=torch.int64, device=device)
+    pad[:t.numel()] = t
+    outs = [torch.zeros(m, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(outs, pad)
+    return [o[:int(k.item())].cpu().numpy() for o, k in zip(outs, ns)]
+
+
+def _send_batch(dist, b, dst, device):
+    import torch
+    parts = [b.data.view(np.uint8), b.reqs.view(np.uint8), b.headers.view(np.uint8)]
+    hdr = torch.tensor([len(p) for p in parts], dtype=torch.int64, device=device)
+    dist.send(hdr, dst)
+    for p in parts:
+        if len(p):
+            dist.send(torch.from_numpy(np.ascontiguousarray(p)).to(device), dst)
+
+
+def _recv_batch(dist, src, device):
+    import torch
+
+    import gpuinspect
+    hdr = torch.zeros(3, dtype=torch.int64, device=device)
+    dist.recv(hdr, src)
+    arrs = []
+    for k in range(3):
+        n = int(hdr[k].item())
+        t = torch.zeros(n, dtype=torch.uint8, device=device)
+        if n:
+            dist.recv(t, src)
+        arrs.append(t.cpu().numpy())
+    return gpuinspect.PackedBatch(arrs[0], arrs[1].view(gpuinspect.REQUEST_DT), arrs[2].view(gpuinspect.HEADER_DT))
+
+
+def rebalance(dist, world: int, rank: int, batch, device):
+    """Byte-balanced split of one request set across ranks.
+
+    `batch` is this rank's chunk of the set (request_set_chunk).  The ranks
+    all-gather the raw byte size of every request, cut the concatenated set
+    with balanced_slices, and send each request whose slice owner differs from
+    its chunk owner to that rank (point-to-point, before any timing).  Returns
+    (this rank's slice as a PackedBatch, (lo, hi) global range, per-rank byte
+    totals)."""
+    import gpuinspect
+    sizes = _gather_i64(dist, batch.request_bytes(), device)
+    counts = [len(x) for x in sizes]
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    allsz = np.concatenate(sizes) if sizes else np.zeros(0, np.int64)
+    sl = balanced_slices(allsz, world)
+    pieces = {}
+    # (owner s of chunk, receiver d of slice): every rank walks the pairs in one order
+    for s in range(world):
+        for d in range(world):
+            lo = max(int(starts[s]), sl[d][0])
+            hi = min(int(starts[s + 1]), sl[d][1])
+            if hi <= lo:
+                continue
+            if s == d:
+                if rank == s:
+                    pieces[lo] = batch.take(lo - int(starts[s]), hi - int(starts[s]))
+                continue
+            if rank == s:
+                _send_batch(dist, batch.take(lo - int(starts[s]), hi - int(starts[s])), d, device)
+            elif rank == d:
+                pieces[lo] = _recv_batch(dist, s, device)
+    mine = gpuinspect.concat([pieces[k] for k in sorted(pieces)])
+    totals = [int(allsz[a:b].sum()) for a, b in sl]
+    return mine, sl[rank], totals
+
+
 class TallyGather:
     """all_gather_into_tensor of every rank's tally vector (int64)."""
 

@@ -53,10 +53,11 @@ extern "C" {
 /* per-request verdict flags (gi_verdict.flags) */
 #define GI_REQ_UNSUPPORTED_URI 0x1   /* request-target outside the supported forms */
 #define GI_REQ_UNSUPPORTED_BODY 0x2  /* body processor not implemented, or a body beyond the engine's limits */
-#define GI_REQ_BODY_LIMIT 0x4        /* body over SecRequestBodyLimit */
+#define GI_REQ_BODY_LIMIT 0x4        /* (no longer set: an over-limit body gets coraza's 413 / ProcessPartial) */
 #define GI_REQ_OVERFLOW 0x8          /* internal per-request capacity exceeded */
 #define GI_REQ_MATCH_TRUNC 0x10      /* more matched rules than matched_cap */
 #define GI_REQ_BODY_ERROR 0x20       /* the body processor rejected the body: REQBODY_ERROR=1 (verdict valid) */
+#define GI_REQ_CAPTURE_TRUNC 0x40    /* more capture records / bytes than the ctx's capture caps (verdict valid) */
 #define GI_REQ_ERROR_MASK 0x0F       /* verdict is not valid when any of these is set */
 
 /* interruption action (coraza types.Interruption.Action) */
@@ -147,12 +148,32 @@ typedef struct {
   uint16_t flags;    /* GI_REQ_* */
   uint32_t match_cnt;                 /* matched rules (may exceed matched_cap) */
   int64_t tx_export[GI_MAX_EXPORTS];  /* Atoi of the exported TX values (0 if unset) */
+  uint32_t capture_cnt;               /* capture records written (gi_results.captures) */
+  uint32_t _pad;
 } gi_verdict;
+
+/* One observable capture (coraza rx.go FindStringSubmatch -> TX.<group>):
+ * the top-level rule whose link captured, the group, and the captured bytes
+ * at capture_bytes[row + off, + len).  Recorded for every capture whose
+ * TX.0-TX.8 value a rule, macro or export can read (the compiler drops the
+ * others: they change no output); in evaluation order. */
+typedef struct {
+  int32_t rule_id;
+  uint32_t group;
+  uint32_t off;
+  uint32_t len;
+} gi_capture;
 
 typedef struct {
   gi_verdict* verdicts;   /* n_req entries */
   uint32_t* matched_ids;  /* n_req * matched_cap entries, row r = request r */
   uint32_t matched_cap;   /* must equal the ctx's matched_cap */
+  /* optional (NULL: not fetched): n_req rows of capture_cap records and of
+   * capture_bytes_cap bytes; the caps must equal the ctx's (gi_ctx_set_capture_cap) */
+  gi_capture* captures;
+  uint8_t* capture_bytes;
+  uint32_t capture_cap;
+  uint32_t capture_bytes_cap;
 } gi_results;
 
 /* Batch-level tallies (what bench/RCCL all-gathers across GPUs). */
@@ -231,6 +252,9 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
  * KATs reconcile_test.go:72-88).  Device buffers are reused; a staged batch
  * is dropped and must be staged again.  rs must outlive its use by the ctx. */
 int gi_ctx_swap_ruleset(gi_ctx* ctx, const gi_ruleset* rs);
+/* Capture-record capacity per request (default 8 records, 512 bytes); takes
+ * effect from the next staged batch.  Overflow sets GI_REQ_CAPTURE_TRUNC. */
+int gi_ctx_set_capture_cap(gi_ctx* ctx, uint32_t records, uint32_t bytes);
 void gi_ctx_free(gi_ctx* ctx);
 const char* gi_last_error(const gi_ctx* ctx);
 
@@ -267,6 +291,12 @@ int gi_selftest_regex(const char* pattern, size_t plen, const uint8_t* s, size_t
  * and the NFA tables (the compiler's fallback for @rx) answered. */
 int gi_selftest_regex_many(const char* pattern, size_t plen, const uint8_t* data, const uint64_t* offs, uint32_t n,
                            uint8_t* out, uint32_t* n_states);
+/* The capture submatch program (pike.h, the code k_eval runs) on the host:
+ * "(?sm)" + pattern over s -> 1 on a match with caps[0 .. *nslot) = group
+ * byte offsets (-1: not set), 0 without a match, or a negative GI_* code.
+ * caps needs 18 entries. */
+int gi_selftest_capture(const char* pattern, size_t plen, const uint8_t* s, size_t n, int32_t* caps,
+                        uint32_t* nslot);
 /* Host emulation of the phase-A scan over every job image of a compiled
  * ruleset (bounds + image walk vs the global tables).  0 = consistent. */
 int gi_selftest_plan(const gi_ruleset* rs, char* err, size_t errcap);

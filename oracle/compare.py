@@ -53,6 +53,15 @@ def compare(res, oracle, error_mask=0x0F, max_report=10):
             a = a if ok else 0
             if int(v["tx_export"][k]) != a:
                 bad.append((i, "tx." + name, a, int(v["tx_export"][k])))
+        # observable captures (rules the compiler lists in its plan's
+        # capture_rules; the others change no output and are not recorded)
+        crules = getattr(res, "capture_rules", None)
+        if crules is not None and getattr(res, "capture_recs", None) is not None:
+            exp_c = [c for c in ov.captures if c[0] in crules]
+            got_c = res.captures(i)
+            trunc = bool(int(v["flags"]) & 0x40)  # GI_REQ_CAPTURE_TRUNC: the records are a prefix
+            if (got_c != exp_c[:len(got_c)]) if trunc else (got_c != exp_c):
+                bad.append((i, "captures", exp_c[:6], got_c[:6]))
         if len(bad) >= max_report:
             break
     return bad

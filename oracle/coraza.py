@@ -59,8 +59,11 @@ SINGLE_VARS = {
     "REQBODY_PROCESSOR", "MULTIPART_STRICT_ERROR", "ARGS_COMBINED_SIZE",
     "FULL_REQUEST_LENGTH", "MATCHED_VAR", "MATCHED_VAR_NAME",
     "REMOTE_ADDR", "REMOTE_PORT", "SERVER_NAME", "URLENCODED_ERROR",
-    "FILES_COMBINED_SIZE",
+    "FILES_COMBINED_SIZE", "INBOUND_DATA_ERROR",
 }
+# FULL_REQUEST_LENGTH and URLENCODED_ERROR are declared variables that
+# coraza v3.3.3's transaction never sets [upstream internal/corazawaf/
+# transaction.go; bodyprocessors/urlencoded.go]: they read "" (parity unpinned).
 MAP_VARS = {
     # name: (source collection(s), case_insensitive_keys)
     "ARGS_GET": (("ARGS_GET",), False),
@@ -1681,6 +1684,8 @@ class Verdict:
     matched: List[int] = field(default_factory=list)
     tx: Dict[str, bytes] = field(default_factory=dict)
     unsupported: bool = False
+    # every capture write in evaluation order: (top-level rule id, group, value)
+    captures: List[Tuple[int, int, bytes]] = field(default_factory=list)
 
 
 class Transaction:
@@ -1705,6 +1710,8 @@ class Transaction:
         self.force_body = False
         self.body = b""
         self.phase = 0
+        self.cur_top = 0
+        self.captures: List[Tuple[int, int, bytes]] = []
 
     # -- request population -------------------------------------------------
     def process_request(self, req: Request):
@@ -1740,10 +1747,17 @@ class Transaction:
             return self._tx_items()
         return self.maps[src]
 
+    def args_combined_size(self) -> bytes:
+        """[upstream internal/collections/sized.go SizeCollection over ARGS_GET
+        and ARGS_POST]: the sum of len(key) + len(value) of every entry."""
+        return str(sum(len(k) + len(v) for src in ("ARGS_GET", "ARGS_POST") for k, v in self.maps[src])).encode()
+
     def get_field(self, rv: RuleVariable):
         """tx.GetField: returns list of (key, value)."""
         name = rv.name
-        if name in SINGLE_VARS:
+        if name == "ARGS_COMBINED_SIZE":
+            vals = [(b"", self.args_combined_size())]
+        elif name in SINGLE_VARS:
             vals = [(b"", self.single.get(name, b""))]
         else:
             if name in MAP_VARS:
@@ -1797,6 +1811,8 @@ class Transaction:
             _, name, key = p
             if name == "TX":
                 out += self.tx.get(key.encode(), b"")
+            elif name == "ARGS_COMBINED_SIZE":
+                out += self.args_combined_size()
             elif name in SINGLE_VARS:
                 out += self.single.get(name, b"")
             elif name in MAP_VARS:
@@ -1825,6 +1841,7 @@ class Transaction:
                         if i == 9:
                             break
                         self.tx[str(i).encode()] = c
+                        self.captures.append((self.cur_top, i, c))
                     res = True
             else:
                 res = op.rx.match_string(value)
@@ -1834,6 +1851,7 @@ class Transaction:
                 caps = _pm_find_all(op.phrases, low, value)
                 for i, c in enumerate(caps[:10]):
                     self.tx[str(i).encode()] = c
+                    self.captures.append((self.cur_top, i, c))
                 res = len(caps) > 0
             else:
                 res = any(p in low for p in op.phrases)
@@ -1873,6 +1891,7 @@ class Transaction:
             res, fp = libinjection.is_sqli(value)
             if res and rule.capture:
                 self.tx[b"0"] = fp.encode()
+                self.captures.append((self.cur_top, 0, fp.encode()))
         elif n == "detectxss":
             res = libinjection.is_xss(value)  # detect_xss.go
         elif n == "validateutf8encoding":
@@ -2041,6 +2060,7 @@ class Transaction:
             # rulegroup.go: MATCHED_VARS(_NAMES) reset before each rule;
             # MATCHED_VAR(_NAME) keep the last match of the transaction
             self.maps["MATCHED_VARS"] = []
+            self.cur_top = r.id
             self.do_evaluate(r)
 
     def process_request_body(self):
@@ -2049,8 +2069,30 @@ class Transaction:
         if self.interruption is not None:
             return
         if self.body_access and len(self.body) > 0:
-            if len(self.body) > self.cfg.request_body_limit:
-                raise UnsupportedInput("request body over SecRequestBodyLimit")
+            # [upstream transaction.go WriteRequestBody]: a body over
+            # SecRequestBodyLimit sets INBOUND_DATA_ERROR; with Reject the
+            # transaction is interrupted with status 413 (no rule id) and
+            # ProcessRequestBody never runs; with ProcessPartial only the first
+            # SecRequestBodyLimit bytes are buffered.  ProcessRequestBody: a
+            # buffer of exactly the limit sets INBOUND_DATA_ERROR too, and with
+            # Reject returns before phase 2.  (DetectionOnly: no interruption,
+            # nothing buffered; parity unpinned.)
+            limit = self.cfg.request_body_limit
+            reject = self.cfg.request_body_limit_action.lower() != "processpartial"
+            if len(self.body) > limit:
+                self.single["INBOUND_DATA_ERROR"] = b"1"
+                if reject:
+                    if self.rule_engine == "On":
+                        self.interruption = (0, 413, "deny", 2)
+                        return
+                    self.body = b""
+                else:
+                    self.body = self.body[:limit]
+            if len(self.body) >= limit and len(self.body) > 0:
+                self.single["INBOUND_DATA_ERROR"] = b"1"
+                if reject:
+                    return
+        if self.body_access and len(self.body) > 0:
             self.single["REQUEST_BODY_LENGTH"] = str(len(self.body)).encode()
             rbp = self.single.get("REQBODY_PROCESSOR", b"")
             if self.force_body:
@@ -2252,6 +2294,7 @@ def inspect(cfg: WafConfig, req: Request, exports=DEFAULT_TX_EXPORTS) -> Verdict
     if tx.interruption is not None:
         out.rule_id, out.status, out.action, out.phase = tx.interruption
     out.matched = list(tx.matched)
+    out.captures = list(tx.captures)
     for name in exports:
         out.tx[name] = tx.tx.get(name.encode(), b"")
     return out

@@ -98,3 +98,61 @@ def test_take_and_request_bytes():
     assert sum(p.n_req for p in parts) == b.n_req
     assert sum(p.raw_bytes() for p in parts) == b.raw_bytes()
     assert parts[1].request(0) == b.request(parts[0].n_req)
+
+
+def test_concat_roundtrip():
+    import gpuinspect
+    import traffic
+    b = traffic.TrafficGen(traffic.SEED + 3).batch(30, post_frac=0.5)
+    c = gpuinspect.concat([b.take(0, 7), b.take(7, 7), b.take(7, 30)])
+    assert c.n_req == b.n_req
+    assert [c.request(i) for i in range(c.n_req)] == [b.request(i) for i in range(b.n_req)]
+
+
+def _rebalance_worker(rank, world, port, q):
+    import hashlib
+
+    import torch.distributed as dist
+
+    import shard
+    import traffic
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # this rank's chunk of the one request set (uneven on purpose: C3 bodies)
+    chunk = traffic.TrafficGen(shard.shard_seed(traffic.SEED, shard.request_set_chunk(rank))).batch(
+        40 + 30 * rank, post_frac=0.6)
+    mine, rng, totals = shard.rebalance(dist, world, rank, chunk, "cpu")
+    digs = [hashlib.sha1(repr(mine.request(i)).encode()).hexdigest() for i in range(mine.n_req)]
+    q.put((rank, rng, totals, digs, int(mine.raw_bytes())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rebalance_one_request_set(world):
+    """bench.py's multi-GPU split: ranks generate their chunks of one seeded
+    request set and exchange requests so each holds a byte-balanced
+    contiguous slice (gloo; the same code runs over RCCL on the GPU box)."""
+    import hashlib
+
+    import shard
+    import traffic
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rebalance_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=180) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = [traffic.TrafficGen(shard.shard_seed(traffic.SEED, k)).batch(40 + 30 * k, post_frac=0.6) for k in range(world)]
+    ref = [hashlib.sha1(repr(b.request(i)).encode()).hexdigest() for b in full for i in range(b.n_req)]
+    sizes = np.concatenate([b.request_bytes() for b in full])
+    assert [o[1] for o in outs] == shard.balanced_slices(sizes, world)
+    assert sum((o[3] for o in outs), []) == ref  # the slices, in rank order, are the whole set
+    for rank, (lo, hi), totals, digs, nbytes in outs:
+        assert nbytes == totals[rank] == int(sizes[lo:hi].sum())
+        assert abs(nbytes - sizes.sum() / world) <= sizes.max()

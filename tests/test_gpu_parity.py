@@ -314,3 +314,48 @@ def test_gpu_parity_matched_vars():
     assert scores[0] % 10 == 5 and scores[1] // 50000000 == 1  # MATCHED_VARS chain; User-Agent name macro
     batch = traffic.TrafficGen(traffic.SEED + 13).batch(600, attack_rate=0.3)
     _parity(MATCHED, batch)
+
+
+CAPTURE_RULES = r"""SecRuleEngine On
+SecRequestBodyAccess On
+SecAction "id:900,phase:1,pass,nolog,setvar:tx.allowed='|application/x-www-form-urlencoded| |multipart/form-data| |application/json|',setvar:tx.charsets='|utf-8| |iso-8859-1|'"
+SecRule REQUEST_HEADERS:Content-Type "@rx ^[^;\s]+" "id:920420,phase:1,pass,capture,t:none,setvar:'tx.content_type=|%{tx.0}|',chain"
+    SecRule TX:content_type "!@within %{tx.allowed}" "t:lowercase,setvar:tx.score=+5"
+SecRule REQUEST_HEADERS:Content-Type "@rx charset\s*=\s*[\"']?([^;\"'\s]+)" "id:920480,phase:1,pass,capture,t:none,chain"
+    SecRule TX:1 "!@within %{tx.charsets}" "t:lowercase,setvar:tx.score=+5"
+SecRule ARGS "@rx (?i)(union|select)\s+(\w+)" "id:942,phase:2,pass,capture,t:urlDecodeUni,setvar:'tx.last=%{tx.2}',setvar:tx.score=+3"
+SecRule ARGS_NAMES "!@rx ^([a-z]+)$" "id:943,phase:2,pass,capture,setvar:'tx.bad=%{tx.0}%{tx.1}'"
+SecRule TX:SCORE "@ge 8" "id:949,phase:2,deny,status:403"
+"""
+
+
+def test_gpu_capture_parity():
+    """Observable captures: the 920420 / 920480 chains read
+    their parent's TX.0 / TX.1, 942 and 943 read their own groups in setvar
+    (943 negated: captures from the names that do not make it match); the
+    capture records (rule, group, bytes) are compared with the oracle's."""
+    rs = gpuinspect.Ruleset(CAPTURE_RULES, tx_exports=["score", "content_type", "last", "bad"])
+    assert rs.capture_rules == frozenset({920420, 920480, 942, 943})
+    cts = [b"application/json; charset=utf-8", b"text/xml;charset=UTF-16", b"multipart/form-data; boundary=x",
+           b"application/x-www-form-urlencoded", b"text/plain; charset = 'latin1'", b";charset=", b"",
+           b"APPLICATION/JSON", b"x/y; charset=\"utf-8\"; a=b"]
+    txs = []
+    gen = traffic.TrafficGen(traffic.SEED + 7).batch(400, attack_rate=0.3)
+    for i in range(gen.n_req):
+        t = gen.request(i)
+        t.headers = [(k, v) for k, v in t.headers if k.lower() != b"content-type"]
+        if i % 3:
+            t.add_request_header("Content-Type", cts[i % len(cts)])
+        if i % 5 == 0:
+            t.uri += b"&q=Union+Select+pass%20word&Q1=x"
+        txs.append(t)
+    batch = gpuinspect.pack(txs)
+    eng = gpuinspect.Engine(rs, matched_cap=64, capture_cap=16, capture_bytes_cap=1024)
+    res = eng.inspect(batch)
+    cfg = coraza.parse_seclang(CAPTURE_RULES)
+    orc = compare.oracle_verdicts(cfg, batch, rs.exports)
+    bad = compare.compare(res, orc)
+    assert not bad, bad
+    ncap = int(res.verdicts["capture_cnt"].sum())
+    assert ncap > 300, ncap
+    assert any(res.captures(i) and res.captures(i)[0][0] == 942 for i in range(batch.n_req))

@@ -93,31 +93,81 @@ def test_capture_without_reader_compiles():
 
 
 CAPTURE_READ = [
-    # a chained link reads the captured value (CRS 920420-style)
-    'SecRule REQUEST_HEADERS:Content-Type "@rx ^([^;]+)" "id:1,phase:1,deny,capture,chain"\n'
-    'SecRule TX:1 "!@within text/plain" ""',
-    # a macro in an operator argument / setvar reads it
-    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture,setvar:tx.seen=%{tx.1}"',
-    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule ARGS "@streq %{TX.0}" "id:2,phase:2,deny"',
-    # whole-collection / regex-keyed TX targets can see TX.0
-    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule TX "@rx aa" "id:2,phase:2,deny"',
-    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule TX:/^[0-9]$/ "@rx aa" "id:2,phase:2,deny"',
-    'SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule &TX:0 "@eq 1" "id:2,phase:2,deny"',
+    # a chained link reads the captured value (CRS 920420 / 920480 style): fed in chain
+    ('SecRule REQUEST_HEADERS:Content-Type "@rx ^([^;]+)" "id:1,phase:1,deny,capture,chain"\n'
+     'SecRule TX:1 "!@within text/plain" ""', False),
+    # the capturing rule's own setvar reads it (its captures precede its actions)
+    ('SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture,setvar:tx.seen=%{tx.1}"', False),
+    # a later rule reads it: every capture of the program is observable
+    ('SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule ARGS "@streq %{TX.0}" "id:2,phase:2,deny"', True),
+    # whole-collection / regex-keyed / counted TX targets can see TX.0
+    ('SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule TX "@rx aa" "id:2,phase:2,deny"', True),
+    ('SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule TX:/^[0-9]$/ "@rx aa" "id:2,phase:2,deny"', True),
+    ('SecRule ARGS "@rx (a+)" "id:1,phase:2,pass,capture"\nSecRule &TX:0 "@eq 1" "id:2,phase:2,deny"', True),
 ]
 
 
-@pytest.mark.parametrize("text", CAPTURE_READ)
-def test_capture_with_reader_is_unsupported(text):
+@pytest.mark.parametrize("text,glob", CAPTURE_READ)
+def test_capture_with_reader_compiles(text, glob):
+    """Observable captures compile to a device submatch program (pike.h); the
+    plan lists the rules whose captures are recorded."""
     coraza.parse_seclang(text)  # valid SecLang
+    rs = gpuinspect.Ruleset(text)
+    assert 1 in rs.capture_rules
+
+
+def test_capture_analysis_keeps_logdata_captures_dropped():
+    """A 920420-style chain makes only its own capture observable: the CRS
+    detection rules' logdata captures stay dropped."""
+    text = (CAPTURE_LOGDATA + 'SecRule REQUEST_HEADERS:Content-Type "@rx ^[^;\\s]+" '
+            '"id:920420,phase:1,pass,capture,setvar:\'tx.ct=|%{tx.0}|\',chain"\n'
+            'SecRule TX:ct "!@within |text/plain|" "setvar:tx.score=+5"\n')
+    rs = gpuinspect.Ruleset(text)
+    assert rs.capture_rules == frozenset({920420})
+    # with a reader outside any chain every capture is observable
+    rs2 = gpuinspect.Ruleset(text + 'SecRule TX:0 "@rx x" "id:9,phase:2,pass"\n')
+    assert rs2.capture_rules == frozenset({1, 920420})
+
+
+def test_capture_observable_on_pm_is_unsupported():
+    text = 'SecRule ARGS "@pm foo bar" "id:1,phase:2,pass,capture"\nSecRule TX:0 "@rx foo" "id:2,phase:2,deny"'
+    coraza.parse_seclang(text)
     with pytest.raises(gpuinspect.SecLangError) as e:
         gpuinspect.Ruleset(text)
     assert e.value.code == gpuinspect.GI_EUNSUPPORTED
 
 
-def test_capture_exported_is_unsupported():
-    with pytest.raises(gpuinspect.SecLangError) as e:
-        gpuinspect.Ruleset(CAPTURE_LOGDATA, tx_exports=["score", "0"])
-    assert e.value.code == gpuinspect.GI_EUNSUPPORTED
+def test_capture_exported_compiles():
+    rs = gpuinspect.Ruleset(CAPTURE_LOGDATA, tx_exports=["score", "0"])
+    assert rs.capture_rules == frozenset({1})
+
+
+CAPTURE_PATTERNS = [
+    r"^[^;\s]+", r"charset\s*=\s*[\"']?([^;\"'\s]+)", r"(a+?)(b*)", r"(a|ab)(c|bcd)(d*)", r"((a)|b)+",
+    r"(?i)(k)(s)?", r"\b(\w+)\b", r"^(.*)$", r"(x)?(y)?z", r"(a{2,3})(a*)", r"(?:(\d+)-)+(\d+)",
+    r"(?i:(select|union)\s+(all\s+)?(\w+))", r"(<)(script|img)([^>]*)(>?)", r"([^\x00-\x7f]+)(.)",
+    r"(a*?)(a*?)b", r"(.)(.)(.)(.)(.)(.)(.)(.)(.)(.)(.)", r"(?m)^(ab|cd)$",
+]
+
+
+@pytest.mark.parametrize("pat", CAPTURE_PATTERNS)
+def test_capture_vm_matches_oracle(pat):
+    """The submatch VM k_eval runs (pike.h, here on the host) against the
+    oracle's FindStringSubmatch restatement on random strings: the match and
+    every group 0..8."""
+    rnd = random.Random(hash(pat) & 0xFFFF)
+    alpha = b"aabbcdxyzkKsS select union all 09-<>script img\n;='\"\xc3\xa9\xe2\x84\xaa\xff"
+    g = goregex.compile_go("(?sm)" + pat)
+    for _ in range(400):
+        s = bytes(rnd.choice(alpha) for _ in range(rnd.randint(0, 24)))
+        got = gpuinspect.selftest_capture(pat, s)
+        exp = g.find_string_submatch(s)
+        if exp is None:
+            assert got is None, (pat, s, got)
+            continue
+        assert got is not None, (pat, s, exp)
+        vals = [s[a:b] if x else b"" for x in got for a, b in [x or (0, 0)]]
+        assert vals == exp[:9], (pat, s, vals, exp)
 
 
 PMF_RULES = """SecRuleEngine On
