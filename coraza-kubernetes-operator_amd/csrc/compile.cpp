@@ -1280,10 +1280,10 @@ struct Lower {
   uint32_t n_det = 0;  // streams with detect vals (DStream.det_id)
   std::map<std::string, size_t> sindex;
 
-  // body collections phase A does not scan (XML stays empty: its processor is not implemented)
+  // body collections phase A does not scan (multipart, XML): tested by k_eval on a clear bit
   static bool residual_collection(const std::string& n) {
     return n == "FILES" || n == "FILES_NAMES" || n == "FILES_SIZES" || n == "FILES_TMPNAMES" ||
-           n == "MULTIPART_PART_HEADERS";
+           n == "MULTIPART_PART_HEADERS" || n == "XML";
   }
   static bool immutable_single(int sid) {
     return sid == S_REQUEST_METHOD || sid == S_REQUEST_PROTOCOL || sid == S_REQUEST_URI ||
@@ -1336,7 +1336,7 @@ struct Lower {
       DVarRef& vr = vrs[vi];
       if ((vr.var < S_COUNT && !immutable_single(vr.var)) || vr.var == V_FILES ||
           vr.var == V_FILES_NAMES || vr.var == V_FILES_SIZES || vr.var == V_FILES_TMPNAMES ||
-          vr.var == V_MULTIPART_PART_HEADERS) {
+          vr.var == V_MULTIPART_PART_HEADERS || vr.var == V_XML) {
         vr.residual = 1;
         continue;
       }
@@ -1360,7 +1360,7 @@ struct Lower {
           case V_ARGS_NAMES: mask = (1 << FK_ARG_GET) | (1 << FK_ARG_POST); names = true; break;
           case V_REQUEST_HEADERS_NAMES: mask = 1 << FK_HEADER; names = true; break;
           case V_REQUEST_COOKIES_NAMES: mask = 1 << FK_COOKIE; names = true; break;
-          default: break;  // XML, FILES*: no phase-A values (their processors are not implemented)
+          default: break;  // XML, FILES*: residual (above)
         }
         if (!mask) continue;
         f.kind_mask = mask;

@@ -81,7 +81,7 @@ enum VarId : uint8_t {
   V_ARGS_NAMES,
   V_REQUEST_HEADERS_NAMES,
   V_REQUEST_COOKIES_NAMES,
-  V_XML,  // XML body processor output: never populated (XML bodies are flagged unsupported)
+  V_XML,  // XML body processor output (kernels.hip parse_xml): FK_XML fields
   // MULTIPART body processor output (kernels.hip parse_multipart)
   V_FILES,                   // ("", file name) per file part
   V_FILES_NAMES,             // ("", part name) per file part
@@ -102,7 +102,9 @@ enum FieldKind : uint8_t {
   FK_ARG_GET = 1, FK_ARG_POST = 2, FK_HEADER = 3, FK_COOKIE = 4,
   // multipart collections (after the phase-1 fields, among the ARGS_POST ones;
   // never phase-A items)
-  FK_FILE = 5, FK_FILE_NAME = 6, FK_FILE_SIZE = 7, FK_PART_HEADER = 8
+  FK_FILE = 5, FK_FILE_NAME = 6, FK_FILE_SIZE = 7, FK_PART_HEADER = 8,
+  // XML body processor output: key "//@*" (attribute values) or "/*" (text)
+  FK_XML = 9
 };
 
 // ------------------------------------------------------------- operators

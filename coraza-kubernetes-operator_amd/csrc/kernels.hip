@@ -17,6 +17,7 @@
 #include <cstdio>
 
 #include "gi_kernels.h"
+#include "html_entities.h"
 #include "libinj.h"
 
 namespace gi {
@@ -43,7 +44,7 @@ struct Slot {
 };
 
 __device__ __constant__ uint8_t kConstStrs[] =
-    "0\0URLENCODED\0JSON\0XML\0MULTIPART\0" "1\0JSON: invalid JSON\0\0\0\0\0\0\0\0";  // padded for load_u32u
+    "0\0URLENCODED\0JSON\0XML\0MULTIPART\0" "1\0JSON: invalid JSON\0" "//@*\0/*\0\0\0\0\0\0\0\0";  // padded for load_u32u
 #define CS_ZERO (kConstStrs + 0)
 #define CS_URLENCODED (kConstStrs + 2)
 #define CS_JSON (kConstStrs + 13)
@@ -51,6 +52,8 @@ __device__ __constant__ uint8_t kConstStrs[] =
 #define CS_MULTIPART (kConstStrs + 22)
 #define CS_ONE (kConstStrs + 32)
 #define CS_JSON_ERR (kConstStrs + 34)
+#define CS_XML_ATTRS (kConstStrs + 53)  // XML collection keys (xml.go: "//@*" attribute values, "/*" text)
+#define CS_XML_TEXT (kConstStrs + 58)
 
 __device__ inline bool ishex(uint8_t c) {
   return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
@@ -2176,6 +2179,721 @@ __device__ __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t
   }
 }
 
+// ------------------------------------------------------------ XML body
+// [upstream coraza internal/bodyprocessors/xml.go readXML over Go's
+// encoding/xml Decoder, Strict = false, AutoClose = HTMLAutoClose, Entity =
+// HTMLEntity]; oracle/xmlbody.py states the same paths.  Output fields
+// (FK_XML): key "//@*" for every attribute value of every start element,
+// then key "/*" for every strings.TrimSpace'd non-empty character-data token,
+// each in document order.  A decoder error -> no fields, *msg = "XML: " +
+// err.Error() in the arena, return 1.  Non-ASCII XML names (Go's XML name
+// range tables) -> GI_REQ_UNSUPPORTED_BODY.  ws: cap words of scratch for the
+// element stack and the text list.
+struct XName {
+  uint32_t so, sn, lo, ln;  // prefix [so, so + sn) and local part [lo, lo + ln) in the body
+};
+
+__device__ inline bool xml_name_byte(uint8_t c) {
+  return (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '_' || c == ':' ||
+         c == '.' || c == '-';
+}
+__device__ inline bool xml_in_range(uint32_t r) {
+  return r == 0x09 || r == 0x0A || r == 0x0D || (r >= 0x20 && r <= 0xD7FF) || (r >= 0xE000 && r <= 0xFFFD) ||
+         (r >= 0x10000 && r <= 0x10FFFF);
+}
+__device__ inline bool go_is_space(uint32_t r) {  // unicode.IsSpace
+  return r == 0x09 || r == 0x0A || r == 0x0B || r == 0x0C || r == 0x0D || r == 0x20 || r == 0x85 || r == 0xA0 ||
+         r == 0x1680 || (r >= 0x2000 && r <= 0x200A) || r == 0x2028 || r == 0x2029 || r == 0x202F || r == 0x205F ||
+         r == 0x3000;
+}
+// HTML 4.01 entity by name (sorted table): code point or -1
+__device__ int32_t html_entity(const uint8_t* nm, uint32_t n) {
+  uint32_t lo = 0, hi = GI_N_HTML_ENT;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint8_t* e = (const uint8_t*)kHtmlEntPool + kHtmlEnt[mid][0];
+    const uint32_t en = kHtmlEnt[mid][1];
+    int c = 0;
+    for (uint32_t k = 0; k < en && k < n && !c; k++) c = (int)e[k] - (int)nm[k];
+    if (!c) c = (int)en - (int)n;
+    if (c == 0) return (int32_t)kHtmlEnt[mid][2];
+    if (c < 0) lo = mid + 1;
+    else hi = mid;
+  }
+  return -1;
+}
+
+template <class C>
+struct XmlDec {
+  C& t;
+  const uint8_t* s;
+  uint32_t n, i, line;
+  int err;          // 0 none, 1 decoder error (msg set), 2 unsupported, 3 arena overflow
+  uint32_t mo, ml;  // error message in the arena
+  __device__ XmlDec(C& tt, const uint8_t* ss, uint32_t nn) : t(tt), s(ss), n(nn), i(0), line(1), err(0), mo(0), ml(0) {}
+  __device__ int getc() {
+    if (i >= n) return -1;
+    const uint8_t b = s[i++];
+    if (b == '\n') line++;
+    return b;
+  }
+  __device__ void ungetc(int b) {
+    if (b == '\n') line--;
+    i--;
+  }
+  // message pieces
+  __device__ void put(const char* p) {
+    for (; *p && err != 3; p++) putb((uint8_t)*p);
+  }
+  __device__ void putb(uint8_t b) {
+    if (t.nb + 1 > t.cap_b) {
+      err = 3;
+      return;
+    }
+    t.bytes[t.nb++] = b;
+    ml++;
+  }
+  __device__ void putn(const uint8_t* p, uint32_t k) {
+    for (uint32_t q = 0; q < k; q++) putb(p[q]);
+  }
+  __device__ void putu(uint32_t v) {
+    uint8_t b[12];
+    const uint32_t k = go_itoa((int64_t)v, b);
+    putn(b, k);
+  }
+  __device__ void begin_msg(bool syntax) {
+    err = 1;
+    mo = t.nb;
+    ml = 0;
+    put("XML: ");
+    if (syntax) {
+      put("XML syntax error on line ");
+      putu(line);
+      put(": ");
+    }
+  }
+  __device__ void syntax(const char* m) {
+    begin_msg(true);
+    put(m);
+  }
+  __device__ int mustgetc() {
+    const int b = getc();
+    if (b < 0) syntax("unexpected EOF");
+    return b;
+  }
+  __device__ void space() {
+    for (;;) {
+      const int b = getc();
+      if (b < 0) return;
+      if (b != ' ' && b != '\r' && b != '\n' && b != '\t') {
+        ungetc(b);
+        return;
+      }
+    }
+  }
+  // readName over the body: [*a, *e); false (nothing read) or err
+  __device__ bool read_name(uint32_t* a, uint32_t* e) {
+    int b = mustgetc();
+    if (b < 0) return false;
+    if (b < 0x80 && !xml_name_byte((uint8_t)b)) {
+      ungetc(b);
+      return false;
+    }
+    *a = i - 1;
+    for (;;) {
+      b = mustgetc();
+      if (b < 0) return false;
+      if (b < 0x80 && !xml_name_byte((uint8_t)b)) {
+        ungetc(b);
+        break;
+      }
+    }
+    *e = i;
+    return true;
+  }
+  // isName for a name read by read_name (err 2 when it has non-ASCII bytes)
+  __device__ bool is_name(uint32_t a, uint32_t e) {
+    if (e == a) return false;
+    for (uint32_t k = a; k < e; k++)
+      if (s[k] >= 0x80) {
+        err = 2;
+        return false;
+      }
+    const uint8_t c = s[a];
+    return (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_' || c == ':';
+  }
+  // name(): false without a name (err unset) or on error
+  __device__ bool name(uint32_t* a, uint32_t* e) {
+    if (!read_name(a, e)) return false;
+    if (!is_name(*a, *e)) {
+      if (err == 2) return false;
+      begin_msg(true);
+      put("invalid XML name: ");
+      putn(s + *a, *e - *a);
+      return false;
+    }
+    return true;
+  }
+  __device__ bool nsname(XName* x) {
+    uint32_t a, e;
+    if (!name(&a, &e)) return false;
+    uint32_t colons = 0, c = e;
+    for (uint32_t k = a; k < e; k++)
+      if (s[k] == ':') {
+        if (!colons) c = k;
+        colons++;
+      }
+    if (colons > 1) return false;
+    if (!colons || c == a || c + 1 == e) {
+      *x = {a, 0, a, e - a};
+    } else {
+      *x = {a, c - a, c + 1, e - c - 1};
+    }
+    return true;
+  }
+  // text(quote, cdata): the decoded bytes appended to the arena at *o (length
+  // *len); false on error.  Decoded text is never longer than its input.
+  __device__ bool text(int quote, bool cdata, uint32_t* o, uint32_t* len) {
+    uint8_t b0 = 0, b1 = 0;
+    uint32_t trunc = 0;
+    const uint32_t start = t.nb;
+    auto wr = [&](uint8_t c) {
+      if (t.nb + 1 > t.cap_b) {
+        err = 3;
+        return false;
+      }
+      t.bytes[t.nb++] = c;
+      return true;
+    };
+    for (;;) {
+      int b = getc();
+      if (b < 0) {
+        if (cdata) {
+          syntax("unexpected EOF in CDATA section");
+          return false;
+        }
+        break;
+      }
+      if (quote < 0 && b0 == ']' && b1 == ']' && b == '>') {
+        if (cdata) {
+          trunc = 2;
+          break;
+        }
+        syntax("unescaped ]]> not in CDATA section");
+        return false;
+      }
+      if (b == '<' && !cdata) {
+        if (quote >= 0) {
+          syntax("unescaped < inside quoted string");
+          return false;
+        }
+        ungetc(b);
+        break;
+      }
+      if (quote >= 0 && b == quote) break;
+      if (b == '&' && !cdata) {
+        const uint32_t before = t.nb;
+        if (!wr('&')) return false;
+        int32_t cp = -1;
+        b = mustgetc();
+        if (b < 0) return false;
+        if (b == '#') {
+          if (!wr('#')) return false;
+          b = mustgetc();
+          if (b < 0) return false;
+          uint32_t base = 10;
+          if (b == 'x') {
+            base = 16;
+            if (!wr('x')) return false;
+            b = mustgetc();
+            if (b < 0) return false;
+          }
+          const uint32_t dstart = t.nb;
+          uint64_t v = 0;
+          bool big = false;
+          while ((b >= '0' && b <= '9') || (base == 16 && ((b >= 'a' && b <= 'f') || (b >= 'A' && b <= 'F')))) {
+            if (!wr((uint8_t)b)) return false;
+            const uint32_t dv = b <= '9' ? b - '0' : ((b | 0x20) - 'a' + 10);
+            if (v > 0x10FFFFull) big = true;
+            else v = v * base + dv;
+            b = mustgetc();
+            if (b < 0) return false;
+          }
+          if (b != ';') {
+            ungetc(b);
+          } else {
+            if (!wr(';')) return false;
+            if (t.nb - 1 > dstart && !big && v <= 0x10FFFF) cp = (v >= 0xD800 && v <= 0xDFFF) ? 0xFFFD : (int32_t)v;
+          }
+        } else {
+          ungetc(b);
+          uint32_t a, e;
+          const bool got = read_name(&a, &e);
+          if (err) return false;
+          if (got)
+            for (uint32_t k = a; k < e; k++)
+              if (!wr(s[k])) return false;
+          b = mustgetc();
+          if (b < 0) return false;
+          if (b != ';') {
+            ungetc(b);
+          } else {
+            const uint8_t* nm = t.bytes + before + 1;
+            const uint32_t nn = t.nb - before - 1;
+            if (!wr(';')) return false;
+            bool ascii = nn > 0;
+            for (uint32_t k = 0; k < nn; k++) ascii &= nm[k] < 0x80;
+            const uint8_t c0 = nn ? nm[0] : 0;
+            if (ascii && ((c0 >= 'A' && c0 <= 'Z') || (c0 >= 'a' && c0 <= 'z') || c0 == '_' || c0 == ':')) {
+              if (nn == 2 && nm[0] == 'l' && nm[1] == 't') cp = '<';
+              else if (nn == 2 && nm[0] == 'g' && nm[1] == 't') cp = '>';
+              else if (nn == 3 && nm[0] == 'a' && nm[1] == 'm' && nm[2] == 'p') cp = '&';
+              else if (nn == 4 && nm[0] == 'a' && nm[1] == 'p' && nm[2] == 'o' && nm[3] == 's') cp = '\'';
+              else if (nn == 4 && nm[0] == 'q' && nm[1] == 'u' && nm[2] == 'o' && nm[3] == 't') cp = '"';
+              else cp = html_entity(nm, nn);
+            }
+          }
+        }
+        if (cp >= 0) {  // replace "&...;" by the rune
+          t.nb = before;
+          uint8_t enc[4];
+          const uint32_t k = encode_rune((uint32_t)cp, enc);
+          for (uint32_t q = 0; q < k; q++)
+            if (!wr(enc[q])) return false;
+        }
+        b0 = b1 = 0;
+        continue;  // non-strict: an unknown entity stays as written
+      }
+      if (b == '\r') {
+        if (!wr('\n')) return false;
+      } else if (!(b1 == '\r' && b == '\n')) {
+        if (!wr((uint8_t)b)) return false;
+      }
+      b0 = b1;
+      b1 = (uint8_t)b;
+    }
+    const uint32_t dn = t.nb - start - trunc;
+    t.nb -= trunc;
+    for (uint32_t k = 0; k < dn;) {  // disallowed characters
+      uint32_t w;
+      const uint32_t r = decode_rune(t.bytes + start, dn, k, &w);
+      if (r == 0xFFFD && w == 1) {
+        syntax("invalid UTF-8");
+        return false;
+      }
+      k += w;
+      if (!xml_in_range(r)) {
+        begin_msg(true);
+        put("illegal character code U+");
+        uint8_t hx[8];
+        uint32_t hn = 0;
+        for (int sh = 20; sh >= 0; sh -= 4) {
+          const uint32_t d = (r >> sh) & 15;
+          if (hn || d || sh < 16) hx[hn++] = (uint8_t)(d < 10 ? '0' + d : 'A' + d - 10);
+        }
+        putn(hx, hn);
+        return false;
+      }
+    }
+    *o = start;
+    *len = dn;
+    return true;
+  }
+  __device__ bool attrval(uint32_t* o, uint32_t* len) {
+    int b = mustgetc();
+    if (b < 0) return false;
+    if (b == '"' || b == '\'') return text(b, false, o, len);
+    ungetc(b);
+    const uint32_t a = i;
+    for (;;) {
+      b = mustgetc();
+      if (b < 0) return false;
+      if ((b >= 'a' && b <= 'z') || (b >= 'A' && b <= 'Z') || (b >= '0' && b <= '9') || b == '_' || b == ':' ||
+          b == '-')
+        continue;
+      ungetc(b);
+      break;
+    }
+    *o = 0xFFFFFFFFu;  // the value is s[a, i): in the body, not the arena
+    *len = i - a;
+    return true;
+  }
+};
+
+enum XTok : uint8_t { XT_NONE = 0, XT_START, XT_END, XT_CHARS, XT_OTHER };
+
+// encoding/xml procInst(param, s): the quoted value of param="..." in s
+__device__ bool xml_proc_inst(const uint8_t* s, uint32_t n, const char* param, uint32_t* vo, uint32_t* vn) {
+  uint32_t lp = 0;
+  while (param[lp]) lp++;  // includes the '='
+  uint32_t i = 0;
+  uint8_t sep = 0;
+  while (i < n) {
+    int64_t k = -1;
+    for (uint32_t q = i; q + lp <= n && k < 0; q++) {
+      bool eq = true;
+      for (uint32_t z = 0; z < lp && eq; z++) eq = s[q + z] == (uint8_t)param[z];
+      if (eq) k = q - i;
+    }
+    if (k < 0 || lp + (uint32_t)k >= n - i) return false;
+    const uint8_t c = s[i + lp + k];
+    i += lp + (uint32_t)k + 1;
+    if (c == '\'' || c == '"') {
+      sep = c;
+      break;
+    }
+  }
+  if (!sep) return false;
+  for (uint32_t j = i; j < n; j++)
+    if (s[j] == sep) {
+      *vo = i;
+      *vn = j - i;
+      return true;
+    }
+  return false;
+}
+
+__device__ inline bool xml_autoclose(const uint8_t* s, uint32_t lo, uint32_t ln) {
+  const char* names[13] = {"basefont", "br", "area", "link", "img", "param", "hr", "input", "col", "frame",
+                           "isindex", "base", "meta"};
+  for (int k = 0; k < 13; k++) {
+    uint32_t m = 0;
+    while (names[k][m]) m++;
+    if (m == ln && eq_ascii_ci(s + lo, ln, (const uint8_t*)names[k], m)) return true;
+  }
+  return false;
+}
+
+template <class C>
+__device__ __noinline__ int parse_xml(C& t, const uint8_t* s, uint32_t n, uint32_t* ws, uint32_t ws_words, Str* msg) {
+  XmlDec<C> d(t, s, n);
+  const uint32_t nf0 = t.nf, nb0 = t.nb;
+  // ws: element stack (XName, 4 words each) from the front, text list ((off, len) pairs) from the back
+  XName* stk = (XName*)ws;
+  uint32_t depth = 0, ntext = 0;
+  const uint32_t cap_items = ws_words / 4;  // stack entries + text pairs / 2 share the space
+  uint32_t* texts = ws + ws_words;          // grows down: texts[-2(k+1)], texts[-2(k+1)+1]
+  bool need_close = false, have_next = false;
+  XName to_close{}, next_name{};
+  uint8_t next_kind = XT_NONE;
+  auto fail_ret = [&]() -> int {
+    t.nf = nf0;
+    if (d.err == 1) {
+      *msg = {t.bytes + d.mo, d.ml};
+      return 1;
+    }
+    t.nb = nb0;
+    t.flags |= d.err == 2 ? GI_REQ_UNSUPPORTED_BODY : GI_REQ_OVERFLOW;
+    return 2;
+  };
+  for (;;) {
+    uint8_t kind = XT_NONE;
+    XName nm{};
+    if (have_next) {
+      kind = next_kind;
+      nm = next_name;
+      have_next = false;
+    } else {
+      // ---- rawToken
+      if (need_close) {
+        need_close = false;
+        kind = XT_END;
+        nm = to_close;
+      } else {
+        int b = d.getc();
+        if (b < 0) {  // EOF
+          if (depth) {
+            d.syntax("unexpected EOF");
+            return fail_ret();
+          }
+          break;
+        }
+        if (b != '<') {
+          d.ungetc(b);
+          uint32_t o, len;
+          if (!d.text(-1, false, &o, &len)) return fail_ret();
+          kind = XT_CHARS;
+          nm = {o, len, 0, 0};
+        } else {
+          b = d.mustgetc();
+          if (b < 0) return fail_ret();
+          if (b == '/') {
+            if (!d.nsname(&nm)) {
+              if (!d.err) d.syntax("expected element name after </");
+              return fail_ret();
+            }
+            d.space();
+            b = d.mustgetc();
+            if (b < 0) return fail_ret();
+            if (b != '>') {
+              d.begin_msg(true);
+              d.put("invalid characters between </");
+              d.putn(s + nm.lo, nm.ln);
+              d.put(" and >");
+              return fail_ret();
+            }
+            kind = XT_END;
+          } else if (b == '?') {
+            uint32_t ta, te;
+            if (!d.name(&ta, &te)) {
+              if (!d.err) d.syntax("expected target name after <?");
+              return fail_ret();
+            }
+            d.space();
+            const uint32_t c0 = d.i;
+            uint8_t p0 = 0;
+            for (;;) {
+              b = d.mustgetc();
+              if (b < 0) return fail_ret();
+              if (p0 == '?' && b == '>') break;
+              p0 = (uint8_t)b;
+            }
+            const uint32_t cn = d.i - 2 - c0;
+            if (te - ta == 3 && s[ta] == 'x' && s[ta + 1] == 'm' && s[ta + 2] == 'l') {
+              uint32_t vo, vn;
+              if (xml_proc_inst(s + c0, cn, "version=", &vo, &vn) && vn &&
+                  !(vn == 3 && s[c0 + vo] == '1' && s[c0 + vo + 1] == '.' && s[c0 + vo + 2] == '0')) {
+                d.begin_msg(false);
+                d.put("xml: unsupported version \"");
+                d.putn(s + c0 + vo, vn);
+                d.put("\"; only version 1.0 is supported");
+                return fail_ret();
+              }
+              if (xml_proc_inst(s + c0, cn, "encoding=", &vo, &vn) && vn &&
+                  !(vn == 5 && eq_ascii_ci(s + c0 + vo, 5, (const uint8_t*)"utf-8", 5))) {
+                d.begin_msg(false);
+                d.put("xml: encoding \"");
+                d.putn(s + c0 + vo, vn);
+                d.put("\" declared but Decoder.CharsetReader is nil");
+                return fail_ret();
+              }
+            }
+            kind = XT_OTHER;
+          } else if (b == '!') {
+            b = d.mustgetc();
+            if (b < 0) return fail_ret();
+            if (b == '-') {
+              b = d.mustgetc();
+              if (b < 0) return fail_ret();
+              if (b != '-') {
+                d.syntax("invalid sequence <!- not part of <!--");
+                return fail_ret();
+              }
+              uint8_t q0 = 0, q1 = 0;
+              for (;;) {
+                b = d.mustgetc();
+                if (b < 0) return fail_ret();
+                if (q0 == '-' && q1 == '-') {
+                  if (b != '>') {
+                    d.syntax("invalid sequence \"--\" not allowed in comments");
+                    return fail_ret();
+                  }
+                  break;
+                }
+                q0 = q1;
+                q1 = (uint8_t)b;
+              }
+              kind = XT_OTHER;
+            } else if (b == '[') {
+              const char* cd = "CDATA[";
+              for (int k = 0; k < 6; k++) {
+                b = d.mustgetc();
+                if (b < 0) return fail_ret();
+                if (b != cd[k]) {
+                  d.syntax("invalid <![ sequence");
+                  return fail_ret();
+                }
+              }
+              uint32_t o, len;
+              if (!d.text(-1, true, &o, &len)) return fail_ret();
+              kind = XT_CHARS;
+              nm = {o, len, 0, 0};
+            } else {  // a directive
+              uint8_t inq = 0;
+              int depth2 = 0;
+              for (;;) {
+                b = d.mustgetc();
+                if (b < 0) return fail_ret();
+                if (inq == 0 && b == '>' && depth2 == 0) break;
+                for (bool again = true; again;) {  // HandleB
+                  again = false;
+                  if (b == inq) {
+                    inq = 0;
+                  } else if (inq != 0) {
+                  } else if (b == '\'' || b == '"') {
+                    inq = (uint8_t)b;
+                  } else if (b == '>') {
+                    depth2--;
+                  } else if (b == '<') {
+                    const char* cm = "!--";
+                    for (int k = 0; k < 3; k++) {
+                      b = d.mustgetc();
+                      if (b < 0) return fail_ret();
+                      if (b != cm[k]) {
+                        depth2++;
+                        again = true;
+                        break;
+                      }
+                    }
+                    if (!again) {
+                      uint8_t q0 = 0, q1 = 0;
+                      for (;;) {
+                        b = d.mustgetc();
+                        if (b < 0) return fail_ret();
+                        if (q0 == '-' && q1 == '-' && b == '>') break;
+                        q0 = q1;
+                        q1 = (uint8_t)b;
+                      }
+                    }
+                  }
+                }
+              }
+              kind = XT_OTHER;
+            }
+          } else {  // an open element
+            d.ungetc(b);
+            if (!d.nsname(&nm)) {
+              if (!d.err) d.syntax("expected element name after <");
+              return fail_ret();
+            }
+            bool empty = false;
+            for (;;) {
+              d.space();
+              b = d.mustgetc();
+              if (b < 0) return fail_ret();
+              if (b == '/') {
+                empty = true;
+                b = d.mustgetc();
+                if (b < 0) return fail_ret();
+                if (b != '>') {
+                  d.syntax("expected /> in element");
+                  return fail_ret();
+                }
+                break;
+              }
+              if (b == '>') break;
+              d.ungetc(b);
+              XName an;
+              if (!d.nsname(&an)) {
+                if (!d.err) d.syntax("expected attribute name in element");
+                return fail_ret();
+              }
+              d.space();
+              b = d.mustgetc();
+              if (b < 0) return fail_ret();
+              const uint8_t* vp;
+              uint32_t vn;
+              if (b != '=') {  // non-strict: the value is the name's local part
+                d.ungetc(b);
+                vp = s + an.lo;
+                vn = an.ln;
+              } else {
+                d.space();
+                uint32_t o, len;
+                if (!d.attrval(&o, &len)) return fail_ret();
+                vp = o == 0xFFFFFFFFu ? s + d.i - len : t.bytes + o;
+                vn = len;
+              }
+              add_field(t, FK_XML, CS_XML_ATTRS, 4, vp, vn);
+              if (t.flags & GI_REQ_ERROR_MASK) {
+                d.err = 3;
+                return fail_ret();
+              }
+            }
+            if (empty) {
+              need_close = true;
+              to_close = nm;
+            }
+            kind = XT_START;
+          }
+        }
+      }
+    }
+    // ---- Token(): autoClose, element stack
+    if (depth && xml_autoclose(s, stk[depth - 1].lo, stk[depth - 1].ln)) {
+      const XName& top = stk[depth - 1];
+      if (!(kind == XT_END && nm.ln == top.ln && eq_ascii_ci_both(s + nm.lo, s + top.lo, top.ln))) {
+        have_next = true;
+        next_kind = kind;
+        next_name = nm;
+        kind = XT_END;
+        nm = top;
+      }
+    }
+    if (kind == XT_START) {
+      if (depth >= cap_items || 4ull * (depth + 1) + 2ull * ntext > ws_words) {
+        d.err = 3;
+        return fail_ret();
+      }
+      stk[depth++] = nm;
+    } else if (kind == XT_END) {
+      if (!depth) {
+        d.begin_msg(true);
+        d.put("unexpected end element </");
+        d.putn(s + nm.lo, nm.ln);
+        d.put(">");
+        return fail_ret();
+      }
+      const XName top = stk[--depth];
+      if (!(top.ln == nm.ln && bytes_equal(s + top.lo, s + nm.lo, nm.ln))) {
+        need_close = true;
+        to_close = nm;
+      } else if (!(top.sn == nm.sn && bytes_equal(s + top.so, s + nm.so, nm.sn))) {
+        d.begin_msg(true);
+        d.put("element <");
+        d.putn(s + top.lo, top.ln);
+        d.put("> in space ");
+        d.putn(s + top.so, top.sn);
+        d.put(" closed by </");
+        d.putn(s + nm.lo, nm.ln);
+        d.put("> in space ");
+        if (nm.sn) d.putn(s + nm.so, nm.sn);
+        else d.put("\"\"");
+        return fail_ret();
+      }
+    } else if (kind == XT_CHARS) {  // strings.TrimSpace; keep a non-empty text for the "/*" list
+      const uint8_t* p = t.bytes + nm.so;
+      uint32_t a = 0, e = nm.sn;
+      while (a < e) {
+        uint32_t w;
+        const uint32_t r = decode_rune(p, e, a, &w);
+        if ((r == 0xFFFD && w == 1) || !go_is_space(r)) break;
+        a += w;
+      }
+      while (e > a) {
+        uint32_t k = e - 1;
+        while (k > a && e - k < 4 && (p[k] & 0xC0) == 0x80) k--;
+        uint32_t w;
+        uint32_t r = decode_rune(p, e, k, &w);
+        if (k + w != e) {
+          k = e - 1;
+          r = 0xFFFD;
+          w = 1;
+        }
+        if ((r == 0xFFFD && w == 1) || !go_is_space(r)) break;
+        e = k;
+      }
+      if (e > a) {
+        if (4ull * depth + 2ull * (ntext + 1) > ws_words) {
+          d.err = 3;
+          return fail_ret();
+        }
+        ntext++;
+        texts[-2 * (int64_t)ntext] = nm.so + a;
+        texts[-2 * (int64_t)ntext + 1] = e - a;
+      }
+    }
+  }
+  for (uint32_t k = 1; k <= ntext; k++) {
+    add_field(t, FK_XML, CS_XML_TEXT, 2, t.bytes + texts[-2 * (int64_t)k], texts[-2 * (int64_t)k + 1]);
+    if (t.flags & GI_REQ_ERROR_MASK) {
+      d.err = 3;
+      return fail_ret();
+    }
+  }
+  return 0;
+}
+
 // net/url shouldEscape(c, encodePath)
 __device__ inline bool should_escape_path(uint8_t c) {
   if (isalnum_(c)) return false;
@@ -2951,6 +3669,7 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
     case V_FILES_NAMES: return kind == FK_FILE_NAME;
     case V_FILES_SIZES: return kind == FK_FILE_SIZE;
     case V_MULTIPART_PART_HEADERS: return kind == FK_PART_HEADER;
+    case V_XML: return kind == FK_XML;
   }
   return false;
 }
@@ -5362,25 +6081,40 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
                 }
                 t.has_post = t.nf > nf0;
               }
-              for (uint32_t f = H->nf; f < t.nf; f++) t.n_mp += t.fields[f].kind >= FK_FILE ? 1u : 0u;
-              {  // list them (the residual clear-bit test of FILES* targets visits only these)
-                const uint32_t pad = (4u - (uint32_t)((uintptr_t)(t.bytes + t.nb) & 3u)) & 3u;
-                if (t.n_mp && (uint64_t)t.nb + pad + 4ull * t.n_mp <= t.cap_b) {
-                  uint32_t* l = (uint32_t*)(t.bytes + t.nb + pad);
-                  uint32_t k = 0;
-                  for (uint32_t f = H->nf; f < t.nf; f++)
-                    if (t.fields[f].kind >= FK_FILE) l[k++] = f;
-                  t.nb += pad + 4 * t.n_mp;
-                  t.mpl = l;
-                }
-              }
               if (err) {
                 t.single[S_MULTIPART_STRICT_ERROR] = {CS_ONE, 1};
                 t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
                 t.single[S_REQBODY_ERROR_MSG] = mp_err_msg(err);
               }
+            } else if (t.body_proc == BP_XML) {
+              // [upstream xml.go]: XML "//@*" / "/*", no REQUEST_BODY; an error ->
+              // generateRequestBodyError (REQBODY_ERROR_MSG "XML: <error>")
+              JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
+              Str msg{CS_ZERO, 0};
+              const int xr = parse_xml(jc, D + rq.body.off, bn, (uint32_t*)t.t0, t.cap_t / 4, &msg);
+              t.nf = jc.nf;
+              t.nb = jc.nb;
+              t.flags = jc.flags;
+              if (xr == 1) {
+                t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
+                t.single[S_REQBODY_ERROR_MSG] = msg;
+              }
             } else if (t.body_proc != BP_NONE) {
               t.flags |= GI_REQ_UNSUPPORTED_BODY;
+            }
+            if (t.body_proc == BP_MULTIPART || t.body_proc == BP_XML) {
+              // the body collections (FILES*, MULTIPART_PART_HEADERS, XML): the
+              // residual clear-bit test of their targets visits only these
+              for (uint32_t f = H->nf; f < t.nf; f++) t.n_mp += t.fields[f].kind >= FK_FILE ? 1u : 0u;
+              const uint32_t pad = (4u - (uint32_t)((uintptr_t)(t.bytes + t.nb) & 3u)) & 3u;
+              if (t.n_mp && (uint64_t)t.nb + pad + 4ull * t.n_mp <= t.cap_b) {
+                uint32_t* l = (uint32_t*)(t.bytes + t.nb + pad);
+                uint32_t k = 0;
+                for (uint32_t f = H->nf; f < t.nf; f++)
+                  if (t.fields[f].kind >= FK_FILE) l[k++] = f;
+                t.nb += pad + 4 * t.n_mp;
+                t.mpl = l;
+              }
             }
           }
         }

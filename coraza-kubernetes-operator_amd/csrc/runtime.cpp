@@ -578,6 +578,18 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
         nls += ch == '\n';
       }
       post_fields = std::min<uint64_t>(seps + 2, q.body.len / 2 + 2);
+      {  // XML (kernels.hip parse_xml): one field per attribute ('=' or a bare name) and text token
+        uint32_t k = 0;
+        while (k < q.body.len && (bd[k] == ' ' || bd[k] == '\t' || bd[k] == '\n' || bd[k] == '\r')) k++;
+        if (k < q.body.len && bd[k] == '<') {
+          uint64_t lt = 0, sp = 0;
+          for (uint32_t j = 0; j < q.body.len; j++) {
+            lt += bd[j] == '<';
+            sp += bd[j] == ' ' || bd[j] == '\t' || bd[j] == '\n' || bd[j] == '\r';
+          }
+          post_fields = std::max<uint64_t>(post_fields, 2 * lt + sp + 2);
+        }
+      }
       // multipart (kernels.hip parse_multipart): a part spends >= 2 lines on
       // its delimiter and header end and yields <= 3 entries + 1 per header line
       if (multipart) post_fields += nls + 8;
@@ -589,6 +601,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     // strings and unescaped parameters are each at most the part header
     // bytes; sizes 24 B per part
     if (multipart) cap_b += 4ull * q.body.len + 1024;
+    // XML (a ctl can pick it for any body): decoded texts <= the body, the error message
+    if (q.body.len) cap_b += q.body.len + 1024;
     {  // a JSON-looking body: room for the flattened "json.a.b" keys + parser stack
       const uint8_t* bd = in->data + q.body.off;
       uint32_t k = 0;

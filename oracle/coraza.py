@@ -36,7 +36,7 @@ import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
-from . import goregex, libinjection, multipart
+from . import goregex, libinjection, multipart, xmlbody
 
 # ---------------------------------------------------------------------------
 # Errors
@@ -73,8 +73,7 @@ MAP_VARS = {
     "REQUEST_COOKIES": (("REQUEST_COOKIES",), False),
     "TX": (("TX",), True),
     "MATCHED_VARS": (("MATCHED_VARS",), True),
-    # populated only by the XML body processor (not implemented: such
-    # requests are flagged unsupported), so always empty here
+    # the XML body processor's values (oracle/xmlbody.py): keys "//@*" and "/*"
     "XML": (("XML",), False),
     # multipart collections (oracle/multipart.py); keys: "" for FILES /
     # FILES_NAMES, the file name for FILES_SIZES, the part name for
@@ -2146,6 +2145,19 @@ class Transaction:
                     self.single["MULTIPART_STRICT_ERROR"] = b"1"
                     self.single["REQBODY_ERROR"] = b"1"
                     self.single["REQBODY_ERROR_MSG"] = b"MULTIPART: " + res["error"].encode()
+            elif rbp == b"XML":
+                # [upstream xml.go ProcessRequest] (oracle/xmlbody.py): XML
+                # "//@*" = attribute values, "/*" = trimmed character data;
+                # an error -> generateRequestBodyError, no XML values
+                try:
+                    attrs, content = xmlbody.read_xml(self.body)
+                except xmlbody.XmlUnsupported as e:
+                    raise UnsupportedInput("xml: %s" % e)
+                except xmlbody.XmlError as e:
+                    self.single["REQBODY_ERROR"] = b"1"
+                    self.single["REQBODY_ERROR_MSG"] = b"XML: " + str(e).encode("latin-1")
+                    attrs, content = [], []
+                self.maps["XML"] = [(b"//@*", v) for v in attrs] + [(b"/*", v) for v in content]
             elif rbp == b"":
                 pass
             else:

@@ -359,3 +359,102 @@ def test_gpu_capture_parity():
     ncap = int(res.verdicts["capture_cnt"].sum())
     assert ncap > 300, ncap
     assert any(res.captures(i) and res.captures(i)[0][0] == 942 for i in range(batch.n_req))
+
+
+XML_RULES = r"""SecRuleEngine On
+SecRequestBodyAccess On
+SecRule REQUEST_HEADERS:Content-Type "^(?:application(?:/soap\+|/)|text/)xml" "id:200000,phase:1,t:none,t:lowercase,pass,nolog,ctl:requestBodyProcessor=XML"
+SecRule REQBODY_ERROR "!@eq 0" "id:200002,phase:2,t:none,deny,status:400,msg:'%{reqbody_error_msg}'"
+SecRule XML:/* "@rx (?i)(union\s+select|<script)" "id:942,phase:2,pass,t:none,t:urlDecodeUni,setvar:tx.score=+5"
+SecRule XML://@* "@rx ^javascript:" "id:941,phase:2,pass,t:none,t:lowercase,setvar:tx.score=+5"
+SecRule XML "@contains evilmonkey" "id:3001,phase:2,pass,setvar:tx.score=+1"
+SecRule &XML:/* "@gt 3" "id:3002,phase:2,pass,setvar:tx.many=1"
+SecRule XML:/* "@detectSQLi" "id:942100,phase:2,pass,setvar:tx.score=+2"
+SecRule TX:SCORE "@ge 5" "id:949,phase:2,deny,status:403"
+"""
+
+XML_BODIES = [
+    b'<a href="x&amp;y" b=\'2\' disabled>hello <b>wor&lt;ld</b>  </a>',
+    b'<?xml version="1.0" encoding="UTF-8"?><r><![CDATA[ union select 1 ]]>t&#65;&#x42;&nbsp;&foo;</r>',
+    b'plain text evilmonkey', b'<a>unclosed', b'<a></b>', b'<x><a></b></x>', b'<br>text<p>x</p><img src="javascript:alert(1)">',
+    b'<?xml version="1.0" encoding="ISO-8859-1"?><a/>', b'<a b=c-d:e>&#0;</a>', b'1 < 2', b'<a>\r\nx\ry\r</a>',
+    b'<!DOCTYPE x [<!ENTITY e "v">]><x a="1">t</x>', b'<a><!-- c -- d --></a>', b'<p:a xmlns:p="u">t</p:a>',
+    b'<p:a></q:a>', b'\xef\xbb\xbf<a>x</a>', b'<a>\xff</a>', b'<q>1 UNION SELECT password FROM users</q>',
+    b'<a>&lt;script&gt;alert(1)&lt;/script&gt;</a>', b'<r><i>1</i><i>2</i><i>3</i><i>4</i><i>5</i></r>',
+    b'<a x="1\n2" y="&quot;z&quot;"/><b>\xc3\xa9t\xc3\xa9</b>', b'', b'<a>\n\t \xc2\xa0</a>', b'<![CDATA[x', b'<?xml version="2.0"?><a/>',
+    b'<a>t]]>u</a>', b'<a b="<">', b'<a =b>', b'<a:b:c/>', b'<a>&#xD800;&#x110000;&#65</a>',
+]
+
+
+def test_gpu_xml_body_parity():
+    """XML body processor (base rule 200000 -> ctl:requestBodyProcessor=XML):
+    XML:/* and XML://@* values and the decoder's errors (REQBODY_ERROR ->
+    200002 -> 400), against oracle/xmlbody.py."""
+    txs = []
+    for i, body in enumerate(XML_BODIES * 4):
+        t = gpuinspect.Transaction(method=b"POST", uri=b"/api?i=%d" % i)
+        t.add_request_header("Host", "x")
+        t.add_request_header("Content-Type", ["application/xml", "text/xml; charset=utf-8", "application/soap+xml",
+                                              "text/plain"][i % 4])
+        t.write_request_body(body)
+        txs.append(t)
+    res = _parity(XML_RULES, gpuinspect.pack(txs))
+    st = [res.interruption(i)["status"] if res.interruption(i) else 200 for i in range(len(txs))]
+    assert 400 in st and 403 in st and 200 in st
+
+
+BODY_LIMIT_RULES = """SecRuleEngine %s
+SecRequestBodyAccess On
+SecRequestBodyLimit 64
+SecRequestBodyLimitAction %s
+SecRule ARGS "@contains evil" "id:1,phase:2,pass,setvar:tx.score=+5"
+SecRule INBOUND_DATA_ERROR "@eq 1" "id:2,phase:2,pass,setvar:tx.limit=1"
+SecRule ARGS_COMBINED_SIZE "@gt 40" "id:3,phase:2,pass,setvar:tx.big=1"
+SecRule REQUEST_HEADERS:X "@rx ." "id:4,phase:1,pass,setvar:tx.p1=1"
+SecRule TX:SCORE "@ge 5" "id:9,phase:2,deny,status:403"
+"""
+
+
+@pytest.mark.parametrize("engine,action", [("On", "Reject"), ("On", "ProcessPartial"), ("DetectionOnly", "Reject")])
+def test_gpu_body_limit(engine, action):
+    """SecRequestBodyLimit: Reject -> 413 (no rule id, phase 1 matches kept),
+    ProcessPartial -> the first limit bytes, a body of exactly the limit, and
+    INBOUND_DATA_ERROR / ARGS_COMBINED_SIZE."""
+    text = BODY_LIMIT_RULES % (engine, action)
+    txs = []
+    for n in (0, 10, 63, 64, 65, 100, 500):
+        for evil_at in (0, 60):
+            body = bytearray(b"a=" + b"x" * max(0, n - 2))[:n]
+            if n >= evil_at + 7:
+                body[evil_at:evil_at + 7] = b"&q=evil"
+            t = gpuinspect.Transaction(method=b"POST", uri=b"/?g=1")
+            t.add_request_header("Content-Type", "application/x-www-form-urlencoded")
+            t.add_request_header("X", "1")
+            t.write_request_body(bytes(body))
+            txs.append(t)
+    rs = gpuinspect.Ruleset(text, tx_exports=["score", "limit", "big", "p1"])
+    eng = gpuinspect.Engine(rs)
+    batch = gpuinspect.pack(txs)
+    res = eng.inspect(batch)
+    orc = compare.oracle_verdicts(coraza.parse_seclang(text), batch, rs.exports)
+    bad = compare.compare(res, orc)
+    assert not bad, bad
+    if engine == "On" and action == "Reject":
+        assert any(res.interruption(i) == {"rule_id": 0, "status": 413, "action": "deny", "phase": 2}
+                   for i in range(len(txs)))
+
+
+def test_gpu_large_body_next_to_small():
+    """One 24 MB body among small requests stages and runs (bounded k_long
+    buffers: ADVICE r02) and every verdict matches the oracle."""
+    text = ("SecRuleEngine On\nSecRequestBodyAccess On\nSecRequestBodyLimit 134217728\n"
+            'SecRule ARGS|REQUEST_BODY "@rx evil[a-z]+monkey" "id:1,phase:2,deny,status:403,t:none,t:lowercase"\n')
+    big = b"a=" + b"x" * (24 << 20) + b"&b=EVILbigMONKEY"
+    txs = []
+    for i in range(64):
+        t = gpuinspect.Transaction(method=b"POST", uri=b"/?i=%d" % i)
+        t.add_request_header("Content-Type", "application/x-www-form-urlencoded")
+        t.write_request_body(big if i == 5 else b"q=evilsmallmonkey" if i % 7 == 0 else b"q=ok")
+        txs.append(t)
+    res = _parity(text, gpuinspect.pack(txs))
+    assert res.interruption(5) is not None and res.interruption(7) is not None and res.interruption(1) is None

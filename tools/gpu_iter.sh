@@ -14,7 +14,7 @@ if [ "${TESTS:-1}" = "1" ]; then
 fi
 for c in ${CONFIGS:-c2 c4 c3}; do
   step $c
-  ex="--no-cpu-baseline"; [ "$c" = "c2" ] && ex=""
+  ex="--no-cpu-baseline"; [ "$c" = "c2" ] && ex=""; [ "${PARITY_ALL:-0}" = "1" ] && ex=""
   GI_DIAG=1 timeout -k 10 400 python -u bench.py --config $c --steps ${STEPS:-3} --warmup 1 $ex ${ARGS:-} > gpurun_out/${TAG}_${c}_bench.json 2> gpurun_out/${TAG}_${c}.err || { tail -20 gpurun_out/${TAG}_${c}.err; exit 1; }
   grep GI_DIAG gpurun_out/${TAG}_${c}.err | tail -2
   python -c "import json; d=json.load(open('gpurun_out/${TAG}_${c}_bench.json')); print(d['value'], d['ms_per_step'], 'void', d['pa_void_requests'], 'parity', d.get('parity_sample',{}).get('mismatches'), {k: v['ms'] for k, v in d['roofline']['secondary']['launches'].items()})"
