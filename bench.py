@@ -79,16 +79,18 @@ def _oracle_worker(args):
     return time.perf_counter() - t0, out
 
 
-def oracle_sample(text, batch, exports, budget_s=15.0, procs=16, n_max=4000, files=None, calib=100):
+def oracle_sample(text, batch, exports, budget_s=15.0, procs=16, n_max=4000, files=None, calib=100, min_n=200):
     """The CPU oracle over a bounded sample of the batch: (verdicts by request
     index, wall seconds, processes).  Sized from a `calib`-request calibration
-    to about budget_s of wall time."""
+    to about budget_s of wall time, at least min(min_n, 2 x procs) requests."""
     blob = (batch.data, batch.reqs, batch.headers)
     calib = min(calib, batch.n_req)
     dt, _ = _oracle_worker((text, blob, range(calib), exports, files))
     per = dt / calib
+    log("oracle calibration: %.2f s per request" % per)
     procs = max(1, min(procs, os.cpu_count() or 1))
-    n_sample = int(min(n_max * procs, max(min(200, 2 * procs), budget_s * procs / max(per, 1e-6)), batch.n_req))
+    n_sample = int(min(n_max * procs, max(min(min_n, 2 * procs), budget_s * procs / max(per, 1e-6)), batch.n_req))
+    log("oracle sample: %d requests in %d processes" % (n_sample, procs))
     chunks = [range(k, n_sample, procs) for k in range(procs)]
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(procs) as pool:
@@ -225,10 +227,16 @@ def main():
     avg_kern_ms = float(np.mean(kern_ms))
     hbm_traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+    traffic_all = None
     if os.path.exists(tpath):  # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)
         tj = json.load(open(tpath))
-        if tj.get("kernel") == dom and tj.get("requests") == batch.n_req:
-            hbm_traffic = tj["hbm_bytes_per_launch"]
+        if tj.get("requests") == batch.n_req:
+            kt = tj.get("kernels", {})
+            rk = ROCPROF_NAMES.get(dom, dom)
+            if rk in kt:
+                hbm_traffic = kt[rk]["hbm_bytes_per_launch"]
+            traffic_all = {"source": "profiles/traffic_%s.json (%s)" % (args.config, tj.get("tag", "")),
+                           "hbm_bytes_per_launch": {k: v["hbm_bytes_per_launch"] for k, v in kt.items()}}
     steps_s = launch_steps.get(dom, 0) / (avg_launch[dom] * 1e-3)
     metric_set = {"c1": "config/samples RuleSet", "c2": "CRS-shaped v4 PL1 stand-in", "c3": "CRS-shaped v4 PL1 stand-in",
                   "c4": "CRS-shaped v4 PL4 stand-in", "c5": "generated 10k-rule set"}[args.config]
@@ -254,7 +262,7 @@ def main():
         "error_requests": int(tally["n_error"]),
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": hbm_traffic,
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": hbm_traffic, "traffic_by_kernel": traffic_all,
             "kernel": dom, "rocprof_kernel": ROCPROF_NAMES.get(dom, dom), "kernel_ms": round(avg_launch[dom], 4),
             "alg_bytes_per_launch": int(req_bytes),
             "alg_bytes_def": "SURVEY.md 8(d): sum of raw request bytes (method+uri+proto+headers+body, each "
@@ -266,8 +274,13 @@ def main():
                 "byte_steps_per_launch": int(launch_steps.get(dom, 0)), "byte_steps_per_s": round(steps_s, 1),
                 "queue_bytes_def": "bytes the launch itself must move once (DESIGN.md §4): item bytes + records "
                                    "in, transformed queue words out (k_stream); queue words in (k_scan)",
+                "byte_steps_def": "k_scan*: automaton transitions; k_stream*: value bytes fed into a stream's "
+                                  "transformation chain (value x streams reading it); k_detect: value bytes "
+                                  "through libinjection",
                 "launches": {k: {"ms": round(v, 4), "queue_bytes": int(launch_bytes[k]),
-                                 "GB/s": round(launch_bytes[k] / (v * 1e-3) / 1e9, 2) if v > 0 else None}
+                                 "GB/s": round(launch_bytes[k] / (v * 1e-3) / 1e9, 2) if v > 0 else None,
+                                 "byte_steps": int(launch_steps.get(k, 0)),
+                                 "byte_steps_per_s": round(launch_steps.get(k, 0) / (v * 1e-3), 1) if v > 0 else None}
                              for k, v in avg_launch.items()}},
         },
         "tally": {"n_req": int(node_tally["n_req"]), "n_interrupted": int(node_tally["n_interrupted"]),
@@ -306,7 +319,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline / parity sample (oracle)")
         verdicts, wall, procs = oracle_sample(text, batch, rs.exports, files=files,
-                                              calib=2 if args.config == "c5" else 100,
+                                              calib=1 if args.config == "c5" else 100,
+                                              min_n=16 if args.config == "c5" else 200,
                                               budget_s=30.0 if args.config == "c5" else 15.0)
         out["cpu_baseline"] = {
             "value": round(len(verdicts) / wall, 1), "unit": "requests/s", "cores": procs, "kind": "port",

@@ -1321,8 +1321,13 @@ struct Lower {
     // after every prefix of the chain: its patterns go into one stream per
     // prefix, all on the link's slot (the bit ORs the candidates: exact
     // superset).  The residual clear-bit path and k_body test final values
-    // only, so a multiMatch link with residual targets stays interpreter-only.
-    if (r.multimatch && residual) return -1;
+    // only, so a multiMatch link with a residual single stays interpreter-only;
+    // one whose residual targets are all body collections (XML, FILES*, part
+    // headers) keeps its phase-A bit: k_eval treats any present residual value
+    // as "maybe" and evaluates the whole link.
+    if (r.multimatch && residual)
+      for (auto& v : r.vars)
+        if (single_id(v.name) >= 0 && !immutable_single(single_id(v.name))) return -1;
     // a detect link reading REQUEST_BODY would go to k_body, which does not run libinjection: interpreter-only
     if ((n == "detectsqli" || n == "detectxss") && residual)
       for (auto& v : r.vars)

@@ -62,7 +62,10 @@ struct DBatch {
   unsigned long long* pool_used;
   uint2* qblk;                // [stream][qcap] queue blocks {word offset, nv | nw << 8}
   unsigned long long* acct;   // algorithmic-byte counters: [0..5) item bytes per bucket, [5..10) queue
-                              // words written per k_stream bucket, [10..13) queue words read per k_scan launch
+                              // words written per k_stream bucket, [10..13) queue words read per k_scan launch,
+                              // [13..16) automaton byte steps per k_scan launch
+  unsigned long long* acct2;  // byte steps: [0..5) value bytes into stream chains per k_stream bucket,
+                              // [5] value bytes through libinjection (k_detect)
   uint32_t qcap;
   void* slow;                 // SlowEnt[slow_cap]
   uint32_t* slow_count;

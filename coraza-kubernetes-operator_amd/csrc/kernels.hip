@@ -1284,8 +1284,7 @@ struct Tx {
     uint32_t var, koff, klen, _pad;
   }* rtgt;
   uint32_t nrtgt;
-  uint32_t n_mp;             // multipart collection entries (FILES*, MULTIPART_PART_HEADERS)
-  const uint32_t* mpl;       // their field indices (nullptr: not listed, scan all fields)
+  const uint32_t* kx;        // kind index (build_kindex; nullptr: scan all fields)
   uint32_t nremoved;
   uint8_t engine, body_access, body_proc, phase;
   uint8_t force_body;
@@ -3094,8 +3093,9 @@ __device__ int64_t slot_int(const Slot& s, bool* ok) {
 __device__ __forceinline__ Str single_val(Tx& t, uint32_t sid, uint8_t* buf) {
   if (sid == S_ARGS_COMBINED_SIZE) {
     uint64_t n = 0;
-    for (uint32_t f = 0; f < t.nf; f++) {
-      const Field& fl = t.fields[f];
+    const uint32_t j0 = t.kx ? t.kx[FK_ARG_GET] : 0u, j1 = t.kx ? t.kx[FK_ARG_POST + 1] : t.nf;
+    for (uint32_t j = j0; j < j1; j++) {
+      const Field& fl = t.fields[t.kx ? t.kx[12 + j] : j];
       if (fl.kind == FK_ARG_GET || fl.kind == FK_ARG_POST) n += (uint64_t)fl.kn + fl.vn;
     }
     return {buf, go_itoa((int64_t)n, buf)};
@@ -3674,6 +3674,47 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
   return false;
 }
 
+// The field kinds a collection reads (field_in), as the range [*lo, *hi]
+// (empty: *lo > *hi).  Every collection's kinds are contiguous.
+__device__ __forceinline__ void var_kinds(uint8_t var, uint32_t* lo, uint32_t* hi) {
+  uint32_t a = 1, b = 0;
+  switch (var) {
+    case V_ARGS_GET: case V_ARGS_GET_NAMES: a = b = FK_ARG_GET; break;
+    case V_ARGS_POST: case V_ARGS_POST_NAMES: a = b = FK_ARG_POST; break;
+    case V_ARGS: case V_ARGS_NAMES: a = FK_ARG_GET; b = FK_ARG_POST; break;
+    case V_REQUEST_HEADERS: case V_REQUEST_HEADERS_NAMES: a = b = FK_HEADER; break;
+    case V_REQUEST_COOKIES: case V_REQUEST_COOKIES_NAMES: a = b = FK_COOKIE; break;
+    case V_FILES: a = b = FK_FILE; break;
+    case V_FILES_NAMES: a = b = FK_FILE_NAME; break;
+    case V_FILES_SIZES: a = b = FK_FILE_SIZE; break;
+    case V_MULTIPART_PART_HEADERS: a = b = FK_PART_HEADER; break;
+    case V_XML: a = b = FK_XML; break;
+  }
+  *lo = a;
+  *hi = b;
+}
+
+// The fields grouped by kind, in the request arena: kx[k] is where kind k
+// starts in the list kx + 12 (kx[10]: its length), each kind in field
+// order.  A collection then visits only its own fields (in the order a scan
+// of all fields would: ARGS' two kinds are GET args, then POST args, and every
+// GET arg precedes every POST arg).  Rebuilt when a body parse adds fields;
+// an arena without room leaves kx null (scan every field).
+__device__ __noinline__ const uint32_t* build_kindex(const Field* fields, uint32_t nf, uint8_t* bytes, uint32_t* nb,
+                                                    uint32_t cap_b) {
+  const uint32_t pad = (4u - (uint32_t)((uintptr_t)(bytes + *nb) & 3u)) & 3u;
+  if ((uint64_t)*nb + pad + 4ull * (12ull + nf) > cap_b) return nullptr;
+  uint32_t* kx = (uint32_t*)(bytes + *nb + pad);
+  *nb += pad + 4u * (12u + nf);
+  for (uint32_t k = 0; k < 12; k++) kx[k] = 0;
+  for (uint32_t f = 0; f < nf; f++) kx[min((uint32_t)fields[f].kind, 9u) + 1]++;
+  for (uint32_t k = 1; k <= 10; k++) kx[k] += kx[k - 1];
+  for (uint32_t f = 0; f < nf; f++) kx[12 + kx[min((uint32_t)fields[f].kind, 9u)]++] = f;
+  for (uint32_t k = 10; k >= 1; k--) kx[k] = kx[k - 1];
+  kx[0] = 0;
+  return kx;
+}
+
 // Test one value: transform, operator, per-match actions.  Returns the number of matches.
 // multiMatch (coraza internal/corazawaf/rule.go executeTransformationsMultimatch):
 // the operator runs on the untransformed value and again after each
@@ -3764,13 +3805,23 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         const DVarRef vr = gi_cload(P.vars, R.var_begin + vi);
         if (!vr.residual) continue;
         if (vr.var == S_REQUEST_BODY && t.body_spec && R.phase >= 2) continue;  // k_body's bit
-        if (vr.var >= S_COUNT) {  // a body collection phase A never scans (multipart): test its entries
-          // (key filters ignored: a superset, the full evaluation below is exact)
-          const uint32_t nscan = t.mpl ? t.n_mp : (t.n_mp ? t.nf : 0u);
-          for (uint32_t k = 0; k < nscan && !any; k++) {
-            const Field fl = t.fields[t.mpl ? t.mpl[k] : k];
+        if (vr.var >= S_COUNT) {  // a body collection phase A never scans (multipart, XML): test its entries
+          // (key filters ignored: a superset, the full evaluation below is
+          // exact; multiMatch: any entry is a "maybe")
+          uint32_t klo, khi, j = 0, je = t.nf;
+          var_kinds(vr.var, &klo, &khi);
+          if (t.kx) {
+            j = klo <= khi ? t.kx[klo] : 0u;
+            je = klo <= khi ? t.kx[khi + 1] : 0u;
+          }
+          for (; j < je && !any; j++) {
+            const Field fl = t.fields[t.kx ? t.kx[12 + j] : j];
             bool names;
             if (!field_in(vr.var, fl.kind, &names)) continue;
+            if (R.flags & RF_MULTIMATCH) {
+              any = true;
+              continue;
+            }
             bool ok;
             const Str tv = transform(t, R, names ? fl.k : fl.v, names ? fl.kn : fl.vn, &ok);
             any = !ok || eval_op(t, o, tv.p, tv.n);
@@ -3895,7 +3946,18 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
                        slot_vexact(P, (uint32_t)R.hit_slot);
     const bool vexact = vskip && t.hset && !(R.flags & RF_MULTIMATCH);
     uint32_t cnt = 0;
-    for (uint32_t f = 0; f < t.nf; f++) {
+    uint32_t klo, khi, j = 0, je = t.nf;
+    var_kinds(vr.var, &klo, &khi);
+    if (t.kx) {  // only the collection's own fields
+      j = klo <= khi ? t.kx[klo] : 0u;
+      je = klo <= khi ? t.kx[khi + 1] : 0u;
+      if (vr.count && vr.key_mode == 0 && !vr.exc_count && !t.nrtgt) {  // &COLLECTION: the entry count
+        cnt = je - j;
+        j = je;
+      }
+    }
+    for (; j < je; j++) {
+      const uint32_t f = t.kx ? t.kx[12 + j] : j;
       const Field fl = t.fields[f];
       bool names;
       if (!field_in(vr.var, fl.kind, &names)) continue;
@@ -4192,6 +4254,16 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t* total) {
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
   for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+  return x;
+}
+
+// Sum over the wave's 64 lanes (every lane gets it).
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, o, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), o, 64);
+    x += ((uint64_t)hi << 32) | lo;
+  }
   return x;
 }
 
@@ -4952,6 +5024,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
   const uint32_t cap = IN ? WT : B.lcap;
   uint64_t pc_item = 0, pc_chain = 0, pc_out = 0, pc_loop = 0, pc_tot = 0, pc_fm = 0, pc_run = 0, pc_slow = 0;
   uint64_t wwords = 0;  // queue words this wave wrote (algorithmic-byte accounting)
+  uint64_t csteps = 0;  // value bytes this lane fed into a stream's chain (secondary roofline)
   const uint64_t pc_start = B.prof ? clock64() : 0;
   for (uint32_t w0 = blockIdx.x * 64; w0 < cnt; w0 += gridDim.x * 64) {
     const uint64_t c_a = B.prof ? clock64() : 0;
@@ -5008,6 +5081,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
       uint32_t osum = summ;  // byte summary of the chain output
       bool maybe = false, glob = !IN;
       if (fm) {
+        csteps += it.vn;
         cn = run_chain<IN != 0>(P, S, src, it.vn, summ, b0, b1, cap, &cur, sumlut, &osum);
         if (B.prof) pc_run += clock64() - c_sa;
         if (cn < 0 && IN) {
@@ -5134,6 +5208,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
     if (B.prof) pc_loop += clock64() - c_b;
   }
   if (lane == 0 && wwords) atomicAdd(&B.acct[5 + bucket], (unsigned long long)wwords);
+  csteps = wave_sum(csteps);
+  if (lane == 0 && csteps) atomicAdd(&B.acct2[bucket], (unsigned long long)csteps);
   if (B.prof && lane == 0) {
     pc_tot = clock64() - pc_start;
     atomicAdd(&B.prof[40 + 5 * bucket + 0], (unsigned long long)pc_item);
@@ -5844,6 +5920,7 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
   T.pool = lp;
   T.hash = lh;
   const uint32_t n = min(*B.det_count, B.det_cap);
+  uint64_t dsteps = 0;  // value bytes through libinjection (secondary roofline)
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const DetEnt x = ((const DetEnt*)B.det)[e];
     GI_BOUND(x.req < B.n_req && x.off + x.len <= B.det_bytes_cap, x.req, x.off);
@@ -5872,10 +5949,22 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
         if (sv.kind == OP_DETECT_SQLI) {
           // (k_stream listed the value for some val of the masked streams: the
           // other kind's prefilter may still settle it)
-          if (sq < 0) sq = li_candidate(true, v, x.len) && li_detect_sqli(v, x.len, &st[threadIdx.x], T) ? 1 : 0;
+          if (sq < 0) {
+            sq = 0;
+            if (li_candidate(true, v, x.len)) {
+              dsteps += x.len;
+              sq = li_detect_sqli(v, x.len, &st[threadIdx.x], T) ? 1 : 0;
+            }
+          }
           res = sq != 0;
         } else if (sv.kind == OP_DETECT_XSS) {
-          if (xs < 0) xs = li_candidate(false, v, x.len) && li_detect_xss(v, x.len) ? 1 : 0;
+          if (xs < 0) {
+            xs = 0;
+            if (li_candidate(false, v, x.len)) {
+              dsteps += x.len;
+              xs = li_detect_xss(v, x.len) ? 1 : 0;
+            }
+          }
           res = xs != 0;
         } else {
           continue;
@@ -5884,6 +5973,8 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
       }
     }
   }
+  dsteps = wave_sum(dsteps);
+  if ((threadIdx.x & 63) == 0 && dsteps) atomicAdd(&B.acct2[5], (unsigned long long)dsteps);
 }
 
 // Slow values (non-ASCII / "maybe"), one thread per list entry: every job of
@@ -5944,8 +6035,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
     t.ntx = 0;
     t.nremoved = 0;
     t.nrtgt = 0;
-    t.n_mp = 0;
-    t.mpl = nullptr;
+    t.kx = nullptr;
     t.engine = P.rule_engine;
     t.body_access = P.body_access;
     t.force_body = 0;
@@ -5985,6 +6075,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
       const gi_header hd = B.headers[rq.hdr_begin + h];
       scanned += hd.name.len + hd.value.len;
     }
+    t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
     const uint64_t c_init = B.prof ? clock64() : 0;
     // phase 1, ProcessRequestBody, phase 2 (one eval_phase call site)
     for (uint8_t ph = 1; ph <= 2 && !(t.flags & GI_REQ_ERROR_MASK); ph++) {
@@ -6102,20 +6193,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
             } else if (t.body_proc != BP_NONE) {
               t.flags |= GI_REQ_UNSUPPORTED_BODY;
             }
-            if (t.body_proc == BP_MULTIPART || t.body_proc == BP_XML) {
-              // the body collections (FILES*, MULTIPART_PART_HEADERS, XML): the
-              // residual clear-bit test of their targets visits only these
-              for (uint32_t f = H->nf; f < t.nf; f++) t.n_mp += t.fields[f].kind >= FK_FILE ? 1u : 0u;
-              const uint32_t pad = (4u - (uint32_t)((uintptr_t)(t.bytes + t.nb) & 3u)) & 3u;
-              if (t.n_mp && (uint64_t)t.nb + pad + 4ull * t.n_mp <= t.cap_b) {
-                uint32_t* l = (uint32_t*)(t.bytes + t.nb + pad);
-                uint32_t k = 0;
-                for (uint32_t f = H->nf; f < t.nf; f++)
-                  if (t.fields[f].kind >= FK_FILE) l[k++] = f;
-                t.nb += pad + 4 * t.n_mp;
-                t.mpl = l;
-              }
-            }
+            if (t.nf != H->nf) t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
           }
         }
         if ((t.flags & GI_REQ_ERROR_MASK) || !run2) break;

@@ -611,6 +611,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       // transient allocation <= that again + n, parser stack 1048 B
       if (k < q.body.len && (bd[k] == '{' || bd[k] == '[')) cap_b += 8ull * q.body.len + 4200;
     }
+    cap_b += 8 * (cap_f + 12) + 8;  // k_eval's kind index, built for phase 1 and again after the body parse
     uint64_t cap_t = 3 * maxv + 64 + (q.body.len ? 8 * 64 : 0);  // k_body: 64 lane slots of 3x + 8 B
     uint64_t cap_mt = 2 * maxv + 512;
     if (cap_f > 0xFFFFFFFFull || cap_b > 0xFFFFFFFFull || cap_t > 0xFFFFFFFFull || cap_mt > 0xFFFFFFFFull)
@@ -724,7 +725,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       return hip_fail(c, e, "alloc lane scratch");
     if ((e = c->pool.ensure(4ull * c->pool_cap)) != hipSuccess) return hip_fail(c, e, "alloc queue pool");
     if ((e = c->qblk.ensure(8ull * ns * c->qcap)) != hipSuccess) return hip_fail(c, e, "alloc queue blocks");
-    if ((e = c->ctr.ensure(352)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+    if ((e = c->ctr.ensure(384)) != hipSuccess) return hip_fail(c, e, "alloc counters");
     (void)ns;
     if ((e = c->slow.ensure(40ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
@@ -819,6 +820,7 @@ int gi_run_staged(gi_ctx* c) {
     B.pool_used = (unsigned long long*)cp;
     B.qblk = (uint2*)c->qblk.p;
     B.acct = (unsigned long long*)(cp + 160);
+    B.acct2 = (unsigned long long*)(cp + 336);  // 6 byte-step counters
     B.qcap = c->qcap;
     B.slow = c->slow.p;
     B.slow_count = (uint32_t*)(cp + 16);
@@ -891,6 +893,8 @@ int gi_sync(gi_ctx* c) {
     // per-launch HIP-event times and algorithmic bytes
     uint64_t acct[16] = {0};
     if (c->ctr.p) (void)hipMemcpy(acct, (uint8_t*)c->ctr.p + 160, 128, hipMemcpyDeviceToHost);
+    uint64_t acct2[6] = {0};
+    if (c->ctr.p) (void)hipMemcpy(acct2, (uint8_t*)c->ctr.p + 336, 48, hipMemcpyDeviceToHost);
     uint32_t ibk[16] = {0};
     if (c->ctr.p) (void)hipMemcpy(ibk, (uint8_t*)c->ctr.p + 64, 64, hipMemcpyDeviceToHost);
     gi_tally tl{};
@@ -919,7 +923,9 @@ int gi_sync(gi_ctx* c) {
       else if (nm == "k_bparse" || nm == "k_mpparse") ab = c->raw_all - c->raw_nobody;
       else if (nm == "k_eval") ab = c->raw_all + (uint64_t)sizeof(gi_verdict) * c->n_req + 4ull * tl.matched_total;
       c->stats.launch_alg_bytes[k] = ab;
-      c->stats.launch_steps[k] = nm == "k_scan" ? acct[13] : nm == "k_scan_big" ? acct[14] : nm == "k_scan_hbm" ? acct[15] : 0;
+      c->stats.launch_steps[k] = nm == "k_scan" ? acct[13] : nm == "k_scan_big" ? acct[14] : nm == "k_scan_hbm" ? acct[15]
+                                 : nm.rfind("k_stream", 0) == 0 ? acct2[nm.back() - '0']
+                                 : nm == "k_detect" ? acct2[5] : 0;
     }
 #ifdef GI_DEBUG
     if (c->ctr.p) {

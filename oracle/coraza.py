@@ -644,7 +644,7 @@ def _x2c(a: int, b: int) -> int:
 
 def t_lowercase(d: bytes) -> bytes:
     # Go strings.ToLower: ASCII fast path, else strings.Map(unicode.ToLower)
-    if all(c < 0x80 for c in d):
+    if d.isascii():
         return d.lower()
     out = bytearray()
     i, n = 0, len(d)
@@ -1711,6 +1711,7 @@ class Transaction:
         self.phase = 0
         self.cur_top = 0
         self.captures: List[Tuple[int, int, bytes]] = []
+        self._tcache: Dict[Tuple[tuple, bytes], bytes] = {}
 
     # -- request population -------------------------------------------------
     def process_request(self, req: Request):
@@ -1853,7 +1854,7 @@ class Transaction:
                     self.captures.append((self.cur_top, i, c))
                 res = len(caps) > 0
             else:
-                res = any(p in low for p in op.phrases)
+                res = _pm_any(op, low)
         elif n == "contains":
             res = self.expand(op.macro) in value
         elif n == "containsword":
@@ -1966,9 +1967,17 @@ class Transaction:
                 self.run_ctl(*obj)
 
     def transform(self, rule: Rule, value: bytes) -> bytes:
+        # transformations are pure: cached per (chain, value) for the transaction
+        key = (tuple(rule.transforms), value)
+        hit = self._tcache.get(key)
+        if hit is not None:
+            return hit
+        v = value
         for t in rule.transforms:
-            value = TRANSFORM_FNS[t](value)
-        return value
+            v = TRANSFORM_FNS[t](v)
+        if len(self._tcache) < 65536:
+            self._tcache[key] = v
+        return v
 
     def match_variable(self, var: str, key: bytes, value: bytes):
         """[upstream transaction.go matchVariable]: MATCHED_VAR(_NAME) = the
@@ -2165,20 +2174,49 @@ class Transaction:
         self.eval_phase(2)
 
 
+def _pm_index(phrases):
+    """(phrase set, distinct lengths longest first) of a phrase list."""
+    key = id(phrases)
+    ix = _PM_INDEX.get(key)
+    if ix is None or ix[0] is not phrases:
+        ps = set(phrases)
+        ix = (phrases, ps, sorted({len(p) for p in ps}, reverse=True))
+        _PM_INDEX[key] = ix
+    return ix[1], ix[2]
+
+
+_PM_INDEX = {}
+
+
+def _pm_any(op, low: bytes) -> bool:
+    """Some phrase occurs in low (the phrases are lowercased already)."""
+    if len(op.phrases) <= 64:
+        return any(p in low for p in op.phrases)
+    ps, lens = _pm_index(op.phrases)
+    if b"" in ps:
+        return True
+    for i in range(len(low)):
+        for n in lens:
+            if i + n <= len(low) and low[i:i + n] in ps:
+                return True
+    return False
+
+
 def _pm_find_all(phrases, low: bytes, orig: bytes):
     """Leftmost-longest non-overlapping matches (aho-corasick MatchKind)."""
+    ps, lens = _pm_index(phrases)
     out = []
     i = 0
     n = len(low)
     while i < n:
-        best = None
-        for p in phrases:
-            if low.startswith(p, i):
-                if best is None or len(p) > len(best):
-                    best = p
-        if best is not None:
-            out.append(orig[i:i + len(best)])
-            i += len(best)
+        best = 0
+        for L in lens:  # longest first
+            if L and i + L <= n and low[i:i + L] in ps:
+                best = L
+                break
+        if best:
+            out.append(orig[i:i + best])
+            i += best
         else:
             i += 1
     return out

@@ -51,6 +51,22 @@ def test_gpu_c5_small_parity():
 
 
 @pytest.mark.gpu
+def test_gpu_c5_2k_rules_256k_multipart_parity():
+    # >= 2k generated rules over >= 256 KB multipart bodies, each request vs the oracle
+    text, files = traffic.c5_ruleset(n_rx=2000, n_phrases=30000)
+    batch = traffic.c5_batch(4, body_bytes=262144, n_rx=2000, n_phrases=30000, hit_rate=0.05)
+    rs = gpuinspect.Ruleset(text, data_files=files)
+    assert rs.info["n_rules"] >= 2000
+    res = gpuinspect.Engine(rs).inspect(batch)
+    cfg = coraza.parse_seclang(text, files)
+    verdicts = compare.oracle_verdicts(cfg, batch, rs.exports)
+    bad = compare.compare(res, verdicts)
+    assert not bad, bad[:3]
+    assert all(len(v.matched) > 5 for v in verdicts.values())
+    assert not any(int(v["flags"]) & 0x0F for v in res.verdicts)
+
+
+@pytest.mark.gpu
 def test_gpu_scan_hbm_forced_parity():
     text = open(os.path.join(ROOT, "rulesets", "crs_pl1.conf")).read()
     batch = traffic.TrafficGen(traffic.SEED + 3).batch(1500, post_frac=0.2)

@@ -1,12 +1,12 @@
 #!/bin/bash
-# rocprofv3 kernel-trace + stats of a bench run (args passed to bench.py).
+# One GPU call: GI_PROF=1 cycle breakdowns (k_stream per bucket, k_body per
+# link, k_eval per request + hottest rule links) on C2 and C4 -- stderr.
 set -u
-R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-mkdir -p "$R/gpurun_out/prof"
-export TMPDIR=/tmp
-cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" "$@" > "$R/gpurun_out/prof_bench.log" 2>&1
-rc=$?
-echo "rocprof rc=$rc"; tail -3 "$R/gpurun_out/prof_bench.log"
-find "$R/gpurun_out/prof" -name "*stats*" | head
-exit $rc
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+TAG=${TAG:-prof}
+for c in ${CONFIGS:-c2 c4}; do
+  echo "== $c $(date +%T)"
+  GI_PROF=1 timeout -k 10 300 python -u bench.py --config $c --steps 1 --warmup 1 --no-cpu-baseline ${ARGS:-} > gpurun_out/${TAG}_${c}_bench.json 2> gpurun_out/${TAG}_${c}.err || { tail -20 gpurun_out/${TAG}_${c}.err; exit 1; }
+  grep GI_PROF -A13 gpurun_out/${TAG}_${c}.err | tail -40
+done

@@ -24,7 +24,7 @@ export TMPDIR=/tmp
 step rocprof
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_prof -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $R/gpurun_out/${TAG}_prof_bench.json 2>$R/gpurun_out/${TAG}_prof_bench.err) || { tail -5 gpurun_out/${TAG}_prof_bench.err; exit 1; }
 step traffic
-timeout -k 10 400 python -u tools/pmc_traffic.py --config c2 --n-req 1000000 --out gpurun_out/${TAG}_traffic_c2.json > gpurun_out/${TAG}_traffic.log 2>&1 || { tail -20 gpurun_out/${TAG}_traffic.log; exit 1; }
+timeout -k 10 400 python -u tools/pmc_traffic.py --config c2 --n-req 1000000 --tag ${TAG} --out gpurun_out/${TAG}_traffic_c2.json > gpurun_out/${TAG}_traffic.log 2>&1 || { tail -20 gpurun_out/${TAG}_traffic.log; exit 1; }
 tail -1 gpurun_out/${TAG}_traffic.log
 step occupancy
 timeout -k 10 400 python -u tools/pmc_occupancy.py --config c2 --n-req 1000000 --out gpurun_out/${TAG}_pmc_c2.json > gpurun_out/${TAG}_occ.log 2>&1 || { tail -20 gpurun_out/${TAG}_occ.log; exit 1; }
