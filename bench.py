@@ -233,8 +233,9 @@ def main():
         if tj.get("requests") == batch.n_req:
             kt = tj.get("kernels", {})
             rk = ROCPROF_NAMES.get(dom, dom)
-            if rk in kt:
-                hbm_traffic = kt[rk]["hbm_bytes_per_launch"]
+            for name in (rk, "gi::" + rk):  # rocprofv3 may report the namespace
+                if name in kt:
+                    hbm_traffic = kt[name]["hbm_bytes_per_launch"]
             traffic_all = {"source": "profiles/traffic_%s.json (%s)" % (args.config, tj.get("tag", "")),
                            "hbm_bytes_per_launch": {k: v["hbm_bytes_per_launch"] for k, v in kt.items()}}
     steps_s = launch_steps.get(dom, 0) / (avg_launch[dom] * 1e-3)

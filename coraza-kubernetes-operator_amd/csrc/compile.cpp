@@ -1280,10 +1280,11 @@ struct Lower {
   uint32_t n_det = 0;  // streams with detect vals (DStream.det_id)
   std::map<std::string, size_t> sindex;
 
-  // body collections phase A does not scan (multipart, XML): tested by k_eval on a clear bit
+  // body collections phase A does not scan (part headers, XML): tested by k_eval on a clear bit.
+  // FILES / FILES_NAMES / FILES_SIZES come out of k_mpparse's speculative
+  // multipart parse before phase A and are scanned like ARGS_POST.
   static bool residual_collection(const std::string& n) {
-    return n == "FILES" || n == "FILES_NAMES" || n == "FILES_SIZES" || n == "FILES_TMPNAMES" ||
-           n == "MULTIPART_PART_HEADERS" || n == "XML";
+    return n == "FILES_TMPNAMES" || n == "MULTIPART_PART_HEADERS" || n == "XML";
   }
   static bool immutable_single(int sid) {
     return sid == S_REQUEST_METHOD || sid == S_REQUEST_PROTOCOL || sid == S_REQUEST_URI ||
@@ -1314,7 +1315,8 @@ struct Lower {
       if (sid < 0 && v.name == "TX") return -1;
       if (v.name.rfind("MATCHED_VAR", 0) == 0) return -1;  // transaction state, not a request variable
       if (residual_collection(v.name)) residual = true;  // body collections phase A does not scan
-      if (v.name == "ARGS" || v.name == "ARGS_POST" || v.name == "ARGS_NAMES" || v.name == "ARGS_POST_NAMES")
+      if (v.name == "ARGS" || v.name == "ARGS_POST" || v.name == "ARGS_NAMES" || v.name == "ARGS_POST_NAMES" ||
+          v.name == "FILES" || v.name == "FILES_NAMES" || v.name == "FILES_SIZES")
         bodydep = true;
     }
     // multiMatch (rule.go executeTransformationsMultimatch) tests the value
@@ -1339,8 +1341,7 @@ struct Lower {
     DVarRef* vrs = &P->vars[d.var_begin];
     for (uint32_t vi = 0; vi < d.var_count; vi++) {
       DVarRef& vr = vrs[vi];
-      if ((vr.var < S_COUNT && !immutable_single(vr.var)) || vr.var == V_FILES ||
-          vr.var == V_FILES_NAMES || vr.var == V_FILES_SIZES || vr.var == V_FILES_TMPNAMES ||
+      if ((vr.var < S_COUNT && !immutable_single(vr.var)) || vr.var == V_FILES_TMPNAMES ||
           vr.var == V_MULTIPART_PART_HEADERS || vr.var == V_XML) {
         vr.residual = 1;
         continue;
@@ -1365,7 +1366,11 @@ struct Lower {
           case V_ARGS_NAMES: mask = (1 << FK_ARG_GET) | (1 << FK_ARG_POST); names = true; break;
           case V_REQUEST_HEADERS_NAMES: mask = 1 << FK_HEADER; names = true; break;
           case V_REQUEST_COOKIES_NAMES: mask = 1 << FK_COOKIE; names = true; break;
-          default: break;  // XML, FILES*: residual (above)
+          // multipart collections: k_mpparse's fields (key "" or the file name)
+          case V_FILES: mask = 1 << FK_FILE; break;
+          case V_FILES_NAMES: mask = 1 << FK_FILE_NAME; break;
+          case V_FILES_SIZES: mask = 1 << FK_FILE_SIZE; break;
+          default: break;  // XML, part headers, FILES_TMPNAMES: residual (above)
         }
         if (!mask) continue;
         f.kind_mask = mask;
@@ -1419,7 +1424,7 @@ struct Lower {
             if (f.single != GI_NO_SINGLE) {
               P->item_singles |= 1u << f.single;
             } else {
-              for (int k = FK_ARG_GET; k <= FK_COOKIE; k++)
+              for (int k = FK_ARG_GET; k <= FK_FILE_SIZE; k++)
                 if ((f.kind_mask >> k) & 1) P->item_sides[k] |= f.names ? 2 : 1;
             }
           }

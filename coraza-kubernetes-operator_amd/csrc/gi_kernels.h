@@ -91,6 +91,10 @@ struct DBatch {
   unsigned long long* prof;   // GI_PROF=1: k_eval cycle / rule counters (stderr at gi_sync)
   uint64_t items_cap;
   uint32_t n_hit_slots;
+  uint32_t* wlist;            // requests k_eval hands to k_eval_wave (a wave each)
+  uint32_t* wcount;
+  uint32_t wave_fields;       // k_eval_wave: requests with this many fields (0: none)
+  uint32_t wave_rules;        // k_eval_wave: every request when the program walks this many rules (0: never)
 };
 
 // k_scan launch plan: job lists for the small-LDS and big-LDS launches.
@@ -111,6 +115,9 @@ struct ScanLaunch {
 #define GI_LONG_MIN 2048     // items at least this long take k_long (one wave per (item, stream)), not the queue
 #define GI_LONG_GRID 512     // k_long workgroups (at most)
 #define GI_LONG_BUDGET (4ull << 30)  // bytes of k_long chain buffers (runtime.cpp gi_stage_batch)
+#define GI_EVAL_WAVE_LDS_WORDS 4096  // k_eval_wave keeps a request's hit words in LDS up to this many
+#define GI_EVAL_WAVE_FIELDS 2048     // default k_eval_wave thresholds (GI_EVAL_WAVE_FIELDS / _RULES env)
+#define GI_EVAL_WAVE_RULES 2048
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.
 uint32_t scan_resident_blocks(uint32_t lds_bytes);

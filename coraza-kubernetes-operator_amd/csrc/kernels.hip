@@ -1269,7 +1269,8 @@ struct Tx {
   uint8_t* txa;
   uint32_t ntx, cap_tx;
   Str* single;               // ReqHdr::single (per-request, in HBM scratch)
-  const uint32_t* hits;      // phase-A hit words [slot/32][n_req]
+  const uint32_t* hits;      // this request's phase-A hit word of slot s at hits[(s / 32) * hstride]
+  uint32_t hstride;          // n_req (the batch's hit words in HBM) or 1 (k_eval_wave's LDS copy)
   const uint32_t* vmap;      // the request's phase-A value signatures (word 2f + side: bit slot % 32)
   const uint32_t* hset;      // the request's exact hit set (nullptr: none, or it overflowed)
   uint32_t hmask;
@@ -3787,13 +3788,50 @@ __device__ __forceinline__ bool slot_vexact(const DProgram& P, uint32_t s) {
   return true;
 }
 
-// Rule.doEvaluate for one link -> number of matched values.
+// Which value of field f a collection target vr of link R tests (side
+// effect free): 0 none, 1 an exact phase-A match (the operator need not run
+// again), 2 evaluate it.  Phase A tested every value of fields [0, nf_pa)
+// this link reads: one whose value-map bit is clear set no hit bit at all,
+// so it cannot match here (value-exact slots only: an always-slot is set
+// without a value); with the exact hit set, a value with a set bit is
+// decided by its key (exact key: a match; maybe key: evaluate; no key: no
+// match).  *names: the key side is tested.
+__device__ __forceinline__ uint32_t field_filter(Tx& t, const DRule& R, const DVarRef& vr, uint32_t f, bool vskip,
+                                                 bool vexact, bool* names) {
+  const DProgram& P = *t.P;
+  const Field fl = t.fields[f];
+  if (!field_in(vr.var, fl.kind, names)) return 0;
+  uint32_t hres = 2;
+  if (vskip && f < t.nf_pa && fl.kind <= FK_FILE_SIZE) {  // phase-A item kinds only
+    const uint32_t vb = 2 * f + (*names ? 1u : 0u);
+    if (!((t.vmap[vb] >> ((uint32_t)R.hit_slot & 31u)) & 1u)) return 0;
+    if (vexact) {
+      hres = hset_lookup(t.hset, t.hmask, (uint32_t)R.hit_slot, vb);
+      if (!hres) return 0;
+    }
+  }
+  if (vr.key_mode == 1) {
+    if (vr.ci ? !eq_ascii_ci(fl.k, fl.kn, P.strpool + vr.key_off, vr.key_len)
+              : !eq_bytes(fl.k, fl.kn, P.strpool + vr.key_off, vr.key_len))
+      return 0;
+  } else if (vr.key_mode == 2) {
+    if (!dfa_match(P, vr.key_dfa, fl.k, fl.kn, vr.ci != 0)) return 0;
+  }
+  if (vr.exc_count && key_excluded(t, vr, fl.k, fl.kn)) return 0;
+  if (t.nrtgt && R.id != 0 && target_removed(t, R.id, vr.var, fl.k, fl.kn)) return 0;
+  return hres;
+}
+
+// Rule.doEvaluate for one link -> number of matched values.  W: k_eval_wave
+// (the request's whole wave runs the interpreter uniformly; collection
+// fields are filtered 64 at a time).
+template <bool W>
 __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   const DProgram& P = *t.P;
   // phase-A filter: a clear hit bit proves no value matches (exact); a set
   // bit (match or "maybe") falls through to the full evaluation below.
   if (R.hit_slot >= 0 && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post)) {
-    const uint32_t w = t.hits[(uint64_t)(R.hit_slot >> 5) * t.n_req + t.req];
+    const uint32_t w = t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride];
     if (!((w >> (R.hit_slot & 31)) & 1u)) {
       if (!(R.flags & RF_RESIDUAL)) return 0;
       // phase A cleared every other target: only the residual (body-phase)
@@ -3935,13 +3973,8 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
       }
       continue;
     }
-    // phase A tested every value of fields [0, nf_pa) this link reads: one
-    // whose value-map bit is clear set no hit bit at all, so it cannot match
-    // here (value-exact slots only: an always-slot is set without a value).
-    // With the exact hit set, a value with a set bit is decided by its key:
-    // an exact key is a match (the operator is not run again), a maybe key
-    // is evaluated, no key is no match.  multiMatch links count candidates
-    // per value, so they always evaluate.
+    // value-map / hit-set filtering (field_filter); multiMatch links count
+    // candidates per value, so they always evaluate.
     const bool vskip = R.hit_slot >= 0 && !vr.count && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
                        slot_vexact(P, (uint32_t)R.hit_slot);
     const bool vexact = vskip && t.hset && !(R.flags & RF_MULTIMATCH);
@@ -3956,37 +3989,58 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         j = je;
       }
     }
-    for (; j < je; j++) {
-      const uint32_t f = t.kx ? t.kx[12 + j] : j;
-      const Field fl = t.fields[f];
-      bool names;
-      if (!field_in(vr.var, fl.kind, &names)) continue;
-      uint32_t hres = 2;  // 2: evaluate the value
-      if (vskip && f < t.nf_pa && fl.kind <= FK_COOKIE) {  // phase-A item kinds only
-        const uint32_t vb = 2 * f + (names ? 1u : 0u);
-        if (!((t.vmap[vb] >> ((uint32_t)R.hit_slot & 31u)) & 1u)) continue;
-        if (vexact) {
-          hres = hset_lookup(t.hset, t.hmask, (uint32_t)R.hit_slot, vb);
-          if (!hres) continue;
-        }
-      }
-      if (vr.key_mode == 1) {
-        if (vr.ci ? !eq_ascii_ci(fl.k, fl.kn, P.strpool + vr.key_off, vr.key_len)
-                  : !eq_bytes(fl.k, fl.kn, P.strpool + vr.key_off, vr.key_len))
+    if (!W) {
+      for (; j < je; j++) {
+        const uint32_t f = t.kx ? t.kx[12 + j] : j;
+        bool names;
+        const uint32_t hres = field_filter(t, R, vr, f, vskip, vexact, &names);
+        if (!hres) continue;
+        if (vr.count) {
+          cnt++;
           continue;
-      } else if (vr.key_mode == 2) {
-        if (!dfa_match(P, vr.key_dfa, fl.k, fl.kn, vr.ci != 0)) continue;
+        }
+        const Field fl = t.fields[f];
+        nmatch += test_value(t, R, o, names ? fl.k : fl.v, names ? fl.kn : fl.vn, vr.var, fl.k, fl.kn, hres == 1);
       }
-      if (vr.exc_count && key_excluded(t, vr, fl.k, fl.kn)) continue;
-      if (t.nrtgt && R.id != 0 && target_removed(t, R.id, vr.var, fl.k, fl.kn)) continue;
-      if (vr.count) {
-        cnt++;
-        continue;
+    } else {
+      // k_eval_wave: the lanes filter 64 fields at a time (pure: value map,
+      // hit set, key selectors, exclusions), then the wave tests the survivors
+      // in field order, uniformly (actions and matched-variable state keep
+      // Coraza's per-value order)
+      const uint32_t lane = threadIdx.x & 63u;
+      for (; j < je; j += 64) {
+        const uint64_t c0 = t.profon ? clock64() : 0;
+        uint32_t f = 0, hres = 0;
+        bool names = false;
+        if (j + lane < je) {
+          f = t.kx ? t.kx[12 + j + lane] : j + lane;
+          hres = field_filter(t, R, vr, f, vskip, vexact, &names);
+        }
+        uint64_t m = __ballot(hres != 0);
+        if (t.profon) {  // GI_PROF (lane 0): fields filtered, survivors exact / to evaluate, cycles
+          unsigned long long* pf = t.prof_rule_cyc - 128;
+          const uint64_t mx = __ballot(hres == 1);
+          atomicAdd(&pf[17], (unsigned long long)min(64u, je - j));
+          atomicAdd(&pf[18], (unsigned long long)__popcll(mx));
+          atomicAdd(&pf[19], (unsigned long long)__popcll(m & ~mx));
+          atomicAdd(&pf[20], (unsigned long long)(clock64() - c0));
+        }
+        if (vr.count) {
+          cnt += (uint32_t)__popcll(m);
+          continue;
+        }
+        const uint64_t c1 = t.profon ? clock64() : 0;
+        while (m) {
+          const int b = __ffsll((unsigned long long)m) - 1;
+          m &= m - 1;
+          const uint32_t fb = (uint32_t)__shfl((int)f, b, 64);
+          const uint32_t hb = (uint32_t)__shfl((int)hres, b, 64);
+          const bool nb = __shfl((int)names, b, 64) != 0;
+          const Field fl = t.fields[fb];
+          nmatch += test_value(t, R, o, nb ? fl.k : fl.v, nb ? fl.kn : fl.vn, vr.var, fl.k, fl.kn, hb == 1);
+        }
+        if (t.profon) atomicAdd(&t.prof_rule_cyc[-128 + 21], (unsigned long long)(clock64() - c1));
       }
-      if (names)
-        nmatch += test_value(t, R, o, fl.k, fl.kn, vr.var, fl.k, fl.kn, hres == 1);
-      else
-        nmatch += test_value(t, R, o, fl.v, fl.vn, vr.var, fl.k, fl.kn, hres == 1);
     }
     if (vr.count) {
       uint8_t buf[24];
@@ -3997,6 +4051,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   return nmatch;
 }
 
+template <bool W>
 __device__ __forceinline__ void eval_top(Tx& t, uint32_t ri) {
   const DProgram& P = *t.P;
   const DRule R = gi_cload(P.rules, ri);
@@ -4006,7 +4061,7 @@ __device__ __forceinline__ void eval_top(Tx& t, uint32_t ri) {
   for (int32_t ci = (int32_t)ri; ci >= 0;) {
     const DRule C = gi_cload(P.rules, (uint64_t)ci);
     const uint64_t c0 = t.profon ? clock64() : 0;
-    const uint32_t nm = eval_rule(t, C);
+    const uint32_t nm = eval_rule<W>(t, C);
     if (t.profon) {
       const uint64_t dc = clock64() - c0;
       t.prof_eval_cyc += dc;
@@ -4033,14 +4088,48 @@ __device__ __forceinline__ void eval_top(Tx& t, uint32_t ri) {
   }
 }
 
+// Is rule index k of the phase walk a no-op for this request in the current
+// state (no skip count pending)?  A removed rule, a marker we are not
+// skipping to, a rule whose first link phase A cleared; with skipAfter
+// pending, every rule but the target marker.  (Used by k_eval_wave to jump
+// over runs of such rules 64 at a time; MATCHED_VARS is reset before every
+// evaluated rule, so skipping the resets of no-op rules changes nothing.)
+__device__ __forceinline__ bool rule_noop(Tx& t, const DRule& R) {
+  if (R.id != 0 && t.nremoved) {
+    for (uint32_t j = 0; j < t.nremoved; j++)
+      if (t.removed[j][0] <= R.id && R.id <= t.removed[j][1]) return true;
+  }
+  if (t.skip_after >= 0) return R.marker != t.skip_after;
+  if (R.flags & RF_MARKER) return true;
+  return R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
+         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u);
+}
+
 // RuleGroup.Eval [upstream corazawaf/rulegroup.go]
+template <bool W>
 __device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
   const DProgram& P = *t.P;
   if (t.engine == ENGINE_OFF) return;
   t.phase = phase;
-  for (uint32_t k = P.top_begin[phase - 1]; k < P.top_end[phase - 1]; k++) {
+  const uint32_t kend = P.top_end[phase - 1];
+  for (uint32_t k = P.top_begin[phase - 1]; k < kend; k++) {
     if (t.interrupted) break;
     if (t.flags & GI_REQ_ERROR_MASK) break;
+    if (W && t.skip == 0) {
+      // the lanes test the next 64 rules; jump to the first that is not a no-op
+      const uint32_t kk = k + (threadIdx.x & 63u);
+      bool need = false;
+      if (kk < kend) {
+        const DRule Rl = P.rules[GI_CONST(uint32_t, P.top)[kk]];
+        need = !rule_noop(t, Rl);
+      }
+      const uint64_t m = __ballot(need);
+      if (!m) {
+        k += 63;
+        continue;
+      }
+      k += (uint32_t)(__ffsll((unsigned long long)m) - 1);
+    }
     const uint32_t ri = GI_CONST(uint32_t, P.top)[k];
     const DRule R = gi_cload(P.rules, ri);
     t.prof_visits++;
@@ -4065,9 +4154,9 @@ __device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
       t.mv->nb = 0;
     }
     if (R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
-        !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.n_req + t.req] >> (R.hit_slot & 31)) & 1u))
+        !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u))
       continue;  // phase A proved the first link matches nothing
-    eval_top(t, ri);
+    eval_top<W>(t, ri);
   }
 }
 
@@ -4278,9 +4367,10 @@ __device__ __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H
   const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck, n_pre = n_get + n_hdr + n_ck;
   for (uint32_t i = 0; i < n_pre + H->n_post; i++) {
     const Field fl = Fd[i];
-    // the body range may hold multipart collections: never phase-A items
+    // the body range may hold multipart collections: FILES / FILES_NAMES /
+    // FILES_SIZES are phase-A items, part headers are not
     const uint8_t kind = i < n_get ? FK_ARG_GET : i < n_get + n_hdr ? FK_HEADER : i < n_pre ? FK_COOKIE : (uint8_t)fl.kind;
-    if (kind != FK_ARG_GET && kind != FK_HEADER && kind != FK_COOKIE && kind != FK_ARG_POST) continue;
+    if (kind < FK_ARG_GET || kind > FK_FILE_SIZE) continue;
     const uint8_t sides = P.item_sides[kind];
     if (sides & 1) f(kind, (uint8_t)0, 0u, i, fl.vn);
     if (sides & 2) f(kind, (uint8_t)0, 1u, i, fl.kn);
@@ -4627,13 +4717,13 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
         H->spec_err = err;
         H->n_post = jc.nf - nf0;
         H->nb = jc.nb;
-        // phase-A item counts of its ARGS_POST fields
-        const uint32_t sides = P.n_streams ? P.item_sides[FK_ARG_POST] : 0u;
-        if (sides) {
+        // phase-A item counts of its ARGS_POST and FILES* fields (for_each_item's kinds)
+        if (P.n_streams) {
           uint32_t cnt[GI_NB] = {0, 0, 0, 0, 0};
           for (uint32_t f = nf0; f < jc.nf; f++) {
             const Field fl = g.fields[f];
-            if (fl.kind != FK_ARG_POST) continue;
+            if (fl.kind < FK_ARG_GET || fl.kind > FK_FILE_SIZE) continue;
+            const uint32_t sides = P.item_sides[fl.kind];
             if (sides & 1) cnt[item_bucket(fl.vn)]++;
             if (sides & 2) cnt[item_bucket(fl.kn)]++;
           }
@@ -5996,6 +6086,267 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
 #ifndef GI_EVAL_WPE
 #define GI_EVAL_WPE 2  // minimum waves per SIMD k_eval is compiled for (register budget; A/B: 2 beats 1 and 4)
 #endif
+// Phase B of request r: RuleGroup.Eval(1) -> ProcessRequestBody ->
+// RuleGroup.Eval(2); my[7] = its tally contributions.  W (k_eval_wave): the
+// request's whole wave runs it uniformly, whits = the request's hit words in
+// LDS (nullptr: read from HBM).
+template <bool W>
+__device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B, uint32_t r, const uint32_t* whits,
+                                             unsigned long long* my) {
+  const uint64_t c_start = B.prof ? clock64() : 0;
+  const gi_request rq = B.reqs[r];
+  Region g = region_of(P, B, r);
+  ReqHdr* H = g.hdr;
+  Tx t;
+  t.prof_visits = t.prof_evals = t.prof_rules = 0;
+  t.prof_eval_cyc = t.prof_act_cyc = 0;
+  const bool lead = !W || (threadIdx.x & 63u) == 0;  // the lane that writes shared counters
+  t.profon = B.prof != nullptr && lead;
+  t.prof_rule_cyc = B.prof ? B.prof + 128 : nullptr;
+  tx_bind(t, P, g);
+  t.hits = whits ? whits : B.hits + r;
+  t.hstride = whits ? 1u : B.n_req;
+  t.vmap = B.vmap + B.layout[r].vmap_bit;
+  {
+    const ReqLayout Lr = B.layout[r];
+    const uint32_t* tab = B.hset + Lr.hset_word;
+    t.hset = (Lr.hset_mask && tab[0] == 0u) ? tab : nullptr;
+    t.hmask = Lr.hset_mask;
+  }
+  t.nf_pa = H->nf;
+  t.n_req = B.n_req;
+  t.req = r;
+  t.slots = B.txslots + r;
+  t.has_post = false;
+  t.body_spec = false;
+  t.pa_void = H->pa_void != 0;
+  t.nf = H->nf;
+  t.nb = H->nb;
+  t.flags = H->flags;
+  t.body_proc = H->body_proc;
+  t.ntx = 0;
+  t.nremoved = 0;
+  t.nrtgt = 0;
+  t.kx = nullptr;
+  t.engine = P.rule_engine;
+  t.body_access = P.body_access;
+  t.force_body = 0;
+  t.phase = 0;
+  t.skip_after = -1;
+  t.skip = 0;
+  t.interrupted = false;
+  t.int_rule = 0;
+  t.int_status = 0;
+  t.int_action = 0;
+  t.int_phase = 0;
+  t.nmatched = 0;
+  t.mout = B.matched + (uint64_t)r * B.mcap;
+  t.cur_id = 0;
+  if (t.capws) {
+    CapHdr* CH = (CapHdr*)t.capws;
+    CH->nrec = CH->nbytes = 0;
+    CH->rec = B.caprec ? B.caprec + 4ull * B.crcap * r : nullptr;
+    CH->bytes = B.capbytes ? B.capbytes + (uint64_t)B.cbcap * r : nullptr;
+    CH->rec_cap = B.crcap;
+    CH->bytes_cap = B.cbcap;
+    CH->trunc = 0;
+  }
+  t.mcap = B.mcap;
+  for (uint32_t s = 0; s < P.n_slots; s++) TXS(t, s).state = 0;
+  if (t.mv) {
+    t.mv->n = t.mv->nb = 0;
+    t.mv->cap_e = g.cap_f + 16;
+    t.mv->cap_a = g.cap_b + g.cap_mt;
+    t.mv->cap_v = g.cap_t;
+    t.mv->cap_n = g.cap_mt;
+    t.mv->cur_vn = t.mv->cur_nn = 0;
+  }
+  const uint8_t* D = B.data;
+  uint64_t scanned = (uint64_t)rq.method.len + rq.uri.len + rq.proto.len + rq.body.len;
+  for (uint32_t h = 0; h < rq.hdr_count; h++) {
+    const gi_header hd = B.headers[rq.hdr_begin + h];
+    scanned += hd.name.len + hd.value.len;
+  }
+  t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
+  const uint64_t c_init = B.prof ? clock64() : 0;
+  // phase 1, ProcessRequestBody, phase 2 (one eval_phase call site)
+  for (uint8_t ph = 1; ph <= 2 && !(t.flags & GI_REQ_ERROR_MASK); ph++) {
+    if (ph == 2) {
+      if (t.interrupted || t.engine == ENGINE_OFF) break;
+      uint32_t bn = rq.body.len;
+      bool run2 = true;
+      if (t.body_access && bn > 0) {
+        // [upstream transaction.go WriteRequestBody]: over SecRequestBodyLimit
+        // -> INBOUND_DATA_ERROR; Reject: interruption 413 (no rule id) and no
+        // ProcessRequestBody; ProcessPartial: the first limit bytes.
+        // ProcessRequestBody: a buffer of exactly the limit sets it too and,
+        // with Reject, returns before phase 2.  (DetectionOnly + Reject:
+        // nothing buffered.)
+        if (bn > P.body_limit) {
+          t.single[S_INBOUND_DATA_ERROR] = {CS_ONE, 1};
+          if (!P.body_partial) {
+            if (t.engine == ENGINE_ON) {
+              t.interrupted = true;
+              t.int_rule = 0;
+              t.int_status = 413;
+              t.int_action = GI_ACTION_DENY;
+              t.int_phase = 2;
+              break;
+            }
+            bn = 0;
+          } else {
+            bn = (uint32_t)P.body_limit;
+          }
+        }
+        if (bn > 0 && bn >= P.body_limit) {
+          t.single[S_INBOUND_DATA_ERROR] = {CS_ONE, 1};
+          if (!P.body_partial) run2 = false;
+        }
+      }
+      if (t.body_access && bn > 0 && run2) {
+        {
+          uint8_t* lb = tx_alloc(t, 24);
+          if (lb) t.single[S_REQUEST_BODY_LENGTH] = {lb, go_itoa((int64_t)bn, lb)};
+          if (t.force_body && t.body_proc == BP_NONE) {
+            t.body_proc = BP_URLENCODED;
+            t.single[S_REQBODY_PROCESSOR] = {CS_URLENCODED, 10};
+          }
+          if (t.body_proc == BP_URLENCODED || t.body_proc == BP_JSON) {
+            t.single[S_REQUEST_BODY] = {D + rq.body.off, bn};
+            if (t.body_proc == H->spec_proc) {
+              t.nf += H->n_post;  // k_collect's fields, already in phase A
+              t.nf_pa = t.nf;
+              t.body_spec = true;
+            } else {
+              const uint32_t nf0 = t.nf;
+              if (t.body_proc == BP_URLENCODED) parse_query(t, D + rq.body.off, bn, FK_ARG_POST);
+              else {
+                JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
+                parse_json_body_ool(&jc, D + rq.body.off, bn);
+                t.nf = jc.nf;
+                t.nb = jc.nb;
+                t.flags = jc.flags;
+                if (t.flags & GI_REQ_BODY_ERROR) {
+                  // readJSON's error -> generateRequestBodyError: REQBODY_ERROR "1",
+                  // REQBODY_ERROR_MSG "<processor>: <error>", no ARGS_POST, no REQUEST_BODY;
+                  // phase 2 still runs (CRS base rule 200002 denies with 400)
+                  t.nf = nf0;
+                  t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
+                  t.single[S_REQBODY_ERROR_MSG] = {CS_JSON_ERR, 18};
+                  t.single[S_REQUEST_BODY] = {CS_ZERO, 0};
+                }
+              }
+              t.has_post = t.nf > nf0;
+            }
+          } else if (t.body_proc == BP_MULTIPART) {
+            // [upstream multipart.go]: collections, no REQUEST_BODY; an error
+            // -> MULTIPART_STRICT_ERROR + generateRequestBodyError (rules
+            // 200002 / 200003 deny with 400)
+            uint8_t err;
+            if (H->spec_proc == BP_MULTIPART) {
+              t.nf += H->n_post;  // k_bparse's fields (ARGS_POST already in phase A)
+              t.nf_pa = t.nf;
+              t.body_spec = true;
+              err = H->spec_err;
+            } else {
+              const uint32_t nf0 = t.nf;
+              JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
+              const Str ct = first_content_type(B, rq);
+              uint64_t comb;
+              bool comb_set;
+              err = parse_multipart(jc, D + rq.body.off, bn, ct.p, ct.n, &comb, &comb_set);
+              t.nf = jc.nf;
+              t.nb = jc.nb;
+              t.flags = jc.flags;
+              if (comb_set && !(t.flags & GI_REQ_ERROR_MASK)) {
+                uint8_t* cb = tx_alloc(t, 24);
+                if (cb) t.single[S_FILES_COMBINED_SIZE] = {cb, go_itoa((int64_t)comb, cb)};
+              }
+              t.has_post = t.nf > nf0;
+            }
+            if (err) {
+              t.single[S_MULTIPART_STRICT_ERROR] = {CS_ONE, 1};
+              t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
+              t.single[S_REQBODY_ERROR_MSG] = mp_err_msg(err);
+            }
+          } else if (t.body_proc == BP_XML) {
+            // [upstream xml.go]: XML "//@*" / "/*", no REQUEST_BODY; an error ->
+            // generateRequestBodyError (REQBODY_ERROR_MSG "XML: <error>")
+            JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
+            Str msg{CS_ZERO, 0};
+            const int xr = parse_xml(jc, D + rq.body.off, bn, (uint32_t*)t.t0, t.cap_t / 4, &msg);
+            t.nf = jc.nf;
+            t.nb = jc.nb;
+            t.flags = jc.flags;
+            if (xr == 1) {
+              t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
+              t.single[S_REQBODY_ERROR_MSG] = msg;
+            }
+          } else if (t.body_proc != BP_NONE) {
+            t.flags |= GI_REQ_UNSUPPORTED_BODY;
+          }
+          if (t.nf != H->nf) t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
+        }
+      }
+      if ((t.flags & GI_REQ_ERROR_MASK) || !run2) break;
+    }
+    const uint64_t c0 = B.prof ? clock64() : 0;
+    eval_phase<W>(t, ph);
+    if (B.prof && lead) atomicAdd(&B.prof[ph], (unsigned long long)(clock64() - c0));
+  }
+  if (B.prof && lead) {
+    atomicAdd(&B.prof[0], (unsigned long long)(c_init - c_start));
+    atomicAdd(&B.prof[3], (unsigned long long)(clock64() - c_start));
+    atomicAdd(&B.prof[4], (unsigned long long)t.prof_visits);
+    atomicAdd(&B.prof[5], (unsigned long long)t.prof_evals);
+    atomicAdd(&B.prof[6], (unsigned long long)t.prof_rules);
+    atomicAdd(&B.prof[7], (unsigned long long)t.prof_eval_cyc);
+    atomicAdd(&B.prof[8], (unsigned long long)t.prof_act_cyc);
+  }
+  gi_verdict v;
+  v.rule_id = t.interrupted ? t.int_rule : 0;
+  v.status = t.interrupted ? t.int_status : 0;
+  v.action = t.interrupted ? t.int_action : 0;
+  v.phase = t.interrupted ? t.int_phase : 0;
+  v.capture_cnt = 0;
+  v._pad = 0;
+  if (t.capws) {
+    const CapHdr* CH = (const CapHdr*)t.capws;
+    v.capture_cnt = CH->nrec;
+    if (CH->trunc) t.flags |= GI_REQ_CAPTURE_TRUNC;
+  }
+  v.flags = t.flags;
+  v.match_cnt = t.nmatched;
+  for (uint32_t e = 0; e < GI_MAX_EXPORTS; e++) {
+    int64_t x = 0;
+    if (e < P.n_exports && P.exports[e] >= 0) {
+      bool okk;
+      x = slot_int(TXS(t, P.exports[e]), &okk);
+      if (!okk) x = 0;
+    }
+    v.tx_export[e] = x;
+  }
+  if (lead) B.verdicts[r] = v;
+  my[0] = 1;
+  my[1] = t.interrupted ? 1 : 0;
+  my[2] = t.nmatched ? 1 : 0;
+  my[3] = (t.flags & GI_REQ_ERROR_MASK) ? 1 : 0;
+  my[4] = scanned;
+  my[5] = t.nmatched;
+  my[6] = t.pa_void ? 1 : 0;
+}
+
+// Requests k_eval hands to k_eval_wave: many fields (a POST body's
+// ARGS_POST, multipart collections) or a large program (rule walks of
+// thousands of rules), where the lanes of one wave split the field loops and
+// the rule walk instead of one lane doing both alone.
+__device__ __forceinline__ bool eval_heavy(const DProgram& P, const DBatch& B, uint32_t r) {
+  if (!B.wlist) return false;
+  if (B.wave_rules && P.top_end[1] - P.top_begin[0] >= B.wave_rules) return true;
+  const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
+  return B.wave_fields && (H->nf + H->n_post >= B.wave_fields || B.reqs[r].body.len >= 16u * B.wave_fields);
+}
+
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVAL_WPE, 8))) k_eval(DProgram P, DBatch B) {
   __shared__ unsigned long long red[7];
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -6003,245 +6354,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
   __syncthreads();
   unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
   if (r < B.n_req) {
-    const uint64_t c_start = B.prof ? clock64() : 0;
-    const gi_request rq = B.reqs[r];
-    Region g = region_of(P, B, r);
-    ReqHdr* H = g.hdr;
-    Tx t;
-    t.prof_visits = t.prof_evals = t.prof_rules = 0;
-    t.prof_eval_cyc = t.prof_act_cyc = 0;
-    t.profon = B.prof != nullptr;
-    t.prof_rule_cyc = B.prof ? B.prof + 128 : nullptr;
-    tx_bind(t, P, g);
-    t.hits = B.hits;
-    t.vmap = B.vmap + B.layout[r].vmap_bit;
-    {
-      const ReqLayout Lr = B.layout[r];
-      const uint32_t* tab = B.hset + Lr.hset_word;
-      t.hset = (Lr.hset_mask && tab[0] == 0u) ? tab : nullptr;
-      t.hmask = Lr.hset_mask;
-    }
-    t.nf_pa = H->nf;
-    t.n_req = B.n_req;
-    t.req = r;
-    t.slots = B.txslots + r;
-    t.has_post = false;
-    t.body_spec = false;
-    t.pa_void = H->pa_void != 0;
-    t.nf = H->nf;
-    t.nb = H->nb;
-    t.flags = H->flags;
-    t.body_proc = H->body_proc;
-    t.ntx = 0;
-    t.nremoved = 0;
-    t.nrtgt = 0;
-    t.kx = nullptr;
-    t.engine = P.rule_engine;
-    t.body_access = P.body_access;
-    t.force_body = 0;
-    t.phase = 0;
-    t.skip_after = -1;
-    t.skip = 0;
-    t.interrupted = false;
-    t.int_rule = 0;
-    t.int_status = 0;
-    t.int_action = 0;
-    t.int_phase = 0;
-    t.nmatched = 0;
-    t.mout = B.matched + (uint64_t)r * B.mcap;
-    t.cur_id = 0;
-    if (t.capws) {
-      CapHdr* CH = (CapHdr*)t.capws;
-      CH->nrec = CH->nbytes = 0;
-      CH->rec = B.caprec ? B.caprec + 4ull * B.crcap * r : nullptr;
-      CH->bytes = B.capbytes ? B.capbytes + (uint64_t)B.cbcap * r : nullptr;
-      CH->rec_cap = B.crcap;
-      CH->bytes_cap = B.cbcap;
-      CH->trunc = 0;
-    }
-    t.mcap = B.mcap;
-    for (uint32_t s = 0; s < P.n_slots; s++) TXS(t, s).state = 0;
-    if (t.mv) {
-      t.mv->n = t.mv->nb = 0;
-      t.mv->cap_e = g.cap_f + 16;
-      t.mv->cap_a = g.cap_b + g.cap_mt;
-      t.mv->cap_v = g.cap_t;
-      t.mv->cap_n = g.cap_mt;
-      t.mv->cur_vn = t.mv->cur_nn = 0;
-    }
-    const uint8_t* D = B.data;
-    uint64_t scanned = (uint64_t)rq.method.len + rq.uri.len + rq.proto.len + rq.body.len;
-    for (uint32_t h = 0; h < rq.hdr_count; h++) {
-      const gi_header hd = B.headers[rq.hdr_begin + h];
-      scanned += hd.name.len + hd.value.len;
-    }
-    t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
-    const uint64_t c_init = B.prof ? clock64() : 0;
-    // phase 1, ProcessRequestBody, phase 2 (one eval_phase call site)
-    for (uint8_t ph = 1; ph <= 2 && !(t.flags & GI_REQ_ERROR_MASK); ph++) {
-      if (ph == 2) {
-        if (t.interrupted || t.engine == ENGINE_OFF) break;
-        uint32_t bn = rq.body.len;
-        bool run2 = true;
-        if (t.body_access && bn > 0) {
-          // [upstream transaction.go WriteRequestBody]: over SecRequestBodyLimit
-          // -> INBOUND_DATA_ERROR; Reject: interruption 413 (no rule id) and no
-          // ProcessRequestBody; ProcessPartial: the first limit bytes.
-          // ProcessRequestBody: a buffer of exactly the limit sets it too and,
-          // with Reject, returns before phase 2.  (DetectionOnly + Reject:
-          // nothing buffered.)
-          if (bn > P.body_limit) {
-            t.single[S_INBOUND_DATA_ERROR] = {CS_ONE, 1};
-            if (!P.body_partial) {
-              if (t.engine == ENGINE_ON) {
-                t.interrupted = true;
-                t.int_rule = 0;
-                t.int_status = 413;
-                t.int_action = GI_ACTION_DENY;
-                t.int_phase = 2;
-                break;
-              }
-              bn = 0;
-            } else {
-              bn = (uint32_t)P.body_limit;
-            }
-          }
-          if (bn > 0 && bn >= P.body_limit) {
-            t.single[S_INBOUND_DATA_ERROR] = {CS_ONE, 1};
-            if (!P.body_partial) run2 = false;
-          }
-        }
-        if (t.body_access && bn > 0 && run2) {
-          {
-            uint8_t* lb = tx_alloc(t, 24);
-            if (lb) t.single[S_REQUEST_BODY_LENGTH] = {lb, go_itoa((int64_t)bn, lb)};
-            if (t.force_body && t.body_proc == BP_NONE) {
-              t.body_proc = BP_URLENCODED;
-              t.single[S_REQBODY_PROCESSOR] = {CS_URLENCODED, 10};
-            }
-            if (t.body_proc == BP_URLENCODED || t.body_proc == BP_JSON) {
-              t.single[S_REQUEST_BODY] = {D + rq.body.off, bn};
-              if (t.body_proc == H->spec_proc) {
-                t.nf += H->n_post;  // k_collect's fields, already in phase A
-                t.nf_pa = t.nf;
-                t.body_spec = true;
-              } else {
-                const uint32_t nf0 = t.nf;
-                if (t.body_proc == BP_URLENCODED) parse_query(t, D + rq.body.off, bn, FK_ARG_POST);
-                else {
-                  JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
-                  parse_json_body_ool(&jc, D + rq.body.off, bn);
-                  t.nf = jc.nf;
-                  t.nb = jc.nb;
-                  t.flags = jc.flags;
-                  if (t.flags & GI_REQ_BODY_ERROR) {
-                    // readJSON's error -> generateRequestBodyError: REQBODY_ERROR "1",
-                    // REQBODY_ERROR_MSG "<processor>: <error>", no ARGS_POST, no REQUEST_BODY;
-                    // phase 2 still runs (CRS base rule 200002 denies with 400)
-                    t.nf = nf0;
-                    t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
-                    t.single[S_REQBODY_ERROR_MSG] = {CS_JSON_ERR, 18};
-                    t.single[S_REQUEST_BODY] = {CS_ZERO, 0};
-                  }
-                }
-                t.has_post = t.nf > nf0;
-              }
-            } else if (t.body_proc == BP_MULTIPART) {
-              // [upstream multipart.go]: collections, no REQUEST_BODY; an error
-              // -> MULTIPART_STRICT_ERROR + generateRequestBodyError (rules
-              // 200002 / 200003 deny with 400)
-              uint8_t err;
-              if (H->spec_proc == BP_MULTIPART) {
-                t.nf += H->n_post;  // k_bparse's fields (ARGS_POST already in phase A)
-                t.nf_pa = t.nf;
-                t.body_spec = true;
-                err = H->spec_err;
-              } else {
-                const uint32_t nf0 = t.nf;
-                JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
-                const Str ct = first_content_type(B, rq);
-                uint64_t comb;
-                bool comb_set;
-                err = parse_multipart(jc, D + rq.body.off, bn, ct.p, ct.n, &comb, &comb_set);
-                t.nf = jc.nf;
-                t.nb = jc.nb;
-                t.flags = jc.flags;
-                if (comb_set && !(t.flags & GI_REQ_ERROR_MASK)) {
-                  uint8_t* cb = tx_alloc(t, 24);
-                  if (cb) t.single[S_FILES_COMBINED_SIZE] = {cb, go_itoa((int64_t)comb, cb)};
-                }
-                t.has_post = t.nf > nf0;
-              }
-              if (err) {
-                t.single[S_MULTIPART_STRICT_ERROR] = {CS_ONE, 1};
-                t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
-                t.single[S_REQBODY_ERROR_MSG] = mp_err_msg(err);
-              }
-            } else if (t.body_proc == BP_XML) {
-              // [upstream xml.go]: XML "//@*" / "/*", no REQUEST_BODY; an error ->
-              // generateRequestBodyError (REQBODY_ERROR_MSG "XML: <error>")
-              JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
-              Str msg{CS_ZERO, 0};
-              const int xr = parse_xml(jc, D + rq.body.off, bn, (uint32_t*)t.t0, t.cap_t / 4, &msg);
-              t.nf = jc.nf;
-              t.nb = jc.nb;
-              t.flags = jc.flags;
-              if (xr == 1) {
-                t.single[S_REQBODY_ERROR] = {CS_ONE, 1};
-                t.single[S_REQBODY_ERROR_MSG] = msg;
-              }
-            } else if (t.body_proc != BP_NONE) {
-              t.flags |= GI_REQ_UNSUPPORTED_BODY;
-            }
-            if (t.nf != H->nf) t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
-          }
-        }
-        if ((t.flags & GI_REQ_ERROR_MASK) || !run2) break;
-      }
-      const uint64_t c0 = B.prof ? clock64() : 0;
-      eval_phase(t, ph);
-      if (B.prof) atomicAdd(&B.prof[ph], (unsigned long long)(clock64() - c0));
-    }
-    if (B.prof) {
-      atomicAdd(&B.prof[0], (unsigned long long)(c_init - c_start));
-      atomicAdd(&B.prof[3], (unsigned long long)(clock64() - c_start));
-      atomicAdd(&B.prof[4], (unsigned long long)t.prof_visits);
-      atomicAdd(&B.prof[5], (unsigned long long)t.prof_evals);
-      atomicAdd(&B.prof[6], (unsigned long long)t.prof_rules);
-      atomicAdd(&B.prof[7], (unsigned long long)t.prof_eval_cyc);
-      atomicAdd(&B.prof[8], (unsigned long long)t.prof_act_cyc);
-    }
-    gi_verdict v;
-    v.rule_id = t.interrupted ? t.int_rule : 0;
-    v.status = t.interrupted ? t.int_status : 0;
-    v.action = t.interrupted ? t.int_action : 0;
-    v.phase = t.interrupted ? t.int_phase : 0;
-    v.capture_cnt = 0;
-    v._pad = 0;
-    if (t.capws) {
-      const CapHdr* CH = (const CapHdr*)t.capws;
-      v.capture_cnt = CH->nrec;
-      if (CH->trunc) t.flags |= GI_REQ_CAPTURE_TRUNC;
-    }
-    v.flags = t.flags;
-    v.match_cnt = t.nmatched;
-    for (uint32_t e = 0; e < GI_MAX_EXPORTS; e++) {
-      int64_t x = 0;
-      if (e < P.n_exports && P.exports[e] >= 0) {
-        bool okk;
-        x = slot_int(TXS(t, P.exports[e]), &okk);
-        if (!okk) x = 0;
-      }
-      v.tx_export[e] = x;
-    }
-    B.verdicts[r] = v;
-    my[0] = 1;
-    my[1] = t.interrupted ? 1 : 0;
-    my[2] = t.nmatched ? 1 : 0;
-    my[3] = (t.flags & GI_REQ_ERROR_MASK) ? 1 : 0;
-    my[4] = scanned;
-    my[5] = t.nmatched;
-    my[6] = t.pa_void ? 1 : 0;
+    if (eval_heavy(P, B, r)) B.wlist[atomicAdd(B.wcount, 1u)] = r;
+    else eval_request<false>(P, B, r, nullptr, my);
   }
   for (int c = 0; c < 7; c++) {
     unsigned long long x = my[c];
@@ -6250,6 +6364,31 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
   }
   __syncthreads();
   if (threadIdx.x < 7) atomicAdd(&B.tally[threadIdx.x], red[threadIdx.x]);
+}
+
+// One wave per heavy request (k_eval's list), persistent over the list.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_EVAL_WPE, 8))) k_eval_wave(DProgram P, DBatch B) {
+  extern __shared__ uint32_t whits[];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t nw = (B.n_hit_slots + 31) / 32;
+  const bool in_lds = nw <= GI_EVAL_WAVE_LDS_WORDS;
+  unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  const uint32_t n = min(*B.wcount, B.n_req);
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t r = B.wlist[i];
+    GI_BOUND(r < B.n_req, r, i);
+    if (in_lds) {
+      __syncthreads();
+      for (uint32_t w = lane; w < nw; w += 64) whits[w] = B.hits[(uint64_t)w * B.n_req + r];
+      __syncthreads();
+    }
+    unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
+    eval_request<true>(P, B, r, in_lds ? whits : nullptr, my);
+    for (int c = 0; c < 7; c++) acc[c] += my[c];
+  }
+  if (lane == 0)
+    for (int c = 0; c < 7; c++)
+      if (acc[c]) atomicAdd(&B.tally[c], acc[c]);
 }
 
 // Detail tally: histogram of the first exported TX value and
@@ -6404,6 +6543,11 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
   {  // small batches (fewer than 4 workgroups of 128 per CU): one wave per workgroup to spread over all CUs
     const uint32_t ev_bs = (B.n_req + 127) / 128 < 1024 ? 64u : 128u;
     GI_LAUNCH("k_eval", k_eval, dim3((B.n_req + ev_bs - 1) / ev_bs), dim3(ev_bs), 0, stream, P, B);
+  }
+  if (B.wlist) {  // heavy requests, one wave each (persistent over k_eval's list)
+    const uint32_t nw = (B.n_hit_slots + 31) / 32;
+    const uint32_t lds = nw <= GI_EVAL_WAVE_LDS_WORDS ? 4 * std::max<uint32_t>(nw, 1u) : 0u;
+    GI_LAUNCH("k_eval_wave", k_eval_wave, dim3(std::min<uint32_t>(B.n_req, 8192)), dim3(64), lds, stream, P, B);
   }
   {
     const uint32_t lds = n_tally_ids <= GI_RHIST_LDS ? 4 * (2 * n_tally_ids + GI_SCORE_BINS) : 0;

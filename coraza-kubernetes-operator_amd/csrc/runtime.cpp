@@ -88,8 +88,9 @@ struct gi_ctx {
   bool cap_on = false;
   std::vector<uint32_t> tally_ids;
   // phase A
-  DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf;
+  DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf, wlist;
   uint32_t long_cap = 0, long_grid = GI_LONG_GRID;
+  uint32_t wave_fields = GI_EVAL_WAVE_FIELDS, wave_rules = GI_EVAL_WAVE_RULES;  // k_eval_wave thresholds
   uint64_t long_bufcap = 0;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0, det_cap = 0;
   uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0, det_bytes_cap = 0;
@@ -451,6 +452,8 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->mcap = matched_cap ? matched_cap : 64;
   c->diag_on = getenv("GI_DIAG") && atoi(getenv("GI_DIAG")) > 0;
   c->prof_on = getenv("GI_PROF") && atoi(getenv("GI_PROF")) > 0;
+  if (getenv("GI_EVAL_WAVE_FIELDS")) c->wave_fields = (uint32_t)atoi(getenv("GI_EVAL_WAVE_FIELDS"));  // A/B, 0: off
+  if (getenv("GI_EVAL_WAVE_RULES")) c->wave_rules = (uint32_t)atoi(getenv("GI_EVAL_WAVE_RULES"));
   c->stop_after = getenv("GI_STOP_AFTER") ? atoi(getenv("GI_STOP_AFTER")) : 0;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -501,7 +504,7 @@ void gi_ctx_free(gi_ctx* c) {
   c->prof.release();
   for (DevBuf* b : {&c->caprec, &c->capbytes, &c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->hset, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
-                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf})
+                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist})
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
@@ -752,6 +755,9 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if ((e = c->det.ensure(std::max<uint64_t>(32ull * c->det_cap, 64))) != hipSuccess) return hip_fail(c, e, "alloc detect list");
     if ((e = c->det_bytes.ensure(c->det_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc detect bytes");
   }
+  // k_eval -> k_eval_wave request list (its counter lives in ctr)
+  if ((e = c->ctr.ensure(384)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+  if ((e = c->wlist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc wave list");
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && n) e = hipMemcpyAsync(c->reqs.p, in->reqs, n * sizeof(gi_request), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && in->n_headers)
@@ -850,6 +856,11 @@ int gi_run_staged(gi_ctx* c) {
     B.n_hit_slots = c->rs->prog.n_hit_slots;
     B.vcause = (unsigned long long*)(cp + 288);  // 5 void-cause counters
     B.dbg = (uint32_t*)(cp + 128);  // 4 words (only written by -DGI_DEBUG builds)
+    const bool wave = (c->wave_fields || c->wave_rules) && c->wlist.p && cp;
+    B.wlist = wave ? (uint32_t*)c->wlist.p : nullptr;
+    B.wcount = wave ? (uint32_t*)(cp + 48) : nullptr;
+    B.wave_fields = c->wave_fields;
+    B.wave_rules = c->wave_rules;
   }
   (void)hipEventRecord(c->ev0, c->stream);
   if (c->ctr.p) {
@@ -955,6 +966,10 @@ int gi_sync(gi_ctx* c) {
                 "GI_PROF k_eval per request: init %.0f cyc, phase1 %.0f, phase2 %.0f, total %.0f; rule visits %.1f, "
                 "evaluated %.1f, matched %.1f; eval_rule %.0f cyc, actions %.0f cyc\n",
                 h[0] / n, h[1] / n, h[2] / n, h[3] / n, h[4] / n, h[5] / n, h[6] / n, h[7] / n, h[8] / n);
+        fprintf(stderr,
+                "GI_PROF k_eval_wave per request: fields filtered %.1f, survivors exact %.1f / evaluated %.1f; "
+                "filter %.0f cyc, ordered tests %.0f cyc\n",
+                h[17] / n, h[18] / n, h[19] / n, h[20] / n, h[21] / n);
         std::vector<unsigned long long> rc(1000);
         if (hipMemcpy(rc.data(), (uint8_t*)c->prof.p + 1024, 8000, hipMemcpyDeviceToHost) == hipSuccess) {
           std::vector<std::pair<unsigned long long, uint32_t>> v;
