@@ -116,7 +116,7 @@ struct ScanLaunch {
 #define GI_LONG_GRID 512     // k_long workgroups (at most)
 #define GI_LONG_BUDGET (4ull << 30)  // bytes of k_long chain buffers (runtime.cpp gi_stage_batch)
 #define GI_EVAL_WAVE_LDS_WORDS 4096  // k_eval_wave keeps a request's hit words in LDS up to this many
-#define GI_EVAL_WAVE_FIELDS 2048     // default k_eval_wave thresholds (GI_EVAL_WAVE_FIELDS / _RULES env)
+#define GI_EVAL_WAVE_FIELDS 4096     // default k_eval_wave thresholds (GI_EVAL_WAVE_FIELDS / _RULES env)
 #define GI_EVAL_WAVE_RULES 2048
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.

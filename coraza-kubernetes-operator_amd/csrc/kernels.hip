@@ -4968,10 +4968,28 @@ __device__ void det_maybe(const DProgram& P, const DBatch& B, uint32_t r, uint32
   }
 }
 
-__device__ void det_push(const DProgram& P, const DBatch& B, uint32_t r, uint32_t vix, uint64_t gm, uint32_t mask,
-                         const uint8_t* v, uint32_t n) {
-  const uint32_t k = atomicAdd(B.det_count, 1u);
-  const unsigned long long off = atomicAdd(B.det_used, (unsigned long long)((n + 15) & ~15u));
+// Called by the whole wave (uniform control flow); lanes with `push` list
+// their value.  One leader lane reserves the wave's entries and bytes (two
+// atomics per wave instead of two per candidate on the same two counters).
+__device__ void det_push(const DProgram& P, const DBatch& B, bool push, uint32_t r, uint32_t vix, uint64_t gm,
+                         uint32_t mask, const uint8_t* v, uint32_t n) {
+  const uint64_t am = __ballot(push);
+  if (!am) return;
+  uint32_t btot;
+  const uint32_t boff = wave_excl_sum(push ? (n + 15) & ~15u : 0u, &btot);
+  const int leader = __ffsll((unsigned long long)am) - 1;
+  uint32_t k0 = 0;
+  unsigned long long o0 = 0;
+  if (lane_id() == (uint32_t)leader) {
+    k0 = atomicAdd(B.det_count, (uint32_t)__popcll(am));
+    o0 = atomicAdd(B.det_used, (unsigned long long)btot);
+  }
+  k0 = (uint32_t)__shfl((int)k0, leader, 64);
+  o0 = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(o0 >> 32), leader, 64) << 32) |
+       (uint32_t)__shfl((int)(uint32_t)o0, leader, 64);
+  if (!push) return;
+  const uint32_t k = k0 + mask_rank(am);
+  const unsigned long long off = o0 + boff;
   if (k >= B.det_cap || off + n > B.det_bytes_cap) {
     det_maybe(P, B, r, vix, gm, mask);
     return;
@@ -5168,6 +5186,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
       pc_fm += c_sa - c_s0;
       const uint8_t* cur = nullptr;
       int64_t cn = 0;
+      bool det_append = false;  // this stream's output is a @detectSQLi/@detectXSS candidate (k_detect)
       uint32_t osum = summ;  // byte summary of the chain output
       bool maybe = false, glob = !IN;
       if (fm) {
@@ -5183,13 +5202,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
           cur = src;
           cn = 0;
         }
-        if (S.val_count) {
-          bool det_append = false;
+        if (S.val_count)
           stream_vals(P, B, it.req, meta_vix(it.meta), S, fm, maybe, cur, (uint32_t)cn, osum, !maybe && cur == src,
                       &rawmask, &det_append);
-          if (det_append) det_push(P, B, it.req, meta_vix(it.meta), gm, 1u << S.det_id, cur, (uint32_t)cn);
-        }
       }
+      if (S.val_count) det_push(P, B, det_append, it.req, meta_vix(it.meta), gm, 1u << S.det_id, cur, (uint32_t)cn);
       const uint64_t c_s1 = B.prof ? clock64() : 0;
       pc_chain += c_s1 - c_s0;
       if (!S.job_count) continue;
@@ -5294,7 +5311,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
       }
       if (B.prof) pc_out += clock64() - c_s2;
     }
-    if (rawmask) det_push(P, B, it.req, meta_vix(it.meta), gm, rawmask, src, it.vn);
+    det_push(P, B, rawmask != 0, it.req, meta_vix(it.meta), gm, rawmask, src, it.vn);
     if (B.prof) pc_loop += clock64() - c_b;
   }
   if (lane == 0 && wwords) atomicAdd(&B.acct[5 + bucket], (unsigned long long)wwords);
@@ -6344,7 +6361,7 @@ __device__ __forceinline__ bool eval_heavy(const DProgram& P, const DBatch& B, u
   if (!B.wlist) return false;
   if (B.wave_rules && P.top_end[1] - P.top_begin[0] >= B.wave_rules) return true;
   const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
-  return B.wave_fields && (H->nf + H->n_post >= B.wave_fields || B.reqs[r].body.len >= 16u * B.wave_fields);
+  return B.wave_fields && H->nf + H->n_post >= B.wave_fields;
 }
 
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVAL_WPE, 8))) k_eval(DProgram P, DBatch B) {
