@@ -111,6 +111,44 @@ def parity(res, verdicts):
                    "ordered matched ids, exported TX values, unsupported flag (oracle/compare.py)"}
 
 
+def e2e_pipelined(rs, eng, batch, device, matched_cap, iters, raw):
+    """Steady-state host-inclusive throughput: two contexts on one GPU take
+    turns; while context A runs batch k, the host fetches batch k-1 from B and
+    stages batch k+1 into B (layout on the host cores, H2D from page-locked
+    memory on B's stream).  The same request set is inspected every time."""
+    eng2 = gpuinspect.Engine(rs, device=device, matched_cap=matched_cap)
+    engines = [eng, eng2]
+    pinned = eng.pin(batch.data, batch.reqs, batch.headers)
+    for e in engines:
+        e.stage(batch)  # allocations happen here, outside the timed loop
+        e.pin(*[a for a in e.result_buffers(batch.n_req)])
+    stage_s = fetch_s = 0.0
+    t0 = time.perf_counter()
+    engines[0].stage(batch)
+    for k in range(iters):
+        cur, other = engines[k % 2], engines[(k + 1) % 2]
+        cur.run()  # asynchronous on cur's stream
+        if k > 0:
+            ta = time.perf_counter()
+            other.fetch(reuse=True)  # batch k-1 (its kernels finished at the last sync)
+            fetch_s += time.perf_counter() - ta
+        if k + 1 < iters:
+            ta = time.perf_counter()
+            other.stage(batch)  # batch k+1
+            stage_s += time.perf_counter() - ta
+        cur.sync()
+    engines[(iters - 1) % 2].fetch(reuse=True)
+    dt = time.perf_counter() - t0
+    eng2.close()
+    eng.unpin()
+    return {"requests_per_s": round(iters * batch.n_req / dt, 1), "GB/s": round(iters * raw / dt / 1e9, 3),
+            "iters": iters, "ms_per_batch": round(dt / iters * 1e3, 2),
+            "host_stage_ms_per_batch": round(stage_s / max(iters - 1, 1) * 1e3, 2),
+            "host_fetch_ms_per_batch": round(fetch_s / max(iters - 1, 1) * 1e3, 2), "pinned_arrays": pinned,
+            "def": "two contexts alternating: H2D of batch k+1 (page-locked) and D2H of batch k-1 overlap batch k's "
+                   "kernels; includes every stage, run and fetch"}
+
+
 def log(msg):
     """Progress on stderr (a long compile or batch must not look hung to a watchdog)."""
     sys.stderr.write("[bench %s] %s\n" % (time.strftime("%H:%M:%S"), msg))
@@ -127,6 +165,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--matched-cap", type=int, default=64)
     ap.add_argument("--no-balance", action="store_true", help="N > 1: keep each rank's own chunk (no byte balancing)")
+    ap.add_argument("--e2e-iters", type=int, default=4, help="batches in the pipelined host-inclusive leg (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -302,8 +341,11 @@ def main():
     }
     if split is not None:
         out["split"] = dict(split, set_requests=int(total_req))
-    # Host-inclusive pass: stage (layout + H2D of pageable numpy buffers) +
-    # pipeline + D2H of verdicts and matched ids.  Never `value`.
+    # Host-inclusive passes (never `value`).  serial: one stage (host layout +
+    # H2D of pageable numpy buffers) + pipeline + D2H of verdicts and matched
+    # ids.  pipelined: the batch's buffers page-locked (gi_host_register) and
+    # two contexts alternating, so batch k+1's staging and batch k-1's fetch
+    # overlap batch k's kernels (steady-state requests/s over e2e_iters batches).
     t1 = time.perf_counter()
     eng.stage(batch)
     t2 = time.perf_counter()
@@ -317,6 +359,11 @@ def main():
                   "fetch_ms": round((t4 - t3) * 1e3, 2),
                   "GB/s": round(raw / (t4 - t1) / 1e9, 3),
                   "def": "one pass incl. gi_stage_batch (host layout + H2D, pageable) and gi_fetch_results (D2H), per GPU"}
+    if args.e2e_iters > 0:
+        try:
+            out["e2e"]["pipelined"] = e2e_pipelined(rs, eng, batch, local, args.matched_cap, args.e2e_iters, raw)
+        except gpuinspect.EngineError as ex:  # e.g. not enough HBM for a second context: reported, not fatal
+            out["e2e"]["pipelined"] = {"error": str(ex)[:200]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline / parity sample (oracle)")
         verdicts, wall, procs = oracle_sample(text, batch, rs.exports, files=files,

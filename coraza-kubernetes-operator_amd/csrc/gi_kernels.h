@@ -64,6 +64,7 @@ struct DBatch {
   unsigned long long* acct;   // algorithmic-byte counters: [0..5) item bytes per bucket, [5..10) queue
                               // words written per k_stream bucket, [10..13) queue words read per k_scan launch,
                               // [13..16) automaton byte steps per k_scan launch
+  unsigned long long* acct3;  // [0..5) items per length bucket, summed over the chunks of a run
   unsigned long long* acct2;  // byte steps: [0..5) value bytes into stream chains per k_stream bucket,
                               // [5] value bytes through libinjection (k_detect)
   uint32_t qcap;
@@ -95,6 +96,8 @@ struct DBatch {
   uint32_t* wcount;
   uint32_t wave_fields;       // k_eval_wave: requests with this many fields (0: none)
   uint32_t wave_rules;        // k_eval_wave: every request when the program walks this many rules (0: never)
+  uint32_t rstride;           // request stride of the request-major SoA arrays (hits, txslots): the staged
+                              // batch's size (a chunk view of it has n_req <= rstride)
 };
 
 // k_scan launch plan: job lists for the small-LDS and big-LDS launches.
@@ -118,6 +121,7 @@ struct ScanLaunch {
 #define GI_EVAL_WAVE_LDS_WORDS 4096  // k_eval_wave keeps a request's hit words in LDS up to this many
 #define GI_EVAL_WAVE_FIELDS 4096     // default k_eval_wave thresholds (GI_EVAL_WAVE_FIELDS / _RULES env)
 #define GI_EVAL_WAVE_RULES 2048
+#define GI_CHUNK_POOL_WORDS 16e9     // queue-pool words (estimate) one request chunk of a batch may need
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.
 uint32_t scan_resident_blocks(uint32_t lds_bytes);
@@ -128,7 +132,7 @@ void scan_allow_lds(uint32_t lds_bytes);
 // ev (optional) = 3 events recorded after k_collect, k_stream and k_scan.
 // Per-launch HIP events of one pipeline run (ev[0] before the first launch,
 // ev[k + 1] after launch k).
-#define GI_MAX_LAUNCHES GI_STATS_LAUNCHES
+#define GI_MAX_LAUNCHES 256  // launches of one run (a chunked batch repeats the pipeline; gi_stats sums by name)
 struct LaunchLog {
   hipEvent_t ev[GI_MAX_LAUNCHES + 1];
   const char* name[GI_MAX_LAUNCHES];

@@ -4298,7 +4298,7 @@ __device__ __noinline__ void gi_dbg_fail(const DBatch& B, uint32_t line, uint64_
 
 __device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
   GI_BOUND(r < B.n_req && slot < B.n_hit_slots, slot, r);
-  atomicOr(&B.hits[(uint64_t)(slot >> 5) * B.n_req + r], 1u << (slot & 31));
+  atomicOr(&B.hits[(uint64_t)(slot >> 5) * B.rstride + r], 1u << (slot & 31));
 }
 
 // cause (GI_VOID_*): which capacity ran out (counted in B.vcause for GI_DIAG)
@@ -4848,6 +4848,7 @@ __global__ void __launch_bounds__(1024) k_ioffsets(DBatch B, uint32_t n_blocks) 
       }
       B.ibk[2 * b] = base_s;
       B.ibk[2 * b + 1] = run;
+      atomicAdd(&B.acct3[b], (unsigned long long)run);
     }
     __syncthreads();
     uint32_t run = base_s + part[t];
@@ -6122,7 +6123,7 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
   t.prof_rule_cyc = B.prof ? B.prof + 128 : nullptr;
   tx_bind(t, P, g);
   t.hits = whits ? whits : B.hits + r;
-  t.hstride = whits ? 1u : B.n_req;
+  t.hstride = whits ? 1u : B.rstride;
   t.vmap = B.vmap + B.layout[r].vmap_bit;
   {
     const ReqLayout Lr = B.layout[r];
@@ -6131,7 +6132,7 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
     t.hmask = Lr.hset_mask;
   }
   t.nf_pa = H->nf;
-  t.n_req = B.n_req;
+  t.n_req = B.rstride;  // TX slot stride
   t.req = r;
   t.slots = B.txslots + r;
   t.has_post = false;
@@ -6396,7 +6397,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_EVAL
     GI_BOUND(r < B.n_req, r, i);
     if (in_lds) {
       __syncthreads();
-      for (uint32_t w = lane; w < nw; w += 64) whits[w] = B.hits[(uint64_t)w * B.n_req + r];
+      for (uint32_t w = lane; w < nw; w += 64) whits[w] = B.hits[(uint64_t)w * B.rstride + r];
       __syncthreads();
     }
     unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -6512,11 +6513,7 @@ uint32_t scan_resident_blocks(uint32_t lds_bytes) {
 void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
                      int stop_after, LaunchLog* log, const uint32_t* tally_ids, uint32_t n_tally_ids) {
   if (!B.n_req) return;
-  int nk = 0;
-  if (log) {
-    log->n = 0;
-    (void)hipEventRecord(log->ev[0], stream);
-  }
+  int nk = 0;  // (the caller resets *log and records its ev[0] before the first chunk)
   const uint32_t cb = (B.n_req + 255) / 256;
   GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
   if (B.n_body && P.body_access) {

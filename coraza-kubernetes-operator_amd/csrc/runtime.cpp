@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -91,6 +92,19 @@ struct gi_ctx {
   DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf, wlist;
   uint32_t long_cap = 0, long_grid = GI_LONG_GRID;
   uint32_t wave_fields = GI_EVAL_WAVE_FIELDS, wave_rules = GI_EVAL_WAVE_RULES;  // k_eval_wave thresholds
+  // A staged batch runs as consecutive request chunks, each a full pipeline
+  // pass over its requests, so the phase-A buffers (items, queue pool, detect
+  // / slow / long lists) are sized for one chunk, not for the whole batch.
+  struct Chunk {
+    uint32_t r0, n;          // requests [r0, r0 + n)
+    uint32_t blist_off;      // its body list (longest first) in blist
+    uint32_t n_body, n_mp;
+  };
+  std::vector<Chunk> chunks;
+  double chunk_pool_words = GI_CHUNK_POOL_WORDS;
+  ReqLayout* lay_host = nullptr;  // page-locked host copy of the staged layout
+  uint32_t lay_host_cap = 0;
+  bool stage_prof = false;        // GI_STAGE_PROF=1: gi_stage_batch phase times on stderr  // queue-pool estimate a chunk may reach (GI_CHUNK_POOL_WORDS env)
   uint64_t long_bufcap = 0;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0, det_cap = 0;
   uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0, det_bytes_cap = 0;
@@ -454,6 +468,8 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->prof_on = getenv("GI_PROF") && atoi(getenv("GI_PROF")) > 0;
   if (getenv("GI_EVAL_WAVE_FIELDS")) c->wave_fields = (uint32_t)atoi(getenv("GI_EVAL_WAVE_FIELDS"));  // A/B, 0: off
   if (getenv("GI_EVAL_WAVE_RULES")) c->wave_rules = (uint32_t)atoi(getenv("GI_EVAL_WAVE_RULES"));
+  c->stage_prof = getenv("GI_STAGE_PROF") && atoi(getenv("GI_STAGE_PROF")) > 0;
+  if (getenv("GI_CHUNK_POOL_WORDS")) c->chunk_pool_words = std::max(1e6, atof(getenv("GI_CHUNK_POOL_WORDS")));
   c->stop_after = getenv("GI_STOP_AFTER") ? atoi(getenv("GI_STOP_AFTER")) : 0;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -512,6 +528,7 @@ void gi_ctx_free(gi_ctx* c) {
     if (ev) (void)hipEventDestroy(ev);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->lay_host) (void)hipHostFree(c->lay_host);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -520,14 +537,39 @@ const char* gi_last_error(const gi_ctx* c) { return c ? c->err.c_str() : "null c
 
 void* gi_ctx_stream(gi_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+int gi_host_register(gi_ctx* c, void* p, size_t n) {
+  if (!c || !p || !n) return GI_EINVAL;
+  (void)hipSetDevice(c->device);
+  const hipError_t e = hipHostRegister(p, n, hipHostRegisterDefault);
+  return e == hipSuccess ? GI_OK : hip_fail(c, e, "hipHostRegister");
+}
+
+int gi_host_unregister(gi_ctx* c, void* p) {
+  if (!c || !p) return GI_EINVAL;
+  (void)hipSetDevice(c->device);
+  const hipError_t e = hipHostUnregister(p);
+  return e == hipSuccess ? GI_OK : hip_fail(c, e, "hipHostUnregister");
+}
+
 int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if (!c || !in) return GI_EINVAL;
   if (in->n_req && (!in->reqs || !in->data)) return fail(c, GI_EINVAL, "null batch arrays");
   (void)hipSetDevice(c->device);
   auto t0 = std::chrono::steady_clock::now();
+  auto t_sizes = t0, t_plan = t0;
   const uint32_t n = in->n_req;
   // validate spans and lay out per-request scratch (lengths only)
-  std::vector<ReqLayout> lay(n);
+  // the layout lives in a page-locked host buffer of the ctx (reused), so its
+  // H2D is a DMA copy
+  if (c->lay_host_cap < n) {
+    if (c->lay_host) (void)hipHostFree(c->lay_host);
+    c->lay_host = nullptr;
+    c->lay_host_cap = 0;
+    if (hipHostMalloc((void**)&c->lay_host, std::max<size_t>(n, 1) * sizeof(ReqLayout)) == hipSuccess) c->lay_host_cap = n;
+    else c->lay_host = nullptr;
+  }
+  std::vector<ReqLayout> lay_v(c->lay_host ? 0 : n);
+  ReqLayout* lay = c->lay_host ? c->lay_host : lay_v.data();
   uint64_t off = 0, items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0, vmap_bits = 0, max_req_bytes = 0;
   uint64_t hset_words = 0;
   uint32_t n_mp_body = 0;
@@ -535,12 +577,25 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   const uint32_t nslots = c->rs->prog.n_slots;
   const Program& PG = c->rs->prog;
   const uint32_t n_single_items = (uint32_t)__builtin_popcount(PG.item_singles);
-  for (uint32_t r = 0; r < n; r++) {
+  // per-request sizes (in parallel on the host cores for large batches),
+  // then the running offsets (region, value map, hit set) in one serial pass
+  struct Sizes {
+    uint64_t region, vmap, hset;
+    uint64_t items, raw, body, post;  // phase-A items, bytes without / of the body, body fields
+    bool mp;                          // multipart body
+  };
+  struct Acc {
+    uint64_t items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0, max_req_bytes = 0;
+    uint32_t n_mp_body = 0, max_cap_t = 64;
+  };
+  std::vector<Sizes> sizes(n);
+  for (auto& z : sizes) z.mp = false;
+  auto size_one = [&](uint32_t r, Acc& a) -> const char* {
     const gi_request& q = in->reqs[r];
     const gi_span* sp[5] = {&q.method, &q.uri, &q.proto, &q.body, &q.remote_addr};
     for (auto* s : sp)
-      if (s->off + s->len > in->data_len) return fail(c, GI_EINVAL, "request span out of range");
-    if ((uint64_t)q.hdr_begin + q.hdr_count > in->n_headers) return fail(c, GI_EINVAL, "header range out of range");
+      if (s->off + s->len > in->data_len) return "request span out of range";
+    if ((uint64_t)q.hdr_begin + q.hdr_count > in->n_headers) return "header range out of range";
     uint64_t maxv = std::max<uint64_t>({(uint64_t)q.uri.len * 3 + 2, (uint64_t)q.method.len + q.uri.len + q.proto.len + 2,
                                         (uint64_t)q.body.len, 64});
     uint64_t cookie = 0, ncookie = 0, hdr_bytes = 0;
@@ -548,7 +603,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     for (uint32_t h = 0; h < q.hdr_count; h++) {
       const gi_header& hd = in->headers[q.hdr_begin + h];
       if (hd.name.off + hd.name.len > in->data_len || hd.value.off + hd.value.len > in->data_len)
-        return fail(c, GI_EINVAL, "header span out of range");
+        return "header span out of range";
       maxv = std::max<uint64_t>(maxv, std::max(hd.name.len, hd.value.len));
       hdr_bytes += hd.name.len + hd.value.len;
       if (hd.name.len == 12 && strncasecmp((const char*)in->data + hd.name.off, "content-type", 12) == 0) {
@@ -596,7 +651,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       // multipart (kernels.hip parse_multipart): a part spends >= 2 lines on
       // its delimiter and header end and yields <= 3 entries + 1 per header line
       if (multipart) post_fields += nls + 8;
-      n_mp_body += multipart ? 1 : 0;
+      a.n_mp_body += multipart ? 1 : 0;
+      sizes[r].mp = multipart;
     }
     uint64_t cap_f = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie) + post_fields;
     uint64_t cap_b = 4ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96 + 16;  // + REMOTE_PORT
@@ -618,20 +674,23 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     uint64_t cap_t = 3 * maxv + 64 + (q.body.len ? 8 * 64 : 0);  // k_body: 64 lane slots of 3x + 8 B
     uint64_t cap_mt = 2 * maxv + 512;
     if (cap_f > 0xFFFFFFFFull || cap_b > 0xFFFFFFFFull || cap_t > 0xFFFFFFFFull || cap_mt > 0xFFFFFFFFull)
-      return fail(c, GI_EINVAL, "request too large");
+      return "request too large";
     // phase-A items: at most both sides of every field (GET args, headers,
     // cookies; POST args appear after phase 1) plus the filtered singles
     const uint64_t pre_body_fields = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie);
-    items_cap += 2 * (pre_body_fields + (PG.body_access ? post_fields : 0)) + n_single_items;
-    post_total += PG.body_access ? post_fields : 0;
-    raw_total += (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
-    raw_body += q.body.len;
-    max_req_bytes = std::max<uint64_t>(max_req_bytes, (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes + q.body.len);
-    max_cap_t = (uint32_t)std::max<uint64_t>(max_cap_t, cap_t);
+    sizes[r].items = 2 * (pre_body_fields + (PG.body_access ? post_fields : 0)) + n_single_items;
+    sizes[r].post = PG.body_access ? post_fields : 0;
+    sizes[r].raw = (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
+    sizes[r].body = q.body.len;
+    a.items_cap += sizes[r].items;
+    a.post_total += PG.body_access ? post_fields : 0;
+    a.raw_total += (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
+    a.raw_body += q.body.len;
+    a.max_req_bytes = std::max<uint64_t>(a.max_req_bytes, (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes + q.body.len);
+    a.max_cap_t = (uint32_t)std::max<uint64_t>(a.max_cap_t, cap_t);
     ReqLayout& L = lay[r];
-    L.vmap_bit = vmap_bits;
     L.vmap_bits = (uint32_t)(2 * cap_f);
-    vmap_bits += (2 * cap_f + 31) & ~31ull;
+    sizes[r].vmap = (2 * cap_f + 31) & ~31ull;
     {  // exact hit set (kernels.hip hset_insert): ~one key per phase-A item; a fuller table
        // only sends the request back to re-evaluation (exact either way)
       uint64_t amps = 1;
@@ -642,10 +701,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       uint64_t cap = 16;
       while (cap < est && cap < (1ull << 16)) cap <<= 1;
       L.hset_mask = PG.streams.empty() ? 0u : (uint32_t)(cap - 1);
-      L.hset_word = hset_words;
-      hset_words += PG.streams.empty() ? 0 : (cap + 1 + 3) & ~3ull;
+      sizes[r].hset = PG.streams.empty() ? 0 : (cap + 1 + 3) & ~3ull;
     }
-    L.base = off;
     L.cap_f = (uint32_t)cap_f;
     L.cap_b = (uint32_t)cap_b;
     L.cap_t = (uint32_t)cap_t;
@@ -659,8 +716,47 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     // arena, MATCHED_VAR copy, name buffer
     if (PG.mv_used)
       sz += 64 + (cap_f + 16) * 32 + (cap_b + cap_mt + 15) / 16 * 16 + (cap_t + 15) / 16 * 16 + (cap_mt + 15) / 16 * 16;
-    off += (sz + 63) / 64 * 64;
+    sizes[r].region = (sz + 63) / 64 * 64;
+    return nullptr;
+  };
+  {
+    const uint32_t nt = n >= 65536 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+    std::vector<Acc> acc(nt);
+    std::vector<const char*> errs(nt, nullptr);
+    auto work = [&](uint32_t k) {
+      const uint32_t lo = (uint32_t)((uint64_t)n * k / nt), hi = (uint32_t)((uint64_t)n * (k + 1) / nt);
+      for (uint32_t r = lo; r < hi && !errs[k]; r++) errs[k] = size_one(r, acc[k]);
+    };
+    if (nt == 1) {
+      work(0);
+    } else {
+      std::vector<std::thread> th;
+      for (uint32_t k = 0; k < nt; k++) th.emplace_back(work, k);
+      for (auto& x : th) x.join();
+    }
+    for (uint32_t k = 0; k < nt; k++)
+      if (errs[k]) return fail(c, GI_EINVAL, errs[k]);
+    t_sizes = std::chrono::steady_clock::now();
+    for (const Acc& a : acc) {
+      items_cap += a.items_cap;
+      raw_total += a.raw_total;
+      raw_body += a.raw_body;
+      post_total += a.post_total;
+      max_req_bytes = std::max(max_req_bytes, a.max_req_bytes);
+      n_mp_body += a.n_mp_body;
+      max_cap_t = std::max(max_cap_t, a.max_cap_t);
+    }
+    for (uint32_t r = 0; r < n; r++) {
+      ReqLayout& L = lay[r];
+      L.base = off;
+      L.vmap_bit = vmap_bits;
+      L.hset_word = hset_words;
+      off += sizes[r].region;
+      vmap_bits += sizes[r].vmap;
+      hset_words += sizes[r].hset;
+    }
   }
+  t_plan = std::chrono::steady_clock::now();
   hipError_t e = hipSuccess;
   hipStream_t s = c->stream;
   // +16: word-granular readers may touch up to 7 bytes past a value's end
@@ -690,15 +786,63 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   c->vmap_words = vmap_bits;  // one u32 slot signature per (field, side): bit (slot % 32) of each slot it hit
   c->hset_words = hset_words;
   if ((e = c->hset.ensure(std::max<uint64_t>(4 * hset_words, 16))) != hipSuccess) return hip_fail(c, e, "alloc hit sets");
-  // k_body's work list: requests with a body, longest first (one wave each)
+  // Request chunks: consecutive requests while the chunk's queue-pool
+  // estimate (the formula sizing the pool below) stays within
+  // chunk_pool_words; each chunk runs the whole pipeline (gi_run_staged).
+  const double pf = pool_factor_env();
+  auto pool_est = [&](uint64_t nn, uint64_t raw, uint64_t body, uint64_t post) {
+    return pf * (1024.0 * nn + 8.0 * raw + (post ? 24.0 * body : 0.0));
+  };
+  struct ChunkSum {
+    uint64_t n = 0, raw = 0, body = 0, post = 0, items = 0;
+  };
+  std::vector<ChunkSum> csum;
+  c->chunks.clear();
+  {
+    ChunkSum cs;
+    uint32_t r0 = 0;
+    for (uint32_t r = 0; r < n; r++) {
+      const Sizes& z = sizes[r];
+      if (cs.n && pool_est(cs.n + 1, cs.raw + z.raw, cs.body + z.body, cs.post + z.post) > c->chunk_pool_words) {
+        c->chunks.push_back({r0, (uint32_t)cs.n, 0, 0, 0});
+        csum.push_back(cs);
+        cs = ChunkSum();
+        r0 = r;
+      }
+      cs.n++;
+      cs.raw += z.raw;
+      cs.body += z.body;
+      cs.post += z.post;
+      cs.items += z.items;
+    }
+    if (cs.n || c->chunks.empty()) {
+      c->chunks.push_back({r0, (uint32_t)cs.n, 0, 0, 0});
+      csum.push_back(cs);
+    }
+  }
+  // k_body's work lists: per chunk, the requests with a body, longest first (one wave each)
   std::vector<uint32_t> blist;
-  for (uint32_t r = 0; r < n; r++)
-    if (in->reqs[r].body.len) blist.push_back(r);
-  std::stable_sort(blist.begin(), blist.end(),
-                   [&](uint32_t x, uint32_t y) { return in->reqs[x].body.len > in->reqs[y].body.len; });
+  for (auto& ch : c->chunks) {
+    ch.blist_off = (uint32_t)blist.size();
+    for (uint32_t r = 0; r < ch.n; r++)
+      if (in->reqs[ch.r0 + r].body.len) {
+        blist.push_back(r);  // chunk-local index
+        ch.n_mp += sizes[ch.r0 + r].mp ? 1u : 0u;
+      }
+    ch.n_body = (uint32_t)blist.size() - ch.blist_off;
+    std::stable_sort(blist.begin() + ch.blist_off, blist.end(), [&](uint32_t x, uint32_t y) {
+      return in->reqs[ch.r0 + x].body.len > in->reqs[ch.r0 + y].body.len;
+    });
+  }
   c->n_body = (uint32_t)blist.size();
   c->n_mp_body = n_mp_body;
   if ((e = upload(&c->blist, blist, s)) != hipSuccess) return hip_fail(c, e, "alloc body list");
+  // per-chunk maxima of the phase-A capacities
+  ChunkSum cmax;
+  for (const ChunkSum& cs : csum) {
+    cmax.n = std::max(cmax.n, cs.n);
+    cmax.items = std::max(cmax.items, cs.items);
+  }
   if ((e = c->vmap.ensure(std::max<uint64_t>(4 * c->vmap_words, 16))) != hipSuccess) return hip_fail(c, e, "alloc value map");
   if ((e = c->hits.ensure(std::max<size_t>((size_t)c->hit_words * n * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc hits");
@@ -706,19 +850,28 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     // phase A: items, per-lane transformation scratch, queue pool + blocks,
     // slow list.  Pool / slow-list overflow only voids the phase-A bits of the
     // requests concerned (k_eval then evaluates their rules in full).
-    const uint32_t cb = (n + 255) / 256;
+    const uint32_t cb = (uint32_t)((cmax.n + 255) / 256);
     const uint32_t ns = (uint32_t)PG.streams.size();
-    c->items_cap = std::max<uint64_t>(items_cap, 1);
+    c->items_cap = std::max<uint64_t>(cmax.items, 1);
     c->lcap = (std::min<uint32_t>(max_cap_t, 4096) + 15) & ~15u;
     // chunked reservations leave at most one partial chunk per (k_stream
     // wave, launch) unused: both capacities carry that slack
     const uint64_t waves = (uint64_t)GI_STREAM_GRID * 5;
     c->qcap = (uint32_t)std::min<uint64_t>(c->items_cap / 64 + 8, 0xFFFFFFFull);  // item-waves
-    const double pf = pool_factor_env();
-    c->pool_cap = std::min<uint64_t>(
-        (uint64_t)(pf * (1024.0 * n + 8.0 * raw_total + (post_total ? 24.0 * raw_body : 0.0))) + waves * GI_PCHUNK + 4096,
-        0x3FFFFFFF0ull);  // qblk cell indices: 2^32 x 16 B
-    c->slow_cap = (uint32_t)std::min<uint64_t>(4ull * n + 4096 + post_total / 4, 0x7FFFFFFFull);
+    uint64_t pool_max = 0, slow_max = 0, long_max = 0, det_max = 0, detb_max = 0;
+    for (const ChunkSum& cs : csum) {
+      pool_max = std::max<uint64_t>(pool_max, (uint64_t)pool_est(cs.n, cs.raw, cs.body, cs.post));
+      slow_max = std::max<uint64_t>(slow_max, 4ull * cs.n + 4096 + cs.post / 4);
+      long_max = std::max<uint64_t>(long_max, ((cs.raw + cs.body) / GI_LONG_MIN + 16) * 2ull * ns);
+      // @detectSQLi/@detectXSS candidates: an item lists its unchanged value once and
+      // each differently transformed output once per detect stream: 2 per item covers the common case
+      const uint64_t dc = std::min<uint64_t>(std::min<uint64_t>(2ull * cs.items, 24ull * cs.n + 2ull * cs.post) + 4096,
+                                             0x7FFFFFFFull);
+      det_max = std::max(det_max, dc);
+      detb_max = std::max<uint64_t>(detb_max, 3ull * (cs.raw + cs.body) + 16ull * dc);
+    }
+    c->pool_cap = std::min<uint64_t>(pool_max + waves * GI_PCHUNK + 4096, 0x3FFFFFFF0ull);  // qblk cell indices: 2^32 x 16 B
+    c->slow_cap = (uint32_t)std::min<uint64_t>(slow_max, 0x7FFFFFFFull);
     c->slow_bytes_cap = 64ull * c->slow_cap;
     if ((e = c->bcounts.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc bcounts");
     if ((e = c->boffs.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc boffs");
@@ -728,13 +881,13 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       return hip_fail(c, e, "alloc lane scratch");
     if ((e = c->pool.ensure(4ull * c->pool_cap)) != hipSuccess) return hip_fail(c, e, "alloc queue pool");
     if ((e = c->qblk.ensure(8ull * ns * c->qcap)) != hipSuccess) return hip_fail(c, e, "alloc queue blocks");
-    if ((e = c->ctr.ensure(384)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+    if ((e = c->ctr.ensure(512)) != hipSuccess) return hip_fail(c, e, "alloc counters");
     (void)ns;
     if ((e = c->slow.ensure(40ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
     // long values (>= GI_LONG_MIN bytes): one k_long wave per (item, stream), each
     // workgroup with two buffers of 3x the longest request (overflow: "maybe", exact)
-    c->long_cap = (uint32_t)std::min<uint64_t>(((raw_total + raw_body) / GI_LONG_MIN + 16) * 2ull * ns, 0x7FFFFFFFull);
+    c->long_cap = (uint32_t)std::min<uint64_t>(long_max, 0x7FFFFFFFull);
     // The buffers are bounded by GI_LONG_BUDGET bytes in total: fewer k_long
     // workgroups when the longest request is large, and a per-buffer cap past
     // which a chain overflows ("maybe": k_eval evaluates those links, exact),
@@ -745,26 +898,30 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if ((e = c->long_buf.ensure((uint64_t)c->long_grid * 2 * c->long_bufcap)) != hipSuccess)
       return hip_fail(c, e, "alloc long-value buffers");
     // @detectSQLi/@detectXSS candidate list (overflow: the vals' bits become "maybe", exact)
-    // an item lists its unchanged value once and each differently transformed
-    // output once per detect stream: 2 entries per item covers the common case
-    c->det_cap = c->prog.n_det_streams
-                     ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(2ull * c->items_cap, 24ull * n + 2ull * post_total) + 4096,
-                                                    0x7FFFFFFFull)
-                     : 0;
-    c->det_bytes_cap = c->prog.n_det_streams ? 3ull * (raw_total + raw_body) + 16ull * c->det_cap : 0;
+    c->det_cap = c->prog.n_det_streams ? (uint32_t)det_max : 0;
+    c->det_bytes_cap = c->prog.n_det_streams ? detb_max : 0;
     if ((e = c->det.ensure(std::max<uint64_t>(32ull * c->det_cap, 64))) != hipSuccess) return hip_fail(c, e, "alloc detect list");
     if ((e = c->det_bytes.ensure(c->det_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc detect bytes");
   }
   // k_eval -> k_eval_wave request list (its counter lives in ctr)
-  if ((e = c->ctr.ensure(384)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+  if ((e = c->ctr.ensure(512)) != hipSuccess) return hip_fail(c, e, "alloc counters");
   if ((e = c->wlist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc wave list");
+  const auto t_h2d0 = std::chrono::steady_clock::now();
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && n) e = hipMemcpyAsync(c->reqs.p, in->reqs, n * sizeof(gi_request), hipMemcpyHostToDevice, s);
   if (e == hipSuccess && in->n_headers)
     e = hipMemcpyAsync(c->hdrs.p, in->headers, in->n_headers * sizeof(gi_header), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && n) e = hipMemcpyAsync(c->layout.p, lay.data(), n * sizeof(ReqLayout), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && n) e = hipMemcpyAsync(c->layout.p, lay, n * sizeof(ReqLayout), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(c, e, "stage H2D");
+  if (c->stage_prof) {
+    auto ms = [&](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t_end = std::chrono::steady_clock::now();
+    fprintf(stderr, "GI_STAGE_PROF n=%u chunks=%zu: sizes %.1f ms, offsets+chunks+lists %.1f ms, allocs %.1f ms, H2D %.1f ms\n",
+            n, c->chunks.size(), ms(t0, t_sizes), ms(t_sizes, t_plan), ms(t_plan, t_h2d0), ms(t_h2d0, t_end));
+  }
   c->n_req = n;
   c->staged = true;
   c->ran = false;
@@ -827,6 +984,7 @@ int gi_run_staged(gi_ctx* c) {
     B.qblk = (uint2*)c->qblk.p;
     B.acct = (unsigned long long*)(cp + 160);
     B.acct2 = (unsigned long long*)(cp + 336);  // 6 byte-step counters
+    B.acct3 = (unsigned long long*)(cp + 384);  // 5 item counts per bucket
     B.qcap = c->qcap;
     B.slow = c->slow.p;
     B.slow_count = (uint32_t*)(cp + 16);
@@ -861,6 +1019,7 @@ int gi_run_staged(gi_ctx* c) {
     B.wcount = wave ? (uint32_t*)(cp + 48) : nullptr;
     B.wave_fields = c->wave_fields;
     B.wave_rules = c->wave_rules;
+    B.rstride = c->n_req;
   }
   (void)hipEventRecord(c->ev0, c->stream);
   if (c->ctr.p) {
@@ -879,8 +1038,33 @@ int gi_run_staged(gi_ctx* c) {
     e = hipMemsetAsync(c->hset.p, 0, 4 * c->hset_words, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "memset hit sets");
   }
-  launch_pipeline(c->prog, B, c->scan, c->stream, c->evs, c->stop_after, &c->log,
-                  (const uint32_t*)c->tally_idbuf.p, (uint32_t)c->tally_ids.size());
+  // the request chunks (gi_stage_batch), one full pipeline pass each; the
+  // phase-A counters [0, 128) of ctr restart per chunk, the accounting ones
+  // accumulate
+  c->log.n = 0;
+  (void)hipEventRecord(c->log.ev[0], c->stream);
+  for (size_t k = 0; k < c->chunks.size(); k++) {
+    const gi_ctx::Chunk& ch = c->chunks[k];
+    if (k && c->ctr.p) {
+      e = hipMemsetAsync(c->ctr.p, 0, 128, c->stream);
+      if (e != hipSuccess) return hip_fail(c, e, "memset chunk counters");
+    }
+    DBatch Bc = B;
+    Bc.n_req = ch.n;
+    Bc.reqs = B.reqs + ch.r0;
+    Bc.layout = B.layout + ch.r0;
+    Bc.verdicts = B.verdicts + ch.r0;
+    Bc.matched = B.matched + (uint64_t)ch.r0 * B.mcap;
+    Bc.caprec = B.caprec ? B.caprec + 4ull * B.crcap * ch.r0 : nullptr;
+    Bc.capbytes = B.capbytes ? B.capbytes + (uint64_t)B.cbcap * ch.r0 : nullptr;
+    Bc.hits = B.hits + ch.r0;
+    Bc.txslots = (Slot*)((uint8_t*)B.txslots + 24ull * ch.r0);  // sizeof(Slot) == 24 (kernels.hip)
+    Bc.body_list = B.body_list + ch.blist_off;
+    Bc.n_body = ch.n_body;
+    Bc.n_mp_body = ch.n_mp;
+    launch_pipeline(c->prog, Bc, c->scan, c->stream, c->evs, c->stop_after, &c->log,
+                    (const uint32_t*)c->tally_idbuf.p, (uint32_t)c->tally_ids.size());
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(c, e, "launch pipeline");
   (void)hipEventRecord(c->ev1, c->stream);
@@ -910,22 +1094,37 @@ int gi_sync(gi_ctx* c) {
     if (c->ctr.p) (void)hipMemcpy(ibk, (uint8_t*)c->ctr.p + 64, 64, hipMemcpyDeviceToHost);
     gi_tally tl{};
     (void)hipMemcpy(&tl, c->tally.p, sizeof(tl), hipMemcpyDeviceToHost);
-    c->stats.n_launches = (uint32_t)c->log.n;
+    uint64_t ibc[5] = {0};  // items per bucket over all chunks (k_ioffsets)
+    if (c->ctr.p) (void)hipMemcpy(ibc, (uint8_t*)c->ctr.p + 384, 40, hipMemcpyDeviceToHost);
     uint64_t slow_bytes = 0;
     if (c->ctr.p) (void)hipMemcpy(&slow_bytes, (uint8_t*)c->ctr.p + 8, 8, hipMemcpyDeviceToHost);
+    // one record per launch name: a chunked batch repeats the pipeline, its
+    // launches of one name are summed
+    uint32_t nrec = 0;
     for (int k = 0; k < c->log.n; k++) {
       float lm = 0;
       (void)hipEventElapsedTime(&lm, c->log.ev[k], c->log.ev[k + 1]);
-      c->stats.launch_ms[k] = lm;
       const std::string nm = c->log.name[k];
-      snprintf(c->stats.launch_name[k], sizeof(c->stats.launch_name[k]), "%s", nm.c_str());
+      uint32_t i = 0;
+      while (i < nrec && nm != c->stats.launch_name[i]) i++;
+      if (i == nrec) {
+        if (nrec == GI_STATS_LAUNCHES) continue;
+        nrec++;
+        c->stats.launch_ms[i] = 0;
+        snprintf(c->stats.launch_name[i], sizeof(c->stats.launch_name[i]), "%s", nm.c_str());
+      }
+      c->stats.launch_ms[i] += lm;
+    }
+    c->stats.n_launches = nrec;
+    for (uint32_t k = 0; k < nrec; k++) {
+      const std::string nm = c->stats.launch_name[k];
       uint64_t ab = 0;
       if (nm == "k_collect") ab = c->raw_nobody + (uint64_t)GI_REQHDR_BYTES * c->n_req;  // request bytes in, ReqHdr out
-      else if (nm == "k_items") ab = 32ull * (ibk[1] + ibk[3] + ibk[5] + ibk[7] + ibk[9]);  // item records out
+      else if (nm == "k_items") ab = 32ull * (ibc[0] + ibc[1] + ibc[2] + ibc[3] + ibc[4]);  // item records out
       else if (nm == "k_ioffsets") ab = 8ull * 5 * ((c->n_req + 255) / 256);             // block counts in, offsets out
       else if (nm.rfind("k_stream", 0) == 0) {
         const int b = nm.back() - '0';
-        ab = acct[b] + 32ull * ibk[2 * b + 1] + 4ull * acct[5 + b];  // item bytes + records in, queue words out
+        ab = acct[b] + 32ull * ibc[b] + 4ull * acct[5 + b];  // item bytes + records in, queue words out
       } else if (nm == "k_scan") ab = 4ull * acct[10];  // each stream's queue words once
       else if (nm == "k_scan_big") ab = 4ull * acct[11];
       else if (nm == "k_scan_hbm") ab = 4ull * acct[12];

@@ -69,7 +69,7 @@ EXPORTED_SYMBOLS = (
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
     "gi_ctx_stream", "gi_selftest_regex", "gi_selftest_plan", "gi_selftest_triggers",
     "gi_ruleset_save", "gi_ruleset_load", "gi_ctx_swap_ruleset", "gi_compiler_rev", "gi_tally_detail_get", "gi_selftest_regex_many",
-    "gi_ctx_set_capture_cap", "gi_selftest_capture",
+    "gi_ctx_set_capture_cap", "gi_selftest_capture", "gi_host_register", "gi_host_unregister",
 )
 SCORE_BINS = 64  # GI_SCORE_BINS
 
@@ -171,6 +171,8 @@ def load_library(path: str = LIB_PATH):
                                         ctypes.POINTER(u32)]
     lib.gi_ctx_stream.argtypes = [vp]
     lib.gi_ctx_stream.restype = vp
+    lib.gi_host_register.argtypes = [vp, ctypes.c_void_p, sz]
+    lib.gi_host_unregister.argtypes = [vp, ctypes.c_void_p]
     lib.gi_selftest_regex.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(u32)]
     lib.gi_selftest_plan.argtypes = [vp, ctypes.c_char_p, sz]
     lib.gi_selftest_regex_many.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.POINTER(u64), u32,
@@ -519,6 +521,8 @@ class Engine:
             raise EngineError("gi_ctx_create failed (%d): no usable HIP device %d" % (rc, device))
         self._h = h
         self._staged = None
+        self._pinned = []   # host arrays page-locked through this ctx (gi_host_register)
+        self._rbuf = None   # reusable result arrays (fetch(reuse=True))
         self.capture_cap, self.capture_bytes_cap = capture_cap, capture_bytes_cap
         self._check(lib.gi_ctx_set_capture_cap(h, capture_cap, capture_bytes_cap), "gi_ctx_set_capture_cap")
 
@@ -533,6 +537,25 @@ class Engine:
         if rc != GI_OK:
             raise EngineError("%s failed (%d): %s" % (what, rc, self._lib.gi_last_error(self._h).decode()))
 
+    def pin(self, *arrays) -> int:
+        """Page-lock host arrays a later batch (or fetch) uses: gi_host_register,
+        the C ABI's optional pinned-host fast path.  Returns how many were
+        pinned (a refusal, e.g. an array sharing pages with one already pinned,
+        leaves that array pageable: staging stays correct, only slower)."""
+        k = 0
+        for a in arrays:
+            if a is None or a.nbytes == 0 or any(a is b for b in self._pinned):
+                continue
+            if self._lib.gi_host_register(self._h, ctypes.c_void_p(a.ctypes.data), ctypes.c_size_t(a.nbytes)) == GI_OK:
+                self._pinned.append(a)
+                k += 1
+        return k
+
+    def unpin(self):
+        for a in self._pinned:
+            self._lib.gi_host_unregister(self._h, ctypes.c_void_p(a.ctypes.data))
+        self._pinned = []
+
     def stage(self, batch: PackedBatch):
         self._staged = batch
         cb = batch.to_ctypes()
@@ -544,12 +567,25 @@ class Engine:
     def sync(self):
         self._check(self._lib.gi_sync(self._h), "gi_sync")
 
-    def fetch(self) -> Results:
+    def result_buffers(self, n: int):
+        """The reusable result arrays for n requests (allocated once)."""
+        if self._rbuf is None or self._rbuf[0] != n:
+            self._rbuf = (n, np.empty(n, VERDICT_DT), np.empty((n, self.matched_cap), np.uint32),
+                          np.empty((n, self.capture_cap), CAPTURE_DT), np.empty((n, self.capture_bytes_cap), np.uint8))
+        return self._rbuf[1:]
+
+    def fetch(self, reuse: bool = False) -> Results:
+        """Verdicts, matched ids and captures of the staged batch (D2H).  reuse:
+        write into this engine's reusable arrays (result_buffers; overwritten by
+        the next fetch) instead of fresh ones."""
         n = self._staged.n_req
-        verd = np.zeros(n, VERDICT_DT)
-        matched = np.zeros((n, self.matched_cap), np.uint32)
-        crec = np.zeros((n, self.capture_cap), CAPTURE_DT)
-        cbytes = np.zeros((n, self.capture_bytes_cap), np.uint8)
+        if reuse:
+            verd, matched, crec, cbytes = self.result_buffers(n)
+        else:
+            verd = np.zeros(n, VERDICT_DT)
+            matched = np.zeros((n, self.matched_cap), np.uint32)
+            crec = np.zeros((n, self.capture_cap), CAPTURE_DT)
+            cbytes = np.zeros((n, self.capture_bytes_cap), np.uint8)
         res = _Results(verd.ctypes.data, matched.ctypes.data, self.matched_cap, crec.ctypes.data, cbytes.ctypes.data,
                        self.capture_cap, self.capture_bytes_cap)
         self._check(self._lib.gi_fetch_results(self._h, ctypes.byref(res)), "gi_fetch_results")
@@ -600,6 +636,7 @@ class Engine:
 
     def close(self):
         if getattr(self, "_h", None):
+            self.unpin()
             self._lib.gi_ctx_free(self._h)
             self._h = None
 

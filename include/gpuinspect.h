@@ -281,6 +281,13 @@ int gi_tally_detail_get(gi_ctx* ctx, uint64_t* score_hist, uint32_t* rule_ids, u
 int gi_stats_get(gi_ctx* ctx, gi_stats* out);
 /* Opaque hipStream_t of the ctx (for HIP-event timing by the caller). */
 void* gi_ctx_stream(gi_ctx* ctx);
+/* Optional pinned-host fast path (input buffers are borrowed
+ * per call, "with an optional pinned-host fast path"): page-lock a caller
+ * buffer that later gi_batch arrays point into, so gi_stage_batch's H2D copies
+ * run as DMA without a bounce buffer.  The caller keeps ownership; unregister
+ * before freeing it.  GI_ENODEV / GI_ENOMEM when the HIP runtime refuses. */
+int gi_host_register(gi_ctx* ctx, void* p, size_t n);
+int gi_host_unregister(gi_ctx* ctx, void* p);
 
 /* ------------------------------------------------------- self-test hooks
  * Compiler self-tests only: run a host-built automaton on the host.  These

@@ -156,3 +156,93 @@ def test_rebalance_one_request_set(world):
     for rank, (lo, hi), totals, digs, nbytes in outs:
         assert nbytes == totals[rank] == int(sizes[lo:hi].sum())
         assert abs(nbytes - sizes.sum() / world) <= sizes.max()
+
+
+# ---------------------------------------------------------------- engine tallies
+# tests/golden/tally_crs_pl1_world2.json: per-rank gi_tally / gi_tally_detail
+# of one seeded CRS-PL1 request set cut into byte-balanced slices, recorded on
+# an MI355X by tools/record_tally.py.  The CPU oracle pins the fixture
+# (test_tally_fixture_matches_oracle); the gloo test all-gathers it the way
+# bench.py --gpus 2 does and checks the node total.
+TALLY_FIXTURE = os.path.join(os.path.dirname(__file__), "golden", "tally_crs_pl1_world2.json")
+
+
+def _fixture():
+    import json
+    return json.load(open(TALLY_FIXTURE))
+
+
+def test_tally_fixture_matches_oracle():
+    """The recorded engine tallies equal the oracle's, slice by slice."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import record_tally
+    import shard
+    from oracle import compare, coraza
+    fx = _fixture()
+    assert fx["seed"] == record_tally.SEED and fx["n_req"] > 0
+    batch = record_tally.request_set(fx["n_req"])
+    slices = shard.balanced_slices(batch.request_bytes(), fx["world"])
+    cfg = coraza.parse_seclang(open(os.path.join(root, fx["ruleset"])).read())
+    for (lo, hi), row in zip(slices, fx["ranks"]):
+        assert row["slice"] == [lo, hi]
+        part = batch.take(lo, hi)
+        ov = compare.oracle_verdicts(cfg, part, tuple(fx["exports"]))
+        assert not any(v.unsupported for v in ov.values())
+        t = row["tally"]
+        assert t["n_req"] == hi - lo
+        assert t["bytes_scanned"] == int(part.request_bytes().sum())
+        assert t["n_interrupted"] == sum(1 for v in ov.values() if v.rule_id or v.status)
+        assert t["n_matched_any"] == sum(1 for v in ov.values() if v.matched)
+        assert t["matched_total"] == sum(len(v.matched) for v in ov.values())
+        assert t["n_error"] == 0 and t["n_pa_void"] == 0
+        hits = {}
+        for v in ov.values():
+            for rid in v.matched:
+                hits[rid] = hits.get(rid, 0) + 1
+        assert {i: h for i, h in zip(row["rule_ids"], row["rule_hits"]) if h} == hits
+        hist = [0] * 64
+        for v in ov.values():
+            a, ok = coraza.go_atoi(v.tx.get(fx["exports"][0], b""))
+            hist[min(max(a if ok else 0, 0), 63)] += 1
+        assert row["score_hist"] == hist
+
+
+def _fixture_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    row = _fixture()["ranks"][rank]
+    g = shard.TallyGather(dist, world, "cpu", n_rules=len(row["rule_ids"]))
+    g.push(row["tally"], {"score_hist": row["score_hist"], "rule_hits": row["rule_hits"]})
+    q.put((rank, g.total()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tally_gather_engine_fixture():
+    """bench.py's N = 2 tally path over the recorded engine tallies."""
+    fx = _fixture()
+    world = fx["world"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fixture_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import shard
+    rows = fx["ranks"]
+    for _, tot in outs:
+        for k in shard.TALLY_KEYS:
+            assert tot[k] == sum(r["tally"][k] for r in rows)
+        assert tot["n_req"] == fx["n_req"]
+        assert tot["rule_hits"] == [sum(r["rule_hits"][k] for r in rows) for k in range(len(rows[0]["rule_ids"]))]
+        assert tot["score_hist"] == [sum(r["score_hist"][b] for r in rows) for b in range(64)]
