@@ -50,8 +50,10 @@ struct DBatch {
   uint32_t n_mp_body;         // of which multipart (k_mpparse)
   Slot* txslots;       // TX variables [n_slots][n_req] (k_eval)
   // phase A (see kernels.hip "phase A")
-  uint32_t* bcounts;          // [k_collect blocks][GI_NB] item counts
-  uint32_t* boffs;            // [k_collect blocks][GI_NB] item offsets
+  uint32_t* bcounts;          // [k_collect blocks][GI_NCLS] item counts per length class
+  uint32_t* boffs;            // [k_collect blocks][GI_NCLS] item offsets within the class
+  uint32_t* ctot;             // [GI_NCLS] items per class (k_ioffsets)
+  uint32_t* cbase;            // [GI_NCLS] first item of each class (k_ibases)
   uint32_t* ibk;              // [GI_NB] (base, count), [GI_NB] item-wave base, total item waves
   void* items;                // Item[items_cap]
   uint64_t* igm;              // [items_cap] global filters admitting each item (k_stream -> k_scan)
@@ -96,6 +98,7 @@ struct DBatch {
   uint32_t* wcount;
   uint32_t wave_fields;       // k_eval_wave: requests with this many fields (0: none)
   uint32_t wave_rules;        // k_eval_wave: every request when the program walks this many rules (0: never)
+  uint32_t bparse_lds;        // k_bparse: JSON bodies up to this many bytes are parsed from LDS (its dynamic LDS)
   uint32_t rstride;           // request stride of the request-major SoA arrays (hits, txslots): the staged
                               // batch's size (a chunk view of it has n_req <= rstride)
 };
@@ -112,6 +115,7 @@ struct ScanLaunch {
   uint32_t mode;                // debugging switches (GI_SCAN_MODE), 0 in production
 };
 
+#define GI_NCLS 145           // item length classes (kernels.hip item_class)
 #define GI_RHIST_LDS 1024     // per-rule match counts k_eval aggregates in LDS (more rules: global atomics)
 #define GI_STREAM_GRID 8192  // k_stream workgroups (64 lanes) per bucket launch (~8 waves/SIMD)
 #define GI_PCHUNK 2048       // pool words a k_stream wave reserves at a time
@@ -121,6 +125,7 @@ struct ScanLaunch {
 #define GI_EVAL_WAVE_LDS_WORDS 4096  // k_eval_wave keeps a request's hit words in LDS up to this many
 #define GI_EVAL_WAVE_FIELDS 4096     // default k_eval_wave thresholds (GI_EVAL_WAVE_FIELDS / _RULES env)
 #define GI_EVAL_WAVE_RULES 2048
+#define GI_BPARSE_LDS 32768          // k_bparse LDS body copy (bytes, GI_BPARSE_LDS env; 0: off)
 #define GI_CHUNK_POOL_WORDS 16e9     // queue-pool words (estimate) one request chunk of a batch may need
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.

@@ -4322,6 +4322,12 @@ __device__ __forceinline__ void void_request(const DBatch& B, uint32_t r, uint32
 __device__ __forceinline__ uint32_t item_bucket(uint32_t n) {
   return n <= 16 ? 0u : n <= 32 ? 1u : n <= 64 ? 2u : n <= 128 ? 3u : 4u;
 }
+// Length classes: k_items orders the items of each bucket by class, so the 64
+// values of an item wave have (nearly) one length -- the lanes of k_stream's
+// chains and k_scan's lockstep automata then run out of work together.
+// Classes 0..128: one per length; 129..144: 128-byte ranges (the last open).
+__device__ __forceinline__ uint32_t item_class(uint32_t n) { return n <= 128 ? n : min(144u, 129u + (n - 129u) / 128u); }
+__device__ __forceinline__ uint32_t class_bucket(uint32_t c) { return c <= 128 ? item_bucket(c) : 4u; }
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
@@ -4523,6 +4529,10 @@ __device__ __forceinline__ void urlenc_segment(const uint8_t* q, uint32_t n, uin
 }
 
 __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
+  // JSON bodies up to B.bparse_lds bytes are parsed out of an LDS copy (the
+  // sequential parser then waits on LDS, not on global memory, per byte)
+  extern __shared__ __attribute__((aligned(16))) uint8_t jlds[];
+  __shared__ uint32_t chist[GI_NCLS];
   const uint32_t L = threadIdx.x;
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
     const uint32_t r = B.body_list[bi];
@@ -4593,17 +4603,30 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
           res[0] = t.nf - nf0;
           res[1] = t.nb;
           res[2] = t.flags;
-        } else {
-          JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
-          parse_json_body(jc, q, n);
-          res[0] = jc.nf - nf0;
-          res[1] = jc.nb;
-          res[2] = jc.flags;
         }
+      }
+      const bool staged = sp == BP_JSON && n <= B.bparse_lds;
+      if (staged) {  // the whole wave copies the body into LDS
+        for (uint32_t k = L; k < n; k += 64) jlds[k] = q[k];
+        __syncthreads();
+      }
+      if (L == 0 && sp == BP_JSON) {
+        JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
+        parse_json_body(jc, staged ? jlds : q, n);
+        res[0] = jc.nf - nf0;
+        res[1] = jc.nb;
+        res[2] = jc.flags;
       }
       n_post = __shfl(res[0], 0, 64);
       nb = __shfl(res[1], 0, 64);
       ok = __shfl(res[2], 0, 64) == 0;
+      if (staged) {  // values that point into the LDS copy point into the body instead
+        for (uint32_t k = L; k < n_post; k += 64) {
+          Field& f = g.fields[nf0 + k];
+          if (f.v >= jlds && f.v <= jlds + n) f.v = q + (f.v - jlds);
+        }
+        __syncthreads();  // the next body's copy overwrites jlds
+      }
     }
     if (!ok) {  // not parsable as guessed: k_eval decides
       n_post = 0;
@@ -4619,21 +4642,22 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
         H->single[S_FILES_COMBINED_SIZE] = {CS_ZERO, 0};
       }
     }
-    // phase-A item counts of the body fields (ARGS_POST sides some filter reads)
+    // phase-A item counts per length class of the body fields (ARGS_POST
+    // sides some filter reads), aggregated in LDS
     const uint32_t sides = P.n_streams ? P.item_sides[FK_ARG_POST] : 0u;
     if (sides) {
-      uint32_t cnt[GI_NB] = {0, 0, 0, 0, 0};
+      for (uint32_t k = L; k < GI_NCLS; k += 64) chist[k] = 0;
+      __syncthreads();
       for (uint32_t i = L; i < n_post; i += 64) {
         const Field fl = g.fields[nf0 + i];
-        if (fl.kind != FK_ARG_POST) continue;  // multipart collections are not phase-A items
-        if (sides & 1) cnt[item_bucket(fl.vn)]++;
-        if (sides & 2) cnt[item_bucket(fl.kn)]++;
+        if (fl.kind != FK_ARG_POST) continue;
+        if (sides & 1) atomicAdd(&chist[item_class(fl.vn)], 1u);
+        if (sides & 2) atomicAdd(&chist[item_class(fl.kn)], 1u);
       }
-      for (uint32_t b = 0; b < GI_NB; b++) {
-        uint32_t x = cnt[b];
-        for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, 64);
-        if (L == 0 && x) atomicAdd(&B.bcounts[(r / 256) * GI_NB + b], x);
-      }
+      __syncthreads();
+      for (uint32_t k = L; k < GI_NCLS; k += 64)
+        if (chist[k]) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + k], chist[k]);
+      __syncthreads();
     }
   }
 }
@@ -4717,18 +4741,16 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
         H->spec_err = err;
         H->n_post = jc.nf - nf0;
         H->nb = jc.nb;
-        // phase-A item counts of its ARGS_POST and FILES* fields (for_each_item's kinds)
+        // phase-A item counts per length class of its ARGS_POST and FILES*
+        // fields (for_each_item's kinds)
         if (P.n_streams) {
-          uint32_t cnt[GI_NB] = {0, 0, 0, 0, 0};
           for (uint32_t f = nf0; f < jc.nf; f++) {
             const Field fl = g.fields[f];
             if (fl.kind < FK_ARG_GET || fl.kind > FK_FILE_SIZE) continue;
             const uint32_t sides = P.item_sides[fl.kind];
-            if (sides & 1) cnt[item_bucket(fl.vn)]++;
-            if (sides & 2) cnt[item_bucket(fl.kn)]++;
+            if (sides & 1) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.vn)], 1u);
+            if (sides & 2) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.kn)], 1u);
           }
-          for (uint32_t b = 0; b < GI_NB; b++)
-            if (cnt[b]) atomicAdd(&B.bcounts[(r / 256) * GI_NB + b], cnt[b]);
         }
       }
     }
@@ -4740,8 +4762,8 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
 // per-block item counts per length bucket (k_ioffsets / k_items) and the hit
 // bits of links without an automaton image.
 __global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
-  __shared__ uint32_t hist[GI_NB];
-  if (threadIdx.x < GI_NB) hist[threadIdx.x] = 0;
+  __shared__ uint32_t hist[GI_NCLS];
+  for (uint32_t k = threadIdx.x; k < GI_NCLS; k += blockDim.x) hist[k] = 0;
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < B.n_req) {
@@ -4750,17 +4772,15 @@ __global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
       const ReqLayout L = B.layout[r];
       const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
       if (!(H->flags & GI_REQ_ERROR_MASK)) {
-        uint32_t c[GI_NB] = {0, 0, 0, 0, 0};
         for_each_item(P, H, (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES),
-                      [&](uint8_t, uint8_t, uint32_t, uint32_t, uint32_t n) { c[item_bucket(n)]++; });
-        for (uint32_t b = 0; b < GI_NB; b++)
-          if (c[b]) atomicAdd(&hist[b], c[b]);
+                      [&](uint8_t, uint8_t, uint32_t, uint32_t, uint32_t n) { atomicAdd(&hist[item_class(n)], 1u); });
       }
       for (uint32_t k = 0; k < P.n_always; k++) set_hit(B, P.always_slots[k], r);
     }
   }
   __syncthreads();
-  if (P.n_streams && threadIdx.x < GI_NB) B.bcounts[blockIdx.x * GI_NB + threadIdx.x] = hist[threadIdx.x];
+  if (P.n_streams)
+    for (uint32_t k = threadIdx.x; k < GI_NCLS; k += blockDim.x) B.bcounts[blockIdx.x * GI_NCLS + k] = hist[k];
 }
 
 
@@ -4825,57 +4845,63 @@ __device__ __forceinline__ void hit_item(const DBatch& B, uint32_t slot, uint32_
   hit_value(B, slot, rm.x, meta_vix(rm.y));
 }
 
-__global__ void __launch_bounds__(1024) k_ioffsets(DBatch B, uint32_t n_blocks) {
-  // bcounts[blk * GI_NB + b] -> boffs (exclusive, bucket-major global order);
-  // ibk[2b] = bucket base, ibk[2b+1] = bucket count
-  __shared__ uint32_t part[1024];
-  __shared__ uint32_t base_s;
-  const uint32_t t = threadIdx.x;
-  const uint32_t chunk = (n_blocks + 1023) / 1024;
-  if (t == 0) base_s = 0;
+// One workgroup per length class: the class's per-block item counts
+// bcounts[blk * GI_NCLS + c] -> per-block offsets within the class (boffs),
+// and the class total (ctot[c]).
+__global__ void __launch_bounds__(256) k_ioffsets(DBatch B, uint32_t n_blocks) {
+  __shared__ uint32_t part[256];
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  const uint32_t chunk = (n_blocks + 255) / 256;
+  const uint32_t k0 = min(n_blocks, t * chunk), k1 = min(n_blocks, (t + 1) * chunk);
+  uint32_t sum = 0;
+  for (uint32_t k = k0; k < k1; k++) sum += B.bcounts[k * GI_NCLS + c];
+  part[t] = sum;
   __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive scan
+    const uint32_t x = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (uint32_t k = k0; k < k1; k++) {
+    const uint32_t x = B.bcounts[k * GI_NCLS + c];
+    B.boffs[k * GI_NCLS + c] = run;
+    run += x;
+  }
+  if (t == 255) B.ctot[c] = part[255];
+}
+
+// Class bases (bucket-major = length order), bucket (base, count), item-wave
+// base per bucket and the total: one lane.
+__global__ void __launch_bounds__(64) k_ibases(DBatch B) {
+  if (threadIdx.x) return;
+  uint32_t run = 0;
+  uint32_t bbase[GI_NB] = {0, 0, 0, 0, 0}, bcnt[GI_NB] = {0, 0, 0, 0, 0};
+  for (uint32_t c = 0; c < GI_NCLS; c++) {
+    const uint32_t b = class_bucket(c);
+    if (c == 0 || class_bucket(c - 1) != b) bbase[b] = run;  // the bucket's first class
+    B.cbase[c] = run;
+    bcnt[b] += B.ctot[c];
+    run += B.ctot[c];
+  }
+  uint32_t iw = 0;
   for (uint32_t b = 0; b < GI_NB; b++) {
-    uint32_t sum = 0;
-    for (uint32_t k = t * chunk; k < min(n_blocks, (t + 1) * chunk); k++) sum += B.bcounts[k * GI_NB + b];
-    part[t] = sum;
-    __syncthreads();
-    if (t == 0) {
-      uint32_t run = 0;
-      for (uint32_t k = 0; k < 1024; k++) {
-        const uint32_t x = part[k];
-        part[k] = run;
-        run += x;
-      }
-      B.ibk[2 * b] = base_s;
-      B.ibk[2 * b + 1] = run;
-      atomicAdd(&B.acct3[b], (unsigned long long)run);
-    }
-    __syncthreads();
-    uint32_t run = base_s + part[t];
-    for (uint32_t k = t * chunk; k < min(n_blocks, (t + 1) * chunk); k++) {
-      const uint32_t x = B.bcounts[k * GI_NB + b];
-      B.boffs[k * GI_NB + b] = run;
-      run += x;
-    }
-    __syncthreads();
-    if (t == 0) base_s += B.ibk[2 * b + 1];
-    __syncthreads();
+    B.ibk[2 * b] = bbase[b];
+    B.ibk[2 * b + 1] = bcnt[b];
+    atomicAdd(&B.acct3[b], (unsigned long long)bcnt[b]);
+    B.ibk[2 * GI_NB + b] = iw;
+    iw += (bcnt[b] + 63) / 64;
   }
-  if (t == 0) {  // item-wave (queue-block index) base per bucket, and the total
-    uint32_t iw = 0;
-    for (uint32_t b = 0; b < GI_NB; b++) {
-      B.ibk[2 * GI_NB + b] = iw;
-      iw += (B.ibk[2 * b + 1] + 63) / 64;
-    }
-    B.ibk[3 * GI_NB] = iw;
-  }
+  B.ibk[3 * GI_NB] = iw;
 }
 
 // One thread per request, same block shape as k_collect.
 __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
-  __shared__ uint32_t rank[GI_NB];
+  __shared__ uint32_t rank[GI_NCLS];
   __shared__ unsigned long long ibytes[GI_NB];
-  if (threadIdx.x < GI_NB) rank[threadIdx.x] = 0, ibytes[threadIdx.x] = 0;
+  for (uint32_t k = threadIdx.x; k < GI_NCLS; k += blockDim.x) rank[k] = 0;
+  if (threadIdx.x < GI_NB) ibytes[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < B.n_req) {
@@ -4883,10 +4909,10 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
     const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
     if (!(H->flags & GI_REQ_ERROR_MASK)) {
       const Field* Fd = (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES);
-      const uint32_t* boff = B.boffs + blockIdx.x * GI_NB;
+      const uint32_t* boff = B.boffs + blockIdx.x * GI_NCLS;
       for_each_item(P, H, Fd, [&](uint8_t kind, uint8_t sg, uint32_t side, uint32_t fi, uint32_t n) {
-        const uint32_t b = item_bucket(n);
-        const uint32_t at = boff[b] + atomicAdd(&rank[b], 1u);
+        const uint32_t b = item_bucket(n), c = item_class(n);
+        const uint32_t at = B.cbase[c] + boff[c] + atomicAdd(&rank[c], 1u);
         GI_BOUND(at < B.items_cap, at, B.items_cap);
         Item it;
         if (kind == 0) {
@@ -5132,6 +5158,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
   uint8_t* b1 = IN ? lb + 64 * (IS + WT) + lane * WT : g1;
   const uint32_t cap = IN ? WT : B.lcap;
   uint64_t pc_item = 0, pc_chain = 0, pc_out = 0, pc_loop = 0, pc_tot = 0, pc_fm = 0, pc_run = 0, pc_slow = 0;
+  uint64_t pc_vals = 0, pc_det = 0;
   uint64_t wwords = 0;  // queue words this wave wrote (algorithmic-byte accounting)
   uint64_t csteps = 0;  // value bytes this lane fed into a stream's chain (secondary roofline)
   const uint64_t pc_start = B.prof ? clock64() : 0;
@@ -5203,11 +5230,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
           cur = src;
           cn = 0;
         }
+        const uint64_t c_v0 = B.prof ? clock64() : 0;
         if (S.val_count)
           stream_vals(P, B, it.req, meta_vix(it.meta), S, fm, maybe, cur, (uint32_t)cn, osum, !maybe && cur == src,
                       &rawmask, &det_append);
+        if (B.prof) pc_vals += clock64() - c_v0;
       }
+      const uint64_t c_d0 = B.prof ? clock64() : 0;
       if (S.val_count) det_push(P, B, det_append, it.req, meta_vix(it.meta), gm, 1u << S.det_id, cur, (uint32_t)cn);
+      if (B.prof) pc_det += clock64() - c_d0;
       const uint64_t c_s1 = B.prof ? clock64() : 0;
       pc_chain += c_s1 - c_s0;
       if (!S.job_count) continue;
@@ -5328,6 +5359,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
     atomicAdd(&B.prof[80 + 3 * bucket + 0], (unsigned long long)pc_fm);
     atomicAdd(&B.prof[80 + 3 * bucket + 1], (unsigned long long)pc_run);
     atomicAdd(&B.prof[80 + 3 * bucket + 2], (unsigned long long)pc_slow);
+    atomicAdd(&B.prof[24 + 2 * bucket], (unsigned long long)pc_vals);
+    atomicAdd(&B.prof[25 + 2 * bucket], (unsigned long long)pc_det);
   }
 }
 
@@ -5448,7 +5481,8 @@ __device__ void value_end(const DProgram& P, const DBatch& B, uint32_t r, const 
 template <uint32_t NB>
 __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B, const DJob& J, const uint8_t* img,
                                              uint32_t K, const uint32_t* trn, const uint32_t* st0, uint32_t umask,
-                                             uint32_t nf, const uint2* d, uint32_t mode) {
+                                             uint32_t nf, const uint2* d, uint32_t mode, uint64_t* prof_real,
+                                             uint64_t* prof_slot) {
   const uint32_t lane = lane_id();
   uint32_t req[NB], len[NB], nwl[NB], nwmax = 0, p0[NB], p1[NB];
   uint64_t fm[NB];
@@ -5486,6 +5520,13 @@ __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B,
     for (uint32_t k = 0; k < GI_JOB_MAX_DFA; k++) st[j][k] = st0[k];
   }
   if (mode & 16) umask = 0;
+  if (prof_real) {  // GI_PROF: bytes stepped by lanes with a value vs the wave's lockstep slots
+    uint64_t real = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < NB; j++) real += len[j] != 0xFFFFFFFFu ? len[j] : 0u;
+    *prof_real += real * K;
+    *prof_slot += (uint64_t)nwmax * 4u * K;  // per lane: words stepped, active or not
+  }
   const uint32_t* jam = (const uint32_t*)img;
   for (uint32_t w = 0; w < nwmax; w++) {
     uint32_t wd[NB];
@@ -5535,6 +5576,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)
                                                uint32_t mode, uint32_t acct_slot) {
   uint64_t rwords = 0;  // queue words of this launch's streams, each counted once (algorithmic bytes)
   uint64_t rsteps = 0;  // automaton byte-steps (padded words x 4 x automata of the job)
+  uint64_t preal = 0, pslot = 0;  // GI_PROF lane utilisation
   extern __shared__ __attribute__((aligned(16))) uint8_t simg[];
   __shared__ uint2 clist[1024];
   __shared__ uint32_t wcnt[16];
@@ -5607,12 +5649,20 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)
         rwords += (first && !(d[j].y & GI_QB_SHARED)) ? w : 0;  // a shared block is counted at its writer
         rsteps += (uint64_t)(d[j].y & 0xFFu) * dnw * 4 * K;
       }
-      scan_qblocks<2>(P, B, J, img, K, trn, st0, umask, nf, d, mode);
+      scan_qblocks<2>(P, B, J, img, K, trn, st0, umask, nf, d, mode, B.prof ? &preal : nullptr, &pslot);
     }
     __syncthreads();  // clist / wcnt reuse
   }
   if ((threadIdx.x & 63) == 0 && rwords) atomicAdd(&B.acct[10 + acct_slot], (unsigned long long)rwords);
   if ((threadIdx.x & 63) == 0 && rsteps) atomicAdd(&B.acct[13 + acct_slot], (unsigned long long)rsteps);
+  if (B.prof) {
+    preal = wave_sum(preal);
+    pslot = wave_sum(pslot);
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&B.prof[34 + acct_slot], (unsigned long long)preal);
+      atomicAdd(&B.prof[37 + acct_slot], (unsigned long long)pslot);
+    }
+  }
 }
 
 // REQUEST_BODY targets of phase-2 links (residual: the variable only exists
@@ -6517,12 +6567,13 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
   const uint32_t cb = (B.n_req + 255) / 256;
   GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
   if (B.n_body && P.body_access) {
-    GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
+    GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), B.bparse_lds, stream, P, B);
     if (B.n_mp_body) GI_LAUNCH("k_mpparse", k_mpparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (P.n_streams) {
-    GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(1), dim3(1024), 0, stream, B, cb);
+    GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(GI_NCLS), dim3(256), 0, stream, B, cb);
+    GI_LAUNCH("k_ibases", k_ibases, dim3(1), dim3(64), 0, stream, B);
     GI_LAUNCH("k_items", k_items, dim3(cb), dim3(256), 0, stream, P, B);
     GI_LAUNCH("k_stream0", (k_stream<16, 20>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 0u);
     GI_LAUNCH("k_stream1", (k_stream<32, 36>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 1u);

@@ -104,7 +104,9 @@ struct gi_ctx {
   double chunk_pool_words = GI_CHUNK_POOL_WORDS;
   ReqLayout* lay_host = nullptr;  // page-locked host copy of the staged layout
   uint32_t lay_host_cap = 0;
-  bool stage_prof = false;        // GI_STAGE_PROF=1: gi_stage_batch phase times on stderr  // queue-pool estimate a chunk may reach (GI_CHUNK_POOL_WORDS env)
+  bool stage_prof = false;
+  uint32_t bparse_lds = GI_BPARSE_LDS;  // GI_BPARSE_LDS env
+  uint64_t max_body = 0;                // longest body of the staged batch        // GI_STAGE_PROF=1: gi_stage_batch phase times on stderr  // queue-pool estimate a chunk may reach (GI_CHUNK_POOL_WORDS env)
   uint64_t long_bufcap = 0;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0, det_cap = 0;
   uint64_t pool_cap = 0, slow_bytes_cap = 0, items_cap = 0, det_bytes_cap = 0;
@@ -469,6 +471,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   if (getenv("GI_EVAL_WAVE_FIELDS")) c->wave_fields = (uint32_t)atoi(getenv("GI_EVAL_WAVE_FIELDS"));  // A/B, 0: off
   if (getenv("GI_EVAL_WAVE_RULES")) c->wave_rules = (uint32_t)atoi(getenv("GI_EVAL_WAVE_RULES"));
   c->stage_prof = getenv("GI_STAGE_PROF") && atoi(getenv("GI_STAGE_PROF")) > 0;
+  if (getenv("GI_BPARSE_LDS")) c->bparse_lds = (uint32_t)std::min(65536, std::max(0, atoi(getenv("GI_BPARSE_LDS"))));
   if (getenv("GI_CHUNK_POOL_WORDS")) c->chunk_pool_words = std::max(1e6, atof(getenv("GI_CHUNK_POOL_WORDS")));
   c->stop_after = getenv("GI_STOP_AFTER") ? atoi(getenv("GI_STOP_AFTER")) : 0;
   hipError_t e = hipSetDevice(device);
@@ -873,15 +876,15 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     c->pool_cap = std::min<uint64_t>(pool_max + waves * GI_PCHUNK + 4096, 0x3FFFFFFF0ull);  // qblk cell indices: 2^32 x 16 B
     c->slow_cap = (uint32_t)std::min<uint64_t>(slow_max, 0x7FFFFFFFull);
     c->slow_bytes_cap = 64ull * c->slow_cap;
-    if ((e = c->bcounts.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc bcounts");
-    if ((e = c->boffs.ensure(4ull * cb * 5)) != hipSuccess) return hip_fail(c, e, "alloc boffs");
+    if ((e = c->bcounts.ensure(4ull * cb * GI_NCLS)) != hipSuccess) return hip_fail(c, e, "alloc bcounts");
+    if ((e = c->boffs.ensure(4ull * cb * GI_NCLS)) != hipSuccess) return hip_fail(c, e, "alloc boffs");
     if ((e = c->items.ensure(32ull * c->items_cap)) != hipSuccess) return hip_fail(c, e, "alloc items");
     if ((e = c->igm.ensure(8ull * c->items_cap)) != hipSuccess) return hip_fail(c, e, "alloc item filter masks");
     if ((e = c->lscratch.ensure((uint64_t)GI_STREAM_GRID * 64 * 2 * c->lcap + 64)) != hipSuccess)
       return hip_fail(c, e, "alloc lane scratch");
     if ((e = c->pool.ensure(4ull * c->pool_cap)) != hipSuccess) return hip_fail(c, e, "alloc queue pool");
     if ((e = c->qblk.ensure(8ull * ns * c->qcap)) != hipSuccess) return hip_fail(c, e, "alloc queue blocks");
-    if ((e = c->ctr.ensure(512)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+    if ((e = c->ctr.ensure(4096)) != hipSuccess) return hip_fail(c, e, "alloc counters");
     (void)ns;
     if ((e = c->slow.ensure(40ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
@@ -904,7 +907,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if ((e = c->det_bytes.ensure(c->det_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc detect bytes");
   }
   // k_eval -> k_eval_wave request list (its counter lives in ctr)
-  if ((e = c->ctr.ensure(512)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+  if ((e = c->ctr.ensure(4096)) != hipSuccess) return hip_fail(c, e, "alloc counters");
   if ((e = c->wlist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc wave list");
   const auto t_h2d0 = std::chrono::steady_clock::now();
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
@@ -923,6 +926,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
             n, c->chunks.size(), ms(t0, t_sizes), ms(t_sizes, t_plan), ms(t_plan, t_h2d0), ms(t_h2d0, t_end));
   }
   c->n_req = n;
+  c->max_body = 0;
+  for (uint32_t r = 0; r < n; r++) c->max_body = std::max<uint64_t>(c->max_body, in->reqs[r].body.len);
   c->staged = true;
   c->ran = false;
   c->stats.last_scratch_bytes = off;
@@ -973,6 +978,8 @@ int gi_run_staged(gi_ctx* c) {
     uint8_t* cp = (uint8_t*)c->ctr.p;
     B.bcounts = (uint32_t*)c->bcounts.p;
     B.boffs = (uint32_t*)c->boffs.p;
+    B.ctot = (uint32_t*)(cp + 1024);   // GI_NCLS words
+    B.cbase = (uint32_t*)(cp + 2048);  // GI_NCLS words
     B.ibk = (uint32_t*)(cp + 64);
     B.items = c->items.p;
     B.igm = (uint64_t*)c->igm.p;
@@ -1020,6 +1027,7 @@ int gi_run_staged(gi_ctx* c) {
     B.wave_fields = c->wave_fields;
     B.wave_rules = c->wave_rules;
     B.rstride = c->n_req;
+    B.bparse_lds = (uint32_t)std::min<uint64_t>(c->bparse_lds, (c->max_body + 15) & ~15ull);
   }
   (void)hipEventRecord(c->ev0, c->stream);
   if (c->ctr.p) {
@@ -1121,7 +1129,7 @@ int gi_sync(gi_ctx* c) {
       uint64_t ab = 0;
       if (nm == "k_collect") ab = c->raw_nobody + (uint64_t)GI_REQHDR_BYTES * c->n_req;  // request bytes in, ReqHdr out
       else if (nm == "k_items") ab = 32ull * (ibc[0] + ibc[1] + ibc[2] + ibc[3] + ibc[4]);  // item records out
-      else if (nm == "k_ioffsets") ab = 8ull * 5 * ((c->n_req + 255) / 256);             // block counts in, offsets out
+      else if (nm == "k_ioffsets") ab = 8ull * GI_NCLS * ((c->n_req + 255) / 256);       // block counts in, offsets out
       else if (nm.rfind("k_stream", 0) == 0) {
         const int b = nm.back() - '0';
         ab = acct[b] + 32ull * ibc[b] + 4ull * acct[5 + b];  // item bytes + records in, queue words out
@@ -1147,13 +1155,18 @@ int gi_sync(gi_ctx* c) {
     if (c->prof_on && c->prof.p) {
       unsigned long long h[128];
       if (hipMemcpy(h, c->prof.p, 1024, hipMemcpyDeviceToHost) == hipSuccess && c->n_req) {
+        for (int b = 0; b < 3; b++)
+          if (h[37 + b])
+            fprintf(stderr, "GI_PROF k_scan launch %d: lane-utilisation %.3f (%.0f M real byte-steps of %.0f M lockstep slots)\n",
+                    b, (double)h[34 + b] / h[37 + b], h[34 + b] / 1e6, h[37 + b] / 1e6);
         for (int b = 0; b < 5; b++)
           fprintf(stderr, "GI_PROF k_stream bucket %d (sum over waves, Mcyc): item %.1f chain %.1f out %.1f loop %.1f total %.1f\n",
                   b, h[40 + 5 * b] / 1e6, h[41 + 5 * b] / 1e6, h[42 + 5 * b] / 1e6, h[43 + 5 * b] / 1e6,
                   h[44 + 5 * b] / 1e6);
         for (int b = 0; b < 5; b++)
-          fprintf(stderr, "GI_PROF k_stream bucket %d: fm+ballot %.1f run_chain(lane max) %.1f slowcheck+collapse %.1f\n", b,
-                  h[80 + 3 * b] / 1e6, h[81 + 3 * b] / 1e6, h[82 + 3 * b] / 1e6);
+          fprintf(stderr, "GI_PROF k_stream bucket %d: fm+ballot %.1f run_chain(lane max) %.1f slowcheck+collapse %.1f "
+                  "stream_vals %.1f det_push %.1f\n", b, h[80 + 3 * b] / 1e6, h[81 + 3 * b] / 1e6, h[82 + 3 * b] / 1e6,
+                  h[24 + 2 * b] / 1e6, h[25 + 2 * b] / 1e6);
         for (uint32_t k = 0; k < 16 && k < c->rs->prog.body_links.size(); k++) {
           const DRule& R = c->rs->prog.rules[c->rs->prog.body_links[k]];
           fprintf(stderr, "GI_PROF k_body link %u id %d chain %u op %d: transform %.1f Mcyc, operator %.1f Mcyc (sum)\n",
