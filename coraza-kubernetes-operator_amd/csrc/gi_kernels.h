@@ -122,6 +122,7 @@ struct ScanLaunch {
 #define GI_LONG_MIN 2048     // items at least this long take k_long (one wave per (item, stream)), not the queue
 #define GI_LONG_GRID 512     // k_long workgroups (at most)
 #define GI_LONG_BUDGET (4ull << 30)  // bytes of k_long chain buffers (runtime.cpp gi_stage_batch)
+#define GI_EVAL_LDS_WORDS 16          // k_eval keeps a request's hit words in LDS up to this many
 #define GI_EVAL_WAVE_LDS_WORDS 4096  // k_eval_wave keeps a request's hit words in LDS up to this many
 #define GI_EVAL_WAVE_FIELDS 4096     // default k_eval_wave thresholds (GI_EVAL_WAVE_FIELDS / _RULES env)
 #define GI_EVAL_WAVE_RULES 2048

@@ -6160,7 +6160,7 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
 // LDS (nullptr: read from HBM).
 template <bool W>
 __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B, uint32_t r, const uint32_t* whits,
-                                             unsigned long long* my) {
+                                             uint32_t wstride, unsigned long long* my) {
   const uint64_t c_start = B.prof ? clock64() : 0;
   const gi_request rq = B.reqs[r];
   Region g = region_of(P, B, r);
@@ -6173,7 +6173,7 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
   t.prof_rule_cyc = B.prof ? B.prof + 128 : nullptr;
   tx_bind(t, P, g);
   t.hits = whits ? whits : B.hits + r;
-  t.hstride = whits ? 1u : B.rstride;
+  t.hstride = whits ? wstride : B.rstride;
   t.vmap = B.vmap + B.layout[r].vmap_bit;
   {
     const ReqLayout Lr = B.layout[r];
@@ -6417,13 +6417,20 @@ __device__ __forceinline__ bool eval_heavy(const DProgram& P, const DBatch& B, u
 
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVAL_WPE, 8))) k_eval(DProgram P, DBatch B) {
   __shared__ unsigned long long red[7];
+  // the block's hit words in LDS ([word][thread]): the rule walk tests one per
+  // rule, and an LDS read waits far less than a global one
+  __shared__ uint32_t lhits[GI_EVAL_LDS_WORDS * 128];
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (threadIdx.x < 7) red[threadIdx.x] = 0;
+  const uint32_t nw = (B.n_hit_slots + 31) / 32;
+  const bool in_lds = nw <= GI_EVAL_LDS_WORDS && blockDim.x <= 128;
+  if (in_lds && r < B.n_req)
+    for (uint32_t w = 0; w < nw; w++) lhits[w * blockDim.x + threadIdx.x] = B.hits[(uint64_t)w * B.rstride + r];
   __syncthreads();
   unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
   if (r < B.n_req) {
     if (eval_heavy(P, B, r)) B.wlist[atomicAdd(B.wcount, 1u)] = r;
-    else eval_request<false>(P, B, r, nullptr, my);
+    else eval_request<false>(P, B, r, in_lds ? lhits + threadIdx.x : nullptr, blockDim.x, my);
   }
   for (int c = 0; c < 7; c++) {
     unsigned long long x = my[c];
@@ -6451,7 +6458,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_EVAL
       __syncthreads();
     }
     unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
-    eval_request<true>(P, B, r, in_lds ? whits : nullptr, my);
+    eval_request<true>(P, B, r, in_lds ? whits : nullptr, 1u, my);
     for (int c = 0; c < 7; c++) acc[c] += my[c];
   }
   if (lane == 0)
