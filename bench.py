@@ -43,8 +43,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
 # launch name (gi_stats) -> kernel name as rocprofv3 reports it
 ROCPROF_NAMES = {
-    "k_stream0": "k_stream<16u, 20u>", "k_stream1": "k_stream<32u, 36u>", "k_stream2": "k_stream<64u, 68u>",
-    "k_stream3": "k_stream<128u, 132u>", "k_stream4": "k_stream<0u, 0u>", "k_scan": "k_scan<true, false>",
+    "k_stream0": "k_stream<16u, 20u, 4u>", "k_stream1": "k_stream<32u, 36u, 3u>", "k_stream2": "k_stream<64u, 68u, 1u>",
+    "k_stream3": "k_stream<128u, 132u, 0u>", "k_stream4": "k_stream<0u, 0u, 0u>", "k_scan": "k_scan<true, false>",
     "k_scan_big": "k_scan<true, true>", "k_scan_hbm": "k_scan<false, false>",
 }
 

@@ -5086,6 +5086,61 @@ __device__ __forceinline__ int64_t run_chain(const DProgram& P, const DStream& S
   return cn;
 }
 
+// Per-item memo of chain results (k_stream, short buckets).  Different
+// streams' chains reduce to the same few effective chains on most values:
+// the identity steps drop out (e.g. t:urlDecodeUni on a value without '%'),
+// and what remains -- t:cmdLine, t:lowercase, ... -- repeats across streams.
+// A lane keeps the last M outputs of the current item keyed by the effective
+// code sequence applied so far (1, then key * 64 + code), and a chain resumes
+// from the longest memoised prefix instead of recomputing it.
+struct ChainMemo {
+  uint64_t key;
+  uint32_t len, sum;
+};
+template <uint32_t M, uint32_t WT>
+__device__ __forceinline__ int64_t run_chain_memo(const DProgram& P, const DStream& S, const uint8_t* v, uint32_t vn,
+                                                  uint32_t summ, uint8_t* slots, ChainMemo* memo, uint32_t* victim,
+                                                  uint8_t* b0, uint8_t* b1, const uint8_t** out, const uint16_t* lut,
+                                                  uint32_t* osumm) {
+  const uint8_t* cur = v;
+  uint32_t cn = vn, cur_slot = M;  // M: cur is not a memo slot
+  uint64_t key = 1;
+  for (uint32_t k = 0; k < S.tchain_len; k++) {
+    const uint8_t code = (uint8_t)GI_CONST(uint32_t, P.tchains32)[S.tchain_off + k];
+    if (transform_identity(summ, code)) continue;
+    key = key * 64u + code;
+    uint32_t hit = M;
+    for (uint32_t m = 0; m < M; m++)
+      if (memo[m * 64].key == key) hit = m;
+    if (hit < M) {
+      cur_slot = hit;
+      cur = slots + hit * 64u * WT;
+      cn = memo[hit * 64].len;
+      summ = memo[hit * 64].sum;
+      continue;
+    }
+    uint32_t vs = *victim;
+    if (vs == cur_slot) vs = (vs + 1) % M;
+    uint8_t* dst;
+    if (vs == cur_slot) {  // M == 1 and the input is the slot: the scratch buffers, not memoised
+      dst = cur == b0 ? b1 : b0;
+      vs = M;
+    } else {
+      *victim = (vs + 1) % M;
+      dst = slots + vs * 64u * WT;
+    }
+    const int64_t m = apply_transform_inl(P, code, cur, cn, dst, WT);
+    if (m < 0) return -1;
+    cur = dst;
+    cur_slot = vs;
+    cn = (uint32_t)m;
+    summ = value_summary_lut(lut, cur, cn);
+    if (vs < M) memo[vs * 64] = ChainMemo{key, cn, summ};
+  }
+  *out = cur;
+  *osumm = summ;
+  return cn;
+}
 
 // Slow-list entry: the transformed bytes are copied into the slow arena.
 struct SlowEnt {
@@ -5134,10 +5189,11 @@ __device__ uint32_t collapse_runes(const uint8_t* s, uint32_t n, uint8_t* d, con
 #ifndef GI_STREAM_WPE
 #define GI_STREAM_WPE 2
 #endif
-template <uint32_t IN, uint32_t WT>
+template <uint32_t IN, uint32_t WT, uint32_t M>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STREAM_WPE, 8))) k_stream(DProgram P, DBatch B, uint32_t bucket) {
   constexpr uint32_t IS = IN ? IN + 4 : 0;  // lane strides = odd dword counts: conflict-free
-  __shared__ __attribute__((aligned(16))) uint8_t lb[IN ? 64 * (IS + 2 * WT) : 16];
+  __shared__ __attribute__((aligned(16))) uint8_t lb[IN ? 64 * (IS + (2 + M) * WT) : 16];
+  __shared__ ChainMemo memo_s[M ? 64 * M : 1];  // [slot][lane]
   // Queue block of (item-wave, stream) = qblk[stream][item-wave index]: no
   // counter.  Pool words are reserved GI_PCHUNK at a time per wave (one
   // workgroup = one wave), so the pool counter sees one atomic per chunk.
@@ -5156,6 +5212,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
   uint8_t* li = IN ? lb + lane * IS : nullptr;
   uint8_t* b0 = IN ? lb + 64 * IS + lane * WT : g0;
   uint8_t* b1 = IN ? lb + 64 * (IS + WT) + lane * WT : g1;
+  uint8_t* mslots = lb + 64 * (IS + 2 * WT) + lane * WT;  // memo slot m of this lane at mslots + m * 64 * WT
+  ChainMemo* memo = memo_s + lane;
+  uint32_t victim = 0;
   const uint32_t cap = IN ? WT : B.lcap;
   uint64_t pc_item = 0, pc_chain = 0, pc_out = 0, pc_loop = 0, pc_tot = 0, pc_fm = 0, pc_run = 0, pc_slow = 0;
   uint64_t pc_vals = 0, pc_det = 0;
@@ -5165,6 +5224,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
   for (uint32_t w0 = blockIdx.x * 64; w0 < cnt; w0 += gridDim.x * 64) {
     const uint64_t c_a = B.prof ? clock64() : 0;
     const uint32_t ii = w0 + lane;
+    for (uint32_t m = 0; m < M; m++) memo[m * 64].key = 0;  // a new item: nothing memoised
     Item it{};
     uint64_t gm = 0;
     const uint8_t* src = nullptr;
@@ -5219,7 +5279,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
       bool maybe = false, glob = !IN;
       if (fm) {
         csteps += it.vn;
-        cn = run_chain<IN != 0>(P, S, src, it.vn, summ, b0, b1, cap, &cur, sumlut, &osum);
+        if (M) cn = run_chain_memo<M, WT>(P, S, src, it.vn, summ, mslots, memo, &victim, b0, b1, &cur, sumlut, &osum);
+        else cn = run_chain<IN != 0>(P, S, src, it.vn, summ, b0, b1, cap, &cur, sumlut, &osum);
         if (B.prof) pc_run += clock64() - c_sa;
         if (cn < 0 && IN) {
           cn = run_chain<false>(P, S, src, it.vn, summ, g0, g1, B.lcap, &cur, sumlut, &osum);
@@ -6582,11 +6643,12 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
     GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(GI_NCLS), dim3(256), 0, stream, B, cb);
     GI_LAUNCH("k_ibases", k_ibases, dim3(1), dim3(64), 0, stream, B);
     GI_LAUNCH("k_items", k_items, dim3(cb), dim3(256), 0, stream, P, B);
-    GI_LAUNCH("k_stream0", (k_stream<16, 20>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 0u);
-    GI_LAUNCH("k_stream1", (k_stream<32, 36>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 1u);
-    GI_LAUNCH("k_stream2", (k_stream<64, 68>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 2u);
-    GI_LAUNCH("k_stream3", (k_stream<128, 132>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
-    GI_LAUNCH("k_stream4", (k_stream<0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
+    // chain memo slots per lane: as many as keep 8 one-wave workgroups per CU within the LDS
+    GI_LAUNCH("k_stream0", (k_stream<16, 20, 4>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 0u);
+    GI_LAUNCH("k_stream1", (k_stream<32, 36, 3>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 1u);
+    GI_LAUNCH("k_stream2", (k_stream<64, 68, 1>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 2u);
+    GI_LAUNCH("k_stream3", (k_stream<128, 132, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
+    GI_LAUNCH("k_stream4", (k_stream<0, 0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
     if (P.n_det_streams) GI_LAUNCH("k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
     if (B.long_cap) GI_LAUNCH("k_long", k_long, dim3(B.long_grid), dim3(64), 0, stream, P, B);
     if (ev) (void)hipEventRecord(ev[1], stream);
