@@ -458,3 +458,46 @@ def test_gpu_large_body_next_to_small():
         txs.append(t)
     res = _parity(text, gpuinspect.pack(txs))
     assert res.interruption(5) is not None and res.interruption(7) is not None and res.interruption(1) is None
+
+
+@pytest.fixture
+def engine_env(monkeypatch):
+    """Engine tunables are read when a context is created (runtime.cpp gi_ctx_create)."""
+    def set_env(**kv):
+        for k, v in kv.items():
+            monkeypatch.setenv(k, str(v))
+    return set_env
+
+
+def test_gpu_eval_wave_forced_crs_pl4(engine_env):
+    """Every request through k_eval_wave (one wave per request: the 64-rule
+    skip walk and the 64-field filters) on the PL4 ruleset and the C3 mix."""
+    engine_env(GI_EVAL_WAVE_FIELDS=1)
+    text = open(os.path.join(ROOT, "rulesets", "crs_pl4.conf")).read()
+    batch = traffic.TrafficGen(traffic.SEED + 41).batch(300, post_frac=0.5, attack_rate=0.3)
+    res = _parity(text, batch)
+    assert int((res.verdicts["action"] != 0).sum()) > 30
+
+
+def test_gpu_chunked_batch_crs_pl1(engine_env):
+    """A tiny per-chunk queue-pool budget cuts the batch into many request
+    chunks (gi_stage_batch), each a full pipeline pass: verdicts, matched ids
+    and the batch tally stay those of one pass."""
+    engine_env(GI_CHUNK_POOL_WORDS=3e5)
+    text = open(CRS).read()
+    batch = traffic.TrafficGen(traffic.SEED + 42).batch(400, post_frac=0.4, attack_rate=0.3)
+    rs = gpuinspect.Ruleset(text)
+    eng = gpuinspect.Engine(rs, matched_cap=128)
+    eng.stage(batch)
+    eng.run()
+    eng.sync()
+    res = eng.fetch()
+    st = eng.stats()
+    cfg = coraza.parse_seclang(text)
+    orc = compare.oracle_verdicts(cfg, batch, rs.exports)
+    assert not compare.compare(res, orc)
+    t = eng.tally()
+    assert t["n_req"] == batch.n_req
+    assert t["matched_total"] == sum(len(v.matched) for v in orc.values())
+    assert t["n_interrupted"] == sum(1 for v in orc.values() if v.rule_id or v.status)
+    assert any(ln["name"] == "k_collect" for ln in st["launches"])
