@@ -115,7 +115,7 @@ struct ScanLaunch {
   uint32_t mode;                // debugging switches (GI_SCAN_MODE), 0 in production
 };
 
-#define GI_NCLS 145           // item length classes (kernels.hip item_class)
+#define GI_NCLS 2320          // item classes: 16 source groups x length classes (kernels.hip item_class)
 #define GI_RHIST_LDS 1024     // per-rule match counts k_eval aggregates in LDS (more rules: global atomics)
 #define GI_STREAM_GRID 8192  // k_stream workgroups (64 lanes) per bucket launch (~8 waves/SIMD)
 #define GI_PCHUNK 2048       // pool words a k_stream wave reserves at a time
@@ -126,7 +126,8 @@ struct ScanLaunch {
 #define GI_EVAL_WAVE_LDS_WORDS 4096  // k_eval_wave keeps a request's hit words in LDS up to this many
 #define GI_EVAL_WAVE_FIELDS 4096     // default k_eval_wave thresholds (GI_EVAL_WAVE_FIELDS / _RULES env)
 #define GI_EVAL_WAVE_RULES 2048
-#define GI_BPARSE_LDS 32768          // k_bparse LDS body copy (bytes, GI_BPARSE_LDS env; 0: off)
+#define GI_BPARSE_LDS 0              // k_bparse LDS copy of JSON bodies up to this size (GI_BPARSE_LDS env; 0: off --
+                                     // measured: 32 KB made C3's k_bparse 81 -> 272 ms, the LDS cut its occupancy)
 #define GI_CHUNK_POOL_WORDS 16e9     // queue-pool words (estimate) one request chunk of a batch may need
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.

@@ -4322,12 +4322,23 @@ __device__ __forceinline__ void void_request(const DBatch& B, uint32_t r, uint32
 __device__ __forceinline__ uint32_t item_bucket(uint32_t n) {
   return n <= 16 ? 0u : n <= 32 ? 1u : n <= 64 ? 2u : n <= 128 ? 3u : 4u;
 }
-// Length classes: k_items orders the items of each bucket by class, so the 64
-// values of an item wave have (nearly) one length -- the lanes of k_stream's
-// chains and k_scan's lockstep automata then run out of work together.
-// Classes 0..128: one per length; 129..144: 128-byte ranges (the last open).
-__device__ __forceinline__ uint32_t item_class(uint32_t n) { return n <= 128 ? n : min(144u, 129u + (n - 129u) / 128u); }
-__device__ __forceinline__ uint32_t class_bucket(uint32_t c) { return c <= 128 ? item_bucket(c) : 4u; }
+// Item classes: k_items orders the items of each bucket by (source group,
+// length class), so the 64 values of an item wave come from one kind of
+// variable (singles; ARGS_GET / ARGS_POST / headers / cookies / FILES*
+// values or keys) and have (nearly) one length.  The streams that do not
+// admit that kind are then skipped by the whole wave (k_stream), and the
+// lanes of a chain or of k_scan's lockstep automata run out of work together.
+// Length classes per bucket: one per length up to 128 bytes, then 16 ranges
+// of 128 bytes (the last open); bucket b holds 16 groups x kNl[b] classes.
+__constant__ uint32_t kClsLo[GI_NB] = {0, 17, 33, 65, 129};
+__constant__ uint32_t kClsN[GI_NB] = {17, 16, 32, 64, 16};
+__constant__ uint32_t kClsBase[GI_NB + 1] = {0, 272, 528, 1040, 2064, 2320};
+__device__ __forceinline__ uint32_t item_class(uint32_t kind, uint32_t side, uint32_t n) {
+  const uint32_t b = item_bucket(n);
+  const uint32_t g = kind ? ((kind << 1) | side) & 15u : 0u;
+  const uint32_t lc = b < 4 ? n - kClsLo[b] : min(15u, (n - 129u) / 128u);
+  return kClsBase[b] + g * kClsN[b] + lc;
+}
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
@@ -4532,7 +4543,7 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
   // JSON bodies up to B.bparse_lds bytes are parsed out of an LDS copy (the
   // sequential parser then waits on LDS, not on global memory, per byte)
   extern __shared__ __attribute__((aligned(16))) uint8_t jlds[];
-  __shared__ uint32_t chist[GI_NCLS];
+  __shared__ uint32_t chist[GI_NCLS];  // item counts per class of this body's fields
   const uint32_t L = threadIdx.x;
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
     const uint32_t r = B.body_list[bi];
@@ -4651,8 +4662,8 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
       for (uint32_t i = L; i < n_post; i += 64) {
         const Field fl = g.fields[nf0 + i];
         if (fl.kind != FK_ARG_POST) continue;
-        if (sides & 1) atomicAdd(&chist[item_class(fl.vn)], 1u);
-        if (sides & 2) atomicAdd(&chist[item_class(fl.kn)], 1u);
+        if (sides & 1) atomicAdd(&chist[item_class(FK_ARG_POST, 0, fl.vn)], 1u);
+        if (sides & 2) atomicAdd(&chist[item_class(FK_ARG_POST, 1, fl.kn)], 1u);
       }
       __syncthreads();
       for (uint32_t k = L; k < GI_NCLS; k += 64)
@@ -4748,8 +4759,8 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
             const Field fl = g.fields[f];
             if (fl.kind < FK_ARG_GET || fl.kind > FK_FILE_SIZE) continue;
             const uint32_t sides = P.item_sides[fl.kind];
-            if (sides & 1) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.vn)], 1u);
-            if (sides & 2) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.kn)], 1u);
+            if (sides & 1) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.kind, 0, fl.vn)], 1u);
+            if (sides & 2) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.kind, 1, fl.kn)], 1u);
           }
         }
       }
@@ -4773,7 +4784,9 @@ __global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
       const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
       if (!(H->flags & GI_REQ_ERROR_MASK)) {
         for_each_item(P, H, (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES),
-                      [&](uint8_t, uint8_t, uint32_t, uint32_t, uint32_t n) { atomicAdd(&hist[item_class(n)], 1u); });
+                      [&](uint8_t kind, uint8_t, uint32_t side, uint32_t, uint32_t n) {
+                        atomicAdd(&hist[item_class(kind, side, n)], 1u);
+                      });
       }
       for (uint32_t k = 0; k < P.n_always; k++) set_hit(B, P.always_slots[k], r);
     }
@@ -4872,28 +4885,43 @@ __global__ void __launch_bounds__(256) k_ioffsets(DBatch B, uint32_t n_blocks) {
   if (t == 255) B.ctot[c] = part[255];
 }
 
-// Class bases (bucket-major = length order), bucket (base, count), item-wave
-// base per bucket and the total: one lane.
-__global__ void __launch_bounds__(64) k_ibases(DBatch B) {
-  if (threadIdx.x) return;
-  uint32_t run = 0;
-  uint32_t bbase[GI_NB] = {0, 0, 0, 0, 0}, bcnt[GI_NB] = {0, 0, 0, 0, 0};
-  for (uint32_t c = 0; c < GI_NCLS; c++) {
-    const uint32_t b = class_bucket(c);
-    if (c == 0 || class_bucket(c - 1) != b) bbase[b] = run;  // the bucket's first class
+// Class bases (bucket-major order), bucket (base, count), item-wave base per
+// bucket and the total: one workgroup scans the class totals.
+__global__ void __launch_bounds__(256) k_ibases(DBatch B) {
+  __shared__ uint32_t part[256];
+  const uint32_t t = threadIdx.x;
+  constexpr uint32_t per = (GI_NCLS + 255) / 256;
+  const uint32_t c0 = min(GI_NCLS, t * per), c1 = min(GI_NCLS, (t + 1) * per);
+  uint32_t sum = 0;
+  for (uint32_t c = c0; c < c1; c++) sum += B.ctot[c];
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {
+    const uint32_t x = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (uint32_t c = c0; c < c1; c++) {
     B.cbase[c] = run;
-    bcnt[b] += B.ctot[c];
     run += B.ctot[c];
   }
-  uint32_t iw = 0;
-  for (uint32_t b = 0; b < GI_NB; b++) {
-    B.ibk[2 * b] = bbase[b];
-    B.ibk[2 * b + 1] = bcnt[b];
-    atomicAdd(&B.acct3[b], (unsigned long long)bcnt[b]);
-    B.ibk[2 * GI_NB + b] = iw;
-    iw += (bcnt[b] + 63) / 64;
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t total = part[255];
+    uint32_t iw = 0;
+    for (uint32_t b = 0; b < GI_NB; b++) {
+      const uint32_t lo = B.cbase[kClsBase[b]];
+      const uint32_t hi = kClsBase[b + 1] < GI_NCLS ? B.cbase[kClsBase[b + 1]] : total;
+      B.ibk[2 * b] = lo;
+      B.ibk[2 * b + 1] = hi - lo;
+      atomicAdd(&B.acct3[b], (unsigned long long)(hi - lo));
+      B.ibk[2 * GI_NB + b] = iw;
+      iw += (hi - lo + 63) / 64;
+    }
+    B.ibk[3 * GI_NB] = iw;
   }
-  B.ibk[3 * GI_NB] = iw;
 }
 
 // One thread per request, same block shape as k_collect.
@@ -4911,7 +4939,7 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
       const Field* Fd = (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES);
       const uint32_t* boff = B.boffs + blockIdx.x * GI_NCLS;
       for_each_item(P, H, Fd, [&](uint8_t kind, uint8_t sg, uint32_t side, uint32_t fi, uint32_t n) {
-        const uint32_t b = item_bucket(n), c = item_class(n);
+        const uint32_t b = item_bucket(n), c = item_class(kind, side, n);
         const uint32_t at = B.cbase[c] + boff[c] + atomicAdd(&rank[c], 1u);
         GI_BOUND(at < B.items_cap, at, B.items_cap);
         Item it;
@@ -6641,7 +6669,7 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (P.n_streams) {
     GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(GI_NCLS), dim3(256), 0, stream, B, cb);
-    GI_LAUNCH("k_ibases", k_ibases, dim3(1), dim3(64), 0, stream, B);
+    GI_LAUNCH("k_ibases", k_ibases, dim3(1), dim3(256), 0, stream, B);
     GI_LAUNCH("k_items", k_items, dim3(cb), dim3(256), 0, stream, P, B);
     // chain memo slots per lane: as many as keep 8 one-wave workgroups per CU within the LDS
     GI_LAUNCH("k_stream0", (k_stream<16, 20, 4>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 0u);

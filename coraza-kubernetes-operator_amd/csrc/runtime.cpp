@@ -884,7 +884,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       return hip_fail(c, e, "alloc lane scratch");
     if ((e = c->pool.ensure(4ull * c->pool_cap)) != hipSuccess) return hip_fail(c, e, "alloc queue pool");
     if ((e = c->qblk.ensure(8ull * ns * c->qcap)) != hipSuccess) return hip_fail(c, e, "alloc queue blocks");
-    if ((e = c->ctr.ensure(4096)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+    if ((e = c->ctr.ensure(4096 + 8ull * ((4 * GI_NCLS + 63) & ~63))) != hipSuccess) return hip_fail(c, e, "alloc counters");
     (void)ns;
     if ((e = c->slow.ensure(40ull * c->slow_cap)) != hipSuccess) return hip_fail(c, e, "alloc slow list");
     if ((e = c->slow_bytes.ensure(c->slow_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc slow bytes");
@@ -907,7 +907,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if ((e = c->det_bytes.ensure(c->det_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc detect bytes");
   }
   // k_eval -> k_eval_wave request list (its counter lives in ctr)
-  if ((e = c->ctr.ensure(4096)) != hipSuccess) return hip_fail(c, e, "alloc counters");
+  if ((e = c->ctr.ensure(4096 + 8ull * ((4 * GI_NCLS + 63) & ~63))) != hipSuccess) return hip_fail(c, e, "alloc counters");
   if ((e = c->wlist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc wave list");
   const auto t_h2d0 = std::chrono::steady_clock::now();
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
@@ -978,8 +978,8 @@ int gi_run_staged(gi_ctx* c) {
     uint8_t* cp = (uint8_t*)c->ctr.p;
     B.bcounts = (uint32_t*)c->bcounts.p;
     B.boffs = (uint32_t*)c->boffs.p;
-    B.ctot = (uint32_t*)(cp + 1024);   // GI_NCLS words
-    B.cbase = (uint32_t*)(cp + 2048);  // GI_NCLS words
+    B.ctot = (uint32_t*)(cp + 4096);  // GI_NCLS words each
+    B.cbase = (uint32_t*)(cp + 4096 + ((4 * GI_NCLS + 63) & ~63));
     B.ibk = (uint32_t*)(cp + 64);
     B.items = c->items.p;
     B.igm = (uint64_t*)c->igm.p;
