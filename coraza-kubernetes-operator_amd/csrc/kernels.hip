@@ -68,7 +68,7 @@ __device__ inline bool isalnum_(uint8_t c) {
 }
 __device__ inline bool isws(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
 
-__device__ bool eq_bytes(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn) {
+__device__ __forceinline__ bool eq_bytes(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn) {
   if (an != bn) return false;
   for (uint32_t i = 0; i < an; i++)
     if (a[i] != b[i]) return false;
@@ -79,7 +79,7 @@ __device__ bool eq_ascii_ci_both(const uint8_t* a, const uint8_t* b, uint32_t n)
     if (alower(a[i]) != alower(b[i])) return false;
   return true;
 }
-__device__ bool eq_ascii_ci(const uint8_t* a, uint32_t an, const uint8_t* lowered, uint32_t bn) {
+__device__ __forceinline__ bool eq_ascii_ci(const uint8_t* a, uint32_t an, const uint8_t* lowered, uint32_t bn) {
   if (an != bn) return false;
   for (uint32_t i = 0; i < an; i++)
     if (alower(a[i]) != lowered[i]) return false;
@@ -132,7 +132,7 @@ __device__ int64_t go_atoi(const uint8_t* s, uint32_t n, bool* ok) {
 }
 
 // strconv.Itoa into buf (>= 21 bytes), returns length.
-__device__ uint32_t go_itoa(int64_t v, uint8_t* buf) {
+__device__ __forceinline__ uint32_t go_itoa(int64_t v, uint8_t* buf) {
   uint8_t tmp[24];
   uint32_t n = 0;
   uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
@@ -3078,7 +3078,7 @@ __device__ __forceinline__ Str slot_str(Tx& t, const Slot& s, uint8_t* buf) {
   if (s.state == 2) return {s.p, s.n};
   return {buf, 0};
 }
-__device__ int64_t slot_int(const Slot& s, bool* ok) {
+__device__ __forceinline__ int64_t slot_int(const Slot& s, bool* ok) {
   if (s.state == 1) {
     *ok = true;
     return s.num;
@@ -3427,7 +3427,13 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
       res = false;
       break;
     case OP_DETECT_SQLI:  // [upstream] detect_sqli.go: libinjection.IsSQLi (capture of the fingerprint is unobservable here)
-      if (DETECT) res = li_detect_sqli(s, n, (LiSqli*)t.mt, li_tables_const());  // state in the macro scratch (>= 512 B)
+      if (DETECT) {
+        // the tokenizer state of this lane in LDS (k_eval's 128-thread blocks;
+        // k_eval_wave's lanes run identical copies): every state access is an
+        // LDS access instead of a round trip to the request's HBM scratch
+        __shared__ LiSqli li_st[128];
+        res = li_detect_sqli(s, n, &li_st[threadIdx.x & 127u], li_tables_const());
+      }
       break;
     case OP_DETECT_XSS:  // detect_xss.go: libinjection.IsXSS
       if (DETECT) res = li_detect_xss(s, n);
