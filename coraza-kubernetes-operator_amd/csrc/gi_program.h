@@ -535,6 +535,7 @@ struct DProgram {
   uint32_t n_lower_pairs;
   uint32_t n_top;
   uint32_t top_begin[2], top_end[2];  // per-phase walks in top[] (phase 1, phase 2)
+  const uint32_t* top_jump;           // per walk entry: where its rule's skipAfter resumes (runtime.cpp)
   uint32_t n_slots;
   uint32_t n_markers;
   int32_t exports[8];           // TX slot per export, -1 = none

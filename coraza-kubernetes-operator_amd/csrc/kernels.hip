@@ -4163,6 +4163,9 @@ __device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u))
       continue;  // phase A proved the first link matches nothing
     eval_top<W>(t, ri);
+    // a skipAfter the rule just set: the rules up to its marker are all
+    // skipped (no side effects), so resume at the marker entry directly
+    if (t.skip_after >= 0) k = GI_CONST(uint32_t, P.top_jump)[k] - 1;
   }
 }
 

@@ -327,6 +327,17 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
     if (ph == 1) n_ph1 = (uint32_t)top_ph.size();
   }
   UP(top, top_ph, uint32_t)
+  // skipAfter jumps: for a walk entry whose rule has skipAfter, the position of
+  // the first later entry of the same walk with that marker (or the walk's end)
+  std::vector<uint32_t> top_jump(top_ph.size(), 0);
+  for (size_t a = 0; a < top_ph.size(); a++) {
+    const size_t end = a < n_ph1 ? n_ph1 : top_ph.size();
+    const int32_t m = P.rules[top_ph[a]].skip_after;
+    size_t j = a + 1;
+    while (m >= 0 && j < end && P.rules[top_ph[j]].marker != m) j++;
+    top_jump[a] = (uint32_t)(m >= 0 ? j : a + 1);
+  }
+  UP(top_jump, top_jump, uint32_t)
   UP(vars, P.vars, DVarRef)
   UP(excs, P.excs, DExc)
   UP(ops, P.ops, DOp)
