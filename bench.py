@@ -54,11 +54,13 @@ CONFIGS = {
            "CRS-shaped v4 PL1 ruleset (rulesets/crs_pl1.conf) x 1M synthetic GET with query args"),
     "c1": ("tests/golden/samples_ruleset.conf", 10_000, 0.0,
            "config/samples RuleSet x 10k synthetic GET"),
-    "c3": ("rulesets/crs_pl1.conf", 50_000, 0.5,
-           "CRS-shaped v4 PL1 x mixed GET/POST (50% POST, 4-64 KB bodies: 60% urlencoded, 40% JSON)"),
-    "c4": ("rulesets/crs_pl4.conf", 50_000, 0.5,
+    "c3": ("rulesets/crs_pl1.conf", 200_000, 0.5,
+           "CRS-shaped v4 PL1 x mixed GET/POST (50% POST, 4-64 KB bodies: 60% urlencoded, 40% JSON), "
+           "200k requests per batch (run as request chunks)"),
+    "c4": ("rulesets/crs_pl4.conf", 200_000, 0.5,
            "CRS-shaped v4 PL4 (blocking paranoia 4: +35 PL2-4 rules, @detectSQLi/@detectXSS) x C3 mix "
-           "(50% POST 4-64 KB urlencoded/JSON); SURVEY C4 = 10M across 8 GPUs = this batch per GPU, repeated"),
+           "(50% POST 4-64 KB urlencoded/JSON), 200k requests per GPU per batch; SURVEY C4 = 10M across 8 GPUs "
+           "= this batch per GPU, repeated"),
     "c5": (None, 32, 1.0,
            "generated 10k @rx rules + 100k-phrase @pmFromFile (traffic.c5_ruleset) x ~1 MB multipart bodies "
            "(traffic.c5_batch)"),

@@ -7,7 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
 mkdir -p gpurun_out
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 STEPS=${STEPS:-all}
 step() { echo "== $1 $(date +%T)"; }
 step pytest
@@ -31,11 +31,11 @@ timeout -k 10 400 python -u tools/pmc_occupancy.py --config c2 --n-req 1000000 -
 cat gpurun_out/${TAG}_occ.log
 [ "${CONFIGS:-1}" = "0" ] && exit 0
 step c3
-timeout -k 10 400 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3.err || { tail -20 gpurun_out/${TAG}_c3.err; exit 1; }
+timeout -k 10 400 python -u bench.py --config c3 --steps 3 --warmup 1 --e2e-iters 0 > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3.err || { tail -20 gpurun_out/${TAG}_c3.err; exit 1; }
 cat gpurun_out/${TAG}_c3_bench.json
 step c4
-timeout -k 10 400 python -u bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_c4_bench.json 2> gpurun_out/${TAG}_c4.err || { tail -20 gpurun_out/${TAG}_c4.err; exit 1; }
+timeout -k 10 400 python -u bench.py --config c4 --steps 3 --warmup 1 --e2e-iters 0 > gpurun_out/${TAG}_c4_bench.json 2> gpurun_out/${TAG}_c4.err || { tail -20 gpurun_out/${TAG}_c4.err; exit 1; }
 cat gpurun_out/${TAG}_c4_bench.json
 step c5
-timeout -k 10 500 python -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_c5_bench.json 2> gpurun_out/${TAG}_c5.err || { tail -20 gpurun_out/${TAG}_c5.err; exit 1; }
+timeout -k 10 500 python -u bench.py --config c5 --steps 3 --warmup 1 --e2e-iters 0 > gpurun_out/${TAG}_c5_bench.json 2> gpurun_out/${TAG}_c5.err || { tail -20 gpurun_out/${TAG}_c5.err; exit 1; }
 cat gpurun_out/${TAG}_c5_bench.json
