@@ -115,6 +115,7 @@ struct ScanLaunch {
   uint32_t mode;                // debugging switches (GI_SCAN_MODE), 0 in production
 };
 
+#define GI_SLOT_BYTES 16      // sizeof(Slot) (kernels.hip): a TX variable of one request
 #define GI_NCLS 2320          // item classes: 16 source groups x length classes (kernels.hip item_class)
 #define GI_RHIST_LDS 1024     // per-rule match counts k_eval aggregates in LDS (more rules: global atomics)
 #define GI_STREAM_GRID 8192  // k_stream workgroups (64 lanes) per bucket launch (~8 waves/SIMD)

@@ -36,12 +36,15 @@ struct Field {
   uint32_t _pad;
 };
 
-struct Slot {
-  int64_t num;
-  const uint8_t* p;
+struct Slot {  // 16 B: a wave's slot-s accesses cover 1 KB (k_eval's TX traffic)
+  union {
+    int64_t num;       // state 1
+    const uint8_t* p;  // state 2 (n bytes)
+  };
   uint32_t n;
   uint32_t state;  // 0 unset, 1 integer (canonical decimal), 2 string
 };
+static_assert(sizeof(Slot) == GI_SLOT_BYTES, "Slot size (runtime.cpp sizes txslots with it)");
 
 __device__ __constant__ uint8_t kConstStrs[] =
     "0\0URLENCODED\0JSON\0XML\0MULTIPART\0" "1\0JSON: invalid JSON\0" "//@*\0/*\0\0\0\0\0\0\0\0";  // padded for load_u32u
@@ -5579,8 +5582,7 @@ __device__ void value_end(const DProgram& P, const DBatch& B, uint32_t r, const 
 template <uint32_t NB>
 __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B, const DJob& J, const uint8_t* img,
                                              uint32_t K, const uint32_t* trn, const uint32_t* st0, uint32_t umask,
-                                             uint32_t nf, const uint2* d, uint32_t mode, uint64_t* prof_real,
-                                             uint64_t* prof_slot) {
+                                             uint32_t nf, const uint2* d, uint32_t mode) {
   const uint32_t lane = lane_id();
   uint32_t req[NB], len[NB], nwl[NB], nwmax = 0, p0[NB], p1[NB];
   uint64_t fm[NB];
@@ -5618,13 +5620,6 @@ __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B,
     for (uint32_t k = 0; k < GI_JOB_MAX_DFA; k++) st[j][k] = st0[k];
   }
   if (mode & 16) umask = 0;
-  if (prof_real) {  // GI_PROF: bytes stepped by lanes with a value vs the wave's lockstep slots
-    uint64_t real = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < NB; j++) real += len[j] != 0xFFFFFFFFu ? len[j] : 0u;
-    *prof_real += real * K;
-    *prof_slot += (uint64_t)nwmax * 4u * K;  // per lane: words stepped, active or not
-  }
   const uint32_t* jam = (const uint32_t*)img;
   for (uint32_t w = 0; w < nwmax; w++) {
     uint32_t wd[NB];
@@ -5674,7 +5669,6 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)
                                                uint32_t mode, uint32_t acct_slot) {
   uint64_t rwords = 0;  // queue words of this launch's streams, each counted once (algorithmic bytes)
   uint64_t rsteps = 0;  // automaton byte-steps (padded words x 4 x automata of the job)
-  uint64_t preal = 0, pslot = 0;  // GI_PROF lane utilisation
   extern __shared__ __attribute__((aligned(16))) uint8_t simg[];
   __shared__ uint2 clist[1024];
   __shared__ uint32_t wcnt[16];
@@ -5747,20 +5741,13 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)
         rwords += (first && !(d[j].y & GI_QB_SHARED)) ? w : 0;  // a shared block is counted at its writer
         rsteps += (uint64_t)(d[j].y & 0xFFu) * dnw * 4 * K;
       }
-      scan_qblocks<2>(P, B, J, img, K, trn, st0, umask, nf, d, mode, B.prof ? &preal : nullptr, &pslot);
+      scan_qblocks<2>(P, B, J, img, K, trn, st0, umask, nf, d, mode);
     }
     __syncthreads();  // clist / wcnt reuse
   }
   if ((threadIdx.x & 63) == 0 && rwords) atomicAdd(&B.acct[10 + acct_slot], (unsigned long long)rwords);
   if ((threadIdx.x & 63) == 0 && rsteps) atomicAdd(&B.acct[13 + acct_slot], (unsigned long long)rsteps);
-  if (B.prof) {
-    preal = wave_sum(preal);
-    pslot = wave_sum(pslot);
-    if ((threadIdx.x & 63) == 0) {
-      atomicAdd(&B.prof[34 + acct_slot], (unsigned long long)preal);
-      atomicAdd(&B.prof[37 + acct_slot], (unsigned long long)pslot);
-    }
-  }
+
 }
 
 // REQUEST_BODY targets of phase-2 links (residual: the variable only exists
@@ -6250,7 +6237,8 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
 // RuleGroup.Eval(1) -> ProcessRequestBody -> RuleGroup.Eval(2) per request,
 // skipping every phase-A rule whose hit bit is clear.
 #ifndef GI_EVAL_WPE
-#define GI_EVAL_WPE 2  // minimum waves per SIMD k_eval is compiled for (register budget; A/B: 2 beats 1 and 4)
+#define GI_EVAL_WPE 2  // minimum waves per SIMD k_eval is compiled for (register budget; A/B: 2 beats 1 and 4;
+                       // round 3: 1 wave has no spills and 25.6 GB PMC traffic instead of 61 GB, but 26.7 ms vs 24.8)
 #endif
 // Phase B of request r: RuleGroup.Eval(1) -> ProcessRequestBody ->
 // RuleGroup.Eval(2); my[7] = its tally contributions.  W (k_eval_wave): the

@@ -721,7 +721,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     L.cap_b = (uint32_t)cap_b;
     L.cap_t = (uint32_t)cap_t;
     L.cap_mt = (uint32_t)cap_mt;
-    uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)nslots * 24 + 15) / 16 * 16 + GI_RM_BYTES + (cap_b + 15) / 16 * 16 +
+    uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)nslots * GI_SLOT_BYTES + 15) / 16 * 16 + GI_RM_BYTES + (cap_b + 15) / 16 * 16 +
                   2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
     // observable captures (kernels.hip region_of): workspace + one value buffer per group
     sz += (4ull * c->prog.cap_ws_words + 15) / 16 * 16 +
@@ -794,7 +794,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if ((e = c->tally.ensure(sizeof(gi_tally))) != hipSuccess) return hip_fail(c, e, "alloc tally");
   if ((e = c->tally_ext.ensure(4ull * (GI_SCORE_BINS + c->tally_ids.size()))) != hipSuccess)
     return hip_fail(c, e, "alloc detail tally");
-  if ((e = c->txslots.ensure(std::max<uint64_t>(24ull * PG.n_slots * n, 64))) != hipSuccess)
+  if ((e = c->txslots.ensure(std::max<uint64_t>((uint64_t)GI_SLOT_BYTES * PG.n_slots * n, 64))) != hipSuccess)
     return hip_fail(c, e, "alloc tx slots");
   c->hit_words = (PG.n_hit_slots + 31) / 32;
   c->vmap_words = vmap_bits;  // one u32 slot signature per (field, side): bit (slot % 32) of each slot it hit
@@ -1077,7 +1077,7 @@ int gi_run_staged(gi_ctx* c) {
     Bc.caprec = B.caprec ? B.caprec + 4ull * B.crcap * ch.r0 : nullptr;
     Bc.capbytes = B.capbytes ? B.capbytes + (uint64_t)B.cbcap * ch.r0 : nullptr;
     Bc.hits = B.hits + ch.r0;
-    Bc.txslots = (Slot*)((uint8_t*)B.txslots + 24ull * ch.r0);  // sizeof(Slot) == 24 (kernels.hip)
+    Bc.txslots = (Slot*)((uint8_t*)B.txslots + (uint64_t)GI_SLOT_BYTES * ch.r0);
     Bc.body_list = B.body_list + ch.blist_off;
     Bc.n_body = ch.n_body;
     Bc.n_mp_body = ch.n_mp;
@@ -1166,10 +1166,6 @@ int gi_sync(gi_ctx* c) {
     if (c->prof_on && c->prof.p) {
       unsigned long long h[128];
       if (hipMemcpy(h, c->prof.p, 1024, hipMemcpyDeviceToHost) == hipSuccess && c->n_req) {
-        for (int b = 0; b < 3; b++)
-          if (h[37 + b])
-            fprintf(stderr, "GI_PROF k_scan launch %d: lane-utilisation %.3f (%.0f M real byte-steps of %.0f M lockstep slots)\n",
-                    b, (double)h[34 + b] / h[37 + b], h[34 + b] / 1e6, h[37 + b] / 1e6);
         for (int b = 0; b < 5; b++)
           fprintf(stderr, "GI_PROF k_stream bucket %d (sum over waves, Mcyc): item %.1f chain %.1f out %.1f loop %.1f total %.1f\n",
                   b, h[40 + 5 * b] / 1e6, h[41 + 5 * b] / 1e6, h[42 + 5 * b] / 1e6, h[43 + 5 * b] / 1e6,
