@@ -1433,6 +1433,15 @@ __device__ uint32_t json_string_end(const uint8_t* s, uint32_t n, uint32_t i, bo
   *esc = false;
   i++;
   while (i < n) {
+    // four plain bytes at a time (none is '"', '\\' or a control byte: the
+    // per-byte step below would only advance over them)
+    while (i + 4 <= n) {
+      const uint32_t w = load_u32u(s + i);
+      const uint32_t q = w ^ 0x22222222u, b = w ^ 0x5C5C5C5Cu;
+      if ((((q - 0x01010101u) & ~q) | ((b - 0x01010101u) & ~b) | ((w - 0x20202020u) & ~w)) & 0x80808080u) break;
+      i += 4;
+    }
+    if (i >= n) break;
     const uint8_t c = s[i];
     if (c == '"') return i + 1;
     if (c < 0x20) return 0;
@@ -1519,6 +1528,20 @@ __device__ uint32_t json_number_end(const uint8_t* s, uint32_t n, uint32_t i) {
     while (i < n && s[i] >= '0' && s[i] <= '9') i++;
   }
   return i;
+}
+
+// d[0, n) = s[0, n), four source bytes per load (s may be read up to 7 bytes
+// past its end: every arena is padded)
+__device__ __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint32_t n) {
+  uint32_t k = 0;
+  for (; k + 4 <= n; k += 4) {
+    const uint32_t w = load_u32u(s + k);
+    d[k] = (uint8_t)w;
+    d[k + 1] = (uint8_t)(w >> 8);
+    d[k + 2] = (uint8_t)(w >> 16);
+    d[k + 3] = (uint8_t)(w >> 24);
+  }
+  for (; k < n; k++) d[k] = s[k];
 }
 
 __device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
@@ -1621,7 +1644,7 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
     if (F.is_arr) {
       key = tx_alloc(t, F.kn + 12);
       if (!key) return;
-      for (uint32_t k = 0; k < F.kn; k++) key[k] = t.bytes[F.koff + k];
+      copy_bytes(key, t.bytes + F.koff, F.kn);
       key[F.kn] = '.';
       kn = F.kn + 1 + go_itoa((int64_t)F.count, key + F.kn + 1);
       t.nb -= F.kn + 12 - kn;  // give back the unused tail
@@ -1635,13 +1658,13 @@ __device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t
       const uint32_t rn = e - i - 2;
       key = tx_alloc(t, F.kn + 1 + rn);
       if (!key) return;
-      for (uint32_t k = 0; k < F.kn; k++) key[k] = t.bytes[F.koff + k];
+      copy_bytes(key, t.bytes + F.koff, F.kn);
       key[F.kn] = '.';
       uint32_t sn = rn;
       if (esc) {
         sn = json_unescape(s + i + 1, rn, key + F.kn + 1);
       } else {
-        for (uint32_t k = 0; k < rn; k++) key[F.kn + 1 + k] = s[i + 1 + k];
+        copy_bytes(key + F.kn + 1, s + i + 1, rn);
       }
       kn = F.kn + 1 + sn;
       t.nb -= rn - sn;
