@@ -5984,7 +5984,7 @@ __device__ bool wave_run_chain(const DProgram& P, uint32_t off, uint32_t len, co
       if (!bad) {
         __syncthreads();  // tmp written; dst (possibly the source) is free
         uint32_t sm = m > 0 ? value_summary(lt, (uint32_t)m) : 0u;
-        for (uint32_t i = 0; i < (uint32_t)m; i++) dst[o0 + i] = lt[i];
+        copy_bytes(dst + o0, lt, (uint32_t)max(m, (int64_t)0));
         for (int x = 32; x > 0; x >>= 1) sm |= (uint32_t)__shfl_xor((int)sm, x, 64);
         summ = sm;
         __syncthreads();
