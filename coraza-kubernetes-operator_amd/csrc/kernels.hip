@@ -5687,8 +5687,11 @@ __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B,
 // per job change; !LDS: the image is read from HBM (automata too large for LDS).
 // BIG: the 1-workgroup-per-CU launch of images above 64 KB (its own symbol,
 // so per-kernel profiles keep the two launches apart).
+#ifndef GI_SCAN_WPE
+#define GI_SCAN_WPE 8  // k_scan: 8 waves/SIMD (64 VGPRs, 25 spills); measured: 4 (85 VGPRs, no spills) is slower (C2 18.4 -> 22.2 ms)
+#endif
 template <bool LDS, bool BIG>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_scan(DProgram P, DBatch B, const uint32_t* __restrict__ jl, uint32_t n_jl,
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GI_SCAN_WPE, 8))) k_scan(DProgram P, DBatch B, const uint32_t* __restrict__ jl, uint32_t n_jl,
                                                uint32_t mode, uint32_t acct_slot) {
   uint64_t rwords = 0;  // queue words of this launch's streams, each counted once (algorithmic bytes)
   uint64_t rsteps = 0;  // automaton byte-steps (padded words x 4 x automata of the job)
