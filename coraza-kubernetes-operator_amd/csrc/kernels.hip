@@ -3142,13 +3142,6 @@ __device__ __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
     const DTmplPart& p = P.tparts[tm.part_begin];
     return {P.strpool + p.off, p.len};
   }
-  if (tm.part_count == 1 && P.tparts[tm.part_begin].kind == TP_TX) {
-    // one string-valued TX variable (e.g. %{tx.restricted_extensions}): its
-    // bytes as they are, not a copy into the macro scratch (not persistent:
-    // a setvar still copies it into the TX arena)
-    const Slot sl = TXS(t, P.tparts[tm.part_begin].slot);
-    if (sl.state == 2) return {sl.p, sl.n};
-  }
   uint32_t o = 0;
   for (uint32_t k = 0; k < tm.part_count; k++) {
     const DTmplPart p = P.tparts[tm.part_begin + k];
