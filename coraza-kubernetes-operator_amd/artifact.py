@@ -47,14 +47,22 @@ def source_digest(rules: str, exports: Sequence[str] = gpuinspect.DEFAULT_EXPORT
     return fnv64(data)
 
 
+def artifact_fields(rules: str, ruleset: Optional[gpuinspect.Ruleset] = None,
+                    data_files: Optional[Dict[str, bytes]] = None) -> Dict:
+    """The GPU artifact of `rules` as the fields an entry carries beside
+    `rules` (the emitter cache.RuleSetCache calls on every Put)."""
+    rs = ruleset if ruleset is not None else gpuinspect.Ruleset(rules, data_files=data_files)
+    return {"gpu_artifact": base64.b64encode(rs.save()).decode(),
+            "gpu_artifact_version": ARTIFACT_VERSION,
+            "gpu_source_digest": "%016x" % rs.info["source_digest"]}
+
+
 def entry(uuid: str, timestamp: str, rules: str, ruleset: Optional[gpuinspect.Ruleset] = None,
           data_files: Optional[Dict[str, bytes]] = None) -> Dict:
     """RuleSetEntry JSON plus the GPU artifact of `rules`."""
-    rs = ruleset if ruleset is not None else gpuinspect.Ruleset(rules, data_files=data_files)
-    return {"uuid": uuid, "timestamp": timestamp, "rules": rules,
-            "gpu_artifact": base64.b64encode(rs.save()).decode(),
-            "gpu_artifact_version": ARTIFACT_VERSION,
-            "gpu_source_digest": "%016x" % rs.info["source_digest"]}
+    e = {"uuid": uuid, "timestamp": timestamp, "rules": rules}
+    e.update(artifact_fields(rules, ruleset, data_files))
+    return e
 
 
 def ruleset_from_entry(e: Dict, exports: Sequence[str] = gpuinspect.DEFAULT_EXPORTS,
