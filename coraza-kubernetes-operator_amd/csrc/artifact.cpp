@@ -287,6 +287,11 @@ bool validate_program(const Program& P, std::string* err) {
         (r.chain_next >= 0 && (uint32_t)r.chain_next >= nrules) || r.phase > 5 ||
         (r.hit_slot >= 0 && (uint32_t)r.hit_slot >= nhit) || r.hit_slot < -1)
       return bad("rule record out of range");
+    // k_eval runs the link's capture program (run_capture reads P.pikes[op.pike] and the
+    // request's capture workspace): only an @rx link with a program may carry the flag
+    if ((r.flags & RF_CAPTURE) &&
+        (r.op < 0 || P.ops[r.op].kind != OP_RX || P.ops[r.op].pike < 0))
+      return bad("capture flag without a capture program");
   }
   for (uint32_t t : P.body_links)
     if (t >= nrules || P.rules[t].op < 0 || P.rules[t].hit_slot < 0) return bad("body link");

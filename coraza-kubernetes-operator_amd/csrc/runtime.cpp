@@ -256,6 +256,7 @@ int gi_ruleset_load(const uint8_t* buf, size_t n, gi_ruleset** out, char* err, s
 void gi_ruleset_free(gi_ruleset* rs) { delete rs; }
 
 const char* gi_compiler_rev(void) { return kCompilerRev; }
+uint32_t gi_abi_version(void) { return GI_ABI_VERSION; }
 
 int gi_ruleset_info_get(const gi_ruleset* rs, gi_ruleset_info* out) {
   if (!rs || !out) return GI_EINVAL;
@@ -744,8 +745,18 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if (nt == 1) {
       work(0);
     } else {
+      // a thread the system refuses (pid / thread limits) must not throw across
+      // the C ABI: its slice runs on the calling thread instead
       std::vector<std::thread> th;
-      for (uint32_t k = 0; k < nt; k++) th.emplace_back(work, k);
+      std::vector<uint32_t> inline_slices;
+      for (uint32_t k = 0; k < nt; k++) {
+        try {
+          th.emplace_back(work, k);
+        } catch (...) {
+          inline_slices.push_back(k);
+        }
+      }
+      for (uint32_t k : inline_slices) work(k);
       for (auto& x : th) x.join();
     }
     for (uint32_t k = 0; k < nt; k++)

@@ -132,6 +132,9 @@ class _Stats(ctypes.Structure):
 _LIB = None
 
 
+ABI_VERSION = 4  # include/gpuinspect.h GI_ABI_VERSION: the ctypes structs below mirror that layout
+
+
 def load_library(path: str = LIB_PATH):
     """Load libgpuinspect.so (raises if it has not been built)."""
     global _LIB
@@ -141,6 +144,10 @@ def load_library(path: str = LIB_PATH):
         raise EngineError("libgpuinspect.so not built (run __graft_entry__.build() or make -C "
                           "coraza-kubernetes-operator_amd)")
     lib = ctypes.CDLL(path)
+    lib.gi_abi_version.restype = ctypes.c_uint32
+    if lib.gi_abi_version() != ABI_VERSION:
+        raise EngineError("libgpuinspect.so has ABI %d, this binding expects %d (rebuild the library)"
+                          % (lib.gi_abi_version(), ABI_VERSION))
     vp, u32, u64, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
     lib.gi_compile.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(_CompileOpts), ctypes.POINTER(vp),
                                ctypes.c_char_p, sz]

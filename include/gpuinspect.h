@@ -213,6 +213,13 @@ typedef struct {
   uint64_t launch_steps[GI_STATS_LAUNCHES];     /* automaton byte-steps of each k_scan launch (secondary bound) */
 } gi_stats;
 
+/* ABI revision of the structs above (gi_batch, gi_results, gi_verdict,
+ * gi_tally, gi_stats, ...).  It changes whenever one of them changes layout;
+ * a binding checks gi_abi_version() == GI_ABI_VERSION before passing any of
+ * them (INTEGRATION.md lists the revisions). */
+#define GI_ABI_VERSION 4
+uint32_t gi_abi_version(void);
+
 /* ------------------------------------------------------------ compile */
 int gi_compile(const char* seclang, size_t n, const gi_compile_opts* opts, gi_ruleset** out,
                char* err, size_t errcap);

@@ -120,6 +120,26 @@ def test_artifact_rejects_out_of_range_records(case):
         gpuinspect.Ruleset.load(_reseal(buf))
 
 
+def test_artifact_rejects_capture_flag_without_program():
+    """RF_CAPTURE on a link without a capture program would make k_eval read
+    P.pikes[-1]: the loader refuses it."""
+    import struct
+    blob = _crs_blob()
+    off, esz, cnt = _sections(blob)[1]  # DRule records (64 B)
+    assert esz == 64
+    for i in range(cnt):
+        op = struct.unpack_from("<i", blob, off + i * esz + 32)[0]
+        flags = blob[off + i * esz + 54]
+        if op >= 0 and not flags & 4:
+            break
+    else:
+        pytest.fail("no operator rule without capture")
+    buf = bytearray(blob)
+    buf[off + i * esz + 54] |= 4  # RF_CAPTURE
+    with pytest.raises(gpuinspect.SecLangError, match="invalid GPU artifact"):
+        gpuinspect.Ruleset.load(_reseal(buf))
+
+
 def test_artifact_other_compiler_revision():
     blob = gpuinspect.Ruleset(TEXTS["samples"]).save()
     off, esz, _ = _sections(blob)[100]  # scalars: compiler_rev is the last u64
