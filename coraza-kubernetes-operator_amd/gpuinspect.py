@@ -64,7 +64,7 @@ CAPTURE_DT = np.dtype([("rule_id", "<i4"), ("group", "<u4"), ("off", "<u4"), ("l
 assert REQUEST_DT.itemsize == 96 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 88
 
 EXPORTED_SYMBOLS = (
-    "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name", "gi_ruleset_describe",
+    "gi_abi_version", "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name", "gi_ruleset_describe",
     "gi_ctx_create", "gi_ctx_free", "gi_last_error", "gi_inspect_batch", "gi_stage_batch",
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
     "gi_ctx_stream", "gi_selftest_regex", "gi_selftest_plan", "gi_selftest_triggers",
