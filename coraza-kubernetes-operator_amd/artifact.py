@@ -26,7 +26,7 @@ from typing import Callable, Dict, Optional, Sequence
 
 import gpuinspect
 
-ARTIFACT_VERSION = 3  # csrc/artifact.h kArtifactVersion
+ARTIFACT_VERSION = 5  # csrc/artifact.h kArtifactVersion
 
 
 def fnv64(data: bytes, h: int = 1469598103934665603) -> int:

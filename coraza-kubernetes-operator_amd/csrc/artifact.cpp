@@ -41,7 +41,7 @@ uint64_t compiler_rev_hash() { return fnv64((const uint8_t*)kCompilerRev, strlen
   X(10, dfas) X(11, trans) X(12, u8pool) X(13, nranges) X(14, strpool) X(15, slot_names) X(16, u64pool)     \
   X(17, streams) X(18, filters) X(19, sfilt) X(20, body_links) X(21, always_slots) X(22, jobs) X(23, jdfas) \
   X(24, pats) X(25, svals) X(26, images) X(27, exports) X(28, nfas) X(29, pikes) X(30, pike_insts)              \
-  X(31, pike_ranges)
+  X(31, pike_ranges) X(32, dyn_sites) X(33, txrx)
 
 constexpr uint32_t kTagScalars = 100, kTagPlan = 101, kTagExportNames = 102;
 
@@ -49,7 +49,7 @@ uint64_t layout_signature() {
   const uint64_t sz[] = {sizeof(DRule), sizeof(DVarRef), sizeof(DExc), sizeof(DOp), sizeof(DAction),
                          sizeof(DTmplPart), sizeof(DTmpl), sizeof(DDfa), sizeof(DStream), sizeof(DFilter),
                          sizeof(DJob), sizeof(DJobDfa), sizeof(DPat), sizeof(DScanVal), sizeof(Scalars),
-                         sizeof(DNfa), sizeof(DPike), sizeof(DPikeInst)};
+                         sizeof(DNfa), sizeof(DPike), sizeof(DPikeInst), sizeof(DDynSite)};
   return fnv64((const uint8_t*)sz, sizeof(sz));
 }
 
@@ -301,6 +301,11 @@ bool validate_program(const Program& P, std::string* err) {
     if (v.key_mode > 2) return bad("variable key mode");
     if (!in(v.exc_begin, v.exc_count, P.excs.size())) return bad("variable exceptions");
     if (v.var == V_TX && v.slot >= (int32_t)nslot) return bad("variable TX slot");
+    if (v.var == V_TX && v.key_mode == 2) {  // static slots the key regex matches
+      if (!in(v.key_off, v.key_len, P.txrx.size())) return bad("TX regex slot list");
+      for (uint32_t k = 0; k < v.key_len; k++)
+        if (P.txrx[v.key_off + k] >= nslot) return bad("TX regex slot");
+    }
   }
   for (const DExc& x : P.excs) {
     if (x.dfa >= 0 ? !single_dfa(x.dfa) : !in(x.off, x.len, nstr)) return bad("exception");
@@ -321,11 +326,12 @@ bool validate_program(const Program& P, std::string* err) {
   }
   for (const DAction& a : P.acts) {
     if (a.kind == A_SETVAR || a.kind == A_SETVAR_DEL) {
-      if (a.slot < 0 || (uint32_t)a.slot >= nslot) return bad("setvar slot");
+      if (a.slot < -1 || (a.slot >= 0 && (uint32_t)a.slot >= nslot)) return bad("setvar slot");
+      if (a.slot == -1 && (a.aux < 0 || (size_t)a.aux >= ntm || P.dyn_sites.empty())) return bad("setvar key template");
       if (a.tmpl >= 0 && (size_t)a.tmpl >= ntm) return bad("setvar template");
       if ((a.a == SV_ADD_SLOT || a.a == SV_SUB_SLOT) && (a.b < 0 || (uint64_t)a.b >= nslot)) return bad("setvar source");
     }
-    if (a.kind == A_CTL_RULE_REMOVE_TARGET && (a.tmpl < 0 || a._pad2 < 0 || !in((uint32_t)a.tmpl, (uint32_t)a._pad2, nstr)))
+    if (a.kind == A_CTL_RULE_REMOVE_TARGET && (a.tmpl < 0 || a.aux < 0 || !in((uint32_t)a.tmpl, (uint32_t)a.aux, nstr)))
       return bad("ctl target key");
   }
   // capture programs (pike.h): every jump inside its program, rune ranges in the pool

@@ -773,6 +773,7 @@ struct Lower {
   std::map<std::string, int> markers;
   std::map<std::string, int> dfa_cache;  // -1: no DFA (state cap), see nfa_cache
   std::map<std::string, int> nfa_cache;
+  std::vector<std::pair<uint32_t, std::string>> tx_rx_vars;  // regex-keyed TX targets: (vars index, key regex)
   uint32_t cap;
 
   uint32_t str(const std::string& s) {
@@ -1103,6 +1104,7 @@ struct Lower {
         if (v.key_rx) {
           vr.key_mode = 2;
           vr.key_dfa = regex_dfa(v.key);
+          if (vr.var == V_TX) tx_rx_vars.emplace_back((uint32_t)P->vars.size(), v.key);
         } else if (!v.key.empty()) {
           vr.key_mode = 1;
           std::string k = vr.ci ? lower(v.key) : v.key;
@@ -1163,11 +1165,100 @@ struct Lower {
     }
   }
 
+  // setvar whose key has a macro [upstream internal/actions/setvar.go: the key
+  // is expanded per execution, then lowercased]: a run-time TX key (k_eval
+  // dyn_slot).  Records how many executions / bytes the action can need per
+  // request (DDynSite, gi_program.h) so the host sizes the dynamic TX area
+  // exactly instead of guessing.
+  void dyn_setvar(const IrRule& r, const IrNd& nd) {
+    DAction a{};
+    a.kind = nd.sv_remove ? A_SETVAR_DEL : A_SETVAR;
+    a.slot = -1;
+    a.aux = tmpl(nd.sv_key);
+    a.tmpl = nd.sv_remove ? -1 : tmpl(nd.sv_value);
+    if (a.kind == A_SETVAR) classify_setvar(&a);
+    DDynSite ds{};
+    ds.mm = r.multimatch ? (uint32_t)r.transforms.size() + 1 : 1;
+    // the link's transformation chain: growth of the matched value on ASCII / any input
+    uint32_t ga = 1, gn = 1;
+    bool ascii = true;
+    for (const std::string& tn : r.transforms) {
+      uint8_t code = 0;
+      transform_code(tn, &code);
+      switch (code) {
+        case T_LOWERCASE:
+        case T_UTF8TOUNICODE:  // a non-ASCII byte: U+FFFD (3 B) / "%uXXXX" for a 2-byte rune
+          ga *= ascii ? 1 : 3;
+          gn *= 3;
+          break;
+        case T_URLENCODE: ga *= 3; gn *= 3; break;
+        case T_HEXENCODE: ga *= 2; gn *= 2; break;
+        case T_BASE64ENCODE: ga *= 2; gn *= 2; break;
+        case T_SHA1: case T_MD5: case T_LENGTH: ds.fixed += 64; break;
+        case T_URLDECODE: case T_URLDECODEUNI: case T_HTMLENTITYDECODE: case T_JSDECODE: case T_CSSDECODE:
+        case T_BASE64DECODE: case T_BASE64DECODEEXT: case T_HEXDECODE: case T_ESCAPESEQDECODE:
+          ascii = false;  // can emit non-ASCII bytes from ASCII input
+          break;
+        default: break;
+      }
+      if (gn > 729) unsup("setvar with a macro key after a transformation chain that grows values " +
+                          std::to_string(gn) + "x");
+    }
+    ds.g_ascii = ga;
+    ds.g_any = gn;
+    const bool own_capture = r.capture && r.has_op && r.op_name == "rx" && !r.op_neg;
+    auto parts = [&](int tid) {
+      if (tid < 0) return;
+      const DTmpl& tm = P->tmpls[tid];
+      for (uint32_t k = 0; k < tm.part_count; k++) {
+        const DTmplPart& p = P->tparts[tm.part_begin + k];
+        if (p.kind == TP_LIT) {
+          ds.lit += p.len;
+        } else if (p.kind == TP_MV) {
+          ds.n_val++;
+        } else if (p.kind == TP_MVNAME) {
+          ds.n_mvname++;
+        } else if (p.kind == TP_TX && own_capture) {
+          const uint32_t no = P->slot_names[2 * p.slot], nn = P->slot_names[2 * p.slot + 1];
+          const bool digit = nn == 1 && P->strpool[no] >= '0' && P->strpool[no] <= '8';
+          if (digit) ds.n_val++;
+          else ds.n_big++;
+        } else {
+          ds.n_big++;
+        }
+      }
+    };
+    parts(a.aux);
+    parts(a.tmpl);
+    for (const IrVar& v : r.vars) {
+      const int sid = single_id(v.name);
+      if (sid >= 0 || v.count) ds.nsingles++;
+      else if (v.name == "REQUEST_HEADERS_NAMES") ds.hdr_names++;
+      else if (v.name == "REQUEST_HEADERS") ds.hdr_vals++;
+      else if (v.name == "TX" || v.name.rfind("MATCHED_VAR", 0) == 0)
+        unsup("setvar with a macro key on a rule reading " + v.name);
+      else ds.other_coll++;
+    }
+    ds.no_targets = r.vars.empty() ? 1 : 0;
+    {  // the key's leading literal (which static TX names the key could ever produce)
+      const DTmpl& tm = P->tmpls[a.aux];
+      const DTmplPart& p0 = P->tparts[tm.part_begin];
+      std::string pre = tm.part_count && p0.kind == TP_LIT ? lower(std::string((const char*)&P->strpool[p0.off], p0.len)) : "";
+      ds.prefix_off = str(pre);
+      ds.prefix_len = (uint32_t)pre.size();
+    }
+    P->dyn_sites.push_back(ds);
+    P->acts.push_back(a);
+  }
+
   void actions(const IrRule& r, DRule* d) {
     d->act_begin = (uint32_t)P->acts.size();
     for (auto& nd : r.nd) {
       if (nd.is_setvar) {
-        if (nd.sv_key.find("%{") != std::string::npos) unsup("setvar with a macro key");
+        if (nd.sv_key.find("%{") != std::string::npos) {
+          dyn_setvar(r, nd);
+          continue;
+        }
         DAction a{};
         a.kind = nd.sv_remove ? A_SETVAR_DEL : A_SETVAR;
         a.slot = slot(nd.sv_key);
@@ -1224,7 +1315,7 @@ struct Lower {
         a.b = hi;
         a.slot = vid;
         a.tmpl = (int32_t)str(key);
-        a._pad2 = (int32_t)key.size();
+        a.aux = (int32_t)key.size();
         P->acts.push_back(a);
       } else if (nd.ctl_name == "ruleengine") {
         DAction a{};
@@ -2117,6 +2208,24 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
     out->export_names = exports;
     for (auto& e : exports) out->exports.push_back(L.slot(e));
     out->n_slots = (uint32_t)L.slots.size();
+    // regex-keyed TX targets: the static slots whose (lowercase) names the key
+    // regex matches, listed once here instead of matched per request; keys a
+    // macro-key setvar creates at run time are matched by k_eval
+    for (const auto& tv : L.tx_rx_vars) {
+      DVarRef& v = out->vars[tv.first];
+      Regex re;
+      Dfa d;
+      std::string e2;
+      if (!re_parse(tv.second, &re, &e2) || !build_regex_dfa(re, &d, &e2, L.cap))
+        unsup("TX key regex " + tv.second + ": " + e2);
+      v.key_off = (uint32_t)out->txrx.size();
+      for (uint32_t sidx = 0; sidx < out->n_slots; sidx++) {
+        const uint8_t* nm = &out->strpool[out->slot_names[2 * sidx]];
+        if (dfa_host_match(d, nm, out->slot_names[2 * sidx + 1])) out->txrx.push_back(sidx);
+      }
+      v.key_len = (uint32_t)out->txrx.size() - v.key_off;
+    }
+    if (out->txrx.empty()) out->txrx.push_back(0);
     out->n_markers = (uint32_t)L.markers.size();
     if (out->strpool.empty()) out->strpool.push_back(0);
     if (out->u8pool.empty()) out->u8pool.push_back(0);

@@ -16,7 +16,7 @@ namespace gi {
 // even when the record layout stays the same.  gi_compile folds it into the
 // source digest and the artifact stores it, so an artifact written by another
 // compiler revision is rejected (and recompiled from the rules text).
-constexpr const char* kCompilerRev = "gi-seclang-compiler/13";
+constexpr const char* kCompilerRev = "gi-seclang-compiler/14";
 
 struct Program {
   std::vector<DRule> rules;
@@ -51,6 +51,8 @@ struct Program {
   std::vector<DPike> pikes;            // submatch programs of observable captures
   std::vector<DPikeInst> pike_insts;
   std::vector<uint32_t> pike_ranges;
+  std::vector<DDynSite> dyn_sites;     // macro-key setvars (run-time TX keys)
+  std::vector<uint32_t> txrx;          // static slots each regex-keyed TX target matches
   uint32_t n_hit_slots = 0;
   uint32_t n_union_dfas = 0;
   uint32_t max_img_bytes = 0;      // largest small-job LDS image

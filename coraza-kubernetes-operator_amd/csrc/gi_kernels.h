@@ -23,6 +23,8 @@ struct ReqLayout {
   uint32_t vmap_bits;  // 2 x cap_f signatures: word 2f = value of field f, 2f + 1 = its key
   uint32_t hset_mask;  // exact phase-A hit set: capacity - 1 (a power of two minus one)
   uint64_t hset_word;  // its first word in DBatch.hset: [0] overflow flag, [1, cap] keys
+  uint32_t dyn_cap;    // dynamic TX area (macro-key setvars): entries
+  uint32_t dyn_capb;   // and bytes (0 / 0: the program has none)
 };
 
 struct DBatch {

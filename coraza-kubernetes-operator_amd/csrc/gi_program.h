@@ -409,7 +409,8 @@ struct DVarRef {
   int32_t key_dfa;
   uint32_t key_off, key_len;  // literal key in string pool (lowercased when ci)
   uint32_t exc_begin, exc_count;
-  int32_t slot;      // TX literal key -> slot
+  int32_t slot;      // TX literal key -> slot (TX regex key: key_off / key_len = the static slots it
+                     // matches in DProgram.txrx; dynamic keys are matched at run time)
   uint8_t residual;  // a body-phase single (REQUEST_BODY, ...) of a phase-A link: phase A does
                      // not see it, so a clear hit bit leaves it for k_eval to test
   uint8_t _pad[3];
@@ -453,10 +454,37 @@ struct DNfa {
 struct DAction {
   uint8_t kind;
   uint8_t _pad[3];
-  int32_t slot;   // A_SETVAR*: TX slot
+  int32_t slot;   // A_SETVAR*: TX slot; -1: the key has a macro (aux = its template, see DDynSite)
   int32_t tmpl;   // A_SETVAR: value template (-1: empty value)
-  int32_t _pad2;
+  int32_t aux;    // A_SETVAR* with slot -1: key template; A_CTL_RULE_REMOVE_TARGET: key length
   int64_t a, b;   // ctl arguments
+};
+
+// A setvar whose key has a macro (setvar:'tx.header_name_920450_%{tx.0}=...')
+// creates TX keys at run time: k_eval keeps them in the request's dynamic TX
+// area (DynHdr + DynEnt[cap] + bytes, kernels.hip dyn_slot).  One record per
+// such action, for the host to size that area from the request (runtime.cpp):
+//   executions <= mm * (nsingles + (hdr_names + hdr_vals) * headers + other_coll * field capacity),
+//                 (each a count of such targets)
+//                 or mm when the rule has no targets (SecAction)
+//   bytes      <= executions * (lit + fixed + 32 * n_mvname)
+//                 + g * (n_val + n_mvname) * (bytes of the values the targets can produce)
+//                 + executions * n_big * max(cap_t, cap_mt)
+// where g is g_ascii when those bytes are ASCII, else g_any (the growth of the
+// link's transformation chain: the matched value a %{tx.<digit>} capture,
+// %{MATCHED_VAR} or %{MATCHED_VAR_NAME} part reads is at most g x its raw bytes).
+struct DDynSite {
+  uint32_t mm;         // multiMatch: transformations + 1, else 1
+  uint32_t lit;        // literal bytes of the key and value templates
+  uint32_t fixed;      // bytes per execution a digest / length transformation may yield
+  uint32_t nsingles;   // single-variable targets
+  uint32_t n_val;      // parts reading the matched value (own capture group, MATCHED_VAR)
+  uint32_t n_mvname;   // MATCHED_VAR_NAME parts
+  uint32_t n_big;      // other macro parts (any TX value, singles, headers): <= max(cap_t, cap_mt) each
+  uint32_t g_ascii, g_any;
+  uint8_t hdr_names, hdr_vals, other_coll;  // targets: REQUEST_HEADERS_NAMES, REQUEST_HEADERS, other collections
+  uint8_t no_targets;
+  uint32_t prefix_off, prefix_len;  // the key template's leading literal (strpool, lowercase)
 };
 
 struct DTmplPart {
@@ -536,10 +564,16 @@ struct DProgram {
   uint32_t n_top;
   uint32_t top_begin[2], top_end[2];  // per-phase walks in top[] (phase 1, phase 2)
   const uint32_t* top_jump;           // per walk entry: where its rule's skipAfter resumes (runtime.cpp)
+  const uint32_t* slot_hash;          // static TX slot by name: open addressing on gi_fnv1a, entry = slot + 1
+  uint32_t slot_hash_mask;            // (runtime.cpp; a macro-key setvar resolves to a static slot first)
+  uint32_t n_dyn_sites;               // macro-key setvars (DDynSite): requests carry a dynamic TX area
+  const uint32_t* txrx;               // static slots a regex-keyed TX target matches (DVarRef.key_off/len)
   uint32_t n_slots;
   uint32_t n_markers;
   int32_t exports[8];           // TX slot per export, -1 = none
   uint32_t n_exports;
+  uint32_t hist_mask;           // exports whose sum the score histogram bins (runtime.cpp: the per-paranoia-level
+                                // inbound scores when exported, else export 0)
   uint8_t rule_engine;          // EngineMode
   uint8_t body_access;
   uint8_t mv_used;              // some target / macro reads MATCHED_VAR(S)(_NAME(S)): k_eval records matches

@@ -1304,6 +1304,7 @@ struct Tx {
   MvState* mv;               // matched-variable state (nullptr unless DProgram.mv_used)
   uint32_t* capws;           // pike_match workspace (observable captures; nullptr: none)
   uint8_t* capbuf;           // per capture group g: cap_t bytes holding TX.g's value
+  uint8_t* dyn;              // TX keys macro-key setvars created (DynHdr; nullptr: the program has none)
   uint32_t cur_id;           // id of the top-level rule being evaluated (capture records)
   bool profon;               // GI_PROF counters (diagnostics)
   uint32_t prof_visits, prof_evals, prof_rules;
@@ -3174,9 +3175,73 @@ __device__ __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
   return {t.mt, o};
 }
 
+// Run-time TX keys (setvar:'tx.header_name_920450_%{tx.0}=...'): the request's
+// dynamic area holds DynHdr, then cap DynEnt records (in creation order), then
+// capb bytes for their keys and string values.  runtime.cpp sizes it from the
+// request (DDynSite), so it never runs out; a full area still only flags
+// GI_REQ_OVERFLOW.
+struct DynHdr {
+  uint32_t n, cap, nb, capb;
+};
+struct DynEnt {
+  const uint8_t* k;
+  uint32_t kn, h;
+  Slot s;
+};
+static_assert(sizeof(DynEnt) == 32, "runtime.cpp sizes DynEnt as 32 bytes");
+__device__ __forceinline__ DynEnt* dyn_ents(uint8_t* d) { return (DynEnt*)(d + sizeof(DynHdr)); }
+__device__ __forceinline__ uint8_t* dyn_alloc(uint8_t* d, uint32_t n) {
+  DynHdr* H = (DynHdr*)d;
+  if (H->nb + n > H->capb) return nullptr;
+  uint8_t* p = d + sizeof(DynHdr) + 32ull * H->cap + H->nb;
+  H->nb += n;
+  return p;
+}
+
+// The slot of a macro-key setvar: the key is expanded and lowercased
+// [upstream setvar.go: strings.ToLower of the expanded key; ASCII here, like
+// the compiler's static TX names]; a key that names a static slot is that
+// slot, otherwise the dynamic entry with that key (created unless delete).
+__device__ __noinline__ Slot* dyn_slot(Tx& t, const DAction& a, bool create) {
+  const DProgram& P = *t.P;
+  bool pers;
+  const Str k = expand(t, a.aux, &pers);
+  if (t.flags & GI_REQ_OVERFLOW) return nullptr;
+  uint8_t* kp = (uint8_t*)k.p;  // the macro scratch (a key with a macro is never a persistent literal)
+  for (uint32_t i = 0; i < k.n; i++) kp[i] = alower(kp[i]);
+  const uint32_t h = gi_fnv1a(kp, k.n, false);
+  for (uint32_t i = h & P.slot_hash_mask;; i = (i + 1) & P.slot_hash_mask) {
+    const uint32_t e = P.slot_hash[i];
+    if (!e) break;
+    const uint32_t sid = e - 1;
+    if (eq_bytes(P.strpool + P.slot_names[2 * sid], P.slot_names[2 * sid + 1], kp, k.n)) return &TXS(t, sid);
+  }
+  DynHdr* H = (DynHdr*)t.dyn;
+  DynEnt* E = dyn_ents(t.dyn);
+  for (uint32_t j = 0; j < H->n; j++)
+    if (E[j].h == h && eq_bytes(E[j].k, E[j].kn, kp, k.n)) return &E[j].s;
+  if (!create) return nullptr;
+  uint8_t* kb = H->n < H->cap ? dyn_alloc(t.dyn, k.n) : nullptr;
+  if (!kb) {
+    t.flags |= GI_REQ_OVERFLOW;
+    return nullptr;
+  }
+  for (uint32_t i = 0; i < k.n; i++) kb[i] = kp[i];
+  DynEnt& ne = E[H->n++];
+  ne.k = kb;
+  ne.kn = k.n;
+  ne.h = h;
+  ne.s.num = 0;
+  ne.s.n = 0;
+  ne.s.state = 0;
+  return &ne.s;
+}
+
 // setvar [upstream internal/actions/setvar.go]
 __device__ __forceinline__ void run_setvar(Tx& t, const DAction& a) {
-  Slot& sl = TXS(t, a.slot);
+  Slot* slp = a.slot >= 0 ? &TXS(t, a.slot) : dyn_slot(t, a, a.kind == A_SETVAR);
+  if (!slp) return;
+  Slot& sl = *slp;
   if (a.kind == A_SETVAR_DEL) {
     sl.state = 0;
     return;
@@ -3243,13 +3308,22 @@ generic:
     sl.n = v.n;
     return;
   }
-  if (t.ntx + v.n > t.cap_tx) {
-    t.flags |= GI_REQ_OVERFLOW;
-    return;
+  uint8_t* dst;
+  if (a.slot < 0) {  // a run-time key: its value lives in the dynamic area the host sized for it
+    dst = dyn_alloc(t.dyn, v.n);
+    if (!dst) {
+      t.flags |= GI_REQ_OVERFLOW;
+      return;
+    }
+  } else {
+    if (t.ntx + v.n > t.cap_tx) {
+      t.flags |= GI_REQ_OVERFLOW;
+      return;
+    }
+    dst = t.txa + t.ntx;
+    t.ntx += v.n;
   }
-  uint8_t* dst = t.txa + t.ntx;
   for (uint32_t i = 0; i < v.n; i++) dst[i] = v.p[i];
-  t.ntx += v.n;
   sl.state = 2;
   sl.p = dst;
   sl.n = v.n;
@@ -3283,7 +3357,7 @@ __device__ __forceinline__ void run_actions(Tx& t, const DRule& R) {
         break;
       case A_CTL_RULE_REMOVE_TARGET:
         if (t.nrtgt < 8) {
-          t.rtgt[t.nrtgt] = {a.a, a.b, (uint32_t)a.slot, (uint32_t)a.tmpl, (uint32_t)a._pad2, 0u};
+          t.rtgt[t.nrtgt] = {a.a, a.b, (uint32_t)a.slot, (uint32_t)a.tmpl, (uint32_t)a.aux, 0u};
           t.nrtgt++;
         } else {
           t.flags |= GI_REQ_OVERFLOW;
@@ -3929,24 +4003,42 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
     }
     if (vr.var == V_TX) {
       uint32_t cnt = 0;
-      // a literal key names at most one slot: visit only that one
+      // static slots: a literal key names at most one; a regex key the ones the
+      // compiler listed (DProgram.txrx); no key all.  Then (no literal key) the
+      // keys macro-key setvars created, in creation order.
       uint32_t sb = 0, se = P.n_slots;
       if (vr.key_mode == 1) {
         sb = vr.slot < 0 ? 0u : (uint32_t)vr.slot;
         se = vr.slot < 0 ? 0u : (uint32_t)vr.slot + 1;
+      } else if (vr.key_mode == 2) {
+        sb = 0;
+        se = vr.key_len;
       }
-      for (uint32_t sid = sb; sid < se; sid++) {
-        if (TXS(t, sid).state == 0) continue;
-        const uint8_t* nm = P.strpool + P.slot_names[sid * 2];
-        uint32_t nn = P.slot_names[sid * 2 + 1];
-        if (vr.key_mode == 2 && !dfa_match(P, vr.key_dfa, nm, nn, false)) continue;
+      const uint32_t ndyn = (vr.key_mode != 1 && t.dyn) ? ((const DynHdr*)t.dyn)->n : 0u;
+      for (uint32_t si = sb; si < se + ndyn; si++) {
+        const uint8_t* nm;
+        uint32_t nn;
+        Slot sl;
+        if (si < se) {
+          const uint32_t sid = vr.key_mode == 2 ? P.txrx[vr.key_off + si] : si;
+          sl = TXS(t, sid);
+          if (sl.state == 0) continue;
+          nm = P.strpool + P.slot_names[sid * 2];
+          nn = P.slot_names[sid * 2 + 1];
+        } else {
+          const DynEnt& de = dyn_ents(t.dyn)[si - se];
+          sl = de.s;
+          if (sl.state == 0) continue;
+          nm = de.k;
+          nn = de.kn;
+          if (vr.key_mode == 2 && !dfa_match(P, vr.key_dfa, nm, nn, false)) continue;
+        }
         if (key_excluded(t, vr, nm, nn)) continue;
         if (t.nrtgt && R.id != 0 && target_removed(t, R.id, V_TX, nm, nn)) continue;
         if (vr.count) {
           cnt++;
           continue;
         }
-        const Slot sl = TXS(t, sid);
         if (sl.state == 1 && R.tchain_len == 0 && o.has_num && o.kind >= OP_EQ && o.kind <= OP_LT) {
           // integer TX value against a numeric literal: eval_op would Atoi the
           // canonical decimal back to sl.num, so compare directly
@@ -4220,6 +4312,7 @@ struct Region {
   uint32_t* capws;
   uint8_t* capbuf;
   MvState* mv;
+  uint8_t* dyn;  // dynamic TX area (DynHdr), nullptr when the program has no macro-key setvar
   uint32_t cap_f, cap_b, cap_t, cap_mt;
 };
 
@@ -4245,6 +4338,8 @@ __device__ inline Region region_of(const DProgram& P, const DBatch& B, uint32_t 
   off += (L.cap_mt + 15) & ~15u;
   g.txa = base + off;
   off += (L.cap_mt + 15) & ~15u;
+  g.dyn = P.n_dyn_sites ? base + off : nullptr;
+  off += P.n_dyn_sites ? 16ull + 32ull * L.dyn_cap + L.dyn_capb : 0ull;
   // observable captures: the submatch workspace and one value buffer per group
   g.capws = P.cap_ws_words ? (uint32_t*)(base + off) : nullptr;
   off += ((uint64_t)P.cap_ws_words * 4 + 15) & ~15ull;
@@ -4278,6 +4373,7 @@ __device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
   t.mv = g.mv;
   t.capws = g.capws;
   t.capbuf = g.capbuf;
+  t.dyn = g.dyn;
 }
 
 __device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
@@ -6333,6 +6429,10 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
   }
   t.mcap = B.mcap;
   for (uint32_t s = 0; s < P.n_slots; s++) TXS(t, s).state = 0;
+  if (t.dyn) {
+    const ReqLayout Lr = B.layout[r];
+    *(DynHdr*)t.dyn = DynHdr{0u, Lr.dyn_cap, 0u, Lr.dyn_capb};
+  }
   if (t.mv) {
     t.mv->n = t.mv->nb = 0;
     t.mv->cap_e = g.cap_f + 16;
@@ -6578,7 +6678,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_EVAL
       if (acc[c]) atomicAdd(&B.tally[c], acc[c]);
 }
 
-// Detail tally: histogram of the first exported TX value and
+// Detail tally: histogram of the exported inbound score (DProgram.hist_mask) and
 // the match count of every rule id, from the verdicts and matched-id rows k_eval
 // wrote.  Lanes walk their request's matched list in step; the lists share
 // long prefixes (the CRS initialisation SecActions match every request), so
@@ -6595,7 +6695,8 @@ __device__ __forceinline__ void wave_hist_add(uint32_t* hist, int32_t b) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_tally(DBatch B, const uint32_t* __restrict__ ids, uint32_t n_ids) {
+__global__ void __launch_bounds__(256) k_tally(DBatch B, const uint32_t* __restrict__ ids, uint32_t n_ids,
+                                               uint32_t hist_mask) {
   extern __shared__ uint32_t sh[];  // [n_ids] sorted ids | [GI_SCORE_BINS + n_ids] counts (LDS mode)
   const bool lds = n_ids <= GI_RHIST_LDS;
   const uint32_t* tid = lds ? sh : ids;
@@ -6616,7 +6717,10 @@ __global__ void __launch_bounds__(256) k_tally(DBatch B, const uint32_t* __restr
     if (r < B.n_req) {
       const gi_verdict v = B.verdicts[r];
       cnt = min(v.match_cnt, B.mcap);
-      sb = (int32_t)min(max(v.tx_export[0], (int64_t)0), (int64_t)(GI_SCORE_BINS - 1));
+      int64_t sc = 0;
+      for (uint32_t e = 0; e < GI_MAX_EXPORTS; e++)  // terms clamped to +-2^50: the sum cannot overflow
+        if ((hist_mask >> e) & 1u) sc += min(max(v.tx_export[e], -(1ll << 50)), 1ll << 50);
+      sb = (int32_t)min(max(sc, (int64_t)0), (int64_t)(GI_SCORE_BINS - 1));
     }
     wave_hist_add(hist, sb);
     const uint32_t steps = wave_max(cnt);
@@ -6737,7 +6841,7 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
   {
     const uint32_t lds = n_tally_ids <= GI_RHIST_LDS ? 4 * (2 * n_tally_ids + GI_SCORE_BINS) : 0;
     const uint32_t nb = std::min<uint32_t>((B.n_req + 255) / 256, 2048);
-    GI_LAUNCH("k_tally", k_tally, dim3(nb), dim3(256), lds, stream, B, tally_ids, n_tally_ids);
+    GI_LAUNCH("k_tally", k_tally, dim3(nb), dim3(256), lds, stream, B, tally_ids, n_tally_ids, P.hist_mask);
   }
 }
 

@@ -371,6 +371,23 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   UP(pikes, P.pikes, DPike)
   UP(pike_insts, P.pike_insts, DPikeInst)
   UP(pike_ranges, P.pike_ranges, uint32_t)
+  // static TX slot by (lowercase) name, for keys a macro-key setvar expands to
+  // at run time: open addressing on gi_fnv1a, entry = slot + 1 (0 empty)
+  std::vector<uint32_t> shash;
+  {
+    uint32_t cap = 16;
+    while (cap < 2 * P.n_slots) cap <<= 1;
+    shash.assign(cap, 0);
+    for (uint32_t sl = 0; sl < P.n_slots; sl++) {
+      const uint32_t h = gi_fnv1a(&P.strpool[P.slot_names[2 * sl]], P.slot_names[2 * sl + 1], false);
+      uint32_t i = h & (cap - 1);
+      while (shash[i]) i = (i + 1) & (cap - 1);
+      shash[i] = sl + 1;
+    }
+    np.slot_hash_mask = cap - 1;
+  }
+  UP(slot_hash, shash, uint32_t)
+  UP(txrx, P.txrx, uint32_t)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return discard(e == hipErrorOutOfMemory ? GI_ENOMEM : GI_ENODEV, "ruleset upload failed");
@@ -394,8 +411,19 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   np.top_begin[1] = n_ph1;
   np.top_end[1] = (uint32_t)top_ph.size();
   np.n_slots = P.n_slots;
+  np.n_dyn_sites = (uint32_t)P.dyn_sites.size();
   np.n_markers = P.n_markers;
   np.n_exports = (uint32_t)P.exports.size();
+  // score histogram (k_tally): the sum of the exported inbound_anomaly_score_pl1..pl4 -- what
+  // 949110 adds up, and, unlike the blocking score, set under a deny default (a phase-2
+  // attack rule interrupts before 949061 sums it) -- else the first export
+  np.hist_mask = 0;
+  for (uint32_t i = 0; i < np.n_exports && i < 8; i++) {
+    const std::string& nm = P.export_names[i];
+    if (nm.size() == 25 && nm.compare(0, 24, "inbound_anomaly_score_pl") == 0 && nm[24] >= '1' && nm[24] <= '4')
+      np.hist_mask |= 1u << i;
+  }
+  if (!np.hist_mask) np.hist_mask = 1;
   for (int i = 0; i < 8; i++) np.exports[i] = i < (int)P.exports.size() ? P.exports[i] : -1;
   np.rule_engine = P.rule_engine;
   np.body_access = P.body_access;
@@ -613,14 +641,17 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     if ((uint64_t)q.hdr_begin + q.hdr_count > in->n_headers) return "header range out of range";
     uint64_t maxv = std::max<uint64_t>({(uint64_t)q.uri.len * 3 + 2, (uint64_t)q.method.len + q.uri.len + q.proto.len + 2,
                                         (uint64_t)q.body.len, 64});
-    uint64_t cookie = 0, ncookie = 0, hdr_bytes = 0;
-    bool multipart = false;
+    uint64_t cookie = 0, ncookie = 0, hdr_bytes = 0, hname_bytes = 0;
+    bool multipart = false, hname_high = false;
     for (uint32_t h = 0; h < q.hdr_count; h++) {
       const gi_header& hd = in->headers[q.hdr_begin + h];
       if (hd.name.off + hd.name.len > in->data_len || hd.value.off + hd.value.len > in->data_len)
         return "header span out of range";
       maxv = std::max<uint64_t>(maxv, std::max(hd.name.len, hd.value.len));
       hdr_bytes += hd.name.len + hd.value.len;
+      hname_bytes += hd.name.len;
+      if (!PG.dyn_sites.empty())
+        for (uint32_t k = 0; k < hd.name.len && !hname_high; k++) hname_high = in->data[hd.name.off + k] >= 0x80;
       if (hd.name.len == 12 && strncasecmp((const char*)in->data + hd.name.off, "content-type", 12) == 0) {
         const char* hv = (const char*)in->data + hd.value.off;
         for (uint32_t k = 0; k + 9 <= hd.value.len && !multipart; k++)
@@ -718,12 +749,33 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       L.hset_mask = PG.streams.empty() ? 0u : (uint32_t)(cap - 1);
       sizes[r].hset = PG.streams.empty() ? 0 : (cap + 1 + 3) & ~3ull;
     }
+    // dynamic TX area (macro-key setvars): the executions each site can reach on
+    // this request and the bytes they can store (gi_program.h DDynSite)
+    uint64_t dyn_e = 0, dyn_b = 0;
+    for (const DDynSite& ds : PG.dyn_sites) {
+      const uint64_t raw_all = (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes + q.body.len;
+      uint64_t ex = ds.mm, src = 0;
+      if (!ds.no_targets) {
+        ex = (uint64_t)ds.mm * (ds.nsingles + (uint64_t)(ds.hdr_names + ds.hdr_vals) * q.hdr_count + (uint64_t)ds.other_coll * cap_f);
+        src = (uint64_t)ds.mm * (ds.nsingles * maxv + (uint64_t)ds.hdr_names * hname_bytes +
+                                 (uint64_t)ds.hdr_vals * (hdr_bytes - hname_bytes) + (uint64_t)ds.other_coll * (raw_all + cap_b));
+      }
+      const bool ascii_src = !ds.hdr_vals && !ds.other_coll && !ds.nsingles && !hname_high;
+      const uint64_t g = ascii_src ? ds.g_ascii : ds.g_any;
+      dyn_e += ex;
+      dyn_b += ex * (ds.lit + ds.fixed + 32ull * ds.n_mvname) + g * (ds.n_val + ds.n_mvname) * src +
+               ex * ds.n_big * std::max(cap_t, cap_mt);
+    }
+    if (dyn_e > 0xFFFFFFFFull || dyn_b > 0xFFFFFFFFull) return "request too large (dynamic TX keys)";
+    L.dyn_cap = PG.dyn_sites.empty() ? 0u : (uint32_t)dyn_e;
+    L.dyn_capb = PG.dyn_sites.empty() ? 0u : (uint32_t)((dyn_b + 15) & ~15ull);
     L.cap_f = (uint32_t)cap_f;
     L.cap_b = (uint32_t)cap_b;
     L.cap_t = (uint32_t)cap_t;
     L.cap_mt = (uint32_t)cap_mt;
     uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)nslots * GI_SLOT_BYTES + 15) / 16 * 16 + GI_RM_BYTES + (cap_b + 15) / 16 * 16 +
                   2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
+    if (!PG.dyn_sites.empty()) sz += 16 + 32ull * L.dyn_cap + L.dyn_capb;  // kernels.hip DynHdr + DynEnt[] + bytes
     // observable captures (kernels.hip region_of): workspace + one value buffer per group
     sz += (4ull * c->prog.cap_ws_words + 15) / 16 * 16 +
           (c->prog.cap_ws_words ? (uint64_t)c->prog.cap_groups * ((cap_t + 15) / 16 * 16) : 0);

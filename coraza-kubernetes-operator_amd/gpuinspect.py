@@ -202,6 +202,17 @@ def aggregate_configmaps(texts: Sequence[str]) -> str:
     return "\n".join(texts)
 
 
+def score_hist_value(tx_export_values, exports):
+    """The score gi_tally_detail_get's histogram bins for one request (k_tally):
+    the sum of the exported inbound_anomaly_score_pl1..pl4 (each clamped to
+    +-2^50), or the first export when none is exported; then clamped to
+    [0, 63]."""
+    idx = [i for i, e in enumerate(exports[:8]) if len(e) == 25 and e.startswith("inbound_anomaly_score_pl")
+           and e[24] in "1234"] or [0]
+    s = sum(min(max(int(tx_export_values[i]), -(1 << 50)), 1 << 50) for i in idx)
+    return min(max(s, 0), 63)
+
+
 DEFAULT_EXPORTS = (
     "blocking_inbound_anomaly_score", "inbound_anomaly_score_pl1", "inbound_anomaly_score_pl2",
     "inbound_anomaly_score_pl3", "inbound_anomaly_score_pl4", "detection_inbound_anomaly_score",

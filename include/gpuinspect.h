@@ -188,8 +188,11 @@ typedef struct {
 } gi_tally;
 
 /* Detail tallies of the last batch (what the multi-GPU tally
- * all-gathers besides gi_tally): a histogram of the first exported TX value
- * (default: blocking_inbound_anomaly_score) clamped to [0, GI_SCORE_BINS-1],
+ * all-gathers besides gi_tally): a histogram of the request's inbound anomaly
+ * score -- the sum of the exported inbound_anomaly_score_pl1..pl4 values (what
+ * CRS 949110 adds up; set even when a phase-2 attack rule interrupts before
+ * 949061 sums blocking_inbound_anomaly_score), or the first exported TX value
+ * when none of those is exported -- clamped to [0, GI_SCORE_BINS-1],
  * and per distinct rule id (ascending) the number of times it appears in the
  * matched-rule lists (MatchedRules) of the batch. */
 #define GI_SCORE_BINS 64

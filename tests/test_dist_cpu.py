@@ -202,11 +202,16 @@ def test_tally_fixture_matches_oracle():
             for rid in v.matched:
                 hits[rid] = hits.get(rid, 0) + 1
         assert {i: h for i, h in zip(row["rule_ids"], row["rule_hits"]) if h} == hits
+        import gpuinspect
         hist = [0] * 64
         for v in ov.values():
-            a, ok = coraza.go_atoi(v.tx.get(fx["exports"][0], b""))
-            hist[min(max(a if ok else 0, 0), 63)] += 1
+            vals = []
+            for e in fx["exports"]:
+                a, ok = coraza.go_atoi(v.tx.get(e, b""))
+                vals.append(a if ok else 0)
+            hist[gpuinspect.score_hist_value(vals, fx["exports"])] += 1
         assert row["score_hist"] == hist
+        assert sum(1 for x in hist if x) > 1  # the histogram carries information
 
 
 def _fixture_worker(rank, world, port, q):

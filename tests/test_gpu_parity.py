@@ -501,3 +501,52 @@ def test_gpu_chunked_batch_crs_pl1(engine_env):
     assert t["matched_total"] == sum(len(v.matched) for v in orc.values())
     assert t["n_interrupted"] == sum(1 for v in orc.values() if v.rule_id or v.status)
     assert any(ln["name"] == "k_collect" for ln in st["launches"])
+
+
+def _restricted_header_batch():
+    """Requests for the CRS v4 920450 / 920451 shape (capture + setvar with a
+    macro key + a chain over TX:/^header_name_9204xx_/ @within the restricted
+    list) and the 921170 / 921180 parameter counters (PL3)."""
+    names = ["Proxy", "Lock-Token", "Content-Range", "If", "Accept-Charset", "X-Http-Method-Override",
+             "content-encoding", "PROXY", "If-None-Match", "Proxy-Connection", "X-Custom", "iF", "Ifx"]
+    txs = []
+    for i, n in enumerate(names):
+        for extra in ([], [("Proxy", "b")], [(n, "again")], [("X-%d" % k, "v") for k in range(40)]):
+            t = gpuinspect.Transaction(method=b"GET", uri=b"/p?a=1&b=%d" % i)
+            t.add_request_header("Host", "example.com")
+            t.add_request_header("User-Agent", "Mozilla/5.0")
+            t.add_request_header(n, "value-%d" % i)
+            for k, v in extra:
+                t.add_request_header(k, v)
+            txs.append(t)
+    for uri in (b"/?a=1&a=2", b"/?a[]=1&a[]=2", b"/?a=1&b=2&A=3", b"/?x=1&x=2&x=3&y[]=1&y[]=2", b"/?q=evilmonkey"):
+        t = gpuinspect.Transaction(method=b"GET", uri=uri)
+        t.add_request_header("Host", "example.com")
+        t.add_request_header("Accept", "*/*")
+        txs.append(t)
+    t = gpuinspect.Transaction(method=b"POST", uri=b"/form?a=1")
+    t.add_request_header("Host", "example.com")
+    t.add_request_header("Content-Type", "application/x-www-form-urlencoded")
+    t.write_request_body(b"a=2&b=3&b=4&c[]=1&c[]=2")
+    txs.append(t)
+    t = gpuinspect.Transaction(method=b"GET", uri=b"/")
+    t.add_request_header("Host", "example.com")
+    t.add_request_header("Pr\xc3\xb6xy", "non-ascii name")
+    t.add_request_header("If", "x")
+    txs.append(t)
+    return gpuinspect.pack(txs)
+
+
+@pytest.mark.parametrize("ruleset", ["crs_pl1", "crs_pl4"])
+def test_gpu_macro_key_setvar_chains(ruleset):
+    """setvar:'tx.header_name_920450_%{tx.0}=/%{tx.0}/' creates TX keys at run
+    time; the chained TX:/^header_name_920450_/ reads them."""
+    text = open(os.path.join(ROOT, "rulesets", ruleset + ".conf")).read()
+    batch = _restricted_header_batch()
+    res = _parity(text, batch)
+    m = [res.matched_rules(i) for i in range(batch.n_req)]
+    assert sum(920450 in x for x in m) >= 20      # Proxy, Lock-Token, Content-Range, If, ...
+    assert sum(920450 not in x for x in m) >= 8   # Accept-Charset, X-Custom, If-None-Match, ...
+    if ruleset == "crs_pl4":
+        assert sum(920451 in x for x in m) >= 4   # Accept-Charset (PL2 extended list)
+        assert sum(921180 in x for x in m) >= 2   # repeated parameter names (PL3)
