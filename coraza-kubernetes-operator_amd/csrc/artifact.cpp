@@ -28,7 +28,8 @@ const char kMagic[8] = {'G', 'I', 'A', 'R', 'T', 'F', 'C', 'T'};
 struct Scalars {
   uint8_t item_sides[8];
   uint32_t item_singles, n_hit_slots, n_union_dfas, max_img_bytes, max_big_img_bytes, n_slots, n_markers;
-  uint8_t rule_engine, body_access, mv_used, body_partial, _pad[4];
+  uint8_t rule_engine, body_access, mv_used, body_partial, fold_on, _pad[3];
+  uint32_t fold_nids, _pad4;
   uint64_t body_limit, source_digest;
   uint64_t compiler_rev;  // fnv64 of kCompilerRev
 };
@@ -41,7 +42,7 @@ uint64_t compiler_rev_hash() { return fnv64((const uint8_t*)kCompilerRev, strlen
   X(10, dfas) X(11, trans) X(12, u8pool) X(13, nranges) X(14, strpool) X(15, slot_names) X(16, u64pool)     \
   X(17, streams) X(18, filters) X(19, sfilt) X(20, body_links) X(21, always_slots) X(22, jobs) X(23, jdfas) \
   X(24, pats) X(25, svals) X(26, images) X(27, exports) X(28, nfas) X(29, pikes) X(30, pike_insts)              \
-  X(31, pike_ranges) X(32, dyn_sites) X(33, txrx)
+  X(31, pike_ranges) X(32, dyn_sites) X(33, txrx) X(34, tx_snap) X(35, fold_ids) X(36, fold_runs)
 
 constexpr uint32_t kTagScalars = 100, kTagPlan = 101, kTagExportNames = 102;
 
@@ -49,7 +50,7 @@ uint64_t layout_signature() {
   const uint64_t sz[] = {sizeof(DRule), sizeof(DVarRef), sizeof(DExc), sizeof(DOp), sizeof(DAction),
                          sizeof(DTmplPart), sizeof(DTmpl), sizeof(DDfa), sizeof(DStream), sizeof(DFilter),
                          sizeof(DJob), sizeof(DJobDfa), sizeof(DPat), sizeof(DScanVal), sizeof(Scalars),
-                         sizeof(DNfa), sizeof(DPike), sizeof(DPikeInst), sizeof(DDynSite)};
+                         sizeof(DNfa), sizeof(DPike), sizeof(DPikeInst), sizeof(DDynSite), sizeof(DSnapSlot)};
   return fnv64((const uint8_t*)sz, sizeof(sz));
 }
 
@@ -94,6 +95,8 @@ std::vector<uint8_t> serialize_program(const Program& P) {
   s.body_access = P.body_access;
   s.mv_used = P.mv_used;
   s.body_partial = P.body_partial;
+  s.fold_on = P.fold_on;
+  s.fold_nids = P.fold_nids;
   s.body_limit = P.body_limit;
   s.source_digest = P.source_digest;
   s.compiler_rev = compiler_rev_hash();
@@ -178,6 +181,8 @@ bool deserialize_program(const uint8_t* buf, size_t n, Program* P, std::string* 
         out.body_access = s.body_access;
         out.mv_used = s.mv_used;
         out.body_partial = s.body_partial;
+        out.fold_on = s.fold_on;
+        out.fold_nids = s.fold_nids;
         out.body_limit = s.body_limit;
         out.source_digest = s.source_digest;
         seen_scalars = true;
@@ -293,6 +298,21 @@ bool validate_program(const Program& P, std::string* err) {
         (r.op < 0 || P.ops[r.op].kind != OP_RX || P.ops[r.op].pike < 0))
       return bad("capture flag without a capture program");
   }
+  // folded prefix (compile.cpp fold_program): snapshot per slot, ids, resume point
+  if (P.tx_snap.size() != nslot) return bad("TX snapshot size");
+  for (const DSnapSlot& z : P.tx_snap)
+    if (z.state > 2 || (z.state == 2 && !in(z.off, z.len, nstr))) return bad("TX snapshot value");
+  if (P.fold_nids > P.fold_ids.size()) return bad("folded ids");
+  if (P.fold_runs.size() % 4) return bad("folded runs");
+  for (size_t q = 0; q + 3 < P.fold_runs.size(); q += 4)
+    if ((uint64_t)P.fold_runs[q] + P.fold_runs[q + 1] > P.fold_nids ||
+        (P.fold_runs[q + 3] != 0xFFFFFFFFu && P.fold_runs[q + 3] >= P.n_markers))
+      return bad("folded run");
+  for (const DRule& r : P.rules)
+    if ((r.flags & RF_FOLDED) && (4ull * r._pad2 + 3 >= P.fold_runs.size() || (r.flags & RF_CHILD)))
+      return bad("folded rule");
+  for (const DRule& r : P.rules)
+    if ((r.flags & RF_CONST) && r.op >= 0 && r.var_count == 0) return bad("constant link without targets");
   for (uint32_t t : P.body_links)
     if (t >= nrules || P.rules[t].op < 0 || P.rules[t].hit_slot < 0) return bad("body link");
   for (const DVarRef& v : P.vars) {

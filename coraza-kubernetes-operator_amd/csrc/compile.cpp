@@ -2159,6 +2159,550 @@ static void capture_analysis(const IrWaf& waf, const std::vector<std::string>& e
   }
 }
 
+// ------------------------------------------------ constant folding
+// CRS starts phase 1 with rules that read nothing but TX variables earlier
+// rules set to constants (the 901 initialisation: `SecRule &TX:x "@eq 0"
+// "setvar:tx.x=<default>"`), and gates every paranoia level on
+// TX:DETECTION_PARANOIA_LEVEL.  Their outcomes are the same for every request,
+// so the compiler evaluates them here, with the interpreter's semantics
+// (kernels.hip eval_top / eval_rule / run_setvar / eval_op), instead of every
+// k_eval lane re-evaluating them:
+//   * prefix: the phase-1 walk from its start while every rule it reaches is
+//     request-independent.  The TX state after it (tx_snap), the ids it
+//     matched (fold_ids) and the walk index where evaluation resumes
+//     (fold_walk) replace that stretch of the walk; k_eval reads TX slots from
+//     the snapshot until the request writes them (copy on write).
+//   * frozen slots: TX slots no rule outside the prefix can write (no setvar
+//     names them, no capture group, no macro-key setvar whose literal key
+//     prefix they start with).  A later request-independent link that reads
+//     only frozen slots matches a fixed number of values (RF_CONST +
+//     DRule._pad2); an operator argument that reads only frozen slots becomes
+//     a literal.
+// A link is request-independent when its targets are literal-key TX
+// variables (or &count), it has no transformation, capture or ctl, its
+// operator is a comparison / string test over literals and TX macros, and its
+// actions are setvars over literals and TX macros.  Anything else stops the
+// prefix (a ruleset that reads MATCHED_VAR / MATCHED_VAR_NAME, which the
+// prefix's matches would set, gets no prefix).
+namespace {
+struct HSlot {
+  uint32_t state = 0;  // 0 unset, 1 integer, 2 string
+  int64_t num = 0;
+  std::string s;
+};
+
+struct Folder {
+  Program& P;
+  std::vector<HSlot> tx;
+  std::vector<bool> frozen;
+  bool mv_single = false;   // MATCHED_VAR / MATCHED_VAR_NAME is read somewhere
+  std::vector<std::pair<int64_t, int64_t>> rtgt_tx;  // ctl:ruleRemoveTargetById ranges naming TX
+
+  explicit Folder(Program& p) : P(p), tx(p.n_slots), frozen(p.n_slots, false) {
+    // MATCHED_VAR / MATCHED_VAR_NAME as an earlier rule left them are read by
+    // those targets, by operator-argument macros (expanded before the link's
+    // own matches) and by the actions of a link without targets; an action
+    // macro of a link with targets reads the link's own match
+    auto mv_parts = [&](int32_t tid) {
+      if (tid < 0) return false;
+      const DTmpl& tm = P.tmpls[tid];
+      for (uint32_t k = 0; k < tm.part_count; k++) {
+        const uint8_t kd = P.tparts[tm.part_begin + k].kind;
+        if (kd == TP_MV || kd == TP_MVNAME) return true;
+      }
+      return false;
+    };
+    for (const DVarRef& v : P.vars)
+      if (v.var == V_MATCHED_VAR || v.var == V_MATCHED_VAR_NAME) mv_single = true;
+    for (const DRule& d : P.rules) {
+      if (d.op >= 0 && mv_parts(P.ops[d.op].tmpl)) mv_single = true;
+      if (d.var_count == 0)
+        for (uint32_t k = 0; k < d.act_count; k++) {
+          const DAction& a = P.acts[d.act_begin + k];
+          if ((a.kind == A_SETVAR || a.kind == A_SETVAR_DEL) && (mv_parts(a.tmpl) || (a.slot < 0 && mv_parts(a.aux))))
+            mv_single = true;
+        }
+    }
+    for (const DAction& a : P.acts)
+      if (a.kind == A_CTL_RULE_REMOVE_TARGET && a.slot == V_TX) rtgt_tx.emplace_back(a.a, a.b);
+  }
+  static int64_t atoi0(const std::string& x) {
+    int64_t v = 0;
+    return go_atoi(x, &v) ? v : 0;
+  }
+  std::string slot_str(uint32_t sl) const {
+    const HSlot& h = tx[sl];
+    return h.state == 1 ? std::to_string(h.num) : h.state == 2 ? h.s : std::string();
+  }
+  bool slot_int(uint32_t sl, int64_t* v) const {
+    const HSlot& h = tx[sl];
+    if (h.state == 1) {
+      *v = h.num;
+      return true;
+    }
+    if (h.state == 2) return go_atoi(h.s, v);
+    return false;
+  }
+  // template parts: literals and TX slots only (all frozen when `need_frozen`)
+  bool tmpl_const(int tid, bool need_frozen) const {
+    if (tid < 0) return true;
+    const DTmpl& tm = P.tmpls[tid];
+    for (uint32_t k = 0; k < tm.part_count; k++) {
+      const DTmplPart& tp = P.tparts[tm.part_begin + k];
+      if (tp.kind == TP_LIT) continue;
+      if (tp.kind != TP_TX || tp.slot < 0) return false;
+      if (need_frozen && !frozen[tp.slot]) return false;
+    }
+    return true;
+  }
+  std::string expand(int tid) const {
+    std::string o;
+    if (tid < 0) return o;
+    const DTmpl& tm = P.tmpls[tid];
+    for (uint32_t k = 0; k < tm.part_count; k++) {
+      const DTmplPart& tp = P.tparts[tm.part_begin + k];
+      if (tp.kind == TP_LIT) o.append((const char*)&P.strpool[tp.off], tp.len);
+      else o += slot_str((uint32_t)tp.slot);
+    }
+    return o;
+  }
+  bool op_const(const DOp& o) const {
+    switch (o.kind) {
+      case OP_EQ: case OP_GE: case OP_GT: case OP_LE: case OP_LT: case OP_STREQ: case OP_WITHIN:
+      case OP_BEGINSWITH: case OP_ENDSWITH: case OP_UNCONDITIONAL: case OP_NOMATCH:
+        break;
+      case OP_CONTAINS:
+        if (o.dfa >= 0) return false;  // literal phrase automaton: not restated here
+        break;
+      default:
+        return false;
+    }
+    return o.arg_is_lit || o.has_num || tmpl_const(o.tmpl, false);
+  }
+  // kernels.hip eval_op over a TX value
+  bool eval_op(const DOp& o, const std::string& v) const {
+    bool res = false;
+    switch (o.kind) {
+      case OP_UNCONDITIONAL: res = true; break;
+      case OP_NOMATCH: res = false; break;
+      case OP_EQ: case OP_GE: case OP_GT: case OP_LE: case OP_LT: {
+        const int64_t a = o.has_num ? o.num : atoi0(expand(o.tmpl));
+        const int64_t b = atoi0(v);
+        res = o.kind == OP_EQ ? b == a : o.kind == OP_GE ? b >= a : o.kind == OP_GT ? b > a : o.kind == OP_LE ? b <= a : b < a;
+        break;
+      }
+      default: {
+        const std::string a = o.arg_is_lit ? std::string((const char*)&P.strpool[o.lit_off], o.lit_len) : expand(o.tmpl);
+        switch (o.kind) {
+          case OP_CONTAINS: res = v.find(a) != std::string::npos; break;
+          case OP_STREQ: res = v == a; break;
+          case OP_BEGINSWITH: res = v.size() >= a.size() && v.compare(0, a.size(), a) == 0; break;
+          case OP_ENDSWITH: res = v.size() >= a.size() && v.compare(v.size() - a.size(), a.size(), a) == 0; break;
+          case OP_WITHIN: res = a.find(v) != std::string::npos; break;
+          default: break;
+        }
+      }
+    }
+    return o.negate ? !res : res;
+  }
+  // kernels.hip run_setvar
+  void setvar(const DAction& a) {
+    HSlot& sl = tx[(uint32_t)a.slot];
+    if (a.kind == A_SETVAR_DEL) {
+      sl.state = 0;
+      return;
+    }
+    if (a.a == SV_SET_INT) {
+      sl.state = 1;
+      sl.num = a.b;
+      return;
+    }
+    if (a.a != SV_GENERIC) {
+      int64_t vv = a.b;
+      bool generic = false;
+      if (a.a == SV_ADD_SLOT || a.a == SV_SUB_SLOT) {
+        const HSlot& src = tx[(uint32_t)a.b];
+        if (src.state == 0) return;
+        if (src.state != 1) generic = true;
+        vv = src.num;
+      }
+      if (!generic) {
+        int64_t me;
+        if (!slot_int((uint32_t)a.slot, &me)) me = 0;
+        const bool add = a.a == SV_ADD_CONST || a.a == SV_ADD_SLOT;
+        sl.state = 1;
+        sl.num = (int64_t)(add ? (uint64_t)me + (uint64_t)vv : (uint64_t)me - (uint64_t)vv);
+        return;
+      }
+    }
+    const std::string v = expand(a.tmpl);
+    if (v.empty()) {
+      sl.state = 2;
+      sl.s.clear();
+      return;
+    }
+    if (v[0] == '+' || v[0] == '-') {
+      int64_t me;
+      if (!slot_int((uint32_t)a.slot, &me)) me = 0;
+      int64_t vv;
+      if (!go_atoi(v.substr(1), &vv)) return;
+      sl.state = 1;
+      sl.num = (int64_t)(v[0] == '+' ? (uint64_t)me + (uint64_t)vv : (uint64_t)me - (uint64_t)vv);
+      return;
+    }
+    int64_t num;
+    if (go_atoi(v, &num) && std::to_string(num) == v) {
+      sl.state = 1;
+      sl.num = num;
+      return;
+    }
+    sl.state = 2;
+    sl.s = v;
+  }
+  bool tmpl_mv(int32_t tid) const {
+    if (tid < 0) return false;
+    const DTmpl& tm = P.tmpls[tid];
+    for (uint32_t k = 0; k < tm.part_count; k++) {
+      const uint8_t kd = P.tparts[tm.part_begin + k].kind;
+      if (kd == TP_MV || kd == TP_MVNAME) return true;
+    }
+    return false;
+  }
+  // link ri's own actions or a later link of its chain read the matched-variable state
+  bool chain_reads_mv(uint32_t ri) const {
+    for (int32_t ci = (int32_t)ri; ci >= 0; ci = P.rules[ci].chain_next) {
+      const DRule& d = P.rules[ci];
+      for (uint32_t k = 0; k < d.act_count; k++) {
+        const DAction& a = P.acts[d.act_begin + k];
+        if ((a.kind == A_SETVAR || a.kind == A_SETVAR_DEL) && (tmpl_mv(a.tmpl) || (a.slot < 0 && tmpl_mv(a.aux))))
+          return true;
+      }
+      if ((uint32_t)ci == ri) continue;
+      if (d.op >= 0 && tmpl_mv(P.ops[d.op].tmpl)) return true;
+      for (uint32_t k = 0; k < d.var_count; k++)
+        if (P.vars[d.var_begin + k].var >= V_MATCHED_VAR) return true;
+    }
+    return false;
+  }
+  // request-independent link (need_frozen: every TX slot it reads is frozen)
+  bool link_ri(const DRule& d, bool need_frozen) const {
+    if (d.flags & (RF_CAPTURE | RF_MARKER)) return false;
+    if (d.tchain_len != 0) return false;
+    if (d.op < 0 && d.var_count != 0) return false;
+    if (d.op >= 0 && (d.var_count == 0 || !op_const(P.ops[d.op]))) return false;
+    if (d.op >= 0 && need_frozen && !P.ops[d.op].arg_is_lit && !P.ops[d.op].has_num &&
+        !tmpl_const(P.ops[d.op].tmpl, true))
+      return false;
+    for (uint32_t k = 0; k < d.var_count; k++) {
+      const DVarRef& v = P.vars[d.var_begin + k];
+      if (v.var != V_TX || v.key_mode != 1 || v.exc_count || v.slot < 0) return false;
+      if (need_frozen && !frozen[v.slot]) return false;
+    }
+    for (const auto& rg : rtgt_tx)
+      if (d.id != 0 && rg.first <= d.id && d.id <= rg.second) return false;
+    for (uint32_t k = 0; k < d.act_count; k++) {
+      const DAction& a = P.acts[d.act_begin + k];
+      if (a.kind != A_SETVAR && a.kind != A_SETVAR_DEL) return false;
+      if (a.slot < 0 || !tmpl_const(a.tmpl, false)) return false;
+    }
+    return true;
+  }
+  // kernels.hip eval_rule on a request-independent link: the number of values
+  // it matches; apply: run the actions per match
+  uint32_t eval_link(const DRule& d, bool apply) {
+    if (d.op < 0) {
+      if (apply)
+        for (uint32_t k = 0; k < d.act_count; k++) setvar(P.acts[d.act_begin + k]);
+      return 1;
+    }
+    const DOp& o = P.ops[d.op];
+    uint32_t nm = 0;
+    for (uint32_t k = 0; k < d.var_count; k++) {
+      const DVarRef& v = P.vars[d.var_begin + k];
+      std::string val;
+      if (v.count) {
+        val = tx[v.slot].state != 0 ? "1" : "0";
+      } else {
+        if (tx[v.slot].state == 0) continue;
+        val = slot_str((uint32_t)v.slot);
+      }
+      if (eval_op(o, val)) {
+        nm++;
+        if (apply)
+          for (uint32_t q = 0; q < d.act_count; q++) setvar(P.acts[d.act_begin + q]);
+      }
+    }
+    return nm;
+  }
+};
+}  // namespace
+
+static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
+  (void)exports;
+  Program& P = *Pp;
+  Folder F(P);
+  // the phase-1 walk (runtime.cpp load_program builds the same list)
+  std::vector<uint32_t> walk;
+  for (uint32_t ri : P.top)
+    if (P.rules[ri].phase == 0 || P.rules[ri].phase == 1) walk.push_back(ri);
+  std::vector<bool> in_prefix(P.rules.size(), false);  // links of folded rules
+  const uint32_t ns = P.n_slots;
+  // the static TX slots a rule chain reads / writes
+  std::vector<int32_t> dyn_site_of(P.acts.size(), -1);
+  {
+    int32_t di = 0;
+    for (size_t q = 0; q < P.acts.size(); q++)
+      if ((P.acts[q].kind == A_SETVAR || P.acts[q].kind == A_SETVAR_DEL) && P.acts[q].slot < 0) dyn_site_of[q] = di++;
+  }
+  auto slot_name = [&](uint32_t sl) {
+    return std::string((const char*)&P.strpool[P.slot_names[2 * sl]], P.slot_names[2 * sl + 1]);
+  };
+  auto touch = [&](uint32_t top, std::vector<bool>& rd, std::vector<bool>& wr) {
+    auto tmpl_reads = [&](int32_t tid) {
+      if (tid < 0) return;
+      const DTmpl& tm = P.tmpls[tid];
+      for (uint32_t q = 0; q < tm.part_count; q++) {
+        const DTmplPart& tp = P.tparts[tm.part_begin + q];
+        if (tp.kind == TP_TX && tp.slot >= 0) rd[tp.slot] = true;
+      }
+    };
+    for (int32_t ci = (int32_t)top; ci >= 0; ci = P.rules[ci].chain_next) {
+      const DRule& d = P.rules[ci];
+      for (uint32_t q = 0; q < d.var_count; q++) {
+        const DVarRef& v = P.vars[d.var_begin + q];
+        if (v.var != V_TX) continue;
+        if (v.key_mode == 1 && v.slot >= 0) rd[v.slot] = true;
+        else if (v.key_mode == 2)
+          for (uint32_t j = 0; j < v.key_len; j++) rd[P.txrx[v.key_off + j]] = true;
+        else if (v.key_mode == 0)
+          for (uint32_t sl = 0; sl < ns; sl++) rd[sl] = true;
+      }
+      if (d.op >= 0) tmpl_reads(P.ops[d.op].tmpl);
+      if (d.flags & RF_CAPTURE)
+        for (uint32_t sl = 0; sl < ns; sl++) {
+          const std::string nm = slot_name(sl);
+          if (nm.size() == 1 && nm[0] >= '0' && nm[0] <= '9') wr[sl] = true;
+        }
+      for (uint32_t q = 0; q < d.act_count; q++) {
+        const uint32_t ai = d.act_begin + q;
+        const DAction& a = P.acts[ai];
+        if (a.kind != A_SETVAR && a.kind != A_SETVAR_DEL) continue;
+        tmpl_reads(a.tmpl);
+        if ((a.a == SV_ADD_SLOT || a.a == SV_SUB_SLOT) && a.b >= 0) rd[a.b] = true;
+        if (a.slot >= 0) {
+          wr[a.slot] = true;
+          rd[a.slot] = true;  // += reads it
+        } else {
+          tmpl_reads(a.aux);
+          const DDynSite& ds = P.dyn_sites[dyn_site_of[ai]];
+          const std::string pre((const char*)&P.strpool[ds.prefix_off], ds.prefix_len);
+          for (uint32_t sl = 0; sl < ns; sl++)
+            if (slot_name(sl).compare(0, pre.size(), pre) == 0) wr[sl] = rd[sl] = true;
+        }
+      }
+    }
+  };
+  // a rule evaluated at run time that could keep a later folded rule from
+  // running (or change its order): a skip, an interruption, ctl on the engine
+  // or on rules
+  auto barrier = [&](uint32_t top) {
+    const DRule& R = P.rules[top];
+    if (P.rule_engine == ENGINE_ON && (R.disruptive == D_DENY || R.disruptive == D_DROP || R.disruptive == D_REDIRECT))
+      return true;
+    for (int32_t ci = (int32_t)top; ci >= 0; ci = P.rules[ci].chain_next) {
+      const DRule& d = P.rules[ci];
+      for (uint32_t q = 0; q < d.act_count; q++) {
+        const uint8_t kd = P.acts[d.act_begin + q].kind;
+        if (kd == A_CTL_RULE_ENGINE || kd == A_CTL_RULE_REMOVE_ID || kd == A_CTL_RULE_REMOVE_TARGET) return true;
+      }
+    }
+    return false;
+  };
+  // Fold every request-independent phase-1 rule that is reached by every
+  // request and whose TX inputs / outputs no earlier run-time rule touches:
+  // its effects are the snapshot (applied when phase 1 starts: a run-time rule
+  // before it neither reads what it writes nor writes what it reads, so the
+  // order does not matter), and its matched id is emitted where the walk
+  // reaches it.  Consecutive folded rules (and the rules their skipAfter
+  // jumps over) form a run: k_eval emits the run's ids and jumps past it.
+  std::vector<bool> dep_r(ns, false), dep_w(ns, false);
+  std::vector<bool> maybe_skipped(walk.size(), false);  // a run-time rule's skip / skipAfter may jump over it
+  if (P.rule_engine != ENGINE_OFF) {
+    int32_t skip_after = -1;
+    int32_t skip = 0;
+    int32_t run = -1;
+    auto close_run = [&](uint32_t at) {
+      if (run < 0) return;
+      P.fold_runs[4 * run + 1] = (uint32_t)P.fold_ids.size() - P.fold_runs[4 * run];
+      P.fold_runs[4 * run + 2] = at;
+      P.fold_runs[4 * run + 3] = (uint32_t)skip_after;  // pending at the walk's end (else -1)
+      run = -1;
+    };
+    uint32_t k = 0;
+    for (; k < walk.size(); k++) {
+      const uint32_t ri = walk[k];
+      const DRule& R = P.rules[ri];
+      if (skip_after >= 0) {  // inside a run: skipped for every request
+        if (R.marker == skip_after) skip_after = -1;
+        continue;
+      }
+      if (skip > 0) {
+        skip--;
+        continue;
+      }
+      if (R.flags & RF_MARKER) continue;
+      bool ri_ok = !maybe_skipped[k];
+      for (int32_t ci = (int32_t)ri; ri_ok && ci >= 0; ci = P.rules[ci].chain_next) {
+        const DRule& C = P.rules[ci];
+        ri_ok = F.link_ri(C, false) && !(F.mv_single && C.var_count);
+      }
+      if (ri_ok) {
+        std::vector<bool> rd(ns, false), wr(ns, false);
+        touch(ri, rd, wr);
+        bool conflict = false;
+        for (uint32_t sl = 0; sl < ns && !conflict; sl++)
+          conflict = (rd[sl] && dep_w[sl]) || (wr[sl] && (dep_r[sl] || dep_w[sl]));
+        if (!conflict) {
+          const std::vector<HSlot> before = F.tx;
+          bool matched = true;
+          for (int32_t ci = (int32_t)ri; ci >= 0; ci = P.rules[ci].chain_next)
+            if (F.eval_link(P.rules[ci], true) == 0) {
+              matched = false;
+              break;
+            }
+          const bool interrupts = matched && P.rule_engine == ENGINE_ON &&
+                                  (R.disruptive == D_DENY || R.disruptive == D_DROP || R.disruptive == D_REDIRECT);
+          if (!interrupts) {
+            for (int32_t ci = (int32_t)ri; ci >= 0; ci = P.rules[ci].chain_next) in_prefix[ci] = true;
+            if (run < 0) {
+              run = (int32_t)(P.fold_runs.size() / 4);
+              P.fold_runs.insert(P.fold_runs.end(), {(uint32_t)P.fold_ids.size(), 0u, 0u, 0xFFFFFFFFu});
+              P.rules[ri].flags |= RF_FOLDED;
+              P.rules[ri]._pad2 = (uint32_t)run;
+            }
+            if (matched) {
+              if (R.skip_after >= 0) skip_after = R.skip_after;
+              if (R.skip) skip = R.skip;
+              if (R.id != 0) P.fold_ids.push_back((uint32_t)R.id);
+            }
+            continue;
+          }
+          F.tx = before;
+        }
+      }
+      // evaluated at run time
+      if (getenv("GI_FOLD_DEBUG"))
+        fprintf(stderr, "fold: run-time rule %d at walk %u (ri_ok %d, barrier %d)\n", R.id, k, (int)ri_ok, (int)barrier(ri));
+      close_run(k);
+      if (barrier(ri)) break;
+      touch(ri, dep_r, dep_w);
+      // the entries its skip / skipAfter can jump over are not reached by every
+      // request: they stay run-time rules (the walk continues after them)
+      if (R.skip_after >= 0) {
+        uint32_t m = k + 1;
+        while (m < walk.size() && P.rules[walk[m]].marker != R.skip_after) m++;
+        for (uint32_t j = k + 1; j < m && j < walk.size(); j++) maybe_skipped[j] = true;
+      }
+      for (uint32_t j = k + 1; j <= k + (uint32_t)std::max(R.skip, 0) && j < walk.size(); j++) maybe_skipped[j] = true;
+    }
+    close_run(k);
+  }
+  P.fold_on = P.fold_runs.empty() ? 0 : 1;
+  if (!P.fold_on) {
+    P.fold_ids.clear();
+    for (auto& h : F.tx) h = HSlot();
+  }
+  // frozen slots: nothing outside the prefix writes them
+  std::vector<bool> written(P.n_slots, false);
+  for (uint32_t ri = 0; ri < P.rules.size(); ri++) {
+    if (in_prefix[ri] && P.fold_on) continue;
+    const DRule& d = P.rules[ri];
+    for (uint32_t q = 0; q < d.act_count; q++) {
+      const DAction& a = P.acts[d.act_begin + q];
+      if ((a.kind == A_SETVAR || a.kind == A_SETVAR_DEL) && a.slot >= 0) written[a.slot] = true;
+    }
+  }
+  for (uint32_t sl = 0; sl < P.n_slots; sl++) {
+    const std::string nm((const char*)&P.strpool[P.slot_names[2 * sl]], P.slot_names[2 * sl + 1]);
+    bool w = written[sl];
+    if (!P.pikes.empty() && nm.size() == 1 && nm[0] >= '0' && nm[0] <= '9') w = true;  // capture groups
+    for (const DDynSite& ds : P.dyn_sites) {
+      const std::string pre((const char*)&P.strpool[ds.prefix_off], ds.prefix_len);
+      if (nm.compare(0, pre.size(), pre) == 0) w = true;  // a run-time key could name it
+    }
+    F.frozen[sl] = !w;
+  }
+  // links outside the prefix: constant outcomes, constant operator arguments
+  uint32_t n_args = 0;
+  if (P.rule_engine != ENGINE_OFF) {
+    for (uint32_t ri = 0; ri < P.rules.size(); ri++) {
+      if (in_prefix[ri] && P.fold_on) continue;
+      DRule& d = P.rules[ri];
+      if (d.op >= 0) {
+        DOp& o = P.ops[d.op];
+        if (!o.arg_is_lit && o.tmpl >= 0 && F.tmpl_const(o.tmpl, true)) {
+          const std::string lit = F.expand(o.tmpl);
+          o.arg_is_lit = 1;
+          o.lit_off = (uint32_t)P.strpool.size();
+          o.lit_len = (uint32_t)lit.size();
+          P.strpool.insert(P.strpool.end(), lit.begin(), lit.end());
+          P.strpool.push_back(0);
+          int64_t v = 0;
+          if (!go_atoi(lit, &v)) v = 0;
+          o.has_num = 1;
+          o.num = v;
+          n_args++;
+        }
+      }
+      if (!F.link_ri(d, true)) continue;
+      // the TX values it reads are the snapshot's for every request that reaches it
+      const uint32_t nm = F.eval_link(d, false);
+      // its matches would set the matched-variable state: fine unless a stale
+      // reader exists (mv_single), or its own actions / later chain links read it
+      if (nm > 0 && P.mv_used && (F.mv_single || F.chain_reads_mv(ri))) continue;
+      d.flags |= RF_CONST;
+      d._pad2 = nm;
+    }
+  }
+  P.tx_snap.resize(P.n_slots);
+  for (uint32_t sl = 0; sl < P.n_slots; sl++) {
+    DSnapSlot z{};
+    const HSlot& h = F.tx[sl];
+    z.state = h.state;
+    z.num = h.num;
+    if (h.state == 2) {
+      z.off = (uint32_t)P.strpool.size();
+      z.len = (uint32_t)h.s.size();
+      P.strpool.insert(P.strpool.end(), h.s.begin(), h.s.end());
+      P.strpool.push_back(0);
+    }
+    P.tx_snap[sl] = z;
+  }
+  P.fold_nids = (uint32_t)P.fold_ids.size();
+  {  // the plan JSON reports what was folded
+    uint32_t nconst = 0, nconst0 = 0;
+    for (const DRule& d : P.rules)
+      if (d.flags & RF_CONST) {
+        nconst++;
+        nconst0 += d._pad2 == 0;
+      }
+    uint32_t nfrozen = 0;
+    for (bool f : F.frozen) nfrozen += f;
+    uint32_t nfold = 0;
+    for (bool f : in_prefix) nfold += f;
+    if (!P.plan_json.empty() && P.plan_json.back() == '}') {
+      P.plan_json.pop_back();
+      P.plan_json += ",\"fold\":{\"runs\":" + std::to_string(P.fold_runs.size() / 4) + ",\"folded_links\":" +
+                     std::to_string(nfold) + ",\"ids\":" +
+                     std::to_string(P.fold_nids) + ",\"const_links\":" + std::to_string(nconst) +
+                     ",\"const_nomatch\":" + std::to_string(nconst0) + ",\"const_args\":" + std::to_string(n_args) +
+                     ",\"frozen_slots\":" + std::to_string(nfrozen) + "}}";
+    }
+  }
+  if (P.fold_ids.empty()) P.fold_ids.push_back(0);  // a non-empty section (fold_nids is the count)
+  if (P.fold_runs.empty()) P.fold_runs.insert(P.fold_runs.end(), {0u, 0u, 0u, 0xFFFFFFFFu});
+}
+
 int compile_program(const std::string& text, const std::vector<std::string>& exports, uint32_t cap,
                     Program* out, std::string* err, const std::map<std::string, std::string>* data_files) {
   struct FilesScope {
@@ -2226,6 +2770,7 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
       v.key_len = (uint32_t)out->txrx.size() - v.key_off;
     }
     if (out->txrx.empty()) out->txrx.push_back(0);
+    fold_program(out, exports);
     out->n_markers = (uint32_t)L.markers.size();
     if (out->strpool.empty()) out->strpool.push_back(0);
     if (out->u8pool.empty()) out->u8pool.push_back(0);

@@ -53,6 +53,12 @@ struct Program {
   std::vector<uint32_t> pike_ranges;
   std::vector<DDynSite> dyn_sites;     // macro-key setvars (run-time TX keys)
   std::vector<uint32_t> txrx;          // static slots each regex-keyed TX target matches
+  std::vector<DSnapSlot> tx_snap;      // folded TX state after the request-independent phase-1 prefix
+  std::vector<uint32_t> fold_ids;      // rule ids that prefix matched
+  std::vector<uint32_t> fold_runs;     // per run of folded phase-1 rules: ids offset, id count, walk end,
+                                       // skipAfter marker pending at the end (0xFFFFFFFF: none)
+  uint32_t fold_nids = 0;              // fold_ids entries (the section holds a placeholder when 0)
+  uint8_t fold_on = 0;
   uint32_t n_hit_slots = 0;
   uint32_t n_union_dfas = 0;
   uint32_t max_img_bytes = 0;      // largest small-job LDS image

@@ -173,6 +173,10 @@ enum TCode : uint8_t {
 enum Disruptive : uint8_t { D_NONE = 0, D_DENY = 1, D_DROP = 2, D_REDIRECT = 3, D_PASS = 4 };
 
 enum RuleFlags : uint8_t {
+  RF_FOLDED = 128,  // first rule of a run of folded request-independent phase-1 rules: k_eval emits the
+                    // run's matched ids and jumps past it (DRule._pad2 = run index, DProgram.fold_runs)
+  RF_CONST = 64,  // request-independent link whose inputs are folded constants (compile.cpp fold_program):
+                  // it matches DRule._pad2 values, whatever the request -- k_eval skips targets and operator
   RF_CHILD = 1,
   RF_MARKER = 2,
   RF_CAPTURE = 4,
@@ -224,7 +228,19 @@ struct DRule {
   uint8_t flags;        // RuleFlags
   uint8_t _pad;
   int32_t hit_slot;     // phase-A hit bit (-1: evaluated by the interpreter only)
-  uint32_t _pad2;
+  uint32_t _pad2;       // RF_CONST: the number of values the link matches (its actions run that often);
+                        // RF_FOLDED: its run
+};
+
+// Folded TX state after the request-independent prefix of phase 1 (compile.cpp
+// fold_program): one record per TX slot, state as in kernels.hip Slot (0 unset,
+// 1 integer num, 2 string strpool[off, off + len)).  The runtime turns it into
+// device Slot records; k_eval reads a slot from it until the request writes
+// the slot (copy on write).
+struct DSnapSlot {
+  int64_t num;
+  uint32_t off, len;
+  uint32_t state, _pad;
 };
 
 // ------------------------------------------------------ phase-A scan plan
@@ -568,6 +584,12 @@ struct DProgram {
   uint32_t slot_hash_mask;            // (runtime.cpp; a macro-key setvar resolves to a static slot first)
   uint32_t n_dyn_sites;               // macro-key setvars (DDynSite): requests carry a dynamic TX area
   const uint32_t* txrx;               // static slots a regex-keyed TX target matches (DVarRef.key_off/len)
+  // request-independent phase-1 rules, evaluated at compile time (fold_program):
+  const uint8_t* tx_snap;             // Slot[n_slots] (kernels.hip) after it
+  const uint32_t* fold_ids;           // the ids the folded rules matched, in walk order
+  const uint32_t* fold_runs;          // per run: ids offset, count, walk index after it, pending skipAfter
+  uint32_t fold_nids;
+  uint32_t fold_on;                   // 0: nothing folded (TX starts empty)
   uint32_t n_slots;
   uint32_t n_markers;
   int32_t exports[8];           // TX slot per export, -1 = none

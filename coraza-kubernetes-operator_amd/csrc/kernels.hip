@@ -1305,6 +1305,8 @@ struct Tx {
   uint32_t* capws;           // pike_match workspace (observable captures; nullptr: none)
   uint8_t* capbuf;           // per capture group g: cap_t bytes holding TX.g's value
   uint8_t* dyn;              // TX keys macro-key setvars created (DynHdr; nullptr: the program has none)
+  uint64_t wm0, wm1;         // TX slots < 128 this request owns (written); the others read the snapshot
+  bool snap;                 // the folded prefix ran (phase 1 started): unowned slots read DProgram.tx_snap
   uint32_t cur_id;           // id of the top-level rule being evaluated (capture records)
   bool profon;               // GI_PROF counters (diagnostics)
   uint32_t prof_visits, prof_evals, prof_rules;
@@ -1313,6 +1315,32 @@ struct Tx {
 };
 
 #define TXS(t, s) ((t).slots[(uint64_t)(s) * (t).n_req])
+
+// TX slot s, copy on write over the folded snapshot (compile.cpp
+// fold_program): a slot the request has not written reads the program's
+// snapshot (once the folded prefix ran; before, every slot is unset), so no
+// per-request TX initialisation touches HBM.  Slots >= 128 are always owned
+// (initialised at phase-1 start).
+__device__ __forceinline__ bool tx_owned(const Tx& t, uint32_t s) {
+  return s >= 128 || ((s < 64 ? t.wm0 >> s : t.wm1 >> (s - 64)) & 1u);
+}
+__device__ __forceinline__ Slot slot_rd(const Tx& t, uint32_t s) {
+  if (tx_owned(t, s)) return TXS(t, s);
+  if (t.snap) return ((const Slot*)t.P->tx_snap)[s];
+  Slot z;
+  z.num = 0;
+  z.n = 0;
+  z.state = 0;
+  return z;
+}
+__device__ __forceinline__ Slot& slot_wr(Tx& t, uint32_t s) {
+  if (!tx_owned(t, s)) {
+    TXS(t, s) = slot_rd(t, s);
+    if (s < 64) t.wm0 |= 1ull << s;
+    else t.wm1 |= 1ull << (s - 64);
+  }
+  return TXS(t, s);
+}
 
 // tx_alloc / add_field serve Tx and the body parser's JsonCtx alike
 template <class C>
@@ -3151,7 +3179,8 @@ __device__ __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
     if (p.kind == TP_LIT) {
       s = {P.strpool + p.off, p.len};
     } else if (p.kind == TP_TX) {
-      s = slot_str(t, TXS(t, p.slot), nb);
+      const Slot sv = slot_rd(t, (uint32_t)p.slot);
+      s = slot_str(t, sv, nb);
     } else if (p.kind == TP_SINGLE) {
       s = single_val(t, p.single, nb);
     } else if (p.kind == TP_MV) {
@@ -3214,7 +3243,7 @@ __device__ __noinline__ Slot* dyn_slot(Tx& t, const DAction& a, bool create) {
     const uint32_t e = P.slot_hash[i];
     if (!e) break;
     const uint32_t sid = e - 1;
-    if (eq_bytes(P.strpool + P.slot_names[2 * sid], P.slot_names[2 * sid + 1], kp, k.n)) return &TXS(t, sid);
+    if (eq_bytes(P.strpool + P.slot_names[2 * sid], P.slot_names[2 * sid + 1], kp, k.n)) return &slot_wr(t, sid);
   }
   DynHdr* H = (DynHdr*)t.dyn;
   DynEnt* E = dyn_ents(t.dyn);
@@ -3239,7 +3268,7 @@ __device__ __noinline__ Slot* dyn_slot(Tx& t, const DAction& a, bool create) {
 
 // setvar [upstream internal/actions/setvar.go]
 __device__ __forceinline__ void run_setvar(Tx& t, const DAction& a) {
-  Slot* slp = a.slot >= 0 ? &TXS(t, a.slot) : dyn_slot(t, a, a.kind == A_SETVAR);
+  Slot* slp = a.slot >= 0 ? &slot_wr(t, (uint32_t)a.slot) : dyn_slot(t, a, a.kind == A_SETVAR);
   if (!slp) return;
   Slot& sl = *slp;
   if (a.kind == A_SETVAR_DEL) {
@@ -3255,7 +3284,7 @@ __device__ __forceinline__ void run_setvar(Tx& t, const DAction& a) {
   if (a.a != SV_GENERIC) {
     int64_t vv = a.b;
     if (a.a == SV_ADD_SLOT || a.a == SV_SUB_SLOT) {
-      const Slot& src = TXS(t, a.b);
+      const Slot src = slot_rd(t, (uint32_t)a.b);
       if (src.state == 0) return;  // "+" alone: Atoi("") fails, no change
       if (src.state != 1) goto generic;
       vv = src.num;
@@ -3934,6 +3963,13 @@ __device__ __forceinline__ uint32_t field_filter(Tx& t, const DRule& R, const DV
 template <bool W>
 __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   const DProgram& P = *t.P;
+  // a folded constant link (compile.cpp fold_program): the values of the TX
+  // slots it reads are the same for every request that reaches it, so it
+  // matches _pad2 values; only its per-match actions remain
+  if (R.flags & RF_CONST) {
+    for (uint32_t k = 0; k < R._pad2; k++) run_actions(t, R);
+    return R._pad2;
+  }
   // phase-A filter: a clear hit bit proves no value matches (exact); a set
   // bit (match or "maybe") falls through to the full evaluation below.
   if (R.hit_slot >= 0 && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post)) {
@@ -4021,7 +4057,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         Slot sl;
         if (si < se) {
           const uint32_t sid = vr.key_mode == 2 ? P.txrx[vr.key_off + si] : si;
-          sl = TXS(t, sid);
+          sl = slot_rd(t, sid);
           if (sl.state == 0) continue;
           nm = P.strpool + P.slot_names[sid * 2];
           nn = P.slot_names[sid * 2 + 1];
@@ -4225,6 +4261,7 @@ __device__ __forceinline__ bool rule_noop(Tx& t, const DRule& R) {
   }
   if (t.skip_after >= 0) return R.marker != t.skip_after;
   if (R.flags & RF_MARKER) return true;
+  if ((R.flags & RF_CONST) && R._pad2 == 0) return true;  // a folded link that matches nothing
   return R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
          !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u);
 }
@@ -4236,7 +4273,17 @@ __device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
   if (t.engine == ENGINE_OFF) return;
   t.phase = phase;
   const uint32_t kend = P.top_end[phase - 1];
-  for (uint32_t k = P.top_begin[phase - 1]; k < kend; k++) {
+  const uint32_t k0 = P.top_begin[phase - 1];
+  if (phase == 1 && P.fold_on) {
+    // the folded request-independent rules (compile.cpp fold_program): their
+    // TX effects are the snapshot from here on (ids: where the walk reaches them)
+    t.snap = true;
+    for (uint32_t s = 128; s < P.n_slots; s++) TXS(t, s) = ((const Slot*)P.tx_snap)[s];
+    if (t.capws)
+      for (uint32_t g = 0; g < 9; g++)
+        if (P.cap_slots[g] >= 0) TXS(t, P.cap_slots[g]) = ((const Slot*)P.tx_snap)[P.cap_slots[g]];
+  }
+  for (uint32_t k = k0; k < kend; k++) {
     if (t.interrupted) break;
     if (t.flags & GI_REQ_ERROR_MASK) break;
     if (W && t.skip == 0) {
@@ -4273,6 +4320,19 @@ __device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
       continue;
     }
     if (R.flags & RF_MARKER) continue;
+    if (R.flags & RF_FOLDED) {
+      // a run of folded rules (compile.cpp fold_program): their TX effects are
+      // the snapshot, their matched ids are fixed; the walk continues after it
+      const uint32_t* fr = P.fold_runs + 4ull * R._pad2;
+      for (uint32_t i = 0; i < fr[1]; i++) {
+        if (t.nmatched < t.mcap) t.mout[t.nmatched] = P.fold_ids[fr[0] + i];
+        else t.flags |= GI_REQ_MATCH_TRUNC;
+        t.nmatched++;
+      }
+      t.skip_after = (int32_t)fr[3];
+      k = fr[2] - 1;
+      continue;
+    }
     if (t.mv) {  // RuleGroup.Eval resets MATCHED_VARS(_NAMES) before each rule
       t.mv->n = 0;
       t.mv->nb = 0;
@@ -4280,6 +4340,7 @@ __device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
     if (R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u))
       continue;  // phase A proved the first link matches nothing
+    if ((R.flags & RF_CONST) && R._pad2 == 0) continue;  // folded: matches nothing for any request
     eval_top<W>(t, ri);
     // a skipAfter the rule just set: the rules up to its marker are all
     // skipped (no side effects), so resume at the marker entry directly
@@ -6428,7 +6489,20 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
     CH->trunc = 0;
   }
   t.mcap = B.mcap;
-  for (uint32_t s = 0; s < P.n_slots; s++) TXS(t, s).state = 0;
+  // TX: copy on write over the folded snapshot; slots >= 128 and the capture
+  // groups (run_capture writes those directly) start owned and unset
+  t.wm0 = t.wm1 = 0;
+  t.snap = false;
+  for (uint32_t s = 128; s < P.n_slots; s++) TXS(t, s).state = 0;
+  if (t.capws)
+    for (uint32_t g = 0; g < 9; g++) {
+      const int32_t cs = P.cap_slots[g];
+      if (cs >= 0) {
+        TXS(t, cs).state = 0;
+        if (cs < 64) t.wm0 |= 1ull << cs;
+        else if (cs < 128) t.wm1 |= 1ull << (cs - 64);
+      }
+    }
   if (t.dyn) {
     const ReqLayout Lr = B.layout[r];
     *(DynHdr*)t.dyn = DynHdr{0u, Lr.dyn_cap, 0u, Lr.dyn_capb};
@@ -6601,7 +6675,7 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
     int64_t x = 0;
     if (e < P.n_exports && P.exports[e] >= 0) {
       bool okk;
-      x = slot_int(TXS(t, P.exports[e]), &okk);
+      x = slot_int(slot_rd(t, (uint32_t)P.exports[e]), &okk);
       if (!okk) x = 0;
     }
     v.tx_export[e] = x;

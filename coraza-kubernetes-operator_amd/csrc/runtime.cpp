@@ -388,6 +388,23 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   }
   UP(slot_hash, shash, uint32_t)
   UP(txrx, P.txrx, uint32_t)
+  // folded TX snapshot as device Slot records (kernels.hip Slot: num | string
+  // pointer into the device string pool, n, state)
+  struct SnapDev {
+    uint64_t v;
+    uint32_t n, state;
+  };
+  static_assert(sizeof(SnapDev) == GI_SLOT_BYTES, "Slot layout");
+  std::vector<SnapDev> snap(std::max<size_t>(P.tx_snap.size(), 1), SnapDev{0, 0, 0});
+  for (size_t i = 0; i < P.tx_snap.size(); i++) {
+    const DSnapSlot& z = P.tx_snap[i];
+    snap[i].state = z.state;
+    snap[i].n = z.state == 2 ? z.len : 0u;
+    snap[i].v = z.state == 1 ? (uint64_t)z.num : z.state == 2 ? (uint64_t)(uintptr_t)(np.strpool + z.off) : 0ull;
+  }
+  UP(tx_snap, snap, uint8_t)
+  UP(fold_ids, P.fold_ids, uint32_t)
+  UP(fold_runs, P.fold_runs, uint32_t)
 #undef UP
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return discard(e == hipErrorOutOfMemory ? GI_ENOMEM : GI_ENODEV, "ruleset upload failed");
@@ -412,6 +429,19 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   np.top_end[1] = (uint32_t)top_ph.size();
   np.n_slots = P.n_slots;
   np.n_dyn_sites = (uint32_t)P.dyn_sites.size();
+  if (P.tx_snap.size() != P.n_slots) return discard(GI_EINVAL, "folded TX snapshot size");
+  // a folded run starts and ends inside the phase-1 walk, at its own rule
+  for (uint32_t a = 0; a < n_ph1; a++) {
+    const DRule& R = P.rules[top_ph[a]];
+    if (!(R.flags & RF_FOLDED)) continue;
+    if (4ull * R._pad2 + 3 >= P.fold_runs.size() || P.fold_runs[4 * R._pad2 + 2] <= a ||
+        P.fold_runs[4 * R._pad2 + 2] > n_ph1)
+      return discard(GI_EINVAL, "folded run out of range");
+  }
+  for (size_t a = n_ph1; a < top_ph.size(); a++)
+    if (P.rules[top_ph[a]].flags & RF_FOLDED) return discard(GI_EINVAL, "folded rule outside phase 1");
+  np.fold_on = P.fold_on;
+  np.fold_nids = P.fold_nids;
   np.n_markers = P.n_markers;
   np.n_exports = (uint32_t)P.exports.size();
   // score histogram (k_tally): the sum of the exported inbound_anomaly_score_pl1..pl4 -- what
