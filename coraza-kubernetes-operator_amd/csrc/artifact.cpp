@@ -29,7 +29,7 @@ struct Scalars {
   uint8_t item_sides[8];
   uint32_t item_singles, n_hit_slots, n_union_dfas, max_img_bytes, max_big_img_bytes, n_slots, n_markers;
   uint8_t rule_engine, body_access, mv_used, body_partial, fold_on, _pad[3];
-  uint32_t fold_nids, _pad4;
+  uint32_t fold_nids, max_tx_lit;
   uint64_t body_limit, source_digest;
   uint64_t compiler_rev;  // fnv64 of kCompilerRev
 };
@@ -97,6 +97,7 @@ std::vector<uint8_t> serialize_program(const Program& P) {
   s.body_partial = P.body_partial;
   s.fold_on = P.fold_on;
   s.fold_nids = P.fold_nids;
+  s.max_tx_lit = P.max_tx_lit;
   s.body_limit = P.body_limit;
   s.source_digest = P.source_digest;
   s.compiler_rev = compiler_rev_hash();
@@ -183,6 +184,7 @@ bool deserialize_program(const uint8_t* buf, size_t n, Program* P, std::string* 
         out.body_partial = s.body_partial;
         out.fold_on = s.fold_on;
         out.fold_nids = s.fold_nids;
+        out.max_tx_lit = s.max_tx_lit;
         out.body_limit = s.body_limit;
         out.source_digest = s.source_digest;
         seen_scalars = true;

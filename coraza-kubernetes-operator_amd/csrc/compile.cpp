@@ -2733,6 +2733,14 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
       }
     }
     L.finish_streams();
+    // chains whose later links read MATCHED_VARS(_NAMES) (the first link reads
+    // them right after RuleGroup.Eval's reset: empty)
+    for (uint32_t ti : out->top)
+      for (int32_t ci = out->rules[ti].chain_next; ci >= 0; ci = out->rules[ci].chain_next)
+        for (uint32_t q = 0; q < out->rules[ci].var_count; q++)
+          if (out->vars[out->rules[ci].var_begin + q].var == V_MATCHED_VARS ||
+              out->vars[out->rules[ci].var_begin + q].var == V_MATCHED_VARS_NAMES)
+            out->rules[ti].flags2 |= RF2_MVS;
     {  // top-level rules with an observable capture link (capture records, gi_capture)
       std::string ids;
       for (uint32_t ti : out->top)
@@ -2771,6 +2779,15 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
     }
     if (out->txrx.empty()) out->txrx.push_back(0);
     fold_program(out, exports);
+    for (const DAction& a : out->acts)  // literal setvar values (snapshot strings are literals or their expansions)
+      if ((a.kind == A_SETVAR) && a.tmpl >= 0) {
+        const DTmpl& tm = out->tmpls[a.tmpl];
+        uint32_t n = 0;
+        for (uint32_t k = 0; k < tm.part_count; k++)
+          if (out->tparts[tm.part_begin + k].kind == TP_LIT) n += out->tparts[tm.part_begin + k].len;
+        out->max_tx_lit = std::max(out->max_tx_lit, n);
+      }
+    for (const DSnapSlot& z : out->tx_snap) out->max_tx_lit = std::max(out->max_tx_lit, z.len);
     out->n_markers = (uint32_t)L.markers.size();
     if (out->strpool.empty()) out->strpool.push_back(0);
     if (out->u8pool.empty()) out->u8pool.push_back(0);

@@ -59,6 +59,7 @@ struct Program {
                                        // skipAfter marker pending at the end (0xFFFFFFFF: none)
   uint32_t fold_nids = 0;              // fold_ids entries (the section holds a placeholder when 0)
   uint8_t fold_on = 0;
+  uint32_t max_tx_lit = 0;             // longest literal a setvar can store (MATCHED_VARS arena bound)
   uint32_t n_hit_slots = 0;
   uint32_t n_union_dfas = 0;
   uint32_t max_img_bytes = 0;      // largest small-job LDS image

@@ -25,6 +25,8 @@ struct ReqLayout {
   uint64_t hset_word;  // its first word in DBatch.hset: [0] overflow flag, [1, cap] keys
   uint32_t dyn_cap;    // dynamic TX area (macro-key setvars): entries
   uint32_t dyn_capb;   // and bytes (0 / 0: the program has none)
+  uint32_t mv_cap_e;   // MATCHED_VARS entries / arena bytes one rule can record (kernels.hip MvState;
+  uint32_t mv_cap_a;   // 0 / 0: the program reads no matched-variable state)
 };
 
 struct DBatch {
@@ -152,6 +154,8 @@ struct LaunchLog {
 // stop_after > 0 (debugging): launch only the first stop_after kernels and
 // synchronise after each, printing the first failing one.
 // tally_ids: the ruleset's distinct rule ids, ascending (k_tally bins).
+// CPU baseline: request 0 of B through the interpreter compiled for the host (kernels.hip)
+void cpu_inspect_one(const DProgram& P, const DBatch& B);
 void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
                      int stop_after, LaunchLog* log, const uint32_t* tally_ids, uint32_t n_tally_ids);
 

@@ -15,16 +15,28 @@
 #define __device__
 #endif
 
+// The per-request interpreter (kernels.hip: collect, transformations,
+// operators, body processors, rule walk) is compiled for the GPU and, once
+// more, for the host: gi_cpu_baseline_inspect runs the same code on the CPU
+// cores as SURVEY §8(d)'s CPU baseline.  GI_HD marks that code; GI_TABLE its
+// read-only tables (the GPU's constant memory; plain const arrays on the host).
+#define GI_HD __host__ __device__
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GI_TABLE __device__ __constant__
+#else
+#define GI_TABLE static const
+#endif
+
 namespace gi {
 
 // Program records are immutable for the life of a context: reading them
 // through the constant address space lets the compiler use scalar loads for
 // wave-uniform indices (rule walk, operators, actions).
-#if defined(__HIPCC__)
+#if defined(__HIP_DEVICE_COMPILE__)
 #define GI_CONST(T, p) ((const __attribute__((address_space(4))) T*)(p))
 // copy record i of array p (sizeof(T) % 4 == 0) through the constant space
 template <class T>
-__device__ __forceinline__ T gi_cload(const T* p, uint64_t i) {
+GI_HD __forceinline__ T gi_cload(const T* p, uint64_t i) {
   static_assert(sizeof(T) % 4 == 0, "record size");
   const __attribute__((address_space(4))) uint32_t* q =
       (const __attribute__((address_space(4))) uint32_t*)(p + i);
@@ -37,6 +49,10 @@ __device__ __forceinline__ T gi_cload(const T* p, uint64_t i) {
 }
 #else
 #define GI_CONST(T, p) ((const T*)(p))
+template <class T>
+GI_HD inline T gi_cload(const T* p, uint64_t i) {
+  return p[i];
+}
 #endif
 
 // ------------------------------------------------------------- variables
@@ -185,6 +201,11 @@ enum RuleFlags : uint8_t {
   RF_MULTIMATCH = 32,  // multiMatch: the operator runs on the value and after every transformation
 };
 
+enum RuleFlags2 : uint8_t {
+  RF2_MVS = 1,  // a later link of this chain reads MATCHED_VARS(_NAMES): k_eval keeps the entries
+                // (otherwise only MATCHED_VAR / MATCHED_VAR_NAME are updated per match)
+};
+
 enum ActKind : uint8_t {
   A_SETVAR = 1,
   A_SETVAR_DEL,
@@ -226,7 +247,7 @@ struct DRule {
   uint8_t phase;
   uint8_t disruptive;
   uint8_t flags;        // RuleFlags
-  uint8_t _pad;
+  uint8_t flags2;       // RF2_* (top-level rules)
   int32_t hit_slot;     // phase-A hit bit (-1: evaluated by the interpreter only)
   uint32_t _pad2;       // RF_CONST: the number of values the link matches (its actions run that often);
                         // RF_FOLDED: its run

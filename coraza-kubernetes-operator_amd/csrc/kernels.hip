@@ -11,6 +11,8 @@
 //              block-reduced tallies (one atomic per block per counter)
 // Semantics follow coraza/v3 v3.3.3 [upstream, see DESIGN.md]; every
 // function names the coraza source it restates.
+// (built with -D__HIP_DEFINE_EXTENDED_HOST_MIN_MAX__=1: the host interpreter,
+// cpu_inspect_one, needs min/max over every integer type, as on the device)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,7 +48,7 @@ struct Slot {  // 16 B: a wave's slot-s accesses cover 1 KB (k_eval's TX traffic
 };
 static_assert(sizeof(Slot) == GI_SLOT_BYTES, "Slot size (runtime.cpp sizes txslots with it)");
 
-__device__ __constant__ uint8_t kConstStrs[] =
+GI_TABLE uint8_t kConstStrs[] =
     "0\0URLENCODED\0JSON\0XML\0MULTIPART\0" "1\0JSON: invalid JSON\0" "//@*\0/*\0\0\0\0\0\0\0\0";  // padded for load_u32u
 #define CS_ZERO (kConstStrs + 0)
 #define CS_URLENCODED (kConstStrs + 2)
@@ -58,37 +60,37 @@ __device__ __constant__ uint8_t kConstStrs[] =
 #define CS_XML_ATTRS (kConstStrs + 53)  // XML collection keys (xml.go: "//@*" attribute values, "/*" text)
 #define CS_XML_TEXT (kConstStrs + 58)
 
-__device__ inline bool ishex(uint8_t c) {
+GI_HD inline bool ishex(uint8_t c) {
   return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
 }
-__device__ inline uint8_t hexv(uint8_t c) {
+GI_HD inline uint8_t hexv(uint8_t c) {
   return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10;
 }
-__device__ inline uint8_t x2c(uint8_t a, uint8_t b) { return (uint8_t)((hexv(a) << 4) | hexv(b)); }
-__device__ inline uint8_t alower(uint8_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
-__device__ inline bool isalnum_(uint8_t c) {
+GI_HD inline uint8_t x2c(uint8_t a, uint8_t b) { return (uint8_t)((hexv(a) << 4) | hexv(b)); }
+GI_HD inline uint8_t alower(uint8_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+GI_HD inline bool isalnum_(uint8_t c) {
   return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z');
 }
-__device__ inline bool isws(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
+GI_HD inline bool isws(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
 
-__device__ __forceinline__ bool eq_bytes(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn) {
+GI_HD __forceinline__ bool eq_bytes(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn) {
   if (an != bn) return false;
   for (uint32_t i = 0; i < an; i++)
     if (a[i] != b[i]) return false;
   return true;
 }
-__device__ bool eq_ascii_ci_both(const uint8_t* a, const uint8_t* b, uint32_t n) {
+GI_HD bool eq_ascii_ci_both(const uint8_t* a, const uint8_t* b, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
     if (alower(a[i]) != alower(b[i])) return false;
   return true;
 }
-__device__ __forceinline__ bool eq_ascii_ci(const uint8_t* a, uint32_t an, const uint8_t* lowered, uint32_t bn) {
+GI_HD __forceinline__ bool eq_ascii_ci(const uint8_t* a, uint32_t an, const uint8_t* lowered, uint32_t bn) {
   if (an != bn) return false;
   for (uint32_t i = 0; i < an; i++)
     if (alower(a[i]) != lowered[i]) return false;
   return true;
 }
-__device__ int64_t find_bytes(const uint8_t* h, uint32_t hn, const uint8_t* nd, uint32_t nn) {
+GI_HD int64_t find_bytes(const uint8_t* h, uint32_t hn, const uint8_t* nd, uint32_t nn) {
   if (nn == 0) return 0;
   if (nn > hn) return -1;
   for (uint32_t i = 0; i + nn <= hn; i++) {
@@ -100,7 +102,7 @@ __device__ int64_t find_bytes(const uint8_t* h, uint32_t hn, const uint8_t* nd, 
 }
 
 // strconv.Atoi: ok=false on syntax error; saturates on range error.
-__device__ int64_t go_atoi(const uint8_t* s, uint32_t n, bool* ok) {
+GI_HD int64_t go_atoi(const uint8_t* s, uint32_t n, bool* ok) {
   uint32_t i = 0;
   bool neg = false;
   if (i < n && (s[i] == '+' || s[i] == '-')) {
@@ -135,7 +137,7 @@ __device__ int64_t go_atoi(const uint8_t* s, uint32_t n, bool* ok) {
 }
 
 // strconv.Itoa into buf (>= 21 bytes), returns length.
-__device__ __forceinline__ uint32_t go_itoa(int64_t v, uint8_t* buf) {
+GI_HD __forceinline__ uint32_t go_itoa(int64_t v, uint8_t* buf) {
   uint8_t tmp[24];
   uint32_t n = 0;
   uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
@@ -150,7 +152,7 @@ __device__ __forceinline__ uint32_t go_itoa(int64_t v, uint8_t* buf) {
 }
 
 // utf8.DecodeRune
-__device__ inline uint32_t decode_rune(const uint8_t* b, uint32_t n, uint32_t i, uint32_t* w) {
+GI_HD inline uint32_t decode_rune(const uint8_t* b, uint32_t n, uint32_t i, uint32_t* w) {
   uint8_t c0 = b[i];
   if (c0 < 0x80) {
     *w = 1;
@@ -179,7 +181,7 @@ __device__ inline uint32_t decode_rune(const uint8_t* b, uint32_t n, uint32_t i,
   return ((c0 & 0x07) << 18) | ((c1 & 0x3F) << 12) | ((b[i + 2] & 0x3F) << 6) | (b[i + 3] & 0x3F);
 }
 
-__device__ inline uint32_t encode_rune(uint32_t r, uint8_t* o) {
+GI_HD inline uint32_t encode_rune(uint32_t r, uint8_t* o) {
   if (r < 0x80) { o[0] = (uint8_t)r; return 1; }
   if (r < 0x800) { o[0] = 0xC0 | (r >> 6); o[1] = 0x80 | (r & 0x3F); return 2; }
   if (r < 0x10000) {
@@ -194,18 +196,61 @@ __device__ inline uint32_t encode_rune(uint32_t r, uint8_t* o) {
 // Four bytes at p (any alignment) from two aligned dword loads: long values
 // are read a word per load instead of a byte per load.  May read up to 7
 // bytes past p (every buffer is padded: runtime.cpp).
-__device__ __forceinline__ uint32_t load_u32u(const uint8_t* p) {
+GI_HD __forceinline__ uint32_t load_u32u(const uint8_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
   const uintptr_t a = (uintptr_t)p;
   const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
   const uint32_t sh = (uint32_t)(a & 3);
   const uint32_t lo = w[0];
   return sh ? __builtin_amdgcn_alignbyte(w[1], lo, sh) : lo;
+#else
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+#endif
+}
+// bit scans the interpreter uses on both targets
+GI_HD __forceinline__ int gi_ffsll(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ffsll((unsigned long long)x);
+#else
+  return __builtin_ffsll((long long)x);
+#endif
+}
+// profiling counters / lane identity (GI_PROF diagnostics): nothing on the host interpreter
+GI_HD __forceinline__ uint64_t gi_clock() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return clock64();
+#else
+  return 0;
+#endif
+}
+GI_HD __forceinline__ void gi_prof_add(unsigned long long* p, unsigned long long v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicAdd(p, v);
+#else
+  *p += v;
+#endif
+}
+GI_HD __forceinline__ uint32_t gi_tid() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return threadIdx.x;
+#else
+  return 0;
+#endif
+}
+GI_HD __forceinline__ int gi_popcll(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popcll((unsigned long long)x);
+#else
+  return __builtin_popcountll((unsigned long long)x);
+#endif
 }
 
 // --------------------------------------------------------------- DFA scan
 // Sticky-accept DFA over rune classes (rune mode: Go UTF-8 decoding) or
 // bytes (phrase automata).  fold: ASCII-lowercase bytes before the lookup.
-__device__ bool dfa_match(const DProgram& P, int32_t id, const uint8_t* s, uint32_t n, bool fold) {
+GI_HD bool dfa_match(const DProgram& P, int32_t id, const uint8_t* s, uint32_t n, bool fold) {
   const DDfa d = P.dfas[id];
   const uint16_t* __restrict__ tr = P.trans + d.trans_off;
   const uint8_t* __restrict__ amap = P.u8pool + d.amap_off;
@@ -269,7 +314,7 @@ __device__ bool dfa_match(const DProgram& P, int32_t id, const uint8_t* s, uint3
 // the epsilon closure from T and from the start (unanchored search) is the
 // union of precomputed rows for (previous, next) rune kinds, which is what
 // ^ $ \b \B look at; a closure holding the match bit is a match.
-__device__ __noinline__ bool nfa_match(const DProgram& P, int32_t id, const uint8_t* s, uint32_t n) {
+GI_HD __noinline__ bool nfa_match(const DProgram& P, int32_t id, const uint8_t* s, uint32_t n) {
   const DNfa N = P.nfas[id];
   const uint32_t W = N.words;
   const uint8_t* amap = P.u8pool + N.amap_off;
@@ -304,7 +349,7 @@ __device__ __noinline__ bool nfa_match(const DProgram& P, int32_t id, const uint
     for (uint32_t k = 0; k < W; k++) S[k] = st[k];
     for (uint32_t k = 0; k < W; k++)
       for (uint64_t b = T[k]; b; b &= b - 1) {
-        const uint64_t* row = F + ((uint64_t)(k * 64 + __ffsll((unsigned long long)b) - 1) * 16 + cmb) * W;
+        const uint64_t* row = F + ((uint64_t)(k * 64 + gi_ffsll(b) - 1) * 16 + cmb) * W;
         for (uint32_t j = 0; j < W; j++) S[j] |= row[j];
       }
     if ((S[N.n_pos >> 6] >> (N.n_pos & 63)) & 1) return true;
@@ -320,7 +365,7 @@ __device__ __noinline__ bool nfa_match(const DProgram& P, int32_t id, const uint
 // Each writes dst (capacity cap) and returns the new length, or -1 on
 // overflow.  [upstream coraza internal/transformations/*.go]
 
-__device__ uint32_t lower_rune(const DProgram& P, uint32_t r) {
+GI_HD uint32_t lower_rune(const DProgram& P, uint32_t r) {
   if (r < 0x80) return (r >= 'A' && r <= 'Z') ? r + 32 : r;
   uint32_t lo = 0, hi = P.n_lower_pairs;
   while (lo < hi) {
@@ -333,7 +378,7 @@ __device__ uint32_t lower_rune(const DProgram& P, uint32_t r) {
 }
 
 // Go strings.ToLower
-__device__ int64_t t_lowercase(const DProgram& P, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_lowercase(const DProgram& P, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   bool ascii = true;
   for (uint32_t i = 0; i < n && ascii; i += 4) {
     uint32_t x = load_u32u(s + i);
@@ -376,7 +421,7 @@ __device__ int64_t t_lowercase(const DProgram& P, const uint8_t* s, uint32_t n, 
 }
 
 // ModSecurity urldecode_nonstrict (t:urlDecode)
-__device__ int64_t t_urldecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_urldecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -398,7 +443,7 @@ __device__ int64_t t_urldecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_
 }
 
 // ModSecurity urldecode_uni_nonstrict (t:urlDecodeUni; %uXXXX low byte, full-width +0x20)
-__device__ int64_t t_urldecodeuni(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_urldecodeuni(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -431,7 +476,7 @@ __device__ int64_t t_urldecodeuni(const uint8_t* s, uint32_t n, uint8_t* d, uint
 }
 
 // strtol(digits, base) & 0xFF, saturating like strtol/ParseInt on overflow
-__device__ uint8_t strtol_byte(const uint8_t* s, uint32_t n, uint32_t base) {
+GI_HD uint8_t strtol_byte(const uint8_t* s, uint32_t n, uint32_t base) {
   uint64_t acc = 0;
   for (uint32_t i = 0; i < n; i++) {
     uint32_t v = base == 16 ? hexv(s[i]) : (uint32_t)(s[i] - '0');
@@ -442,7 +487,7 @@ __device__ uint8_t strtol_byte(const uint8_t* s, uint32_t n, uint32_t base) {
 }
 
 // ModSecurity html_entities_decode_inplace (t:htmlEntityDecode)
-__device__ int64_t t_htmlentitydecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_htmlentitydecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -501,9 +546,9 @@ __device__ int64_t t_htmlentitydecode(const uint8_t* s, uint32_t n, uint8_t* d, 
   return o;
 }
 
-__device__ inline bool ws_or_nbsp(uint8_t c) { return isws(c) || c == 0xA0; }
+GI_HD inline bool ws_or_nbsp(uint8_t c) { return isws(c) || c == 0xA0; }
 
-__device__ int64_t t_simple(uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_simple(uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n + 1 > cap) return -1;
   uint32_t o = 0;
   switch (code) {
@@ -585,14 +630,14 @@ __device__ int64_t t_simple(uint8_t code, const uint8_t* s, uint32_t n, uint8_t*
 }
 
 // Go unicode.IsSpace
-__device__ inline bool go_isspace(uint32_t r) {
+GI_HD inline bool go_isspace(uint32_t r) {
   if (r <= 0xFF) return r == ' ' || (r >= 9 && r <= 13) || r == 0x85 || r == 0xA0;
   return r == 0x1680 || (r >= 0x2000 && r <= 0x200A) || r == 0x2028 || r == 0x2029 || r == 0x202F ||
          r == 0x205F || r == 0x3000;
 }
 
 // Go strings.TrimLeft/TrimRight(unicode.IsSpace)
-__device__ int64_t t_trim(uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_trim(uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   uint32_t a = 0, e = n;
   if (code == T_TRIM || code == T_TRIMLEFT) {
     while (a < e) {
@@ -637,7 +682,7 @@ __device__ int64_t t_trim(uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d
 }
 
 // Go path.Clean + coraza normalisePath wrapper
-__device__ int64_t t_normpath(bool win, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_normpath(bool win, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n == 0) return 0;
   if (n + 2 > cap) return -1;
   // work on a '\\' -> '/' view for Win
@@ -678,10 +723,10 @@ __device__ int64_t t_normpath(bool win, const uint8_t* s, uint32_t n, uint8_t* d
   return w;
 }
 
-__device__ inline bool isodigit(uint8_t c) { return c >= '0' && c <= '7'; }
+GI_HD inline bool isodigit(uint8_t c) { return c >= '0' && c <= '7'; }
 
 // ModSecurity js_decode_nonstrict_inplace (t:jsDecode)
-__device__ int64_t t_jsdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_jsdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -732,7 +777,7 @@ __device__ int64_t t_jsdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t
 
 // t:utf8toUnicode: valid multi-byte UTF-8 -> %uXXXX (lowercase hex, >= 4
 // digits); ASCII and invalid bytes copied.  [upstream utf8toUnicode.go]
-__device__ int64_t t_utf8tounicode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_utf8tounicode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   uint32_t o = 0, i = 0;
   const char* hx = "0123456789abcdef";
   while (i < n) {
@@ -766,7 +811,7 @@ __device__ int64_t t_utf8tounicode(const uint8_t* s, uint32_t n, uint8_t* d, uin
 // escapeseqdecode.go, removecommentschar.go; ModSecurity ports].  Kept out of
 // line so k_stream's inlined LDS chains do not carry their code.
 
-__device__ inline int b64_val(uint8_t c) {
+GI_HD inline int b64_val(uint8_t c) {
   if (c >= 'A' && c <= 'Z') return c - 'A';
   if (c >= 'a' && c <= 'z') return c - 'a' + 26;
   if (c >= '0' && c <= '9') return c - '0' + 52;
@@ -777,7 +822,7 @@ __device__ inline int b64_val(uint8_t c) {
 
 // ext = false: base64decode (CR/LF skipped, stop at the first other byte
 // outside the alphabet); ext = true: base64decodeext (every such byte skipped)
-__device__ int64_t t_b64decode(bool ext, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_b64decode(bool ext, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, x = 0, k = 0;
   for (uint32_t i = 0; i < n; i++) {
@@ -805,7 +850,7 @@ __device__ int64_t t_b64decode(bool ext, const uint8_t* s, uint32_t n, uint8_t* 
   return o;
 }
 
-__device__ int64_t t_b64encode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_b64encode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   const char* al = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
   const uint64_t out = 4ull * ((n + 2) / 3);
   if (out > cap) return -1;
@@ -826,7 +871,7 @@ __device__ int64_t t_b64encode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_
 
 // hex.DecodeString; an error (odd length, non-hex byte) keeps the value
 // (rule.go executeTransformations skips a failed transformation)
-__device__ int64_t t_hexdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_hexdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n > cap) return -1;
   bool ok = (n & 1) == 0;
   for (uint32_t i = 0; i < n && ok; i++) ok = ishex(s[i]);
@@ -838,7 +883,7 @@ __device__ int64_t t_hexdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_
   return n / 2;
 }
 
-__device__ int64_t t_hexencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_hexencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (2ull * n > cap) return -1;
   const char* hx = "0123456789abcdef";
   for (uint32_t i = 0; i < n; i++) {
@@ -848,7 +893,7 @@ __device__ int64_t t_hexencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_
   return 2 * n;
 }
 
-__device__ int64_t t_urlencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_urlencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   const char* hx = "0123456789abcdef";
   uint32_t o = 0;
   for (uint32_t i = 0; i < n; i++) {
@@ -867,10 +912,10 @@ __device__ int64_t t_urlencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_
   return o;
 }
 
-__device__ inline bool c_isspace(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
+GI_HD inline bool c_isspace(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
 
 // ModSecurity css_decode_inplace
-__device__ int64_t t_cssdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_cssdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -906,7 +951,7 @@ __device__ int64_t t_cssdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_
 }
 
 // ModSecurity ansi_c_sequences_decode_inplace
-__device__ int64_t t_escapeseqdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_escapeseqdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -955,7 +1000,7 @@ __device__ int64_t t_escapeseqdecode(const uint8_t* s, uint32_t n, uint8_t* d, u
 }
 
 // ModSecurity remove_comments_char
-__device__ int64_t t_removecommentschar(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_removecommentschar(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -981,7 +1026,7 @@ __device__ int64_t t_removecommentschar(const uint8_t* s, uint32_t n, uint8_t* d
 
 // Message padding shared by SHA-1 (big-endian length) and MD5 (little-endian):
 // 64-byte block b of the padded message s (n bytes).
-__device__ inline void digest_block(const uint8_t* s, uint32_t n, uint32_t b, bool be, uint32_t* w) {
+GI_HD inline void digest_block(const uint8_t* s, uint32_t n, uint32_t b, bool be, uint32_t* w) {
   uint8_t blk[64];
   const uint64_t bits = (uint64_t)n * 8;
   const uint32_t nb = (n + 9 + 63) / 64;
@@ -996,9 +1041,9 @@ __device__ inline void digest_block(const uint8_t* s, uint32_t n, uint32_t b, bo
               : ((uint32_t)blk[4 * k + 3] << 24) | ((uint32_t)blk[4 * k + 2] << 16) | ((uint32_t)blk[4 * k + 1] << 8) | blk[4 * k];
 }
 
-__device__ inline uint32_t rotl(uint32_t x, uint32_t c) { return (x << c) | (x >> (32 - c)); }
+GI_HD inline uint32_t rotl(uint32_t x, uint32_t c) { return (x << c) | (x >> (32 - c)); }
 
-__device__ int64_t t_sha1(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_sha1(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (cap < 20) return -1;
   uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
   const uint32_t nb = (n + 9 + 63) / 64;
@@ -1031,7 +1076,7 @@ __device__ int64_t t_sha1(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap
   return 20;
 }
 
-__device__ __constant__ uint32_t kMd5K[64] = {
+GI_TABLE uint32_t kMd5K[64] = {
     0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
     0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
     0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
@@ -1040,9 +1085,9 @@ __device__ __constant__ uint32_t kMd5K[64] = {
     0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
     0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
     0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
-__device__ __constant__ uint8_t kMd5S[16] = {7, 12, 17, 22, 5, 9, 14, 20, 4, 11, 16, 23, 6, 10, 15, 21};
+GI_TABLE uint8_t kMd5S[16] = {7, 12, 17, 22, 5, 9, 14, 20, 4, 11, 16, 23, 6, 10, 15, 21};
 
-__device__ int64_t t_md5(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD int64_t t_md5(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   if (cap < 16) return -1;
   uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
   const uint32_t nb = (n + 9 + 63) / 64;
@@ -1071,7 +1116,7 @@ __device__ int64_t t_md5(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap)
   return 16;
 }
 
-__device__ __noinline__ int64_t t_ext(uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+GI_HD __noinline__ int64_t t_ext(uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
   switch (code) {
     case T_BASE64DECODE: return t_b64decode(false, s, n, d, cap);
     case T_BASE64DECODEEXT: return t_b64decode(true, s, n, d, cap);
@@ -1088,7 +1133,7 @@ __device__ __noinline__ int64_t t_ext(uint8_t code, const uint8_t* s, uint32_t n
   return -1;
 }
 
-__device__ __forceinline__ int64_t apply_transform_inl(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n,
+GI_HD __forceinline__ int64_t apply_transform_inl(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n,
                                                       uint8_t* d, uint32_t cap) {
   switch (code) {
     case T_UTF8TOUNICODE: return t_utf8tounicode(s, n, d, cap);
@@ -1109,12 +1154,12 @@ __device__ __forceinline__ int64_t apply_transform_inl(const DProgram& P, uint8_
 
 // Out-of-line instance (generic pointers): k_eval, HBM buffers.  k_stream's
 // LDS path inlines apply_transform_inl so every buffer access is a ds_* op.
-__device__ __noinline__ int64_t apply_transform(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n,
+GI_HD __noinline__ int64_t apply_transform(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n,
                                                 uint8_t* d, uint32_t cap) {
   return apply_transform_inl(P, code, s, n, d, cap);
 }
 
-__device__ uint32_t value_summary(const uint8_t* s, uint32_t n) {
+GI_HD uint32_t value_summary(const uint8_t* s, uint32_t n) {
   uint32_t m = 0;
   uint32_t i = 0;
   for (; i + 4 <= n; i += 4) {
@@ -1126,7 +1171,7 @@ __device__ uint32_t value_summary(const uint8_t* s, uint32_t n) {
   return m;
 }
 // the same through a 256-entry table (k_stream keeps it in LDS)
-__device__ __forceinline__ uint32_t value_summary_lut(const uint16_t* lut, const uint8_t* s, uint32_t n) {
+GI_HD __forceinline__ uint32_t value_summary_lut(const uint16_t* lut, const uint8_t* s, uint32_t n) {
   uint32_t m = 0;
   for (uint32_t i = 0; i < n; i++) m |= lut[s[i]];
   return m;
@@ -1150,17 +1195,18 @@ struct MvState {
   uint32_t nb, cap_a;      // arena bytes used (reset with the entries)
   uint32_t cap_v, cap_n;
   uint32_t cur_vn, cur_nn; // MATCHED_VAR / MATCHED_VAR_NAME lengths (persist across rules)
-  uint32_t _pad[8];
+  uint32_t keep;           // the current rule's chain reads MATCHED_VARS(_NAMES): record the entries (RF2_MVS)
+  uint32_t _pad[7];
 };
 static_assert(sizeof(MvState) == 64 && sizeof(MvEnt) == 32, "MvState layout");
 
-__device__ inline MvEnt* mv_ents(MvState* m) { return (MvEnt*)(m + 1); }
-__device__ inline uint8_t* mv_arena(MvState* m) { return (uint8_t*)(mv_ents(m) + m->cap_e); }
-__device__ inline uint8_t* mv_curval(MvState* m) { return mv_arena(m) + ((m->cap_a + 15) & ~15u); }
-__device__ inline uint8_t* mv_curname(MvState* m) { return mv_curval(m) + ((m->cap_v + 15) & ~15u); }
+GI_HD inline MvEnt* mv_ents(MvState* m) { return (MvEnt*)(m + 1); }
+GI_HD inline uint8_t* mv_arena(MvState* m) { return (uint8_t*)(mv_ents(m) + m->cap_e); }
+GI_HD inline uint8_t* mv_curval(MvState* m) { return mv_arena(m) + ((m->cap_a + 15) & ~15u); }
+GI_HD inline uint8_t* mv_curname(MvState* m) { return mv_curval(m) + ((m->cap_v + 15) & ~15u); }
 
 // The variable's name as a rule writes it (coraza RuleVariable.Name()).
-__device__ const char* var_name(uint32_t var) {
+GI_HD const char* var_name(uint32_t var) {
   switch (var) {
     case S_REQUEST_METHOD: return "REQUEST_METHOD";
     case S_REQUEST_PROTOCOL: return "REQUEST_PROTOCOL";
@@ -1209,7 +1255,7 @@ __device__ const char* var_name(uint32_t var) {
 }
 
 // tx.matchVariable; false when a capacity is exceeded (the request is flagged).
-__device__ __noinline__ bool mv_record(MvState* m, uint32_t var, const uint8_t* k, uint32_t kn, const uint8_t* v,
+GI_HD __noinline__ bool mv_record(MvState* m, uint32_t var, const uint8_t* k, uint32_t kn, const uint8_t* v,
                                        uint32_t vn) {
   const char* vnm = var_name(var);
   uint32_t vl = 0;
@@ -1227,6 +1273,7 @@ __device__ __noinline__ bool mv_record(MvState* m, uint32_t var, const uint8_t* 
   uint8_t* cv = mv_curval(m);
   for (uint32_t i = 0; i < vn; i++) cv[i] = v[i];
   m->cur_vn = vn;
+  if (!m->keep) return true;  // nothing reads this rule's MATCHED_VARS
   // MATCHED_VARS SetIndex(name, 0, value)
   MvEnt* e = mv_ents(m);
   uint32_t at = m->n;
@@ -1321,10 +1368,10 @@ struct Tx {
 // snapshot (once the folded prefix ran; before, every slot is unset), so no
 // per-request TX initialisation touches HBM.  Slots >= 128 are always owned
 // (initialised at phase-1 start).
-__device__ __forceinline__ bool tx_owned(const Tx& t, uint32_t s) {
+GI_HD __forceinline__ bool tx_owned(const Tx& t, uint32_t s) {
   return s >= 128 || ((s < 64 ? t.wm0 >> s : t.wm1 >> (s - 64)) & 1u);
 }
-__device__ __forceinline__ Slot slot_rd(const Tx& t, uint32_t s) {
+GI_HD __forceinline__ Slot slot_rd(const Tx& t, uint32_t s) {
   if (tx_owned(t, s)) return TXS(t, s);
   if (t.snap) return ((const Slot*)t.P->tx_snap)[s];
   Slot z;
@@ -1333,7 +1380,7 @@ __device__ __forceinline__ Slot slot_rd(const Tx& t, uint32_t s) {
   z.state = 0;
   return z;
 }
-__device__ __forceinline__ Slot& slot_wr(Tx& t, uint32_t s) {
+GI_HD __forceinline__ Slot& slot_wr(Tx& t, uint32_t s) {
   if (!tx_owned(t, s)) {
     TXS(t, s) = slot_rd(t, s);
     if (s < 64) t.wm0 |= 1ull << s;
@@ -1344,7 +1391,7 @@ __device__ __forceinline__ Slot& slot_wr(Tx& t, uint32_t s) {
 
 // tx_alloc / add_field serve Tx and the body parser's JsonCtx alike
 template <class C>
-__device__ inline uint8_t* tx_alloc(C& t, uint32_t n) {
+GI_HD inline uint8_t* tx_alloc(C& t, uint32_t n) {
   if (t.nb + n > t.cap_b) {
     t.flags |= GI_REQ_OVERFLOW;
     return nullptr;
@@ -1355,7 +1402,7 @@ __device__ inline uint8_t* tx_alloc(C& t, uint32_t n) {
 }
 
 template <class C>
-__device__ inline void add_field(C& t, uint8_t kind, const uint8_t* k, uint32_t kn, const uint8_t* v, uint32_t vn) {
+GI_HD inline void add_field(C& t, uint8_t kind, const uint8_t* k, uint32_t kn, const uint8_t* v, uint32_t vn) {
   if (t.nf >= t.cap_f) {
     t.flags |= GI_REQ_OVERFLOW;
     return;
@@ -1369,7 +1416,7 @@ __device__ inline void add_field(C& t, uint8_t kind, const uint8_t* k, uint32_t 
 }
 
 // lenient %XX / '+' decoding (coraza internal/url QueryUnescape)
-__device__ uint32_t query_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
+GI_HD uint32_t query_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
   uint32_t o = 0, i = 0;
   while (i < n) {
     uint8_t c = s[i];
@@ -1387,7 +1434,7 @@ __device__ uint32_t query_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
 // coraza internal/url ParseQuery(query, '&') -> fields of `kind`.  A key or
 // value without '%' / '+' is its own decoding: the field points into the
 // request bytes, and only escaped parts are decoded into the arena.
-__device__ __forceinline__ void parse_query(Tx& t, const uint8_t* q, uint32_t n, uint8_t kind) {
+GI_HD __forceinline__ void parse_query(Tx& t, const uint8_t* q, uint32_t n, uint8_t kind) {
   uint32_t i = 0;
   while (i < n) {
     uint32_t j = i, e = 0xFFFFFFFFu;
@@ -1450,15 +1497,15 @@ struct JFrame {
   uint32_t is_arr;
 };
 
-__device__ inline bool json_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+GI_HD inline bool json_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 
-__device__ inline uint32_t hex4(const uint8_t* s) {
+GI_HD inline uint32_t hex4(const uint8_t* s) {
   return (hexv(s[0]) << 12) | (hexv(s[1]) << 8) | (hexv(s[2]) << 4) | hexv(s[3]);
 }
 
 // Validates the string whose opening quote is at s[i]; returns the index
 // after the closing quote (0 on error) and whether it holds escapes.
-__device__ uint32_t json_string_end(const uint8_t* s, uint32_t n, uint32_t i, bool* esc) {
+GI_HD uint32_t json_string_end(const uint8_t* s, uint32_t n, uint32_t i, bool* esc) {
   *esc = false;
   i++;
   while (i < n) {
@@ -1492,7 +1539,7 @@ __device__ uint32_t json_string_end(const uint8_t* s, uint32_t n, uint32_t i, bo
   return 0;
 }
 
-__device__ inline uint32_t utf8_put(uint32_t r, uint8_t* d) {
+GI_HD inline uint32_t utf8_put(uint32_t r, uint8_t* d) {
   if ((r >= 0xD800 && r <= 0xDFFF) || r > 0x10FFFF) r = 0xFFFD;
   if (r < 0x80) { d[0] = (uint8_t)r; return 1; }
   if (r < 0x800) { d[0] = 0xC0 | (r >> 6); d[1] = 0x80 | (r & 0x3F); return 2; }
@@ -1505,7 +1552,7 @@ __device__ inline uint32_t utf8_put(uint32_t r, uint8_t* d) {
 }
 
 // gjson unescape of a validated string body; never longer than its input.
-__device__ uint32_t json_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
+GI_HD uint32_t json_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
   uint32_t o = 0, i = 0;
   while (i < n) {
     const uint8_t c = s[i];
@@ -1537,7 +1584,7 @@ __device__ uint32_t json_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
 }
 
 // gjson validnumber at s[i]; returns the end index (0 on error).
-__device__ uint32_t json_number_end(const uint8_t* s, uint32_t n, uint32_t i) {
+GI_HD uint32_t json_number_end(const uint8_t* s, uint32_t n, uint32_t i) {
   if (i < n && s[i] == '-') i++;
   if (i >= n || s[i] < '0' || s[i] > '9') return 0;
   if (s[i] == '0') {
@@ -1561,7 +1608,7 @@ __device__ uint32_t json_number_end(const uint8_t* s, uint32_t n, uint32_t i) {
 
 // d[0, n) = s[0, n), four source bytes per load (s may be read up to 7 bytes
 // past its end: every arena is padded)
-__device__ __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint32_t n) {
+GI_HD __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint32_t n) {
   uint32_t k = 0;
   for (; k + 4 <= n; k += 4) {
     const uint32_t w = load_u32u(s + k);
@@ -1573,7 +1620,7 @@ __device__ __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint32_
   for (; k < n; k++) d[k] = s[k];
 }
 
-__device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
+GI_HD inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
     if (a[i] != b[i]) return false;
   return true;
@@ -1582,7 +1629,7 @@ __device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t 
 // Fold repeated keys of fields [f0, t.nf) (first position, last value) with
 // an open-addressing table in the transform scratch t.t1.
 template <class C>
-__device__ __forceinline__ void json_fold_keys(C& t, uint32_t f0) {
+GI_HD __forceinline__ void json_fold_keys(C& t, uint32_t f0) {
   const uint32_t nf = t.nf - f0;
   const uint32_t tsize = t.cap_t / 4;  // > body/2 + 2 >= nf (runtime.cpp sizing)
   if (nf < 2) return;
@@ -1621,7 +1668,7 @@ __device__ __forceinline__ void json_fold_keys(C& t, uint32_t f0) {
 }
 
 template <class C>
-__device__ __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t n) {
+GI_HD __forceinline__ void parse_json_body(C& t, const uint8_t* s, uint32_t n) {
   const uint32_t f0 = t.nf;
   uint32_t i = 0;
   while (i < n && json_ws(s[i])) i++;
@@ -1772,7 +1819,7 @@ struct JsonCtx {
   uint16_t flags;
 };
 
-__device__ __noinline__ void parse_json_body_ool(JsonCtx* c, const uint8_t* s, uint32_t n) {
+GI_HD __noinline__ void parse_json_body_ool(JsonCtx* c, const uint8_t* s, uint32_t n) {
   parse_json_body(*c, s, n);
 }
 
@@ -1790,14 +1837,14 @@ enum MpErr : uint8_t {
   MP_E_DATA, MP_E_COUNT
 };
 // REQBODY_ERROR_MSG per error class ("<processor>: <error>", generateRequestBodyError)
-__device__ __constant__ char kMpErrMsg[MP_E_COUNT][56] = {
+GI_TABLE char kMpErrMsg[MP_E_COUNT][56] = {
     "", "MULTIPART: mime: invalid media type", "MULTIPART: not a multipart body",
     "MULTIPART: multipart: boundary is empty", "MULTIPART: multipart: NextPart: EOF",
     "MULTIPART: multipart: NextPart: bufio: buffer full", "MULTIPART: multipart: expecting a new Part",
     "MULTIPART: multipart: unexpected line in Next()", "MULTIPART: multipart: NextPart: malformed MIME header",
     "MULTIPART: unexpected EOF"};
 
-__device__ inline bool mp_tspecial(uint8_t c) {
+GI_HD inline bool mp_tspecial(uint8_t c) {
   switch (c) {
     case '(': case ')': case '<': case '>': case '@': case ',': case ';': case ':': case '\\': case '"':
     case '/': case '[': case ']': case '?': case '=':
@@ -1805,11 +1852,11 @@ __device__ inline bool mp_tspecial(uint8_t c) {
   }
   return false;
 }
-__device__ inline bool mp_token(uint8_t c) { return c > 0x20 && c < 0x7F && !mp_tspecial(c); }
-__device__ inline bool mp_lws(uint8_t c) { return c == ' ' || c == '\t'; }
+GI_HD inline bool mp_token(uint8_t c) { return c > 0x20 && c < 0x7F && !mp_tspecial(c); }
+GI_HD inline bool mp_lws(uint8_t c) { return c == ' ' || c == '\t'; }
 
 // Next ";key=value" of a media type at v[*i]: 0 ok, 1 no more, -1 syntax error.
-__device__ int mp_next_param(const uint8_t* v, uint32_t n, uint32_t* i, uint32_t* ks, uint32_t* ke, uint32_t* vs,
+GI_HD int mp_next_param(const uint8_t* v, uint32_t n, uint32_t* i, uint32_t* ks, uint32_t* ke, uint32_t* vs,
                              uint32_t* ve, bool* quoted) {
   uint32_t p = *i;
   while (p < n && mp_lws(v[p])) p++;
@@ -1857,7 +1904,7 @@ __device__ int mp_next_param(const uint8_t* v, uint32_t n, uint32_t* i, uint32_t
 // lowercase literals; values unescaped into the arena when quoted with
 // escapes).  Returns 0 ok, 1 error, 2 unsupported (RFC 2231 parameter).
 template <class C>
-__device__ int mp_media(C& t, const uint8_t* v, uint32_t n, uint32_t* ts, uint32_t* te, const char* w0, Str* o0,
+GI_HD int mp_media(C& t, const uint8_t* v, uint32_t n, uint32_t* ts, uint32_t* te, const char* w0, Str* o0,
                         const char* w1, Str* o1) {
   o0->p = CS_ZERO;
   o0->n = 0;
@@ -1930,7 +1977,7 @@ __device__ int mp_media(C& t, const uint8_t* v, uint32_t n, uint32_t* ts, uint32
 }
 
 // line [*ls, *le) at s[i] without its "\r\n" / "\n"; *nx = the next line
-__device__ inline bool mp_line(const uint8_t* s, uint32_t n, uint32_t i, uint32_t* ls, uint32_t* le, uint32_t* nx) {
+GI_HD inline bool mp_line(const uint8_t* s, uint32_t n, uint32_t i, uint32_t* ls, uint32_t* le, uint32_t* nx) {
   if (i >= n) return false;
   uint32_t j = i;
   while (j < n && s[j] != '\n') j++;
@@ -1942,7 +1989,7 @@ __device__ inline bool mp_line(const uint8_t* s, uint32_t n, uint32_t i, uint32_
 }
 
 // textproto.CanonicalMIMEHeaderKey with its validity check
-__device__ inline bool mp_canonical(const uint8_t* k, uint32_t kn, bool* already) {
+GI_HD inline bool mp_canonical(const uint8_t* k, uint32_t kn, bool* already) {
   if (kn == 0) return false;
   bool up = true, same = true;
   for (uint32_t i = 0; i < kn; i++) {
@@ -1956,7 +2003,7 @@ __device__ inline bool mp_canonical(const uint8_t* k, uint32_t kn, bool* already
   return true;
 }
 
-__device__ inline bool mp_is_final(const uint8_t* s, uint32_t ls, uint32_t le_nl, const uint8_t* bd, uint32_t bn,
+GI_HD inline bool mp_is_final(const uint8_t* s, uint32_t ls, uint32_t le_nl, const uint8_t* bd, uint32_t bn,
                                    bool lf) {
   // line s[ls, le_nl) including its NL: ^--boundary--[ \t]*(NL)?$
   const uint32_t n = le_nl - ls;
@@ -1970,7 +2017,7 @@ __device__ inline bool mp_is_final(const uint8_t* s, uint32_t ls, uint32_t le_nl
 }
 
 // matchAfterPrefix == +1 at s[k]
-__device__ inline bool mp_after_ok(const uint8_t* s, uint32_t n, uint32_t k) {
+GI_HD inline bool mp_after_ok(const uint8_t* s, uint32_t n, uint32_t k) {
   if (k >= n) return true;
   const uint8_t c = s[k];
   if (c == ' ' || c == '\t' || c == '\r' || c == '\n') return true;
@@ -1984,7 +2031,7 @@ __device__ inline bool mp_after_ok(const uint8_t* s, uint32_t n, uint32_t k) {
 // "--" + boundary, ascending -- the delimiter search of a part's data then
 // walks this list instead of every byte of the part.
 template <class C>
-__device__ __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, const uint8_t* ct, uint32_t ctn,
+GI_HD __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, const uint8_t* ct, uint32_t ctn,
                                                 uint64_t* combined, bool* combined_set,
                                                 const uint32_t* cand = nullptr, uint32_t ncand = 0) {
   uint32_t ci = 0;  // next candidate
@@ -2248,21 +2295,21 @@ struct XName {
   uint32_t so, sn, lo, ln;  // prefix [so, so + sn) and local part [lo, lo + ln) in the body
 };
 
-__device__ inline bool xml_name_byte(uint8_t c) {
+GI_HD inline bool xml_name_byte(uint8_t c) {
   return (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '_' || c == ':' ||
          c == '.' || c == '-';
 }
-__device__ inline bool xml_in_range(uint32_t r) {
+GI_HD inline bool xml_in_range(uint32_t r) {
   return r == 0x09 || r == 0x0A || r == 0x0D || (r >= 0x20 && r <= 0xD7FF) || (r >= 0xE000 && r <= 0xFFFD) ||
          (r >= 0x10000 && r <= 0x10FFFF);
 }
-__device__ inline bool go_is_space(uint32_t r) {  // unicode.IsSpace
+GI_HD inline bool go_is_space(uint32_t r) {  // unicode.IsSpace
   return r == 0x09 || r == 0x0A || r == 0x0B || r == 0x0C || r == 0x0D || r == 0x20 || r == 0x85 || r == 0xA0 ||
          r == 0x1680 || (r >= 0x2000 && r <= 0x200A) || r == 0x2028 || r == 0x2029 || r == 0x202F || r == 0x205F ||
          r == 0x3000;
 }
 // HTML 4.01 entity by name (sorted table): code point or -1
-__device__ int32_t html_entity(const uint8_t* nm, uint32_t n) {
+GI_HD int32_t html_entity(const uint8_t* nm, uint32_t n) {
   uint32_t lo = 0, hi = GI_N_HTML_ENT;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -2285,22 +2332,22 @@ struct XmlDec {
   uint32_t n, i, line;
   int err;          // 0 none, 1 decoder error (msg set), 2 unsupported, 3 arena overflow
   uint32_t mo, ml;  // error message in the arena
-  __device__ XmlDec(C& tt, const uint8_t* ss, uint32_t nn) : t(tt), s(ss), n(nn), i(0), line(1), err(0), mo(0), ml(0) {}
-  __device__ int getc() {
+  GI_HD XmlDec(C& tt, const uint8_t* ss, uint32_t nn) : t(tt), s(ss), n(nn), i(0), line(1), err(0), mo(0), ml(0) {}
+  GI_HD int getc() {
     if (i >= n) return -1;
     const uint8_t b = s[i++];
     if (b == '\n') line++;
     return b;
   }
-  __device__ void ungetc(int b) {
+  GI_HD void ungetc(int b) {
     if (b == '\n') line--;
     i--;
   }
   // message pieces
-  __device__ void put(const char* p) {
+  GI_HD void put(const char* p) {
     for (; *p && err != 3; p++) putb((uint8_t)*p);
   }
-  __device__ void putb(uint8_t b) {
+  GI_HD void putb(uint8_t b) {
     if (t.nb + 1 > t.cap_b) {
       err = 3;
       return;
@@ -2308,15 +2355,15 @@ struct XmlDec {
     t.bytes[t.nb++] = b;
     ml++;
   }
-  __device__ void putn(const uint8_t* p, uint32_t k) {
+  GI_HD void putn(const uint8_t* p, uint32_t k) {
     for (uint32_t q = 0; q < k; q++) putb(p[q]);
   }
-  __device__ void putu(uint32_t v) {
+  GI_HD void putu(uint32_t v) {
     uint8_t b[12];
     const uint32_t k = go_itoa((int64_t)v, b);
     putn(b, k);
   }
-  __device__ void begin_msg(bool syntax) {
+  GI_HD void begin_msg(bool syntax) {
     err = 1;
     mo = t.nb;
     ml = 0;
@@ -2327,16 +2374,16 @@ struct XmlDec {
       put(": ");
     }
   }
-  __device__ void syntax(const char* m) {
+  GI_HD void syntax(const char* m) {
     begin_msg(true);
     put(m);
   }
-  __device__ int mustgetc() {
+  GI_HD int mustgetc() {
     const int b = getc();
     if (b < 0) syntax("unexpected EOF");
     return b;
   }
-  __device__ void space() {
+  GI_HD void space() {
     for (;;) {
       const int b = getc();
       if (b < 0) return;
@@ -2347,7 +2394,7 @@ struct XmlDec {
     }
   }
   // readName over the body: [*a, *e); false (nothing read) or err
-  __device__ bool read_name(uint32_t* a, uint32_t* e) {
+  GI_HD bool read_name(uint32_t* a, uint32_t* e) {
     int b = mustgetc();
     if (b < 0) return false;
     if (b < 0x80 && !xml_name_byte((uint8_t)b)) {
@@ -2367,7 +2414,7 @@ struct XmlDec {
     return true;
   }
   // isName for a name read by read_name (err 2 when it has non-ASCII bytes)
-  __device__ bool is_name(uint32_t a, uint32_t e) {
+  GI_HD bool is_name(uint32_t a, uint32_t e) {
     if (e == a) return false;
     for (uint32_t k = a; k < e; k++)
       if (s[k] >= 0x80) {
@@ -2378,7 +2425,7 @@ struct XmlDec {
     return (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_' || c == ':';
   }
   // name(): false without a name (err unset) or on error
-  __device__ bool name(uint32_t* a, uint32_t* e) {
+  GI_HD bool name(uint32_t* a, uint32_t* e) {
     if (!read_name(a, e)) return false;
     if (!is_name(*a, *e)) {
       if (err == 2) return false;
@@ -2389,7 +2436,7 @@ struct XmlDec {
     }
     return true;
   }
-  __device__ bool nsname(XName* x) {
+  GI_HD bool nsname(XName* x) {
     uint32_t a, e;
     if (!name(&a, &e)) return false;
     uint32_t colons = 0, c = e;
@@ -2408,7 +2455,7 @@ struct XmlDec {
   }
   // text(quote, cdata): the decoded bytes appended to the arena at *o (length
   // *len); false on error.  Decoded text is never longer than its input.
-  __device__ bool text(int quote, bool cdata, uint32_t* o, uint32_t* len) {
+  GI_HD bool text(int quote, bool cdata, uint32_t* o, uint32_t* len) {
     uint8_t b0 = 0, b1 = 0;
     uint32_t trunc = 0;
     const uint32_t start = t.nb;
@@ -2554,7 +2601,7 @@ struct XmlDec {
     *len = dn;
     return true;
   }
-  __device__ bool attrval(uint32_t* o, uint32_t* len) {
+  GI_HD bool attrval(uint32_t* o, uint32_t* len) {
     int b = mustgetc();
     if (b < 0) return false;
     if (b == '"' || b == '\'') return text(b, false, o, len);
@@ -2578,7 +2625,7 @@ struct XmlDec {
 enum XTok : uint8_t { XT_NONE = 0, XT_START, XT_END, XT_CHARS, XT_OTHER };
 
 // encoding/xml procInst(param, s): the quoted value of param="..." in s
-__device__ bool xml_proc_inst(const uint8_t* s, uint32_t n, const char* param, uint32_t* vo, uint32_t* vn) {
+GI_HD bool xml_proc_inst(const uint8_t* s, uint32_t n, const char* param, uint32_t* vo, uint32_t* vn) {
   uint32_t lp = 0;
   while (param[lp]) lp++;  // includes the '='
   uint32_t i = 0;
@@ -2608,7 +2655,7 @@ __device__ bool xml_proc_inst(const uint8_t* s, uint32_t n, const char* param, u
   return false;
 }
 
-__device__ inline bool xml_autoclose(const uint8_t* s, uint32_t lo, uint32_t ln) {
+GI_HD inline bool xml_autoclose(const uint8_t* s, uint32_t lo, uint32_t ln) {
   const char* names[13] = {"basefont", "br", "area", "link", "img", "param", "hr", "input", "col", "frame",
                            "isindex", "base", "meta"};
   for (int k = 0; k < 13; k++) {
@@ -2620,7 +2667,7 @@ __device__ inline bool xml_autoclose(const uint8_t* s, uint32_t lo, uint32_t ln)
 }
 
 template <class C>
-__device__ __noinline__ int parse_xml(C& t, const uint8_t* s, uint32_t n, uint32_t* ws, uint32_t ws_words, Str* msg) {
+GI_HD __noinline__ int parse_xml(C& t, const uint8_t* s, uint32_t n, uint32_t* ws, uint32_t ws_words, Str* msg) {
   XmlDec<C> d(t, s, n);
   const uint32_t nf0 = t.nf, nb0 = t.nb;
   // ws: element stack (XName, 4 words each) from the front, text list ((off, len) pairs) from the back
@@ -2950,7 +2997,7 @@ __device__ __noinline__ int parse_xml(C& t, const uint8_t* s, uint32_t n, uint32
 }
 
 // net/url shouldEscape(c, encodePath)
-__device__ inline bool should_escape_path(uint8_t c) {
+GI_HD inline bool should_escape_path(uint8_t c) {
   if (isalnum_(c)) return false;
   switch (c) {
     case '-': case '_': case '.': case '~': return false;
@@ -2959,7 +3006,7 @@ __device__ inline bool should_escape_path(uint8_t c) {
   }
   return true;
 }
-__device__ inline bool valid_encoded_path_char(uint8_t c) {
+GI_HD inline bool valid_encoded_path_char(uint8_t c) {
   switch (c) {
     case '!': case '$': case '&': case '\'': case '(': case ')': case '*': case '+': case ',': case ';':
     case '=': case ':': case '@': case '[': case ']': case '%':
@@ -2969,7 +3016,7 @@ __device__ inline bool valid_encoded_path_char(uint8_t c) {
 }
 
 // ProcessURI [upstream corazawaf/transaction.go] + Go net/url Parse/String
-__device__ bool process_uri(Tx& t, const uint8_t* uri, uint32_t un) {
+GI_HD bool process_uri(Tx& t, const uint8_t* uri, uint32_t un) {
   t.single[S_REQUEST_URI_RAW] = {uri, un};
   uint32_t n = un;
   for (uint32_t i = 0; i < un; i++)
@@ -3091,7 +3138,7 @@ __device__ bool process_uri(Tx& t, const uint8_t* uri, uint32_t un) {
   return true;
 }
 
-__device__ void parse_cookies(Tx& t, const uint8_t* v, uint32_t n) {
+GI_HD void parse_cookies(Tx& t, const uint8_t* v, uint32_t n) {
   uint32_t a = 0, e = n;
   while (a < e && isws(v[a])) a++;
   while (e > a && isws(v[e - 1])) e--;
@@ -3114,26 +3161,26 @@ __device__ void parse_cookies(Tx& t, const uint8_t* v, uint32_t n) {
   }
 }
 
-__device__ inline bool starts_ci(const uint8_t* s, uint32_t n, const char* lit) {
+GI_HD inline bool starts_ci(const uint8_t* s, uint32_t n, const char* lit) {
   uint32_t i = 0;
   for (; lit[i]; i++)
     if (i >= n || alower(s[i]) != (uint8_t)lit[i]) return false;
   return true;
 }
 
-__device__ inline bool contains_ci(const uint8_t* s, uint32_t n, const char* lit) {
+GI_HD inline bool contains_ci(const uint8_t* s, uint32_t n, const char* lit) {
   for (uint32_t i = 0; i < n; i++)
     if (starts_ci(s + i, n - i, lit)) return true;
   return false;
 }
 
 // ------------------------------------------------------------ TX / macros
-__device__ __forceinline__ Str slot_str(Tx& t, const Slot& s, uint8_t* buf) {
+GI_HD __forceinline__ Str slot_str(Tx& t, const Slot& s, uint8_t* buf) {
   if (s.state == 1) return {buf, go_itoa(s.num, buf)};
   if (s.state == 2) return {s.p, s.n};
   return {buf, 0};
 }
-__device__ __forceinline__ int64_t slot_int(const Slot& s, bool* ok) {
+GI_HD __forceinline__ int64_t slot_int(const Slot& s, bool* ok) {
   if (s.state == 1) {
     *ok = true;
     return s.num;
@@ -3146,7 +3193,7 @@ __device__ __forceinline__ int64_t slot_int(const Slot& s, bool* ok) {
 // A single's value.  ARGS_COMBINED_SIZE is computed when read [upstream
 // internal/collections/sized.go SizeCollection over ARGS_GET + ARGS_POST:
 // the sum of len(key) + len(value) of every entry]; buf >= 24 bytes.
-__device__ __forceinline__ Str single_val(Tx& t, uint32_t sid, uint8_t* buf) {
+GI_HD __forceinline__ Str single_val(Tx& t, uint32_t sid, uint8_t* buf) {
   if (sid == S_ARGS_COMBINED_SIZE) {
     uint64_t n = 0;
     const uint32_t j0 = t.kx ? t.kx[FK_ARG_GET] : 0u, j1 = t.kx ? t.kx[FK_ARG_POST + 1] : t.nf;
@@ -3161,7 +3208,7 @@ __device__ __forceinline__ Str single_val(Tx& t, uint32_t sid, uint8_t* buf) {
 
 // Expand a %{..} template.  *persistent: result points into the program's
 // string pool (safe to keep in TX); otherwise into the macro scratch.
-__device__ __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
+GI_HD __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
   const DProgram& P = *t.P;
   *persistent = false;
   if (tid < 0) return {t.mt, 0};
@@ -3218,8 +3265,8 @@ struct DynEnt {
   Slot s;
 };
 static_assert(sizeof(DynEnt) == 32, "runtime.cpp sizes DynEnt as 32 bytes");
-__device__ __forceinline__ DynEnt* dyn_ents(uint8_t* d) { return (DynEnt*)(d + sizeof(DynHdr)); }
-__device__ __forceinline__ uint8_t* dyn_alloc(uint8_t* d, uint32_t n) {
+GI_HD __forceinline__ DynEnt* dyn_ents(uint8_t* d) { return (DynEnt*)(d + sizeof(DynHdr)); }
+GI_HD __forceinline__ uint8_t* dyn_alloc(uint8_t* d, uint32_t n) {
   DynHdr* H = (DynHdr*)d;
   if (H->nb + n > H->capb) return nullptr;
   uint8_t* p = d + sizeof(DynHdr) + 32ull * H->cap + H->nb;
@@ -3231,7 +3278,7 @@ __device__ __forceinline__ uint8_t* dyn_alloc(uint8_t* d, uint32_t n) {
 // [upstream setvar.go: strings.ToLower of the expanded key; ASCII here, like
 // the compiler's static TX names]; a key that names a static slot is that
 // slot, otherwise the dynamic entry with that key (created unless delete).
-__device__ __noinline__ Slot* dyn_slot(Tx& t, const DAction& a, bool create) {
+GI_HD __noinline__ Slot* dyn_slot(Tx& t, const DAction& a, bool create) {
   const DProgram& P = *t.P;
   bool pers;
   const Str k = expand(t, a.aux, &pers);
@@ -3267,7 +3314,7 @@ __device__ __noinline__ Slot* dyn_slot(Tx& t, const DAction& a, bool create) {
 }
 
 // setvar [upstream internal/actions/setvar.go]
-__device__ __forceinline__ void run_setvar(Tx& t, const DAction& a) {
+GI_HD __forceinline__ void run_setvar(Tx& t, const DAction& a) {
   Slot* slp = a.slot >= 0 ? &slot_wr(t, (uint32_t)a.slot) : dyn_slot(t, a, a.kind == A_SETVAR);
   if (!slp) return;
   Slot& sl = *slp;
@@ -3358,14 +3405,14 @@ generic:
   sl.n = v.n;
 }
 
-__device__ __forceinline__ void run_actions(Tx& t, const DRule& R) {
+GI_HD __forceinline__ void run_actions(Tx& t, const DRule& R) {
   const DProgram& P = *t.P;
-  const uint64_t c0 = t.profon ? clock64() : 0;
+  const uint64_t c0 = t.profon ? gi_clock() : 0;
   struct ProfEnd {
     Tx& t;
     uint64_t c0;
-    __device__ ~ProfEnd() {
-      if (t.profon) t.prof_act_cyc += clock64() - c0;
+    GI_HD ~ProfEnd() {
+      if (t.profon) t.prof_act_cyc += gi_clock() - c0;
     }
   } prof_end{t, c0};
   for (uint32_t k = 0; k < R.act_count; k++) {
@@ -3416,7 +3463,7 @@ __device__ __forceinline__ void run_actions(Tx& t, const DRule& R) {
 // ------------------------------------------------------------- operators
 // Go net.ParseIP (compile.cpp go_parse_ip) + IP.To4: *n = 4 (IPv4, or an
 // IPv4-mapped IPv6 address) or 16.
-__device__ bool dev_parse_ipv4(const uint8_t* s, uint32_t len, uint8_t* out) {
+GI_HD bool dev_parse_ipv4(const uint8_t* s, uint32_t len, uint8_t* out) {
   uint32_t i = 0;
   for (int f = 0; f < 4; f++) {
     if (f) {
@@ -3431,7 +3478,7 @@ __device__ bool dev_parse_ipv4(const uint8_t* s, uint32_t len, uint8_t* out) {
   }
   return i == len;
 }
-__device__ bool dev_parse_ip(const uint8_t* s, uint32_t len, uint8_t* out, uint32_t* n) {
+GI_HD bool dev_parse_ip(const uint8_t* s, uint32_t len, uint8_t* out, uint32_t* n) {
   bool colon = false;
   for (uint32_t i = 0; i < len; i++) {
     if (s[i] == ':') colon = true;
@@ -3499,7 +3546,7 @@ __device__ bool dev_parse_ip(const uint8_t* s, uint32_t len, uint8_t* out, uint3
 }
 
 // coraza ipmatch.go Evaluate: net.ParseIP(value), then IPNet.Contains per network.
-__device__ bool ip_match(const uint8_t* recs, uint32_t rlen, const uint8_t* s, uint32_t n) {
+GI_HD bool ip_match(const uint8_t* recs, uint32_t rlen, const uint8_t* s, uint32_t n) {
   uint8_t ip[16];
   uint32_t fam;
   if (!dev_parse_ip(s, n, ip, &fam)) return false;
@@ -3519,7 +3566,7 @@ __device__ bool ip_match(const uint8_t* recs, uint32_t rlen, const uint8_t* s, u
   return false;
 }
 
-__device__ bool contains_word(const uint8_t* v, uint32_t vn, const uint8_t* w, uint32_t wn) {
+GI_HD bool contains_word(const uint8_t* v, uint32_t vn, const uint8_t* w, uint32_t wn) {
   if (wn == 0) return true;
   for (uint32_t i = 0; i + wn <= vn; i++) {
     uint32_t k = 0;
@@ -3537,7 +3584,7 @@ __device__ bool contains_word(const uint8_t* v, uint32_t vn, const uint8_t* w, u
 // compiler keeps REQUEST_BODY detect links out of k_body), so the kernel does
 // not link libinjection and keeps its register budget.
 template <bool DETECT = true>
-__device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, uint32_t n) {
+GI_HD __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, uint32_t n) {
   const DProgram& P = *t.P;
   bool res = false;
   switch (o.kind) {
@@ -3560,8 +3607,13 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
         // the tokenizer state of this lane in LDS (k_eval's 128-thread blocks;
         // k_eval_wave's lanes run identical copies): every state access is an
         // LDS access instead of a round trip to the request's HBM scratch
+#if defined(__HIP_DEVICE_COMPILE__)
         __shared__ LiSqli li_st[128];
         res = li_detect_sqli(s, n, &li_st[threadIdx.x & 127u], li_tables_const());
+#else
+        LiSqli li_st;  // the host interpreter: a stack copy
+        res = li_detect_sqli(s, n, &li_st, li_tables_const());
+#endif
       }
       break;
     case OP_DETECT_XSS:  // detect_xss.go: libinjection.IsXSS
@@ -3637,10 +3689,10 @@ __device__ __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, u
 // slot with neither key cannot match the link.  Keys need slot < 65535 and
 // vix < 32768; a request with a key outside that range, or whose table fills,
 // gets the overflow word set and k_eval re-evaluates as without the set.
-__device__ __forceinline__ uint32_t hset_key(uint32_t slot, uint32_t vix, uint32_t maybe) {
+GI_HD __forceinline__ uint32_t hset_key(uint32_t slot, uint32_t vix, uint32_t maybe) {
   return ((slot + 1u) << 16) | (vix << 1) | maybe;
 }
-__device__ __forceinline__ uint32_t hset_hash(uint32_t k) {
+GI_HD __forceinline__ uint32_t hset_hash(uint32_t k) {
   k ^= k >> 15;
   k *= 0x2C1B3C6Du;
   k ^= k >> 12;
@@ -3662,7 +3714,7 @@ __device__ __noinline__ void hset_insert(const DBatch& B, const ReqLayout& L, ui
   tab[0] = 1u;  // full
 }
 // k_eval: 0 = no key, 1 = exact match, 2 = maybe (evaluate the value)
-__device__ __forceinline__ uint32_t hset_lookup(const uint32_t* tab, uint32_t mask, uint32_t slot, uint32_t vix) {
+GI_HD __forceinline__ uint32_t hset_lookup(const uint32_t* tab, uint32_t mask, uint32_t slot, uint32_t vix) {
   uint32_t res = 0;
   for (uint32_t m = 0; m < 2 && !res; m++) {
     const uint32_t key = hset_key(slot, vix, m);
@@ -3698,7 +3750,7 @@ static_assert(sizeof(CapHdr) == 4 * GI_CAPWS_HDR, "CapHdr layout");
 // 0..8 -> TX.0..TX.8 (transaction.go CaptureField: TX SetIndex(strconv.Itoa(i)),
 // unset groups ""), each value copied into its group's buffer; one capture
 // record per group.  Returns GI_REQ_OVERFLOW when the value does not fit.
-__device__ __noinline__ uint32_t run_capture(const DProgram& P, uint32_t* capws, uint8_t* capbuf, uint32_t cap_t,
+GI_HD __noinline__ uint32_t run_capture(const DProgram& P, uint32_t* capws, uint8_t* capbuf, uint32_t cap_t,
                                              Slot* slots, uint32_t n_req, uint32_t rule_id, int32_t pike,
                                              const uint8_t* v, uint32_t n) {
   const DPike pk = P.pikes[pike];
@@ -3739,7 +3791,7 @@ __device__ __noinline__ uint32_t run_capture(const DProgram& P, uint32_t* capws,
 
 // ------------------------------------------------------------ evaluation
 // Apply the rule's transformation chain; returns the value to test.
-__device__ __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uint32_t vn, bool* ok,
+GI_HD __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uint32_t vn, bool* ok,
                                        uint32_t kmax = 0xffffffffu) {
   const DProgram& P = *t.P;
   Str cur{v, vn};
@@ -3765,7 +3817,7 @@ __device__ __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v
 // ctl:ruleRemoveTargetById: the link's rule id removed variable `var`
 // entries with key k (coraza rule.go doEvaluate adds them to the variable's
 // exceptions: compared with the lowercased key; a single's key is "")
-__device__ __noinline__ bool target_removed_in(const Tx::RmTarget* rt, uint32_t n, const uint8_t* strpool, int32_t id,
+GI_HD __noinline__ bool target_removed_in(const Tx::RmTarget* rt, uint32_t n, const uint8_t* strpool, int32_t id,
                                                uint32_t var, const uint8_t* k, uint32_t kn) {
   for (uint32_t e = 0; e < n; e++) {
     const Tx::RmTarget x = rt[e];
@@ -3775,7 +3827,7 @@ __device__ __noinline__ bool target_removed_in(const Tx::RmTarget* rt, uint32_t 
 }
 #define target_removed(t, id, var, k, kn) target_removed_in((t).rtgt, (t).nrtgt, (t).P->strpool, (id), (var), (k), (kn))
 
-__device__ __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
+GI_HD __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
   const DProgram& P = *t.P;
   for (uint32_t e = 0; e < vr.exc_count; e++) {
     const DExc x = P.excs[vr.exc_begin + e];
@@ -3788,7 +3840,7 @@ __device__ __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uin
   return false;
 }
 
-__device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
+GI_HD inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
   *names = false;
   switch (var) {
     case V_ARGS_GET: return kind == FK_ARG_GET;
@@ -3812,7 +3864,7 @@ __device__ inline bool field_in(uint8_t var, uint32_t kind, bool* names) {
 
 // The field kinds a collection reads (field_in), as the range [*lo, *hi]
 // (empty: *lo > *hi).  Every collection's kinds are contiguous.
-__device__ __forceinline__ void var_kinds(uint8_t var, uint32_t* lo, uint32_t* hi) {
+GI_HD __forceinline__ void var_kinds(uint8_t var, uint32_t* lo, uint32_t* hi) {
   uint32_t a = 1, b = 0;
   switch (var) {
     case V_ARGS_GET: case V_ARGS_GET_NAMES: a = b = FK_ARG_GET; break;
@@ -3836,7 +3888,7 @@ __device__ __forceinline__ void var_kinds(uint8_t var, uint32_t* lo, uint32_t* h
 // of all fields would: ARGS' two kinds are GET args, then POST args, and every
 // GET arg precedes every POST arg).  Rebuilt when a body parse adds fields;
 // an arena without room leaves kx null (scan every field).
-__device__ __noinline__ const uint32_t* build_kindex(const Field* fields, uint32_t nf, uint8_t* bytes, uint32_t* nb,
+GI_HD __noinline__ const uint32_t* build_kindex(const Field* fields, uint32_t nf, uint8_t* bytes, uint32_t* nb,
                                                     uint32_t cap_b) {
   const uint32_t pad = (4u - (uint32_t)((uintptr_t)(bytes + *nb) & 3u)) & 3u;
   if ((uint64_t)*nb + pad + 4ull * (12ull + nf) > cap_b) return nullptr;
@@ -3861,7 +3913,7 @@ __device__ __noinline__ const uint32_t* build_kindex(const Field* fields, uint32
 // exact (non-multiMatch links): phase A proved the transformed value matches
 // (k_eval's hit set): the operator does not run again, and the chain runs
 // only when the matched-variable state needs the transformed value.
-__device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn,
+GI_HD __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, const uint8_t* v, uint32_t vn,
                                                uint32_t var, const uint8_t* key, uint32_t kn, bool exact = false) {
   uint32_t nm = 0;
   const uint8_t* cp = v;  // current candidate
@@ -3917,7 +3969,7 @@ __device__ __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp&
 
 // Hit slot s is set only by per-value phase-A evaluation (each such hit also
 // marks its value in the value map): not an always-slot.
-__device__ __forceinline__ bool slot_vexact(const DProgram& P, uint32_t s) {
+GI_HD __forceinline__ bool slot_vexact(const DProgram& P, uint32_t s) {
   for (uint32_t k = 0; k < P.n_always; k++)
     if (P.always_slots[k] == s) return false;
   return true;
@@ -3931,7 +3983,7 @@ __device__ __forceinline__ bool slot_vexact(const DProgram& P, uint32_t s) {
 // without a value); with the exact hit set, a value with a set bit is
 // decided by its key (exact key: a match; maybe key: evaluate; no key: no
 // match).  *names: the key side is tested.
-__device__ __forceinline__ uint32_t field_filter(Tx& t, const DRule& R, const DVarRef& vr, uint32_t f, bool vskip,
+GI_HD __forceinline__ uint32_t field_filter(Tx& t, const DRule& R, const DVarRef& vr, uint32_t f, bool vskip,
                                                  bool vexact, bool* names) {
   const DProgram& P = *t.P;
   const Field fl = t.fields[f];
@@ -3961,7 +4013,7 @@ __device__ __forceinline__ uint32_t field_filter(Tx& t, const DRule& R, const DV
 // (the request's whole wave runs the interpreter uniformly; collection
 // fields are filtered 64 at a time).
 template <bool W>
-__device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
+GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   const DProgram& P = *t.P;
   // a folded constant link (compile.cpp fold_program): the values of the TX
   // slots it reads are the same for every request that reaches it, so it
@@ -4083,6 +4135,10 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
                      : o.kind == OP_LE ? b <= a : b < a;
           if (o.negate) res = !res;
           if (res) {
+            if (t.mv) {  // the matched-variable state, as test_value records it
+              uint8_t vb[24];
+              if (!mv_record(t.mv, V_TX, nm, nn, vb, go_itoa(sl.num, vb))) t.flags |= GI_REQ_OVERFLOW;
+            }
             run_actions(t, R);
             nmatch++;
           }
@@ -4149,7 +4205,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         j = je;
       }
     }
-    if (!W) {
+    if constexpr (!W) {
       for (; j < je; j++) {
         const uint32_t f = t.kx ? t.kx[12 + j] : j;
         bool names;
@@ -4169,7 +4225,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
       // Coraza's per-value order)
       const uint32_t lane = threadIdx.x & 63u;
       for (; j < je; j += 64) {
-        const uint64_t c0 = t.profon ? clock64() : 0;
+        const uint64_t c0 = t.profon ? gi_clock() : 0;
         uint32_t f = 0, hres = 0;
         bool names = false;
         if (j + lane < je) {
@@ -4183,13 +4239,13 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
           atomicAdd(&pf[17], (unsigned long long)min(64u, je - j));
           atomicAdd(&pf[18], (unsigned long long)__popcll(mx));
           atomicAdd(&pf[19], (unsigned long long)__popcll(m & ~mx));
-          atomicAdd(&pf[20], (unsigned long long)(clock64() - c0));
+          atomicAdd(&pf[20], (unsigned long long)(gi_clock() - c0));
         }
         if (vr.count) {
           cnt += (uint32_t)__popcll(m);
           continue;
         }
-        const uint64_t c1 = t.profon ? clock64() : 0;
+        const uint64_t c1 = t.profon ? gi_clock() : 0;
         while (m) {
           const int b = __ffsll((unsigned long long)m) - 1;
           m &= m - 1;
@@ -4199,7 +4255,7 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
           const Field fl = t.fields[fb];
           nmatch += test_value(t, R, o, nb ? fl.k : fl.v, nb ? fl.kn : fl.vn, vr.var, fl.k, fl.kn, hb == 1);
         }
-        if (t.profon) atomicAdd(&t.prof_rule_cyc[-128 + 21], (unsigned long long)(clock64() - c1));
+        if (t.profon) gi_prof_add(&t.prof_rule_cyc[-128 + 21], (unsigned long long)(gi_clock() - c1));
       }
     }
     if (vr.count) {
@@ -4212,20 +4268,21 @@ __device__ __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
 }
 
 template <bool W>
-__device__ __forceinline__ void eval_top(Tx& t, uint32_t ri) {
+GI_HD __forceinline__ void eval_top(Tx& t, uint32_t ri) {
   const DProgram& P = *t.P;
   const DRule R = gi_cload(P.rules, ri);
   // the rule and its chain links; all must match (one eval_rule call site)
   t.prof_evals++;
   t.cur_id = (uint32_t)R.id;
+  if (t.mv) t.mv->keep = R.flags2 & RF2_MVS;
   for (int32_t ci = (int32_t)ri; ci >= 0;) {
     const DRule C = gi_cload(P.rules, (uint64_t)ci);
-    const uint64_t c0 = t.profon ? clock64() : 0;
+    const uint64_t c0 = t.profon ? gi_clock() : 0;
     const uint32_t nm = eval_rule<W>(t, C);
     if (t.profon) {
-      const uint64_t dc = clock64() - c0;
+      const uint64_t dc = gi_clock() - c0;
       t.prof_eval_cyc += dc;
-      if (ci < 1000) atomicAdd(&t.prof_rule_cyc[ci], (unsigned long long)dc);
+      if (ci < 1000) gi_prof_add(&t.prof_rule_cyc[ci], (unsigned long long)dc);
     }
     if (nm == 0) return;
     ci = C.chain_next;
@@ -4254,7 +4311,7 @@ __device__ __forceinline__ void eval_top(Tx& t, uint32_t ri) {
 // pending, every rule but the target marker.  (Used by k_eval_wave to jump
 // over runs of such rules 64 at a time; MATCHED_VARS is reset before every
 // evaluated rule, so skipping the resets of no-op rules changes nothing.)
-__device__ __forceinline__ bool rule_noop(Tx& t, const DRule& R) {
+GI_HD __forceinline__ bool rule_noop(Tx& t, const DRule& R) {
   if (R.id != 0 && t.nremoved) {
     for (uint32_t j = 0; j < t.nremoved; j++)
       if (t.removed[j][0] <= R.id && R.id <= t.removed[j][1]) return true;
@@ -4268,7 +4325,7 @@ __device__ __forceinline__ bool rule_noop(Tx& t, const DRule& R) {
 
 // RuleGroup.Eval [upstream corazawaf/rulegroup.go]
 template <bool W>
-__device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
+GI_HD __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
   const DProgram& P = *t.P;
   if (t.engine == ENGINE_OFF) return;
   t.phase = phase;
@@ -4286,20 +4343,22 @@ __device__ __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
   for (uint32_t k = k0; k < kend; k++) {
     if (t.interrupted) break;
     if (t.flags & GI_REQ_ERROR_MASK) break;
-    if (W && t.skip == 0) {
-      // the lanes test the next 64 rules; jump to the first that is not a no-op
-      const uint32_t kk = k + (threadIdx.x & 63u);
-      bool need = false;
-      if (kk < kend) {
-        const DRule Rl = P.rules[GI_CONST(uint32_t, P.top)[kk]];
-        need = !rule_noop(t, Rl);
+    if constexpr (W) {
+      if (t.skip == 0) {
+        // the lanes test the next 64 rules; jump to the first that is not a no-op
+        const uint32_t kk = k + (threadIdx.x & 63u);
+        bool need = false;
+        if (kk < kend) {
+          const DRule Rl = P.rules[GI_CONST(uint32_t, P.top)[kk]];
+          need = !rule_noop(t, Rl);
+        }
+        const uint64_t m = __ballot(need);
+        if (!m) {
+          k += 63;
+          continue;
+        }
+        k += (uint32_t)(__ffsll((unsigned long long)m) - 1);
       }
-      const uint64_t m = __ballot(need);
-      if (!m) {
-        k += 63;
-        continue;
-      }
-      k += (uint32_t)(__ffsll((unsigned long long)m) - 1);
     }
     const uint32_t ri = GI_CONST(uint32_t, P.top)[k];
     const DRule R = gi_cload(P.rules, ri);
@@ -4377,7 +4436,7 @@ struct Region {
   uint32_t cap_f, cap_b, cap_t, cap_mt;
 };
 
-__device__ inline Region region_of(const DProgram& P, const DBatch& B, uint32_t r) {
+GI_HD inline Region region_of(const DProgram& P, const DBatch& B, uint32_t r) {
   const ReqLayout L = B.layout[r];
   uint8_t* base = B.scratch + L.base;
   Region g;
@@ -4414,7 +4473,7 @@ __device__ inline Region region_of(const DProgram& P, const DBatch& B, uint32_t 
   return g;
 }
 
-__device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
+GI_HD inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
   t.P = &P;
   t.fields = g.fields;
   t.cap_f = g.cap_f;
@@ -4437,7 +4496,7 @@ __device__ inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
   t.dyn = g.dyn;
 }
 
-__device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
+GI_HD inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
   if (kind == OP_VALIDATE_BYTE_RANGE) {
     for (uint32_t i = 0; i < n; i++)
       if (!((bits[s[i] >> 5] >> (s[i] & 31)) & 1)) return true;
@@ -4467,7 +4526,7 @@ __device__ inline bool validate_op(uint8_t kind, const uint32_t* bits, const uin
 // Debug builds (-DGI_DEBUG): bounds violations are recorded in B.dbg
 // ([0] first source line, [1] count, [2..3] operands) and the access skipped.
 #ifdef GI_DEBUG
-__device__ __noinline__ void gi_dbg_fail(const DBatch& B, uint32_t line, uint64_t a, uint64_t b) {
+GI_HD __noinline__ void gi_dbg_fail(const DBatch& B, uint32_t line, uint64_t a, uint64_t b) {
   if (!B.dbg) return;
   if (atomicCAS(&B.dbg[0], 0u, line) == 0u) {
     B.dbg[2] = (uint32_t)a;
@@ -4499,7 +4558,7 @@ __device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
 #define GI_VOID_SLOW 2
 #define GI_VOID_QCAP 3
 #define GI_VOID_POOL 4
-__device__ __forceinline__ void void_request(const DBatch& B, uint32_t r, uint32_t cause) {
+GI_HD __forceinline__ void void_request(const DBatch& B, uint32_t r, uint32_t cause) {
   ReqHdr* H = (ReqHdr*)(B.scratch + B.layout[r].base);
   H->pa_void = 1;
   atomicAdd(&B.vcause[cause], 1ull);
@@ -4511,7 +4570,7 @@ __device__ __forceinline__ void void_request(const DBatch& B, uint32_t r, uint32
 #define GI_QB_SHARED 0x80000000u
 #define GI_QB_HDR 2  // lane header words of a queue block: global item index, value length
 #define GI_QB_NW_MASK 0x7FFFFFu
-__device__ __forceinline__ uint32_t item_bucket(uint32_t n) {
+GI_HD __forceinline__ uint32_t item_bucket(uint32_t n) {
   return n <= 16 ? 0u : n <= 32 ? 1u : n <= 64 ? 2u : n <= 128 ? 3u : 4u;
 }
 // Item classes: k_items orders the items of each bucket by (source group,
@@ -4550,13 +4609,13 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t* total) {
   return inc - x;
 }
 
-__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+GI_HD __forceinline__ uint32_t wave_max(uint32_t x) {
   for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
   return x;
 }
 
 // Sum over the wave's 64 lanes (every lane gets it).
-__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
+GI_HD __forceinline__ uint64_t wave_sum(uint64_t x) {
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, o, 64);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), o, 64);
@@ -4568,7 +4627,7 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 // Visits the items of one request: singles some filter reads, then the
 // (value, key) sides of every field kind some filter reads.
 template <class F>
-__device__ __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H, const Field* Fd, F&& f) {
+GI_HD __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H, const Field* Fd, F&& f) {
   for (uint32_t m = P.item_singles; m; m &= m - 1) {
     const uint32_t sg = __ffs(m) - 1;
     f((uint8_t)0, (uint8_t)sg, 0u, (uint32_t)0xFFFFFFFFu, H->single[sg].n);
@@ -4589,7 +4648,7 @@ __device__ __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H
 // ------------------------------------------------ stage 1: k_collect
 // ProcessURI + AddRequestHeader* for one request per thread.  Fields are
 // grouped by kind so each scan group walks only its own range.
-__device__ void collect_request(const DProgram& P, const DBatch& B, uint32_t r) {
+GI_HD void collect_request(const DProgram& P, const DBatch& B, uint32_t r) {
   const gi_request rq = B.reqs[r];
   Region g = region_of(P, B, r);
   Tx t;
@@ -4689,7 +4748,7 @@ __device__ void collect_request(const DProgram& P, const DBatch& B, uint32_t r) 
 }
 
 // The first Content-Type request header's value (coraza ProcessRequestBody's mime)
-__device__ inline Str first_content_type(const DBatch& B, const gi_request& rq) {
+GI_HD inline Str first_content_type(const DBatch& B, const gi_request& rq) {
   for (uint32_t h = 0; h < rq.hdr_count; h++) {
     const gi_header hd = B.headers[rq.hdr_begin + h];
     if (hd.name.len == 12 && eq_ascii_ci(B.data + hd.name.off, 12, (const uint8_t*)"content-type", 12))
@@ -4698,7 +4757,7 @@ __device__ inline Str first_content_type(const DBatch& B, const gi_request& rq) 
   return {CS_ZERO, 0};
 }
 
-__device__ inline Str mp_err_msg(uint8_t e) {
+GI_HD inline Str mp_err_msg(uint8_t e) {
   const uint8_t* m = (const uint8_t*)kMpErrMsg[e];
   uint32_t k = 0;
   while (m[k]) k++;
@@ -5440,9 +5499,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
   uint64_t pc_vals = 0, pc_det = 0;
   uint64_t wwords = 0;  // queue words this wave wrote (algorithmic-byte accounting)
   uint64_t csteps = 0;  // value bytes this lane fed into a stream's chain (secondary roofline)
-  const uint64_t pc_start = B.prof ? clock64() : 0;
+  const uint64_t pc_start = B.prof ? gi_clock() : 0;
   for (uint32_t w0 = blockIdx.x * 64; w0 < cnt; w0 += gridDim.x * 64) {
-    const uint64_t c_a = B.prof ? clock64() : 0;
+    const uint64_t c_a = B.prof ? gi_clock() : 0;
     const uint32_t ii = w0 + lane;
     for (uint32_t m = 0; m < M; m++) memo[m * 64].key = 0;  // a new item: nothing memoised
     Item it{};
@@ -5464,7 +5523,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
       summ = value_summary_lut(sumlut, src, it.vn);
     }
     const uint32_t blk = iw_base + w0 / 64;
-    const uint64_t c_b = B.prof ? clock64() : 0;
+    const uint64_t c_b = B.prof ? gi_clock() : 0;
     pc_item += c_b - c_a;
     // Blocks whose every value left its chain unchanged hold the raw item
     // bytes: a later stream with the same lane set points its qblk entry at
@@ -5477,7 +5536,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
     // a long value (>= GI_LONG_MIN bytes) takes k_long: one wave per (item, stream), no queue block
     const bool is_long = IN == 0 && B.long_cap && ii < cnt && it.vn >= GI_LONG_MIN;
     for (uint32_t s = 0; s < P.n_streams; s++) {
-      const uint64_t c_s0 = B.prof ? clock64() : 0;
+      const uint64_t c_s0 = B.prof ? gi_clock() : 0;
       const DStream S = gi_cload(P.streams, s);
       const uint64_t fm0 = gm & S.gmask;
       if (is_long && fm0) {
@@ -5490,7 +5549,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
         if (lane == 0 && S.job_count && blk < B.qcap) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2(0u, 0u);
         continue;
       }
-      const uint64_t c_sa = B.prof ? clock64() : 0;
+      const uint64_t c_sa = B.prof ? gi_clock() : 0;
       pc_fm += c_sa - c_s0;
       const uint8_t* cur = nullptr;
       int64_t cn = 0;
@@ -5501,7 +5560,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
         csteps += it.vn;
         if (M) cn = run_chain_memo<M, WT>(P, S, src, it.vn, summ, mslots, memo, &victim, b0, b1, &cur, sumlut, &osum);
         else cn = run_chain<IN != 0>(P, S, src, it.vn, summ, b0, b1, cap, &cur, sumlut, &osum);
-        if (B.prof) pc_run += clock64() - c_sa;
+        if (B.prof) pc_run += gi_clock() - c_sa;
         if (cn < 0 && IN) {
           cn = run_chain<false>(P, S, src, it.vn, summ, g0, g1, B.lcap, &cur, sumlut, &osum);
           glob = true;
@@ -5511,16 +5570,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
           cur = src;
           cn = 0;
         }
-        const uint64_t c_v0 = B.prof ? clock64() : 0;
+        const uint64_t c_v0 = B.prof ? gi_clock() : 0;
         if (S.val_count)
           stream_vals(P, B, it.req, meta_vix(it.meta), S, fm, maybe, cur, (uint32_t)cn, osum, !maybe && cur == src,
                       &rawmask, &det_append);
-        if (B.prof) pc_vals += clock64() - c_v0;
+        if (B.prof) pc_vals += gi_clock() - c_v0;
       }
-      const uint64_t c_d0 = B.prof ? clock64() : 0;
+      const uint64_t c_d0 = B.prof ? gi_clock() : 0;
       if (S.val_count) det_push(P, B, det_append, it.req, meta_vix(it.meta), gm, 1u << S.det_id, cur, (uint32_t)cn);
-      if (B.prof) pc_det += clock64() - c_d0;
-      const uint64_t c_s1 = B.prof ? clock64() : 0;
+      if (B.prof) pc_det += gi_clock() - c_d0;
+      const uint64_t c_s1 = B.prof ? gi_clock() : 0;
       pc_chain += c_s1 - c_s0;
       if (!S.job_count) continue;
       bool slow = maybe;
@@ -5557,7 +5616,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
           ((SlowEnt*)B.slow)[k] = e;
         }
       }
-      const uint64_t c_s2 = B.prof ? clock64() : 0;
+      const uint64_t c_s2 = B.prof ? gi_clock() : 0;
       pc_slow += c_s2 - c_s1;
       const bool out = fm && !slow;
       const uint64_t om = __ballot(out);
@@ -5622,26 +5681,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
           }
         }
       }
-      if (B.prof) pc_out += clock64() - c_s2;
+      if (B.prof) pc_out += gi_clock() - c_s2;
     }
     det_push(P, B, rawmask != 0, it.req, meta_vix(it.meta), gm, rawmask, src, it.vn);
-    if (B.prof) pc_loop += clock64() - c_b;
+    if (B.prof) pc_loop += gi_clock() - c_b;
   }
   if (lane == 0 && wwords) atomicAdd(&B.acct[5 + bucket], (unsigned long long)wwords);
   csteps = wave_sum(csteps);
   if (lane == 0 && csteps) atomicAdd(&B.acct2[bucket], (unsigned long long)csteps);
   if (B.prof && lane == 0) {
-    pc_tot = clock64() - pc_start;
-    atomicAdd(&B.prof[40 + 5 * bucket + 0], (unsigned long long)pc_item);
-    atomicAdd(&B.prof[40 + 5 * bucket + 1], (unsigned long long)pc_chain);
-    atomicAdd(&B.prof[40 + 5 * bucket + 2], (unsigned long long)pc_out);
-    atomicAdd(&B.prof[40 + 5 * bucket + 3], (unsigned long long)pc_loop);
-    atomicAdd(&B.prof[40 + 5 * bucket + 4], (unsigned long long)pc_tot);
-    atomicAdd(&B.prof[80 + 3 * bucket + 0], (unsigned long long)pc_fm);
-    atomicAdd(&B.prof[80 + 3 * bucket + 1], (unsigned long long)pc_run);
-    atomicAdd(&B.prof[80 + 3 * bucket + 2], (unsigned long long)pc_slow);
-    atomicAdd(&B.prof[24 + 2 * bucket], (unsigned long long)pc_vals);
-    atomicAdd(&B.prof[25 + 2 * bucket], (unsigned long long)pc_det);
+    pc_tot = gi_clock() - pc_start;
+    gi_prof_add(&B.prof[40 + 5 * bucket + 0], (unsigned long long)pc_item);
+    gi_prof_add(&B.prof[40 + 5 * bucket + 1], (unsigned long long)pc_chain);
+    gi_prof_add(&B.prof[40 + 5 * bucket + 2], (unsigned long long)pc_out);
+    gi_prof_add(&B.prof[40 + 5 * bucket + 3], (unsigned long long)pc_loop);
+    gi_prof_add(&B.prof[40 + 5 * bucket + 4], (unsigned long long)pc_tot);
+    gi_prof_add(&B.prof[80 + 3 * bucket + 0], (unsigned long long)pc_fm);
+    gi_prof_add(&B.prof[80 + 3 * bucket + 1], (unsigned long long)pc_run);
+    gi_prof_add(&B.prof[80 + 3 * bucket + 2], (unsigned long long)pc_slow);
+    gi_prof_add(&B.prof[24 + 2 * bucket], (unsigned long long)pc_vals);
+    gi_prof_add(&B.prof[25 + 2 * bucket], (unsigned long long)pc_det);
   }
 }
 
@@ -6193,7 +6252,7 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
     for (uint32_t k = 0; k < P.n_body_links; k++) {
       const DRule R = gi_cload(P.rules, (uint64_t)P.body_links[k]);
       const DOp o = gi_cload(P.ops, (uint64_t)R.op);
-      const uint64_t c0 = B.prof ? clock64() : 0;
+      const uint64_t c0 = B.prof ? gi_clock() : 0;
       bool same = R.tchain_len == prev_len;
       for (uint32_t q = 0; same && q < R.tchain_len; q++)
         same = P.tchains[R.tchain_off + q] == P.tchains[prev_off + q];
@@ -6213,7 +6272,7 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
         }
         ok = wave_run_chain(P, R.tchain_off, R.tchain_len, body, g.t0, g.t1, g.cap_t, summ, &cur, &cn);
       }
-      const uint64_t c1 = B.prof ? clock64() : 0;
+      const uint64_t c1 = B.prof ? gi_clock() : 0;
       bool hit;
       if (!ok) {
         hit = true;  // chain overflow: maybe
@@ -6241,8 +6300,8 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
       }
       if (hit && L == 0) set_hit(B, (uint32_t)R.hit_slot, r);
       if (B.prof && k < 16 && L == 0) {  // GI_PROF: cycles per link (transform, operator), per body
-        atomicAdd(&B.prof[96 + 2 * k], (unsigned long long)(c1 - c0));
-        atomicAdd(&B.prof[97 + 2 * k], (unsigned long long)(clock64() - c1));
+        gi_prof_add(&B.prof[96 + 2 * k], (unsigned long long)(c1 - c0));
+        gi_prof_add(&B.prof[97 + 2 * k], (unsigned long long)(gi_clock() - c1));
       }
     }
   }
@@ -6428,16 +6487,16 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
 // request's whole wave runs it uniformly, whits = the request's hit words in
 // LDS (nullptr: read from HBM).
 template <bool W>
-__device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B, uint32_t r, const uint32_t* whits,
+GI_HD __forceinline__ void eval_request(const DProgram& P, const DBatch& B, uint32_t r, const uint32_t* whits,
                                              uint32_t wstride, unsigned long long* my) {
-  const uint64_t c_start = B.prof ? clock64() : 0;
+  const uint64_t c_start = B.prof ? gi_clock() : 0;
   const gi_request rq = B.reqs[r];
   Region g = region_of(P, B, r);
   ReqHdr* H = g.hdr;
   Tx t;
   t.prof_visits = t.prof_evals = t.prof_rules = 0;
   t.prof_eval_cyc = t.prof_act_cyc = 0;
-  const bool lead = !W || (threadIdx.x & 63u) == 0;  // the lane that writes shared counters
+  const bool lead = !W || (gi_tid() & 63u) == 0;  // the lane that writes shared counters
   t.profon = B.prof != nullptr && lead;
   t.prof_rule_cyc = B.prof ? B.prof + 128 : nullptr;
   tx_bind(t, P, g);
@@ -6508,9 +6567,11 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
     *(DynHdr*)t.dyn = DynHdr{0u, Lr.dyn_cap, 0u, Lr.dyn_capb};
   }
   if (t.mv) {
+    const ReqLayout Lm = B.layout[r];
     t.mv->n = t.mv->nb = 0;
-    t.mv->cap_e = g.cap_f + 16;
-    t.mv->cap_a = g.cap_b + g.cap_mt;
+    t.mv->keep = 0;
+    t.mv->cap_e = Lm.mv_cap_e;
+    t.mv->cap_a = Lm.mv_cap_a;
     t.mv->cap_v = g.cap_t;
     t.mv->cap_n = g.cap_mt;
     t.mv->cur_vn = t.mv->cur_nn = 0;
@@ -6522,7 +6583,7 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
     scanned += hd.name.len + hd.value.len;
   }
   t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
-  const uint64_t c_init = B.prof ? clock64() : 0;
+  const uint64_t c_init = B.prof ? gi_clock() : 0;
   // phase 1, ProcessRequestBody, phase 2 (one eval_phase call site)
   for (uint8_t ph = 1; ph <= 2 && !(t.flags & GI_REQ_ERROR_MASK); ph++) {
     if (ph == 2) {
@@ -6644,18 +6705,18 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
       }
       if ((t.flags & GI_REQ_ERROR_MASK) || !run2) break;
     }
-    const uint64_t c0 = B.prof ? clock64() : 0;
+    const uint64_t c0 = B.prof ? gi_clock() : 0;
     eval_phase<W>(t, ph);
-    if (B.prof && lead) atomicAdd(&B.prof[ph], (unsigned long long)(clock64() - c0));
+    if (B.prof && lead) gi_prof_add(&B.prof[ph], (unsigned long long)(gi_clock() - c0));
   }
   if (B.prof && lead) {
-    atomicAdd(&B.prof[0], (unsigned long long)(c_init - c_start));
-    atomicAdd(&B.prof[3], (unsigned long long)(clock64() - c_start));
-    atomicAdd(&B.prof[4], (unsigned long long)t.prof_visits);
-    atomicAdd(&B.prof[5], (unsigned long long)t.prof_evals);
-    atomicAdd(&B.prof[6], (unsigned long long)t.prof_rules);
-    atomicAdd(&B.prof[7], (unsigned long long)t.prof_eval_cyc);
-    atomicAdd(&B.prof[8], (unsigned long long)t.prof_act_cyc);
+    gi_prof_add(&B.prof[0], (unsigned long long)(c_init - c_start));
+    gi_prof_add(&B.prof[3], (unsigned long long)(gi_clock() - c_start));
+    gi_prof_add(&B.prof[4], (unsigned long long)t.prof_visits);
+    gi_prof_add(&B.prof[5], (unsigned long long)t.prof_evals);
+    gi_prof_add(&B.prof[6], (unsigned long long)t.prof_rules);
+    gi_prof_add(&B.prof[7], (unsigned long long)t.prof_eval_cyc);
+    gi_prof_add(&B.prof[8], (unsigned long long)t.prof_act_cyc);
   }
   gi_verdict v;
   v.rule_id = t.interrupted ? t.int_rule : 0;
@@ -6694,7 +6755,7 @@ __device__ __forceinline__ void eval_request(const DProgram& P, const DBatch& B,
 // ARGS_POST, multipart collections) or a large program (rule walks of
 // thousands of rules), where the lanes of one wave split the field loops and
 // the rule walk instead of one lane doing both alone.
-__device__ __forceinline__ bool eval_heavy(const DProgram& P, const DBatch& B, uint32_t r) {
+GI_HD __forceinline__ bool eval_heavy(const DProgram& P, const DBatch& B, uint32_t r) {
   if (!B.wlist) return false;
   if (B.wave_rules && P.top_end[1] - P.top_begin[0] >= B.wave_rules) return true;
   const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
@@ -6758,7 +6819,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_EVAL
 // long prefixes (the CRS initialisation SecActions match every request), so
 // equal bins are first aggregated across the wave (one LDS atomic per distinct
 // bin per step instead of 64 on one address).
-__device__ __forceinline__ void wave_hist_add(uint32_t* hist, int32_t b) {
+GI_HD __forceinline__ void wave_hist_add(uint32_t* hist, int32_t b) {
   uint64_t active = __ballot(b >= 0);
   while (active) {
     const int leader = __ffsll((unsigned long long)active) - 1;
@@ -6856,6 +6917,20 @@ uint32_t scan_resident_blocks(uint32_t lds_bytes) {
       if (e_ != hipSuccess) return;                                                       \
     }                                                                                     \
   } while (0)
+
+// CPU baseline ("the build's own C++ CPU restatement", not
+// Coraza): request 0 of B through the same interpreter, compiled for the
+// host.  ProcessURI / headers / cookies (collect_request), then phase B with
+// phase A void -- every rule link evaluated by the interpreter, the body
+// parsed in phase B -- and the verdict, matched ids and exports in B.
+void cpu_inspect_one(const DProgram& P, const DBatch& B) {
+  collect_request(P, B, 0);
+  ReqHdr* H = (ReqHdr*)(B.scratch + B.layout[0].base);
+  H->spec_proc = BP_NONE;
+  H->pa_void = 1;
+  unsigned long long my[8];
+  eval_request<false>(P, B, 0, nullptr, 0, my);
+}
 
 void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
                      int stop_after, LaunchLog* log, const uint32_t* tally_ids, uint32_t n_tally_ids) {

@@ -56,12 +56,12 @@ struct LiSqli {
   uint32_t _pad[2];  // 200 B = 50 dwords: k_detect's per-lane LDS states hit ~2-way, not 16-way, bank conflicts
 };
 
-__device__ __forceinline__ LiTables li_tables_const() { return LiTables{kLiWords, kLiPool, kLiHash}; }
+GI_HD __forceinline__ LiTables li_tables_const() { return LiTables{kLiWords, kLiPool, kLiHash}; }
 
-__device__ __forceinline__ uint8_t li_up(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
+GI_HD __forceinline__ uint8_t li_up(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
 
 // byte i of the lookup key: a, or a + ' ' + b (syntax_merge_words), upper-cased
-__device__ __forceinline__ uint8_t li_key_at(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t i) {
+GI_HD __forceinline__ uint8_t li_key_at(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t i) {
   if (i < an) return li_up(a[i]);
   if (i == an) return ' ';
   return li_up(b[i - an - 1]);
@@ -70,7 +70,7 @@ __device__ __forceinline__ uint8_t li_key_at(const uint8_t* a, uint32_t an, cons
 // bsearch_keyword_type restated as a hash probe: the index of the word equal
 // to the upper-cased key (a, or a + ' ' + b), -1 if none.  FNV-1a over the
 // upper-cased bytes into an open-addressing table (tools/gen_libinj_tables.py).
-__device__ __forceinline__ int li_find(const LiTables& T, const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn,
+GI_HD __forceinline__ int li_find(const LiTables& T, const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn,
                                     bool two) {
   const uint32_t kn = two ? an + 1 + bn : an;
   if (kn == 0 || kn >= LI_TOKEN_SIZE) return -1;
@@ -91,24 +91,24 @@ __device__ __forceinline__ int li_find(const LiTables& T, const uint8_t* a, uint
     if (eq) return (int)(idx - 1);
   }
 }
-__device__ __forceinline__ uint8_t li_lookup(const LiTables& T, const uint8_t* a, uint32_t an) {
+GI_HD __forceinline__ uint8_t li_lookup(const LiTables& T, const uint8_t* a, uint32_t an) {
   const int i = li_find(T, a, an, nullptr, 0, false);
   return i < 0 ? (uint8_t)0 : (uint8_t)(T.words[i] >> 24);
 }
 
 // cstrcasecmp(lit, tok, tok.len) == 0 (lit upper case, no NUL)
-__device__ __forceinline__ bool li_tok_is(const LiTok& t, const char* lit) {
+GI_HD __forceinline__ bool li_tok_is(const LiTok& t, const char* lit) {
   uint32_t i = 0;
   for (; lit[i]; i++)
     if (i >= t.len || li_up(t.p[i]) != (uint8_t)lit[i]) return false;
   return i == t.len;
 }
 
-__device__ __forceinline__ bool li_white(uint8_t c) {  // char_is_white: " \t\n\v\f\r\240\000"
+GI_HD __forceinline__ bool li_white(uint8_t c) {  // char_is_white: " \t\n\v\f\r\240\000"
   return c == ' ' || (c >= 9 && c <= 13) || c == 0xA0 || c == 0;
 }
 
-__device__ __forceinline__ bool li_word_stop(uint8_t c) {
+GI_HD __forceinline__ bool li_word_stop(uint8_t c) {
   // parse_word's strlencspn set " []{}<>:\\?=@!#~+-*/&|^%(),';\t\n\v\f\r\"\240\000"
   switch (c) {
     case ' ': case '[': case ']': case '{': case '}': case '<': case '>': case ':': case '\\': case '?':
@@ -119,7 +119,7 @@ __device__ __forceinline__ bool li_word_stop(uint8_t c) {
   return false;
 }
 
-__device__ __forceinline__ bool li_var_stop(uint8_t c) {
+GI_HD __forceinline__ bool li_var_stop(uint8_t c) {
   // parse_var's set " <>:\\?=@!#~+-*/&|^%(),';\t\n\v\f\r'`\""
   switch (c) {
     case ' ': case '<': case '>': case ':': case '\\': case '?': case '=': case '@': case '!': case '#':
@@ -130,14 +130,14 @@ __device__ __forceinline__ bool li_var_stop(uint8_t c) {
   return false;
 }
 
-__device__ __forceinline__ bool li_isdigit(uint8_t c) { return c >= '0' && c <= '9'; }
-__device__ __forceinline__ bool li_ishex(uint8_t c) {
+GI_HD __forceinline__ bool li_isdigit(uint8_t c) { return c >= '0' && c <= '9'; }
+GI_HD __forceinline__ bool li_ishex(uint8_t c) {
   return li_isdigit(c) || (c >= 'A' && c <= 'F') || (c >= 'a' && c <= 'f');
 }
 
 // memchr2: first i in [b, e - 1) with s[i] == c0 && s[i + 1] == c1; a c0
 // not followed by c1 skips two bytes, as the C loop does.  -1 if none.
-__device__ int64_t li_memchr2(const uint8_t* s, uint32_t b, uint32_t e, uint8_t c0, uint8_t c1) {
+GI_HD int64_t li_memchr2(const uint8_t* s, uint32_t b, uint32_t e, uint8_t c0, uint8_t c1) {
   if (e < b + 2) return -1;
   uint32_t cur = b;
   const uint32_t last = e - 1;
@@ -152,18 +152,18 @@ __device__ int64_t li_memchr2(const uint8_t* s, uint32_t b, uint32_t e, uint8_t 
   return -1;
 }
 
-__device__ __forceinline__ int64_t li_memchr(const uint8_t* s, uint32_t b, uint32_t e, uint8_t c) {
+GI_HD __forceinline__ int64_t li_memchr(const uint8_t* s, uint32_t b, uint32_t e, uint8_t c) {
   for (uint32_t i = b; i < e; i++)
     if (s[i] == c) return i;
   return -1;
 }
 
-__device__ __forceinline__ void li_assign(LiTok& t, uint8_t type, const uint8_t* p, uint32_t len) {
+GI_HD __forceinline__ void li_assign(LiTok& t, uint8_t type, const uint8_t* p, uint32_t len) {
   t.type = type;
   t.p = p;
   t.len = (uint16_t)(len < LI_TOKEN_SIZE - 1 ? len : LI_TOKEN_SIZE - 1);
 }
-__device__ __forceinline__ void li_clear(LiTok& t) {
+GI_HD __forceinline__ void li_clear(LiTok& t) {
   t.p = nullptr;
   t.len = 0;
   t.type = 0;
@@ -171,7 +171,7 @@ __device__ __forceinline__ void li_clear(LiTok& t) {
 }
 
 // parse_string_core: string at pos (first quote skipped when offset > 0)
-__device__ uint32_t li_string_core(const uint8_t* s, uint32_t slen, uint32_t pos, LiTok& st, uint8_t delim,
+GI_HD uint32_t li_string_core(const uint8_t* s, uint32_t slen, uint32_t pos, LiTok& st, uint8_t delim,
                                    uint32_t offset) {
   const uint32_t start = pos + offset;
   int64_t q = li_memchr(s, start, slen, delim);
@@ -205,7 +205,7 @@ enum : uint8_t {
 };
 
 // char_parse_map
-__device__ __forceinline__ uint8_t li_parser(uint8_t c) {
+GI_HD __forceinline__ uint8_t li_parser(uint8_t c) {
   if (c <= 32 || c == 127 || c == 160) return LP_WHITE;
   if (li_isdigit(c) || c == '.') return LP_NUMBER;
   switch (c) {
@@ -232,7 +232,7 @@ __device__ __forceinline__ uint8_t li_parser(uint8_t c) {
   return LP_WORD;
 }
 
-__device__ __forceinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos) {
+GI_HD __forceinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint8_t* s = S.s;
   uint32_t e = pos;
   while (e < S.slen && !li_word_stop(s[e])) e++;
@@ -256,7 +256,7 @@ __device__ __forceinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t 
   return pos + wlen;
 }
 
-__device__ uint32_t li_parse_eol_comment(LiSqli& S, LiTok& c, uint32_t pos) {
+GI_HD uint32_t li_parse_eol_comment(LiSqli& S, LiTok& c, uint32_t pos) {
   const int64_t e = li_memchr(S.s, pos, S.slen, '\n');
   if (e < 0) {
     li_assign(c, 'c', S.s + pos, S.slen - pos);
@@ -266,7 +266,7 @@ __device__ uint32_t li_parse_eol_comment(LiSqli& S, LiTok& c, uint32_t pos) {
   return (uint32_t)e + 1;
 }
 
-__device__ uint32_t li_parse_qstring_core(LiSqli& S, LiTok& c, uint32_t p0, uint32_t offset) {
+GI_HD uint32_t li_parse_qstring_core(LiSqli& S, LiTok& c, uint32_t p0, uint32_t offset) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen, pos = p0 + offset;
   if (pos >= slen || (s[pos] != 'q' && s[pos] != 'Q') || pos + 2 >= slen || s[pos + 1] != '\'')
@@ -286,19 +286,19 @@ __device__ uint32_t li_parse_qstring_core(LiSqli& S, LiTok& c, uint32_t p0, uint
   return (uint32_t)e + 2;
 }
 
-__device__ uint32_t li_parse_estring(LiSqli& S, LiTok& c, uint32_t pos) {
+GI_HD uint32_t li_parse_estring(LiSqli& S, LiTok& c, uint32_t pos) {
   if (pos + 2 >= S.slen || S.s[pos + 1] != '\'') return li_parse_word(S, c, pos);
   return li_string_core(S.s, S.slen, pos, c, '\'', 2);
 }
 
-__device__ uint32_t li_parse_tick(LiSqli& S, LiTok& c, uint32_t pos) {
+GI_HD uint32_t li_parse_tick(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint32_t np = li_string_core(S.s, S.slen, pos, c, '`', 1);
   const uint8_t ch = li_lookup(S.T, c.p, c.len);
   c.type = ch == 'f' ? 'f' : 'n';
   return np;
 }
 
-__device__ __forceinline__ uint32_t li_parse_money(LiSqli& S, LiTok& c, uint32_t pos) {
+GI_HD __forceinline__ uint32_t li_parse_money(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen;
   if (pos + 1 == slen) {
@@ -352,7 +352,7 @@ __device__ __forceinline__ uint32_t li_parse_money(LiSqli& S, LiTok& c, uint32_t
   return pos + 1 + xlen;
 }
 
-__device__ __forceinline__ uint32_t li_parse_number(LiSqli& S, LiTok& c, uint32_t pos) {
+GI_HD __forceinline__ uint32_t li_parse_number(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen;
   if (s[pos] == '0' && pos + 1 < slen) {
@@ -402,7 +402,7 @@ __device__ __forceinline__ uint32_t li_parse_number(LiSqli& S, LiTok& c, uint32_
 }
 
 // one parser step at S.pos into token c: returns the new position
-__device__ __forceinline__ uint32_t li_parse(LiSqli& S, LiTok& c) {
+GI_HD __forceinline__ uint32_t li_parse(LiSqli& S, LiTok& c) {
   const uint8_t* s = S.s;
   const uint32_t slen = S.slen, pos = S.pos;
   const uint8_t ch = s[pos];
@@ -528,7 +528,7 @@ __device__ __forceinline__ uint32_t li_parse(LiSqli& S, LiTok& c) {
 }
 
 // libinjection_sqli_tokenize into tv[S.cur]
-__device__ __forceinline__ bool li_tokenize(LiSqli& S) {
+GI_HD __forceinline__ bool li_tokenize(LiSqli& S) {
   if (S.slen == 0) return false;
   LiTok& c = S.tv[S.cur];
   li_clear(c);
@@ -547,25 +547,25 @@ __device__ __forceinline__ bool li_tokenize(LiSqli& S) {
   return false;
 }
 
-__device__ __forceinline__ bool li_unary(const LiTok& t) {  // st_is_unary_op
+GI_HD __forceinline__ bool li_unary(const LiTok& t) {  // st_is_unary_op
   if (t.type != 'o') return false;
   if (t.len == 1) return t.p[0] == '+' || t.p[0] == '-' || t.p[0] == '!' || t.p[0] == '~';
   if (t.len == 2) return t.p[0] == '!' && t.p[1] == '!';
   if (t.len == 3) return li_tok_is(t, "NOT");
   return false;
 }
-__device__ __forceinline__ bool li_arith(const LiTok& t) {
+GI_HD __forceinline__ bool li_arith(const LiTok& t) {
   const uint8_t ch = t.len ? t.p[0] : 0;
   return t.type == 'o' && t.len == 1 && (ch == '*' || ch == '/' || ch == '-' || ch == '+' || ch == '%');
 }
-__device__ __forceinline__ bool li_in(uint8_t c, const char* set) {
+GI_HD __forceinline__ bool li_in(uint8_t c, const char* set) {
   for (uint32_t i = 0; set[i]; i++)
     if ((uint8_t)set[i] == c) return true;
   return false;
 }
 
 // syntax_merge_words: a's value becomes the keyword pool entry of "a b"
-__device__ __forceinline__ bool li_merge(const LiTables& T, LiTok& a, const LiTok& b) {
+GI_HD __forceinline__ bool li_merge(const LiTables& T, LiTok& a, const LiTok& b) {
   if (!li_in(a.type, "knoUfETt") || !li_in(b.type, "knoUfETt&")) return false;
   const uint32_t sz3 = (uint32_t)a.len + b.len + 1;
   if (sz3 >= LI_TOKEN_SIZE) return false;
@@ -578,7 +578,7 @@ __device__ __forceinline__ bool li_merge(const LiTables& T, LiTok& a, const LiTo
   return true;
 }
 
-__device__ __forceinline__ bool li_func_word(const LiTok& t) {
+GI_HD __forceinline__ bool li_func_word(const LiTok& t) {
   return li_tok_is(t, "USER_ID") || li_tok_is(t, "USER_NAME") || li_tok_is(t, "DATABASE") ||
          li_tok_is(t, "PASSWORD") || li_tok_is(t, "USER") || li_tok_is(t, "CURRENT_USER") ||
          li_tok_is(t, "CURRENT_DATE") || li_tok_is(t, "CURRENT_TIME") || li_tok_is(t, "CURRENT_TIMESTAMP") ||
@@ -586,7 +586,7 @@ __device__ __forceinline__ bool li_func_word(const LiTok& t) {
 }
 
 // the next token into tv[pos] (comments go to last_comment): libinjection_sqli_fold's inner loops
-__device__ __forceinline__ void li_pull(LiSqli& S, uint32_t& pos, bool& more, LiTok& last) {
+GI_HD __forceinline__ void li_pull(LiSqli& S, uint32_t& pos, bool& more, LiTok& last) {
   S.cur = pos;
   more = li_tokenize(S);
   if (more) {
@@ -600,7 +600,7 @@ __device__ __forceinline__ void li_pull(LiSqli& S, uint32_t& pos, bool& more, Li
 }
 
 // libinjection_sqli_fold -> number of fingerprint tokens
-__device__ __noinline__ uint32_t li_fold(LiSqli& S) {
+GI_HD __noinline__ uint32_t li_fold(LiSqli& S) {
   LiTok* tv = S.tv;
   uint32_t pos = 0, left = 0;
   bool more = true;
@@ -733,7 +733,7 @@ __device__ __noinline__ uint32_t li_fold(LiSqli& S) {
 
 // fingerprint blacklist: the authored grammar of libinj_tables.FINGERPRINT_RULES
 // (f upper-cased, n <= 5), matched by hand
-__device__ __noinline__ bool li_fp_black(const uint8_t* f, uint32_t n) {
+GI_HD __noinline__ bool li_fp_black(const uint8_t* f, uint32_t n) {
   if (n == 0) return false;
   auto at = [&](uint32_t i) -> uint8_t { return i < n ? f[i] : (uint8_t)0; };
   auto val1s = [&](uint8_t c) { return c == '1' || c == 'S'; };
@@ -780,10 +780,10 @@ __device__ __noinline__ bool li_fp_black(const uint8_t* f, uint32_t n) {
   return false;
 }
 
-__device__ __forceinline__ uint8_t li_fpc(const LiSqli& S, uint32_t i) { return S.tv[i].type; }
+GI_HD __forceinline__ uint8_t li_fpc(const LiSqli& S, uint32_t i) { return S.tv[i].type; }
 
 // libinjection_sqli_not_whitelist (fp = the fingerprint, tlen tokens)
-__device__ __noinline__ bool li_not_whitelist(const LiSqli& S, const uint8_t* fp, uint32_t tlen) {
+GI_HD __noinline__ bool li_not_whitelist(const LiSqli& S, const uint8_t* fp, uint32_t tlen) {
   const LiTok* tv = S.tv;
   if (tlen > 1 && fp[tlen - 1] == 'c') {
     const uint8_t* s = S.s;
@@ -828,7 +828,7 @@ __device__ __noinline__ bool li_not_whitelist(const LiSqli& S, const uint8_t* fp
 }
 
 // libinjection_sqli_fingerprint + the blacklist/whitelist check for one context
-__device__ __noinline__ bool li_sqli_ctx(LiSqli& S, uint32_t flags) {
+GI_HD __noinline__ bool li_sqli_ctx(LiSqli& S, uint32_t flags) {
   S.flags = flags;
   S.pos = 0;
   S.cur = 0;
@@ -860,7 +860,7 @@ __device__ __noinline__ bool li_sqli_ctx(LiSqli& S, uint32_t flags) {
 // libinjection_is_sqli.  `st` is the caller's state buffer (LDS in k_detect,
 // the request's macro scratch in k_eval): kept in memory, the tokenizer state
 // does not inflate the register budget of every kernel that can call this.
-__device__ __noinline__ bool li_detect_sqli(const uint8_t* s, uint32_t n, LiSqli* st, const LiTables& T) {
+GI_HD __noinline__ bool li_detect_sqli(const uint8_t* s, uint32_t n, LiSqli* st, const LiTables& T) {
   if (n == 0) return false;
   LiSqli& S = *st;
   S.T = T;
@@ -887,17 +887,17 @@ __device__ __noinline__ bool li_detect_sqli(const uint8_t* s, uint32_t n, LiSqli
 // two-token fingerprint of that shape survives blacklist + whitelist (the only
 // blacklisted one, value + UNION, is whitelisted at two tokens) -- so it is
 // never SQLi.  tests/test_libinjection.py checks the claim on a corpus.
-__device__ __forceinline__ bool li_sqli_byte(uint8_t c) {
+GI_HD __forceinline__ bool li_sqli_byte(uint8_t c) {
   return !((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_');
 }
 // Exact prefilter: without any of  NUL \t \n \v \f \r space < > = ' " ` /
 // each of the five start states yields a single DATA_TEXT / ATTR_NAME /
 // ATTR_VALUE token with no black attribute before it -- never XSS.
-__device__ __forceinline__ bool li_xss_byte(uint8_t c) {
+GI_HD __forceinline__ bool li_xss_byte(uint8_t c) {
   return c == 0 || (c >= 9 && c <= 13) || c == ' ' || c == '<' || c == '>' || c == '=' || c == '\'' || c == '"' ||
          c == '`' || c == '/';
 }
-__device__ inline bool li_candidate(bool sqli, const uint8_t* s, uint32_t n) {
+GI_HD inline bool li_candidate(bool sqli, const uint8_t* s, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
     if (sqli ? li_sqli_byte(s[i]) : li_xss_byte(s[i])) return true;
   return false;
@@ -922,17 +922,17 @@ struct H5 {
   uint8_t tt, state, is_close, _pad;
 };
 
-__device__ __forceinline__ bool h5_white(uint8_t c) {  // strchr(" \t\n\v\f\r", ch): NUL matches the terminator
+GI_HD __forceinline__ bool h5_white(uint8_t c) {  // strchr(" \t\n\v\f\r", ch): NUL matches the terminator
   return c == ' ' || (c >= 9 && c <= 13) || c == 0;
 }
-__device__ __forceinline__ bool h5_alpha(uint8_t c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
-__device__ __forceinline__ void h5_tok(H5& h, uint32_t st, uint32_t n, uint8_t t) {
+GI_HD __forceinline__ bool h5_alpha(uint8_t c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+GI_HD __forceinline__ void h5_tok(H5& h, uint32_t st, uint32_t n, uint8_t t) {
   h.ts = st;
   h.tl = n;
   h.tt = t;
 }
 // h5_skip_white: next non-white byte, -1 at the end
-__device__ __forceinline__ int h5_skip_white(H5& h) {
+GI_HD __forceinline__ int h5_skip_white(H5& h) {
   while (h.pos < h.len) {
     const uint8_t c = h.s[h.pos];
     if (c == 0 || c == ' ' || (c >= 9 && c <= 13)) h.pos++;
@@ -944,7 +944,7 @@ __device__ __forceinline__ int h5_skip_white(H5& h) {
 // libinjection_h5_next: one token (false at the end).  `run` is the state
 // code to execute (a C tail call jumps to another state's code without
 // changing the persistent h.state).
-__device__ __noinline__ bool h5_next(H5& h) {
+GI_HD __noinline__ bool h5_next(H5& h) {
   uint8_t run = h.state;
   const uint8_t* s = h.s;
   for (uint32_t guard = 0; guard < 64; guard++) {
@@ -1269,7 +1269,7 @@ __device__ __noinline__ bool h5_next(H5& h) {
 }
 
 // cstrcasecmp_with_null(lit, b, n) == 0: NULs in b are skipped (lit from a pool)
-__device__ bool li_eq_with_null(const uint8_t* lit, uint32_t ln, const uint8_t* b, uint32_t n) {
+GI_HD bool li_eq_with_null(const uint8_t* lit, uint32_t ln, const uint8_t* b, uint32_t n) {
   uint32_t j = 0;
   for (uint32_t i = 0; i < n; i++) {
     uint8_t c = b[i];
@@ -1281,7 +1281,7 @@ __device__ bool li_eq_with_null(const uint8_t* lit, uint32_t ln, const uint8_t* 
   return j == ln;
 }
 
-__device__ __noinline__ bool li_black_tag(const uint8_t* s, uint32_t n) {
+GI_HD __noinline__ bool li_black_tag(const uint8_t* s, uint32_t n) {
   if (n < 3) return false;
   for (uint32_t k = 0; k < LI_NTAGS; k++) {
     const uint32_t e = kLiTags[k];
@@ -1292,7 +1292,7 @@ __device__ __noinline__ bool li_black_tag(const uint8_t* s, uint32_t n) {
   return false;
 }
 
-__device__ __noinline__ uint32_t li_black_attr(const uint8_t* s, uint32_t n) {
+GI_HD __noinline__ uint32_t li_black_attr(const uint8_t* s, uint32_t n) {
   if (n < 2) return 0;
   if (n >= 5) {
     if ((s[0] == 'o' || s[0] == 'O') && (s[1] == 'n' || s[1] == 'N')) return 1;
@@ -1305,7 +1305,7 @@ __device__ __noinline__ uint32_t li_black_attr(const uint8_t* s, uint32_t n) {
   return 0;
 }
 
-__device__ __forceinline__ int li_hexv(uint8_t c) {
+GI_HD __forceinline__ int li_hexv(uint8_t c) {
   if (c >= '0' && c <= '9') return c - '0';
   if (c >= 'A' && c <= 'F') return c - 'A' + 10;
   if (c >= 'a' && c <= 'f') return c - 'a' + 10;
@@ -1313,7 +1313,7 @@ __device__ __forceinline__ int li_hexv(uint8_t c) {
 }
 
 // html_decode_char_at over s[0, n) (bytes past n read as 0, the C NUL terminator)
-__device__ int li_html_decode_char_at(const uint8_t* s, uint32_t n, uint32_t* used) {
+GI_HD int li_html_decode_char_at(const uint8_t* s, uint32_t n, uint32_t* used) {
   auto at = [&](uint32_t k) -> uint8_t { return k < n ? s[k] : (uint8_t)0; };
   if (n == 0) {
     *used = 0;
@@ -1367,7 +1367,7 @@ __device__ int li_html_decode_char_at(const uint8_t* s, uint32_t n, uint32_t* us
   return val;
 }
 
-__device__ bool li_htmlencode_startswith(const char* prefix, const uint8_t* s, uint32_t n) {
+GI_HD bool li_htmlencode_startswith(const char* prefix, const uint8_t* s, uint32_t n) {
   uint32_t j = 0;
   bool first = true;
   while (n > 0) {
@@ -1386,7 +1386,7 @@ __device__ bool li_htmlencode_startswith(const char* prefix, const uint8_t* s, u
   return !prefix[j];
 }
 
-__device__ __noinline__ bool li_black_url(const uint8_t* s, uint32_t n) {
+GI_HD __noinline__ bool li_black_url(const uint8_t* s, uint32_t n) {
   while (n > 0 && (s[0] <= 32 || s[0] >= 127)) {
     s++;
     n--;
@@ -1396,7 +1396,7 @@ __device__ __noinline__ bool li_black_url(const uint8_t* s, uint32_t n) {
 }
 
 // libinjection_is_xss for one start state
-__device__ __noinline__ bool li_xss_ctx(const uint8_t* s, uint32_t n, uint8_t start) {
+GI_HD __noinline__ bool li_xss_ctx(const uint8_t* s, uint32_t n, uint8_t start) {
   H5 h;
   h.s = s;
   h.len = n;
@@ -1438,7 +1438,7 @@ __device__ __noinline__ bool li_xss_ctx(const uint8_t* s, uint32_t n, uint8_t st
 }
 
 // libinjection_xss: the five start states
-__device__ __noinline__ bool li_detect_xss(const uint8_t* s, uint32_t n) {
+GI_HD __noinline__ bool li_detect_xss(const uint8_t* s, uint32_t n) {
   return li_xss_ctx(s, n, HS_DATA) || li_xss_ctx(s, n, HS_BEFORE_ATTR_NAME) || li_xss_ctx(s, n, HS_VALUE_SQ) ||
          li_xss_ctx(s, n, HS_VALUE_DQ) || li_xss_ctx(s, n, HS_VALUE_BQ);
 }

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <chrono>
 #include <thread>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -290,38 +291,26 @@ int64_t gi_ruleset_describe(const gi_ruleset* rs, char* buf, size_t cap) {
 // context switches to it (and frees the old buffers) only once every step
 // succeeded, so a failed swap leaves the old ruleset fully in place.  The
 // staged batch is dropped (its scratch layout depends on the program).
-static int load_program(gi_ctx* c, const gi_ruleset* rs) {
-  hipError_t e = hipSuccess;
-  const Program& P = rs->prog;
-  if (P.streams.size() > GI_MAX_STREAMS) return fail(c, GI_EINVAL, "ruleset has more phase-A streams than supported");
-  std::vector<DevBuf> nbufs(48);
-  DevBuf njoblist;
-  DProgram np{};
-  ScanLaunch nscan{};
-  auto discard = [&](int code, const char* what) {
-    for (auto& b : nbufs) b.release();
-    njoblist.release();
-    return fail(c, code, what);
-  };
+// Every DProgram field from the compiled Program.  put(p, bytes) stores one
+// table where the interpreter reads it and returns that address: HBM for a
+// context (load_program), host memory for the CPU baseline
+// (gi_cpu_baseline_inspect).  Returns nullptr or an error message.
+}  // extern "C"
+template <class Put>
+static const char* fill_dprogram(const Program& P, DProgram& np, Put&& put, std::vector<uint32_t>& top_ph,
+                                 uint32_t& n_ph1) {
   std::vector<uint32_t> lower;
   lower.reserve(GI_N_LOWER_PAIRS * 2);
   for (int i = 0; i < GI_N_LOWER_PAIRS; i++) {
     lower.push_back(kLowerPairs[i][0]);
     lower.push_back(kLowerPairs[i][1]);
   }
-  hipStream_t s = c->stream;
-  int k = 0;
-#define UP(field, vec, T)                                   \
-  if (e == hipSuccess) {                                    \
-    e = upload(&nbufs[k], vec, s);                          \
-    np.field = (const T*)nbufs[k].p;                        \
-    k++;                                                    \
-  }
+#define UP(field, vec, T) np.field = (const T*)put((vec).data(), (vec).size() * sizeof((vec)[0]));
   UP(rules, P.rules, DRule)
   // per-phase rule walks: rules of that phase plus phase-0 records (SecMarker),
   // in file order -- what RuleGroup.Eval(phase) visits
-  std::vector<uint32_t> top_ph;
-  uint32_t n_ph1 = 0;
+  top_ph.clear();
+  n_ph1 = 0;
   for (int ph = 1; ph <= 2; ph++) {
     for (uint32_t ri : P.top)
       if (P.rules[ri].phase == 0 || P.rules[ri].phase == ph) top_ph.push_back(ri);
@@ -406,8 +395,6 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   UP(fold_ids, P.fold_ids, uint32_t)
   UP(fold_runs, P.fold_runs, uint32_t)
 #undef UP
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return discard(e == hipErrorOutOfMemory ? GI_ENOMEM : GI_ENODEV, "ruleset upload failed");
   np.n_lower_pairs = GI_N_LOWER_PAIRS;
   // observable captures: per-request submatch workspace (kernels.hip CapHdr +
   // pike_match) and the TX slots of the keys "0".."8"
@@ -429,17 +416,17 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   np.top_end[1] = (uint32_t)top_ph.size();
   np.n_slots = P.n_slots;
   np.n_dyn_sites = (uint32_t)P.dyn_sites.size();
-  if (P.tx_snap.size() != P.n_slots) return discard(GI_EINVAL, "folded TX snapshot size");
+  if (P.tx_snap.size() != P.n_slots) return "folded TX snapshot size";
   // a folded run starts and ends inside the phase-1 walk, at its own rule
   for (uint32_t a = 0; a < n_ph1; a++) {
     const DRule& R = P.rules[top_ph[a]];
     if (!(R.flags & RF_FOLDED)) continue;
     if (4ull * R._pad2 + 3 >= P.fold_runs.size() || P.fold_runs[4 * R._pad2 + 2] <= a ||
         P.fold_runs[4 * R._pad2 + 2] > n_ph1)
-      return discard(GI_EINVAL, "folded run out of range");
+      return "folded run out of range";
   }
   for (size_t a = n_ph1; a < top_ph.size(); a++)
-    if (P.rules[top_ph[a]].flags & RF_FOLDED) return discard(GI_EINVAL, "folded rule outside phase 1");
+    if (P.rules[top_ph[a]].flags & RF_FOLDED) return "folded rule outside phase 1";
   np.fold_on = P.fold_on;
   np.fold_nids = P.fold_nids;
   np.n_markers = P.n_markers;
@@ -476,6 +463,40 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   np.item_singles = P.item_singles;
   for (int k = 0; k < 8; k++) np.item_sides[k] = P.item_sides[k];
   np.n_hit_slots = P.n_hit_slots;
+  return nullptr;
+}
+extern "C" {
+
+static int load_program(gi_ctx* c, const gi_ruleset* rs) {
+  hipError_t e = hipSuccess;
+  const Program& P = rs->prog;
+  if (P.streams.size() > GI_MAX_STREAMS) return fail(c, GI_EINVAL, "ruleset has more phase-A streams than supported");
+  std::vector<DevBuf> nbufs(48);
+  DevBuf njoblist;
+  DProgram np{};
+  ScanLaunch nscan{};
+  auto discard = [&](int code, const char* what) {
+    for (auto& b : nbufs) b.release();
+    njoblist.release();
+    return fail(c, code, what);
+  };
+  hipStream_t s = c->stream;
+  int k = 0;
+  auto put = [&](const void* src, size_t bytes) -> const void* {
+    if (e != hipSuccess || k >= (int)nbufs.size()) {
+      if (e == hipSuccess) e = hipErrorOutOfMemory;
+      return nullptr;
+    }
+    DevBuf& b = nbufs[k++];
+    e = b.ensure(std::max<size_t>(bytes, 16));
+    if (e == hipSuccess && bytes) e = hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice);
+    return b.p;
+  };
+  std::vector<uint32_t> top_ph;
+  uint32_t n_ph1 = 0;
+  const char* ferr = fill_dprogram(P, np, put, top_ph, n_ph1);
+  if (e != hipSuccess) return discard(e == hipErrorOutOfMemory ? GI_ENOMEM : GI_ENODEV, "ruleset upload failed");
+  if (ferr) return discard(GI_EINVAL, ferr);
   // k_scan plan: LDS jobs that fit the small image go to the 2-per-CU launch,
   // the rest (big images, global-table automata) to the 1-per-CU launch.
   std::vector<uint32_t> jl[3];
@@ -624,6 +645,188 @@ int gi_host_unregister(gi_ctx* c, void* p) {
   return e == hipSuccess ? GI_OK : hip_fail(c, e, "hipHostUnregister");
 }
 
+}  // extern "C"
+// One request's scratch layout and capacities (lengths only): its region in
+// the batch scratch (ReqLayout), the phase-A item / hit-set sizes, and the
+// batch totals it adds to.  Shared by gi_stage_batch and the CPU baseline.
+struct LayoutSizes {
+  uint64_t region, vmap, hset;
+  uint64_t items, raw, body, post;  // phase-A items, bytes without / of the body, body fields
+  bool mp;                          // multipart body
+};
+struct LayoutAcc {
+  uint64_t items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0, max_req_bytes = 0;
+  uint32_t n_mp_body = 0, max_cap_t = 64;
+};
+static const char* request_layout(const Program& PG, uint32_t cap_ws_words, uint32_t cap_groups, const gi_batch* in,
+                                  uint32_t r, ReqLayout& L, LayoutSizes& z, LayoutAcc& a) {
+  const uint32_t n_single_items = (uint32_t)__builtin_popcount(PG.item_singles);
+  z.mp = false;
+  const gi_request& q = in->reqs[r];
+  const gi_span* sp[5] = {&q.method, &q.uri, &q.proto, &q.body, &q.remote_addr};
+  for (auto* s : sp)
+    if (s->off + s->len > in->data_len) return "request span out of range";
+  if ((uint64_t)q.hdr_begin + q.hdr_count > in->n_headers) return "header range out of range";
+  uint64_t maxv = std::max<uint64_t>({(uint64_t)q.uri.len * 3 + 2, (uint64_t)q.method.len + q.uri.len + q.proto.len + 2,
+                                      (uint64_t)q.body.len, 64});
+  uint64_t cookie = 0, ncookie = 0, hdr_bytes = 0, hname_bytes = 0;
+  bool multipart = false, hname_high = false;
+  for (uint32_t h = 0; h < q.hdr_count; h++) {
+    const gi_header& hd = in->headers[q.hdr_begin + h];
+    if (hd.name.off + hd.name.len > in->data_len || hd.value.off + hd.value.len > in->data_len)
+      return "header span out of range";
+    maxv = std::max<uint64_t>(maxv, std::max(hd.name.len, hd.value.len));
+    hdr_bytes += hd.name.len + hd.value.len;
+    hname_bytes += hd.name.len;
+    if (!PG.dyn_sites.empty())
+      for (uint32_t k = 0; k < hd.name.len && !hname_high; k++) hname_high = in->data[hd.name.off + k] >= 0x80;
+    if (hd.name.len == 12 && strncasecmp((const char*)in->data + hd.name.off, "content-type", 12) == 0) {
+      const char* hv = (const char*)in->data + hd.value.off;
+      for (uint32_t k = 0; k + 9 <= hd.value.len && !multipart; k++)
+        multipart = strncasecmp(hv + k, "multipart", 9) == 0;
+    }
+    if (hd.name.len == 6) {
+      const uint8_t* nm = in->data + hd.name.off;
+      bool ck = true;
+      const char* lit = "cookie";
+      for (int i = 0; i < 6; i++)
+        if ((nm[i] | 0x20) != lit[i]) ck = false;
+      if (ck) {
+        cookie += hd.value.len;
+        ncookie++;
+      }
+    }
+  }
+  // ARGS_POST fields a body can yield: urlencoded <= '&' + 1; JSON <=
+  // ',' + 2 '[' + '{' + 1 (elements past the first of a container need a
+  // comma, and each non-empty array adds its own count entry)
+  uint64_t post_fields = 0;
+  if (q.body.len) {
+    const uint8_t* bd = in->data + q.body.off;
+    uint64_t seps = 0, nls = 0;
+    for (uint32_t k = 0; k < q.body.len; k++) {
+      const uint8_t ch = bd[k];
+      seps += (ch == '&') + (ch == ',') + 2 * (ch == '[') + (ch == '{');
+      nls += ch == '\n';
+    }
+    post_fields = std::min<uint64_t>(seps + 2, q.body.len / 2 + 2);
+    {  // XML (kernels.hip parse_xml): one field per attribute ('=' or a bare name) and text token
+      uint32_t k = 0;
+      while (k < q.body.len && (bd[k] == ' ' || bd[k] == '\t' || bd[k] == '\n' || bd[k] == '\r')) k++;
+      if (k < q.body.len && bd[k] == '<') {
+        uint64_t lt = 0, sp = 0;
+        for (uint32_t j = 0; j < q.body.len; j++) {
+          lt += bd[j] == '<';
+          sp += bd[j] == ' ' || bd[j] == '\t' || bd[j] == '\n' || bd[j] == '\r';
+        }
+        post_fields = std::max<uint64_t>(post_fields, 2 * lt + sp + 2);
+      }
+    }
+    // multipart (kernels.hip parse_multipart): a part spends >= 2 lines on
+    // its delimiter and header end and yields <= 3 entries + 1 per header line
+    if (multipart) post_fields += nls + 8;
+    a.n_mp_body += multipart ? 1 : 0;
+    z.mp = multipart;
+  }
+  uint64_t cap_f = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie) + post_fields;
+  uint64_t cap_b = 4ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96 + 16;  // + REMOTE_PORT
+  // multipart: canonical keys, joined continuation lines, "Key: value"
+  // strings and unescaped parameters are each at most the part header
+  // bytes; sizes 24 B per part
+  if (multipart) cap_b += 4ull * q.body.len + 1024;
+  // XML (a ctl can pick it for any body): decoded texts <= the body, the error message
+  if (q.body.len) cap_b += q.body.len + 1024;
+  {  // a JSON-looking body: room for the flattened "json.a.b" keys + parser stack
+    const uint8_t* bd = in->data + q.body.off;
+    uint32_t k = 0;
+    while (k < q.body.len && (bd[k] == ' ' || bd[k] == '\t' || bd[k] == '\n' || bd[k] == '\r')) k++;
+    // kernels.hip parse_json_body: flattened bytes <= 4n + 1024, one
+    // transient allocation <= that again + n, parser stack 1048 B
+    if (k < q.body.len && (bd[k] == '{' || bd[k] == '[')) cap_b += 8ull * q.body.len + 4200;
+  }
+  cap_b += 8 * (cap_f + 12) + 8;  // k_eval's kind index, built for phase 1 and again after the body parse
+  uint64_t cap_t = 3 * maxv + 64 + (q.body.len ? 8 * 64 : 0);  // k_body: 64 lane slots of 3x + 8 B
+  uint64_t cap_mt = 2 * maxv + 512;
+  if (cap_f > 0xFFFFFFFFull || cap_b > 0xFFFFFFFFull || cap_t > 0xFFFFFFFFull || cap_mt > 0xFFFFFFFFull)
+    return "request too large";
+  // phase-A items: at most both sides of every field (GET args, headers,
+  // cookies; POST args appear after phase 1) plus the filtered singles
+  const uint64_t pre_body_fields = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie);
+  z.items = 2 * (pre_body_fields + (PG.body_access ? post_fields : 0)) + n_single_items;
+  z.post = PG.body_access ? post_fields : 0;
+  z.raw = (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
+  z.body = q.body.len;
+  a.items_cap += z.items;
+  a.post_total += PG.body_access ? post_fields : 0;
+  a.raw_total += (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
+  a.raw_body += q.body.len;
+  a.max_req_bytes = std::max<uint64_t>(a.max_req_bytes, (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes + q.body.len);
+  a.max_cap_t = (uint32_t)std::max<uint64_t>(a.max_cap_t, cap_t);
+  
+  L.vmap_bits = (uint32_t)(2 * cap_f);
+  z.vmap = (2 * cap_f + 31) & ~31ull;
+  {  // exact hit set (kernels.hip hset_insert): ~one key per phase-A item; a fuller table
+     // only sends the request back to re-evaluation (exact either way)
+    uint64_t amps = 1;
+    const uint8_t* u = in->data + q.uri.off;
+    for (uint32_t k = 0; k < q.uri.len; k++) amps += u[k] == '&';
+    const uint64_t est = 2 * (amps + q.hdr_count + 2 * ncookie + cookie / 8 + (PG.body_access ? post_fields : 0)) +
+                         n_single_items;
+    uint64_t cap = 16;
+    while (cap < est && cap < (1ull << 16)) cap <<= 1;
+    L.hset_mask = PG.streams.empty() ? 0u : (uint32_t)(cap - 1);
+    z.hset = PG.streams.empty() ? 0 : (cap + 1 + 3) & ~3ull;
+  }
+  // dynamic TX area (macro-key setvars): the executions each site can reach on
+  // this request and the bytes they can store (gi_program.h DDynSite)
+  uint64_t dyn_e = 0, dyn_b = 0;
+  for (const DDynSite& ds : PG.dyn_sites) {
+    const uint64_t raw_all = (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes + q.body.len;
+    uint64_t ex = ds.mm, src = 0;
+    if (!ds.no_targets) {
+      ex = (uint64_t)ds.mm * (ds.nsingles + (uint64_t)(ds.hdr_names + ds.hdr_vals) * q.hdr_count + (uint64_t)ds.other_coll * cap_f);
+      src = (uint64_t)ds.mm * (ds.nsingles * maxv + (uint64_t)ds.hdr_names * hname_bytes +
+                               (uint64_t)ds.hdr_vals * (hdr_bytes - hname_bytes) + (uint64_t)ds.other_coll * (raw_all + cap_b));
+    }
+    const bool ascii_src = !ds.hdr_vals && !ds.other_coll && !ds.nsingles && !hname_high;
+    const uint64_t g = ascii_src ? ds.g_ascii : ds.g_any;
+    dyn_e += ex;
+    dyn_b += ex * (ds.lit + ds.fixed + 32ull * ds.n_mvname) + g * (ds.n_val + ds.n_mvname) * src +
+             ex * ds.n_big * std::max(cap_t, cap_mt);
+  }
+  if (dyn_e > 0xFFFFFFFFull || dyn_b > 0xFFFFFFFFull) return "request too large (dynamic TX keys)";
+  L.dyn_cap = PG.dyn_sites.empty() ? 0u : (uint32_t)dyn_e;
+  L.dyn_capb = PG.dyn_sites.empty() ? 0u : (uint32_t)((dyn_b + 15) & ~15ull);
+  L.cap_f = (uint32_t)cap_f;
+  L.cap_b = (uint32_t)cap_b;
+  L.cap_t = (uint32_t)cap_t;
+  L.cap_mt = (uint32_t)cap_mt;
+  uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)PG.n_slots * GI_SLOT_BYTES + 15) / 16 * 16 + GI_RM_BYTES + (cap_b + 15) / 16 * 16 +
+                2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
+  if (!PG.dyn_sites.empty()) sz += 16 + 32ull * L.dyn_cap + L.dyn_capb;  // kernels.hip DynHdr + DynEnt[] + bytes
+  // observable captures (kernels.hip region_of): workspace + one value buffer per group
+  sz += (4ull * cap_ws_words + 15) / 16 * 16 +
+        (cap_ws_words ? (uint64_t)cap_groups * ((cap_t + 15) / 16 * 16) : 0);
+  // matched-variable state (kernels.hip MvState): header, entries, value
+  // arena, MATCHED_VAR copy, name buffer
+  if (PG.mv_used) {
+    // MATCHED_VARS of one rule: a value per field (transformed: <= cap_t... the
+    // arena holds what phase B copies), plus the TX entries a TX target can
+    // match -- the static slots (values <= the longest setvar literal or a
+    // macro expansion) and the run-time keys
+    const uint64_t e = cap_f + 16 + PG.n_slots + L.dyn_cap;
+    const uint64_t ab = cap_b + cap_mt + L.dyn_capb + 40ull * (PG.n_slots + L.dyn_cap) +
+                        (uint64_t)PG.n_slots * std::max<uint64_t>(cap_mt, PG.max_tx_lit);
+    if (e > 0xFFFFFFFFull || ab > 0xFFFFFFFFull) return "request too large (matched variables)";
+    L.mv_cap_e = (uint32_t)e;
+    L.mv_cap_a = (uint32_t)((ab + 15) & ~15ull);
+    sz += 64 + e * 32 + L.mv_cap_a + (cap_t + 15) / 16 * 16 + (cap_mt + 15) / 16 * 16;
+  }
+  z.region = (sz + 63) / 64 * 64;
+  return nullptr;
+}
+
+extern "C" {
 int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if (!c || !in) return GI_EINVAL;
   if (in->n_req && (!in->reqs || !in->data)) return fail(c, GI_EINVAL, "null batch arrays");
@@ -652,169 +855,12 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   const uint32_t n_single_items = (uint32_t)__builtin_popcount(PG.item_singles);
   // per-request sizes (in parallel on the host cores for large batches),
   // then the running offsets (region, value map, hit set) in one serial pass
-  struct Sizes {
-    uint64_t region, vmap, hset;
-    uint64_t items, raw, body, post;  // phase-A items, bytes without / of the body, body fields
-    bool mp;                          // multipart body
-  };
-  struct Acc {
-    uint64_t items_cap = 0, raw_total = 0, raw_body = 0, post_total = 0, max_req_bytes = 0;
-    uint32_t n_mp_body = 0, max_cap_t = 64;
-  };
+  using Sizes = LayoutSizes;
+  using Acc = LayoutAcc;
   std::vector<Sizes> sizes(n);
   for (auto& z : sizes) z.mp = false;
   auto size_one = [&](uint32_t r, Acc& a) -> const char* {
-    const gi_request& q = in->reqs[r];
-    const gi_span* sp[5] = {&q.method, &q.uri, &q.proto, &q.body, &q.remote_addr};
-    for (auto* s : sp)
-      if (s->off + s->len > in->data_len) return "request span out of range";
-    if ((uint64_t)q.hdr_begin + q.hdr_count > in->n_headers) return "header range out of range";
-    uint64_t maxv = std::max<uint64_t>({(uint64_t)q.uri.len * 3 + 2, (uint64_t)q.method.len + q.uri.len + q.proto.len + 2,
-                                        (uint64_t)q.body.len, 64});
-    uint64_t cookie = 0, ncookie = 0, hdr_bytes = 0, hname_bytes = 0;
-    bool multipart = false, hname_high = false;
-    for (uint32_t h = 0; h < q.hdr_count; h++) {
-      const gi_header& hd = in->headers[q.hdr_begin + h];
-      if (hd.name.off + hd.name.len > in->data_len || hd.value.off + hd.value.len > in->data_len)
-        return "header span out of range";
-      maxv = std::max<uint64_t>(maxv, std::max(hd.name.len, hd.value.len));
-      hdr_bytes += hd.name.len + hd.value.len;
-      hname_bytes += hd.name.len;
-      if (!PG.dyn_sites.empty())
-        for (uint32_t k = 0; k < hd.name.len && !hname_high; k++) hname_high = in->data[hd.name.off + k] >= 0x80;
-      if (hd.name.len == 12 && strncasecmp((const char*)in->data + hd.name.off, "content-type", 12) == 0) {
-        const char* hv = (const char*)in->data + hd.value.off;
-        for (uint32_t k = 0; k + 9 <= hd.value.len && !multipart; k++)
-          multipart = strncasecmp(hv + k, "multipart", 9) == 0;
-      }
-      if (hd.name.len == 6) {
-        const uint8_t* nm = in->data + hd.name.off;
-        bool ck = true;
-        const char* lit = "cookie";
-        for (int i = 0; i < 6; i++)
-          if ((nm[i] | 0x20) != lit[i]) ck = false;
-        if (ck) {
-          cookie += hd.value.len;
-          ncookie++;
-        }
-      }
-    }
-    // ARGS_POST fields a body can yield: urlencoded <= '&' + 1; JSON <=
-    // ',' + 2 '[' + '{' + 1 (elements past the first of a container need a
-    // comma, and each non-empty array adds its own count entry)
-    uint64_t post_fields = 0;
-    if (q.body.len) {
-      const uint8_t* bd = in->data + q.body.off;
-      uint64_t seps = 0, nls = 0;
-      for (uint32_t k = 0; k < q.body.len; k++) {
-        const uint8_t ch = bd[k];
-        seps += (ch == '&') + (ch == ',') + 2 * (ch == '[') + (ch == '{');
-        nls += ch == '\n';
-      }
-      post_fields = std::min<uint64_t>(seps + 2, q.body.len / 2 + 2);
-      {  // XML (kernels.hip parse_xml): one field per attribute ('=' or a bare name) and text token
-        uint32_t k = 0;
-        while (k < q.body.len && (bd[k] == ' ' || bd[k] == '\t' || bd[k] == '\n' || bd[k] == '\r')) k++;
-        if (k < q.body.len && bd[k] == '<') {
-          uint64_t lt = 0, sp = 0;
-          for (uint32_t j = 0; j < q.body.len; j++) {
-            lt += bd[j] == '<';
-            sp += bd[j] == ' ' || bd[j] == '\t' || bd[j] == '\n' || bd[j] == '\r';
-          }
-          post_fields = std::max<uint64_t>(post_fields, 2 * lt + sp + 2);
-        }
-      }
-      // multipart (kernels.hip parse_multipart): a part spends >= 2 lines on
-      // its delimiter and header end and yields <= 3 entries + 1 per header line
-      if (multipart) post_fields += nls + 8;
-      a.n_mp_body += multipart ? 1 : 0;
-      sizes[r].mp = multipart;
-    }
-    uint64_t cap_f = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie) + post_fields;
-    uint64_t cap_b = 4ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96 + 16;  // + REMOTE_PORT
-    // multipart: canonical keys, joined continuation lines, "Key: value"
-    // strings and unescaped parameters are each at most the part header
-    // bytes; sizes 24 B per part
-    if (multipart) cap_b += 4ull * q.body.len + 1024;
-    // XML (a ctl can pick it for any body): decoded texts <= the body, the error message
-    if (q.body.len) cap_b += q.body.len + 1024;
-    {  // a JSON-looking body: room for the flattened "json.a.b" keys + parser stack
-      const uint8_t* bd = in->data + q.body.off;
-      uint32_t k = 0;
-      while (k < q.body.len && (bd[k] == ' ' || bd[k] == '\t' || bd[k] == '\n' || bd[k] == '\r')) k++;
-      // kernels.hip parse_json_body: flattened bytes <= 4n + 1024, one
-      // transient allocation <= that again + n, parser stack 1048 B
-      if (k < q.body.len && (bd[k] == '{' || bd[k] == '[')) cap_b += 8ull * q.body.len + 4200;
-    }
-    cap_b += 8 * (cap_f + 12) + 8;  // k_eval's kind index, built for phase 1 and again after the body parse
-    uint64_t cap_t = 3 * maxv + 64 + (q.body.len ? 8 * 64 : 0);  // k_body: 64 lane slots of 3x + 8 B
-    uint64_t cap_mt = 2 * maxv + 512;
-    if (cap_f > 0xFFFFFFFFull || cap_b > 0xFFFFFFFFull || cap_t > 0xFFFFFFFFull || cap_mt > 0xFFFFFFFFull)
-      return "request too large";
-    // phase-A items: at most both sides of every field (GET args, headers,
-    // cookies; POST args appear after phase 1) plus the filtered singles
-    const uint64_t pre_body_fields = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie);
-    sizes[r].items = 2 * (pre_body_fields + (PG.body_access ? post_fields : 0)) + n_single_items;
-    sizes[r].post = PG.body_access ? post_fields : 0;
-    sizes[r].raw = (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
-    sizes[r].body = q.body.len;
-    a.items_cap += sizes[r].items;
-    a.post_total += PG.body_access ? post_fields : 0;
-    a.raw_total += (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes;
-    a.raw_body += q.body.len;
-    a.max_req_bytes = std::max<uint64_t>(a.max_req_bytes, (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes + q.body.len);
-    a.max_cap_t = (uint32_t)std::max<uint64_t>(a.max_cap_t, cap_t);
-    ReqLayout& L = lay[r];
-    L.vmap_bits = (uint32_t)(2 * cap_f);
-    sizes[r].vmap = (2 * cap_f + 31) & ~31ull;
-    {  // exact hit set (kernels.hip hset_insert): ~one key per phase-A item; a fuller table
-       // only sends the request back to re-evaluation (exact either way)
-      uint64_t amps = 1;
-      const uint8_t* u = in->data + q.uri.off;
-      for (uint32_t k = 0; k < q.uri.len; k++) amps += u[k] == '&';
-      const uint64_t est = 2 * (amps + q.hdr_count + 2 * ncookie + cookie / 8 + (PG.body_access ? post_fields : 0)) +
-                           n_single_items;
-      uint64_t cap = 16;
-      while (cap < est && cap < (1ull << 16)) cap <<= 1;
-      L.hset_mask = PG.streams.empty() ? 0u : (uint32_t)(cap - 1);
-      sizes[r].hset = PG.streams.empty() ? 0 : (cap + 1 + 3) & ~3ull;
-    }
-    // dynamic TX area (macro-key setvars): the executions each site can reach on
-    // this request and the bytes they can store (gi_program.h DDynSite)
-    uint64_t dyn_e = 0, dyn_b = 0;
-    for (const DDynSite& ds : PG.dyn_sites) {
-      const uint64_t raw_all = (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes + q.body.len;
-      uint64_t ex = ds.mm, src = 0;
-      if (!ds.no_targets) {
-        ex = (uint64_t)ds.mm * (ds.nsingles + (uint64_t)(ds.hdr_names + ds.hdr_vals) * q.hdr_count + (uint64_t)ds.other_coll * cap_f);
-        src = (uint64_t)ds.mm * (ds.nsingles * maxv + (uint64_t)ds.hdr_names * hname_bytes +
-                                 (uint64_t)ds.hdr_vals * (hdr_bytes - hname_bytes) + (uint64_t)ds.other_coll * (raw_all + cap_b));
-      }
-      const bool ascii_src = !ds.hdr_vals && !ds.other_coll && !ds.nsingles && !hname_high;
-      const uint64_t g = ascii_src ? ds.g_ascii : ds.g_any;
-      dyn_e += ex;
-      dyn_b += ex * (ds.lit + ds.fixed + 32ull * ds.n_mvname) + g * (ds.n_val + ds.n_mvname) * src +
-               ex * ds.n_big * std::max(cap_t, cap_mt);
-    }
-    if (dyn_e > 0xFFFFFFFFull || dyn_b > 0xFFFFFFFFull) return "request too large (dynamic TX keys)";
-    L.dyn_cap = PG.dyn_sites.empty() ? 0u : (uint32_t)dyn_e;
-    L.dyn_capb = PG.dyn_sites.empty() ? 0u : (uint32_t)((dyn_b + 15) & ~15ull);
-    L.cap_f = (uint32_t)cap_f;
-    L.cap_b = (uint32_t)cap_b;
-    L.cap_t = (uint32_t)cap_t;
-    L.cap_mt = (uint32_t)cap_mt;
-    uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)nslots * GI_SLOT_BYTES + 15) / 16 * 16 + GI_RM_BYTES + (cap_b + 15) / 16 * 16 +
-                  2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
-    if (!PG.dyn_sites.empty()) sz += 16 + 32ull * L.dyn_cap + L.dyn_capb;  // kernels.hip DynHdr + DynEnt[] + bytes
-    // observable captures (kernels.hip region_of): workspace + one value buffer per group
-    sz += (4ull * c->prog.cap_ws_words + 15) / 16 * 16 +
-          (c->prog.cap_ws_words ? (uint64_t)c->prog.cap_groups * ((cap_t + 15) / 16 * 16) : 0);
-    // matched-variable state (kernels.hip MvState): header, entries, value
-    // arena, MATCHED_VAR copy, name buffer
-    if (PG.mv_used)
-      sz += 64 + (cap_f + 16) * 32 + (cap_b + cap_mt + 15) / 16 * 16 + (cap_t + 15) / 16 * 16 + (cap_mt + 15) / 16 * 16;
-    sizes[r].region = (sz + 63) / 64 * 64;
-    return nullptr;
+    return request_layout(PG, c->prog.cap_ws_words, c->prog.cap_groups, in, r, lay[r], sizes[r], a);
   };
   {
     const uint32_t nt = n >= 65536 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
@@ -1385,6 +1431,96 @@ int gi_stats_get(gi_ctx* c, gi_stats* out) {
   if (!c || !out) return GI_EINVAL;
   *out = c->stats;
   return GI_OK;
+}
+
+// CPU baseline (Coraza Go is absent here, so "the build's own
+// C++ CPU restatement, multi-threaded on all cores and labelled as such"):
+// the interpreter k_collect / k_eval run, compiled for the host
+// (kernels.hip cpu_inspect_one), one request at a time per thread, with no
+// phase A (every rule link evaluated by the interpreter).  Not a fallback of
+// the inspection path: gi_inspect_* never calls it.
+int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results* out, uint32_t n_threads,
+                            double* eval_seconds) {
+  if (!rs || !in || !out || !out->verdicts || !out->matched_ids || out->matched_cap == 0) return GI_EINVAL;
+  if (in->n_req && (!in->reqs || !in->data)) return GI_EINVAL;
+  try {
+    const Program& PG = rs->prog;
+    std::vector<std::vector<uint8_t>> store;
+    auto put = [&](const void* src, size_t bytes) -> const void* {
+      store.emplace_back(bytes + 64, 0);
+      if (bytes) memcpy(store.back().data(), src, bytes);
+      return store.back().data();
+    };
+    DProgram np{};
+    std::vector<uint32_t> top_ph;
+    uint32_t n_ph1 = 0;
+    if (const char* ferr = fill_dprogram(PG, np, put, top_ph, n_ph1)) {
+      (void)ferr;
+      return GI_EINVAL;
+    }
+    // the interpreter's word readers may look up to 7 bytes past a value: a padded arena
+    std::vector<uint8_t> data(in->data_len + 64, 0);
+    if (in->data_len) memcpy(data.data(), in->data, in->data_len);
+    const uint32_t n = in->n_req;
+    const uint32_t nt = std::max(1u, std::min<uint32_t>(n_threads ? n_threads : std::thread::hardware_concurrency(),
+                                                        std::max(1u, n)));
+    std::atomic<uint32_t> next(0);
+    std::atomic<int> bad(GI_OK);
+    auto work = [&]() {
+      std::vector<uint64_t> scratch;
+      std::vector<uint64_t> txs(2ull * std::max<uint32_t>(PG.n_slots, 1));
+      for (;;) {
+        const uint32_t lo = next.fetch_add(64);
+        if (lo >= n || bad.load() != GI_OK) return;
+        for (uint32_t r = lo; r < std::min(n, lo + 64); r++) {
+          ReqLayout L{};
+          LayoutSizes z{};
+          LayoutAcc acc;
+          if (request_layout(PG, np.cap_ws_words, np.cap_groups, in, r, L, z, acc)) {
+            bad.store(GI_EINVAL);
+            return;
+          }
+          L.base = 0;
+          L.vmap_bit = 0;
+          L.hset_word = 0;
+          L.hset_mask = 0;  // no phase A: no hit set
+          const size_t words = (z.region + 64) / 8 + 8;
+          if (scratch.size() < words) scratch.assign(words, 0);
+          DBatch B{};
+          B.data = data.data();
+          B.reqs = in->reqs + r;
+          B.headers = in->headers;
+          B.n_req = 1;
+          B.rstride = 1;
+          B.mcap = out->matched_cap;
+          B.scratch = (uint8_t*)scratch.data();
+          B.layout = &L;
+          B.verdicts = out->verdicts + r;
+          B.matched = out->matched_ids + (uint64_t)r * out->matched_cap;
+          B.txslots = (Slot*)txs.data();
+          cpu_inspect_one(np, B);
+        }
+      }
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (uint32_t k = 1; k < nt; k++) {
+      try {
+        th.emplace_back(work);
+      } catch (...) {
+        break;  // run with the threads the system gave us
+      }
+    }
+    work();
+    for (auto& x : th) x.join();
+    if (eval_seconds)
+      *eval_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return bad.load();
+  } catch (const std::bad_alloc&) {
+    return GI_ENOMEM;
+  } catch (...) {
+    return GI_EINVAL;
+  }
 }
 
 int gi_inspect_batch(gi_ctx* c, const gi_batch* in, gi_results* out) {

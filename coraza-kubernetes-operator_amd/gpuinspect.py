@@ -64,7 +64,7 @@ CAPTURE_DT = np.dtype([("rule_id", "<i4"), ("group", "<u4"), ("off", "<u4"), ("l
 assert REQUEST_DT.itemsize == 96 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 88
 
 EXPORTED_SYMBOLS = (
-    "gi_abi_version", "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name", "gi_ruleset_describe",
+    "gi_abi_version", "gi_cpu_baseline_inspect", "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name", "gi_ruleset_describe",
     "gi_ctx_create", "gi_ctx_free", "gi_last_error", "gi_inspect_batch", "gi_stage_batch",
     "gi_run_staged", "gi_sync", "gi_fetch_results", "gi_tally_get", "gi_stats_get",
     "gi_ctx_stream", "gi_selftest_regex", "gi_selftest_plan", "gi_selftest_triggers",
@@ -132,7 +132,7 @@ class _Stats(ctypes.Structure):
 _LIB = None
 
 
-ABI_VERSION = 4  # include/gpuinspect.h GI_ABI_VERSION: the ctypes structs below mirror that layout
+ABI_VERSION = 5  # include/gpuinspect.h GI_ABI_VERSION: the ctypes structs below mirror that layout
 
 
 def load_library(path: str = LIB_PATH):
@@ -178,6 +178,8 @@ def load_library(path: str = LIB_PATH):
                                         ctypes.POINTER(u32)]
     lib.gi_ctx_stream.argtypes = [vp]
     lib.gi_ctx_stream.restype = vp
+    lib.gi_cpu_baseline_inspect.argtypes = [vp, ctypes.POINTER(_Batch), ctypes.POINTER(_Results), u32,
+                                            ctypes.POINTER(ctypes.c_double)]
     lib.gi_host_register.argtypes = [vp, ctypes.c_void_p, sz]
     lib.gi_host_unregister.argtypes = [vp, ctypes.c_void_p]
     lib.gi_selftest_regex.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(u32)]
@@ -522,6 +524,27 @@ class Results:
 
     def tx(self, i: int, name: str) -> int:
         return int(self.verdicts[i]["tx_export"][self.exports.index(name)])
+
+
+def cpu_baseline_inspect(ruleset: "Ruleset", batch, threads: int = 0, matched_cap: int = 64):
+    """The CPU baseline (gi_cpu_baseline_inspect): this engine's
+    interpreter compiled for the host, `threads` host threads (0: all cores),
+    every rule link evaluated without phase A.  Not Coraza, and never a
+    fallback of Engine (which only runs on the GPU).  Returns (Results without
+    captures, evaluation seconds)."""
+    lib = load_library()
+    if not isinstance(batch, PackedBatch):
+        batch = pack(batch)
+    n = batch.n_req
+    verd = np.zeros(n, VERDICT_DT)
+    matched = np.zeros((n, matched_cap), np.uint32)
+    res = _Results(verd.ctypes.data, matched.ctypes.data, matched_cap, None, None, 0, 0)
+    cb = batch.to_ctypes()
+    secs = ctypes.c_double(0.0)
+    rc = lib.gi_cpu_baseline_inspect(ruleset._h, ctypes.byref(cb), ctypes.byref(res), threads, ctypes.byref(secs))
+    if rc != GI_OK:
+        raise EngineError("gi_cpu_baseline_inspect failed (%d)" % rc)
+    return Results(verd, matched, ruleset.exports), secs.value
 
 
 class Engine:

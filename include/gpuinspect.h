@@ -220,7 +220,7 @@ typedef struct {
  * gi_tally, gi_stats, ...).  It changes whenever one of them changes layout;
  * a binding checks gi_abi_version() == GI_ABI_VERSION before passing any of
  * them (INTEGRATION.md lists the revisions). */
-#define GI_ABI_VERSION 4
+#define GI_ABI_VERSION 5
 uint32_t gi_abi_version(void);
 
 /* ------------------------------------------------------------ compile */
@@ -298,6 +298,21 @@ void* gi_ctx_stream(gi_ctx* ctx);
  * before freeing it.  GI_ENODEV / GI_ENOMEM when the HIP runtime refuses. */
 int gi_host_register(gi_ctx* ctx, void* p, size_t n);
 int gi_host_unregister(gi_ctx* ctx, void* p);
+
+/* ---------------------------------------------------------- CPU baseline
+ * with no Coraza Go toolchain on the GPU box, the reported CPU
+ * number is "the build's own C++ CPU restatement, multi-threaded on all cores
+ * and labelled as such (not Coraza)".  This is the engine's own per-request
+ * interpreter (kernels.hip: ProcessURI / headers / cookies, body processors,
+ * transformations, operators incl. libinjection, the rule walk) compiled a
+ * second time for the host and run one request per thread at a time over
+ * n_threads threads (0: all cores), without phase A: every rule link is
+ * evaluated by the interpreter.  Results land in out->verdicts /
+ * out->matched_ids (captures are not recorded).  *eval_seconds (optional) is
+ * the wall time of the evaluation alone.  It is a baseline, never a fallback:
+ * gi_inspect_* only run on the GPU. */
+int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results* out, uint32_t n_threads,
+                            double* eval_seconds);
 
 /* ------------------------------------------------------- self-test hooks
  * Compiler self-tests only: run a host-built automaton on the host.  These

@@ -1,0 +1,89 @@
+"""The CPU baseline (gi_cpu_baseline_inspect): the engine's own
+interpreter compiled for the host, every rule link evaluated without phase A.
+
+It is not the product path (gi_inspect_* only runs on the GPU) but it runs the
+same interpreter source, so on CPU it also checks the interpreter-level
+features against the oracle: compile-time folding (snapshot TX, folded runs,
+constant links), macro-key setvar chains, body processors, libinjection.
+"""
+import os
+
+import pytest
+
+import gpuinspect
+import traffic
+from oracle import compare, coraza
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def _check(text, batch, threads=4):
+    rs = gpuinspect.Ruleset(text)
+    res, secs = gpuinspect.cpu_baseline_inspect(rs, batch, threads=threads, matched_cap=128)
+    orc = compare.oracle_verdicts(coraza.parse_seclang(text), batch, rs.exports)
+    bad = compare.compare(res, orc)
+    assert not bad, bad
+    assert secs > 0
+    return res
+
+
+CASES = [
+    ("samples", os.path.join(GOLDEN, "samples_ruleset.conf"), 600, dict(attack_rate=0.3)),
+    ("crs_pl1_get", os.path.join(ROOT, "rulesets", "crs_pl1.conf"), 400, dict(attack_rate=0.3)),
+    ("crs_pl1_post", os.path.join(ROOT, "rulesets", "crs_pl1.conf"), 60, dict(attack_rate=0.3, post_frac=0.5)),
+    ("crs_pl4_mix", os.path.join(ROOT, "rulesets", "crs_pl4.conf"), 120, dict(attack_rate=0.3, post_frac=0.5)),
+    ("crs_ftw", os.path.join(ROOT, "rulesets", "crs_ftw.conf"), 150, dict(attack_rate=0.5)),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_cpu_baseline_matches_oracle(case):
+    _, path, n, kw = case
+    batch = traffic.TrafficGen(traffic.SEED + 11).batch(n, **kw)
+    res = _check(open(path).read(), batch)
+    assert int(res.verdicts["match_cnt"].astype(bool).sum()) > 0
+
+
+@pytest.mark.parametrize("ruleset", ["crs_pl1", "crs_pl4"])
+def test_cpu_baseline_macro_key_chains(ruleset):
+    """CRS v4 920450 / 920451 (capture + setvar:'tx.header_name_9204xx_%{tx.0}=...'
+    + TX:/^header_name_9204xx_/ chain) and 921170 / 921180 (paramcounter)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("tgp", os.path.join(ROOT, "tests", "test_gpu_parity.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    batch = m._restricted_header_batch()
+    res = _check(open(os.path.join(ROOT, "rulesets", ruleset + ".conf")).read(), batch)
+    ids = [res.matched_rules(i) for i in range(batch.n_req)]
+    assert sum(920450 in x for x in ids) >= 20
+    if ruleset == "crs_pl4":
+        assert sum(920451 in x for x in ids) >= 4 and sum(921180 in x for x in ids) >= 2
+
+
+def test_cpu_baseline_kats():
+    import json
+    kats = json.load(open(os.path.join(GOLDEN, "kats.json")))
+    for sc in kats["scenarios"]:
+        rs = gpuinspect.Ruleset(gpuinspect.aggregate_configmaps(sc["configmaps"]))
+        txs = []
+        for r in sc["requests"]:
+            t = gpuinspect.Transaction()
+            t.process_uri(r["uri"], r["method"], r["proto"])
+            for k, v in r["headers"]:
+                t.add_request_header(k, v)
+            t.write_request_body(r["body"])
+            txs.append(t)
+        res, _ = gpuinspect.cpu_baseline_inspect(rs, txs, threads=2)
+        for i, r in enumerate(sc["requests"]):
+            it = res.interruption(i)
+            assert (it["status"] if it else 200) == r["expect_status"], (sc["name"], r["uri"])
+
+
+def test_cpu_baseline_threads_agree():
+    text = open(os.path.join(ROOT, "rulesets", "crs_pl1.conf")).read()
+    rs = gpuinspect.Ruleset(text)
+    batch = traffic.TrafficGen(traffic.SEED + 12).batch(300, attack_rate=0.3)
+    a, _ = gpuinspect.cpu_baseline_inspect(rs, batch, threads=1)
+    b, _ = gpuinspect.cpu_baseline_inspect(rs, batch, threads=7)
+    assert (a.verdicts == b.verdicts).all() and (a.matched == b.matched).all()
