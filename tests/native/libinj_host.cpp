@@ -5,6 +5,8 @@
 #define __constant__
 #define __noinline__ __attribute__((noinline))
 #define __forceinline__ inline
+#define GI_HD             // gi_program.h's markers, host build
+#define GI_TABLE static const
 #include "../../coraza-kubernetes-operator_amd/csrc/libinj.h"
 
 extern "C" int li_host_sqli(const uint8_t* s, uint32_t n) {
