@@ -14,9 +14,9 @@ seed SEED + k), cut into byte-balanced contiguous slices before timing
 N > 1 is launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env).
 Prints ONE JSON line on rank 0.
 
-Self-check: the verdicts of the timed batch are compared with the CPU oracle
-on the cpu_baseline sample (`parity_sample`); a mismatch is reported, never
-hidden.  `e2e` times one more pass including host staging (layout + H2D of
+Self-checks: the verdicts of the timed batch are compared with the CPU oracle
+on a sample (`parity_sample`) and with the C++ CPU baseline on its sample
+(`cpu_baseline.agrees_with_gpu`); a mismatch is reported, never hidden.  `e2e` times one more pass including host staging (layout + H2D of
 pageable buffers) and the verdict D2H.
 """
 
@@ -102,6 +102,43 @@ def oracle_sample(text, batch, exports, budget_s=15.0, procs=16, n_max=4000, fil
     for _, o in outs:
         verdicts.update(o)
     return verdicts, wall, procs
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(rs, batch, res, budget_s=10.0, threads=None):
+    """SURVEY §8(d)'s CPU baseline when Coraza Go is absent: the engine's own
+    C++ interpreter (gi_cpu_baseline_inspect: kernels.hip compiled for the
+    host, every rule link evaluated, no phase A) on `threads` host cores, over
+    a prefix of the benchmark batch sized from a calibration to ~budget_s.
+    Its verdicts are also compared with the GPU's for the same requests (the
+    same interpreter source: they must agree bit for bit)."""
+    threads = threads or max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+    n_cal = min(batch.n_req, 64 * threads)
+    _, dt = gpuinspect.cpu_baseline_inspect(rs, batch.take(0, n_cal), threads=threads,
+                                            matched_cap=res.matched.shape[1])
+    n = int(min(batch.n_req, max(n_cal, budget_s * n_cal / max(dt, 1e-6))))
+    sample = batch.take(0, n)
+    cres, secs = gpuinspect.cpu_baseline_inspect(rs, sample, threads=threads, matched_cap=res.matched.shape[1])
+    agree = int(((cres.verdicts[:n]["rule_id"] == res.verdicts[:n]["rule_id"]) &
+                 (cres.verdicts[:n]["status"] == res.verdicts[:n]["status"]) &
+                 (cres.verdicts[:n]["match_cnt"] == res.verdicts[:n]["match_cnt"]) &
+                 (cres.verdicts[:n]["tx_export"] == res.verdicts[:n]["tx_export"]).all(axis=1) &
+                 (cres.matched[:n] == res.matched[:n]).all(axis=1)).sum())
+    return {"value": round(n / secs, 1), "unit": "requests/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": "first %d requests of the benchmark batch through gi_cpu_baseline_inspect: this engine's "
+                      "own interpreter (kernels.hip) compiled for the host, %d threads, every rule link evaluated "
+                      "(no phase A) -- a C++ restatement, not Coraza (no Go toolchain on the box)" % (n, threads),
+            "seconds": round(secs, 3), "agrees_with_gpu": agree, "agree_of": n}
 
 
 def parity(res, verdicts):
@@ -367,16 +404,16 @@ def main():
         except gpuinspect.EngineError as ex:  # e.g. not enough HBM for a second context: reported, not fatal
             out["e2e"]["pipelined"] = {"error": str(ex)[:200]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("cpu baseline / parity sample (oracle)")
+        log("cpu baseline (C++ interpreter on the host cores)")
+        out["cpu_baseline"] = cpu_baseline(rs, batch, res, budget_s=10.0)
+        log("parity sample (oracle)")
         verdicts, wall, procs = oracle_sample(text, batch, rs.exports, files=files,
                                               calib=1 if args.config == "c5" else 100,
                                               min_n=16 if args.config == "c5" else 200,
                                               budget_s=30.0 if args.config == "c5" else 15.0)
-        out["cpu_baseline"] = {
-            "value": round(len(verdicts) / wall, 1), "unit": "requests/s", "cores": procs, "kind": "port",
-            "sample": "%d requests of the benchmark batch, oracle/coraza.py (pure-Python Coraza restatement, "
-                      "CPython re for @rx) in %d processes" % (len(verdicts), procs)}
         out["parity_sample"] = parity(res, verdicts)
+        out["parity_sample"]["oracle_requests_per_s"] = round(len(verdicts) / wall, 1)
+        out["parity_sample"]["oracle_procs"] = procs
     elif world > 1:
         # every rank checks a small sample of its own batch against the oracle
         from oracle import compare, coraza
