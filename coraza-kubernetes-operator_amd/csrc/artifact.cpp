@@ -283,7 +283,6 @@ bool validate_program(const Program& P, std::string* err) {
     if (p.kind == TP_TX && (p.slot < 0 || (uint32_t)p.slot >= nslot)) return bad("template TX slot");
     if (p.kind == TP_SINGLE && p.single >= S_COUNT) return bad("template variable");
     if ((p.kind == TP_LIT || p.kind == TP_HEADER) && !in(p.off, p.len, nstr)) return bad("template string");
-    if ((p.kind == TP_MV || p.kind == TP_MVNAME) && !P.mv_used) return bad("template matched-var without state");
   }
   // rule records
   for (uint32_t t : P.top)
@@ -322,7 +321,9 @@ bool validate_program(const Program& P, std::string* err) {
     if (v.key_mode == 2 && !single_dfa(v.key_dfa)) return bad("variable key automaton");
     if (v.key_mode > 2) return bad("variable key mode");
     if (!in(v.exc_begin, v.exc_count, P.excs.size())) return bad("variable exceptions");
-    if (v.var == V_TX && v.slot >= (int32_t)nslot) return bad("variable TX slot");
+    if (v.var == V_TX && v.key_mode != 2 && v.slot >= (int32_t)nslot) return bad("variable TX slot");
+    if (v.pre_len && (v.var != V_TX || v.key_mode != 2 || v.slot < 0 || !in((uint32_t)v.slot, v.pre_len, nstr)))
+      return bad("TX key prefix");
     if (v.var == V_TX && v.key_mode == 2) {  // static slots the key regex matches
       if (!in(v.key_off, v.key_len, P.txrx.size())) return bad("TX regex slot list");
       for (uint32_t k = 0; k < v.key_len; k++)
@@ -359,7 +360,7 @@ bool validate_program(const Program& P, std::string* err) {
   // capture programs (pike.h): every jump inside its program, rune ranges in the pool
   for (const DPike& k : P.pikes) {
     if (!in(k.inst_off, k.n_inst, P.pike_insts.size()) || k.n_inst == 0 || k.start >= k.n_inst ||
-        k.nslot < 2 || k.nslot > GI_PIKE_MAX_SLOTS || (k.nslot & 1))
+        k.nslot < 2 || k.nslot > GI_PIKE_MAX_SLOTS || (k.nslot & 1) || k.whole > 1 || (k.whole && k.nslot != 2))
       return bad("capture program");
     for (uint32_t i = 0; i < k.n_inst; i++) {
       const DPikeInst& I = P.pike_insts[k.inst_off + i];

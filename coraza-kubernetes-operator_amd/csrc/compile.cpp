@@ -1104,7 +1104,16 @@ struct Lower {
         if (v.key_rx) {
           vr.key_mode = 2;
           vr.key_dfa = regex_dfa(v.key);
-          if (vr.var == V_TX) tx_rx_vars.emplace_back((uint32_t)P->vars.size(), v.key);
+          if (vr.var == V_TX) {
+            tx_rx_vars.emplace_back((uint32_t)P->vars.size(), v.key);
+            // "^literal": keys created at run time are tested by a prefix compare
+            bool lit = v.key.size() >= 2 && v.key.size() <= 256 && v.key[0] == '^';
+            for (size_t q = 1; lit && q < v.key.size(); q++) lit = !strchr("\\.+*?()[]{}|$^", v.key[q]);
+            if (lit) {
+              vr.slot = (int32_t)str(v.key.substr(1));
+              vr.pre_len = (uint8_t)(v.key.size() - 1);
+            }
+          }
         } else if (!v.key.empty()) {
           vr.key_mode = 1;
           std::string k = vr.ci ? lower(v.key) : v.key;
@@ -1949,6 +1958,9 @@ struct Lower {
       if (!re_parse("(?sm)" + r.op_arg, &re, &err)) perr("invalid regex " + r.op_arg + ": " + err);
       DPike pk{};
       if (!build_pike(re, &P->pike_insts, &P->pike_ranges, &pk, &err)) unsup("capture: " + err);
+      // CRS's "capture the whole value" idiom (920450 / 920451 on header names):
+      // with (?s) the dot takes every rune, so group 0 is always [0, n)
+      pk.whole = (r.op_arg == "^.*$" && pk.nslot == 2) ? 1u : 0u;
       P->pikes.push_back(pk);
       P->ops[d.op].pike = (int32_t)P->pikes.size() - 1;
       for (int g = 0; g < 9; g++) slot(std::to_string(g));  // TX.0-TX.8 (CaptureField keys)
@@ -2446,6 +2458,7 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
   for (uint32_t ri : P.top)
     if (P.rules[ri].phase == 0 || P.rules[ri].phase == 1) walk.push_back(ri);
   std::vector<bool> in_prefix(P.rules.size(), false);  // links of folded rules
+  std::vector<bool> fmatched(P.rules.size(), false);   // folded top-level rules that matched
   const uint32_t ns = P.n_slots;
   // the static TX slots a rule chain reads / writes
   std::vector<int32_t> dyn_site_of(P.acts.size(), -1);
@@ -2581,6 +2594,7 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
               P.rules[ri]._pad2 = (uint32_t)run;
             }
             if (matched) {
+              fmatched[ri] = true;
               if (R.skip_after >= 0) skip_after = R.skip_after;
               if (R.skip) skip = R.skip;
               if (R.id != 0) P.fold_ids.push_back((uint32_t)R.id);
@@ -2664,6 +2678,105 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
       d._pad2 = nm;
     }
   }
+  // Regions no request reaches: the rules between a constant gate (a rule whose
+  // links all match for every request, RF_CONST / folded, with skipAfter:M,
+  // that no ctl:ruleRemoveById can remove) and M, when no other rule's skip /
+  // skipAfter can land inside.  Their matched-variable reads and macro-key
+  // setvars then cost nothing: the per-request matched-variable state and
+  // dynamic TX area are sized for the reachable rules only.
+  std::vector<bool> dead(P.rules.size(), false);
+  if (P.rule_engine != ENGINE_OFF) {
+    std::vector<std::pair<int64_t, int64_t>> removable;
+    for (const DAction& a : P.acts)
+      if (a.kind == A_CTL_RULE_REMOVE_ID) removable.emplace_back(a.a, a.b);
+    for (int ph = 1; ph <= 2; ph++) {
+      std::vector<uint32_t> w;
+      for (uint32_t ri : P.top)
+        if (P.rules[ri].phase == 0 || P.rules[ri].phase == (uint8_t)ph) w.push_back(ri);
+      std::vector<uint32_t> mpos(P.n_markers, 0xFFFFFFFFu);  // first walk position of each marker
+      for (uint32_t q = 0; q < w.size(); q++) {
+        const int32_t m = P.rules[w[q]].marker;
+        if (m >= 0 && mpos[m] == 0xFFFFFFFFu) mpos[m] = q;
+      }
+      for (uint32_t g = 0; g < w.size(); g++) {
+        const DRule& G = P.rules[w[g]];
+        if (G.skip_after < 0 || (G.flags & RF_MARKER)) continue;
+        // every link matches for every request: constant links, or a folded rule that matched
+        bool always = P.fold_on && in_prefix[w[g]] ? (bool)fmatched[w[g]] : true;
+        for (int32_t ci = (int32_t)w[g]; always && ci >= 0 && !(P.fold_on && in_prefix[w[g]]); ci = P.rules[ci].chain_next)
+          always = (P.rules[ci].flags & RF_CONST) && P.rules[ci]._pad2 > 0;
+        if (!always) continue;
+        for (const auto& rg : removable)
+          if (G.id != 0 && rg.first <= G.id && G.id <= rg.second) always = false;
+        const uint32_t me = G.skip_after < (int32_t)P.n_markers ? mpos[G.skip_after] : 0xFFFFFFFFu;
+        if (!always || me == 0xFFFFFFFFu || me <= g + 1) continue;
+        // nothing outside (g, me) lands inside it
+        bool sealed = true;
+        for (uint32_t q = 0; q < w.size() && sealed; q++) {
+          if (q > g && q < me) continue;
+          const DRule& Q = P.rules[w[q]];
+          if (Q.skip_after >= 0 && Q.skip_after < (int32_t)P.n_markers && mpos[Q.skip_after] > g &&
+              mpos[Q.skip_after] < me)
+            sealed = false;
+          if (Q.skip > 0 && q < g && q + (uint32_t)Q.skip >= g) sealed = false;
+        }
+        if (!sealed) continue;
+        for (uint32_t q = g + 1; q < me; q++)
+          for (int32_t ci = (int32_t)w[q]; ci >= 0; ci = P.rules[ci].chain_next) dead[ci] = true;
+      }
+    }
+  }
+  {  // matched-variable readers among the reachable rules
+    bool mv = false;
+    for (uint32_t ri = 0; ri < P.rules.size() && !mv; ri++) {
+      if (dead[ri]) continue;
+      const DRule& d = P.rules[ri];
+      for (uint32_t q = 0; q < d.var_count; q++)
+        if (P.vars[d.var_begin + q].var >= V_MATCHED_VAR) mv = true;
+      if (d.op >= 0 && F.tmpl_mv(P.ops[d.op].tmpl)) mv = true;
+      for (uint32_t q = 0; q < d.act_count; q++) {
+        const DAction& a = P.acts[d.act_begin + q];
+        if ((a.kind == A_SETVAR || a.kind == A_SETVAR_DEL) && (F.tmpl_mv(a.tmpl) || (a.slot < 0 && F.tmpl_mv(a.aux))))
+          mv = true;
+      }
+    }
+    P.mv_used = mv ? 1 : 0;
+  }
+  {  // macro-key setvars in unreachable rules: no dynamic area for them
+    std::vector<int32_t> site_rule(P.dyn_sites.size(), -1);
+    uint32_t k = 0;
+    for (uint32_t q = 0; q < P.acts.size(); q++)
+      if ((P.acts[q].kind == A_SETVAR || P.acts[q].kind == A_SETVAR_DEL) && P.acts[q].slot < 0) {
+        for (uint32_t ri = 0; ri < P.rules.size(); ri++)
+          if (q >= P.rules[ri].act_begin && q < P.rules[ri].act_begin + P.rules[ri].act_count) site_rule[k] = (int32_t)ri;
+        k++;
+      }
+    for (size_t q = 0; q < P.dyn_sites.size(); q++)
+      if (site_rule[q] >= 0 && dead[site_rule[q]]) P.dyn_sites[q].dead = 1;
+  }
+  {  // the plan JSON reports what was folded
+    uint32_t nconst = 0, nconst0 = 0;
+    for (const DRule& d : P.rules)
+      if (d.flags & RF_CONST) {
+        nconst++;
+        nconst0 += d._pad2 == 0;
+      }
+    uint32_t nfrozen = 0;
+    for (bool f : F.frozen) nfrozen += f;
+    uint32_t ndead = 0;
+    for (bool x : dead) ndead += x;
+    uint32_t nfold = 0;
+    for (bool f : in_prefix) nfold += f;
+    if (!P.plan_json.empty() && P.plan_json.back() == '}') {
+      P.plan_json.pop_back();
+      P.plan_json += ",\"fold\":{\"runs\":" + std::to_string(P.fold_runs.size() / 4) + ",\"folded_links\":" +
+                     std::to_string(nfold) + ",\"ids\":" +
+                     std::to_string(P.fold_ids.size()) + ",\"const_links\":" + std::to_string(nconst) +
+                     ",\"const_nomatch\":" + std::to_string(nconst0) + ",\"const_args\":" + std::to_string(n_args) +
+                     ",\"frozen_slots\":" + std::to_string(nfrozen) + ",\"dead_links\":" + std::to_string(ndead) +
+                     ",\"mv_used\":" + std::to_string((int)P.mv_used) + "}}";
+    }
+  }
   P.tx_snap.resize(P.n_slots);
   for (uint32_t sl = 0; sl < P.n_slots; sl++) {
     DSnapSlot z{};
@@ -2679,26 +2792,6 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
     P.tx_snap[sl] = z;
   }
   P.fold_nids = (uint32_t)P.fold_ids.size();
-  {  // the plan JSON reports what was folded
-    uint32_t nconst = 0, nconst0 = 0;
-    for (const DRule& d : P.rules)
-      if (d.flags & RF_CONST) {
-        nconst++;
-        nconst0 += d._pad2 == 0;
-      }
-    uint32_t nfrozen = 0;
-    for (bool f : F.frozen) nfrozen += f;
-    uint32_t nfold = 0;
-    for (bool f : in_prefix) nfold += f;
-    if (!P.plan_json.empty() && P.plan_json.back() == '}') {
-      P.plan_json.pop_back();
-      P.plan_json += ",\"fold\":{\"runs\":" + std::to_string(P.fold_runs.size() / 4) + ",\"folded_links\":" +
-                     std::to_string(nfold) + ",\"ids\":" +
-                     std::to_string(P.fold_nids) + ",\"const_links\":" + std::to_string(nconst) +
-                     ",\"const_nomatch\":" + std::to_string(nconst0) + ",\"const_args\":" + std::to_string(n_args) +
-                     ",\"frozen_slots\":" + std::to_string(nfrozen) + "}}";
-    }
-  }
   if (P.fold_ids.empty()) P.fold_ids.push_back(0);  // a non-empty section (fold_nids is the count)
   if (P.fold_runs.empty()) P.fold_runs.insert(P.fold_runs.end(), {0u, 0u, 0u, 0xFFFFFFFFu});
 }
@@ -2760,6 +2853,7 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
     out->export_names = exports;
     for (auto& e : exports) out->exports.push_back(L.slot(e));
     out->n_slots = (uint32_t)L.slots.size();
+    out->n_markers = (uint32_t)L.markers.size();
     // regex-keyed TX targets: the static slots whose (lowercase) names the key
     // regex matches, listed once here instead of matched per request; keys a
     // macro-key setvar creates at run time are matched by k_eval
@@ -2788,7 +2882,6 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
         out->max_tx_lit = std::max(out->max_tx_lit, n);
       }
     for (const DSnapSlot& z : out->tx_snap) out->max_tx_lit = std::max(out->max_tx_lit, z.len);
-    out->n_markers = (uint32_t)L.markers.size();
     if (out->strpool.empty()) out->strpool.push_back(0);
     if (out->u8pool.empty()) out->u8pool.push_back(0);
     if (out->trans.empty()) out->trans.push_back(0);

@@ -450,7 +450,9 @@ struct DVarRef {
                      // matches in DProgram.txrx; dynamic keys are matched at run time)
   uint8_t residual;  // a body-phase single (REQUEST_BODY, ...) of a phase-A link: phase A does
                      // not see it, so a clear hit bit leaves it for k_eval to test
-  uint8_t _pad[3];
+  uint8_t pre_len;   // TX regex key of the form ^<literal>: the literal's length (slot = its strpool
+                     // offset): run-time keys are matched by a prefix compare instead of the automaton
+  uint8_t _pad[2];
 };
 
 struct DExc {
@@ -522,6 +524,7 @@ struct DDynSite {
   uint8_t hdr_names, hdr_vals, other_coll;  // targets: REQUEST_HEADERS_NAMES, REQUEST_HEADERS, other collections
   uint8_t no_targets;
   uint32_t prefix_off, prefix_len;  // the key template's leading literal (strpool, lowercase)
+  uint32_t dead;                    // the rule is unreachable (behind a constant gate): no area for it
 };
 
 struct DTmplPart {

@@ -3231,9 +3231,9 @@ GI_HD __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
     } else if (p.kind == TP_SINGLE) {
       s = single_val(t, p.single, nb);
     } else if (p.kind == TP_MV) {
-      s = {mv_curval(t.mv), t.mv->cur_vn};
+      if (t.mv) s = {mv_curval(t.mv), t.mv->cur_vn};  // (no state: an unreachable rule, compile.cpp dead)
     } else if (p.kind == TP_MVNAME) {
-      s = {mv_curname(t.mv), t.mv->cur_nn};
+      if (t.mv) s = {mv_curname(t.mv), t.mv->cur_nn};
     } else if (p.kind == TP_HEADER) {
       for (uint32_t f = 0; f < t.nf; f++)
         if (t.fields[f].kind == FK_HEADER && eq_ascii_ci(t.fields[f].k, t.fields[f].kn, P.strpool + p.off, p.len)) {
@@ -3756,7 +3756,12 @@ GI_HD __noinline__ uint32_t run_capture(const DProgram& P, uint32_t* capws, uint
   const DPike pk = P.pikes[pike];
   int32_t caps[GI_PIKE_MAX_SLOTS];
   CapHdr* H = (CapHdr*)capws;
-  if (!pike_match(P.pike_insts + pk.inst_off, P.pike_ranges, pk, v, n, capws + GI_CAPWS_HDR, caps)) return 0;
+  if (pk.whole) {  // (?sm)^.*$: the whole value, without running the VM
+    caps[0] = 0;
+    caps[1] = (int32_t)n;
+  } else if (!pike_match(P.pike_insts + pk.inst_off, P.pike_ranges, pk, v, n, capws + GI_CAPWS_HDR, caps)) {
+    return 0;
+  }
   if (n > cap_t) return GI_REQ_OVERFLOW;
   const uint32_t stride = (cap_t + 15) & ~15u;
   for (uint32_t g = 0; 2 * g < pk.nslot && g < 9; g++) {
@@ -4119,7 +4124,13 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
           if (sl.state == 0) continue;
           nm = de.k;
           nn = de.kn;
-          if (vr.key_mode == 2 && !dfa_match(P, vr.key_dfa, nm, nn, false)) continue;
+          if (vr.key_mode == 2) {
+            if (vr.pre_len) {  // ^literal
+              if (nn < vr.pre_len || !eq_bytes(nm, vr.pre_len, P.strpool + vr.slot, vr.pre_len)) continue;
+            } else if (!dfa_match(P, vr.key_dfa, nm, nn, false)) {
+              continue;
+            }
+          }
         }
         if (key_excluded(t, vr, nm, nn)) continue;
         if (t.nrtgt && R.id != 0 && target_removed(t, R.id, V_TX, nm, nn)) continue;
@@ -4157,6 +4168,7 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
     }
     if (vr.var >= V_MATCHED_VAR) {  // the matched-variable state (t.mv is set: mv_used)
       MvState* m = t.mv;
+      if (!m) continue;  // no state: only unreachable rules read it (compile.cpp fold_program)
       if (vr.var == V_MATCHED_VAR || vr.var == V_MATCHED_VAR_NAME) {
         uint8_t one = '1';
         Str s = vr.count ? Str{&one, 1u}

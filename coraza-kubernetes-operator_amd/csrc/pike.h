@@ -41,6 +41,7 @@ struct DPike {
   uint32_t inst_off, n_inst;
   uint32_t nslot;  // capture slots tracked: 2 x (groups + 1), at most 18 (TX.0-TX.8)
   uint32_t start;
+  uint32_t whole;  // the pattern is (?sm)^.*$: every value matches whole (group 0 = [0, n)), no VM run
 };
 
 // Go regexp/syntax EmptyOp bits

@@ -781,6 +781,7 @@ static const char* request_layout(const Program& PG, uint32_t cap_ws_words, uint
   // this request and the bytes they can store (gi_program.h DDynSite)
   uint64_t dyn_e = 0, dyn_b = 0;
   for (const DDynSite& ds : PG.dyn_sites) {
+    if (ds.dead) continue;  // an unreachable rule's setvar never runs
     const uint64_t raw_all = (uint64_t)q.method.len + q.uri.len + q.proto.len + hdr_bytes + q.body.len;
     uint64_t ex = ds.mm, src = 0;
     if (!ds.no_targets) {
