@@ -67,6 +67,90 @@ bool go_atoi(const std::string& s, int64_t* v) {
   return true;
 }
 
+// @within over a constant argument (a literal, or TX macros the fold resolved):
+// "value is a substring of arg" is a finite language; its DFA is arg's suffix
+// automaton.  Stored as a byte-mode DDfa whose every state accepts except the
+// last (dead, absorbing): k_eval walks the value through it -- O(len(value))
+// instead of a naive substring search of the whole argument.  Returns the DFA
+// id, or -1 (no automaton: the argument is too large).
+int within_dfa(std::vector<DDfa>& dfas, std::vector<uint16_t>& trans, std::vector<uint8_t>& u8pool,
+               const std::string& arg) {
+  struct St {
+    int len, link;
+    int next[256];
+  };
+  if (arg.size() > 8000) return -1;
+  std::vector<St> st;
+  st.reserve(2 * arg.size() + 2);
+  auto fresh = [&](int len) {
+    St x;
+    x.len = len;
+    x.link = -1;
+    for (int& n : x.next) n = -1;
+    st.push_back(x);
+    return (int)st.size() - 1;
+  };
+  fresh(0);
+  int last = 0;
+  for (unsigned char c : arg) {
+    const int cur = fresh(st[last].len + 1);
+    int p = last;
+    while (p != -1 && st[p].next[c] < 0) {
+      st[p].next[c] = cur;
+      p = st[p].link;
+    }
+    if (p == -1) {
+      st[cur].link = 0;
+    } else {
+      const int q = st[p].next[c];
+      if (st[p].len + 1 == st[q].len) {
+        st[cur].link = q;
+      } else {
+        const int clone = fresh(st[p].len + 1);
+        std::copy(st[q].next, st[q].next + 256, st[clone].next);
+        st[clone].link = st[q].link;
+        while (p != -1 && st[p].next[c] == q) {
+          st[p].next[c] = clone;
+          p = st[p].link;
+        }
+        st[q].link = st[cur].link = clone;
+      }
+    }
+    last = cur;
+  }
+  uint8_t cls[256];
+  int ncls = 0;
+  for (int b = 0; b < 256; b++) cls[b] = 0xFF;
+  for (unsigned char c : arg)
+    if (cls[c] == 0xFF) cls[c] = (uint8_t)ncls++;
+  const int other = ncls++;
+  for (int b = 0; b < 256; b++)
+    if (cls[b] == 0xFF) cls[b] = (uint8_t)other;
+  const uint32_t n = (uint32_t)st.size() + 1, dead = (uint32_t)st.size();
+  if (n > 32768 || (uint64_t)n * ncls > (1u << 18)) return -1;
+  DDfa h{};
+  h.n_states = n;
+  h.n_classes = (uint32_t)ncls;
+  h.start = 0;
+  h.accept = dead;  // (not a sticky accept: the dead state; only k_eval's @within walk reads this automaton)
+  h.byte_mode = 1;
+  h.trans_off = (uint32_t)trans.size();
+  int rep[256];  // a byte of each class of the argument
+  for (int b = 0; b < 256; b++)
+    if (cls[b] != other) rep[cls[b]] = b;
+  for (uint32_t q = 0; q < n; q++)
+    for (int c = 0; c < ncls; c++) {
+      const int nx = (q == dead || c == other) ? -1 : st[q].next[rep[c]];
+      trans.push_back((uint16_t)(nx < 0 ? dead : (uint32_t)nx));
+    }
+  h.endacc_off = (uint32_t)u8pool.size();
+  for (uint32_t q = 0; q < n; q++) u8pool.push_back(q == dead ? 0 : 1);
+  h.amap_off = (uint32_t)u8pool.size();
+  for (int b = 0; b < 256; b++) u8pool.push_back(cls[b]);
+  dfas.push_back(h);
+  return (int)dfas.size() - 1;
+}
+
 struct CompileError {
   int code;
   std::string msg;
@@ -1077,6 +1161,7 @@ struct Lower {
         o.has_num = 1;
         o.num = v;
         if (o.kind == OP_CONTAINS) o.dfa = phrase_dfa({lit}, false, "contains:" + lit);
+        if (o.kind == OP_WITHIN) o.dfa = within_dfa(P->dfas, P->trans, P->u8pool, lit);
       }
     }
     P->ops.push_back(o);
@@ -2665,6 +2750,7 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
           if (!go_atoi(lit, &v)) v = 0;
           o.has_num = 1;
           o.num = v;
+          if (o.kind == OP_WITHIN) o.dfa = within_dfa(P.dfas, P.trans, P.u8pool, lit);
           n_args++;
         }
       }

@@ -3675,7 +3675,18 @@ GI_HD __forceinline__ bool eval_op(Tx& t, const DOp& o, const uint8_t* s, uint32
         case OP_STREQ: res = eq_bytes(s, n, a.p, a.n); break;
         case OP_BEGINSWITH: res = n >= a.n && eq_bytes(s, a.n, a.p, a.n); break;
         case OP_ENDSWITH: res = n >= a.n && eq_bytes(s + n - a.n, a.n, a.p, a.n); break;
-        case OP_WITHIN: res = find_bytes(a.p, a.n, s, n) >= 0; break;
+        case OP_WITHIN:
+          if (o.arg_is_lit && o.dfa >= 0) {  // the argument's suffix automaton (compile.cpp within_dfa)
+            const DDfa d = gi_cload(P.dfas, (uint64_t)o.dfa);
+            const uint16_t* tr = P.trans + d.trans_off;
+            const uint8_t* am = P.u8pool + d.amap_off;
+            uint32_t st = d.start;
+            for (uint32_t i = 0; i < n && st != d.accept; i++) st = tr[st * d.n_classes + am[s[i]]];
+            res = st != d.accept;
+          } else {
+            res = find_bytes(a.p, a.n, s, n) >= 0;
+          }
+          break;
       }
     }
   }

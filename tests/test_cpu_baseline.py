@@ -87,3 +87,30 @@ def test_cpu_baseline_threads_agree():
     a, _ = gpuinspect.cpu_baseline_inspect(rs, batch, threads=1)
     b, _ = gpuinspect.cpu_baseline_inspect(rs, batch, threads=7)
     assert (a.verdicts == b.verdicts).all() and (a.matched == b.matched).all()
+
+
+def within_batch():
+    """@within over a constant argument (compile.cpp within_dfa: the argument's
+    suffix automaton) -- substrings, near misses, bytes >= 0x80, empty."""
+    import random
+    import urllib.parse
+    rnd = random.Random(1)
+    arg = "/content-encoding/ /proxy/ /lock-token/ /content-range/ /if/ /x-http-method-override/ GET HEAD POST \x01\xff ab\xc3\xa9"
+    vals = ["", "/proxy/", "/proxy", "proxy/ /", "GET", "get", "/if/ /x", "zz", "\x01\xff", "\xc3\xa9", arg, arg + "x", " "]
+    vals += ["".join(rnd.choice(arg) for _ in range(rnd.randint(1, 6))) for _ in range(300)]
+    vals += [arg[i:j] for i, j in (sorted(rnd.sample(range(len(arg) + 1), 2)) for _ in range(300))]
+    txs = []
+    for v in vals:
+        t = gpuinspect.Transaction(method=b"GET", uri=b"/?a=" + urllib.parse.quote(v.encode("latin-1")).encode())
+        t.add_request_header("Host", "x")
+        txs.append(t)
+    text = ('SecRuleEngine On\nSecAction "id:9,phase:1,pass,setvar:tx.list=%s"\n'
+            'SecRule ARGS "@within %s" "id:1,phase:2,pass,setvar:tx.anomaly_score=+1"\n'
+            'SecRule ARGS "@within %%{tx.list}" "id:2,phase:2,deny,status:403"\n' % (arg[:40], arg))
+    return text, gpuinspect.pack(txs)
+
+
+def test_cpu_baseline_within_automaton():
+    text, batch = within_batch()
+    res = _check(text, batch)
+    assert int((res.verdicts["status"] == 403).sum()) > 50

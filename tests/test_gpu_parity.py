@@ -550,3 +550,15 @@ def test_gpu_macro_key_setvar_chains(ruleset):
     if ruleset == "crs_pl4":
         assert sum(920451 in x for x in m) >= 4   # Accept-Charset (PL2 extended list)
         assert sum(921180 in x for x in m) >= 2   # repeated parameter names (PL3)
+
+
+def test_gpu_within_automaton():
+    """@within over a literal / folded-constant argument runs the argument's
+    suffix automaton on the device (compile.cpp within_dfa)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("tcb", os.path.join(ROOT, "tests", "test_cpu_baseline.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    text, batch = m.within_batch()
+    res = _parity(text, batch)
+    assert int((res.verdicts["status"] == 403).sum()) > 50
