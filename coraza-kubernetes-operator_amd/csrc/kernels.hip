@@ -3274,38 +3274,38 @@ GI_HD __forceinline__ uint8_t* dyn_alloc(uint8_t* d, uint32_t n) {
   return p;
 }
 
-// The slot of a macro-key setvar: the key is expanded and lowercased
-// [upstream setvar.go: strings.ToLower of the expanded key; ASCII here, like
-// the compiler's static TX names]; a key that names a static slot is that
-// slot, otherwise the dynamic entry with that key (created unless delete).
-GI_HD __noinline__ Slot* dyn_slot(Tx& t, const DAction& a, bool create) {
-  const DProgram& P = *t.P;
-  bool pers;
-  const Str k = expand(t, a.aux, &pers);
-  if (t.flags & GI_REQ_OVERFLOW) return nullptr;
-  uint8_t* kp = (uint8_t*)k.p;  // the macro scratch (a key with a macro is never a persistent literal)
-  for (uint32_t i = 0; i < k.n; i++) kp[i] = alower(kp[i]);
-  const uint32_t h = gi_fnv1a(kp, k.n, false);
+// The slot of a macro-key setvar, given its expanded key in kp (lowercased
+// here) [upstream setvar.go: strings.ToLower of the expanded key; ASCII, like
+// the compiler's static TX names]: a key that names a static slot returns
+// *sid = that slot; otherwise the dynamic entry with that key (created unless
+// delete).  *ovf: the area is full.  No Tx& parameter: a non-inlined callee
+// taking the Tx by reference would force k_eval's Tx out of registers.
+GI_HD __noinline__ Slot* dyn_lookup(const DProgram& P, uint8_t* dyn, uint8_t* kp, uint32_t kn, bool create,
+                                    int32_t* sid, bool* ovf) {
+  for (uint32_t i = 0; i < kn; i++) kp[i] = alower(kp[i]);
+  const uint32_t h = gi_fnv1a(kp, kn, false);
   for (uint32_t i = h & P.slot_hash_mask;; i = (i + 1) & P.slot_hash_mask) {
     const uint32_t e = P.slot_hash[i];
     if (!e) break;
-    const uint32_t sid = e - 1;
-    if (eq_bytes(P.strpool + P.slot_names[2 * sid], P.slot_names[2 * sid + 1], kp, k.n)) return &slot_wr(t, sid);
+    if (eq_bytes(P.strpool + P.slot_names[2 * (e - 1)], P.slot_names[2 * (e - 1) + 1], kp, kn)) {
+      *sid = (int32_t)(e - 1);
+      return nullptr;
+    }
   }
-  DynHdr* H = (DynHdr*)t.dyn;
-  DynEnt* E = dyn_ents(t.dyn);
+  DynHdr* H = (DynHdr*)dyn;
+  DynEnt* E = dyn_ents(dyn);
   for (uint32_t j = 0; j < H->n; j++)
-    if (E[j].h == h && eq_bytes(E[j].k, E[j].kn, kp, k.n)) return &E[j].s;
+    if (E[j].h == h && eq_bytes(E[j].k, E[j].kn, kp, kn)) return &E[j].s;
   if (!create) return nullptr;
-  uint8_t* kb = H->n < H->cap ? dyn_alloc(t.dyn, k.n) : nullptr;
+  uint8_t* kb = H->n < H->cap ? dyn_alloc(dyn, kn) : nullptr;
   if (!kb) {
-    t.flags |= GI_REQ_OVERFLOW;
+    *ovf = true;
     return nullptr;
   }
-  for (uint32_t i = 0; i < k.n; i++) kb[i] = kp[i];
+  for (uint32_t i = 0; i < kn; i++) kb[i] = kp[i];
   DynEnt& ne = E[H->n++];
   ne.k = kb;
-  ne.kn = k.n;
+  ne.kn = kn;
   ne.h = h;
   ne.s.num = 0;
   ne.s.n = 0;
@@ -3315,7 +3315,22 @@ GI_HD __noinline__ Slot* dyn_slot(Tx& t, const DAction& a, bool create) {
 
 // setvar [upstream internal/actions/setvar.go]
 GI_HD __forceinline__ void run_setvar(Tx& t, const DAction& a) {
-  Slot* slp = a.slot >= 0 ? &slot_wr(t, (uint32_t)a.slot) : dyn_slot(t, a, a.kind == A_SETVAR);
+  Slot* slp;
+  if (a.slot >= 0) {
+    slp = &slot_wr(t, (uint32_t)a.slot);
+  } else {  // a key with a macro: expanded into the macro scratch, then looked up
+    bool kpers;
+    const Str k = expand(t, a.aux, &kpers);
+    if (t.flags & GI_REQ_OVERFLOW) return;
+    int32_t sid = -1;
+    bool ovf = false;
+    slp = dyn_lookup(*t.P, t.dyn, (uint8_t*)k.p, k.n, a.kind == A_SETVAR, &sid, &ovf);
+    if (ovf) {
+      t.flags |= GI_REQ_OVERFLOW;
+      return;
+    }
+    if (sid >= 0) slp = &slot_wr(t, (uint32_t)sid);
+  }
   if (!slp) return;
   Slot& sl = *slp;
   if (a.kind == A_SETVAR_DEL) {

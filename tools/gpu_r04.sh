@@ -11,7 +11,7 @@ TAG=${TAG:-r04}
 step() { echo "== $1 $(date +%T)"; }
 if [ -n "${FIRST:-}" ]; then
   step first
-  timeout -k 10 300 python -u -m pytest $FIRST -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_first.log 2>&1 || { tail -40 gpurun_out/${TAG}_first.log; exit 1; }
+  timeout -k 10 300 python -u -m pytest $FIRST ${FIRST_K:+-k "$FIRST_K"} -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_first.log 2>&1 || { tail -40 gpurun_out/${TAG}_first.log; exit 1; }
   tail -1 gpurun_out/${TAG}_first.log
 fi
 if [ "${SUITE:-1}" = "1" ]; then
@@ -46,3 +46,14 @@ if [ "${PROF:-0}" = "1" ]; then
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_prof -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $R/gpurun_out/${TAG}_prof_bench.json 2>$R/gpurun_out/${TAG}_prof_bench.err) || { tail -5 gpurun_out/${TAG}_prof_bench.err; exit 1; }
 fi
 echo done
+if [ "${TRAFFIC:-0}" = "1" ]; then
+  step traffic
+  timeout -k 10 400 python -u tools/pmc_traffic.py --config c2 --n-req 1000000 --tag ${TAG} --out gpurun_out/${TAG}_traffic_c2.json > gpurun_out/${TAG}_traffic.log 2>&1 || { tail -20 gpurun_out/${TAG}_traffic.log; exit 1; }
+  tail -3 gpurun_out/${TAG}_traffic.log
+fi
+if [ "${OCC:-0}" = "1" ]; then
+  step occupancy
+  timeout -k 10 400 python -u tools/pmc_occupancy.py --config c2 --n-req 1000000 --out gpurun_out/${TAG}_pmc_c2.json > gpurun_out/${TAG}_occ.log 2>&1 || { tail -20 gpurun_out/${TAG}_occ.log; exit 1; }
+  cat gpurun_out/${TAG}_occ.log
+fi
+echo done2
