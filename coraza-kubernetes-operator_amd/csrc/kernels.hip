@@ -5836,8 +5836,15 @@ __device__ void union_accept(const DProgram& P, const DBatch& B, uint32_t r, con
 }
 
 // End of a value: end-of-input matches of every automaton (negation applied).
-__device__ void value_end(const DProgram& P, const DBatch& B, uint32_t r, const DJob& J, const uint8_t* img,
+// The value's hits are committed together: its item record and request layout
+// are read once, its value-signature bits go out in one atomicOr, and the hit
+// words of slots < 128 are ORed per word first (one atomic per touched word
+// instead of one per hit).  The exact hit-set keys stay one per hit.
+__device__ void value_end(const DProgram& P, const DBatch& B, uint32_t idx, const DJob& J, const uint8_t* img,
                           uint32_t nf, uint32_t K, uint64_t fm, const uint32_t* st) {
+  uint32_t r = 0, vix = GI_NO_VIX, vbits = 0, hw0 = 0, hw1 = 0, hw2 = 0, hw3 = 0;
+  bool any = false;
+  ReqLayout L{};
   for (uint32_t q = 0; q < K; q++) {
     const DJobDfa jd = gi_cload(P.jdfas, J.jdfa_begin + q);
     GI_BOUND(st[q] < P.dfas[jd.dfa].n_states, st[q], q);
@@ -5847,8 +5854,38 @@ __device__ void value_end(const DProgram& P, const DBatch& B, uint32_t r, const 
     uint64_t bits;
     if (d.multi) bits = *(const uint64_t*)(img + jd.lds_endacc + 8 * st[q]);
     else bits = img[jd.lds_endacc + st[q]] ? 1ull : 0ull;
-    const uint64_t x = (bits ^ jd.neg_mask) & al;
-    if (x) emit_img(B, r, img, jd.lds_slots, x);
+    uint64_t x = (bits ^ jd.neg_mask) & al;
+    if (x && !any) {
+      any = true;
+      GI_BOUND(idx < B.items_cap, idx, B.items_cap);
+      const uint2 rm = *(const uint2*)((const uint8_t*)B.items + 32ull * idx + 24);  // (req, meta)
+      r = rm.x;
+      vix = meta_vix(rm.y);
+      if (vix != GI_NO_VIX) L = B.layout[r];
+    }
+    while (x) {
+      const int k = __ffsll((unsigned long long)x) - 1;
+      x &= x - 1;
+      const uint32_t slot = *(const uint32_t*)(img + jd.lds_slots + 4 * k);
+      const uint32_t bit = 1u << (slot & 31);
+      vbits |= bit;
+      const uint32_t w = slot >> 5;
+      hw0 |= w == 0 ? bit : 0u;
+      hw1 |= w == 1 ? bit : 0u;
+      hw2 |= w == 2 ? bit : 0u;
+      hw3 |= w == 3 ? bit : 0u;
+      if (w >= 4) set_hit(B, slot, r);
+      if (vix != GI_NO_VIX && L.hset_mask) hset_insert(B, L, slot, vix, 0u);
+    }
+  }
+  if (!any) return;
+  if (hw0) atomicOr(&B.hits[r], hw0);
+  if (hw1) atomicOr(&B.hits[(uint64_t)B.rstride + r], hw1);
+  if (hw2) atomicOr(&B.hits[2ull * B.rstride + r], hw2);
+  if (hw3) atomicOr(&B.hits[3ull * B.rstride + r], hw3);
+  if (vix != GI_NO_VIX) {
+    GI_BOUND(vix < L.vmap_bits, vix, L.vmap_bits);
+    atomicOr(&B.vmap[L.vmap_bit + vix], vbits);  // the value's slot signature
   }
 }
 
