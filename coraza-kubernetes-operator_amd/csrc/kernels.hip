@@ -3016,105 +3016,298 @@ GI_HD inline bool valid_encoded_path_char(uint8_t c) {
 }
 
 // ProcessURI [upstream corazawaf/transaction.go] + Go net/url Parse/String
+// Go net/url shouldEscape for the host and userinfo modes (path: should_escape_path)
+GI_HD inline bool should_escape_host(uint8_t c) {
+  if (isalnum_(c)) return false;
+  switch (c) {
+    case '!': case '$': case '&': case '\'': case '(': case ')': case '*': case '+': case ',': case ';':
+    case '=': case ':': case '[': case ']': case '<': case '>': case '"':
+    case '-': case '_': case '.': case '~':
+      return false;
+  }
+  return true;
+}
+GI_HD inline bool should_escape_user(uint8_t c) {
+  if (isalnum_(c)) return false;
+  switch (c) {
+    case '-': case '_': case '.': case '~': return false;
+    case '$': case '&': case '+': case ',': case ';': case '=': return false;
+    case '/': case ':': case '?': case '@': return true;
+  }
+  return true;
+}
+// net/url unescape's validation pass: mode 0 path / userinfo, 1 host (%XX only
+// for non-ASCII bytes or %25; no ASCII byte the host mode escapes)
+GI_HD inline bool url_unescape_ok(const uint8_t* s, uint32_t n, int mode) {
+  for (uint32_t i = 0; i < n;) {
+    if (s[i] == '%') {
+      if (i + 2 >= n || !ishex(s[i + 1]) || !ishex(s[i + 2])) return false;
+      if (mode == 1 && hexv(s[i + 1]) < 8 && !(s[i + 1] == '2' && s[i + 2] == '5')) return false;
+      i += 3;
+    } else {
+      if (mode == 1 && s[i] < 0x80 && should_escape_host(s[i])) return false;
+      i++;
+    }
+  }
+  return true;
+}
+GI_HD inline uint32_t url_unescape(const uint8_t* s, uint32_t n, uint8_t* d) {
+  uint32_t o = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (s[i] == '%') {
+      d[o++] = x2c(s[i + 1], s[i + 2]);
+      i += 2;
+    } else {
+      d[o++] = s[i];
+    }
+  }
+  return o;
+}
+// escape(s, mode) appended at d (mode 0 path, 1 host, 2 userinfo); returns the length
+GI_HD inline uint32_t url_escape(const uint8_t* s, uint32_t n, int mode, uint8_t* d) {
+  const char* hx = "0123456789ABCDEF";
+  uint32_t o = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t c = s[i];
+    const bool e = mode == 0 ? should_escape_path(c) : mode == 1 ? should_escape_host(c) : should_escape_user(c);
+    if (e) {
+      d[o++] = '%';
+      d[o++] = hx[c >> 4];
+      d[o++] = hx[c & 15];
+    } else {
+      d[o++] = c;
+    }
+  }
+  return o;
+}
+GI_HD inline bool valid_port(const uint8_t* s, uint32_t n) {  // "" or ":" digits
+  if (n == 0) return true;
+  if (s[0] != ':') return false;
+  for (uint32_t i = 1; i < n; i++)
+    if (s[i] < '0' || s[i] > '9') return false;
+  return true;
+}
+
+// [upstream corazawaf/transaction.go ProcessURI + Go net/url Parse / String]:
+// REQUEST_URI_RAW; the '#'-stripped target through url.Parse: REQUEST_URI =
+// URL.String(), REQUEST_FILENAME = URL.Path, QUERY_STRING = URL.RawQuery,
+// ARGS_GET; a Parse error leaves REQUEST_URI / REQUEST_FILENAME = the target
+// and no GET args.  Every form Parse accepts: origin, absolute
+// ("http://user@h:80/p"), scheme-relative ("//h/p"), asterisk, opaque
+// ("mailto:x"), relative ("a/b").  An IPv6 zone ("[fe80::1%25en0]") sets
+// GI_REQ_UNSUPPORTED_URI (the oracle flags it the same way).
 GI_HD bool process_uri(Tx& t, const uint8_t* uri, uint32_t un) {
   t.single[S_REQUEST_URI_RAW] = {uri, un};
   uint32_t n = un;
   for (uint32_t i = 0; i < un; i++)
     if (uri[i] == '#') { n = i; break; }
-  bool ctl = false;
-  for (uint32_t i = 0; i < n; i++)
-    if (uri[i] < 0x20 || uri[i] == 0x7F) { ctl = true; break; }
   Str path{uri, n}, query{uri, 0};
-  if (ctl) {
-    t.single[S_REQUEST_URI] = {uri, n};
-  } else if (n == 1 && uri[0] == '*') {
+  bool err = false;
+  for (uint32_t i = 0; i < n; i++)
+    if (uri[i] < 0x20 || uri[i] == 0x7F) { err = true; break; }
+  if (!err && n == 1 && uri[0] == '*') {
     t.single[S_REQUEST_URI] = {uri, 1};
-  } else {
-    if (n == 0 || uri[0] != '/' || (n >= 2 && uri[1] == '/')) {
-      t.flags |= GI_REQ_UNSUPPORTED_URI;
-      return false;
+  } else if (!err) {
+    // getScheme
+    uint32_t sn = 0, r0 = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint8_t c = uri[i];
+      if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z')) continue;
+      if ((c >= '0' && c <= '9') || c == '+' || c == '-' || c == '.') {
+        if (i == 0) break;
+        continue;
+      }
+      if (c == ':') {
+        if (i == 0) err = true;
+        sn = i;
+        r0 = i + 1;
+      }
+      break;
     }
+    // rest = uri[r0, n): RawQuery (ForceQuery when the only '?' ends it)
     uint32_t nq = 0, q = n;
-    for (uint32_t i = 0; i < n; i++)
+    for (uint32_t i = r0; i < n; i++)
       if (uri[i] == '?') {
         if (q == n) q = i;
         nq++;
       }
-    bool force_q = n > 0 && uri[n - 1] == '?' && nq == 1;
-    uint32_t rest_n = q;
-    if (force_q) {
-      query = {uri + n, 0};
-    } else if (q < n) {
-      query = {uri + q + 1, n - q - 1};
-    }
-    // strict unescape(rest, encodePath)
-    bool bad = false, has_pct = false;
-    for (uint32_t i = 0; i < rest_n; i++)
-      if (uri[i] == '%') {
-        has_pct = true;
-        if (i + 2 >= rest_n || !ishex(uri[i + 1]) || !ishex(uri[i + 2])) { bad = true; break; }
-        i += 2;
+    const bool force_q = n > r0 && uri[n - 1] == '?' && nq == 1;
+    const uint8_t* rest = uri + r0;
+    uint32_t rn = q - r0;
+    if (force_q) query = {uri + n, 0};
+    else if (q < n) query = {uri + q + 1, n - q - 1};
+    const uint32_t tail = (force_q || query.n) ? 1 + query.n : 0u;
+    const uint8_t* hostp = nullptr;
+    uint32_t hn = 0, un_ = 0;
+    const uint8_t* userp = nullptr;  // userinfo (escaped form, String()) / its length
+    bool has_user = false, omit_host = false, opaque = false, had_auth = false;
+    if (!err && !(rn > 0 && rest[0] == '/')) {
+      if (sn) {
+        opaque = true;
+      } else {
+        for (uint32_t i = 0; i < rn && rest[i] != '/'; i++)
+          if (rest[i] == ':') { err = true; break; }
       }
-    if (bad) {
-      t.single[S_REQUEST_URI] = {uri, n};
-      path = {uri, n};
-      query = {uri, 0};
-    } else {
-      const uint8_t* p = uri;
-      uint32_t pn = rest_n;
-      if (has_pct) {
-        uint8_t* dp = tx_alloc(t, rest_n);
-        if (!dp) return false;
-        uint32_t o = 0;
-        for (uint32_t i = 0; i < rest_n; i++) {
-          if (uri[i] == '%') {
-            dp[o++] = x2c(uri[i + 1], uri[i + 2]);
-            i += 2;
-          } else {
-            dp[o++] = uri[i];
+    }
+    if (!err && !opaque) {
+      if ((sn || !(rn >= 3 && rest[0] == '/' && rest[1] == '/' && rest[2] == '/')) && rn >= 2 && rest[0] == '/' &&
+          rest[1] == '/') {
+        had_auth = true;
+        const uint8_t* au = rest + 2;
+        uint32_t an = rn - 2;
+        bool slash = false;
+        for (uint32_t i = 0; i < an; i++)
+          if (au[i] == '/') {
+            rest = au + i;
+            rn = an - i;
+            an = i;
+            slash = true;
+            break;
+          }
+        if (!slash) {  // no '/' after the authority: the path is empty
+          rest = au + an;
+          rn = 0;
+        }
+        // parseAuthority: userinfo '@' host
+        int64_t at = -1;
+        for (uint32_t i = 0; i < an; i++)
+          if (au[i] == '@') at = i;
+        const uint8_t* h = at >= 0 ? au + at + 1 : au;
+        const uint32_t hl = at >= 0 ? an - (uint32_t)at - 1 : an;
+        // parseHost
+        if (hl > 0 && h[0] == '[') {
+          int64_t rb = -1;
+          for (uint32_t i = 0; i < hl; i++)
+            if (h[i] == ']') rb = i;
+          if (rb < 0 || !valid_port(h + rb + 1, hl - (uint32_t)rb - 1)) err = true;
+          for (uint32_t i = 0; !err && i + 2 < (uint32_t)rb; i++)
+            if (h[i] == '%' && h[i + 1] == '2' && h[i + 2] == '5') {  // RFC 6874 zone: not restated
+              t.flags |= GI_REQ_UNSUPPORTED_URI;
+              return false;
+            }
+        } else {
+          int64_t co = -1;
+          for (uint32_t i = 0; i < hl; i++)
+            if (h[i] == ':') co = i;
+          if (co >= 0 && !valid_port(h + co, hl - (uint32_t)co)) err = true;
+        }
+        if (!err && !url_unescape_ok(h, hl, 1)) err = true;
+        if (!err) {
+          uint8_t* hd = tx_alloc(t, hl);
+          if (!hd && hl) return false;
+          hn = url_unescape(h, hl, hd);
+          hostp = hd;
+        }
+        if (!err && at >= 0) {  // validUserinfo, then unescape + escape of user [":" password]
+          const uint32_t ul = (uint32_t)at;
+          for (uint32_t i = 0; i < ul && !err; i++) {
+            const uint8_t c = au[i];
+            bool okc = isalnum_(c);
+            switch (c) {
+              case '-': case '.': case '_': case ':': case '~': case '!': case '$': case '&': case '\'': case '(':
+              case ')': case '*': case '+': case ',': case ';': case '=': case '%': case '@':
+                okc = true;
+            }
+            if (!okc) err = true;
+          }
+          int64_t co = -1;
+          for (uint32_t i = 0; i < ul && co < 0; i++)
+            if (au[i] == ':') co = i;
+          const uint32_t n1 = co >= 0 ? (uint32_t)co : ul;
+          if (!err && (!url_unescape_ok(au, n1, 0) || (co >= 0 && !url_unescape_ok(au + co + 1, ul - n1 - 1, 0))))
+            err = true;
+          if (!err) {
+            uint8_t* tmp = tx_alloc(t, ul);
+            uint8_t* ue = tx_alloc(t, 3 * ul + 1);
+            if ((!tmp && ul) || !ue) return false;
+            uint32_t k = url_escape(tmp, url_unescape(au, n1, tmp), 2, ue);
+            if (co >= 0) {
+              ue[k++] = ':';
+              const uint32_t m = url_unescape(au + co + 1, ul - n1 - 1, tmp);
+              k += url_escape(tmp, m, 2, ue + k);
+            }
+            userp = ue;
+            un_ = k;
+            has_user = true;
           }
         }
-        p = dp;
-        pn = o;
+      } else if (sn && rn > 0 && rest[0] == '/') {
+        omit_host = true;
       }
-      parse_query(t, query.p, query.n, FK_ARG_GET);
-      // EscapedPath: rest if escape(path) == rest or validEncoded(rest), else escape(path)
-      bool valid = true;
-      for (uint32_t i = 0; i < rest_n; i++)
-        if (!valid_encoded_path_char(uri[i])) { valid = false; break; }
+    }
+    if (!err && !opaque && !url_unescape_ok(rest, rn, 0)) err = true;
+    if (!err) {
+      // Path (decoded) and EscapedPath (the raw path when it encodes Path, else escape(Path))
+      const uint8_t* p = rest;
+      uint32_t pn = rn;
+      bool has_pct = false;
+      for (uint32_t i = 0; i < rn && !opaque; i++) has_pct |= rest[i] == '%';
+      if (opaque) {
+        p = rest;
+        pn = 0;
+      } else if (has_pct) {
+        uint8_t* dp = tx_alloc(t, rn);
+        if (!dp) return false;
+        pn = url_unescape(rest, rn, dp);
+        p = dp;
+      }
+      bool raw_ok = true;
+      for (uint32_t i = 0; i < rn && !opaque; i++)
+        if (!valid_encoded_path_char(rest[i])) { raw_ok = false; break; }
       uint32_t esc_len = 0;
       for (uint32_t i = 0; i < pn; i++) esc_len += should_escape_path(p[i]) ? 3 : 1;
-      bool same = false;
-      if (!valid && esc_len == rest_n) {
-        same = true;
+      if (!raw_ok && !opaque && esc_len == rn) {  // escape(Path) == raw path
+        raw_ok = true;
         uint32_t o = 0;
         const char* hx = "0123456789ABCDEF";
-        for (uint32_t i = 0; i < pn && same; i++) {
+        for (uint32_t i = 0; i < pn && raw_ok; i++) {
           if (should_escape_path(p[i])) {
-            same = uri[o] == '%' && uri[o + 1] == hx[p[i] >> 4] && uri[o + 2] == hx[p[i] & 15];
+            raw_ok = rest[o] == '%' && rest[o + 1] == hx[p[i] >> 4] && rest[o + 2] == hx[p[i] & 15];
             o += 3;
           } else {
-            same = uri[o] == p[i];
+            raw_ok = rest[o] == p[i];
             o++;
           }
         }
       }
-      if (valid || same) {
-        // String() reproduces the fragment-stripped input: rest + "?" + query
+      const uint32_t en = opaque ? 0u : raw_ok ? rn : esc_len;
+      if (!sn && !had_auth && raw_ok && !opaque) {
+        // a path (origin-form) target: String() is the target itself (a
+        // relative one with ':' in its first segment failed Parse above)
         t.single[S_REQUEST_URI] = {uri, n};
       } else {
-        const uint32_t tail = (force_q || query.n) ? 1 + query.n : 0;
-        uint8_t* o = tx_alloc(t, esc_len + tail);
+        uint8_t* o = tx_alloc(t, sn + 1 + (opaque ? rn : 0) + 2 + un_ + 1 + 3 * hn + 3 + en + tail);
         if (!o) return false;
         uint32_t k = 0;
-        const char* hx = "0123456789ABCDEF";
-        for (uint32_t i = 0; i < pn; i++) {
-          if (should_escape_path(p[i])) {
-            o[k++] = '%';
-            o[k++] = hx[p[i] >> 4];
-            o[k++] = hx[p[i] & 15];
+        for (uint32_t i = 0; i < sn; i++) o[k++] = alower(uri[i]);
+        if (sn) o[k++] = ':';
+        if (opaque) {
+          for (uint32_t i = 0; i < rn; i++) o[k++] = rest[i];
+        } else {
+          if ((sn || hn || has_user) && !(omit_host && !hn && !has_user)) {
+            if (hn || pn || has_user) {
+              o[k++] = '/';
+              o[k++] = '/';
+            }
+            if (has_user) {
+              for (uint32_t i = 0; i < un_; i++) o[k++] = userp[i];
+              o[k++] = '@';
+            }
+            k += url_escape(hostp, hn, 1, o + k);
+          }
+          if (en && (raw_ok ? rest[0] : (should_escape_path(p[0]) ? (uint8_t)'%' : p[0])) != '/' && hn) o[k++] = '/';
+          if (k == 0) {  // a first segment with ':' would read as a scheme
+            bool colon = false;
+            for (uint32_t i = 0; i < pn && p[i] != '/'; i++) colon |= p[i] == ':';
+            if (colon) {
+              o[k++] = '.';
+              o[k++] = '/';
+            }
+          }
+          if (raw_ok) {
+            for (uint32_t i = 0; i < rn; i++) o[k++] = rest[i];
           } else {
-            o[k++] = p[i];
+            k += url_escape(p, pn, 0, o + k);
           }
         }
         if (tail) {
@@ -3123,8 +3316,14 @@ GI_HD bool process_uri(Tx& t, const uint8_t* uri, uint32_t un) {
         }
         t.single[S_REQUEST_URI] = {o, k};
       }
+      parse_query(t, query.p, query.n, FK_ARG_GET);
       path = {p, pn};
     }
+  }
+  if (err) {
+    t.single[S_REQUEST_URI] = {uri, n};
+    path = {uri, n};
+    query = {uri, 0};
   }
   t.single[S_REQUEST_FILENAME] = path;
   t.single[S_QUERY_STRING] = query;

@@ -729,7 +729,8 @@ static const char* request_layout(const Program& PG, uint32_t cap_ws_words, uint
     z.mp = multipart;
   }
   uint64_t cap_f = q.hdr_count + (q.uri.len / 2 + 2) + (cookie / 2 + 2 * ncookie) + post_fields;
-  uint64_t cap_b = 4ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96 + 16;  // + REMOTE_PORT
+  // + REMOTE_PORT; the URI: REQUEST_LINE, decoded path / host / userinfo, String() (<= 3x each part)
+  uint64_t cap_b = 12ull * q.uri.len + q.method.len + q.proto.len + q.body.len + 96 + 16;
   // multipart: canonical keys, joined continuation lines, "Key: value"
   // strings and unescaped parameters are each at most the part header
   // bytes; sizes 24 B per part
@@ -851,9 +852,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   uint64_t hset_words = 0;
   uint32_t n_mp_body = 0;
   uint32_t max_cap_t = 64;
-  const uint32_t nslots = c->rs->prog.n_slots;
   const Program& PG = c->rs->prog;
-  const uint32_t n_single_items = (uint32_t)__builtin_popcount(PG.item_singles);
   // per-request sizes (in parallel on the host cores for large batches),
   // then the running offsets (region, value map, hit set) in one serial pass
   using Sizes = LayoutSizes;
@@ -1498,6 +1497,12 @@ int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results
           B.layout = &L;
           B.verdicts = out->verdicts + r;
           B.matched = out->matched_ids + (uint64_t)r * out->matched_cap;
+          if (out->captures && out->capture_bytes && out->capture_cap) {  // capture records, as gi_fetch_results
+            B.caprec = (uint32_t*)(out->captures + (uint64_t)r * out->capture_cap);
+            B.capbytes = out->capture_bytes + (uint64_t)r * out->capture_bytes_cap;
+            B.crcap = out->capture_cap;
+            B.cbcap = out->capture_bytes_cap;
+          }
           B.txslots = (Slot*)txs.data();
           cpu_inspect_one(np, B);
         }

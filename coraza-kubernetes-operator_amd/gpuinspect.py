@@ -526,7 +526,8 @@ class Results:
         return int(self.verdicts[i]["tx_export"][self.exports.index(name)])
 
 
-def cpu_baseline_inspect(ruleset: "Ruleset", batch, threads: int = 0, matched_cap: int = 64):
+def cpu_baseline_inspect(ruleset: "Ruleset", batch, threads: int = 0, matched_cap: int = 64,
+                         capture_cap: int = 0, capture_bytes_cap: int = 512):
     """The CPU baseline (gi_cpu_baseline_inspect): this engine's
     interpreter compiled for the host, `threads` host threads (0: all cores),
     every rule link evaluated without phase A.  Not Coraza, and never a
@@ -538,12 +539,20 @@ def cpu_baseline_inspect(ruleset: "Ruleset", batch, threads: int = 0, matched_ca
     n = batch.n_req
     verd = np.zeros(n, VERDICT_DT)
     matched = np.zeros((n, matched_cap), np.uint32)
-    res = _Results(verd.ctypes.data, matched.ctypes.data, matched_cap, None, None, 0, 0)
+    crec = cbytes = None
+    if capture_cap:
+        crec = np.zeros((n, capture_cap), CAPTURE_DT)
+        cbytes = np.zeros((n, capture_bytes_cap), np.uint8)
+    res = _Results(verd.ctypes.data, matched.ctypes.data, matched_cap,
+                   crec.ctypes.data if capture_cap else None, cbytes.ctypes.data if capture_cap else None,
+                   capture_cap, capture_bytes_cap if capture_cap else 0)
     cb = batch.to_ctypes()
     secs = ctypes.c_double(0.0)
     rc = lib.gi_cpu_baseline_inspect(ruleset._h, ctypes.byref(cb), ctypes.byref(res), threads, ctypes.byref(secs))
     if rc != GI_OK:
         raise EngineError("gi_cpu_baseline_inspect failed (%d)" % rc)
+    if capture_cap:
+        return Results(verd, matched, ruleset.exports, crec, cbytes, ruleset.capture_rules), secs.value
     return Results(verd, matched, ruleset.exports), secs.value
 
 

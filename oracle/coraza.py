@@ -1343,12 +1343,181 @@ def _go_unescape_path(s: bytes):
     return bytes(out)
 
 
-def process_uri(uri: bytes):
-    """Returns dict of URI-derived variables + ARGS_GET list.
+class _GoURLError(ValueError):
+    """net/url.Parse returned an error."""
 
-    Supported subset: origin-form ('/' not followed by '/') and '*'.
-    Anything else raises UnsupportedInput (the GPU engine flags the same
-    requests with GI_REQ_UNSUPPORTED_URI).
+
+def _go_should_escape(c: int, mode: str) -> bool:
+    """net/url shouldEscape for the modes ProcessURI's url.Parse / String use:
+    "path", "host", "user" (encodePath, encodeHost, encodeUserPassword)."""
+    if 65 <= c <= 90 or 97 <= c <= 122 or 48 <= c <= 57:
+        return False
+    if mode == "host" and c in b"!$&'()*+,;=:[]<>\"":
+        return False
+    if c in b"-_.~":
+        return False
+    if c in b"$&+,/:;=?@":
+        if mode == "user":
+            return c in b"@/?:"
+        if mode == "path":
+            return c == 0x3F
+    return True
+
+
+def _go_escape(s: bytes, mode: str) -> bytes:
+    out = bytearray()
+    for c in s:
+        if _go_should_escape(c, mode):
+            out += b"%" + ("%02X" % c).encode()
+        else:
+            out.append(c)
+    return bytes(out)
+
+
+def _go_unescape(s: bytes, mode: str) -> bytes:
+    """net/url unescape (strict: a malformed escape is an error; in a host,
+    %-escapes only for non-ASCII bytes or %25, and no ASCII byte that must be
+    escaped)."""
+    i, n = 0, len(s)
+    while i < n:
+        c = s[i]
+        if c == 0x25:
+            if i + 2 >= n or not _ishex(s[i + 1]) or not _ishex(s[i + 2]):
+                raise _GoURLError("invalid URL escape")
+            if mode == "host" and int(chr(s[i + 1]), 16) < 8 and s[i:i + 3] != b"%25":
+                raise _GoURLError("invalid URL escape")
+            i += 3
+        else:
+            if mode == "host" and c < 0x80 and _go_should_escape(c, "host"):
+                raise _GoURLError("invalid character in host name")
+            i += 1
+    out = bytearray()
+    i = 0
+    while i < n:
+        if s[i] == 0x25:
+            out.append(_x2c(s[i + 1], s[i + 2]))
+            i += 3
+        else:
+            out.append(s[i])
+            i += 1
+    return bytes(out)
+
+
+def _go_valid_port(p: bytes) -> bool:
+    if p == b"":
+        return True
+    return p[:1] == b":" and all(0x30 <= c <= 0x39 for c in p[1:])
+
+
+def _go_parse_host(h: bytes) -> bytes:
+    if h.startswith(b"["):
+        i = h.rfind(b"]")
+        if i < 0:
+            raise _GoURLError("missing ']' in host")
+        if not _go_valid_port(h[i + 1:]):
+            raise _GoURLError("invalid port")
+        if h[:i].find(b"%25") >= 0:
+            # RFC 6874 zone identifiers: not restated (the GPU flags them the same way)
+            raise UnsupportedInput("IPv6 zone in the request-target host")
+    else:
+        i = h.rfind(b":")
+        if i >= 0 and not _go_valid_port(h[i:]):
+            raise _GoURLError("invalid port")
+    return _go_unescape(h, "host")
+
+
+_USER_OK = b"-._:~!$&'()*+,;=%@"
+
+
+def _go_parse_authority(a: bytes):
+    """-> (userinfo string as URL.String() writes it, or None; host)."""
+    i = a.rfind(b"@")
+    host = _go_parse_host(a if i < 0 else a[i + 1:])
+    if i < 0:
+        return None, host
+    ui = a[:i]
+    for c in ui:
+        if not (65 <= c <= 90 or 97 <= c <= 122 or 48 <= c <= 57 or c in _USER_OK):
+            raise _GoURLError("invalid userinfo")
+    if b":" not in ui:
+        return _go_escape(_go_unescape(ui, "user"), "user"), host
+    u, _, pw = ui.partition(b":")
+    return _go_escape(_go_unescape(u, "user"), "user") + b":" + _go_escape(_go_unescape(pw, "user"), "user"), host
+
+
+def _go_url_parse(u: bytes):
+    """[Go net/url] Parse(u) (no fragment: ProcessURI cut it) and String():
+    -> (String(), Path, RawQuery).  Raises _GoURLError where Parse fails."""
+    if u == b"*":
+        return b"*", b"*", b""
+    scheme, rest = b"", u
+    for i, c in enumerate(u):  # getScheme
+        if 65 <= c <= 90 or 97 <= c <= 122:
+            continue
+        if 48 <= c <= 57 or c in b"+-.":
+            if i == 0:
+                break
+            continue
+        if c == 0x3A:
+            if i == 0:
+                raise _GoURLError("missing protocol scheme")
+            scheme, rest = u[:i].lower(), u[i + 1:]
+        break
+    force_q = rest.endswith(b"?") and rest.count(b"?") == 1
+    if force_q:
+        rest, query = rest[:-1], b""
+    else:
+        rest, _, query = rest.partition(b"?")
+    tail = b"?" + query if (force_q or query) else b""
+    if not rest.startswith(b"/"):
+        if scheme:  # rootless: opaque
+            return scheme + b":" + rest + tail, b"", query
+        if b":" in rest.split(b"/", 1)[0]:
+            raise _GoURLError("first path segment in URL cannot contain colon")
+    user, host, omit_host = None, b"", False
+    if (scheme or not rest.startswith(b"///")) and rest.startswith(b"//"):
+        auth, rest = rest[2:], b""
+        j = auth.find(b"/")
+        if j >= 0:
+            auth, rest = auth[:j], auth[j:]
+        user, host = _go_parse_authority(auth)
+    elif scheme and rest.startswith(b"/"):
+        omit_host = True
+    path = _go_unescape(rest, "path")
+    # EscapedPath: the raw path when it is a valid encoding of Path
+    if _go_escape_path(path) == rest or _go_valid_encoded_path(rest):
+        esc = rest
+    else:
+        esc = _go_escape_path(path)
+    out = b""
+    if scheme:
+        out += scheme + b":"
+    if scheme or host or user is not None:
+        if not (omit_host and host == b"" and user is None):
+            if host or path or user is not None:
+                out += b"//"
+            if user is not None:
+                out += user + b"@"
+            if host:
+                out += _go_escape(host, "host")
+    if esc and esc[:1] != b"/" and host:
+        out += b"/"
+    if out == b"" and b":" in esc.split(b"/", 1)[0]:
+        out += b"./"
+    return out + esc + tail, path, query
+
+
+def process_uri(uri: bytes):
+    """[upstream corazawaf/transaction.go ProcessURI]: REQUEST_URI_RAW, then
+    url.Parse of the '#'-stripped target -> REQUEST_URI = URL.String(),
+    REQUEST_FILENAME = URL.Path, QUERY_STRING = URL.RawQuery, ARGS_GET; when
+    url.Parse fails, REQUEST_URI / REQUEST_FILENAME are the target itself and
+    there are no GET args.  Returns (dict of the URI variables, ARGS_GET).
+
+    Every request-target form Parse accepts: origin ("/p?q"), absolute
+    ("http://user@h:80/p"), scheme-relative ("//h/p"), asterisk, opaque
+    ("mailto:x"), relative ("p/q").  Only an IPv6 zone identifier
+    ("[fe80::1%25en0]") raises UnsupportedInput (flagged the same way on the GPU).
     """
     v = {"REQUEST_URI_RAW": uri}
     u = uri
@@ -1356,44 +1525,15 @@ def process_uri(uri: bytes):
     if h >= 0:
         u = u[:h]
     args = []
-    ctl = any(c < 0x20 or c == 0x7F for c in u)
-    if ctl:
+    try:
+        if any(c < 0x20 or c == 0x7F for c in u):
+            raise _GoURLError("invalid control character in URL")
+        s_, path, query = _go_url_parse(u)
+        v["REQUEST_URI"] = s_
+        args = parse_query(query)
+    except _GoURLError:
         v["REQUEST_URI"] = u
-        path = u
-        query = b""
-    elif u == b"*":
-        v["REQUEST_URI"] = b"*"
-        path = b"*"
-        query = b""
-    else:
-        if not u.startswith(b"/") or u.startswith(b"//"):
-            raise UnsupportedInput("non origin-form request URI")
-        q = u.find(b"?")
-        force_q = False
-        if u.endswith(b"?") and u.count(b"?") == 1:
-            force_q = True
-            rest, query = u[:-1], b""
-        elif q >= 0:
-            rest, query = u[:q], u[q + 1:]
-        else:
-            rest, query = u, b""
-        p = _go_unescape_path(rest)
-        if p is None:
-            # url.Parse error -> raw uri, no GET args
-            v["REQUEST_URI"] = u
-            path = u
-            query = b""
-        else:
-            args = parse_query(query)
-            if _go_escape_path(p) == rest or _go_valid_encoded_path(rest):
-                esc = rest
-            else:
-                esc = _go_escape_path(p)
-            s = esc
-            if force_q or query:
-                s += b"?" + query
-            v["REQUEST_URI"] = s
-            path = p
+        path, query = u, b""
     v["REQUEST_FILENAME"] = path
     v["QUERY_STRING"] = query
     off = path.rfind(b"/")

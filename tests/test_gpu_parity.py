@@ -562,3 +562,20 @@ def test_gpu_within_automaton():
     text, batch = m.within_batch()
     res = _parity(text, batch)
     assert int((res.verdicts["status"] == 403).sum()) > 50
+
+
+def test_gpu_uri_forms():
+    """Absolute, scheme-relative, opaque, relative and invalid request-targets
+    through the device's url.Parse / String restatement (k_collect), every
+    URI variable compared through capture records."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("tcb", os.path.join(ROOT, "tests", "test_cpu_baseline.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    text, batch = m.uri_batch()
+    rs = gpuinspect.Ruleset(text)
+    eng = gpuinspect.Engine(rs, capture_cap=16, capture_bytes_cap=4096)
+    res = eng.inspect(batch)
+    orc = compare.oracle_verdicts(coraza.parse_seclang(text), batch, rs.exports)
+    bad = compare.compare(res, orc, max_report=100)
+    assert not bad, bad
