@@ -40,6 +40,11 @@ import shard  # noqa: E402
 import traffic  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+# ds_read_b32 lanes/s with every CU streaming (MI355X_MICROARCH.md: ~75 TB/s
+# aggregate for ds_read_b32, 4 B per lane): one automaton transition of k_scan
+# is one such LDS lane read, so k_scan's transitions/s over this is its LDS
+# (secondary) roofline fraction
+LDS_B32_LANES_PER_S = 75e12 / 4
 
 # launch name (gi_stats) -> kernel name as rocprofv3 reports it
 ROCPROF_NAMES = {
@@ -359,8 +364,13 @@ def main():
                 "launches": {k: {"ms": round(v, 4), "queue_bytes": int(launch_bytes[k]),
                                  "GB/s": round(launch_bytes[k] / (v * 1e-3) / 1e9, 2) if v > 0 else None,
                                  "byte_steps": int(launch_steps.get(k, 0)),
-                                 "byte_steps_per_s": round(launch_steps.get(k, 0) / (v * 1e-3), 1) if v > 0 else None}
-                             for k, v in avg_launch.items()}},
+                                 "byte_steps_per_s": round(launch_steps.get(k, 0) / (v * 1e-3), 1) if v > 0 else None,
+                                 **({"lds_frac": round(launch_steps.get(k, 0) / (v * 1e-3) / LDS_B32_LANES_PER_S, 5)}
+                                    if k.startswith("k_scan") and v > 0 else {})}
+                             for k, v in avg_launch.items()},
+                "lds_peak_lanes_per_s": LDS_B32_LANES_PER_S,
+                "lds_frac_def": "k_scan*: automaton transitions/s (one ds_read_b32 lane each) / the chip's "
+                                "ds_read_b32 lane rate (MI355X_MICROARCH.md: ~75 TB/s)"},
         },
         "tally": {"n_req": int(node_tally["n_req"]), "n_interrupted": int(node_tally["n_interrupted"]),
                   "matched_total": int(node_tally["matched_total"]),

@@ -7089,10 +7089,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_EVAL
 
 // Detail tally: histogram of the exported inbound score (DProgram.hist_mask) and
 // the match count of every rule id, from the verdicts and matched-id rows k_eval
-// wrote.  Lanes walk their request's matched list in step; the lists share
-// long prefixes (the CRS initialisation SecActions match every request), so
-// equal bins are first aggregated across the wave (one LDS atomic per distinct
-// bin per step instead of 64 on one address).
+// wrote.  A wave takes 64 requests: the score bins lane-per-request (equal bins
+// aggregated across the wave: one atomic per distinct bin), then the 64
+// matched-id rows as one flattened list, 64 consecutive entries per step.
 GI_HD __forceinline__ void wave_hist_add(uint32_t* hist, int32_t b) {
   uint64_t active = __ballot(b >= 0);
   while (active) {
@@ -7132,21 +7131,44 @@ __global__ void __launch_bounds__(256) k_tally(DBatch B, const uint32_t* __restr
       sb = (int32_t)min(max(sc, (int64_t)0), (int64_t)(GI_SCORE_BINS - 1));
     }
     wave_hist_add(hist, sb);
-    const uint32_t steps = wave_max(cnt);
-    const uint32_t* row = B.matched + (uint64_t)r * B.mcap;
-    for (uint32_t j = 0; j < steps; j++) {
-      int32_t b = -1;
-      if (j < cnt) {
-        const uint32_t id = row[j];
-        uint32_t lo = 0, hi = n_ids;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (tid[mid] < id) lo = mid + 1;
-          else hi = mid;
+    // The wave's 64 matched-id rows as one flattened list (inclusive prefix of
+    // the counts across the lanes): lane i takes entry base + i, so a wave's
+    // reads walk each row contiguously instead of 64 rows at one column.
+    uint32_t incl = cnt;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane_id() >= o) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    const uint32_t excl = incl - cnt;
+    for (uint32_t base = 0; base < total; base += 64) {
+      const uint32_t j = base + lane_id();
+      uint32_t lo = 0, hi = 63;  // owner: the first lane whose inclusive prefix exceeds j
+      for (int it = 0; it < 6; it++) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint32_t v = __shfl(incl, (int)mid, 64);
+        if (lo < hi) {
+          if (v > j) hi = mid;
+          else lo = mid + 1;
         }
-        if (lo < n_ids && tid[lo] == id) b = (int32_t)(GI_SCORE_BINS + lo);
       }
-      wave_hist_add(hist, b);
+      const uint32_t q_excl = __shfl(excl, (int)lo, 64);
+      int32_t b = -1;
+      if (j < total) {
+        const uint32_t id = B.matched[(uint64_t)(w * 64 + lo) * B.mcap + (j - q_excl)];
+        uint32_t a = 0, e = n_ids;
+        while (a < e) {
+          const uint32_t mid = (a + e) >> 1;
+          if (tid[mid] < id) a = mid + 1;
+          else e = mid;
+        }
+        if (a < n_ids && tid[a] == id) b = (int32_t)(GI_SCORE_BINS + a);
+      }
+      if (lds) {  // the lanes hold a few requests' lists: mostly distinct bins
+        if (b >= 0) atomicAdd(&hist[b], 1u);
+      } else {
+        wave_hist_add(hist, b);
+      }
     }
   }
   if (lds) {
