@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 
 #include "gi_kernels.h"
 #include "html_entities.h"
@@ -72,6 +73,88 @@ GI_HD inline bool isalnum_(uint8_t c) {
   return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z');
 }
 GI_HD inline bool isws(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
+
+// Four bytes at p (any alignment) from two aligned dword loads: long values
+// are read a word per load instead of a byte per load.  May read up to 7
+// bytes past p (every buffer is padded: runtime.cpp).
+GI_HD __forceinline__ uint32_t load_u32u(const uint8_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t lo = w[0];
+  return sh ? __builtin_amdgcn_alignbyte(w[1], lo, sh) : lo;
+#else
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+#endif
+}
+
+// Word-at-a-time byte helpers for the interpreter's per-request strings
+// (k_eval: one lane per request, so every byte access is a scattered memory
+// instruction of its own).  Sources must be padded buffers (the batch data,
+// the request scratch, the program's string pool: runtime.cpp pads each by
+// >= 16 bytes) -- they may read up to 8 bytes past the end; never a stack array.
+GI_HD __forceinline__ uint32_t tail_mask(uint32_t r) { return r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u; }
+// ASCII 'A'-'Z' | 0x20 in each byte of x (other bytes unchanged)
+GI_HD __forceinline__ uint32_t lower4(uint32_t x) {
+  const uint32_t ge_a = (x & 0x7F7F7F7Fu) + 0x3F3F3F3Fu;  // bit 7: byte & 0x7F >= 'A'
+  const uint32_t gt_z = (x & 0x7F7F7F7Fu) + 0x25252525u;  // bit 7: byte & 0x7F > 'Z'
+  return x | (((ge_a ^ gt_z) & ~x & 0x80808080u) >> 2);
+}
+// n bytes s -> d (any alignments): the head up to d's dword alignment and the
+// tail byte-wise, the rest one aligned dword store per 4 bytes.  A source on
+// the stack (a number formatted into a local buffer) is copied byte-wise.
+GI_HD __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint32_t n) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  if (n) memcpy(d, s, n);
+#else
+  uint32_t i = 0;
+  if (n >= 8 && !__builtin_amdgcn_is_private(s)) {
+    const uint32_t head = (4u - ((uint32_t)(uintptr_t)d & 3u)) & 3u;
+    for (; i < head; i++) d[i] = s[i];
+    for (; i + 4 <= n; i += 4) *(uint32_t*)(d + i) = load_u32u(s + i);
+  }
+  for (; i < n; i++) d[i] = s[i];
+#endif
+}
+// the same, ASCII-lowercasing
+GI_HD __forceinline__ void copy_lower(uint8_t* d, const uint8_t* s, uint32_t n) {
+  uint32_t i = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (n >= 8 && !__builtin_amdgcn_is_private(s)) {
+    const uint32_t head = (4u - ((uint32_t)(uintptr_t)d & 3u)) & 3u;
+    for (; i < head; i++) d[i] = alower(s[i]);
+    for (; i + 4 <= n; i += 4) *(uint32_t*)(d + i) = lower4(load_u32u(s + i));
+  }
+#endif
+  for (; i < n; i++) d[i] = alower(s[i]);
+}
+// byte equality of two padded strings, a word per step
+GI_HD __forceinline__ bool eq_bytes_w(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn) {
+  if (an != bn) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (uint32_t i = 0; i < an; i += 4)
+    if ((load_u32u(a + i) ^ load_u32u(b + i)) & tail_mask(an - i)) return false;
+  return true;
+#else
+  return an == 0 || memcmp(a, b, an) == 0;
+#endif
+}
+// gi_fnv1a(s, n, false) over a padded string, a word loaded per 4 bytes
+GI_HD __forceinline__ uint32_t fnv1a_w(const uint8_t* s, uint32_t n) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return gi_fnv1a(s, n, false);
+#endif
+  uint32_t h = 2166136261u;
+  for (uint32_t i = 0; i < n; i += 4) {
+    const uint32_t x = load_u32u(s + i);
+    const uint32_t m = n - i < 4 ? n - i : 4u;
+    for (uint32_t k = 0; k < m; k++) h = (h ^ ((x >> (8 * k)) & 0xFFu)) * 16777619u;
+  }
+  return h;
+}
 
 GI_HD __forceinline__ bool eq_bytes(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn) {
   if (an != bn) return false;
@@ -193,22 +276,6 @@ GI_HD inline uint32_t encode_rune(uint32_t r, uint8_t* o) {
   return 4;
 }
 
-// Four bytes at p (any alignment) from two aligned dword loads: long values
-// are read a word per load instead of a byte per load.  May read up to 7
-// bytes past p (every buffer is padded: runtime.cpp).
-GI_HD __forceinline__ uint32_t load_u32u(const uint8_t* p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(a & 3);
-  const uint32_t lo = w[0];
-  return sh ? __builtin_amdgcn_alignbyte(w[1], lo, sh) : lo;
-#else
-  uint32_t v;
-  __builtin_memcpy(&v, p, 4);
-  return v;
-#endif
-}
 // bit scans the interpreter uses on both targets
 GI_HD __forceinline__ int gi_ffsll(uint64_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1267,11 +1334,11 @@ GI_HD __noinline__ bool mv_record(MvState* m, uint32_t var, const uint8_t* k, ui
   for (uint32_t i = 0; i < vl; i++) cn[i] = (uint8_t)vnm[i];
   if (kn) {
     cn[vl] = ':';
-    for (uint32_t i = 0; i < kn; i++) cn[vl + 1 + i] = k[i];
+    copy_bytes(cn + vl + 1, k, kn);
   }
   m->cur_nn = nn;
   uint8_t* cv = mv_curval(m);
-  for (uint32_t i = 0; i < vn; i++) cv[i] = v[i];
+  copy_bytes(cv, v, vn);
   m->cur_vn = vn;
   if (!m->keep) return true;  // nothing reads this rule's MATCHED_VARS
   // MATCHED_VARS SetIndex(name, 0, value)
@@ -1285,18 +1352,18 @@ GI_HD __noinline__ bool mv_record(MvState* m, uint32_t var, const uint8_t* k, ui
   const uint32_t need = vn + (at == m->n ? nn : 0);
   if (m->nb + need > m->cap_a || (at == m->n && m->n >= m->cap_e)) return false;
   uint8_t* a = mv_arena(m) + m->nb;
-  for (uint32_t i = 0; i < vn; i++) a[i] = v[i];
+  copy_bytes(a, v, vn);
   e[at].v = a;
   e[at].vn = vn;
   if (at == m->n) {
     uint8_t* nm = a + vn;
-    for (uint32_t i = 0; i < nn; i++) nm[i] = cn[i];
+    copy_bytes(nm, cn, nn);
     e[at].name = nm;
     e[at].nn = nn;
     m->n++;
   } else {  // the key as last written (a case-insensitive equal name has the same length)
     uint8_t* nm = (uint8_t*)e[at].name;
-    for (uint32_t i = 0; i < nn; i++) nm[i] = cn[i];
+    copy_bytes(nm, cn, nn);
   }
   m->nb += need;
   return true;
@@ -1606,19 +1673,6 @@ GI_HD uint32_t json_number_end(const uint8_t* s, uint32_t n, uint32_t i) {
   return i;
 }
 
-// d[0, n) = s[0, n), four source bytes per load (s may be read up to 7 bytes
-// past its end: every arena is padded)
-GI_HD __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint32_t n) {
-  uint32_t k = 0;
-  for (; k + 4 <= n; k += 4) {
-    const uint32_t w = load_u32u(s + k);
-    d[k] = (uint8_t)w;
-    d[k + 1] = (uint8_t)(w >> 8);
-    d[k + 2] = (uint8_t)(w >> 16);
-    d[k + 3] = (uint8_t)(w >> 24);
-  }
-  for (; k < n; k++) d[k] = s[k];
-}
 
 GI_HD inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
@@ -3444,7 +3498,7 @@ GI_HD __forceinline__ Str expand(Tx& t, int32_t tid, bool* persistent) {
       t.flags |= GI_REQ_OVERFLOW;
       return {t.mt, 0};
     }
-    for (uint32_t i = 0; i < s.n; i++) t.mt[o + i] = s.p[i];
+    copy_bytes(t.mt + o, s.p, s.n);
     o += s.n;
   }
   return {t.mt, o};
@@ -3481,12 +3535,12 @@ GI_HD __forceinline__ uint8_t* dyn_alloc(uint8_t* d, uint32_t n) {
 // taking the Tx by reference would force k_eval's Tx out of registers.
 GI_HD __noinline__ Slot* dyn_lookup(const DProgram& P, uint8_t* dyn, uint8_t* kp, uint32_t kn, bool create,
                                     int32_t* sid, bool* ovf) {
-  for (uint32_t i = 0; i < kn; i++) kp[i] = alower(kp[i]);
-  const uint32_t h = gi_fnv1a(kp, kn, false);
+  copy_lower(kp, kp, kn);
+  const uint32_t h = fnv1a_w(kp, kn);
   for (uint32_t i = h & P.slot_hash_mask;; i = (i + 1) & P.slot_hash_mask) {
     const uint32_t e = P.slot_hash[i];
     if (!e) break;
-    if (eq_bytes(P.strpool + P.slot_names[2 * (e - 1)], P.slot_names[2 * (e - 1) + 1], kp, kn)) {
+    if (eq_bytes_w(P.strpool + P.slot_names[2 * (e - 1)], P.slot_names[2 * (e - 1) + 1], kp, kn)) {
       *sid = (int32_t)(e - 1);
       return nullptr;
     }
@@ -3494,14 +3548,14 @@ GI_HD __noinline__ Slot* dyn_lookup(const DProgram& P, uint8_t* dyn, uint8_t* kp
   DynHdr* H = (DynHdr*)dyn;
   DynEnt* E = dyn_ents(dyn);
   for (uint32_t j = 0; j < H->n; j++)
-    if (E[j].h == h && eq_bytes(E[j].k, E[j].kn, kp, kn)) return &E[j].s;
+    if (E[j].h == h && eq_bytes_w(E[j].k, E[j].kn, kp, kn)) return &E[j].s;
   if (!create) return nullptr;
   uint8_t* kb = H->n < H->cap ? dyn_alloc(dyn, kn) : nullptr;
   if (!kb) {
     *ovf = true;
     return nullptr;
   }
-  for (uint32_t i = 0; i < kn; i++) kb[i] = kp[i];
+  copy_bytes(kb, kp, kn);
   DynEnt& ne = E[H->n++];
   ne.k = kb;
   ne.kn = kn;
@@ -3613,7 +3667,7 @@ generic:
     dst = t.txa + t.ntx;
     t.ntx += v.n;
   }
-  for (uint32_t i = 0; i < v.n; i++) dst[i] = v.p[i];
+  copy_bytes(dst, v.p, v.n);
   sl.state = 2;
   sl.p = dst;
   sl.n = v.n;
@@ -3993,7 +4047,7 @@ GI_HD __noinline__ uint32_t run_capture(const DProgram& P, uint32_t* capws, uint
     const int32_t a = caps[2 * g], b = caps[2 * g + 1];
     const uint32_t len = (a >= 0 && b >= a) ? (uint32_t)(b - a) : 0u;
     uint8_t* dst = capbuf + (uint64_t)g * stride;
-    for (uint32_t i = 0; i < len; i++) dst[i] = v[a + i];
+    copy_bytes(dst, v + a, len);
     const int32_t sl = P.cap_slots[g];
     if (sl >= 0) {
       Slot& x = slots[(uint64_t)sl * n_req];
@@ -4008,7 +4062,7 @@ GI_HD __noinline__ uint32_t run_capture(const DProgram& P, uint32_t* capws, uint
         r[1] = g;
         r[2] = H->nbytes;
         r[3] = len;
-        for (uint32_t i = 0; i < len; i++) H->bytes[H->nbytes + i] = dst[i];
+        copy_bytes(H->bytes + H->nbytes, dst, len);
         H->nbytes += len;
         H->nrec++;
       } else {
@@ -4351,7 +4405,7 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
           nn = de.kn;
           if (vr.key_mode == 2) {
             if (vr.pre_len) {  // ^literal
-              if (nn < vr.pre_len || !eq_bytes(nm, vr.pre_len, P.strpool + vr.slot, vr.pre_len)) continue;
+              if (nn < vr.pre_len || !eq_bytes_w(nm, vr.pre_len, P.strpool + vr.slot, vr.pre_len)) continue;
             } else if (!dfa_match(P, vr.key_dfa, nm, nn, false)) {
               continue;
             }
@@ -4915,11 +4969,14 @@ GI_HD void collect_request(const DProgram& P, const DBatch& B, uint32_t r) {
   uint8_t* ln = tx_alloc(t, method.n + uri.n + proto.n + 2);
   if (ln) {
     uint32_t k = 0;
-    for (uint32_t i = 0; i < method.n; i++) ln[k++] = method.p[i];
+    copy_bytes(ln + k, method.p, method.n);
+    k += method.n;
     ln[k++] = ' ';
-    for (uint32_t i = 0; i < uri.n; i++) ln[k++] = uri.p[i];
+    copy_bytes(ln + k, uri.p, uri.n);
+    k += uri.n;
     ln[k++] = ' ';
-    for (uint32_t i = 0; i < proto.n; i++) ln[k++] = proto.p[i];
+    copy_bytes(ln + k, proto.p, proto.n);
+    k += proto.n;
     t.single[S_REQUEST_LINE] = {ln, k};
   }
   const bool ok = process_uri(t, uri.p, uri.n);
@@ -5537,7 +5594,7 @@ __device__ void det_push(const DProgram& P, const DBatch& B, bool push, uint32_t
     det_maybe(P, B, r, vix, gm, mask);
     return;
   }
-  for (uint32_t i = 0; i < n; i++) B.det_bytes[off + i] = v[i];
+  copy_bytes(B.det_bytes + off, v, n);
   DetEnt e;
   e.req = r;
   e.vix = vix;
@@ -5840,7 +5897,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
         if (k >= B.slow_cap || off + (uint64_t)cn > B.slow_bytes_cap) {
           void_request(B, it.req, GI_VOID_SLOW);
         } else {
-          for (uint32_t i = 0; i < (uint32_t)cn; i++) B.slow_bytes[off + i] = cur[i];
+          copy_bytes(B.slow_bytes + off, cur, (uint32_t)cn);
           SlowEnt e;
           e.req = it.req;
           e.stream = s;
@@ -6177,8 +6234,15 @@ __device__ __forceinline__ void scan_qblocks(const DProgram& P, const DBatch& B,
 // per job change; !LDS: the image is read from HBM (automata too large for LDS).
 // BIG: the 1-workgroup-per-CU launch of images above 64 KB (its own symbol,
 // so per-kernel profiles keep the two launches apart).
+#ifndef GI_SCAN_NB
+// queue blocks a wave steps at once (independent LDS transition chains).
+// Measured on C2 (1M): 1 block at 8 waves/SIMD, 62 VGPRs, no spills: 17.96 ms,
+// WRITE_SIZE 1.37 GB; 2 blocks at 8 waves/SIMD (64 VGPRs, 27 spills, 112 B
+// scratch/lane): 18.89 ms, 9.3 GB of spill writes; 2 at 6 waves: 22.6 ms.
+#define GI_SCAN_NB 1
+#endif
 #ifndef GI_SCAN_WPE
-#define GI_SCAN_WPE 8  // k_scan: 8 waves/SIMD (64 VGPRs, 25 spills); measured: 4 (85 VGPRs, no spills) is slower (C2 18.4 -> 22.2 ms)
+#define GI_SCAN_WPE 8  // k_scan: 8 waves/SIMD; 6 (1 block: 21.9 ms) and 4 (2 blocks: 22.2 ms) are slower
 #endif
 template <bool LDS, bool BIG>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GI_SCAN_WPE, 8))) k_scan(DProgram P, DBatch B, const uint32_t* __restrict__ jl, uint32_t n_jl,
@@ -6246,18 +6310,18 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GI_SC
     }
     // jl is sorted by stream: only the first job of a stream counts its words
     const bool first = jj == 0 || gi_cload(P.jobs, jl[jj - 1]).stream != J.stream;
-    for (uint32_t i = wv; i < total; i += 2 * nwv) {  // two blocks per wave at a time
-      uint2 d[2];
-      d[0] = clist[i];
-      d[1] = i + nwv < total ? clist[i + nwv] : make_uint2(0u, 0u);
+    for (uint32_t i = wv; i < total; i += GI_SCAN_NB * nwv) {  // GI_SCAN_NB blocks per wave at a time
+      uint2 d[GI_SCAN_NB];
 #pragma unroll
-      for (uint32_t j = 0; j < 2; j++) {
+      for (uint32_t j = 0; j < GI_SCAN_NB; j++) d[j] = i + j * nwv < total ? clist[i + j * nwv] : make_uint2(0u, 0u);
+#pragma unroll
+      for (uint32_t j = 0; j < GI_SCAN_NB; j++) {
         const uint32_t dnw = (d[j].y >> 8) & GI_QB_NW_MASK;
         const uint64_t w = (uint64_t)(d[j].y & 0xFFu) * (GI_QB_HDR + dnw);
         rwords += (first && !(d[j].y & GI_QB_SHARED)) ? w : 0;  // a shared block is counted at its writer
         rsteps += (uint64_t)(d[j].y & 0xFFu) * dnw * 4 * K;
       }
-      scan_qblocks<2>(P, B, J, img, K, trn, st0, umask, nf, d, mode);
+      scan_qblocks<GI_SCAN_NB>(P, B, J, img, K, trn, st0, umask, nf, d, mode);
     }
     __syncthreads();  // clist / wcnt reuse
   }

@@ -488,7 +488,7 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
       return nullptr;
     }
     DevBuf& b = nbufs[k++];
-    e = b.ensure(std::max<size_t>(bytes, 16));
+    e = b.ensure(bytes + 64);  // padded: the word readers (load_u32u, copy_bytes) read up to 8 bytes past a string
     if (e == hipSuccess && bytes) e = hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice);
     return b.p;
   };
