@@ -2771,6 +2771,7 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
   // setvars then cost nothing: the per-request matched-variable state and
   // dynamic TX area are sized for the reachable rules only.
   std::vector<bool> dead(P.rules.size(), false);
+  uint32_t n_mvcur = 0;  // chains recording MATCHED_VAR(_NAME) (RF2_MVCUR)
   if (P.rule_engine != ENGINE_OFF) {
     std::vector<std::pair<int64_t, int64_t>> removable;
     for (const DAction& a : P.acts)
@@ -2827,6 +2828,32 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
       }
     }
     P.mv_used = mv ? 1 : 0;
+    // MATCHED_VAR / MATCHED_VAR_NAME liveness: a chain's matches set them, and
+    // only a later link of the same chain (or the link's own setvars) can read
+    // what it set -- unless some reachable first link reads them before its
+    // own match overwrites them (a MATCHED_VAR target, an operator argument or,
+    // for a rule without operator, a setvar macro), in which case every chain
+    // records them.  Chains whose values nobody reads skip the copies.
+    bool first_reads = false;
+    for (uint32_t ti : P.top) {
+      if (dead[ti]) continue;
+      const DRule& d = P.rules[ti];
+      for (uint32_t q = 0; q < d.var_count; q++)
+        if (P.vars[d.var_begin + q].var >= V_MATCHED_VAR) first_reads = true;
+      if (d.op >= 0 && F.tmpl_mv(P.ops[d.op].tmpl)) first_reads = true;
+      if (d.op < 0)
+        for (uint32_t q = 0; q < d.act_count; q++) {
+          const DAction& a = P.acts[d.act_begin + q];
+          if ((a.kind == A_SETVAR || a.kind == A_SETVAR_DEL) && (F.tmpl_mv(a.tmpl) || (a.slot < 0 && F.tmpl_mv(a.aux))))
+            first_reads = true;
+        }
+    }
+    n_mvcur = 0;
+    for (uint32_t ti : P.top)
+      if (mv && (first_reads || F.chain_reads_mv(ti))) {
+        P.rules[ti].flags2 |= RF2_MVCUR;
+        n_mvcur++;
+      }
   }
   {  // macro-key setvars in unreachable rules: no dynamic area for them
     std::vector<int32_t> site_rule(P.dyn_sites.size(), -1);
@@ -2860,7 +2887,8 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
                      std::to_string(P.fold_ids.size()) + ",\"const_links\":" + std::to_string(nconst) +
                      ",\"const_nomatch\":" + std::to_string(nconst0) + ",\"const_args\":" + std::to_string(n_args) +
                      ",\"frozen_slots\":" + std::to_string(nfrozen) + ",\"dead_links\":" + std::to_string(ndead) +
-                     ",\"mv_used\":" + std::to_string((int)P.mv_used) + "}}";
+                     ",\"mv_used\":" + std::to_string((int)P.mv_used) + ",\"mv_cur_chains\":" +
+                     std::to_string(n_mvcur) + "}}";
     }
   }
   P.tx_snap.resize(P.n_slots);

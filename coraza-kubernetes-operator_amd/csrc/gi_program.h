@@ -203,6 +203,7 @@ enum RuleFlags : uint8_t {
 
 enum RuleFlags2 : uint8_t {
   RF2_MVS = 1,  // a later link of this chain reads MATCHED_VARS(_NAMES): k_eval keeps the entries
+  RF2_MVCUR = 2,  // MATCHED_VAR / MATCHED_VAR_NAME this chain's matches set can be read (compile.cpp fold_program)
                 // (otherwise only MATCHED_VAR / MATCHED_VAR_NAME are updated per match)
 };
 

@@ -1263,7 +1263,8 @@ struct MvState {
   uint32_t cap_v, cap_n;
   uint32_t cur_vn, cur_nn; // MATCHED_VAR / MATCHED_VAR_NAME lengths (persist across rules)
   uint32_t keep;           // the current rule's chain reads MATCHED_VARS(_NAMES): record the entries (RF2_MVS)
-  uint32_t _pad[7];
+  uint32_t cur;            // MATCHED_VAR(_NAME) of the current rule's matches can be read (RF2_MVCUR)
+  uint32_t _pad[6];
 };
 static_assert(sizeof(MvState) == 64 && sizeof(MvEnt) == 32, "MvState layout");
 
@@ -1324,6 +1325,7 @@ GI_HD const char* var_name(uint32_t var) {
 // tx.matchVariable; false when a capacity is exceeded (the request is flagged).
 GI_HD __noinline__ bool mv_record(MvState* m, uint32_t var, const uint8_t* k, uint32_t kn, const uint8_t* v,
                                        uint32_t vn) {
+  if (!m->cur && !m->keep) return true;  // nothing can read what this match sets
   const char* vnm = var_name(var);
   uint32_t vl = 0;
   while (vnm[vl]) vl++;
@@ -4565,7 +4567,10 @@ GI_HD __forceinline__ void eval_top(Tx& t, uint32_t ri) {
   // the rule and its chain links; all must match (one eval_rule call site)
   t.prof_evals++;
   t.cur_id = (uint32_t)R.id;
-  if (t.mv) t.mv->keep = R.flags2 & RF2_MVS;
+  if (t.mv) {
+    t.mv->keep = R.flags2 & RF2_MVS;
+    t.mv->cur = R.flags2 & RF2_MVCUR;
+  }
   for (int32_t ci = (int32_t)ri; ci >= 0;) {
     const DRule C = gi_cload(P.rules, (uint64_t)ci);
     const uint64_t c0 = t.profon ? gi_clock() : 0;
@@ -6908,6 +6913,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& P, const DBatch& B, uint
     const ReqLayout Lm = B.layout[r];
     t.mv->n = t.mv->nb = 0;
     t.mv->keep = 0;
+    t.mv->cur = 0;
     t.mv->cap_e = Lm.mv_cap_e;
     t.mv->cap_a = Lm.mv_cap_a;
     t.mv->cap_v = g.cap_t;
