@@ -5969,15 +5969,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
             if (4 * w + 4 > (uint32_t)cn) x &= (1u << (8 * ((uint32_t)cn - 4 * w))) - 1u;
             q[GI_QB_HDR * nv + (uint64_t)w * nv + i] = x;
           }
-        } else {
-          for (uint32_t w = 0; w < nwi; w++) {
-            uint32_t x = 0;
-            for (uint32_t b = 0; b < 4; b++) {
-              const uint32_t at = 4 * w + b;
-              x |= (at < (uint32_t)cn ? (uint32_t)cur[at] : 0u) << (8 * b);
-            }
-            q[GI_QB_HDR * nv + (uint64_t)w * nv + i] = x;
-          }
+        } else {  // cur in HBM (the item value or a lane's global buffer, both padded): a word per read
+          for (uint32_t w = 0; w < nwi; w++)
+            q[GI_QB_HDR * nv + (uint64_t)w * nv + i] = load_u32u(cur + 4 * w) & tail_mask((uint32_t)cn - 4 * w);
         }
       }
       if (B.prof) pc_out += gi_clock() - c_s2;
