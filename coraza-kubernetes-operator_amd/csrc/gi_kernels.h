@@ -27,6 +27,7 @@ struct ReqLayout {
   uint32_t dyn_capb;   // and bytes (0 / 0: the program has none)
   uint32_t mv_cap_e;   // MATCHED_VARS entries / arena bytes one rule can record (kernels.hip MvState;
   uint32_t mv_cap_a;   // 0 / 0: the program reads no matched-variable state)
+  uint64_t cap_off;    // observable captures: the request's area in DBatch.cappool (chunk-relative)
 };
 
 struct DBatch {
@@ -36,6 +37,7 @@ struct DBatch {
   uint32_t n_req;
   uint32_t mcap;
   uint8_t* scratch;
+  uint8_t* cappool;           // capture areas of the running chunk (CapHdr + pike workspace + group values)
   const ReqLayout* layout;
   gi_verdict* verdicts;
   uint32_t* matched;

@@ -4756,11 +4756,10 @@ GI_HD inline Region region_of(const DProgram& P, const DBatch& B, uint32_t r) {
   off += (L.cap_mt + 15) & ~15u;
   g.dyn = P.n_dyn_sites ? base + off : nullptr;
   off += P.n_dyn_sites ? 16ull + 32ull * L.dyn_cap + L.dyn_capb : 0ull;
-  // observable captures: the submatch workspace and one value buffer per group
-  g.capws = P.cap_ws_words ? (uint32_t*)(base + off) : nullptr;
-  off += ((uint64_t)P.cap_ws_words * 4 + 15) & ~15ull;
-  g.capbuf = P.cap_ws_words ? base + off : nullptr;
-  off += P.cap_ws_words ? (uint64_t)P.cap_groups * ((L.cap_t + 15) & ~15u) : 0ull;
+  // observable captures: the submatch workspace and one value buffer per group,
+  // in the chunk's capture pool (runtime.cpp sizes a chunk to fit it)
+  g.capws = P.cap_ws_words ? (uint32_t*)(B.cappool + L.cap_off) : nullptr;
+  g.capbuf = P.cap_ws_words ? B.cappool + L.cap_off + (((uint64_t)P.cap_ws_words * 4 + 15) & ~15ull) : nullptr;
   g.mv = P.mv_used ? (MvState*)(base + off) : nullptr;
   g.cap_f = L.cap_f;
   g.cap_b = L.cap_b;

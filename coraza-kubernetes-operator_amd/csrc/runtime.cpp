@@ -82,6 +82,7 @@ struct gi_ctx {
   DProgram prog{};
   std::vector<DevBuf> pbufs;
   // batch buffers
+  DevBuf cappool;  // capture areas of one request chunk (reused by every chunk)
   DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, tally_ext, hits, vmap, hset, blist, joblist, txslots;
   DevBuf tally_idbuf;                  // distinct rule ids, ascending (k_tally bins)
   DevBuf caprec, capbytes;             // capture records / bytes (observable captures)
@@ -103,6 +104,7 @@ struct gi_ctx {
   };
   std::vector<Chunk> chunks;
   double chunk_pool_words = GI_CHUNK_POOL_WORDS;
+  uint64_t chunk_cap_bytes = 2ull << 30;  // capture pool a chunk may use (GI_CHUNK_CAP_BYTES env)
   ReqLayout* lay_host = nullptr;  // page-locked host copy of the staged layout
   uint32_t lay_host_cap = 0;
   bool stage_prof = false;
@@ -401,7 +403,8 @@ static const char* fill_dprogram(const Program& P, DProgram& np, Put&& put, std:
   np.cap_ws_words = 0;
   np.cap_groups = 0;
   for (const DPike& k : P.pikes) {
-    np.cap_ws_words = (uint32_t)std::max<uint64_t>(np.cap_ws_words, 16 + pike_ws_words(k.n_inst, k.nslot));
+    // (a whole-value capture, (?sm)^.*$, runs no VM: the CapHdr alone)
+    np.cap_ws_words = (uint32_t)std::max<uint64_t>(np.cap_ws_words, 16 + (k.whole ? 0 : pike_ws_words(k.n_inst, k.nslot)));
     np.cap_groups = std::max<uint32_t>(np.cap_groups, k.nslot / 2);
   }
   for (int g = 0; g < 9; g++) {
@@ -564,6 +567,7 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   c->stage_prof = getenv("GI_STAGE_PROF") && atoi(getenv("GI_STAGE_PROF")) > 0;
   if (getenv("GI_BPARSE_LDS")) c->bparse_lds = (uint32_t)std::min(65536, std::max(0, atoi(getenv("GI_BPARSE_LDS"))));
   if (getenv("GI_CHUNK_POOL_WORDS")) c->chunk_pool_words = std::max(1e6, atof(getenv("GI_CHUNK_POOL_WORDS")));
+  if (getenv("GI_CHUNK_CAP_BYTES")) c->chunk_cap_bytes = std::max<uint64_t>(1ull << 16, strtoull(getenv("GI_CHUNK_CAP_BYTES"), nullptr, 10));
   c->stop_after = getenv("GI_STOP_AFTER") ? atoi(getenv("GI_STOP_AFTER")) : 0;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -651,6 +655,7 @@ int gi_host_unregister(gi_ctx* c, void* p) {
 // batch totals it adds to.  Shared by gi_stage_batch and the CPU baseline.
 struct LayoutSizes {
   uint64_t region, vmap, hset;
+  uint64_t capb;                    // capture area (DBatch.cappool), outside the region
   uint64_t items, raw, body, post;  // phase-A items, bytes without / of the body, body fields
   bool mp;                          // multipart body
 };
@@ -806,9 +811,9 @@ static const char* request_layout(const Program& PG, uint32_t cap_ws_words, uint
   uint64_t sz = GI_REQHDR_BYTES + cap_f * 32 + ((uint64_t)PG.n_slots * GI_SLOT_BYTES + 15) / 16 * 16 + GI_RM_BYTES + (cap_b + 15) / 16 * 16 +
                 2 * ((cap_t + 15) / 16 * 16) + 2 * ((cap_mt + 15) / 16 * 16);
   if (!PG.dyn_sites.empty()) sz += 16 + 32ull * L.dyn_cap + L.dyn_capb;  // kernels.hip DynHdr + DynEnt[] + bytes
-  // observable captures (kernels.hip region_of): workspace + one value buffer per group
-  sz += (4ull * cap_ws_words + 15) / 16 * 16 +
-        (cap_ws_words ? (uint64_t)cap_groups * ((cap_t + 15) / 16 * 16) : 0);
+  // observable captures (kernels.hip region_of): workspace + one value buffer
+  // per group, in the chunk's capture pool rather than the region
+  z.capb = cap_ws_words ? (4ull * cap_ws_words + 15) / 16 * 16 + (uint64_t)cap_groups * ((cap_t + 15) / 16 * 16) : 0;
   // matched-variable state (kernels.hip MvState): header, entries, value
   // arena, MATCHED_VAR copy, name buffer
   if (PG.mv_used) {
@@ -947,7 +952,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     return pf * (1024.0 * nn + 8.0 * raw + (post ? 24.0 * body : 0.0));
   };
   struct ChunkSum {
-    uint64_t n = 0, raw = 0, body = 0, post = 0, items = 0;
+    uint64_t n = 0, raw = 0, body = 0, post = 0, items = 0, capb = 0;
   };
   std::vector<ChunkSum> csum;
   c->chunks.clear();
@@ -956,7 +961,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     uint32_t r0 = 0;
     for (uint32_t r = 0; r < n; r++) {
       const Sizes& z = sizes[r];
-      if (cs.n && pool_est(cs.n + 1, cs.raw + z.raw, cs.body + z.body, cs.post + z.post) > c->chunk_pool_words) {
+      if (cs.n && (pool_est(cs.n + 1, cs.raw + z.raw, cs.body + z.body, cs.post + z.post) > c->chunk_pool_words ||
+                   cs.capb + z.capb > c->chunk_cap_bytes)) {
         c->chunks.push_back({r0, (uint32_t)cs.n, 0, 0, 0});
         csum.push_back(cs);
         cs = ChunkSum();
@@ -967,6 +973,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       cs.body += z.body;
       cs.post += z.post;
       cs.items += z.items;
+      lay[r].cap_off = cs.capb;  // chunk-relative: every chunk reuses the pool
+      cs.capb += z.capb;
     }
     if (cs.n || c->chunks.empty()) {
       c->chunks.push_back({r0, (uint32_t)cs.n, 0, 0, 0});
@@ -995,7 +1003,9 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   for (const ChunkSum& cs : csum) {
     cmax.n = std::max(cmax.n, cs.n);
     cmax.items = std::max(cmax.items, cs.items);
+    cmax.capb = std::max(cmax.capb, cs.capb);
   }
+  if ((e = c->cappool.ensure(std::max<uint64_t>(cmax.capb + 64, 64))) != hipSuccess) return hip_fail(c, e, "alloc capture pool");
   if ((e = c->vmap.ensure(std::max<uint64_t>(4 * c->vmap_words, 16))) != hipSuccess) return hip_fail(c, e, "alloc value map");
   if ((e = c->hits.ensure(std::max<size_t>((size_t)c->hit_words * n * 4, 16))) != hipSuccess)
     return hip_fail(c, e, "alloc hits");
@@ -1104,6 +1114,7 @@ int gi_run_staged(gi_ctx* c) {
   B.n_req = c->n_req;
   B.mcap = c->mcap;
   B.scratch = (uint8_t*)c->scratch.p;
+  B.cappool = (uint8_t*)c->cappool.p;
   B.layout = (const ReqLayout*)c->layout.p;
   B.verdicts = (gi_verdict*)c->verdicts.p;
   B.matched = (uint32_t*)c->matched.p;
@@ -1467,7 +1478,7 @@ int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results
     std::atomic<uint32_t> next(0);
     std::atomic<int> bad(GI_OK);
     auto work = [&]() {
-      std::vector<uint64_t> scratch;
+      std::vector<uint64_t> scratch, capture;
       std::vector<uint64_t> txs(2ull * std::max<uint32_t>(PG.n_slots, 1));
       for (;;) {
         const uint32_t lo = next.fetch_add(64);
@@ -1484,8 +1495,11 @@ int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results
           L.vmap_bit = 0;
           L.hset_word = 0;
           L.hset_mask = 0;  // no phase A: no hit set
+          L.cap_off = 0;
           const size_t words = (z.region + 64) / 8 + 8;
           if (scratch.size() < words) scratch.assign(words, 0);
+          const size_t cwords = (z.capb + 64) / 8 + 8;
+          if (capture.size() < cwords) capture.assign(cwords, 0);
           DBatch B{};
           B.data = data.data();
           B.reqs = in->reqs + r;
@@ -1494,6 +1508,7 @@ int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results
           B.rstride = 1;
           B.mcap = out->matched_cap;
           B.scratch = (uint8_t*)scratch.data();
+          B.cappool = (uint8_t*)capture.data();
           B.layout = &L;
           B.verdicts = out->verdicts + r;
           B.matched = out->matched_ids + (uint64_t)r * out->matched_cap;

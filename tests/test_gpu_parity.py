@@ -361,6 +361,30 @@ def test_gpu_capture_parity():
     assert any(res.captures(i) and res.captures(i)[0][0] == 942 for i in range(batch.n_req))
 
 
+def test_gpu_capture_pool_chunked(monkeypatch):
+    """The capture areas live in one chunk-sized pool (runtime.cpp
+    chunk_cap_bytes): a 64 KB budget cuts the batch into many request chunks
+    that reuse it; verdicts, exports and capture records stay the oracle's."""
+    monkeypatch.setenv("GI_CHUNK_CAP_BYTES", "65536")
+    rs = gpuinspect.Ruleset(CAPTURE_RULES, tx_exports=["score", "content_type", "last", "bad"])
+    txs = []
+    gen = traffic.TrafficGen(traffic.SEED + 9).batch(600, attack_rate=0.3)
+    for i in range(gen.n_req):
+        t = gen.request(i)
+        t.headers = [(k, v) for k, v in t.headers if k.lower() != b"content-type"]
+        t.add_request_header("Content-Type", b"application/json; charset=utf-8" if i % 2 else b"text/xml;charset=x")
+        if i % 4 == 0:
+            t.uri += b"&q=Union+Select+pass%20word"
+        txs.append(t)
+    batch = gpuinspect.pack(txs)
+    eng = gpuinspect.Engine(rs, matched_cap=64, capture_cap=16, capture_bytes_cap=1024)
+    res = eng.inspect(batch)
+    orc = compare.oracle_verdicts(coraza.parse_seclang(CAPTURE_RULES), batch, rs.exports)
+    bad = compare.compare(res, orc)
+    assert not bad, bad
+    assert int(res.verdicts["capture_cnt"].sum()) > 600
+
+
 XML_RULES = r"""SecRuleEngine On
 SecRequestBodyAccess On
 SecRule REQUEST_HEADERS:Content-Type "^(?:application(?:/soap\+|/)|text/)xml" "id:200000,phase:1,t:none,t:lowercase,pass,nolog,ctl:requestBodyProcessor=XML"
