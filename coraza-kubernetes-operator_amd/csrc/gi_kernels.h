@@ -38,6 +38,7 @@ struct DBatch {
   uint32_t mcap;
   uint8_t* scratch;
   uint8_t* cappool;           // capture areas of the running chunk (CapHdr + pike workspace + group values)
+  const DProgram* prog;       // the program in device memory (k_eval's interpreter reads it through this)
   const ReqLayout* layout;
   gi_verdict* verdicts;
   uint32_t* matched;

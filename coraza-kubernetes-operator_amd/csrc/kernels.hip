@@ -6823,8 +6823,14 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
 // request's whole wave runs it uniformly, whits = the request's hit words in
 // LDS (nullptr: read from HBM).
 template <bool W>
-GI_HD __forceinline__ void eval_request(const DProgram& P, const DBatch& B, uint32_t r, const uint32_t* whits,
+GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uint32_t r, const uint32_t* whits,
                                              uint32_t wstride, unsigned long long* my) {
+  // The interpreter reads the program through B.prog, a copy of the kernel's
+  // DProgram in device memory: the non-inlined helpers take it by reference,
+  // and a reference to the by-value kernel argument would make every lane copy
+  // the whole struct into its scratch at entry (and read it back from there).
+  (void)Pk;
+  const DProgram& P = *B.prog;
   const uint64_t c_start = B.prof ? gi_clock() : 0;
   const gi_request rq = B.reqs[r];
   Region g = region_of(P, B, r);

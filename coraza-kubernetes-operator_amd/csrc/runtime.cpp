@@ -83,6 +83,7 @@ struct gi_ctx {
   std::vector<DevBuf> pbufs;
   // batch buffers
   DevBuf cappool;  // capture areas of one request chunk (reused by every chunk)
+  DevBuf progdev;  // the DProgram struct itself in device memory (DBatch.prog)
   DevBuf data, reqs, hdrs, layout, scratch, verdicts, matched, tally, tally_ext, hits, vmap, hset, blist, joblist, txslots;
   DevBuf tally_idbuf;                  // distinct rule ids, ascending (k_tally bins)
   DevBuf caprec, capbytes;             // capture records / bytes (observable captures)
@@ -523,6 +524,12 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
     nidbuf.release();
     return discard(GI_ENOMEM, "scan plan upload failed");
   }
+  DevBuf nprog;
+  if (nprog.ensure(sizeof(DProgram)) != hipSuccess || hipMemcpy(nprog.p, &np, sizeof(DProgram), hipMemcpyHostToDevice) != hipSuccess) {
+    nprog.release();
+    nidbuf.release();
+    return discard(GI_ENOMEM, "program upload failed");
+  }
   for (int b = 0; b < 2; b++) {
     nscan.jobs[b] = (const uint32_t*)njoblist.p + (b ? jl[0].size() : 0);
     nscan.n_jobs[b] = (uint32_t)jl[b].size();
@@ -539,6 +546,8 @@ static int load_program(gi_ctx* c, const gi_ruleset* rs) {
   for (auto& b : c->pbufs) b.release();
   c->joblist.release();
   c->tally_idbuf.release();
+  c->progdev.release();
+  c->progdev = nprog;
   c->pbufs.swap(nbufs);
   c->joblist = njoblist;
   c->tally_idbuf = nidbuf;
@@ -618,7 +627,8 @@ void gi_ctx_free(gi_ctx* c) {
   c->prof.release();
   for (DevBuf* b : {&c->caprec, &c->capbytes, &c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->hset, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
-                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist})
+                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist,
+                    &c->cappool, &c->progdev})
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
@@ -1115,6 +1125,7 @@ int gi_run_staged(gi_ctx* c) {
   B.mcap = c->mcap;
   B.scratch = (uint8_t*)c->scratch.p;
   B.cappool = (uint8_t*)c->cappool.p;
+  B.prog = (const DProgram*)c->progdev.p;
   B.layout = (const ReqLayout*)c->layout.p;
   B.verdicts = (gi_verdict*)c->verdicts.p;
   B.matched = (uint32_t*)c->matched.p;
@@ -1509,6 +1520,7 @@ int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results
           B.mcap = out->matched_cap;
           B.scratch = (uint8_t*)scratch.data();
           B.cappool = (uint8_t*)capture.data();
+          B.prog = &np;
           B.layout = &L;
           B.verdicts = out->verdicts + r;
           B.matched = out->matched_ids + (uint64_t)r * out->matched_cap;
