@@ -105,7 +105,9 @@ struct gi_ctx {
   };
   std::vector<Chunk> chunks;
   double chunk_pool_words = GI_CHUNK_POOL_WORDS;
-  uint64_t chunk_cap_bytes = 2ull << 30;  // capture pool a chunk may use (GI_CHUNK_CAP_BYTES env)
+  // capture pool a chunk may use (GI_CHUNK_CAP_BYTES env): C2's 1M requests need
+  // ~8 GB (one chunk); a ruleset with a huge capture regex runs in more chunks
+  uint64_t chunk_cap_bytes = 16ull << 30;
   ReqLayout* lay_host = nullptr;  // page-locked host copy of the staged layout
   uint32_t lay_host_cap = 0;
   bool stage_prof = false;
