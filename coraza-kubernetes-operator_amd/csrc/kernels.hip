@@ -4361,201 +4361,273 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   }
   const DOp o = gi_cload(P.ops, (uint64_t)R.op);
   uint32_t nmatch = 0;
-  for (uint32_t vi = 0; vi < R.var_count; vi++) {
-    const DVarRef vr = gi_cload(P.vars, R.var_begin + vi);
-    if (vr.var < S_COUNT) {
-      if (t.nrtgt && R.id != 0 && target_removed(t, R.id, vr.var, nullptr, 0)) continue;
-      if (vr.count) {
-        uint8_t one = '1';
-        nmatch += test_value(t, R, o, &one, 1, vr.var, nullptr, 0);
-      } else {
-        uint8_t sb[24];
-        const Str s = single_val(t, vr.var, sb);
-        nmatch += test_value(t, R, o, s.p, s.n, vr.var, nullptr, 0);
-      }
-      continue;
-    }
-    if (vr.var == V_TX) {
-      uint32_t cnt = 0;
-      // static slots: a literal key names at most one; a regex key the ones the
-      // compiler listed (DProgram.txrx); no key all.  Then (no literal key) the
-      // keys macro-key setvars created, in creation order.
-      uint32_t sb = 0, se = P.n_slots;
-      if (vr.key_mode == 1) {
-        sb = vr.slot < 0 ? 0u : (uint32_t)vr.slot;
-        se = vr.slot < 0 ? 0u : (uint32_t)vr.slot + 1;
-      } else if (vr.key_mode == 2) {
-        sb = 0;
-        se = vr.key_len;
-      }
-      const uint32_t ndyn = (vr.key_mode != 1 && t.dyn) ? ((const DynHdr*)t.dyn)->n : 0u;
-      for (uint32_t si = sb; si < se + ndyn; si++) {
-        const uint8_t* nm;
-        uint32_t nn;
-        Slot sl;
-        if (si < se) {
-          const uint32_t sid = vr.key_mode == 2 ? P.txrx[vr.key_off + si] : si;
-          sl = slot_rd(t, sid);
-          if (sl.state == 0) continue;
-          nm = P.strpool + P.slot_names[sid * 2];
-          nn = P.slot_names[sid * 2 + 1];
-        } else {
-          const DynEnt& de = dyn_ents(t.dyn)[si - se];
-          sl = de.s;
-          if (sl.state == 0) continue;
-          nm = de.k;
-          nn = de.kn;
-          if (vr.key_mode == 2) {
-            if (vr.pre_len) {  // ^literal
-              if (nn < vr.pre_len || !eq_bytes_w(nm, vr.pre_len, P.strpool + vr.slot, vr.pre_len)) continue;
-            } else if (!dfa_match(P, vr.key_dfa, nm, nn, false)) {
-              continue;
-            }
+  // The link's targets as one sequence of candidate values, in Coraza's order
+  // (variables in rule order; a collection's entries in field order, TX keys
+  // static then created; a count target's count after its walk), tested at
+  // ONE test_value site: test_value (chain, operator dispatch, capture,
+  // matched-variable state, actions) is inlined once instead of once per kind
+  // of target, which kept k_eval's code and register pressure several times
+  // larger.
+  uint8_t nbuf[24];        // a candidate formatted as a number (counts, integer TX values)
+  uint32_t vi = 0;         // the variable being walked
+  bool in_var = false;     // its walk has started
+  DVarRef vr{};
+  uint32_t j = 0, je = 0, cnt = 0, se = 0;  // walk position / end, count, TX: end of the static slots
+  bool vskip = false, vexact = false;
+  uint64_t wm = 0;         // k_eval_wave: survivors of the current 64-field block
+  uint32_t wf = 0, wh = 0;
+  bool wn = false;
+  for (;;) {
+    const uint8_t* cv = nullptr;
+    const uint8_t* ck = nullptr;
+    uint32_t cvn = 0, cvar = 0, ckn = 0;
+    bool cex = false, have = false;
+    while (!have) {
+      if (!in_var) {
+        if (vi >= R.var_count) break;
+        vr = gi_cload(P.vars, R.var_begin + vi);
+        in_var = true;
+        cnt = 0;
+        j = je = 0;
+        wm = 0;
+        if (vr.var < S_COUNT) {  // a single: one candidate
+          in_var = false;
+          vi++;
+          if (t.nrtgt && R.id != 0 && target_removed(t, R.id, vr.var, nullptr, 0)) continue;
+          if (vr.count) {
+            nbuf[0] = '1';
+            cv = nbuf;
+            cvn = 1;
+          } else {
+            const Str sv = single_val(t, vr.var, nbuf);
+            cv = sv.p;
+            cvn = sv.n;
           }
-        }
-        if (key_excluded(t, vr, nm, nn)) continue;
-        if (t.nrtgt && R.id != 0 && target_removed(t, R.id, V_TX, nm, nn)) continue;
-        if (vr.count) {
-          cnt++;
+          cvar = vr.var;
+          have = true;
           continue;
         }
-        if (sl.state == 1 && R.tchain_len == 0 && o.has_num && o.kind >= OP_EQ && o.kind <= OP_LT) {
-          // integer TX value against a numeric literal: eval_op would Atoi the
-          // canonical decimal back to sl.num, so compare directly
-          const int64_t a = o.num, b = sl.num;
-          bool res = o.kind == OP_EQ ? b == a : o.kind == OP_GE ? b >= a : o.kind == OP_GT ? b > a
-                     : o.kind == OP_LE ? b <= a : b < a;
-          if (o.negate) res = !res;
-          if (res) {
-            if (t.mv) {  // the matched-variable state, as test_value records it
-              uint8_t vb[24];
-              if (!mv_record(t.mv, V_TX, nm, nn, vb, go_itoa(sl.num, vb))) t.flags |= GI_REQ_OVERFLOW;
-            }
-            run_actions(t, R);
-            nmatch++;
+        if (vr.var == V_TX) {
+          // static slots: a literal key names at most one; a regex key the ones the
+          // compiler listed (DProgram.txrx); no key all.  Then (no literal key) the
+          // keys macro-key setvars created, in creation order.
+          uint32_t sb = 0;
+          se = P.n_slots;
+          if (vr.key_mode == 1) {
+            sb = vr.slot < 0 ? 0u : (uint32_t)vr.slot;
+            se = vr.slot < 0 ? 0u : (uint32_t)vr.slot + 1;
+          } else if (vr.key_mode == 2) {
+            se = vr.key_len;
           }
+          j = sb;
+          je = se + ((vr.key_mode != 1 && t.dyn) ? ((const DynHdr*)t.dyn)->n : 0u);
           continue;
         }
-        uint8_t nb[24];
-        Str s = slot_str(t, sl, nb);
-        nmatch += test_value(t, R, o, s.p, s.n, V_TX, nm, nn);
-      }
-      if (vr.count) {
-        uint8_t buf[24];
-        uint32_t k = go_itoa(cnt, buf);
-        nmatch += test_value(t, R, o, buf, k, V_TX, nullptr, 0);
-      }
-      continue;
-    }
-    if (vr.var >= V_MATCHED_VAR) {  // the matched-variable state (t.mv is set: mv_used)
-      MvState* m = t.mv;
-      if (!m) continue;  // no state: only unreachable rules read it (compile.cpp fold_program)
-      if (vr.var == V_MATCHED_VAR || vr.var == V_MATCHED_VAR_NAME) {
-        uint8_t one = '1';
-        Str s = vr.count ? Str{&one, 1u}
-                         : vr.var == V_MATCHED_VAR ? Str{mv_curval(m), m->cur_vn} : Str{mv_curname(m), m->cur_nn};
-        nmatch += test_value(t, R, o, s.p, s.n, vr.var, nullptr, 0);
+        if (vr.var >= V_MATCHED_VAR) {  // the matched-variable state (t.mv is set: mv_used)
+          MvState* m = t.mv;
+          if (!m) {  // no state: only unreachable rules read it (compile.cpp fold_program)
+            in_var = false;
+            vi++;
+            continue;
+          }
+          if (vr.var == V_MATCHED_VAR || vr.var == V_MATCHED_VAR_NAME) {
+            in_var = false;
+            vi++;
+            if (vr.count) {
+              nbuf[0] = '1';
+              cv = nbuf;
+              cvn = 1;
+            } else if (vr.var == V_MATCHED_VAR) {
+              cv = mv_curval(m);
+              cvn = m->cur_vn;
+            } else {
+              cv = mv_curname(m);
+              cvn = m->cur_nn;
+            }
+            cvar = vr.var;
+            have = true;
+            continue;
+          }
+          je = m->n;  // MATCHED_VARS(_NAMES): the entries as they stood when the link started
+          continue;
+        }
+        // a collection: value-map / hit-set filtering (field_filter); multiMatch
+        // links count candidates per value, so they always evaluate
+        vskip = R.hit_slot >= 0 && !vr.count && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
+                slot_vexact(P, (uint32_t)R.hit_slot);
+        vexact = vskip && t.hset && !(R.flags & RF_MULTIMATCH);
+        uint32_t klo, khi;
+        je = t.nf;
+        var_kinds(vr.var, &klo, &khi);
+        if (t.kx) {  // only the collection's own fields
+          j = klo <= khi ? t.kx[klo] : 0u;
+          je = klo <= khi ? t.kx[khi + 1] : 0u;
+          if (vr.count && vr.key_mode == 0 && !vr.exc_count && !t.nrtgt) {  // &COLLECTION: the entry count
+            cnt = je - j;
+            j = je;
+          }
+        }
         continue;
       }
-      // MATCHED_VARS(_NAMES): the entries as they stood when the link started
-      const uint32_t n0 = m->n;
-      uint32_t cnt = 0;
-      for (uint32_t j = 0; j < n0; j++) {
-        const MvEnt e = mv_ents(m)[j];
-        if (vr.key_mode == 1) {
-          if (!eq_ascii_ci(e.name, e.nn, P.strpool + vr.key_off, vr.key_len)) continue;
-        } else if (vr.key_mode == 2) {
-          if (!dfa_match(P, vr.key_dfa, e.name, e.nn, true)) continue;
-        }
-        if (vr.exc_count && key_excluded(t, vr, e.name, e.nn)) continue;
-        if (vr.count) {
-          cnt++;
+      // the walk of variable vi: its next candidate, if any
+      if (vr.var == V_TX) {
+        if (j < je) {
+          const uint32_t si = j++;
+          const uint8_t* nm;
+          uint32_t nn;
+          Slot sl;
+          if (si < se) {
+            const uint32_t sid = vr.key_mode == 2 ? P.txrx[vr.key_off + si] : si;
+            sl = slot_rd(t, sid);
+            if (sl.state == 0) continue;
+            nm = P.strpool + P.slot_names[sid * 2];
+            nn = P.slot_names[sid * 2 + 1];
+          } else {
+            const DynEnt& de = dyn_ents(t.dyn)[si - se];
+            sl = de.s;
+            if (sl.state == 0) continue;
+            nm = de.k;
+            nn = de.kn;
+            if (vr.key_mode == 2) {
+              if (vr.pre_len) {  // ^literal
+                if (nn < vr.pre_len || !eq_bytes_w(nm, vr.pre_len, P.strpool + vr.slot, vr.pre_len)) continue;
+              } else if (!dfa_match(P, vr.key_dfa, nm, nn, false)) {
+                continue;
+              }
+            }
+          }
+          if (key_excluded(t, vr, nm, nn)) continue;
+          if (t.nrtgt && R.id != 0 && target_removed(t, R.id, V_TX, nm, nn)) continue;
+          if (vr.count) {
+            cnt++;
+            continue;
+          }
+          if (sl.state == 1 && R.tchain_len == 0 && o.has_num && o.kind >= OP_EQ && o.kind <= OP_LT) {
+            // integer TX value against a numeric literal: eval_op would Atoi the
+            // canonical decimal back to sl.num, so compare directly (an exact
+            // candidate; its decimal only for the matched-variable state)
+            const int64_t a = o.num, b = sl.num;
+            bool res = o.kind == OP_EQ ? b == a : o.kind == OP_GE ? b >= a : o.kind == OP_GT ? b > a
+                       : o.kind == OP_LE ? b <= a : b < a;
+            if (o.negate) res = !res;
+            if (!res) continue;
+            cv = nbuf;
+            cvn = t.mv ? go_itoa(sl.num, nbuf) : 0u;
+            cex = true;
+          } else {
+            const Str sv = slot_str(t, sl, nbuf);
+            cv = sv.p;
+            cvn = sv.n;
+          }
+          cvar = V_TX;
+          ck = nm;
+          ckn = nn;
+          have = true;
           continue;
         }
-        if (vr.var == V_MATCHED_VARS_NAMES) nmatch += test_value(t, R, o, e.name, e.nn, vr.var, e.name, e.nn);
-        else nmatch += test_value(t, R, o, e.v, e.vn, vr.var, e.name, e.nn);
+      } else if (vr.var >= V_MATCHED_VAR) {
+        if (j < je) {
+          const MvEnt e = mv_ents(t.mv)[j++];
+          if (vr.key_mode == 1) {
+            if (!eq_ascii_ci(e.name, e.nn, P.strpool + vr.key_off, vr.key_len)) continue;
+          } else if (vr.key_mode == 2) {
+            if (!dfa_match(P, vr.key_dfa, e.name, e.nn, true)) continue;
+          }
+          if (vr.exc_count && key_excluded(t, vr, e.name, e.nn)) continue;
+          if (vr.count) {
+            cnt++;
+            continue;
+          }
+          const bool nms = vr.var == V_MATCHED_VARS_NAMES;
+          cv = nms ? e.name : e.v;
+          cvn = nms ? e.nn : e.vn;
+          cvar = vr.var;
+          ck = e.name;
+          ckn = e.nn;
+          have = true;
+          continue;
+        }
+      } else {
+        if constexpr (!W) {
+          if (j < je) {
+            const uint32_t f = t.kx ? t.kx[12 + j] : j;
+            j++;
+            bool names;
+            const uint32_t hres = field_filter(t, R, vr, f, vskip, vexact, &names);
+            if (!hres) continue;
+            if (vr.count) {
+              cnt++;
+              continue;
+            }
+            const Field fl = t.fields[f];
+            cv = names ? fl.k : fl.v;
+            cvn = names ? fl.kn : fl.vn;
+            cvar = vr.var;
+            ck = fl.k;
+            ckn = fl.kn;
+            cex = hres == 1;
+            have = true;
+            continue;
+          }
+        } else {
+          // k_eval_wave: the lanes filter 64 fields at a time (pure: value map,
+          // hit set, key selectors, exclusions), then the wave tests the
+          // survivors in field order, uniformly (actions and matched-variable
+          // state keep Coraza's per-value order)
+          if (wm) {
+            const int b = __ffsll((unsigned long long)wm) - 1;
+            wm &= wm - 1;
+            const uint32_t fb = (uint32_t)__shfl((int)wf, b, 64);
+            const uint32_t hb = (uint32_t)__shfl((int)wh, b, 64);
+            const bool nb = __shfl((int)wn, b, 64) != 0;
+            const Field fl = t.fields[fb];
+            cv = nb ? fl.k : fl.v;
+            cvn = nb ? fl.kn : fl.vn;
+            cvar = vr.var;
+            ck = fl.k;
+            ckn = fl.kn;
+            cex = hb == 1;
+            have = true;
+            continue;
+          }
+          if (j < je) {
+            const uint32_t lane = threadIdx.x & 63u;
+            const uint64_t c0 = t.profon ? gi_clock() : 0;
+            wf = 0;
+            wh = 0;
+            wn = false;
+            if (j + lane < je) {
+              wf = t.kx ? t.kx[12 + j + lane] : j + lane;
+              wh = field_filter(t, R, vr, wf, vskip, vexact, &wn);
+            }
+            const uint64_t m = __ballot(wh != 0);
+            if (t.profon) {  // GI_PROF (lane 0): fields filtered, survivors exact / to evaluate, cycles
+              unsigned long long* pf = t.prof_rule_cyc - 128;
+              const uint64_t mx = __ballot(wh == 1);
+              atomicAdd(&pf[17], (unsigned long long)min(64u, je - j));
+              atomicAdd(&pf[18], (unsigned long long)__popcll(mx));
+              atomicAdd(&pf[19], (unsigned long long)__popcll(m & ~mx));
+              atomicAdd(&pf[20], (unsigned long long)(gi_clock() - c0));
+            }
+            j += 64;
+            if (vr.count) cnt += (uint32_t)__popcll(m);
+            else wm = m;
+            continue;
+          }
+        }
       }
+      // the walk of variable vi ended: a count target's candidate is its count
+      in_var = false;
+      vi++;
       if (vr.count) {
-        uint8_t buf[24];
-        uint32_t k = go_itoa(cnt, buf);
-        nmatch += test_value(t, R, o, buf, k, vr.var, nullptr, 0);
-      }
-      continue;
-    }
-    // value-map / hit-set filtering (field_filter); multiMatch links count
-    // candidates per value, so they always evaluate.
-    const bool vskip = R.hit_slot >= 0 && !vr.count && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
-                       slot_vexact(P, (uint32_t)R.hit_slot);
-    const bool vexact = vskip && t.hset && !(R.flags & RF_MULTIMATCH);
-    uint32_t cnt = 0;
-    uint32_t klo, khi, j = 0, je = t.nf;
-    var_kinds(vr.var, &klo, &khi);
-    if (t.kx) {  // only the collection's own fields
-      j = klo <= khi ? t.kx[klo] : 0u;
-      je = klo <= khi ? t.kx[khi + 1] : 0u;
-      if (vr.count && vr.key_mode == 0 && !vr.exc_count && !t.nrtgt) {  // &COLLECTION: the entry count
-        cnt = je - j;
-        j = je;
+        cv = nbuf;
+        cvn = go_itoa(cnt, nbuf);
+        cvar = vr.var;
+        have = true;
       }
     }
-    if constexpr (!W) {
-      for (; j < je; j++) {
-        const uint32_t f = t.kx ? t.kx[12 + j] : j;
-        bool names;
-        const uint32_t hres = field_filter(t, R, vr, f, vskip, vexact, &names);
-        if (!hres) continue;
-        if (vr.count) {
-          cnt++;
-          continue;
-        }
-        const Field fl = t.fields[f];
-        nmatch += test_value(t, R, o, names ? fl.k : fl.v, names ? fl.kn : fl.vn, vr.var, fl.k, fl.kn, hres == 1);
-      }
-    } else {
-      // k_eval_wave: the lanes filter 64 fields at a time (pure: value map,
-      // hit set, key selectors, exclusions), then the wave tests the survivors
-      // in field order, uniformly (actions and matched-variable state keep
-      // Coraza's per-value order)
-      const uint32_t lane = threadIdx.x & 63u;
-      for (; j < je; j += 64) {
-        const uint64_t c0 = t.profon ? gi_clock() : 0;
-        uint32_t f = 0, hres = 0;
-        bool names = false;
-        if (j + lane < je) {
-          f = t.kx ? t.kx[12 + j + lane] : j + lane;
-          hres = field_filter(t, R, vr, f, vskip, vexact, &names);
-        }
-        uint64_t m = __ballot(hres != 0);
-        if (t.profon) {  // GI_PROF (lane 0): fields filtered, survivors exact / to evaluate, cycles
-          unsigned long long* pf = t.prof_rule_cyc - 128;
-          const uint64_t mx = __ballot(hres == 1);
-          atomicAdd(&pf[17], (unsigned long long)min(64u, je - j));
-          atomicAdd(&pf[18], (unsigned long long)__popcll(mx));
-          atomicAdd(&pf[19], (unsigned long long)__popcll(m & ~mx));
-          atomicAdd(&pf[20], (unsigned long long)(gi_clock() - c0));
-        }
-        if (vr.count) {
-          cnt += (uint32_t)__popcll(m);
-          continue;
-        }
-        const uint64_t c1 = t.profon ? gi_clock() : 0;
-        while (m) {
-          const int b = __ffsll((unsigned long long)m) - 1;
-          m &= m - 1;
-          const uint32_t fb = (uint32_t)__shfl((int)f, b, 64);
-          const uint32_t hb = (uint32_t)__shfl((int)hres, b, 64);
-          const bool nb = __shfl((int)names, b, 64) != 0;
-          const Field fl = t.fields[fb];
-          nmatch += test_value(t, R, o, nb ? fl.k : fl.v, nb ? fl.kn : fl.vn, vr.var, fl.k, fl.kn, hb == 1);
-        }
-        if (t.profon) gi_prof_add(&t.prof_rule_cyc[-128 + 21], (unsigned long long)(gi_clock() - c1));
-      }
-    }
-    if (vr.count) {
-      uint8_t buf[24];
-      uint32_t k = go_itoa(cnt, buf);
-      nmatch += test_value(t, R, o, buf, k, vr.var, nullptr, 0);
-    }
+    if (!have) break;
+    nmatch += test_value(t, R, o, cv, cvn, cvar, ck, ckn, cex);
   }
   return nmatch;
 }
