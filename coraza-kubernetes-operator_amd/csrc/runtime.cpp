@@ -834,8 +834,12 @@ static const char* request_layout(const Program& PG, uint32_t cap_ws_words, uint
     // match -- the static slots (values <= the longest setvar literal or a
     // macro expansion) and the run-time keys
     const uint64_t e = cap_f + 16 + PG.n_slots + L.dyn_cap;
-    const uint64_t ab = cap_b + cap_mt + L.dyn_capb + 40ull * (PG.n_slots + L.dyn_cap) +
-                        (uint64_t)PG.n_slots * std::max<uint64_t>(cap_mt, PG.max_tx_lit);
+    // TX values: every string a slot can hold lives in the TX string arena
+    // (cap_mt bytes in all), the string pool (one literal per slot), the
+    // dynamic area, a capture buffer or a formatted integer -- so their sum,
+    // not n_slots x the largest, bounds one rule's MATCHED_VARS copies
+    const uint64_t tx_vals = cap_mt + (uint64_t)PG.n_slots * (PG.max_tx_lit + 24) + L.dyn_capb + 9ull * cap_t;
+    const uint64_t ab = cap_b + cap_mt + L.dyn_capb + 40ull * (PG.n_slots + L.dyn_cap) + tx_vals;
     if (e > 0xFFFFFFFFull || ab > 0xFFFFFFFFull) return "request too large (matched variables)";
     L.mv_cap_e = (uint32_t)e;
     L.mv_cap_a = (uint32_t)((ab + 15) & ~15ull);
