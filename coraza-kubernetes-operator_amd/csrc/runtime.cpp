@@ -834,11 +834,13 @@ static const char* request_layout(const Program& PG, uint32_t cap_ws_words, uint
     // match -- the static slots (values <= the longest setvar literal or a
     // macro expansion) and the run-time keys
     const uint64_t e = cap_f + 16 + PG.n_slots + L.dyn_cap;
-    // TX values: every string a slot can hold lives in the TX string arena
-    // (cap_mt bytes in all), the string pool (one literal per slot), the
-    // dynamic area, a capture buffer or a formatted integer -- so their sum,
-    // not n_slots x the largest, bounds one rule's MATCHED_VARS copies
-    const uint64_t tx_vals = cap_mt + (uint64_t)PG.n_slots * (PG.max_tx_lit + 24) + L.dyn_capb + 9ull * cap_t;
+    // TX values: a string a slot holds lives in the TX string arena (cap_mt
+    // bytes in all), the string pool (one literal per slot), the dynamic area
+    // (dyn_capb) or is a formatted integer -- so their sum, not n_slots x the
+    // largest, bounds one rule's MATCHED_VARS copies of them.  (A capture
+    // group's value is not counted: a rule whose TX target copies long
+    // captures may flag GI_REQ_OVERFLOW.)
+    const uint64_t tx_vals = cap_mt + (uint64_t)PG.n_slots * (PG.max_tx_lit + 24);
     const uint64_t ab = cap_b + cap_mt + L.dyn_capb + 40ull * (PG.n_slots + L.dyn_cap) + tx_vals;
     if (e > 0xFFFFFFFFull || ab > 0xFFFFFFFFull) return "request too large (matched variables)";
     L.mv_cap_e = (uint32_t)e;
@@ -1513,6 +1515,10 @@ int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results
           L.hset_word = 0;
           L.hset_mask = 0;  // no phase A: no hit set
           L.cap_off = 0;
+          if (getenv("GI_LAYOUT_DEBUG") && z.region > (1u << 20))  // diagnostics: what sizes a large region
+            fprintf(stderr, "GI_LAYOUT r=%u region=%llu cap_f=%u cap_b=%u cap_t=%u cap_mt=%u dyn=%u/%u mv=%u/%u capb=%llu\n", r,
+                    (unsigned long long)z.region, L.cap_f, L.cap_b, L.cap_t, L.cap_mt, L.dyn_cap, L.dyn_capb, L.mv_cap_e,
+                    L.mv_cap_a, (unsigned long long)z.capb);
           const size_t words = (z.region + 64) / 8 + 8;
           if (scratch.size() < words) scratch.assign(words, 0);
           const size_t cwords = (z.capb + 64) / 8 + 8;
