@@ -127,12 +127,19 @@ def cpu_baseline(rs, batch, res, budget_s=10.0, threads=None):
     Its verdicts are also compared with the GPU's for the same requests (the
     same interpreter source: they must agree bit for bit)."""
     threads = threads or max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
-    n_cal = min(batch.n_req, 64 * threads)
-    _, dt = gpuinspect.cpu_baseline_inspect(rs, batch.take(0, n_cal), threads=threads,
-                                            matched_cap=res.matched.shape[1])
-    n = int(min(batch.n_req, max(n_cal, budget_s * n_cal / max(dt, 1e-6))))
-    sample = batch.take(0, n)
-    cres, secs = gpuinspect.cpu_baseline_inspect(rs, sample, threads=threads, matched_cap=res.matched.shape[1])
+    # calibration sample: one request per thread when requests are large (C5's
+    # 1 MB bodies take seconds each on a core), else 64 per thread
+    big = len(batch.data) > 65536 * max(batch.n_req, 1)
+    n_cal = min(batch.n_req, threads if big else 64 * threads)
+    log("cpu baseline calibration: %d requests, %d threads" % (n_cal, threads))
+    cres, dt = gpuinspect.cpu_baseline_inspect(rs, batch.take(0, n_cal), threads=threads,
+                                               matched_cap=res.matched.shape[1])
+    n, secs = n_cal, dt
+    if dt < budget_s / 2 and n_cal < batch.n_req:  # else the calibration is the sample
+        n = int(min(batch.n_req, max(n_cal, budget_s * n_cal / max(dt, 1e-6))))
+        log("cpu baseline: %d requests" % n)
+        cres, secs = gpuinspect.cpu_baseline_inspect(rs, batch.take(0, n), threads=threads,
+                                                     matched_cap=res.matched.shape[1])
     agree = int(((cres.verdicts[:n]["rule_id"] == res.verdicts[:n]["rule_id"]) &
                  (cres.verdicts[:n]["status"] == res.verdicts[:n]["status"]) &
                  (cres.verdicts[:n]["match_cnt"] == res.verdicts[:n]["match_cnt"]) &
