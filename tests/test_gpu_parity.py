@@ -76,7 +76,10 @@ def test_gpu_parity_edge_uris():
         t.add_request_header("Host", "x")
         t.add_request_header("Cookie", " a=1; b ; =c;d=evilmonkey ")
         txs.append(t)
-    _parity(text, gpuinspect.pack(txs))
+    res = _parity(text, gpuinspect.pack(txs))
+    # every request-target form (absolute, scheme-relative, "*", control bytes)
+    # is evaluated: none is flagged unsupported on either side
+    assert not (res.verdicts["flags"] & 0x0F).any(), [int(f) for f in res.verdicts["flags"]]
 
 
 CRS = os.path.join(ROOT, "rulesets", "crs_pl1.conf")
