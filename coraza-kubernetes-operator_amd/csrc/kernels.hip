@@ -7416,7 +7416,9 @@ void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hi
     GI_LAUNCH("k_body", k_body, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[2], stream);
   {  // small batches (fewer than 4 workgroups of 128 per CU): one wave per workgroup to spread over all CUs
-    const uint32_t ev_bs = (B.n_req + 127) / 128 < 1024 ? 64u : 128u;
+    // GI_EVAL_BS A/B (C2, 1M): 128 threads 26.2 ms, 64 threads 32.1 ms
+    static const uint32_t ev_env = getenv("GI_EVAL_BS") ? (uint32_t)atoi(getenv("GI_EVAL_BS")) : 0u;
+    const uint32_t ev_bs = (ev_env == 64 || ev_env == 128) ? ev_env : (B.n_req + 127) / 128 < 1024 ? 64u : 128u;
     GI_LAUNCH("k_eval", k_eval, dim3((B.n_req + ev_bs - 1) / ev_bs), dim3(ev_bs), 0, stream, P, B);
   }
   if (B.wlist) {  // heavy requests, one wave each (persistent over k_eval's list)
