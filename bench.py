@@ -119,6 +119,31 @@ def cpu_model():
     return "unknown"
 
 
+def host_cpu_share():
+    """The host cores this process may use, and why that many: the CPU
+    affinity mask (os.sched_getaffinity), the cgroup CPU quota (cpu.max), and
+    OMP_NUM_THREADS (the GPU box sets it to the job's CPU share, 16, while
+    os.cpu_count() reports the whole machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp_n = int(omp) if omp and omp.isdigit() else None
+    cands = [("affinity", aff)]
+    if quota:
+        cands.append(("cgroup cpu.max", max(1, int(quota))))
+    if omp_n:
+        cands.append(("OMP_NUM_THREADS", omp_n))
+    why, n = min(cands, key=lambda c: c[1])
+    return {"threads": max(1, n), "limited_by": why, "affinity": aff, "cpu_count": os.cpu_count(),
+            "cgroup_quota": quota, "omp_num_threads": omp_n}
+
+
 def cpu_baseline(rs, batch, res, budget_s=10.0, threads=None):
     """SURVEY §8(d)'s CPU baseline when Coraza Go is absent: the engine's own
     C++ interpreter (gi_cpu_baseline_inspect: kernels.hip compiled for the
@@ -126,7 +151,8 @@ def cpu_baseline(rs, batch, res, budget_s=10.0, threads=None):
     a prefix of the benchmark batch sized from a calibration to ~budget_s.
     Its verdicts are also compared with the GPU's for the same requests (the
     same interpreter source: they must agree bit for bit)."""
-    threads = threads or max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+    share = host_cpu_share()
+    threads = threads or share["threads"]
     # calibration sample: one request per thread when requests are large (C5's
     # 1 MB bodies take seconds each on a core), else 64 per thread
     big = len(batch.data) > 65536 * max(batch.n_req, 1)
@@ -150,7 +176,7 @@ def cpu_baseline(rs, batch, res, budget_s=10.0, threads=None):
             "sample": "first %d requests of the benchmark batch through gi_cpu_baseline_inspect: this engine's "
                       "own interpreter (kernels.hip) compiled for the host, %d threads, every rule link evaluated "
                       "(no phase A) -- a C++ restatement, not Coraza (no Go toolchain on the box)" % (n, threads),
-            "seconds": round(secs, 3), "agrees_with_gpu": agree, "agree_of": n}
+            "seconds": round(secs, 3), "agrees_with_gpu": agree, "agree_of": n, "host_cpu_share": share}
 
 
 def parity(res, verdicts):

@@ -97,6 +97,14 @@ class RuleSetEntry:
         d.update(self.artifact)
         return d
 
+    def size(self) -> int:
+        """Bytes the entry holds: len(Rules) as cache.go:113-124 counts it,
+        plus the string fields of the GPU artifact stored beside it (the
+        reference stores no artifact; its base64 program -- automata included,
+        often larger than the rules text -- must count against the same
+        SizeLimit or PruneBySize would not bound the cache's memory)."""
+        return len(self.rules) + sum(len(v) for v in self.artifact.values() if isinstance(v, (str, bytes)))
+
 
 class RuleSetCache:
     """Thread-safe versioned RuleSet store (cache.go:46-231)."""
@@ -126,13 +134,28 @@ class RuleSetCache:
                     return e
             return None
 
+    def _artifact_of(self, instance: str, rules: str) -> Optional[Dict]:
+        """The artifact of an entry of `instance` with the same rules text:
+        the reconciler Puts on every reconcile (ruleset_controller.go:181),
+        mostly with unchanged rules -- reused instead of recompiled."""
+        with self._mu:
+            got = self._entries.get(instance)
+            for e in reversed(got[1] if got else []):
+                if e.rules == rules and e.artifact:
+                    return e.artifact
+        return None
+
     def put(self, instance: str, rules: str) -> RuleSetEntry:
         art: Dict = {}
         if self._emitter is not None:
-            try:
-                art = self._emitter(rules) or {}
-            except Exception:  # noqa: BLE001 -- the entry is stored without an artifact
-                art = {}
+            prev = self._artifact_of(instance, rules)
+            if prev is not None:
+                art = prev
+            else:
+                try:
+                    art = self._emitter(rules) or {}
+                except Exception:  # noqa: BLE001 -- the entry is stored without an artifact
+                    art = {}
         with self._mu:
             e = RuleSetEntry(str(_uuid.uuid4()), self._now(), rules, art)
             if instance not in self._entries:
@@ -148,7 +171,7 @@ class RuleSetCache:
 
     def total_size(self) -> int:
         with self._mu:
-            return sum(len(e.rules) for _, ents in self._entries.values() for e in ents)
+            return sum(e.size() for _, ents in self._entries.values() for e in ents)
 
     def set_entry_timestamp(self, instance: str, index: int, timestamp_ns: int) -> None:
         with self._mu:
@@ -179,9 +202,10 @@ class RuleSetCache:
 
     def prune_by_size(self, max_size: int) -> int:
         """Drop the oldest entries (instance by instance) until the total
-        len(rules) is at most max_size, never an instance's latest."""
+        entry size (RuleSetEntry.size) is at most max_size, never an
+        instance's latest."""
         with self._mu:
-            cur = sum(len(e.rules) for _, ents in self._entries.values() for e in ents)
+            cur = sum(e.size() for _, ents in self._entries.values() for e in ents)
             if cur <= max_size:
                 return 0
             pruned = 0
@@ -193,7 +217,7 @@ class RuleSetCache:
                     if e.uuid == latest:
                         keep.append(e)
                     elif cur > max_size:
-                        cur -= len(e.rules)
+                        cur -= e.size()
                         pruned += 1
                     else:
                         keep.append(e)

@@ -12,6 +12,8 @@
 
 #include <string.h>
 
+#include <algorithm>
+
 #include "../../include/gpuinspect.h"
 
 namespace gi {
@@ -30,6 +32,7 @@ struct Scalars {
   uint32_t item_singles, n_hit_slots, n_union_dfas, max_img_bytes, max_big_img_bytes, n_slots, n_markers;
   uint8_t rule_engine, body_access, mv_used, body_partial, fold_on, _pad[3];
   uint32_t fold_nids, max_tx_lit;
+  uint32_t n_rm_groups, args_limit;
   uint64_t body_limit, source_digest;
   uint64_t compiler_rev;  // fnv64 of kCompilerRev
 };
@@ -42,7 +45,8 @@ uint64_t compiler_rev_hash() { return fnv64((const uint8_t*)kCompilerRev, strlen
   X(10, dfas) X(11, trans) X(12, u8pool) X(13, nranges) X(14, strpool) X(15, slot_names) X(16, u64pool)     \
   X(17, streams) X(18, filters) X(19, sfilt) X(20, body_links) X(21, always_slots) X(22, jobs) X(23, jdfas) \
   X(24, pats) X(25, svals) X(26, images) X(27, exports) X(28, nfas) X(29, pikes) X(30, pike_insts)              \
-  X(31, pike_ranges) X(32, dyn_sites) X(33, txrx) X(34, tx_snap) X(35, fold_ids) X(36, fold_runs)
+  X(31, pike_ranges) X(32, dyn_sites) X(33, txrx) X(34, tx_snap) X(35, fold_ids) X(36, fold_runs) \
+  X(37, rule_groups)
 
 constexpr uint32_t kTagScalars = 100, kTagPlan = 101, kTagExportNames = 102;
 
@@ -98,6 +102,8 @@ std::vector<uint8_t> serialize_program(const Program& P) {
   s.fold_on = P.fold_on;
   s.fold_nids = P.fold_nids;
   s.max_tx_lit = P.max_tx_lit;
+  s.n_rm_groups = P.n_rm_groups;
+  s.args_limit = P.args_limit;
   s.body_limit = P.body_limit;
   s.source_digest = P.source_digest;
   s.compiler_rev = compiler_rev_hash();
@@ -185,6 +191,8 @@ bool deserialize_program(const uint8_t* buf, size_t n, Program* P, std::string* 
         out.fold_on = s.fold_on;
         out.fold_nids = s.fold_nids;
         out.max_tx_lit = s.max_tx_lit;
+        out.n_rm_groups = s.n_rm_groups;
+        out.args_limit = s.args_limit;
         out.body_limit = s.body_limit;
         out.source_digest = s.source_digest;
         seen_scalars = true;
@@ -291,7 +299,7 @@ bool validate_program(const Program& P, std::string* err) {
     if (!in(r.var_begin, r.var_count, P.vars.size()) || (r.op >= 0 && (uint32_t)r.op >= P.ops.size()) ||
         !in(r.act_begin, r.act_count, P.acts.size()) || !in(r.tchain_off, r.tchain_len, P.tchains.size()) ||
         (r.chain_next >= 0 && (uint32_t)r.chain_next >= nrules) || r.phase > 5 ||
-        (r.hit_slot >= 0 && (uint32_t)r.hit_slot >= nhit) || r.hit_slot < -1)
+        (r.hit_slot >= 0 && (uint32_t)r.hit_slot >= nhit) || r.hit_slot < -1 || r.disruptive > D_ALLOW_REQUEST)
       return bad("rule record out of range");
     // k_eval runs the link's capture program (run_capture reads P.pikes[op.pike] and the
     // request's capture workspace): only an @rx link with a program may carry the flag
@@ -356,6 +364,14 @@ bool validate_program(const Program& P, std::string* err) {
     }
     if (a.kind == A_CTL_RULE_REMOVE_TARGET && (a.tmpl < 0 || a.aux < 0 || !in((uint32_t)a.tmpl, (uint32_t)a.aux, nstr)))
       return bad("ctl target key");
+    if ((a.kind == A_CTL_RULE_REMOVE_GROUP && (a.a < 0 || a.a >= (int64_t)P.n_rm_groups)) ||
+        (a.kind == A_CTL_RULE_REMOVE_TARGET && a.a == GI_RM_GROUP_MODE && (a.b < 0 || a.b >= (int64_t)P.n_rm_groups)))
+      return bad("ctl removal group");
+  }
+  if (P.n_rm_groups > GI_MAX_RM_GROUPS || P.rule_groups.size() != std::max<size_t>(nrules, 1)) return bad("removal groups");
+  for (uint32_t m : P.rule_groups)
+    if (P.n_rm_groups < 32 && (m >> P.n_rm_groups)) return bad("rule removal group mask");
+  {
   }
   // capture programs (pike.h): every jump inside its program, rune ranges in the pool
   for (const DPike& k : P.pikes) {

@@ -15,7 +15,7 @@
 
 namespace gi {
 
-constexpr uint32_t kArtifactVersion = 5;
+constexpr uint32_t kArtifactVersion = 6;
 
 // FNV-1a 64 (artifact checksum and SecLang source digest).
 uint64_t fnv64(const uint8_t* p, size_t n, uint64_t h = 1469598103934665603ull);

@@ -11,7 +11,11 @@
 #include "compile.h"
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
+#include <chrono>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <set>
 #include <memory>
@@ -174,6 +178,13 @@ struct IrNd {  // non-disruptive action in order
 };
 struct IrRule {
   int id = 0, phase = 2, line = 0;
+  std::vector<std::string> tags;  // tag:'...' values (SecRuleRemoveByTag, ctl:ruleRemove*ByTag)
+  std::string msg;                // msg:'...' as written (SecRuleRemoveByMsg, ctl:ruleRemove*ByMsg)
+  // a construct coraza.NewWAF accepts that this engine does not evaluate (a
+  // RESPONSE_* variable, an operator / transformation / ctl of the response
+  // path): harmless in a phase 3-5 rule (never evaluated by the request path),
+  // GI_EUNSUPPORTED in a phase 1-2 rule
+  std::string deferred;
   std::vector<IrVar> vars;
   bool has_op = false;
   std::string op_name, op_arg;
@@ -192,6 +203,7 @@ struct IrRule {
 using Actions = std::vector<std::pair<std::string, std::string>>;
 struct IrWaf {
   std::string engine = "On";
+  int64_t args_limit = 1000;  // SecArgumentsLimit (coraza WAF.ArgumentLimit)
   bool body_access = false;
   int64_t body_limit = 134217728;
   bool body_partial = false;
@@ -215,6 +227,7 @@ const std::map<std::string, std::string>& action_types() {
       {"expirevar", "nondisruptive"}, {"initcol", "nondisruptive"},
       {"sanitisearg", "nondisruptive"}, {"sanitisematched", "nondisruptive"},
       {"setenv", "nondisruptive"}, {"append", "nondisruptive"},
+      {"sanitiserequestheader", "nondisruptive"}, {"sanitiseresponseheader", "nondisruptive"},
   };
   return t;
 }
@@ -229,8 +242,9 @@ bool ignored_directive(const std::string& d) {
       "secdatadir", "secargumentseparator", "seccollectiontimeout", "secrequestbodynofileslimit",
       "secuploaddir", "secuploadkeepfiles", "secuploadfilemode", "secunicodemap",
       "secpcrematchlimit", "secpcrematchlimitrecursion", "secstatusengine", "secconnengine",
-      "secserversignature", "sechttpblkey", "secwebappid", "secsensorid", "secargumentslimit",
-      "secrequestbodyjsondepthlimit"};
+      "secserversignature", "sechttpblkey", "secwebappid", "secsensorid",
+      "secrequestbodyjsondepthlimit", "secresponsebodymimetypesclear", "seccookieformat",
+      "secuploadfilelimit", "secignorerulecompilationerrors"};
   for (auto* s : ign)
     if (d == s) return true;
   return starts_with(d, "secaudit") || starts_with(d, "secdebug");
@@ -301,7 +315,7 @@ const std::vector<std::string>& single_names() {
       "REQUEST_FILENAME", "REQUEST_BASENAME", "QUERY_STRING", "REQUEST_BODY",
       "REQUEST_BODY_LENGTH", "REQBODY_ERROR", "REQBODY_ERROR_MSG", "REQBODY_PROCESSOR",
       "MULTIPART_STRICT_ERROR", "REMOTE_ADDR", "REMOTE_PORT", "FILES_COMBINED_SIZE", "ARGS_COMBINED_SIZE",
-      "FULL_REQUEST_LENGTH", "URLENCODED_ERROR", "INBOUND_DATA_ERROR"};
+      "FULL_REQUEST_LENGTH", "URLENCODED_ERROR", "INBOUND_DATA_ERROR", "SERVER_NAME"};
   return v;
 }
 const std::map<std::string, int>& collection_ids() {
@@ -317,9 +331,21 @@ const std::map<std::string, int>& collection_ids() {
       {"MATCHED_VARS", V_MATCHED_VARS}, {"MATCHED_VARS_NAMES", V_MATCHED_VARS_NAMES}};
   return m;
 }
-// variables the oracle knows but this engine does not evaluate yet
+// Variables coraza v3.3.3 declares [upstream internal/variables/variables.go]
+// that the request path does not evaluate: the response phases' variables
+// (RESPONSE-950..980 read RESPONSE_BODY / RESPONSE_STATUS / RESPONSE_HEADERS),
+// and a few request-side ones this engine has no value for.  The parser
+// accepts them, as NewWAF does; a phase 1-2 rule that reads one is
+// GI_EUNSUPPORTED (IrRule::deferred).
 bool known_unsupported_var(const std::string& n) {
-  static const char* u[] = {"SERVER_NAME"};
+  static const char* u[] = {
+      "RESPONSE_BODY", "RESPONSE_STATUS", "RESPONSE_HEADERS", "RESPONSE_HEADERS_NAMES", "RESPONSE_PROTOCOL",
+      "RESPONSE_CONTENT_TYPE", "RESPONSE_CONTENT_LENGTH", "RESPONSE_ARGS", "RESPONSE_XML", "RES_BODY_PROCESSOR",
+      "OUTBOUND_DATA_ERROR", "STATUS_LINE", "SERVER_ADDR", "SERVER_PORT", "UNIQUE_ID", "REMOTE_HOST",
+      "HIGHEST_SEVERITY", "DURATION", "REQBODY_PROCESSOR_ERROR", "REQBODY_PROCESSOR_ERROR_MSG", "ARGS_PATH",
+      "FILES_TMP_CONTENT", "MULTIPART_FILENAME", "MULTIPART_NAME", "MULTIPART_DATA_AFTER", "GEO", "RULE", "JSON",
+      "ENV", "REQUEST_XML", "AUTH_TYPE", "TIME", "TIME_DAY", "TIME_EPOCH", "TIME_HOUR", "TIME_MIN", "TIME_MON",
+      "TIME_SEC", "TIME_WDAY", "TIME_YEAR"};
   for (auto* s : u)
     if (n == s) return true;
   return false;
@@ -375,6 +401,7 @@ void parse_variables(const std::string& s, IrRule* rule) {
     }
     name = upper(name);
     if (!is_known_var(name)) perr("unknown variable " + name);
+    if (known_unsupported_var(name) && rule->deferred.empty()) rule->deferred = "unsupported variable " + name;
     bool key_rx = false;
     if (key.size() >= 2 && key.front() == '\'' && key.back() == '\'') key = key.substr(1, key.size() - 2);
     if (key.size() > 2 && key.front() == '/' && key.back() == '/') {
@@ -591,10 +618,21 @@ void parse_operator(std::string opstr, IrRule* rule) {
                                 "unconditionalmatch", "nomatch", "validatebyterange",
                                 "validateurlencoding", "validateutf8encoding", "pmfromfile", "ipmatch",
                                 "ipmatchfromfile", "ipmatchf", "detectsqli", "detectxss"};
+  // operators coraza v3.3.3 has [upstream internal/operators] that this engine does not evaluate
+  static const char* later[] = {"geolookup", "inspectfile", "pmfromdataset", "ipmatchfromdataset", "rbl",
+                                "restpath", "strmatch", "validatenid", "validateschema", "verifycc",
+                                "verifycpf", "verifyssn", "fuzzyhash"};
   bool ok = false;
   for (auto* k : known)
     if (rule->op_name == k) ok = true;
-  if (!ok) unsup("unsupported operator @" + name);
+  if (!ok) {
+    for (auto* k : later)
+      if (rule->op_name == k) {
+        if (rule->deferred.empty()) rule->deferred = "unsupported operator @" + name;
+        return;
+      }
+    perr("invalid operator @" + name);
+  }
   if (rule->op_name == "pmfromfile") {
     if (!g_data_files || !g_data_files->count(data)) perr("open " + data + ": no such file or directory");
     rule->phrases = pm_file_phrases(g_data_files->at(data));
@@ -647,8 +685,19 @@ void apply_actions(IrRule* rule, const Actions& acts) {
       rule->phase = parse_phase(v);
     } else if (k == "deny" || k == "drop" || k == "pass" || k == "block" || k == "redirect" ||
                k == "allow") {
-      if (k == "allow") unsup("action allow is not supported");
       rule->disruptive = k;
+      if (k == "allow") {
+        // [upstream internal/actions/allow.go Init]: "" every phase, "phase", "request"
+        const std::string a = lower(v);
+        if (a.empty()) rule->disruptive = "allow";
+        else if (a == "phase") rule->disruptive = "allow:phase";
+        else if (a == "request") rule->disruptive = "allow:request";
+        else perr("invalid argument " + v + " for allow");
+      }
+    } else if (k == "tag") {
+      rule->tags.push_back(v);
+    } else if (k == "msg") {
+      rule->msg = v;
     } else if (k == "status") {
       int64_t st;
       if (!go_atoi(v, &st)) perr("invalid status " + v);
@@ -667,7 +716,14 @@ void apply_actions(IrRule* rule, const Actions& acts) {
         rule->transforms.clear();
       } else {
         uint8_t code;
-        if (!transform_code(tl, &code)) unsup("unsupported transformation t:" + v);
+        if (!transform_code(tl, &code)) {
+          // coraza v3.3.3's other transformations [upstream internal/transformations]
+          if (tl == "removecomments" || tl == "sqlhexdecode" || tl == "uppercase") {
+            if (rule->deferred.empty()) rule->deferred = "unsupported transformation t:" + v;
+            continue;
+          }
+          perr("invalid transformation t:" + v);
+        }
         rule->transforms.push_back(tl);
       }
     } else if (k == "capture") {
@@ -700,10 +756,27 @@ void apply_actions(IrRule* rule, const Actions& acts) {
       size_t eq = v.find('=');
       nd.ctl_name = lower(trim(eq == std::string::npos ? v : v.substr(0, eq)));
       nd.ctl_value = trim(eq == std::string::npos ? "" : v.substr(eq + 1));
-      if (nd.ctl_name != "ruleremovebyid" && nd.ctl_name != "ruleremovetargetbyid" && nd.ctl_name != "ruleengine" &&
-          nd.ctl_name != "requestbodyprocessor" && nd.ctl_name != "requestbodyaccess" &&
-          nd.ctl_name != "forcerequestbodyvariable")
-        unsup("unsupported ctl " + nd.ctl_name);
+      // [upstream internal/actions/ctl.go]: the ctl options coraza v3.3.3 parses
+      static const char* evaluated[] = {"ruleremovebyid", "ruleremovetargetbyid", "ruleremovebytag",
+                                        "ruleremovetargetbytag", "ruleremovebymsg", "ruleremovetargetbymsg",
+                                        "ruleengine", "requestbodyprocessor", "requestbodyaccess",
+                                        "forcerequestbodyvariable"};
+      // audit / debug logging and the response body: no effect on a request-phase verdict
+      static const char* no_effect[] = {"auditengine", "auditlogparts", "debugloglevel", "responsebodyaccess",
+                                        "responsebodylimit", "responsebodyprocessor", "forceresponsebodyvariable",
+                                        "hashengine", "hashenforcement"};
+      bool known = false;
+      for (auto* c : evaluated) known = known || nd.ctl_name == c;
+      if (!known) {
+        bool ign = false;
+        for (auto* c : no_effect) ign = ign || nd.ctl_name == c;
+        if (ign) continue;
+        if (nd.ctl_name == "requestbodylimit") {
+          if (rule->deferred.empty()) rule->deferred = "unsupported ctl " + nd.ctl_name;
+          continue;
+        }
+        perr("unknown ctl " + nd.ctl_name);
+      }
       rule->nd.push_back(nd);
     }
   }
@@ -732,8 +805,38 @@ Actions merge_defaults(const Actions& acts, const Actions& defs) {
   return res;
 }
 
+// id or "lo-hi" (coraza directives.go / ctl.go rangeToInts)
+bool parse_id_range(const std::string& s, int64_t* lo, int64_t* hi) {
+  const size_t dash = s.find('-', 1);
+  if (dash == std::string::npos) {
+    if (!go_atoi(s, lo)) return false;
+    *hi = *lo;
+    return true;
+  }
+  return go_atoi(s.substr(0, dash), lo) && go_atoi(s.substr(dash + 1), hi);
+}
+
 IrWaf parse_seclang(const std::string& text) {
   IrWaf waf;
+  // top-level rule ids in the group (coraza RuleGroup.Add rejects a repeated
+  // non-zero id: "there is a another rule with id"); removal frees an id
+  std::map<int, int> id_count;
+  auto erase_rules = [&](const std::function<bool(const IrRule&)>& pred) {
+    std::vector<IrRule> kept;
+    kept.reserve(waf.rules.size());
+    for (auto& r : waf.rules) {
+      if (pred(r)) {
+        if (r.id != 0 && --id_count[r.id] == 0) id_count.erase(r.id);
+      } else {
+        kept.push_back(std::move(r));
+      }
+    }
+    waf.rules.swap(kept);
+  };
+  auto has_tag = [](const IrRule& r, const std::string& t) {
+    return std::find(r.tags.begin(), r.tags.end(), t) != r.tags.end();
+  };
+  auto strip_q = [](const std::string& x) { return trim(trim(x), "\""); };
   std::vector<std::pair<int, std::string>> lines;
   {
     std::string buf;
@@ -783,6 +886,69 @@ IrWaf parse_seclang(const std::string& text) {
       if (o == "processpartial") waf.body_partial = true;
       else if (o == "reject") waf.body_partial = false;
       else perr("invalid SecRequestBodyLimitAction " + opts);
+    } else if (d == "secargumentslimit") {
+      int64_t v;
+      if (!go_atoi(trim(opts), &v)) perr("syntax error: SecArgumentsLimit [POSITIVE_INT]");
+      waf.args_limit = v;
+    } else if (d == "secruleremovebyid" || d == "secruleremovebytag" || d == "secruleremovebymsg") {
+      // [upstream internal/seclang/directives.go directiveSecRuleRemoveBy{ID,Tag,Msg}]:
+      // the rules defined so far leave the group (a chain goes with its parent)
+      if (parent) perr(directive + " inside a chain");
+      if (trim(opts).empty()) perr("expected options for " + directive);
+      if (d == "secruleremovebyid") {
+        std::stringstream ss(opts);
+        std::string part;
+        while (ss >> part) {
+          int64_t lo, hi;
+          if (!parse_id_range(part, &lo, &hi)) perr("invalid id " + part + " for SecRuleRemoveById");
+          erase_rules([&](const IrRule& r) { return r.id >= lo && r.id <= hi; });
+        }
+      } else if (d == "secruleremovebytag") {
+        const std::string tag = strip_q(opts);
+        erase_rules([&](const IrRule& r) { return has_tag(r, tag); });
+      } else {
+        const std::string msg = strip_q(opts);
+        erase_rules([&](const IrRule& r) { return r.secmark.empty() && r.msg == msg; });
+      }
+    } else if (d == "secruleupdatetargetbyid" || d == "secruleupdatetargetbytag" ||
+               d == "secruleupdatetargetbymsg" || d == "secruleupdateactionbyid") {
+      // [upstream directives.go directiveSecRuleUpdate{Target,Action}By*]: the
+      // variables (negations add exceptions to the rule's existing targets) or
+      // actions are parsed into the matching rules defined so far
+      if (parent) perr(directive + " inside a chain");
+      const std::string o = trim(opts);
+      const size_t sp2 = o.find(' ');
+      if (sp2 == std::string::npos) perr("syntax error: " + directive + " <selector> \"...\"");
+      const std::string sel = strip_q(o.substr(0, sp2)), arg = strip_q(o.substr(sp2 + 1));
+      std::vector<IrRule*> hit;
+      int64_t lo = 0, hi = -1;
+      if (d == "secruleupdatetargetbyid" || d == "secruleupdateactionbyid") {
+        if (!parse_id_range(sel, &lo, &hi)) perr("invalid id " + sel + " for " + directive);
+      }
+      for (auto& r : waf.rules) {
+        if (!r.secmark.empty()) continue;
+        const bool m = d == "secruleupdatetargetbytag" ? has_tag(r, sel)
+                       : d == "secruleupdatetargetbymsg" ? r.msg == sel
+                                                         : (r.id >= lo && r.id <= hi);
+        if (m) hit.push_back(&r);
+      }
+      if ((d == "secruleupdatetargetbyid" || d == "secruleupdateactionbyid") && lo == hi && hit.empty())
+        perr(directive + ": rule \"" + sel + "\" not found");
+      for (IrRule* r : hit) {
+        if (d == "secruleupdateactionbyid") {
+          const Actions acts = parse_actions(arg);
+          bool disr = false;
+          for (auto& kv : acts) {
+            if (kv.first == "id" || kv.first == "chain") perr("SecRuleUpdateActionById: action " + kv.first + " cannot be updated");
+            disr = disr || action_types().at(kv.first) == "disruptive";
+          }
+          if (disr) r->disruptive.clear();  // [upstream] Rule.ClearDisruptiveActions
+          apply_actions(r, acts);
+          for (auto& c : r->children) c.phase = r->phase;
+        } else {
+          parse_variables(arg, r);
+        }
+      }
     } else if (d == "secdefaultaction") {
       Actions acts = parse_actions(opts);
       int phase = 2;
@@ -838,6 +1004,8 @@ IrWaf parse_seclang(const std::string& text) {
         if (!more) parent = nullptr;
       } else {
         if (rule.id == 0) perr("rule id is required (line " + std::to_string(ln.first) + ")");
+        if (id_count.count(rule.id)) perr("there is a another rule with id " + std::to_string(rule.id));
+        id_count[rule.id]++;
         waf.rules.push_back(rule);
         if (rule.has_chain) parent = &waf.rules.back();
       }
@@ -847,6 +1015,31 @@ IrWaf parse_seclang(const std::string& text) {
     }
   }
   if (parent) perr("unterminated chain");
+  // The request path evaluates phases 1 and 2 (and phase-0 SecMarker records,
+  // RuleGroup.Eval's "Phase_ == 0 always runs").  Rules of phases 3-5 are
+  // parsed and validated like NewWAF does, then left out of the program: they
+  // cannot change a phase 1-2 verdict (skip:N does not count rules of other
+  // phases; their setvar / ctl run only after ProcessRequestBody).
+  for (const IrRule& r : waf.rules) {
+    if (r.phase != 1 && r.phase != 2) continue;
+    if (!r.deferred.empty()) unsup(r.deferred + " (rule " + std::to_string(r.id) + ", phase " + std::to_string(r.phase) + ")");
+    for (const IrRule& c : r.children)
+      if (!c.deferred.empty()) unsup(c.deferred + " (chain of rule " + std::to_string(r.id) + ")");
+  }
+  waf.rules.erase(std::remove_if(waf.rules.begin(), waf.rules.end(), [](const IrRule& r) { return r.phase >= 3; }),
+                  waf.rules.end());
+  // SecMarkers no remaining skipAfter names (the response files' END-* markers)
+  // are no-ops of every walk -- unless a skip:N counts them
+  bool any_skip = false;
+  std::set<std::string> targets;
+  for (const IrRule& r : waf.rules) {
+    any_skip = any_skip || r.skip > 0;
+    if (!r.skip_after.empty()) targets.insert(r.skip_after);
+  }
+  if (!any_skip)
+    waf.rules.erase(std::remove_if(waf.rules.begin(), waf.rules.end(),
+                                   [&](const IrRule& r) { return !r.secmark.empty() && !targets.count(r.secmark); }),
+                    waf.rules.end());
   return waf;
 }
 
@@ -855,6 +1048,7 @@ struct Lower {
   Program* P;
   std::map<std::string, int> slots;
   std::map<std::string, int> markers;
+  std::map<std::string, int> rm_groups;  // ctl removal groups: "t:<tag>" / "m:<msg>" -> bit
   std::map<std::string, int> dfa_cache;  // -1: no DFA (state cap), see nfa_cache
   std::map<std::string, int> nfa_cache;
   std::vector<std::pair<uint32_t, std::string>> tx_rx_vars;  // regex-keyed TX targets: (vars index, key regex)
@@ -874,6 +1068,14 @@ struct Lower {
     slots[k] = id;
     P->slot_names.push_back(str(k));
     P->slot_names.push_back((uint32_t)k.size());
+    return id;
+  }
+  int rm_group(const std::string& key) {
+    auto it = rm_groups.find(key);
+    if (it != rm_groups.end()) return it->second;
+    if (rm_groups.size() >= GI_MAX_RM_GROUPS) unsup("more than 32 distinct ctl:ruleRemove*ByTag / ByMsg values");
+    const int id = (int)rm_groups.size();
+    rm_groups[key] = id;
     return id;
   }
   int marker(const std::string& name) {
@@ -989,18 +1191,41 @@ struct Lower {
     for (auto& p : phrases) total += p.size();
     *ngroups = 0;
     if (total <= kPhraseGroupBytes) return phrase_dfa(phrases, fold, key);
-    auto groups = phrase_groups(phrases);
-    std::vector<Dfa> ds(groups.size());
-    std::string err;
-    for (size_t k = 0; k < groups.size(); k++)
-      if (!build_phrase_dfa(groups[k], fold, &ds[k], &err, cap)) unsup(err);
+    std::vector<Dfa> ds = phrase_group_dfas(phrases, fold);
     int first = -1;
     for (auto& d : ds) {
       const int id = add_dfa(d);
       if (first < 0) first = id;
     }
-    *ngroups = (uint32_t)groups.size();
+    *ngroups = (uint32_t)ds.size();
     return first;
+  }
+  // The group automata of a large phrase set, built on all host cores (each
+  // group is an independent Aho-Corasick automaton) and kept for the phase-A
+  // plan, which scans the same groups.
+  std::map<std::pair<bool, std::vector<std::string>>, std::vector<Dfa>> group_cache;
+  std::vector<Dfa> phrase_group_dfas(const std::vector<std::string>& phrases, bool fold) {
+    auto key = std::make_pair(fold, phrases);
+    auto it = group_cache.find(key);
+    if (it != group_cache.end()) return it->second;
+    const auto groups = phrase_groups(phrases);
+    std::vector<Dfa> ds(groups.size());
+    std::vector<std::string> errs(groups.size());
+    std::vector<char> ok(groups.size(), 0);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t k; (k = next.fetch_add(1)) < groups.size();)
+        ok[k] = build_phrase_dfa(groups[k], fold, &ds[k], &errs[k], cap) ? 1 : 0;
+    };
+    const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16));
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt && t < groups.size(); t++) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    for (size_t k = 0; k < groups.size(); k++)
+      if (!ok[k]) unsup(errs[k]);
+    group_cache[key] = ds;
+    return ds;
   }
   int phrase_dfa(const std::vector<std::string>& phrases, bool fold, const std::string& key) {
     auto it = dfa_cache.find(key);
@@ -1380,19 +1605,25 @@ struct Lower {
           a.b = hi;
           P->acts.push_back(a);
         }
-      } else if (nd.ctl_name == "ruleremovetargetbyid") {
-        // "ID[-ID];VARIABLE[:key]" [upstream internal/actions/ctl.go]
+      } else if (nd.ctl_name == "ruleremovebytag" || nd.ctl_name == "ruleremovebymsg") {
+        // [upstream internal/actions/ctl.go]: every rule whose tags contain the
+        // value (whose msg equals it) is removed by id for the transaction
+        DAction a{};
+        a.kind = A_CTL_RULE_REMOVE_GROUP;
+        a.a = rm_group((nd.ctl_name == "ruleremovebytag" ? "t:" : "m:") + nd.ctl_value);
+        P->acts.push_back(a);
+      } else if (nd.ctl_name == "ruleremovetargetbyid" || nd.ctl_name == "ruleremovetargetbytag" ||
+                 nd.ctl_name == "ruleremovetargetbymsg") {
+        // "ID[-ID];VARIABLE[:key]" / "TAG;VARIABLE[:key]" / "MSG;VARIABLE[:key]" [upstream internal/actions/ctl.go]
         const size_t semi = nd.ctl_value.find(';');
-        if (semi == std::string::npos) perr("invalid ctl:ruleRemoveTargetById " + nd.ctl_value);
+        if (semi == std::string::npos) perr("invalid ctl:" + nd.ctl_name + " " + nd.ctl_value);
         const std::string ids = trim(nd.ctl_value.substr(0, semi)), tgt = trim(nd.ctl_value.substr(semi + 1));
         int64_t lo, hi;
-        const size_t dash = ids.find('-');
-        if (dash != std::string::npos && dash > 0) {
-          if (!go_atoi(ids.substr(0, dash), &lo) || !go_atoi(ids.substr(dash + 1), &hi))
-            perr("invalid ctl:ruleRemoveTargetById " + nd.ctl_value);
-        } else {
-          if (!go_atoi(ids, &lo)) perr("invalid ctl:ruleRemoveTargetById " + nd.ctl_value);
-          hi = lo;
+        if (nd.ctl_name != "ruleremovetargetbyid") {
+          lo = GI_RM_GROUP_MODE;
+          hi = rm_group((nd.ctl_name == "ruleremovetargetbytag" ? "t:" : "m:") + ids);
+        } else if (!parse_id_range(ids, &lo, &hi)) {
+          perr("invalid ctl:ruleRemoveTargetById " + nd.ctl_value);
         }
         const size_t colon = tgt.find(':');
         const std::string vname = upper(trim(tgt.substr(0, colon)));
@@ -1474,7 +1705,8 @@ struct Lower {
   static bool immutable_single(int sid) {
     return sid == S_REQUEST_METHOD || sid == S_REQUEST_PROTOCOL || sid == S_REQUEST_URI ||
            sid == S_REQUEST_URI_RAW || sid == S_REQUEST_LINE || sid == S_REQUEST_FILENAME ||
-           sid == S_REQUEST_BASENAME || sid == S_QUERY_STRING || sid == S_REMOTE_ADDR || sid == S_REMOTE_PORT;
+           sid == S_REQUEST_BASENAME || sid == S_QUERY_STRING || sid == S_REMOTE_ADDR || sid == S_REMOTE_PORT ||
+           sid == S_SERVER_NAME;
   }
 
   // Assigns a hit slot and registers the link's patterns, or returns -1 when
@@ -1734,6 +1966,8 @@ struct Lower {
         }
         return false;
       };
+      // patterns that may share a union automaton, in order (packed below)
+      std::vector<std::pair<const PatEntry*, std::unique_ptr<Regex>>> unionable;
       for (auto& pe : sb.pats) {
         auto re = std::make_unique<Regex>();
         bool ok;
@@ -1744,11 +1978,7 @@ struct Lower {
             P->always_slots.push_back(pe.slot);
             continue;
           }
-          for (auto& g : phrase_groups(pe.phrases)) {
-            Dfa d;
-            if (!build_phrase_dfa(g, pe.kind == 1, &d, &err, cap)) unsup(err);
-            autos.push_back({std::move(d), {&pe}});
-          }
+          for (auto& d : phrase_group_dfas(pe.phrases, pe.kind == 1)) autos.push_back({std::move(d), {&pe}});
           continue;
         }
         if (pe.kind == 0) {
@@ -1772,35 +2002,93 @@ struct Lower {
           autos.push_back({std::move(single), {&pe}});
           continue;
         }
-        Dfa trial;
-        cur.push_back(re.get());
-        curp.push_back(&pe);
-        if (cur.size() <= 64 && build_union_dfa(cur, &trial, &err, 16384) && img_bytes(trial) <= kUnionTableBytes) {
-          curd = std::move(trial);
-          owned.push_back(std::move(re));
-          continue;
-        }
-        cur.pop_back();
-        curp.pop_back();
-        flush();
-        cur.push_back(re.get());
-        curp.push_back(&pe);
-        if (build_union_dfa(cur, &trial, &err, 16384) && img_bytes(trial) <= kUnionTableBytes) {
-          curd = std::move(trial);
-          owned.push_back(std::move(re));
-          continue;
-        }
-        // too large for an LDS union automaton: single sticky DFA (global tables)
-        Dfa single;
-        cur.clear();
-        curp.clear();
-        if (!single_or_relaxed(pe, *re, &single)) {  // no automaton: the link is always "maybe"
-          P->always_slots.push_back(pe.slot);
-          continue;
-        }
-        autos.push_back({std::move(single), {&pe}});
-        owned.push_back(std::move(re));
+        unionable.emplace_back(&pe, std::move(re));
       }
+      // Greedy packing: each union automaton takes the longest run of the next
+      // patterns (<= 64) whose union DFA stays within 16384 states and the LDS
+      // table budget.  The run length is found by galloping + bisection over
+      // the prefix length (a longer prefix only adds states), so a union of n
+      // patterns costs O(log n) builds instead of n.  Runs of kPackChunk
+      // patterns are packed independently, on all host cores (a chunk boundary
+      // also ends a union: the plan does not depend on the thread count).
+      constexpr size_t kPackChunk = 512;
+      struct Packed {
+        std::vector<AutoBuild> autos;  // in order; an empty pes list marks an "always" slot
+        std::vector<const PatEntry*> always;
+      };
+      const size_t nchunks = (unionable.size() + kPackChunk - 1) / kPackChunk;
+      std::vector<Packed> packed(nchunks);
+      auto pack_chunk = [&](size_t ch) {
+        std::string lerr;
+        Packed& out = packed[ch];
+        const size_t end = std::min(unionable.size(), (ch + 1) * kPackChunk);
+        for (size_t i = ch * kPackChunk; i < end;) {
+          const size_t maxn = std::min<size_t>(64, end - i);
+          auto fits = [&](size_t n, Dfa* d) {
+            std::vector<const Regex*> rs;
+            for (size_t k = 0; k < n; k++) rs.push_back(unionable[i + k].second.get());
+            return build_union_dfa(rs, d, &lerr, 16384, kUnionTableBytes) && img_bytes(*d) <= kUnionTableBytes;
+          };
+          size_t lo = 0, hi = maxn + 1, step = 1;  // a union of lo patterns fits, of hi does not
+          Dfa best;
+          while (lo < maxn) {
+            const size_t n = std::min(lo + step, maxn);
+            Dfa t;
+            if (!fits(n, &t)) {
+              hi = n;
+              break;
+            }
+            lo = n;
+            best = std::move(t);
+            step *= 2;
+          }
+          while (hi - lo > 1) {
+            const size_t mid = (lo + hi) / 2;
+            Dfa t;
+            if (fits(mid, &t)) {
+              lo = mid;
+              best = std::move(t);
+            } else {
+              hi = mid;
+            }
+          }
+          if (lo > 0) {
+            std::vector<const PatEntry*> ps;
+            for (size_t k = 0; k < lo; k++) ps.push_back(unionable[i + k].first);
+            out.autos.push_back({std::move(best), ps});
+            i += lo;
+            continue;
+          }
+          // too large for an LDS union automaton: single sticky DFA (global tables)
+          const PatEntry& pe = *unionable[i].first;
+          Dfa single;
+          bool ok = build_regex_dfa(*unionable[i].second, &single, &lerr, cap);
+          for (int lvl = 1; !ok && !pe.negate && pe.kind == 0 && lvl <= 3; lvl++) {
+            Regex rr = *unionable[i].second;
+            relax_regex(&rr, lvl);
+            ok = build_regex_dfa(rr, &single, &lerr, cap);
+          }
+          if (ok) out.autos.push_back({std::move(single), {&pe}});
+          else out.always.push_back(&pe);  // no automaton: the link is always "maybe"
+          i++;
+        }
+      };
+      {
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+          for (size_t ch; (ch = next.fetch_add(1)) < nchunks;) pack_chunk(ch);
+        };
+        const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16));
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nt && t < nchunks; t++) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+      }
+      for (auto& pk : packed) {
+        for (auto& ab : pk.autos) autos.push_back(std::move(ab));
+        for (const PatEntry* pe : pk.always) P->always_slots.push_back(pe->slot);
+      }
+      for (auto& u : unionable) owned.push_back(std::move(u.second));
       flush();
       // 1b. rune map: the joint partition of non-ASCII runes over the stream's
       // image automata.  Every rune of a joint class falls in one class of
@@ -2033,7 +2321,8 @@ struct Lower {
     if (r.multimatch) d.flags |= RF_MULTIMATCH;
     const std::string& dis = r.disruptive;
     d.disruptive = dis == "deny" ? D_DENY : dis == "drop" ? D_DROP : dis == "redirect" ? D_REDIRECT
-                   : dis == "pass" ? D_PASS : D_NONE;
+                   : dis == "pass" ? D_PASS : dis == "allow" ? D_ALLOW_ALL : dis == "allow:phase" ? D_ALLOW_PHASE
+                   : dis == "allow:request" ? D_ALLOW_REQUEST : D_NONE;
     if (dis == "block") d.disruptive = D_NONE;  // block without a default disruptive action
     vars(r, &d);
     if (r.has_op) d.op = op(r);
@@ -2605,13 +2894,14 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
   // or on rules
   auto barrier = [&](uint32_t top) {
     const DRule& R = P.rules[top];
-    if (P.rule_engine == ENGINE_ON && (R.disruptive == D_DENY || R.disruptive == D_DROP || R.disruptive == D_REDIRECT))
-      return true;
+    if (P.rule_engine == ENGINE_ON && R.disruptive != D_NONE && R.disruptive != D_PASS) return true;  // deny/drop/redirect/allow
     for (int32_t ci = (int32_t)top; ci >= 0; ci = P.rules[ci].chain_next) {
       const DRule& d = P.rules[ci];
       for (uint32_t q = 0; q < d.act_count; q++) {
         const uint8_t kd = P.acts[d.act_begin + q].kind;
-        if (kd == A_CTL_RULE_ENGINE || kd == A_CTL_RULE_REMOVE_ID || kd == A_CTL_RULE_REMOVE_TARGET) return true;
+        if (kd == A_CTL_RULE_ENGINE || kd == A_CTL_RULE_REMOVE_ID || kd == A_CTL_RULE_REMOVE_TARGET ||
+            kd == A_CTL_RULE_REMOVE_GROUP)
+          return true;
       }
     }
     return false;
@@ -2668,8 +2958,8 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
               matched = false;
               break;
             }
-          const bool interrupts = matched && P.rule_engine == ENGINE_ON &&
-                                  (R.disruptive == D_DENY || R.disruptive == D_DROP || R.disruptive == D_REDIRECT);
+          const bool interrupts = matched && P.rule_engine == ENGINE_ON && R.disruptive != D_NONE &&
+                                  R.disruptive != D_PASS;  // deny/drop/redirect, or allow (ends the walk)
           if (!interrupts) {
             for (int32_t ci = (int32_t)ri; ci >= 0; ci = P.rules[ci].chain_next) in_prefix[ci] = true;
             if (run < 0) {
@@ -2795,6 +3085,7 @@ static void fold_program(Program* Pp, const std::vector<std::string>& exports) {
         if (!always) continue;
         for (const auto& rg : removable)
           if (G.id != 0 && rg.first <= G.id && G.id <= rg.second) always = false;
+        if (P.n_rm_groups && P.rule_groups[w[g]]) always = false;
         const uint32_t me = G.skip_after < (int32_t)P.n_markers ? mpos[G.skip_after] : 0xFFFFFFFFu;
         if (!always || me == 0xFFFFFFFFu || me <= g + 1) continue;
         // nothing outside (g, me) lands inside it
@@ -2916,8 +3207,17 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
     explicit FilesScope(const std::map<std::string, std::string>* f) { g_data_files = f; }
     ~FilesScope() { g_data_files = nullptr; }
   } files_scope(data_files);
+  const bool timing = getenv("GI_COMPILE_TIMING") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!timing) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "gi_compile: %-16s %8.3f s\n", what, std::chrono::duration<double>(now - t_prev).count());
+    t_prev = now;
+  };
   try {
     IrWaf waf = parse_seclang(text);
+    lap("parse");
     Lower L;
     L.P = out;
     L.cap = cap ? cap : 60000;
@@ -2939,7 +3239,25 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
         prev = ci;
       }
     }
+    lap("lower rules");
     L.finish_streams();
+    lap("scan plan");
+    // ctl removal groups: each top-level rule's membership (its tags / msg)
+    out->n_rm_groups = (uint32_t)L.rm_groups.size();
+    out->rule_groups.assign(std::max<size_t>(out->rules.size(), 1), 0u);
+    if (out->n_rm_groups)
+      for (size_t ti = 0; ti < waf.rules.size(); ti++) {
+        const IrRule& r = waf.rules[ti];
+        uint32_t m = 0;
+        for (const auto& g : L.rm_groups) {
+          const bool tag = g.first[0] == 't';
+          const std::string v = g.first.substr(2);
+          if (tag ? std::find(r.tags.begin(), r.tags.end(), v) != r.tags.end() : (r.secmark.empty() && r.msg == v))
+            m |= 1u << g.second;
+        }
+        out->rule_groups[out->top[ti]] = m;
+      }
+    out->args_limit = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(waf.args_limit, 0x7FFFFFFF));
     // chains whose later links read MATCHED_VARS(_NAMES) (the first link reads
     // them right after RuleGroup.Eval's reset: empty)
     for (uint32_t ti : out->top)
@@ -2986,7 +3304,9 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
       v.key_len = (uint32_t)out->txrx.size() - v.key_off;
     }
     if (out->txrx.empty()) out->txrx.push_back(0);
+    lap("tx regex keys");
     fold_program(out, exports);
+    lap("fold");
     for (const DAction& a : out->acts)  // literal setvar values (snapshot strings are literals or their expansions)
       if ((a.kind == A_SETVAR) && a.tmpl >= 0) {
         const DTmpl& tm = out->tmpls[a.tmpl];

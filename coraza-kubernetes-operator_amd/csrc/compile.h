@@ -16,7 +16,7 @@ namespace gi {
 // even when the record layout stays the same.  gi_compile folds it into the
 // source digest and the artifact stores it, so an artifact written by another
 // compiler revision is rejected (and recompiled from the rules text).
-constexpr const char* kCompilerRev = "gi-seclang-compiler/15";
+constexpr const char* kCompilerRev = "gi-seclang-compiler/16";
 
 struct Program {
   std::vector<DRule> rules;
@@ -55,6 +55,9 @@ struct Program {
   std::vector<uint32_t> txrx;          // static slots each regex-keyed TX target matches
   std::vector<DSnapSlot> tx_snap;      // folded TX state after the request-independent phase-1 prefix
   std::vector<uint32_t> fold_ids;      // rule ids that prefix matched
+  std::vector<uint32_t> rule_groups;   // per rule record: ctl removal-group mask (ByTag / ByMsg); [0] when none
+  uint32_t n_rm_groups = 0;
+  uint32_t args_limit = 1000;          // SecArgumentsLimit
   std::vector<uint32_t> fold_runs;     // per run of folded phase-1 rules: ids offset, id count, walk end,
                                        // skipAfter marker pending at the end (0xFFFFFFFF: none)
   uint32_t fold_nids = 0;              // fold_ids entries (the section holds a placeholder when 0)

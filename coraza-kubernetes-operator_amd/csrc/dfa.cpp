@@ -329,7 +329,7 @@ bool partition_classes(const std::vector<const Regex*>& pats, ClassPart* cp, std
 
 // Shared subset construction over a list of patterns.
 bool build_core(const std::vector<const Regex*>& pats, bool multi, Dfa* out, std::string* err,
-                uint32_t state_cap) {
+                uint32_t state_cap, uint32_t byte_budget = 0) {
   *out = Dfa();
   out->multi = multi;
   out->n_pat = (uint32_t)pats.size();
@@ -341,6 +341,7 @@ bool build_core(const std::vector<const Regex*>& pats, bool multi, Dfa* out, std
   if (!partition_classes(pats, &cp, err)) return false;
   const std::vector<std::vector<int>>& node_set = cp.node_set;
   const uint32_t ncls = cp.ncls;
+  if (byte_budget) state_cap = std::min<uint32_t>(state_cap, byte_budget / (2 * ncls + (multi ? 8 : 1)) + 1);
   out->n_classes = ncls;
   out->amap = cp.amap;
   out->nranges = cp.nranges;
@@ -511,8 +512,9 @@ bool build_regex_dfa(const Regex& re, Dfa* out, std::string* err, uint32_t state
   return build_core({&re}, false, out, err, state_cap);
 }
 
-bool build_union_dfa(const std::vector<const Regex*>& pats, Dfa* out, std::string* err, uint32_t state_cap) {
-  return build_core(pats, true, out, err, state_cap);
+bool build_union_dfa(const std::vector<const Regex*>& pats, Dfa* out, std::string* err, uint32_t state_cap,
+                     uint32_t byte_budget) {
+  return build_core(pats, true, out, err, state_cap, byte_budget);
 }
 
 // Position tables of the Thompson NFA (exact matcher for patterns whose DFA

@@ -108,6 +108,16 @@ struct DBatch {
   uint32_t bparse_lds;        // k_bparse: JSON bodies up to this many bytes are parsed from LDS (its dynamic LDS)
   uint32_t rstride;           // request stride of the request-major SoA arrays (hits, txslots): the staged
                               // batch's size (a chunk view of it has n_req <= rstride)
+  // Phase-1 gate (launch_pipeline): stage 1 runs phase A over the phase-1
+  // fields and evaluates phase 1 (whole requests without a body); a request a
+  // phase-1 rule interrupted is final there -- coraza never calls
+  // WriteRequestBody for it.  Stage 2 parses the bodies of the other (pending)
+  // requests, runs phase A over their body fields and evaluates them in full.
+  uint32_t stage;             // 0: one pass (no gate); 1: phase-1 stage; 2: body stage
+  uint32_t gate;              // the host allows the gate (GI_GATE=0 turns it off)
+  uint8_t* pend;              // [n_req] stage 1 -> 2: 1 = the request continues to the body stage
+  uint32_t* plist;            // the pending requests (stage-1 k_eval appends), *pcount of them
+  uint32_t* pcount;
 };
 
 // k_scan launch plan: job lists for the small-LDS and big-LDS launches.

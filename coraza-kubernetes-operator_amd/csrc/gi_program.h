@@ -79,6 +79,7 @@ enum SingleId : uint8_t {
   S_FULL_REQUEST_LENGTH,  // declared, never set by coraza v3.3.3: ""
   S_URLENCODED_ERROR,     // declared, never set by coraza v3.3.3: ""
   S_INBOUND_DATA_ERROR,   // "1" when the body reached SecRequestBodyLimit
+  S_SERVER_NAME,          // Transaction.SetServerName (gi_request.server_name; "" when not set)
   S_COUNT
 };
 #define GI_REQHDR_BYTES 384
@@ -186,7 +187,12 @@ enum TCode : uint8_t {
   T_COUNT
 };
 
-enum Disruptive : uint8_t { D_NONE = 0, D_DENY = 1, D_DROP = 2, D_REDIRECT = 3, D_PASS = 4 };
+// D_ALLOW_*: the allow action [upstream internal/actions/allow.go]: "allow" (every remaining phase but
+// logging), "allow:phase" (the rest of the current phase), "allow:request" (the rest of the request phases)
+enum Disruptive : uint8_t {
+  D_NONE = 0, D_DENY = 1, D_DROP = 2, D_REDIRECT = 3, D_PASS = 4,
+  D_ALLOW_ALL = 5, D_ALLOW_PHASE = 6, D_ALLOW_REQUEST = 7
+};
 
 enum RuleFlags : uint8_t {
   RF_FOLDED = 128,  // first rule of a run of folded request-independent phase-1 rules: k_eval emits the
@@ -215,8 +221,15 @@ enum ActKind : uint8_t {
   A_CTL_BODY_PROCESSOR,
   A_CTL_BODY_ACCESS,
   A_CTL_FORCE_BODY,
-  A_CTL_RULE_REMOVE_TARGET,  // ctl:ruleRemoveTargetById: a..b ids, slot = VarId, tmpl/_pad2 = key (strpool, lowercase)
+  A_CTL_RULE_REMOVE_TARGET,  // ctl:ruleRemoveTargetById: a..b ids, slot = VarId, tmpl/_pad2 = key (strpool, lowercase);
+                             // ctl:ruleRemoveTargetByTag / ByMsg: a = GI_RM_GROUP_MODE, b = the group's bit
+  A_CTL_RULE_REMOVE_GROUP,   // ctl:ruleRemoveByTag / ruleRemoveByMsg: a = the group's bit (DProgram.rule_groups)
 };
+// ctl:ruleRemove*ByTag / ByMsg [upstream internal/actions/ctl.go]: the rules whose tags contain the value
+// (whose msg equals it) are a "removal group" fixed at compile time; a request's removed groups are a
+// 32-bit mask tested against DProgram.rule_groups[rule index]
+#define GI_MAX_RM_GROUPS 32
+#define GI_RM_GROUP_MODE INT64_MIN
 
 // setvar fast forms (DAction.a for A_SETVAR)
 enum SetvarForm : int64_t {
@@ -626,6 +639,9 @@ struct DProgram {
   uint8_t mv_used;              // some target / macro reads MATCHED_VAR(S)(_NAME(S)): k_eval records matches
   uint8_t body_partial;         // SecRequestBodyLimitAction ProcessPartial (else Reject)
   uint64_t body_limit;
+  const uint32_t* rule_groups;  // per rule record: the ctl removal groups (ByTag / ByMsg) it belongs to
+  uint32_t n_rm_groups;         // 0: no ctl:ruleRemove*ByTag / ByMsg in the program
+  uint32_t args_limit;          // SecArgumentsLimit (coraza WAF.ArgumentLimit, default 1000): ARGS_GET
   uint32_t n_det_streams;       // streams with @detectSQLi/@detectXSS vals (k_detect entries carry a mask)
   uint32_t det_streams[GI_MAX_DET_STREAMS];
 };

@@ -292,6 +292,16 @@ GI_HD __forceinline__ uint64_t gi_clock() {
   return 0;
 #endif
 }
+// a list slot (the gate's pending list; the host interpreter never appends)
+GI_HD __forceinline__ uint32_t gi_fetch_add(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicAdd(p, v);
+#else
+  const uint32_t o = *p;
+  *p = o + v;
+  return o;
+#endif
+}
 GI_HD __forceinline__ void gi_prof_add(unsigned long long* p, unsigned long long v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   atomicAdd(p, v);
@@ -1291,6 +1301,7 @@ GI_HD const char* var_name(uint32_t var) {
     case S_REQBODY_PROCESSOR: return "REQBODY_PROCESSOR";
     case S_MULTIPART_STRICT_ERROR: return "MULTIPART_STRICT_ERROR";
     case S_REMOTE_ADDR: return "REMOTE_ADDR";
+    case S_SERVER_NAME: return "SERVER_NAME";
     case S_REMOTE_PORT: return "REMOTE_PORT";
     case S_FILES_COMBINED_SIZE: return "FILES_COMBINED_SIZE";
     case S_ARGS_COMBINED_SIZE: return "ARGS_COMBINED_SIZE";
@@ -1406,6 +1417,9 @@ struct Tx {
   uint32_t nrtgt;
   const uint32_t* kx;        // kind index (build_kindex; nullptr: scan all fields)
   uint32_t nremoved;
+  uint32_t rm_groups;        // ctl:ruleRemoveByTag / ByMsg groups removed (DProgram.rule_groups)
+  uint32_t cur_groups;       // removal groups of the top-level rule being evaluated
+  uint8_t allow;             // allow action in effect (D_ALLOW_*; 0: none)
   uint8_t engine, body_access, body_proc, phase;
   uint8_t force_body;
   int32_t skip_after;
@@ -3709,6 +3723,9 @@ GI_HD __forceinline__ void run_actions(Tx& t, const DRule& R) {
           t.flags |= GI_REQ_OVERFLOW;
         }
         break;
+      case A_CTL_RULE_REMOVE_GROUP:
+        t.rm_groups |= 1u << (uint32_t)a.a;
+        break;
       case A_CTL_RULE_ENGINE:
         t.engine = (uint8_t)a.a;
         break;
@@ -4103,15 +4120,19 @@ GI_HD __forceinline__ Str transform(Tx& t, const DRule& R, const uint8_t* v, uin
 // ctl:ruleRemoveTargetById: the link's rule id removed variable `var`
 // entries with key k (coraza rule.go doEvaluate adds them to the variable's
 // exceptions: compared with the lowercased key; a single's key is "")
+// (ctl:ruleRemoveTargetByTag / ByMsg entries name a removal group: the rule's
+// groups `groups` must hold it)
 GI_HD __noinline__ bool target_removed_in(const Tx::RmTarget* rt, uint32_t n, const uint8_t* strpool, int32_t id,
-                                               uint32_t var, const uint8_t* k, uint32_t kn) {
+                                               uint32_t groups, uint32_t var, const uint8_t* k, uint32_t kn) {
   for (uint32_t e = 0; e < n; e++) {
     const Tx::RmTarget x = rt[e];
-    if (x.var == var && x.lo <= id && id <= x.hi && eq_ascii_ci(k, kn, strpool + x.koff, x.klen)) return true;
+    const bool sel = x.lo == GI_RM_GROUP_MODE ? ((groups >> (uint32_t)x.hi) & 1u) != 0u : (x.lo <= id && id <= x.hi);
+    if (x.var == var && sel && eq_ascii_ci(k, kn, strpool + x.koff, x.klen)) return true;
   }
   return false;
 }
-#define target_removed(t, id, var, k, kn) target_removed_in((t).rtgt, (t).nrtgt, (t).P->strpool, (id), (var), (k), (kn))
+#define target_removed(t, id, var, k, kn) \
+  target_removed_in((t).rtgt, (t).nrtgt, (t).P->strpool, (id), (t).cur_groups, (var), (k), (kn))
 
 GI_HD __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
   const DProgram& P = *t.P;
@@ -4639,6 +4660,7 @@ GI_HD __forceinline__ void eval_top(Tx& t, uint32_t ri) {
   // the rule and its chain links; all must match (one eval_rule call site)
   t.prof_evals++;
   t.cur_id = (uint32_t)R.id;
+  t.cur_groups = P.n_rm_groups ? P.rule_groups[ri] : 0u;
   if (t.mv) {
     t.mv->keep = R.flags2 & RF2_MVS;
     t.mv->cur = R.flags2 & RF2_MVCUR;
@@ -4665,6 +4687,8 @@ GI_HD __forceinline__ void eval_top(Tx& t, uint32_t ri) {
     t.int_action = R.disruptive == D_DENY ? GI_ACTION_DENY : R.disruptive == D_DROP ? GI_ACTION_DROP
                                                                                      : GI_ACTION_REDIRECT;
     t.int_phase = t.phase;
+  } else if (R.disruptive >= D_ALLOW_ALL && t.engine == ENGINE_ON) {
+    t.allow = R.disruptive;  // [upstream allow.go Evaluate: tx.AllowType]; eval_phase ends the walk
   }
   if (R.id != 0) {
     if (t.nmatched < t.mcap) t.mout[t.nmatched] = (uint32_t)R.id;
@@ -4679,11 +4703,12 @@ GI_HD __forceinline__ void eval_top(Tx& t, uint32_t ri) {
 // pending, every rule but the target marker.  (Used by k_eval_wave to jump
 // over runs of such rules 64 at a time; MATCHED_VARS is reset before every
 // evaluated rule, so skipping the resets of no-op rules changes nothing.)
-GI_HD __forceinline__ bool rule_noop(Tx& t, const DRule& R) {
+GI_HD __forceinline__ bool rule_noop(Tx& t, const DRule& R, uint32_t ri) {
   if (R.id != 0 && t.nremoved) {
     for (uint32_t j = 0; j < t.nremoved; j++)
       if (t.removed[j][0] <= R.id && R.id <= t.removed[j][1]) return true;
   }
+  if (t.rm_groups && (t.P->rule_groups[ri] & t.rm_groups)) return true;
   if (t.skip_after >= 0) return R.marker != t.skip_after;
   if (R.flags & RF_MARKER) return true;
   if ((R.flags & RF_CONST) && R._pad2 == 0) return true;  // a folded link that matches nothing
@@ -4696,6 +4721,9 @@ template <bool W>
 GI_HD __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
   const DProgram& P = *t.P;
   if (t.engine == ENGINE_OFF) return;
+  // an allow of an earlier phase: "allow" skips every later phase but logging,
+  // "allow:request" the rest of the request phases -- both end here (phases 1, 2)
+  if (t.allow == D_ALLOW_ALL || t.allow == D_ALLOW_REQUEST) return;
   t.phase = phase;
   const uint32_t kend = P.top_end[phase - 1];
   const uint32_t k0 = P.top_begin[phase - 1];
@@ -4717,8 +4745,9 @@ GI_HD __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
         const uint32_t kk = k + (threadIdx.x & 63u);
         bool need = false;
         if (kk < kend) {
-          const DRule Rl = P.rules[GI_CONST(uint32_t, P.top)[kk]];
-          need = !rule_noop(t, Rl);
+          const uint32_t rl = GI_CONST(uint32_t, P.top)[kk];
+          const DRule Rl = P.rules[rl];
+          need = !rule_noop(t, Rl, rl);
         }
         const uint64_t m = __ballot(need);
         if (!m) {
@@ -4738,6 +4767,7 @@ GI_HD __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
         if (t.removed[j][0] <= id && id <= t.removed[j][1]) rm = true;
       if (rm) continue;
     }
+    if (t.rm_groups && (P.rule_groups[ri] & t.rm_groups)) continue;  // ctl:ruleRemoveByTag / ByMsg
     if (t.skip_after >= 0) {
       if (R.marker == t.skip_after) t.skip_after = -1;
       continue;
@@ -4769,6 +4799,10 @@ GI_HD __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
       continue;  // phase A proved the first link matches nothing
     if ((R.flags & RF_CONST) && R._pad2 == 0) continue;  // folded: matches nothing for any request
     eval_top<W>(t, ri);
+    if (t.allow) {  // the allow rule ends this phase's walk (allow:phase: only this one)
+      if (t.allow == D_ALLOW_PHASE) t.allow = 0;
+      break;
+    }
     // a skipAfter the rule just set: the rules up to its marker are all
     // skipped (no side effects), so resume at the marker entry directly
     if (t.skip_after >= 0) k = GI_CONST(uint32_t, P.top_jump)[k] - 1;
@@ -4992,15 +5026,18 @@ GI_HD __forceinline__ uint64_t wave_sum(uint64_t x) {
 }
 
 // Visits the items of one request: singles some filter reads, then the
-// (value, key) sides of every field kind some filter reads.
+// (value, key) sides of every field kind some filter reads.  body_only (the
+// gate's body stage): the body fields alone -- the phase-1 stage scanned the rest.
 template <class F>
-GI_HD __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H, const Field* Fd, F&& f) {
-  for (uint32_t m = P.item_singles; m; m &= m - 1) {
-    const uint32_t sg = __ffs(m) - 1;
-    f((uint8_t)0, (uint8_t)sg, 0u, (uint32_t)0xFFFFFFFFu, H->single[sg].n);
-  }
+GI_HD __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H, const Field* Fd, F&& f,
+                                         bool body_only = false) {
+  if (!body_only)
+    for (uint32_t m = P.item_singles; m; m &= m - 1) {
+      const uint32_t sg = __ffs(m) - 1;
+      f((uint8_t)0, (uint8_t)sg, 0u, (uint32_t)0xFFFFFFFFu, H->single[sg].n);
+    }
   const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck, n_pre = n_get + n_hdr + n_ck;
-  for (uint32_t i = 0; i < n_pre + H->n_post; i++) {
+  for (uint32_t i = body_only ? n_pre : 0u; i < n_pre + H->n_post; i++) {
     const Field fl = Fd[i];
     // the body range may hold multipart collections: FILES / FILES_NAMES /
     // FILES_SIZES are phase-A items, part headers are not
@@ -5034,6 +5071,7 @@ GI_HD void collect_request(const DProgram& P, const DBatch& B, uint32_t r) {
   t.single[S_REQUEST_METHOD] = method;
   t.single[S_REQUEST_PROTOCOL] = proto;
   t.single[S_REMOTE_ADDR] = {D + rq.remote_addr.off, rq.remote_addr.len};
+  t.single[S_SERVER_NAME] = {D + rq.server_name.off, rq.server_name.len};
   {  // REMOTE_PORT: strconv.Itoa(port)
     uint8_t* pb = tx_alloc(t, 12);
     if (pb) {
@@ -5057,6 +5095,11 @@ GI_HD void collect_request(const DProgram& P, const DBatch& B, uint32_t r) {
   }
   const bool ok = process_uri(t, uri.p, uri.n);
   const uint32_t n_get = t.nf;
+  // SecArgumentsLimit [upstream transaction.go AddGetRequestArgument / checkArgumentLimit]:
+  // an argument is dropped once ARGS_GET holds `limit` distinct keys -- which ones
+  // depends on Go's map order (urlutil.ParseQuery), so a request that can reach
+  // the limit (more than `limit` arguments) is flagged instead of guessed
+  if (n_get > P.args_limit) t.flags |= GI_REQ_UNSUPPORTED_URI;
   if (ok) {
     for (uint32_t h = 0; h < rq.hdr_count; h++) {
       const gi_header hd = B.headers[rq.hdr_begin + h];
@@ -5169,6 +5212,7 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
     const uint32_t r = B.body_list[bi];
     GI_BOUND(r < B.n_req, r, bi);
+    if (B.stage == 2 && !B.pend[r]) continue;  // decided in phase 1 (wave-uniform)
     Region g = region_of(P, B, r);
     ReqHdr* H = g.hdr;
     const uint8_t sp = H->spec_proc;
@@ -5308,6 +5352,7 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
     const uint32_t r = B.body_list[bi];
     GI_BOUND(r < B.n_req, r, bi);
+    if (B.stage == 2 && !B.pend[r]) continue;  // decided in phase 1 (wave-uniform)
     Region g = region_of(P, B, r);
     ReqHdr* H = g.hdr;
     if (H->spec_proc != BP_MULTIPART || (H->flags & GI_REQ_ERROR_MASK)) continue;  // wave-uniform
@@ -5553,7 +5598,7 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
   if (threadIdx.x < GI_NB) ibytes[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < B.n_req) {
+  if (r < B.n_req && (B.stage != 2 || B.pend[r])) {
     const ReqLayout L = B.layout[r];
     const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
     if (!(H->flags & GI_REQ_ERROR_MASK)) {
@@ -5580,7 +5625,7 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
         if (kind && fi > GI_MAX_ITEM_FIELD) void_request(B, r, GI_VOID_FIELD);  // no value-map index: no phase-A bit trusted
         ((Item*)B.items)[at] = it;
         atomicAdd(&ibytes[b], (unsigned long long)n);
-      });
+      }, B.stage == 2);
     }
   }
   __syncthreads();
@@ -6647,6 +6692,7 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
     const uint32_t r = B.body_list[bi];
     GI_BOUND(r < B.n_req, r, bi);
+    if (B.stage == 2 && !B.pend[r]) continue;  // decided in phase 1
     const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
     if (H->spec_proc == BP_NONE || (H->flags & GI_REQ_ERROR_MASK)) continue;
     const Region g = region_of(P, B, r);
@@ -6937,6 +6983,9 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
   t.ntx = 0;
   t.nremoved = 0;
   t.nrtgt = 0;
+  t.rm_groups = 0;
+  t.cur_groups = 0;
+  t.allow = 0;
   t.kx = nullptr;
   t.engine = P.rule_engine;
   t.body_access = P.body_access;
@@ -6999,10 +7048,25 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
   }
   t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
   const uint64_t c_init = B.prof ? gi_clock() : 0;
+  // the gate's phase-1 stage: a request with a body stops after phase 1
+  // unless phase 1 decided it; the only request state phase 1 writes outside
+  // this thread's registers and its re-initialised scratch is REQBODY_PROCESSOR
+  // (ctl:requestBodyProcessor), restored for the body stage's re-run
+  const bool gate1 = B.stage == 1 && rq.body.len > 0;
+  const Str rbp0 = t.single[S_REQBODY_PROCESSOR];
   // phase 1, ProcessRequestBody, phase 2 (one eval_phase call site)
   for (uint8_t ph = 1; ph <= 2 && !(t.flags & GI_REQ_ERROR_MASK); ph++) {
     if (ph == 2) {
       if (t.interrupted || t.engine == ENGINE_OFF) break;
+      if (gate1) {
+        if (lead) {
+          t.single[S_REQBODY_PROCESSOR] = rbp0;
+          B.pend[r] = 1;
+          B.plist[gi_fetch_add(B.pcount, 1u)] = r;
+        }
+        for (int c = 0; c < 7; c++) my[c] = 0;
+        return;
+      }
       uint32_t bn = rq.body.len;
       bool run2 = true;
       if (t.body_access && bn > 0) {
@@ -7156,7 +7220,10 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
     }
     v.tx_export[e] = x;
   }
-  if (lead) B.verdicts[r] = v;
+  if (lead) {
+    B.verdicts[r] = v;
+    if (B.stage == 1) B.pend[r] = 0;
+  }
   my[0] = 1;
   my[1] = t.interrupted ? 1 : 0;
   my[2] = t.nmatched ? 1 : 0;
@@ -7186,13 +7253,18 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
   if (threadIdx.x < 7) red[threadIdx.x] = 0;
   const uint32_t nw = (B.n_hit_slots + 31) / 32;
   const bool in_lds = nw <= GI_EVAL_LDS_WORDS && blockDim.x <= 128;
-  if (in_lds && r < B.n_req)
-    for (uint32_t w = 0; w < nw; w++) lhits[w * blockDim.x + threadIdx.x] = B.hits[(uint64_t)w * B.rstride + r];
+  {
+    const uint32_t rl = B.stage == 2 ? (r < *B.pcount ? B.plist[r] : 0xFFFFFFFFu) : r;
+    if (in_lds && rl < B.n_req)
+      for (uint32_t w = 0; w < nw; w++) lhits[w * blockDim.x + threadIdx.x] = B.hits[(uint64_t)w * B.rstride + rl];
+  }
   __syncthreads();
   unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
-  if (r < B.n_req) {
-    if (eval_heavy(P, B, r)) B.wlist[atomicAdd(B.wcount, 1u)] = r;
-    else eval_request<false>(P, B, r, in_lds ? lhits + threadIdx.x : nullptr, blockDim.x, my);
+  // the gate's body stage: the pending requests of the phase-1 stage, in its list
+  const uint32_t rr = B.stage == 2 ? (r < *B.pcount ? B.plist[r] : 0xFFFFFFFFu) : r;
+  if (rr < B.n_req) {
+    if (eval_heavy(P, B, rr)) B.wlist[atomicAdd(B.wcount, 1u)] = rr;
+    else eval_request<false>(P, B, rr, in_lds ? lhits + threadIdx.x : nullptr, blockDim.x, my);
   }
   for (int c = 0; c < 7; c++) {
     unsigned long long x = my[c];
@@ -7369,62 +7441,98 @@ void cpu_inspect_one(const DProgram& P, const DBatch& B) {
   eval_request<false>(P, B, 0, nullptr, 0, my);
 }
 
-void launch_pipeline(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
-                     int stop_after, LaunchLog* log, const uint32_t* tally_ids, uint32_t n_tally_ids) {
-  if (!B.n_req) return;
-  int nk = 0;  // (the caller resets *log and records its ev[0] before the first chunk)
+// Phase A over the items of the current stage: item records, the streams'
+// transformation chains, libinjection, long values and the automaton scans.
+static void launch_phase_a(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream,
+                           hipEvent_t* ev, int stop_after, LaunchLog* log, int& nk) {
   const uint32_t cb = (B.n_req + 255) / 256;
-  GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
-  if (B.n_body && P.body_access) {
-    GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), B.bparse_lds, stream, P, B);
-    if (B.n_mp_body) GI_LAUNCH("k_mpparse", k_mpparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
-  }
-  if (ev) (void)hipEventRecord(ev[0], stream);
-  if (P.n_streams) {
-    GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(GI_NCLS), dim3(256), 0, stream, B, cb);
-    GI_LAUNCH("k_ibases", k_ibases, dim3(1), dim3(256), 0, stream, B);
-    GI_LAUNCH("k_items", k_items, dim3(cb), dim3(256), 0, stream, P, B);
-    // chain memo slots per lane: as many as keep 8 one-wave workgroups per CU within the LDS
-    GI_LAUNCH("k_stream0", (k_stream<16, 20, 4>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 0u);
-    GI_LAUNCH("k_stream1", (k_stream<32, 36, 3>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 1u);
-    GI_LAUNCH("k_stream2", (k_stream<64, 68, 1>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 2u);
-    GI_LAUNCH("k_stream3", (k_stream<128, 132, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
-    GI_LAUNCH("k_stream4", (k_stream<0, 0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
-    if (P.n_det_streams) GI_LAUNCH("k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
-    if (B.long_cap) GI_LAUNCH("k_long", k_long, dim3(B.long_grid), dim3(64), 0, stream, P, B);
-    if (ev) (void)hipEventRecord(ev[1], stream);
-    for (int big = 0; big < 2; big++)
-      if (S.n_jobs[big])
-      {
-        if (big)
-          GI_LAUNCH("k_scan_big", (k_scan<true, true>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
-                    S.jobs[big], S.n_jobs[big], S.mode, 1u);
-        else
-          GI_LAUNCH("k_scan", (k_scan<true, false>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
-                    S.jobs[big], S.n_jobs[big], S.mode, 0u);
-      }
-    if (S.n_global)
-      GI_LAUNCH("k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
-                S.n_global, S.mode, 2u);
-    GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
-  } else if (ev) {
-    (void)hipEventRecord(ev[1], stream);
-  }
-  // REQUEST_BODY links (a ruleset may have them without any phase-A stream):
-  // one wave (workgroup) per body
-  if (P.n_body_links && B.n_body)
-    GI_LAUNCH("k_body", k_body, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
-  if (ev) (void)hipEventRecord(ev[2], stream);
+  GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(GI_NCLS), dim3(256), 0, stream, B, cb);
+  GI_LAUNCH("k_ibases", k_ibases, dim3(1), dim3(256), 0, stream, B);
+  GI_LAUNCH("k_items", k_items, dim3(cb), dim3(256), 0, stream, P, B);
+  // chain memo slots per lane: as many as keep 8 one-wave workgroups per CU within the LDS
+  GI_LAUNCH("k_stream0", (k_stream<16, 20, 4>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 0u);
+  GI_LAUNCH("k_stream1", (k_stream<32, 36, 3>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 1u);
+  GI_LAUNCH("k_stream2", (k_stream<64, 68, 1>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 2u);
+  GI_LAUNCH("k_stream3", (k_stream<128, 132, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
+  GI_LAUNCH("k_stream4", (k_stream<0, 0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
+  if (P.n_det_streams) GI_LAUNCH("k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
+  if (B.long_cap) GI_LAUNCH("k_long", k_long, dim3(B.long_grid), dim3(64), 0, stream, P, B);
+  if (ev) (void)hipEventRecord(ev[1], stream);
+  for (int big = 0; big < 2; big++)
+    if (S.n_jobs[big]) {
+      if (big)
+        GI_LAUNCH("k_scan_big", (k_scan<true, true>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
+                  S.jobs[big], S.n_jobs[big], S.mode, 1u);
+      else
+        GI_LAUNCH("k_scan", (k_scan<true, false>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
+                  S.jobs[big], S.n_jobs[big], S.mode, 0u);
+    }
+  if (S.n_global)
+    GI_LAUNCH("k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
+              S.n_global, S.mode, 2u);
+  GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
+}
+
+static void launch_eval(const DProgram& P, const DBatch& B, hipStream_t stream, int stop_after, LaunchLog* log,
+                        int& nk) {
   {  // small batches (fewer than 4 workgroups of 128 per CU): one wave per workgroup to spread over all CUs
     // GI_EVAL_BS A/B (C2, 1M): 128 threads 26.2 ms, 64 threads 32.1 ms
     static const uint32_t ev_env = getenv("GI_EVAL_BS") ? (uint32_t)atoi(getenv("GI_EVAL_BS")) : 0u;
     const uint32_t ev_bs = (ev_env == 64 || ev_env == 128) ? ev_env : (B.n_req + 127) / 128 < 1024 ? 64u : 128u;
-    GI_LAUNCH("k_eval", k_eval, dim3((B.n_req + ev_bs - 1) / ev_bs), dim3(ev_bs), 0, stream, P, B);
+    GI_LAUNCH(B.stage == 2 ? "k_eval2" : "k_eval", k_eval, dim3((B.n_req + ev_bs - 1) / ev_bs), dim3(ev_bs), 0, stream, P,
+              B);
   }
   if (B.wlist) {  // heavy requests, one wave each (persistent over k_eval's list)
     const uint32_t nw = (B.n_hit_slots + 31) / 32;
     const uint32_t lds = nw <= GI_EVAL_WAVE_LDS_WORDS ? 4 * std::max<uint32_t>(nw, 1u) : 0u;
-    GI_LAUNCH("k_eval_wave", k_eval_wave, dim3(std::min<uint32_t>(B.n_req, 8192)), dim3(64), lds, stream, P, B);
+    GI_LAUNCH(B.stage == 2 ? "k_eval_wave2" : "k_eval_wave", k_eval_wave, dim3(std::min<uint32_t>(B.n_req, 8192)),
+              dim3(64), lds, stream, P, B);
+  }
+}
+
+void launch_pipeline(const DProgram& P, const DBatch& B0, const ScanLaunch& S, hipStream_t stream, hipEvent_t* ev,
+                     int stop_after, LaunchLog* log, const uint32_t* tally_ids, uint32_t n_tally_ids) {
+  if (!B0.n_req) return;
+  int nk = 0;  // (the caller resets *log and records its ev[0] before the first chunk)
+  const uint32_t cb = (B0.n_req + 255) / 256;
+  // The phase-1 gate: when the batch has bodies to parse, phase 1 runs first and
+  // the body work (parsers, body phase A, k_body, phase 2) only for the requests
+  // phase 1 did not decide (ProcessRequestHeaders' interruption
+  // ends the transaction before WriteRequestBody).
+  const bool gated = B0.gate && B0.n_body && P.body_access && B0.pend && B0.plist && B0.pcount;
+  DBatch B = B0;
+  B.stage = gated ? 1u : 0u;
+  if (gated) (void)hipMemsetAsync(B.pcount, 0, 4, stream);
+  GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
+  if (!gated && B.n_body && P.body_access) {
+    GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), B.bparse_lds, stream, P, B);
+    if (B.n_mp_body) GI_LAUNCH("k_mpparse", k_mpparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
+  }
+  if (ev) (void)hipEventRecord(ev[0], stream);
+  if (P.n_streams) launch_phase_a(P, B, S, stream, ev, stop_after, log, nk);
+  else if (ev) (void)hipEventRecord(ev[1], stream);
+  if (stop_after && nk >= stop_after) return;
+  // REQUEST_BODY links (a ruleset may have them without any phase-A stream):
+  // one wave (workgroup) per body
+  if (!gated && P.n_body_links && B.n_body)
+    GI_LAUNCH("k_body", k_body, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
+  if (ev) (void)hipEventRecord(ev[2], stream);
+  launch_eval(P, B, stream, stop_after, log, nk);
+  if (gated) {
+    // the body stage: phase-A counters restart (the hit words, value
+    // signatures and hit sets keep the phase-1 stage's bits), the item counts
+    // are the body parsers' own
+    DBatch B2 = B0;
+    B2.stage = 2;
+    (void)hipMemsetAsync((void*)B2.pool_used, 0, 128, stream);  // ctr[0, 128): pool, slow, detect, long, wave list, buckets
+    if (P.n_streams) (void)hipMemsetAsync(B2.bcounts, 0, 4ull * cb * GI_NCLS, stream);
+    GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B2.n_body, 1u << 20)), dim3(64), B2.bparse_lds, stream, P, B2);
+    if (B2.n_mp_body)
+      GI_LAUNCH("k_mpparse", k_mpparse, dim3(std::min<uint32_t>(B2.n_body, 1u << 20)), dim3(64), 0, stream, P, B2);
+    if (P.n_streams) launch_phase_a(P, B2, S, stream, nullptr, stop_after, log, nk);
+    if (P.n_body_links)
+      GI_LAUNCH("k_body", k_body, dim3(std::min<uint32_t>(B2.n_body, 1u << 20)), dim3(64), 0, stream, P, B2);
+    launch_eval(P, B2, stream, stop_after, log, nk);
   }
   {
     const uint32_t lds = n_tally_ids <= GI_RHIST_LDS ? 4 * (2 * n_tally_ids + GI_SCORE_BINS) : 0;

@@ -83,8 +83,11 @@ bool build_regex_dfa(const Regex& re, Dfa* out, std::string* err, uint32_t state
 
 // Union (multi-pattern) search DFA over up to 64 patterns: the scan reports,
 // for every pattern, whether it matches somewhere in the input.
+// byte_budget (0: none): the union is abandoned as soon as its states could no
+// longer fit that many table bytes (2 B per transition + 8 B of accept masks
+// per state) -- a failing trial stops early instead of running to state_cap.
 bool build_union_dfa(const std::vector<const Regex*>& pats, Dfa* out, std::string* err,
-                     uint32_t state_cap = 8192);
+                     uint32_t state_cap = 8192, uint32_t byte_budget = 0);
 
 // @pm phrase set / @contains literal as a regex AST (search semantics).
 // fold_ascii: ASCII-only case folding (aho-corasick AsciiCaseInsensitive).

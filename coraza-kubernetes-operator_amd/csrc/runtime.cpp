@@ -93,6 +93,7 @@ struct gi_ctx {
   std::vector<uint32_t> tally_ids;
   // phase A
   DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf, wlist;
+  DevBuf pend, plist;  // phase-1 gate (launch_pipeline): pending flags + list
   uint32_t long_cap = 0, long_grid = GI_LONG_GRID;
   uint32_t wave_fields = GI_EVAL_WAVE_FIELDS, wave_rules = GI_EVAL_WAVE_RULES;  // k_eval_wave thresholds
   // A staged batch runs as consecutive request chunks, each a full pipeline
@@ -399,7 +400,10 @@ static const char* fill_dprogram(const Program& P, DProgram& np, Put&& put, std:
   UP(tx_snap, snap, uint8_t)
   UP(fold_ids, P.fold_ids, uint32_t)
   UP(fold_runs, P.fold_runs, uint32_t)
+  UP(rule_groups, P.rule_groups, uint32_t)
 #undef UP
+  np.n_rm_groups = P.n_rm_groups;
+  np.args_limit = P.args_limit;
   np.n_lower_pairs = GI_N_LOWER_PAIRS;
   // observable captures: per-request submatch workspace (kernels.hip CapHdr +
   // pike_match) and the TX slots of the keys "0".."8"
@@ -629,7 +633,7 @@ void gi_ctx_free(gi_ctx* c) {
   c->prof.release();
   for (DevBuf* b : {&c->caprec, &c->capbytes, &c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->hset, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
-                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist,
+                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist, &c->pend, &c->plist,
                     &c->cappool, &c->progdev})
     b->release();
   for (auto& ev : c->evs)
@@ -680,12 +684,12 @@ static const char* request_layout(const Program& PG, uint32_t cap_ws_words, uint
   const uint32_t n_single_items = (uint32_t)__builtin_popcount(PG.item_singles);
   z.mp = false;
   const gi_request& q = in->reqs[r];
-  const gi_span* sp[5] = {&q.method, &q.uri, &q.proto, &q.body, &q.remote_addr};
+  const gi_span* sp[6] = {&q.method, &q.uri, &q.proto, &q.body, &q.remote_addr, &q.server_name};
   for (auto* s : sp)
     if (s->off + s->len > in->data_len) return "request span out of range";
   if ((uint64_t)q.hdr_begin + q.hdr_count > in->n_headers) return "header range out of range";
   uint64_t maxv = std::max<uint64_t>({(uint64_t)q.uri.len * 3 + 2, (uint64_t)q.method.len + q.uri.len + q.proto.len + 2,
-                                      (uint64_t)q.body.len, 64});
+                                      (uint64_t)q.body.len, (uint64_t)q.server_name.len, 64});
   uint64_t cookie = 0, ncookie = 0, hdr_bytes = 0, hname_bytes = 0;
   bool multipart = false, hname_high = false;
   for (uint32_t h = 0; h < q.hdr_count; h++) {
@@ -837,10 +841,9 @@ static const char* request_layout(const Program& PG, uint32_t cap_ws_words, uint
     // TX values: a string a slot holds lives in the TX string arena (cap_mt
     // bytes in all), the string pool (one literal per slot), the dynamic area
     // (dyn_capb) or is a formatted integer -- so their sum, not n_slots x the
-    // largest, bounds one rule's MATCHED_VARS copies of them.  (A capture
-    // group's value is not counted: a rule whose TX target copies long
-    // captures may flag GI_REQ_OVERFLOW.)
-    const uint64_t tx_vals = cap_mt + (uint64_t)PG.n_slots * (PG.max_tx_lit + 24);
+    // largest, bounds one rule's MATCHED_VARS copies of them; a capture group
+    // (TX.0 .. TX.<cap_groups - 1>) holds at most cap_t bytes of its value buffer
+    const uint64_t tx_vals = cap_mt + (uint64_t)PG.n_slots * (PG.max_tx_lit + 24) + (uint64_t)cap_groups * cap_t;
     const uint64_t ab = cap_b + cap_mt + L.dyn_capb + 40ull * (PG.n_slots + L.dyn_cap) + tx_vals;
     if (e > 0xFFFFFFFFull || ab > 0xFFFFFFFFull) return "request too large (matched variables)";
     L.mv_cap_e = (uint32_t)e;
@@ -1087,6 +1090,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   // k_eval -> k_eval_wave request list (its counter lives in ctr)
   if ((e = c->ctr.ensure(4096 + 8ull * ((4 * GI_NCLS + 63) & ~63))) != hipSuccess) return hip_fail(c, e, "alloc counters");
   if ((e = c->wlist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc wave list");
+  if ((e = c->pend.ensure(std::max<uint64_t>(n, 16))) != hipSuccess) return hip_fail(c, e, "alloc gate flags");
+  if ((e = c->plist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc gate list");
   const auto t_h2d0 = std::chrono::steady_clock::now();
   if (in->data_len) e = hipMemcpyAsync(c->data.p, in->data, in->data_len, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && n) e = hipMemcpyAsync(c->reqs.p, in->reqs, n * sizeof(gi_request), hipMemcpyHostToDevice, s);
@@ -1207,6 +1212,13 @@ int gi_run_staged(gi_ctx* c) {
     B.wave_fields = c->wave_fields;
     B.wave_rules = c->wave_rules;
     B.rstride = c->n_req;
+    // the phase-1 gate (GI_GATE=0: one pass, bodies parsed before phase 1)
+    static const bool gate_env = !(getenv("GI_GATE") && atoi(getenv("GI_GATE")) == 0);
+    B.stage = 0;
+    B.gate = gate_env ? 1u : 0u;
+    B.pend = (uint8_t*)c->pend.p;
+    B.plist = (uint32_t*)c->plist.p;
+    B.pcount = (uint32_t*)(cp + 512);
     B.bparse_lds = (uint32_t)std::min<uint64_t>(c->bparse_lds, (c->max_body + 15) & ~15ull);
   }
   (void)hipEventRecord(c->ev0, c->stream);
@@ -1248,6 +1260,7 @@ int gi_run_staged(gi_ctx* c) {
     Bc.hits = B.hits + ch.r0;
     Bc.txslots = (Slot*)((uint8_t*)B.txslots + (uint64_t)GI_SLOT_BYTES * ch.r0);
     Bc.body_list = B.body_list + ch.blist_off;
+    Bc.pend = B.pend ? B.pend + ch.r0 : nullptr;
     Bc.n_body = ch.n_body;
     Bc.n_mp_body = ch.n_mp;
     launch_pipeline(c->prog, Bc, c->scan, c->stream, c->evs, c->stop_after, &c->log,
@@ -1496,6 +1509,7 @@ int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results
                                                         std::max(1u, n)));
     std::atomic<uint32_t> next(0);
     std::atomic<int> bad(GI_OK);
+    const bool layout_debug = getenv("GI_LAYOUT_DEBUG") != nullptr;  // read once, before the threads
     auto work = [&]() {
       std::vector<uint64_t> scratch, capture;
       std::vector<uint64_t> txs(2ull * std::max<uint32_t>(PG.n_slots, 1));
@@ -1506,16 +1520,23 @@ int gi_cpu_baseline_inspect(const gi_ruleset* rs, const gi_batch* in, gi_results
           ReqLayout L{};
           LayoutSizes z{};
           LayoutAcc acc;
-          if (request_layout(PG, np.cap_ws_words, np.cap_groups, in, r, L, z, acc)) {
-            bad.store(GI_EINVAL);
-            return;
+          if (const char* lerr = request_layout(PG, np.cap_ws_words, np.cap_groups, in, r, L, z, acc)) {
+            if (strncmp(lerr, "request too large", 17) != 0) {  // malformed input: the call fails
+              bad.store(GI_EINVAL);
+              return;
+            }
+            // a request beyond the per-request capacities: flagged, like the GPU path does
+            gi_verdict& v = out->verdicts[r];
+            memset(&v, 0, sizeof(v));
+            v.flags = GI_REQ_OVERFLOW;
+            continue;
           }
           L.base = 0;
           L.vmap_bit = 0;
           L.hset_word = 0;
           L.hset_mask = 0;  // no phase A: no hit set
           L.cap_off = 0;
-          if (getenv("GI_LAYOUT_DEBUG") && z.region > (1u << 20))  // diagnostics: what sizes a large region
+          if (layout_debug && z.region > (1u << 20))  // diagnostics: what sizes a large region
             fprintf(stderr, "GI_LAYOUT r=%u region=%llu cap_f=%u cap_b=%u cap_t=%u cap_mt=%u dyn=%u/%u mv=%u/%u capb=%llu\n", r,
                     (unsigned long long)z.region, L.cap_f, L.cap_b, L.cap_t, L.cap_mt, L.dyn_cap, L.dyn_capb, L.mv_cap_e,
                     L.mv_cap_a, (unsigned long long)z.capb);

@@ -55,13 +55,13 @@ MAX_EXPORTS = 8
 SPAN_DT = np.dtype([("off", "<u8"), ("len", "<u4"), ("_pad", "<u4")])
 REQUEST_DT = np.dtype([("method", SPAN_DT), ("uri", SPAN_DT), ("proto", SPAN_DT), ("body", SPAN_DT),
                        ("hdr_begin", "<u4"), ("hdr_count", "<u4"), ("remote_addr", SPAN_DT),
-                       ("remote_port", "<u4"), ("_pad", "<u4")])
+                       ("remote_port", "<u4"), ("_pad", "<u4"), ("server_name", SPAN_DT)])
 HEADER_DT = np.dtype([("name", SPAN_DT), ("value", SPAN_DT)])
 VERDICT_DT = np.dtype([("rule_id", "<i4"), ("status", "<i4"), ("action", "u1"), ("phase", "u1"),
                        ("flags", "<u2"), ("match_cnt", "<u4"), ("tx_export", "<i8", (MAX_EXPORTS,)),
                        ("capture_cnt", "<u4"), ("_pad", "<u4")])
 CAPTURE_DT = np.dtype([("rule_id", "<i4"), ("group", "<u4"), ("off", "<u4"), ("len", "<u4")])
-assert REQUEST_DT.itemsize == 96 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 88
+assert REQUEST_DT.itemsize == 112 and HEADER_DT.itemsize == 32 and VERDICT_DT.itemsize == 88
 
 EXPORTED_SYMBOLS = (
     "gi_abi_version", "gi_cpu_baseline_inspect", "gi_compile", "gi_ruleset_free", "gi_ruleset_info_get", "gi_ruleset_export_name", "gi_ruleset_describe",
@@ -132,7 +132,7 @@ class _Stats(ctypes.Structure):
 _LIB = None
 
 
-ABI_VERSION = 5  # include/gpuinspect.h GI_ABI_VERSION: the ctypes structs below mirror that layout
+ABI_VERSION = 6  # include/gpuinspect.h GI_ABI_VERSION: the ctypes structs below mirror that layout
 
 
 def load_library(path: str = LIB_PATH):
@@ -321,11 +321,17 @@ class Transaction:
     body: bytes = b""
     remote_addr: bytes = b""
     remote_port: int = 0
+    server_name: bytes = b""
 
     def process_connection(self, client, cport, server=b"", sport=0):
         """ProcessConnection: REMOTE_ADDR / REMOTE_PORT (the server side is not
         a variable this engine evaluates)."""
         self.remote_addr, self.remote_port = _b(client), int(cport)
+
+    def set_server_name(self, name):
+        """SetServerName: SERVER_NAME (coraza-proxy-wasm passes :authority
+        without its port)."""
+        self.server_name = _b(name)
 
     def process_uri(self, uri, method, proto):
         self.uri, self.method, self.proto = _b(uri), _b(method), _b(proto)
@@ -378,6 +384,10 @@ class PackedBatch:
         headers = self.headers[h0:h1].copy()
         starts = [reqs[n]["off"] for n in ("method", "uri", "proto", "body", "remote_addr")]
         ends = [reqs[n]["off"] + reqs[n]["len"] for n in ("method", "uri", "proto", "body", "remote_addr")]
+        sn = reqs["server_name"]["len"] > 0
+        if sn.any():
+            starts.append(reqs["server_name"]["off"][sn])
+            ends.append(reqs["server_name"]["off"][sn] + reqs["server_name"]["len"][sn])
         if len(headers):
             starts += [headers["name"]["off"], headers["value"]["off"]]
             ends += [headers["name"]["off"] + headers["name"]["len"], headers["value"]["off"] + headers["value"]["len"]]
@@ -385,6 +395,7 @@ class PackedBatch:
         d1 = int(max(int(x.max()) for x in ends))
         for n in ("method", "uri", "proto", "body", "remote_addr"):
             reqs[n]["off"] -= d0
+        reqs["server_name"]["off"] = np.where(sn, reqs["server_name"]["off"] - d0, 0)
         if len(headers):
             headers["name"]["off"] -= d0
             headers["value"]["off"] -= d0
@@ -405,7 +416,7 @@ class PackedBatch:
         hs = [(sp(h["name"]), sp(h["value"])) for h in
               self.headers[int(q["hdr_begin"]):int(q["hdr_begin"]) + int(q["hdr_count"])]]
         return Transaction(sp(q["method"]), sp(q["uri"]), sp(q["proto"]), hs, sp(q["body"]),
-                           sp(q["remote_addr"]), int(q["remote_port"]))
+                           sp(q["remote_addr"]), int(q["remote_port"]), sp(q["server_name"]))
 
 
 def concat(batches: Sequence[PackedBatch]) -> PackedBatch:
@@ -417,6 +428,7 @@ def concat(batches: Sequence[PackedBatch]) -> PackedBatch:
         h = b.headers.copy()
         for n in ("method", "uri", "proto", "body", "remote_addr"):
             r[n]["off"] += doff
+        r["server_name"]["off"] = np.where(r["server_name"]["len"] > 0, r["server_name"]["off"] + doff, 0)
         h["name"]["off"] += doff
         h["value"]["off"] += doff
         r["hdr_begin"] += hoff
@@ -448,7 +460,17 @@ def pack(txs: Sequence) -> PackedBatch:
             parts.append(k)
             parts.append(v)
         nh[i] = len(t.headers)
-    return pack_parts(parts, nh, ports)
+    pb = pack_parts(parts, nh, ports)
+    names = [getattr(t, "server_name", b"") for t in txs]
+    if any(names):  # SERVER_NAME values after the request parts
+        base = sum(map(len, parts))
+        extra = np.frombuffer(b"".join(names), dtype=np.uint8)
+        pb.data = np.concatenate([pb.data[:base], extra])
+        lens = np.array([len(x) for x in names], np.int64)
+        offs = base + np.concatenate([[0], np.cumsum(lens)[:-1]])
+        pb.reqs["server_name"]["off"] = np.where(lens > 0, offs, 0)
+        pb.reqs["server_name"]["len"] = lens
+    return pb
 
 
 NFIXED = 5  # fixed parts per request in pack_parts: method, uri, proto, body, remote_addr

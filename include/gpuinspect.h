@@ -123,6 +123,8 @@ typedef struct {
   gi_span remote_addr;  /* ProcessConnection client address -> REMOTE_ADDR (may be empty) */
   uint32_t remote_port; /* -> REMOTE_PORT */
   uint32_t _pad;
+  gi_span server_name;  /* Transaction.SetServerName -> SERVER_NAME (may be empty; coraza-proxy-wasm
+                         * sets it from :authority without the port) */
 } gi_request;
 
 typedef struct {
@@ -220,7 +222,7 @@ typedef struct {
  * gi_tally, gi_stats, ...).  It changes whenever one of them changes layout;
  * a binding checks gi_abi_version() == GI_ABI_VERSION before passing any of
  * them (INTEGRATION.md lists the revisions). */
-#define GI_ABI_VERSION 5
+#define GI_ABI_VERSION 6
 uint32_t gi_abi_version(void);
 
 /* ------------------------------------------------------------ compile */

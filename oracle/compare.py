@@ -18,7 +18,8 @@ ACTION_CODES = {"": 0, "deny": 1, "drop": 2, "redirect": 3}
 def oracle_request(t):
     """gpuinspect.Transaction -> the oracle's Request (the same inputs)."""
     return coraza.Request(t.method, t.uri, t.proto, list(t.headers), t.body,
-                          getattr(t, "remote_addr", b""), int(getattr(t, "remote_port", 0)))
+                          getattr(t, "remote_addr", b""), int(getattr(t, "remote_port", 0)),
+                          getattr(t, "server_name", b""))
 
 
 def oracle_verdicts(cfg, batch, exports, idx=None):

@@ -47,6 +47,14 @@ class SecLangError(ValueError):
     """A directive that coraza.NewWAF would reject (ruleset_controller.go:160)."""
 
 
+class SecLangUnsupported(SecLangError):
+    """SecLang coraza.NewWAF accepts whose request-phase evaluation this
+    oracle (and the engine, GI_EUNSUPPORTED) does not model: a phase 1-2 rule
+    reading a response variable, or using an operator / transformation / ctl
+    of the response path.  The same constructs in phase 3-5 rules are fine:
+    the request path never evaluates those phases."""
+
+
 # ---------------------------------------------------------------------------
 # Variables (coraza internal/variables) -- name -> (kind, case_insensitive)
 # kind: 'single' | 'map' | 'names' | 'args' | 'argnames' | 'tx' | 'matched'
@@ -92,7 +100,29 @@ NAMES_VARS = {
     "REQUEST_COOKIES_NAMES": (("REQUEST_COOKIES",), False),
     "MATCHED_VARS_NAMES": (("MATCHED_VARS",), True),
 }
-ALL_VARS = SINGLE_VARS | set(MAP_VARS) | set(NAMES_VARS)
+# [upstream internal/variables/variables.go]: declared variables the request
+# path does not evaluate (the response phases', and a few without a value here)
+DEFERRED_VARS = {
+    "RESPONSE_BODY", "RESPONSE_STATUS", "RESPONSE_HEADERS", "RESPONSE_HEADERS_NAMES", "RESPONSE_PROTOCOL",
+    "RESPONSE_CONTENT_TYPE", "RESPONSE_CONTENT_LENGTH", "RESPONSE_ARGS", "RESPONSE_XML", "RES_BODY_PROCESSOR",
+    "OUTBOUND_DATA_ERROR", "STATUS_LINE", "SERVER_ADDR", "SERVER_PORT", "UNIQUE_ID", "REMOTE_HOST",
+    "HIGHEST_SEVERITY", "DURATION", "REQBODY_PROCESSOR_ERROR", "REQBODY_PROCESSOR_ERROR_MSG", "ARGS_PATH",
+    "FILES_TMP_CONTENT", "MULTIPART_FILENAME", "MULTIPART_NAME", "MULTIPART_DATA_AFTER", "GEO", "RULE", "JSON",
+    "ENV", "REQUEST_XML", "AUTH_TYPE", "TIME", "TIME_DAY", "TIME_EPOCH", "TIME_HOUR", "TIME_MIN", "TIME_MON",
+    "TIME_SEC", "TIME_WDAY", "TIME_YEAR",
+}
+ALL_VARS = SINGLE_VARS | set(MAP_VARS) | set(NAMES_VARS) | DEFERRED_VARS
+# operators / transformations coraza v3.3.3 has that are not modelled here
+DEFERRED_OPERATORS = {"geolookup", "inspectfile", "pmfromdataset", "ipmatchfromdataset", "rbl", "restpath",
+                      "strmatch", "validatenid", "validateschema", "verifycc", "verifycpf", "verifyssn",
+                      "fuzzyhash"}
+DEFERRED_TRANSFORMS = {"removecomments", "sqlhexdecode", "uppercase"}
+# [upstream internal/actions/ctl.go]: evaluated / without effect on a request-phase verdict
+CTL_EVALUATED = {"ruleremovebyid", "ruleremovetargetbyid", "ruleremovebytag", "ruleremovetargetbytag",
+                 "ruleremovebymsg", "ruleremovetargetbymsg", "ruleengine", "requestbodyprocessor",
+                 "requestbodyaccess", "forcerequestbodyvariable"}
+CTL_NO_EFFECT = {"auditengine", "auditlogparts", "debugloglevel", "responsebodyaccess", "responsebodylimit",
+                 "responsebodyprocessor", "forceresponsebodyvariable", "hashengine", "hashenforcement"}
 
 
 @dataclass
@@ -145,6 +175,8 @@ class Rule:
     parent_id: int = 0
     has_chain_action: bool = False
     tags: List[str] = field(default_factory=list)
+    msg: str = ""
+    deferred: str = ""   # a construct of the response path (SecLangUnsupported in phases 1-2)
 
 
 @dataclass
@@ -153,6 +185,7 @@ class WafConfig:
     request_body_access: bool = False
     request_body_limit: int = 134217728
     request_body_limit_action: str = "Reject"
+    args_limit: int = 1000        # SecArgumentsLimit (WAF.ArgumentLimit)
     rules: List[Rule] = field(default_factory=list)
     default_actions: Dict[int, str] = field(default_factory=dict)
 
@@ -173,7 +206,8 @@ IGNORED_DIRECTIVES = {
     "secuploadfilemode", "secunicodemap", "secpcrematchlimit",
     "secpcrematchlimitrecursion", "secstatusengine", "secconnengine",
     "secserversignature", "sechttpblkey", "secwebappid", "secsensorid",
-    "secargumentslimit", "secrequestbodyjsondepthlimit", "secmarker_",
+    "secrequestbodyjsondepthlimit", "secmarker_", "secresponsebodymimetypesclear", "seccookieformat",
+    "secuploadfilelimit", "secignorerulecompilationerrors",
 }
 
 ACTION_TYPES = {
@@ -196,6 +230,7 @@ ACTION_TYPES = {
     "expirevar": "nondisruptive", "initcol": "nondisruptive",
     "sanitisearg": "nondisruptive", "sanitisematched": "nondisruptive",
     "setenv": "nondisruptive", "append": "nondisruptive",
+    "sanitiserequestheader": "nondisruptive", "sanitiseresponseheader": "nondisruptive",
 }
 
 PHASE_NAMES = {"request": 2, "response": 4, "logging": 5}
@@ -308,6 +343,8 @@ def _parse_variables(s: str, rule: Rule):
         name = name.upper()
         if name not in ALL_VARS:
             raise SecLangError("unknown variable %r" % name)
+        if name in DEFERRED_VARS and not rule.deferred:
+            rule.deferred = "unsupported variable " + name
         key_rx = None
         if len(key) >= 2 and key[0] == "'" and key[-1] == "'":
             key = key[1:-1]
@@ -371,7 +408,7 @@ def pm_file_phrases(data: bytes):
     return out
 
 
-def _parse_operator(opstr: str, data_files=None) -> Operator:
+def _parse_operator(opstr: str, data_files=None, rule=None) -> Operator:
     # rule_parser.go ParseOperator: default operator is @rx
     if len(opstr) == 0 or (opstr[0] != "@" and (len(opstr) < 2 or opstr[1] != "@")):
         opstr = "@rx " + opstr
@@ -437,8 +474,11 @@ def _parse_operator(opstr: str, data_files=None) -> Operator:
                 lines.append(line.decode("latin-1"))
         op.name = "ipmatch"
         op.nets = ipmatch_networks(",".join(lines))
+    elif name_l in DEFERRED_OPERATORS:
+        if rule is not None and not rule.deferred:
+            rule.deferred = "unsupported operator @" + name
     else:
-        raise SecLangError("unsupported operator @%s" % name)
+        raise SecLangError("invalid operator @%s" % name)
     return op
 
 
@@ -460,9 +500,14 @@ def _apply_actions(rule: Rule, actions, is_child: bool):
             vl = v.lower()
             rule.phase = PHASE_NAMES[vl] if vl in PHASE_NAMES else int(v)
         elif k in ("deny", "drop", "pass", "block", "redirect", "allow"):
-            if k == "allow":
-                raise SecLangError("action allow is not supported")
             rule.disruptive = k
+            if k == "allow":
+                # [upstream internal/actions/allow.go Init]
+                a = v.lower()
+                if a in ("phase", "request"):
+                    rule.disruptive = "allow:" + a
+                elif a:
+                    raise SecLangError("invalid argument %s for allow" % v)
         elif k == "status":
             rule.status = int(v)
         elif k == "chain":
@@ -476,8 +521,12 @@ def _apply_actions(rule: Rule, actions, is_child: bool):
             if tl == "none":
                 rule.transforms = []
             else:
+                if tl in DEFERRED_TRANSFORMS:
+                    if not rule.deferred:
+                        rule.deferred = "unsupported transformation t:" + v
+                    continue
                 if tl not in TRANSFORMS_SUPPORTED:
-                    raise SecLangError("unsupported transformation t:%s" % v)
+                    raise SecLangError("invalid transformation t:%s" % v)
                 rule.transforms.append(tl)
         elif k == "capture":
             rule.capture = True
@@ -485,6 +534,8 @@ def _apply_actions(rule: Rule, actions, is_child: bool):
             rule.multimatch = True
         elif k == "tag":
             rule.tags.append(v)
+        elif k == "msg":
+            rule.msg = v
         elif k == "setvar":
             sv = _parse_setvar(v)
             rule.setvars.append(sv)
@@ -493,9 +544,14 @@ def _apply_actions(rule: Rule, actions, is_child: bool):
             name, _, val = v.partition("=")
             name = name.strip()
             cl = (name.lower(), val.strip())
-            if cl[0] not in ("ruleremovebyid", "ruleremovetargetbyid", "ruleengine", "requestbodyprocessor",
-                             "requestbodyaccess", "forcerequestbodyvariable"):
-                raise SecLangError("unsupported ctl %s" % name)
+            if cl[0] in CTL_NO_EFFECT:
+                continue
+            if cl[0] == "requestbodylimit":
+                if not rule.deferred:
+                    rule.deferred = "unsupported ctl requestbodylimit"
+                continue
+            if cl[0] not in CTL_EVALUATED:
+                raise SecLangError("unknown ctl %s" % name)
             rule.ctls.append(cl)
             rule.nondisruptive_order.append(("ctl", cl))
 
@@ -541,10 +597,42 @@ def merge_default_actions(actions, defaults):
     return res
 
 
+def _id_range(s: str):
+    """An id or "lo-hi" (directives.go / ctl.go rangeToInts) -> (lo, hi)."""
+    a, dash, b = s[1:].partition("-") if s[:1] == "-" else s.partition("-")
+    if s[:1] == "-":
+        a = "-" + a
+    lo, ok = go_atoi(a.encode())
+    if not ok:
+        raise SecLangError("invalid id %s" % s)
+    if not dash:
+        return lo, lo
+    hi, ok = go_atoi(b.encode())
+    if not ok:
+        raise SecLangError("invalid id %s" % s)
+    return lo, hi
+
+
 def parse_seclang(text: str, data_files=None) -> WafConfig:
     cfg = WafConfig()
     pending_parent: Optional[Rule] = None
     chain_tail: Optional[Rule] = None
+    ids = {}  # top-level rule id -> count (RuleGroup.Add rejects a repeated non-zero id)
+
+    def strip_q(x):
+        return x.strip().strip('"')
+
+    def remove(pred):
+        kept = []
+        for r in cfg.rules:
+            if pred(r):
+                if r.id:
+                    ids[r.id] -= 1
+                    if not ids[r.id]:
+                        del ids[r.id]
+            else:
+                kept.append(r)
+        cfg.rules = kept
     for lineno, line in _split_lines(text):
         if not line or line[0] == "#":
             continue
@@ -561,6 +649,57 @@ def parse_seclang(text: str, data_files=None) -> WafConfig:
             cfg.request_body_limit = int(opts.strip())
         elif d == "secrequestbodylimitaction":
             cfg.request_body_limit_action = opts.strip()
+        elif d == "secargumentslimit":
+            v, ok = go_atoi(opts.strip().encode())
+            if not ok:
+                raise SecLangError("syntax error: SecArgumentsLimit [POSITIVE_INT]")
+            cfg.args_limit = v
+        elif d in ("secruleremovebyid", "secruleremovebytag", "secruleremovebymsg"):
+            # [upstream internal/seclang/directives.go directiveSecRuleRemoveBy*]
+            if pending_parent is not None:
+                raise SecLangError("%s inside a chain" % directive)
+            if not opts.strip():
+                raise SecLangError("expected options for %s" % directive)
+            if d == "secruleremovebyid":
+                for part in opts.split():
+                    lo, hi = _id_range(part)
+                    remove(lambda r: lo <= r.id <= hi)
+            elif d == "secruleremovebytag":
+                tag = strip_q(opts)
+                remove(lambda r: tag in r.tags)
+            else:
+                msg = strip_q(opts)
+                remove(lambda r: not r.secmark and r.msg == msg)
+        elif d in ("secruleupdatetargetbyid", "secruleupdatetargetbytag", "secruleupdatetargetbymsg",
+                   "secruleupdateactionbyid"):
+            # [upstream directives.go directiveSecRuleUpdate{Target,Action}By*]
+            if pending_parent is not None:
+                raise SecLangError("%s inside a chain" % directive)
+            sel, sp, arg = opts.strip().partition(" ")
+            if not sp:
+                raise SecLangError("syntax error: %s" % directive)
+            sel, arg = strip_q(sel), strip_q(arg)
+            by_id = d in ("secruleupdatetargetbyid", "secruleupdateactionbyid")
+            lo, hi = _id_range(sel) if by_id else (0, -1)
+            hit = [r for r in cfg.rules if not r.secmark and (
+                (lo <= r.id <= hi) if by_id else (sel in r.tags if d.endswith("bytag") else r.msg == sel))]
+            if by_id and lo == hi and not hit:
+                raise SecLangError('%s: rule "%s" not found' % (directive, sel))
+            for r in hit:
+                if d == "secruleupdateactionbyid":
+                    acts = _parse_actions_list(arg)
+                    for k, _ in acts:
+                        if k in ("id", "chain"):
+                            raise SecLangError("SecRuleUpdateActionById: action %s cannot be updated" % k)
+                    if any(ACTION_TYPES[k] == "disruptive" for k, _ in acts):
+                        r.disruptive = ""  # [upstream] Rule.ClearDisruptiveActions
+                    _apply_actions(r, acts, False)
+                    c = r.chain
+                    while c is not None:
+                        c.phase = r.phase
+                        c = c.chain
+                else:
+                    _parse_variables(arg, r)
         elif d == "secdefaultaction":
             acts = _parse_actions_list(opts)
             phase = 2
@@ -585,7 +724,7 @@ def parse_seclang(text: str, data_files=None) -> WafConfig:
                 _parse_variables(vars_s, rule)
                 rest = rest.strip()
                 opstr, rest = _cut_quoted(rest)
-                rule.op = _parse_operator(opstr, data_files)
+                rule.op = _parse_operator(opstr, data_files, rule)
                 rest = rest.strip()
                 acts_s = rest.strip('"') if rest else ""
             else:
@@ -613,6 +752,9 @@ def parse_seclang(text: str, data_files=None) -> WafConfig:
             else:
                 if rule.id == 0:
                     raise SecLangError("rule id is required (line %d)" % lineno)
+                if rule.id in ids:
+                    raise SecLangError("there is a another rule with id %d" % rule.id)
+                ids[rule.id] = 1
                 cfg.rules.append(rule)
                 if rule.has_chain_action:
                     pending_parent = rule
@@ -623,6 +765,16 @@ def parse_seclang(text: str, data_files=None) -> WafConfig:
             raise SecLangError("unknown directive %r" % directive)
     if pending_parent is not None:
         raise SecLangError("unterminated chain")
+    # phases 3-5 are never evaluated by the request path: their response-side
+    # constructs are accepted there, and rejected in a phase 1-2 rule
+    for r in cfg.rules:
+        if r.phase not in (1, 2):
+            continue
+        c = r
+        while c is not None:
+            if c.deferred:
+                raise SecLangUnsupported("%s (rule %d, phase %d)" % (c.deferred, r.id, r.phase))
+            c = c.chain
     return cfg
 
 
@@ -1255,6 +1407,7 @@ class Request:
     body: bytes = b""
     remote_addr: bytes = b""   # ProcessConnection client -> REMOTE_ADDR
     remote_port: int = 0       # -> REMOTE_PORT (strconv.Itoa)
+    server_name: bytes = b""   # SetServerName -> SERVER_NAME
 
 
 class UnsupportedInput(ValueError):
@@ -1837,6 +1990,7 @@ class Transaction:
         self.tx: Dict[bytes, bytes] = {}       # lowercase key -> value
         self.skip_after = ""
         self.skip = 0
+        self.allow = ""  # allow action in effect: "allow" | "allow:phase" | "allow:request"
         self.removed: List[Tuple[int, int]] = []
         self.removed_targets: List[Tuple[int, int, str, str]] = []
         self.single: Dict[str, bytes] = {k: b"" for k in SINGLE_VARS}
@@ -1862,6 +2016,11 @@ class Transaction:
         self.single["REQUEST_LINE"] = req.method + b" " + req.uri + b" " + req.proto
         self.single["REMOTE_ADDR"] = req.remote_addr
         self.single["REMOTE_PORT"] = str(req.remote_port).encode()
+        self.single["SERVER_NAME"] = req.server_name
+        if len(args) > self.cfg.args_limit:
+            # SecArgumentsLimit [upstream transaction.go AddGetRequestArgument]:
+            # which arguments are dropped depends on Go's map order -- flagged
+            raise UnsupportedInput("more ARGS_GET than SecArgumentsLimit")
         self.maps["ARGS_GET"] = list(args)
         for k, val in req.headers:
             if k == b"":
@@ -2077,6 +2236,19 @@ class Transaction:
                     self.removed.append((int(a), int(b)))
                 else:
                     self.removed.append((int(part), int(part)))
+        elif name in ("ruleremovebytag", "ruleremovebymsg"):
+            # [upstream ctl.go]: tx.RemoveRuleByID for every rule whose tags
+            # contain the value (whose msg equals it)
+            for r in self.cfg.rules:
+                if r.id and (val in r.tags if name == "ruleremovebytag" else r.msg == val):
+                    self.removed.append((r.id, r.id))
+        elif name in ("ruleremovetargetbytag", "ruleremovetargetbymsg"):
+            sel, _, tgt = val.partition(";")
+            sel = sel.strip()
+            var, _, key = tgt.strip().partition(":")
+            for r in self.cfg.rules:
+                if r.id and (sel in r.tags if name == "ruleremovetargetbytag" else r.msg == sel):
+                    self.removed_targets.append((r.id, r.id, var.strip().upper(), key.lower()))
         elif name == "ruleremovetargetbyid":
             # [upstream internal/actions/ctl.go]: "ID[-ID];VARIABLE[:key]" ->
             # tx.RemoveRuleTargetByID: rule.go doEvaluate adds (key) to the
@@ -2180,6 +2352,8 @@ class Transaction:
                 self.skip = rule.skip
             if rule.disruptive in ("deny", "drop", "redirect") and self.rule_engine == "On":
                 self.interruption = (rule.id, rule.status, rule.disruptive, self.phase)
+            elif rule.disruptive.startswith("allow") and self.rule_engine == "On":
+                self.allow = rule.disruptive  # [upstream allow.go: tx.AllowType]
             if rule.id != 0:
                 self.matched.append(rule.id)
         return nmatch
@@ -2187,6 +2361,10 @@ class Transaction:
     def eval_phase(self, phase: int):
         """RuleGroup.Eval."""
         if self.rule_engine == "Off":
+            return
+        # [upstream] an earlier "allow" (every phase) or "allow:request" ends
+        # the remaining request phases
+        if self.allow in ("allow", "allow:request"):
             return
         self.phase = phase
         for r in self.cfg.rules:
@@ -2210,6 +2388,10 @@ class Transaction:
             self.maps["MATCHED_VARS"] = []
             self.cur_top = r.id
             self.do_evaluate(r)
+            if self.allow:  # the allow rule ends this phase ("allow:phase": only this one)
+                if self.allow == "allow:phase":
+                    self.allow = ""
+                break
 
     def process_request_body(self):
         if self.rule_engine == "Off":

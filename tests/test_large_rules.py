@@ -66,6 +66,37 @@ def test_gpu_c5_2k_rules_256k_multipart_parity():
     assert not any(int(v["flags"]) & 0x0F for v in res.verdicts)
 
 
+def _c5_oracle_worker(args):
+    text, files, blob, i, exports = args
+    cfg = coraza.parse_seclang(text, files)
+    b = gpuinspect.PackedBatch(*blob)
+    return i, coraza.inspect(cfg, compare.oracle_request(b.request(i)), exports)
+
+
+@pytest.mark.gpu
+def test_gpu_c5_full_shape_parity():
+    """BASELINE configs[4] at its configured shape: 10k generated @rx rules +
+    a 100k-phrase @pmFromFile list over ~1 MB multipart bodies, each request
+    against the oracle.  The oracle (~40 s per request) runs in one forked
+    process per request while the engine compiles and inspects."""
+    import multiprocessing as mp
+    text, files = traffic.c5_ruleset()
+    batch = traffic.c5_batch(2)
+    assert batch.raw_bytes() > 2_000_000
+    blob = (batch.data, batch.reqs, batch.headers)
+    exports = ["anomaly_score"]
+    with mp.get_context("fork").Pool(2) as pool:
+        pending = pool.map_async(_c5_oracle_worker, [(text, files, blob, i, exports) for i in range(2)])
+        rs = gpuinspect.Ruleset(text, tx_exports=exports, data_files=files)
+        assert rs.info["n_rules"] == 10003
+        res = gpuinspect.Engine(rs).inspect(batch)
+        verdicts = dict(pending.get(timeout=110))
+    bad = compare.compare(res, verdicts)
+    assert not bad, bad[:3]
+    assert all(len(v.matched) > 50 and v.rule_id == 99100 for v in verdicts.values())
+    assert not any(int(v["flags"]) & 0x0F for v in res.verdicts)
+
+
 @pytest.mark.gpu
 def test_gpu_scan_hbm_forced_parity():
     text = open(os.path.join(ROOT, "rulesets", "crs_pl1.conf")).read()
