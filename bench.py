@@ -376,6 +376,9 @@ def main():
         "gb_per_s_scanned": round(gbs, 3),
         "interrupted_frac": round(tally["n_interrupted"] / max(tally["n_req"], 1), 4),
         "pa_void_requests": int(tally["n_pa_void"]),
+        # the phase gate: requests with a body it evaluated in its
+        # first stage, and of those the ones its body stage scanned and evaluated again
+        "gate": {"body_requests": int(st.get("gate_requests", 0)), "pending": int(st.get("gate_pending", 0))},
         "error_requests": int(tally["n_error"]),
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",

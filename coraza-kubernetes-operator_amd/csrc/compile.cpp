@@ -1966,9 +1966,14 @@ struct Lower {
         }
         return false;
       };
-      // patterns that may share a union automaton, in order (packed below)
+      // Pass 1: the automata of patterns that never share a union (large
+      // phrase sets, non-ASCII phrases, negated operators) -- kept per pattern
+      // position -- and the list of patterns that may (packed in pass 2).
+      std::vector<std::vector<AutoBuild>> fixed(sb.pats.size());
+      std::vector<char> is_union(sb.pats.size(), 0);
       std::vector<std::pair<const PatEntry*, std::unique_ptr<Regex>>> unionable;
-      for (auto& pe : sb.pats) {
+      for (size_t pi = 0; pi < sb.pats.size(); pi++) {
+        const PatEntry& pe = sb.pats[pi];
         auto re = std::make_unique<Regex>();
         bool ok;
         size_t pbytes = 0;
@@ -1978,7 +1983,7 @@ struct Lower {
             P->always_slots.push_back(pe.slot);
             continue;
           }
-          for (auto& d : phrase_group_dfas(pe.phrases, pe.kind == 1)) autos.push_back({std::move(d), {&pe}});
+          for (auto& d : phrase_group_dfas(pe.phrases, pe.kind == 1)) fixed[pi].push_back({std::move(d), {&pe}});
           continue;
         }
         if (pe.kind == 0) {
@@ -1990,7 +1995,7 @@ struct Lower {
         if (!ok) {  // non-ASCII phrase: its own byte-mode automaton
           Dfa d;
           if (!build_phrase_dfa(pe.phrases, pe.kind == 1, &d, &err, cap)) unsup(err);
-          autos.push_back({std::move(d), {&pe}});
+          fixed[pi].push_back({std::move(d), {&pe}});
           continue;
         }
         if (pe.negate) {  // negated operators stay out of union automata (the scan emits union hits eagerly)
@@ -1999,77 +2004,70 @@ struct Lower {
             P->always_slots.push_back(pe.slot);
             continue;
           }
-          autos.push_back({std::move(single), {&pe}});
+          fixed[pi].push_back({std::move(single), {&pe}});
           continue;
         }
+        is_union[pi] = 1;
         unionable.emplace_back(&pe, std::move(re));
       }
-      // Greedy packing: each union automaton takes the longest run of the next
-      // patterns (<= 64) whose union DFA stays within 16384 states and the LDS
-      // table budget.  The run length is found by galloping + bisection over
-      // the prefix length (a longer prefix only adds states), so a union of n
-      // patterns costs O(log n) builds instead of n.  Runs of kPackChunk
-      // patterns are packed independently, on all host cores (a chunk boundary
-      // also ends a union: the plan does not depend on the thread count).
+      // Pass 2, greedy packing: each union automaton takes the next patterns
+      // (<= 64) until adding one more would leave 16384 states or the LDS
+      // table budget (a failing trial stops as soon as its states exceed the
+      // byte budget: build_union_dfa's byte_budget).  A pattern that does not
+      // fit even alone gets its own sticky DFA (or is always "maybe").  Runs of
+      // kPackChunk patterns are packed independently, on all host cores (a
+      // chunk boundary also ends a union: the plan does not depend on the
+      // thread count).
       constexpr size_t kPackChunk = 512;
-      struct Packed {
-        std::vector<AutoBuild> autos;  // in order; an empty pes list marks an "always" slot
-        std::vector<const PatEntry*> always;
+      struct Group {
+        AutoBuild ab;
+        size_t n = 0;         // patterns of the group
+        bool unioned = false;
+        bool always = false;  // no automaton at all
       };
       const size_t nchunks = (unionable.size() + kPackChunk - 1) / kPackChunk;
-      std::vector<Packed> packed(nchunks);
+      std::vector<std::vector<Group>> packed(nchunks);
       auto pack_chunk = [&](size_t ch) {
         std::string lerr;
-        Packed& out = packed[ch];
+        std::vector<Group>& out = packed[ch];
         const size_t end = std::min(unionable.size(), (ch + 1) * kPackChunk);
         for (size_t i = ch * kPackChunk; i < end;) {
           const size_t maxn = std::min<size_t>(64, end - i);
           auto fits = [&](size_t n, Dfa* d) {
             std::vector<const Regex*> rs;
             for (size_t k = 0; k < n; k++) rs.push_back(unionable[i + k].second.get());
-            return build_union_dfa(rs, d, &lerr, 16384, kUnionTableBytes) && img_bytes(*d) <= kUnionTableBytes;
+            return build_union_dfa(rs, d, &lerr, 16384, 4 * kUnionTableBytes) && img_bytes(*d) <= kUnionTableBytes;
           };
-          size_t lo = 0, hi = maxn + 1, step = 1;  // a union of lo patterns fits, of hi does not
+          size_t lo = 0;  // a union of the next lo patterns fits; lo + 1 does not
           Dfa best;
           while (lo < maxn) {
-            const size_t n = std::min(lo + step, maxn);
             Dfa t;
-            if (!fits(n, &t)) {
-              hi = n;
-              break;
-            }
-            lo = n;
+            if (!fits(lo + 1, &t)) break;
+            lo++;
             best = std::move(t);
-            step *= 2;
           }
-          while (hi - lo > 1) {
-            const size_t mid = (lo + hi) / 2;
-            Dfa t;
-            if (fits(mid, &t)) {
-              lo = mid;
-              best = std::move(t);
-            } else {
-              hi = mid;
-            }
-          }
+          Group g;
           if (lo > 0) {
-            std::vector<const PatEntry*> ps;
-            for (size_t k = 0; k < lo; k++) ps.push_back(unionable[i + k].first);
-            out.autos.push_back({std::move(best), ps});
+            for (size_t k = 0; k < lo; k++) g.ab.pes.push_back(unionable[i + k].first);
+            g.ab.d = std::move(best);
+            g.n = lo;
+            g.unioned = true;
+            out.push_back(std::move(g));
             i += lo;
             continue;
           }
           // too large for an LDS union automaton: single sticky DFA (global tables)
           const PatEntry& pe = *unionable[i].first;
-          Dfa single;
-          bool ok = build_regex_dfa(*unionable[i].second, &single, &lerr, cap);
+          bool ok = build_regex_dfa(*unionable[i].second, &g.ab.d, &lerr, cap);
           for (int lvl = 1; !ok && !pe.negate && pe.kind == 0 && lvl <= 3; lvl++) {
             Regex rr = *unionable[i].second;
             relax_regex(&rr, lvl);
-            ok = build_regex_dfa(rr, &single, &lerr, cap);
+            ok = build_regex_dfa(rr, &g.ab.d, &lerr, cap);
           }
-          if (ok) out.autos.push_back({std::move(single), {&pe}});
-          else out.always.push_back(&pe);  // no automaton: the link is always "maybe"
+          g.ab.pes = {&pe};
+          g.n = 1;
+          g.always = !ok;  // no automaton: the link is always "maybe"
+          out.push_back(std::move(g));
           i++;
         }
       };
@@ -2084,9 +2082,35 @@ struct Lower {
         work();
         for (auto& t : th) t.join();
       }
-      for (auto& pk : packed) {
-        for (auto& ab : pk.autos) autos.push_back(std::move(ab));
-        for (const PatEntry* pe : pk.always) P->always_slots.push_back(pe->slot);
+      // Emit in pattern order as a one-pattern-at-a-time greedy pass would: a
+      // fixed automaton where its pattern stands, a union when the pattern
+      // after its last one is reached (or at the end), a single right away.
+      {
+        std::vector<Group*> groups;
+        for (auto& ch : packed)
+          for (auto& g : ch) groups.push_back(&g);
+        size_t gi = 0, left = 0;  // current group, its patterns not yet visited
+        Group* open = nullptr;    // union waiting for its flush
+        auto emit = [&](Group* g) {
+          if (g->always) P->always_slots.push_back(g->ab.pes[0]->slot);
+          else autos.push_back(std::move(g->ab));
+        };
+        for (size_t pi = 0; pi < sb.pats.size(); pi++) {
+          if (!is_union[pi]) {
+            for (auto& ab : fixed[pi]) autos.push_back(std::move(ab));
+            continue;
+          }
+          if (left == 0) {  // this pattern starts the next group
+            if (open) emit(open);
+            open = nullptr;
+            Group* g = groups[gi++];
+            left = g->n;
+            if (g->unioned) open = g;
+            else emit(g);
+          }
+          left--;
+        }
+        if (open) emit(open);
       }
       for (auto& u : unionable) owned.push_back(std::move(u.second));
       flush();
@@ -3266,6 +3290,65 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
           if (out->vars[out->rules[ci].var_begin + q].var == V_MATCHED_VARS ||
               out->vars[out->rules[ci].var_begin + q].var == V_MATCHED_VARS_NAMES)
             out->rules[ti].flags2 |= RF2_MVS;
+    // chains whose evaluation over a body needs the body's phase-A scan (RF2_BODY_PA)
+    for (uint32_t ti : out->top)
+      for (int32_t ci = (int32_t)ti; ci >= 0; ci = out->rules[ci].chain_next) {
+        const DRule& d = out->rules[ci];
+        if (d.op < 0) continue;
+        const uint8_t k = out->ops[d.op].kind;
+        if (k != OP_RX && k != OP_PM && k != OP_CONTAINS && k != OP_CONTAINSWORD && k != OP_DETECT_SQLI &&
+            k != OP_DETECT_XSS)
+          continue;
+        bool body = false;
+        for (uint32_t q = 0; q < d.var_count && !body; q++) {
+          const uint8_t v = out->vars[d.var_begin + q].var;
+          // (REQUEST_BODY: k_body's bits, computed in the gate's first stage)
+          body = v == V_ARGS_POST || v == V_ARGS || v == V_ARGS_POST_NAMES ||
+                 v == V_ARGS_NAMES || v == V_XML || v == V_FILES || v == V_FILES_NAMES || v == V_FILES_SIZES ||
+                 v == V_FILES_TMPNAMES || v == V_MULTIPART_PART_HEADERS;
+        }
+        if (body) {
+          out->rules[ti].flags2 |= RF2_BODY_PA;
+          break;
+        }
+      }
+    // the gate's prefix: the links of the phase-2 rules before the first RF2_BODY_PA
+    // rule, and every phase-A stream one of them registered a pattern / value test in
+    {
+      std::vector<int32_t> slot_link(out->n_hit_slots, -1);
+      for (size_t ri = 0; ri < out->rules.size(); ri++)
+        if (out->rules[ri].hit_slot >= 0 && (uint32_t)out->rules[ri].hit_slot < out->n_hit_slots)
+          slot_link[out->rules[ri].hit_slot] = (int32_t)ri;
+      for (uint32_t ti : out->top) {
+        if (out->rules[ti].phase != 2) continue;
+        if (out->rules[ti].flags2 & RF2_BODY_PA) {
+          if (timing) fprintf(stderr, "gi_compile: gate prefix ends at rule %d\n", out->rules[ti].id);
+          break;
+        }
+        for (int32_t ci = (int32_t)ti; ci >= 0; ci = out->rules[ci].chain_next) out->rules[ci].flags2 |= RF2_PREFIX;
+      }
+      auto prefix_slot = [&](uint32_t sl) {
+        return sl < slot_link.size() && slot_link[sl] >= 0 && (out->rules[slot_link[sl]].flags2 & RF2_PREFIX);
+      };
+      for (DStream& st : out->streams) {
+        bool pre = false;
+        for (uint32_t q = 0; q < st.val_count && !pre; q++) pre = prefix_slot(out->svals[st.val_begin + q].slot);
+        for (uint32_t j = 0; j < st.job_count && !pre; j++) {
+          const DJob& J = out->jobs[st.job_begin + j];
+          for (uint32_t q = 0; q < J.jdfa_count && !pre; q++) {
+            const DJobDfa& jd = out->jdfas[J.jdfa_begin + q];
+            for (uint32_t k = 0; k < jd.n_pat && !pre; k++) pre = prefix_slot(out->pats[jd.pat_begin + k].slot);
+          }
+        }
+        st.prefix = pre ? 1 : 0;
+      }
+      if (timing) {
+        uint32_t np = 0, nl = 0;
+        for (const DStream& st : out->streams) np += st.prefix;
+        for (const DRule& d : out->rules) nl += (d.flags2 & RF2_PREFIX) ? 1 : 0;
+        fprintf(stderr, "gi_compile: gate prefix: %u links, %u of %zu streams\n", nl, np, out->streams.size());
+      }
+    }
     {  // top-level rules with an observable capture link (capture records, gi_capture)
       std::string ids;
       for (uint32_t ti : out->top)

@@ -118,6 +118,7 @@ struct DBatch {
   uint8_t* pend;              // [n_req] stage 1 -> 2: 1 = the request continues to the body stage
   uint32_t* plist;            // the pending requests (stage-1 k_eval appends), *pcount of them
   uint32_t* pcount;
+  uint32_t prefix_budget;     // RF2_BODY_PA rules a first-stage request evaluates over its unscanned body
 };
 
 // k_scan launch plan: job lists for the small-LDS and big-LDS launches.
@@ -146,6 +147,8 @@ struct ScanLaunch {
 #define GI_EVAL_WAVE_RULES 2048
 #define GI_BPARSE_LDS 0              // k_bparse LDS copy of JSON bodies up to this size (GI_BPARSE_LDS env; 0: off --
                                      // measured: 32 KB made C3's k_bparse 81 -> 272 ms, the LDS cut its occupancy)
+#define GI_PREFIX_BUDGET 0             // default DBatch.prefix_budget (GI_PREFIX_BUDGET env; round 5: the
+                                     // interpreter is ~500 cycles per body byte per automaton link)
 #define GI_CHUNK_POOL_WORDS 16e9     // queue-pool words (estimate) one request chunk of a batch may need
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.

@@ -211,6 +211,13 @@ enum RuleFlags2 : uint8_t {
   RF2_MVS = 1,  // a later link of this chain reads MATCHED_VARS(_NAMES): k_eval keeps the entries
   RF2_MVCUR = 2,  // MATCHED_VAR / MATCHED_VAR_NAME this chain's matches set can be read (compile.cpp fold_program)
                 // (otherwise only MATCHED_VAR / MATCHED_VAR_NAME are updated per match)
+  RF2_BODY_PA = 4,  // a link of the chain runs an automaton / libinjection operator (@rx @pm @contains
+                    // @containsWord @detectSQLi @detectXSS) over a body field collection: the gate's
+                    // first stage (kernels.hip launch_pipeline) stops the phase-2 walk here until
+                    // phase A has scanned the request's body fields
+  RF2_PREFIX = 8,   // (any link) a link of a phase-2 rule before the first RF2_BODY_PA rule: its phase-A
+                    // streams are "prefix" streams (DStream.prefix), which the gate's first stage runs over
+                    // the body fields too -- its hit bits are complete there
 };
 
 enum ActKind : uint8_t {
@@ -312,7 +319,7 @@ struct DStream {
                       // becomes one byte, GI_RUNE_MARK (rmap_cnt 0: the automata agree on all of
                       // them) or 0x80 + its joint class (rmap triples (lo, hi, byte) in nranges)
   uint8_t det_id;     // index in DProgram.det_streams if some val is @detectSQLi/@detectXSS, else 0xFF
-  uint8_t _pad;
+  uint8_t prefix;     // a RF2_PREFIX link reads it: the gate's first stage scans body fields through it
   uint32_t rmap_off, rmap_cnt;
   uint32_t _pad2;
 };

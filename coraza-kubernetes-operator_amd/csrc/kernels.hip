@@ -1420,6 +1420,9 @@ struct Tx {
   uint32_t rm_groups;        // ctl:ruleRemoveByTag / ByMsg groups removed (DProgram.rule_groups)
   uint32_t cur_groups;       // removal groups of the top-level rule being evaluated
   uint8_t allow;             // allow action in effect (D_ALLOW_*; 0: none)
+  bool prefix;               // gate stage 1, the request's body processed: stop at the first RF2_BODY_PA rule
+  bool bail;                 // ... and it stopped there (the body stage re-evaluates it)
+  uint32_t pa_budget;        // RF2_BODY_PA rules the first stage still evaluates itself (DBatch.prefix_budget)
   uint8_t engine, body_access, body_proc, phase;
   uint8_t force_body;
   int32_t skip_after;
@@ -4134,6 +4137,13 @@ GI_HD __noinline__ bool target_removed_in(const Tx::RmTarget* rt, uint32_t n, co
 #define target_removed(t, id, var, k, kn) \
   target_removed_in((t).rtgt, (t).nrtgt, (t).P->strpool, (id), (t).cur_groups, (var), (k), (kn))
 
+// The link's phase-A bits are void: it can see ARGS_POST / body fields phase A
+// did not scan for it (the gate's first stage scans body fields only through
+// the prefix streams, so there a RF2_PREFIX link's bits stay valid).
+GI_HD __forceinline__ bool bodydep_void(const Tx& t, const DRule& R) {
+  return (R.flags & RF_BODYDEP) && t.has_post && !(t.prefix && (R.flags2 & RF2_PREFIX));
+}
+
 GI_HD __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
   const DProgram& P = *t.P;
   for (uint32_t e = 0; e < vr.exc_count; e++) {
@@ -4195,18 +4205,26 @@ GI_HD __forceinline__ void var_kinds(uint8_t var, uint32_t* lo, uint32_t* hi) {
 // of all fields would: ARGS' two kinds are GET args, then POST args, and every
 // GET arg precedes every POST arg).  Rebuilt when a body parse adds fields;
 // an arena without room leaves kx null (scan every field).
-GI_HD __noinline__ const uint32_t* build_kindex(const Field* fields, uint32_t nf, uint8_t* bytes, uint32_t* nb,
+// (nb by value, the arena bytes it used returned in kx[11]: a pointer into the
+// caller's Tx would pin the whole Tx in scratch memory)
+GI_HD __noinline__ const uint32_t* build_kindex(const Field* fields, uint32_t nf, uint8_t* bytes, uint32_t nb,
                                                     uint32_t cap_b) {
-  const uint32_t pad = (4u - (uint32_t)((uintptr_t)(bytes + *nb) & 3u)) & 3u;
-  if ((uint64_t)*nb + pad + 4ull * (12ull + nf) > cap_b) return nullptr;
-  uint32_t* kx = (uint32_t*)(bytes + *nb + pad);
-  *nb += pad + 4u * (12u + nf);
+  const uint32_t pad = (4u - (uint32_t)((uintptr_t)(bytes + nb) & 3u)) & 3u;
+  if ((uint64_t)nb + pad + 4ull * (12ull + nf) > cap_b) return nullptr;
+  uint32_t* kx = (uint32_t*)(bytes + nb + pad);
   for (uint32_t k = 0; k < 12; k++) kx[k] = 0;
   for (uint32_t f = 0; f < nf; f++) kx[min((uint32_t)fields[f].kind, 9u) + 1]++;
   for (uint32_t k = 1; k <= 10; k++) kx[k] += kx[k - 1];
   for (uint32_t f = 0; f < nf; f++) kx[12 + kx[min((uint32_t)fields[f].kind, 9u)]++] = f;
   for (uint32_t k = 10; k >= 1; k--) kx[k] = kx[k - 1];
   kx[0] = 0;
+  kx[11] = pad + 4u * (12u + nf);
+  return kx;
+}
+GI_HD __forceinline__ const uint32_t* kindex_into(const Field* fields, uint32_t nf, uint8_t* bytes, uint32_t& nb,
+                                                  uint32_t cap_b) {
+  const uint32_t* kx = build_kindex(fields, nf, bytes, nb, cap_b);
+  if (kx) nb += kx[11];
   return kx;
 }
 
@@ -4331,7 +4349,7 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   }
   // phase-A filter: a clear hit bit proves no value matches (exact); a set
   // bit (match or "maybe") falls through to the full evaluation below.
-  if (R.hit_slot >= 0 && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post)) {
+  if (R.hit_slot >= 0 && !t.pa_void && !bodydep_void(t, R)) {
     const uint32_t w = t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride];
     if (!((w >> (R.hit_slot & 31)) & 1u)) {
       if (!(R.flags & RF_RESIDUAL)) return 0;
@@ -4474,7 +4492,7 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
         }
         // a collection: value-map / hit-set filtering (field_filter); multiMatch
         // links count candidates per value, so they always evaluate
-        vskip = R.hit_slot >= 0 && !vr.count && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
+        vskip = R.hit_slot >= 0 && !vr.count && !t.pa_void && !bodydep_void(t, R) &&
                 slot_vexact(P, (uint32_t)R.hit_slot);
         vexact = vskip && t.hset && !(R.flags & RF_MULTIMATCH);
         uint32_t klo, khi;
@@ -4712,7 +4730,7 @@ GI_HD __forceinline__ bool rule_noop(Tx& t, const DRule& R, uint32_t ri) {
   if (t.skip_after >= 0) return R.marker != t.skip_after;
   if (R.flags & RF_MARKER) return true;
   if ((R.flags & RF_CONST) && R._pad2 == 0) return true;  // a folded link that matches nothing
-  return R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
+  return R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !bodydep_void(t, R) &&
          !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u);
 }
 
@@ -4794,10 +4812,17 @@ GI_HD __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
       t.mv->n = 0;
       t.mv->nb = 0;
     }
-    if (R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !((R.flags & RF_BODYDEP) && t.has_post) &&
+    if (R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !bodydep_void(t, R) &&
         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u))
       continue;  // phase A proved the first link matches nothing
     if ((R.flags & RF_CONST) && R._pad2 == 0) continue;  // folded: matches nothing for any request
+    if (t.prefix && (R.flags2 & RF2_BODY_PA)) {  // evaluated over the unscanned body by the interpreter, up to
+      if (t.pa_budget == 0) {                     // a budget of such rules; then the first stage ends here
+        t.bail = true;
+        break;
+      }
+      t.pa_budget--;
+    }
     eval_top<W>(t, ri);
     if (t.allow) {  // the allow rule ends this phase's walk (allow:phase: only this one)
       if (t.allow == D_ALLOW_PHASE) t.allow = 0;
@@ -5026,18 +5051,20 @@ GI_HD __forceinline__ uint64_t wave_sum(uint64_t x) {
 }
 
 // Visits the items of one request: singles some filter reads, then the
-// (value, key) sides of every field kind some filter reads.  body_only (the
-// gate's body stage): the body fields alone -- the phase-1 stage scanned the rest.
+// (value, key) sides of every field kind some filter reads.  part (the gate,
+// launch_pipeline): 0 all items, 1 the phase-1 items (no body field), 2 the
+// body fields alone.
 template <class F>
 GI_HD __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H, const Field* Fd, F&& f,
-                                         bool body_only = false) {
-  if (!body_only)
+                                         uint32_t part = 0) {
+  if (part != 2)
     for (uint32_t m = P.item_singles; m; m &= m - 1) {
       const uint32_t sg = __ffs(m) - 1;
       f((uint8_t)0, (uint8_t)sg, 0u, (uint32_t)0xFFFFFFFFu, H->single[sg].n);
     }
   const uint32_t n_get = H->n_get, n_hdr = H->n_hdr, n_ck = H->n_ck, n_pre = n_get + n_hdr + n_ck;
-  for (uint32_t i = body_only ? n_pre : 0u; i < n_pre + H->n_post; i++) {
+  const uint32_t i_end = part == 1 ? n_pre : n_pre + H->n_post;
+  for (uint32_t i = part == 2 ? n_pre : 0u; i < i_end; i++) {
     const Field fl = Fd[i];
     // the body range may hold multipart collections: FILES / FILES_NAMES /
     // FILES_SIZES are phase-A items, part headers are not
@@ -5463,6 +5490,27 @@ __global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
 }
 
 
+// The gate's body stage (launch_pipeline): per-block item counts of the body
+// fields of the pending requests (k_collect's layout: one thread per request,
+// 256 per block).
+__global__ void __launch_bounds__(256) k_bcounts(DProgram P, DBatch B) {
+  __shared__ uint32_t hist[GI_NCLS];
+  for (uint32_t k = threadIdx.x; k < GI_NCLS; k += blockDim.x) hist[k] = 0;
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < B.n_req && B.pend[r]) {
+    const ReqLayout L = B.layout[r];
+    const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
+    if (!(H->flags & GI_REQ_ERROR_MASK))
+      for_each_item(P, H, (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES),
+                    [&](uint8_t kind, uint8_t, uint32_t side, uint32_t, uint32_t n) {
+                      atomicAdd(&hist[item_class(kind, side, n)], 1u);
+                    }, 2u);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < GI_NCLS; k += blockDim.x) B.bcounts[blockIdx.x * GI_NCLS + k] = hist[k];
+}
+
 // ============================================================== phase A
 // Data-parallel operator evaluation (SURVEY §2 rx_dfa_scan / ac_scan /
 // simple_ops).  Every rule link whose operator is a pure function of one
@@ -5625,7 +5673,7 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
         if (kind && fi > GI_MAX_ITEM_FIELD) void_request(B, r, GI_VOID_FIELD);  // no value-map index: no phase-A bit trusted
         ((Item*)B.items)[at] = it;
         atomicAdd(&ibytes[b], (unsigned long long)n);
-      }, B.stage == 2);
+      }, B.stage == 2 ? 2u : 0u);  // the body stage: the pending requests' body fields
     }
   }
   __syncthreads();
@@ -5950,10 +5998,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
     uint32_t rawmask = 0;  // detect streams whose output is the unchanged item (one k_detect entry per item)
     // a long value (>= GI_LONG_MIN bytes) takes k_long: one wave per (item, stream), no queue block
     const bool is_long = IN == 0 && B.long_cap && ii < cnt && it.vn >= GI_LONG_MIN;
+    // the gate (launch_pipeline): the first stage scans body fields through the
+    // prefix streams only, the body stage through the others
+    const uint32_t ik = item_kind(it);
+    const bool body_item = ik == FK_ARG_POST || (ik >= FK_FILE && ik <= FK_FILE_SIZE);
     for (uint32_t s = 0; s < P.n_streams; s++) {
       const uint64_t c_s0 = B.prof ? gi_clock() : 0;
       const DStream S = gi_cload(P.streams, s);
-      const uint64_t fm0 = gm & S.gmask;
+      const bool skip_s = (B.stage == 1 && body_item && !S.prefix) || (B.stage == 2 && S.prefix);
+      const uint64_t fm0 = skip_s ? 0ull : gm & S.gmask;
       if (is_long && fm0) {
         const uint32_t k = atomicAdd(B.long_count, 1u);
         if (k < B.long_cap) B.long_list[k] = make_uint2(base + ii, s);
@@ -6933,8 +6986,9 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
 // RuleGroup.Eval(1) -> ProcessRequestBody -> RuleGroup.Eval(2) per request,
 // skipping every phase-A rule whose hit bit is clear.
 #ifndef GI_EVAL_WPE
-#define GI_EVAL_WPE 2  // minimum waves per SIMD k_eval is compiled for (register budget; A/B: 2 beats 1 and 4;
-                       // round 3: 1 wave has no spills and 25.6 GB PMC traffic instead of 61 GB, but 26.7 ms vs 24.8)
+#define GI_EVAL_WPE 1  // minimum waves per SIMD k_eval is compiled for (register budget).  Round 5, C2 A/B on
+                       // one box: the Tx in registers (build_kindex no longer takes &t.nb) at 1 wave/SIMD, no
+                       // spills: 25.5 ms; at 2 waves (418 VGPR spills) 30.0 ms; the Tx in scratch at 2: 27.6 ms
 #endif
 // Phase B of request r: RuleGroup.Eval(1) -> ProcessRequestBody ->
 // RuleGroup.Eval(2); my[7] = its tally contributions.  W (k_eval_wave): the
@@ -6986,6 +7040,9 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
   t.rm_groups = 0;
   t.cur_groups = 0;
   t.allow = 0;
+  t.prefix = false;
+  t.bail = false;
+  t.pa_budget = B.prefix_budget;
   t.kx = nullptr;
   t.engine = P.rule_engine;
   t.body_access = P.body_access;
@@ -7046,27 +7103,18 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
     const gi_header hd = B.headers[rq.hdr_begin + h];
     scanned += hd.name.len + hd.value.len;
   }
-  t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
+  t.kx = kindex_into(t.fields, t.nf, t.bytes, t.nb, t.cap_b);
   const uint64_t c_init = B.prof ? gi_clock() : 0;
-  // the gate's phase-1 stage: a request with a body stops after phase 1
-  // unless phase 1 decided it; the only request state phase 1 writes outside
-  // this thread's registers and its re-initialised scratch is REQBODY_PROCESSOR
-  // (ctl:requestBodyProcessor), restored for the body stage's re-run
-  const bool gate1 = B.stage == 1 && rq.body.len > 0;
+  // the gate's first stage: phase A has not scanned the body fields yet, so a
+  // request with a body runs phase 1 and the phase-2 rules before the first
+  // one whose evaluation needs that scan (RF2_BODY_PA), with the body fields
+  // evaluated by the interpreter (their hit bits void: has_post); reaching
+  // that rule undecided, it continues in the body stage (launch_pipeline)
   const Str rbp0 = t.single[S_REQBODY_PROCESSOR];
   // phase 1, ProcessRequestBody, phase 2 (one eval_phase call site)
   for (uint8_t ph = 1; ph <= 2 && !(t.flags & GI_REQ_ERROR_MASK); ph++) {
     if (ph == 2) {
       if (t.interrupted || t.engine == ENGINE_OFF) break;
-      if (gate1) {
-        if (lead) {
-          t.single[S_REQBODY_PROCESSOR] = rbp0;
-          B.pend[r] = 1;
-          B.plist[gi_fetch_add(B.pcount, 1u)] = r;
-        }
-        for (int c = 0; c < 7; c++) my[c] = 0;
-        return;
-      }
       uint32_t bn = rq.body.len;
       bool run2 = true;
       if (t.body_access && bn > 0) {
@@ -7107,8 +7155,13 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
           }
           if (t.body_proc == BP_URLENCODED || t.body_proc == BP_JSON) {
             t.single[S_REQUEST_BODY] = {D + rq.body.off, bn};
-            if (t.body_proc == H->spec_proc) {
-              t.nf += H->n_post;  // k_collect's fields, already in phase A
+            if (t.body_proc == H->spec_proc && B.stage == 1) {
+              t.nf += H->n_post;  // k_bparse's fields: scanned through the prefix streams only
+              t.nf_pa = t.nf;      // (value map valid for RF2_PREFIX links; the others' bits are void)
+              t.has_post = H->n_post > 0;
+              t.body_spec = true;  // k_body (first stage) tested REQUEST_BODY
+            } else if (t.body_proc == H->spec_proc) {
+              t.nf += H->n_post;  // k_bparse's fields, already in phase A
               t.nf_pa = t.nf;
               t.body_spec = true;
             } else {
@@ -7137,8 +7190,13 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
             // -> MULTIPART_STRICT_ERROR + generateRequestBodyError (rules
             // 200002 / 200003 deny with 400)
             uint8_t err;
-            if (H->spec_proc == BP_MULTIPART) {
-              t.nf += H->n_post;  // k_bparse's fields (ARGS_POST already in phase A)
+            if (H->spec_proc == BP_MULTIPART && B.stage == 1) {
+              t.nf += H->n_post;  // k_mpparse's fields: scanned through the prefix streams only
+              t.nf_pa = t.nf;
+              t.has_post = H->n_post > 0;
+              err = H->spec_err;
+            } else if (H->spec_proc == BP_MULTIPART) {
+              t.nf += H->n_post;  // k_mpparse's fields (ARGS_POST already in phase A)
               t.nf_pa = t.nf;
               t.body_spec = true;
               err = H->spec_err;
@@ -7179,14 +7237,36 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
           } else if (t.body_proc != BP_NONE) {
             t.flags |= GI_REQ_UNSUPPORTED_BODY;
           }
-          if (t.nf != H->nf) t.kx = build_kindex(t.fields, t.nf, t.bytes, &t.nb, t.cap_b);
+          if (t.nf != H->nf) t.kx = kindex_into(t.fields, t.nf, t.bytes, t.nb, t.cap_b);
         }
       }
       if ((t.flags & GI_REQ_ERROR_MASK) || !run2) break;
+      // (body fields or a REQUEST_BODY phase A has not seen: XML values are never phase-A items)
+      t.prefix = B.stage == 1 && (t.has_post || t.single[S_REQUEST_BODY].n > 0);
     }
     const uint64_t c0 = B.prof ? gi_clock() : 0;
     eval_phase<W>(t, ph);
     if (B.prof && lead) gi_prof_add(&B.prof[ph], (unsigned long long)(gi_clock() - c0));
+  }
+  if (t.bail) {
+    // undecided before a rule that needs the body's phase-A scan: the body
+    // stage evaluates the request again from the start.  The request state
+    // the phase-2 prologue wrote goes back to k_collect's / the parsers' values.
+    if (lead) {
+      t.single[S_REQBODY_PROCESSOR] = rbp0;
+      t.single[S_INBOUND_DATA_ERROR] = {CS_ZERO, 0};
+      t.single[S_REQUEST_BODY_LENGTH] = {CS_ZERO, 0};
+      t.single[S_REQUEST_BODY] = {CS_ZERO, 0};
+      t.single[S_REQBODY_ERROR] = {CS_ZERO, 1};
+      t.single[S_REQBODY_ERROR_MSG] = {CS_ZERO, 0};
+      t.single[S_MULTIPART_STRICT_ERROR] = {CS_ZERO, 1};
+      if (H->spec_proc != BP_MULTIPART) t.single[S_FILES_COMBINED_SIZE] = {CS_ZERO, 0};
+      B.pend[r] = 1;
+      B.plist[gi_fetch_add(B.pcount, 1u)] = r;
+      gi_fetch_add(B.pcount + 1, 1u);  // pending requests of the whole run (gi_stats.gate_pending)
+    }
+    for (int c = 0; c < 7; c++) my[c] = 0;
+    return;
   }
   if (B.prof && lead) {
     gi_prof_add(&B.prof[0], (unsigned long long)(c_init - c_start));
@@ -7446,31 +7526,32 @@ void cpu_inspect_one(const DProgram& P, const DBatch& B) {
 static void launch_phase_a(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream,
                            hipEvent_t* ev, int stop_after, LaunchLog* log, int& nk) {
   const uint32_t cb = (B.n_req + 255) / 256;
-  GI_LAUNCH("k_ioffsets", k_ioffsets, dim3(GI_NCLS), dim3(256), 0, stream, B, cb);
-  GI_LAUNCH("k_ibases", k_ibases, dim3(1), dim3(256), 0, stream, B);
-  GI_LAUNCH("k_items", k_items, dim3(cb), dim3(256), 0, stream, P, B);
+  const bool s2 = B.stage == 2;  // the gate's body stage: its launches are timed under their own names
+  GI_LAUNCH(s2 ? "k_ioffsets.2" : "k_ioffsets", k_ioffsets, dim3(GI_NCLS), dim3(256), 0, stream, B, cb);
+  GI_LAUNCH(s2 ? "k_ibases.2" : "k_ibases", k_ibases, dim3(1), dim3(256), 0, stream, B);
+  GI_LAUNCH(s2 ? "k_items.2" : "k_items", k_items, dim3(cb), dim3(256), 0, stream, P, B);
   // chain memo slots per lane: as many as keep 8 one-wave workgroups per CU within the LDS
-  GI_LAUNCH("k_stream0", (k_stream<16, 20, 4>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 0u);
-  GI_LAUNCH("k_stream1", (k_stream<32, 36, 3>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 1u);
-  GI_LAUNCH("k_stream2", (k_stream<64, 68, 1>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 2u);
-  GI_LAUNCH("k_stream3", (k_stream<128, 132, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
-  GI_LAUNCH("k_stream4", (k_stream<0, 0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
-  if (P.n_det_streams) GI_LAUNCH("k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
-  if (B.long_cap) GI_LAUNCH("k_long", k_long, dim3(B.long_grid), dim3(64), 0, stream, P, B);
+  GI_LAUNCH(s2 ? "k_stream0.2" : "k_stream0", (k_stream<16, 20, 4>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 0u);
+  GI_LAUNCH(s2 ? "k_stream1.2" : "k_stream1", (k_stream<32, 36, 3>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 1u);
+  GI_LAUNCH(s2 ? "k_stream2.2" : "k_stream2", (k_stream<64, 68, 1>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 2u);
+  GI_LAUNCH(s2 ? "k_stream3.2" : "k_stream3", (k_stream<128, 132, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
+  GI_LAUNCH(s2 ? "k_stream4.2" : "k_stream4", (k_stream<0, 0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
+  if (P.n_det_streams) GI_LAUNCH(s2 ? "k_detect.2" : "k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
+  if (B.long_cap) GI_LAUNCH(s2 ? "k_long.2" : "k_long", k_long, dim3(B.long_grid), dim3(64), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[1], stream);
   for (int big = 0; big < 2; big++)
     if (S.n_jobs[big]) {
       if (big)
-        GI_LAUNCH("k_scan_big", (k_scan<true, true>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
+        GI_LAUNCH(s2 ? "k_scan_big.2" : "k_scan_big", (k_scan<true, true>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
                   S.jobs[big], S.n_jobs[big], S.mode, 1u);
       else
-        GI_LAUNCH("k_scan", (k_scan<true, false>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
+        GI_LAUNCH(s2 ? "k_scan.2" : "k_scan", (k_scan<true, false>), dim3(S.blocks[big]), dim3(1024), S.lds[big], stream, P, B,
                   S.jobs[big], S.n_jobs[big], S.mode, 0u);
     }
   if (S.n_global)
-    GI_LAUNCH("k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
+    GI_LAUNCH(s2 ? "k_scan_hbm.2" : "k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
               S.n_global, S.mode, 2u);
-  GI_LAUNCH("k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
+  GI_LAUNCH(s2 ? "k_scan_slow.2" : "k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
 }
 
 static void launch_eval(const DProgram& P, const DBatch& B, hipStream_t stream, int stop_after, LaunchLog* log,
@@ -7479,13 +7560,13 @@ static void launch_eval(const DProgram& P, const DBatch& B, hipStream_t stream, 
     // GI_EVAL_BS A/B (C2, 1M): 128 threads 26.2 ms, 64 threads 32.1 ms
     static const uint32_t ev_env = getenv("GI_EVAL_BS") ? (uint32_t)atoi(getenv("GI_EVAL_BS")) : 0u;
     const uint32_t ev_bs = (ev_env == 64 || ev_env == 128) ? ev_env : (B.n_req + 127) / 128 < 1024 ? 64u : 128u;
-    GI_LAUNCH(B.stage == 2 ? "k_eval2" : "k_eval", k_eval, dim3((B.n_req + ev_bs - 1) / ev_bs), dim3(ev_bs), 0, stream, P,
+    GI_LAUNCH(B.stage == 2 ? "k_eval.2" : "k_eval", k_eval, dim3((B.n_req + ev_bs - 1) / ev_bs), dim3(ev_bs), 0, stream, P,
               B);
   }
   if (B.wlist) {  // heavy requests, one wave each (persistent over k_eval's list)
     const uint32_t nw = (B.n_hit_slots + 31) / 32;
     const uint32_t lds = nw <= GI_EVAL_WAVE_LDS_WORDS ? 4 * std::max<uint32_t>(nw, 1u) : 0u;
-    GI_LAUNCH(B.stage == 2 ? "k_eval_wave2" : "k_eval_wave", k_eval_wave, dim3(std::min<uint32_t>(B.n_req, 8192)),
+    GI_LAUNCH(B.stage == 2 ? "k_eval_wave.2" : "k_eval_wave", k_eval_wave, dim3(std::min<uint32_t>(B.n_req, 8192)),
               dim3(64), lds, stream, P, B);
   }
 }
@@ -7495,16 +7576,19 @@ void launch_pipeline(const DProgram& P, const DBatch& B0, const ScanLaunch& S, h
   if (!B0.n_req) return;
   int nk = 0;  // (the caller resets *log and records its ev[0] before the first chunk)
   const uint32_t cb = (B0.n_req + 255) / 256;
-  // The phase-1 gate: when the batch has bodies to parse, phase 1 runs first and
-  // the body work (parsers, body phase A, k_body, phase 2) only for the requests
-  // phase 1 did not decide (ProcessRequestHeaders' interruption
-  // ends the transaction before WriteRequestBody).
+  // The gate: when the batch has bodies, the first stage parses them and runs
+  // k_body (REQUEST_BODY links) but scans only the phase-1 items, and
+  // evaluates every request up to the first phase-2 rule that needs its body
+  // fields' phase-A scan (RF2_BODY_PA): requests with no body, and those phase
+  // 1 or the phase-2 rules before it decide (CRS's ARGS-count / byte-range
+  // checks, REQBODY_ERROR), are final there.  The second stage scans the other
+  // (pending) requests' body fields and evaluates them in full.
   const bool gated = B0.gate && B0.n_body && P.body_access && B0.pend && B0.plist && B0.pcount;
   DBatch B = B0;
   B.stage = gated ? 1u : 0u;
   if (gated) (void)hipMemsetAsync(B.pcount, 0, 4, stream);
   GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
-  if (!gated && B.n_body && P.body_access) {
+  if (B.n_body && P.body_access) {
     GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), B.bparse_lds, stream, P, B);
     if (B.n_mp_body) GI_LAUNCH("k_mpparse", k_mpparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
   }
@@ -7514,24 +7598,20 @@ void launch_pipeline(const DProgram& P, const DBatch& B0, const ScanLaunch& S, h
   if (stop_after && nk >= stop_after) return;
   // REQUEST_BODY links (a ruleset may have them without any phase-A stream):
   // one wave (workgroup) per body
-  if (!gated && P.n_body_links && B.n_body)
+  if (P.n_body_links && B.n_body)
     GI_LAUNCH("k_body", k_body, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[2], stream);
   launch_eval(P, B, stream, stop_after, log, nk);
   if (gated) {
     // the body stage: phase-A counters restart (the hit words, value
-    // signatures and hit sets keep the phase-1 stage's bits), the item counts
-    // are the body parsers' own
+    // signatures and hit sets keep the first stage's bits)
     DBatch B2 = B0;
     B2.stage = 2;
     (void)hipMemsetAsync((void*)B2.pool_used, 0, 128, stream);  // ctr[0, 128): pool, slow, detect, long, wave list, buckets
-    if (P.n_streams) (void)hipMemsetAsync(B2.bcounts, 0, 4ull * cb * GI_NCLS, stream);
-    GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B2.n_body, 1u << 20)), dim3(64), B2.bparse_lds, stream, P, B2);
-    if (B2.n_mp_body)
-      GI_LAUNCH("k_mpparse", k_mpparse, dim3(std::min<uint32_t>(B2.n_body, 1u << 20)), dim3(64), 0, stream, P, B2);
-    if (P.n_streams) launch_phase_a(P, B2, S, stream, nullptr, stop_after, log, nk);
-    if (P.n_body_links)
-      GI_LAUNCH("k_body", k_body, dim3(std::min<uint32_t>(B2.n_body, 1u << 20)), dim3(64), 0, stream, P, B2);
+    if (P.n_streams) {
+      GI_LAUNCH("k_bcounts", k_bcounts, dim3(cb), dim3(256), 0, stream, P, B2);
+      launch_phase_a(P, B2, S, stream, nullptr, stop_after, log, nk);
+    }
     launch_eval(P, B2, stream, stop_after, log, nk);
   }
   {

@@ -1219,6 +1219,9 @@ int gi_run_staged(gi_ctx* c) {
     B.pend = (uint8_t*)c->pend.p;
     B.plist = (uint32_t*)c->plist.p;
     B.pcount = (uint32_t*)(cp + 512);
+    static const uint32_t budget_env =
+        getenv("GI_PREFIX_BUDGET") ? (uint32_t)atoi(getenv("GI_PREFIX_BUDGET")) : GI_PREFIX_BUDGET;
+    B.prefix_budget = budget_env;
     B.bparse_lds = (uint32_t)std::min<uint64_t>(c->bparse_lds, (c->max_body + 15) & ~15ull);
   }
   (void)hipEventRecord(c->ev0, c->stream);
@@ -1243,8 +1246,10 @@ int gi_run_staged(gi_ctx* c) {
   // accumulate
   c->log.n = 0;
   (void)hipEventRecord(c->log.ev[0], c->stream);
+  c->stats.gate_requests = 0;
   for (size_t k = 0; k < c->chunks.size(); k++) {
     const gi_ctx::Chunk& ch = c->chunks[k];
+    if (B.gate && ch.n_body && c->prog.body_access) c->stats.gate_requests += ch.n_body;
     if (k && c->ctr.p) {
       e = hipMemsetAsync(c->ctr.p, 0, 128, c->stream);
       if (e != hipSuccess) return hip_fail(c, e, "memset chunk counters");
@@ -1299,6 +1304,9 @@ int gi_sync(gi_ctx* c) {
     if (c->ctr.p) (void)hipMemcpy(ibc, (uint8_t*)c->ctr.p + 384, 40, hipMemcpyDeviceToHost);
     uint64_t slow_bytes = 0;
     if (c->ctr.p) (void)hipMemcpy(&slow_bytes, (uint8_t*)c->ctr.p + 8, 8, hipMemcpyDeviceToHost);
+    uint32_t gate_pending = 0;  // DBatch.pcount[1] (kernels.hip eval_request)
+    if (c->ctr.p) (void)hipMemcpy(&gate_pending, (uint8_t*)c->ctr.p + 516, 4, hipMemcpyDeviceToHost);
+    c->stats.gate_pending = c->stats.gate_requests ? gate_pending : 0;
     // one record per launch name: a chunked batch repeats the pipeline, its
     // launches of one name are summed
     uint32_t nrec = 0;

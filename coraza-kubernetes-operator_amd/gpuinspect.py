@@ -51,6 +51,7 @@ GI_REQ_ERROR_MASK = 0x0F
 
 ACTIONS = {0: "", 1: "deny", 2: "drop", 3: "redirect"}
 MAX_EXPORTS = 8
+STATS_LAUNCHES = 48  # include/gpuinspect.h GI_STATS_LAUNCHES
 
 SPAN_DT = np.dtype([("off", "<u8"), ("len", "<u4"), ("_pad", "<u4")])
 REQUEST_DT = np.dtype([("method", SPAN_DT), ("uri", SPAN_DT), ("proto", SPAN_DT), ("body", SPAN_DT),
@@ -125,8 +126,9 @@ class _Stats(ctypes.Structure):
                 ("last_eval_ms", ctypes.c_double), ("last_stream_ms", ctypes.c_double),
                 ("last_pa_bytes", ctypes.c_uint64), ("diag", ctypes.c_uint64 * 8),
                 ("n_launches", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
-                ("launch_ms", ctypes.c_double * 24), ("launch_alg_bytes", ctypes.c_uint64 * 24),
-                ("launch_name", (ctypes.c_char * 16) * 24), ("launch_steps", ctypes.c_uint64 * 24)]
+                ("launch_ms", ctypes.c_double * STATS_LAUNCHES), ("launch_alg_bytes", ctypes.c_uint64 * STATS_LAUNCHES),
+                ("launch_name", (ctypes.c_char * 16) * STATS_LAUNCHES), ("launch_steps", ctypes.c_uint64 * STATS_LAUNCHES),
+                ("gate_requests", ctypes.c_uint64), ("gate_pending", ctypes.c_uint64)]
 
 
 _LIB = None

@@ -44,7 +44,7 @@ extern "C" {
 #define GI_EPARSE -1       /* SecLang syntax error (coraza.NewWAF error) */
 #define GI_EUNSUPPORTED -2 /* valid SecLang this engine does not implement */
 #define GI_EINVAL -3
-#define GI_STATS_LAUNCHES 24 /* gi_stats per-launch records */
+#define GI_STATS_LAUNCHES 48 /* gi_stats per-launch records */
 #define GI_ENODEV -4       /* no HIP device / kernel launch failure */
 #define GI_ENOMEM -5
 #define GI_ETRUNC -6       /* caller-provided result capacity too small */
@@ -216,6 +216,8 @@ typedef struct {
   uint64_t launch_alg_bytes[GI_STATS_LAUNCHES]; /* algorithmic bytes each launch must move */
   char launch_name[GI_STATS_LAUNCHES][16];
   uint64_t launch_steps[GI_STATS_LAUNCHES];     /* automaton byte-steps of each k_scan launch (secondary bound) */
+  uint64_t gate_requests;  /* requests with a body the phase gate's first stage evaluated (0: no gate) */
+  uint64_t gate_pending;   /* of which undecided there: scanned and evaluated again by the body stage */
 } gi_stats;
 
 /* ABI revision of the structs above (gi_batch, gi_results, gi_verdict,
