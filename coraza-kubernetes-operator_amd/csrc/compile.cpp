@@ -1935,9 +1935,18 @@ struct Lower {
     std::ostringstream js;
     js << "{\"streams\":[";
     bool first_s = true;
+    // the gate's prefix links (RF2_PREFIX, marked before the plan): their
+    // patterns get automata and jobs of their own, so the first stage can run
+    // them over body fields without the other patterns of their streams
+    std::vector<char> slot_prefix(P->n_hit_slots, 0);
+    for (const DRule& d : P->rules)
+      if (d.hit_slot >= 0 && (uint32_t)d.hit_slot < P->n_hit_slots && (d.flags2 & RF2_PREFIX)) slot_prefix[d.hit_slot] = 1;
+    auto pe_prefix = [&](const PatEntry& pe) { return pe.slot < slot_prefix.size() && slot_prefix[pe.slot]; };
     for (auto& sb : sbuild) {
-      std::stable_sort(sb.pats.begin(), sb.pats.end(),
-                       [](const PatEntry& a, const PatEntry& b) { return a.fmask < b.fmask; });
+      std::stable_sort(sb.pats.begin(), sb.pats.end(), [&](const PatEntry& a, const PatEntry& b) {
+        const bool pa = pe_prefix(a), pb = pe_prefix(b);
+        return pa != pb ? pa : a.fmask < b.fmask;
+      });
       // 1. automata: greedy union packing
       std::vector<AutoBuild> autos;
       std::vector<std::unique_ptr<Regex>> owned;
@@ -2019,19 +2028,25 @@ struct Lower {
       // chunk boundary also ends a union: the plan does not depend on the
       // thread count).
       constexpr size_t kPackChunk = 512;
+      size_t n_pre_u = 0;  // the prefix patterns lead the list: a union never mixes them with the others
+      while (n_pre_u < unionable.size() && pe_prefix(*unionable[n_pre_u].first)) n_pre_u++;
       struct Group {
         AutoBuild ab;
         size_t n = 0;         // patterns of the group
         bool unioned = false;
         bool always = false;  // no automaton at all
       };
-      const size_t nchunks = (unionable.size() + kPackChunk - 1) / kPackChunk;
+      std::vector<std::pair<size_t, size_t>> chunks;  // [begin, end): kPackChunk runs of each part
+      for (size_t b0 = 0; b0 < n_pre_u; b0 += kPackChunk) chunks.push_back({b0, std::min(n_pre_u, b0 + kPackChunk)});
+      for (size_t b0 = n_pre_u; b0 < unionable.size(); b0 += kPackChunk)
+        chunks.push_back({b0, std::min(unionable.size(), b0 + kPackChunk)});
+      const size_t nchunks = chunks.size();
       std::vector<std::vector<Group>> packed(nchunks);
       auto pack_chunk = [&](size_t ch) {
         std::string lerr;
         std::vector<Group>& out = packed[ch];
-        const size_t end = std::min(unionable.size(), (ch + 1) * kPackChunk);
-        for (size_t i = ch * kPackChunk; i < end;) {
+        const size_t end = chunks[ch].second;
+        for (size_t i = chunks[ch].first; i < end;) {
           const size_t maxn = std::min<size_t>(64, end - i);
           auto fits = [&](size_t n, Dfa* d) {
             std::vector<const Regex*> rs;
@@ -2220,6 +2235,10 @@ struct Lower {
         uint32_t need = GI_JAMAP_BYTES;
         while (a < autos.size() && pick.size() < GI_JOB_MAX_DFA) {
           const Dfa& d = autos[a].d;
+          // a job holds prefix automata or others, not both (DJob.prefix)
+          if (!pick.empty() && !autos[a].pes.empty() && !autos[pick[0]].pes.empty() &&
+              pe_prefix(*autos[a].pes[0]) != pe_prefix(*autos[pick[0]].pes[0]))
+            break;
           if (!img_ok(d)) {  // no image form: its patterns are always "maybe" (k_eval decides)
             for (const PatEntry* pe : autos[a].pes) P->always_slots.push_back(pe->slot);
             a++;
@@ -3264,6 +3283,39 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
       }
     }
     lap("lower rules");
+    // chains whose evaluation over a body needs the body's phase-A scan (RF2_BODY_PA)
+    for (uint32_t ti : out->top)
+      for (int32_t ci = (int32_t)ti; ci >= 0; ci = out->rules[ci].chain_next) {
+        const DRule& d = out->rules[ci];
+        if (d.op < 0) continue;
+        const uint8_t k = out->ops[d.op].kind;
+        if (k != OP_RX && k != OP_PM && k != OP_CONTAINS && k != OP_CONTAINSWORD && k != OP_DETECT_SQLI &&
+            k != OP_DETECT_XSS)
+          continue;
+        bool body = false;
+        for (uint32_t q = 0; q < d.var_count && !body; q++) {
+          const uint8_t v = out->vars[d.var_begin + q].var;
+          // (REQUEST_BODY: k_body's bits, computed in the gate's first stage)
+          body = v == V_ARGS_POST || v == V_ARGS || v == V_ARGS_POST_NAMES ||
+                 v == V_ARGS_NAMES || v == V_XML || v == V_FILES || v == V_FILES_NAMES || v == V_FILES_SIZES ||
+                 v == V_FILES_TMPNAMES || v == V_MULTIPART_PART_HEADERS;
+        }
+        if (body) {
+          out->rules[ti].flags2 |= RF2_BODY_PA;
+          break;
+        }
+      }
+    // the gate's prefix links: those of the phase-2 rules before the first RF2_BODY_PA rule
+    {
+      for (uint32_t ti : out->top) {
+        if (out->rules[ti].phase != 2) continue;
+        if (out->rules[ti].flags2 & RF2_BODY_PA) {
+          if (timing) fprintf(stderr, "gi_compile: gate prefix ends at rule %d\n", out->rules[ti].id);
+          break;
+        }
+        for (int32_t ci = (int32_t)ti; ci >= 0; ci = out->rules[ci].chain_next) out->rules[ci].flags2 |= RF2_PREFIX;
+      }
+    }
     L.finish_streams();
     lap("scan plan");
     // ctl removal groups: each top-level rule's membership (its tags / msg)
@@ -3290,28 +3342,6 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
           if (out->vars[out->rules[ci].var_begin + q].var == V_MATCHED_VARS ||
               out->vars[out->rules[ci].var_begin + q].var == V_MATCHED_VARS_NAMES)
             out->rules[ti].flags2 |= RF2_MVS;
-    // chains whose evaluation over a body needs the body's phase-A scan (RF2_BODY_PA)
-    for (uint32_t ti : out->top)
-      for (int32_t ci = (int32_t)ti; ci >= 0; ci = out->rules[ci].chain_next) {
-        const DRule& d = out->rules[ci];
-        if (d.op < 0) continue;
-        const uint8_t k = out->ops[d.op].kind;
-        if (k != OP_RX && k != OP_PM && k != OP_CONTAINS && k != OP_CONTAINSWORD && k != OP_DETECT_SQLI &&
-            k != OP_DETECT_XSS)
-          continue;
-        bool body = false;
-        for (uint32_t q = 0; q < d.var_count && !body; q++) {
-          const uint8_t v = out->vars[d.var_begin + q].var;
-          // (REQUEST_BODY: k_body's bits, computed in the gate's first stage)
-          body = v == V_ARGS_POST || v == V_ARGS || v == V_ARGS_POST_NAMES ||
-                 v == V_ARGS_NAMES || v == V_XML || v == V_FILES || v == V_FILES_NAMES || v == V_FILES_SIZES ||
-                 v == V_FILES_TMPNAMES || v == V_MULTIPART_PART_HEADERS;
-        }
-        if (body) {
-          out->rules[ti].flags2 |= RF2_BODY_PA;
-          break;
-        }
-      }
     // the gate's prefix: the links of the phase-2 rules before the first RF2_BODY_PA
     // rule, and every phase-A stream one of them registered a pattern / value test in
     {
@@ -3319,34 +3349,31 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
       for (size_t ri = 0; ri < out->rules.size(); ri++)
         if (out->rules[ri].hit_slot >= 0 && (uint32_t)out->rules[ri].hit_slot < out->n_hit_slots)
           slot_link[out->rules[ri].hit_slot] = (int32_t)ri;
-      for (uint32_t ti : out->top) {
-        if (out->rules[ti].phase != 2) continue;
-        if (out->rules[ti].flags2 & RF2_BODY_PA) {
-          if (timing) fprintf(stderr, "gi_compile: gate prefix ends at rule %d\n", out->rules[ti].id);
-          break;
-        }
-        for (int32_t ci = (int32_t)ti; ci >= 0; ci = out->rules[ci].chain_next) out->rules[ci].flags2 |= RF2_PREFIX;
-      }
       auto prefix_slot = [&](uint32_t sl) {
         return sl < slot_link.size() && slot_link[sl] >= 0 && (out->rules[slot_link[sl]].flags2 & RF2_PREFIX);
       };
+      for (DScanVal& v : out->svals) v.prefix = prefix_slot(v.slot) ? 1 : 0;
+      for (DJob& J : out->jobs) {
+        bool pre = false;
+        for (uint32_t q = 0; q < J.jdfa_count && !pre; q++) {
+          const DJobDfa& jd = out->jdfas[J.jdfa_begin + q];
+          for (uint32_t k = 0; k < jd.n_pat && !pre; k++) pre = prefix_slot(out->pats[jd.pat_begin + k].slot);
+        }
+        J.prefix = pre ? 1 : 0;
+      }
       for (DStream& st : out->streams) {
         bool pre = false;
-        for (uint32_t q = 0; q < st.val_count && !pre; q++) pre = prefix_slot(out->svals[st.val_begin + q].slot);
-        for (uint32_t j = 0; j < st.job_count && !pre; j++) {
-          const DJob& J = out->jobs[st.job_begin + j];
-          for (uint32_t q = 0; q < J.jdfa_count && !pre; q++) {
-            const DJobDfa& jd = out->jdfas[J.jdfa_begin + q];
-            for (uint32_t k = 0; k < jd.n_pat && !pre; k++) pre = prefix_slot(out->pats[jd.pat_begin + k].slot);
-          }
-        }
+        for (uint32_t q = 0; q < st.val_count; q++) pre = pre || out->svals[st.val_begin + q].prefix;
+        for (uint32_t j = 0; j < st.job_count; j++) pre = pre || out->jobs[st.job_begin + j].prefix;
         st.prefix = pre ? 1 : 0;
       }
       if (timing) {
-        uint32_t np = 0, nl = 0;
+        uint32_t np = 0, nl = 0, nj = 0;
         for (const DStream& st : out->streams) np += st.prefix;
+        for (const DJob& J : out->jobs) nj += J.prefix;
         for (const DRule& d : out->rules) nl += (d.flags2 & RF2_PREFIX) ? 1 : 0;
-        fprintf(stderr, "gi_compile: gate prefix: %u links, %u of %zu streams\n", nl, np, out->streams.size());
+        fprintf(stderr, "gi_compile: gate prefix: %u links, %u of %zu streams, %u of %zu jobs\n", nl, np,
+                out->streams.size(), nj, out->jobs.size());
       }
     }
     {  // top-level rules with an observable capture link (capture records, gi_capture)

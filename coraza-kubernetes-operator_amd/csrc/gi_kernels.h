@@ -149,6 +149,7 @@ struct ScanLaunch {
                                      // measured: 32 KB made C3's k_bparse 81 -> 272 ms, the LDS cut its occupancy)
 #define GI_PREFIX_BUDGET 0             // default DBatch.prefix_budget (GI_PREFIX_BUDGET env; round 5: the
                                      // interpreter is ~500 cycles per body byte per automaton link)
+#define GI_GATE_PENDING_MAX 0.5       // the adaptive gate runs while at most this share of body requests stays pending
 #define GI_CHUNK_POOL_WORDS 16e9     // queue-pool words (estimate) one request chunk of a batch may need
 
 // Resident k_scan workgroups (1024 threads) with lds_bytes of dynamic LDS.

@@ -319,7 +319,8 @@ struct DStream {
                       // becomes one byte, GI_RUNE_MARK (rmap_cnt 0: the automata agree on all of
                       // them) or 0x80 + its joint class (rmap triples (lo, hi, byte) in nranges)
   uint8_t det_id;     // index in DProgram.det_streams if some val is @detectSQLi/@detectXSS, else 0xFF
-  uint8_t prefix;     // a RF2_PREFIX link reads it: the gate's first stage scans body fields through it
+  uint8_t prefix;     // some job / value test of it is DJob.prefix / DScanVal.prefix: the gate's first stage
+                      // runs body fields through its chain
   uint32_t rmap_off, rmap_cnt;
   uint32_t _pad2;
 };
@@ -429,7 +430,9 @@ struct DJob {
   uint32_t lds_fmask;              // image offset of the fmask table
   uint8_t lds;                     // 1: all automata in the image; 0: one automaton on global tables
   uint8_t big;                     // image > GI_JOB_LDS_BYTES (big-LDS launch)
-  uint8_t _pad[2];
+  uint8_t prefix;                  // a RF2_PREFIX link's pattern is in it: the gate's first stage runs it over
+                                   // body fields (the body stage the others)
+  uint8_t _pad;
 };
 
 struct DJobDfa {
@@ -453,7 +456,8 @@ struct DPat {
 struct DScanVal {     // @validateByteRange / @validateUrlEncoding / @validateUtf8Encoding / @detectSQLi / @detectXSS
   uint8_t kind;
   uint8_t negate;
-  uint8_t _pad[2];
+  uint8_t prefix;     // a RF2_PREFIX link's value test (as DJob.prefix)
+  uint8_t _pad;
   uint32_t slot;
   uint64_t fmask;     // admitting filters (global filter ids)
   uint32_t bits[8];

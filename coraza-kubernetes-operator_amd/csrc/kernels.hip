@@ -4994,8 +4994,16 @@ GI_HD __forceinline__ void void_request(const DBatch& B, uint32_t r, uint32_t ca
 // qblk entry {pool word offset, nv | nw << 8 | shared}: shared = the block was
 // written for an earlier stream of the same item-wave (raw item bytes)
 #define GI_QB_SHARED 0x80000000u
+#define GI_QB_BODY 0x40000000u  // every value of the block is a body field (the gate: DJob.prefix selects the jobs)
 #define GI_QB_HDR 2  // lane header words of a queue block: global item index, value length
-#define GI_QB_NW_MASK 0x7FFFFFu
+#define GI_QB_NW_MASK 0x3FFFFFu
+// The gate (launch_pipeline): does this stage run a job / value test (its
+// DJob.prefix / DScanVal.prefix) over a body field (body) or a phase-1 item?
+// The first stage runs every one over phase-1 items and the prefix ones over
+// body fields; the body stage (body fields only) the others.
+__device__ __forceinline__ bool stage_runs(const DBatch& B, bool body, uint8_t prefix) {
+  return B.stage == 0 || (B.stage == 1 ? (!body || prefix) : (body && !prefix));
+}
 GI_HD __forceinline__ uint32_t item_bucket(uint32_t n) {
   return n <= 16 ? 0u : n <= 32 ? 1u : n <= 64 ? 2u : n <= 128 ? 3u : 4u;
 }
@@ -5781,10 +5789,10 @@ __device__ void det_push(const DProgram& P, const DBatch& B, bool push, uint32_t
 // else once for this stream's output (*det_append).
 __device__ void stream_vals(const DProgram& P, const DBatch& B, uint32_t r, uint32_t vix, const DStream& S, uint64_t fm,
                             bool maybe, const uint8_t* v, uint32_t n, uint32_t osum, bool raw, uint32_t* rawmask,
-                            bool* det_append) {
+                            bool* det_append, bool body) {
   for (uint32_t q = 0; q < S.val_count; q++) {
     const DScanVal sv = gi_cload(P.svals, S.val_begin + q);  // wave-uniform: scalar loads
-    if (!(fm & sv.fmask)) continue;
+    if (!(fm & sv.fmask) || !stage_runs(B, body, sv.prefix)) continue;
     if (sv.kind == OP_DETECT_SQLI || sv.kind == OP_DETECT_XSS) {
       if (maybe) {
         hit_value(B, sv.slot, r, vix, 1u);
@@ -6005,7 +6013,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
     for (uint32_t s = 0; s < P.n_streams; s++) {
       const uint64_t c_s0 = B.prof ? gi_clock() : 0;
       const DStream S = gi_cload(P.streams, s);
-      const bool skip_s = (B.stage == 1 && body_item && !S.prefix) || (B.stage == 2 && S.prefix);
+      const bool skip_s = B.stage == 1 && body_item && !S.prefix;
       const uint64_t fm0 = skip_s ? 0ull : gm & S.gmask;
       if (is_long && fm0) {
         const uint32_t k = atomicAdd(B.long_count, 1u);
@@ -6041,7 +6049,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
         const uint64_t c_v0 = B.prof ? gi_clock() : 0;
         if (S.val_count)
           stream_vals(P, B, it.req, meta_vix(it.meta), S, fm, maybe, cur, (uint32_t)cn, osum, !maybe && cur == src,
-                      &rawmask, &det_append);
+                      &rawmask, &det_append, body_item);
         if (B.prof) pc_vals += gi_clock() - c_v0;
       }
       const uint64_t c_d0 = B.prof ? gi_clock() : 0;
@@ -6076,7 +6084,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
           e.req = it.req;
           e.stream = s;
           e.fm = fm;
-          e.flags = maybe ? 1u : 0u;
+          e.flags = (maybe ? 1u : 0u) | (body_item ? 2u : 0u);
           e.vix = meta_vix(it.meta);
           e._pad = 0;
           e.off = off;
@@ -6094,6 +6102,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
       }
       const uint32_t nv = __popcll(om);
       const uint32_t nw = wave_max(out ? ((uint32_t)cn + 3) / 4 : 0u);
+      const uint32_t qbody = __ballot(out && !body_item) ? 0u : GI_QB_BODY;  // (a wave may straddle kinds)
       const bool raw = __ballot(out && cur != src) == 0;  // every output is the staged item
       if (raw && (om == rom0 || om == rom1)) {
         if (lane == 0 && blk < B.qcap)
@@ -6120,10 +6129,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
         if (lane == 0 && blk < B.qcap) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2(0u, 0u);
         continue;
       }
-      if (lane == 0) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2((uint32_t)(woff >> 2), nv | (nw << 8));
+      if (lane == 0) B.qblk[(uint64_t)s * B.qcap + blk] = make_uint2((uint32_t)(woff >> 2), nv | (nw << 8) | qbody);
       if (raw) {  // remember it (two most recent lane sets)
         rom1 = rom0, rq1 = rq0, rw1 = rw0;
-        rom0 = om, rq0 = nv | (nw << 8) | GI_QB_SHARED, rw0 = (uint32_t)(woff >> 2);
+        rom0 = om, rq0 = nv | (nw << 8) | GI_QB_SHARED | qbody, rw0 = (uint32_t)(woff >> 2);
       }
       if (out) {
         const uint32_t i = mask_rank(om);
@@ -6450,6 +6459,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GI_SC
     const uint32_t e = chunk * per_unit + wv * 64 + lane;
     uint2 mine = make_uint2(0u, 0u);
     if (e < n_iw) mine = B.qblk[(uint64_t)J.stream * B.qcap + e];
+    if (!stage_runs(B, (mine.y & GI_QB_BODY) != 0, J.prefix)) mine.y = 0;
     const uint64_t live = __ballot((mine.y & 0xFFu) != 0);
     if (lane == 0) wcnt[wv] = __popcll(live);
     __syncthreads();
@@ -6834,6 +6844,8 @@ __global__ void __launch_bounds__(64) k_long(DProgram P, DBatch B) {
     const DStream S = P.streams[ent.y];
     const uint64_t fm = B.igm[ent.x] & S.gmask;
     const uint32_t r = it.req, vix = meta_vix(it.meta);
+    const uint32_t ik = item_kind(it);
+    const bool body = ik == FK_ARG_POST || (ik >= FK_FILE && ik <= FK_FILE_SIZE);
     uint32_t summ;
     {
       uint32_t a, b;
@@ -6848,7 +6860,7 @@ __global__ void __launch_bounds__(64) k_long(DProgram P, DBatch B) {
     // validate / detect operators of the stream
     for (uint32_t q = 0; q < S.val_count; q++) {
       const DScanVal sv = P.svals[S.val_begin + q];
-      if (!(fm & sv.fmask)) continue;
+      if (!(fm & sv.fmask) || !stage_runs(B, body, sv.prefix)) continue;
       bool hit = true;
       if (ok) {
         bool res;
@@ -6873,6 +6885,7 @@ __global__ void __launch_bounds__(64) k_long(DProgram P, DBatch B) {
     uint32_t pair = 0;
     for (uint32_t j = 0; j < S.job_count; j++) {
       const DJob J = P.jobs[S.job_begin + j];
+      if (!stage_runs(B, body, J.prefix)) continue;
       for (uint32_t q = 0; q < J.jdfa_count; q++, pair++) {
         if ((pair & 63u) != L) continue;
         const DJobDfa jd = P.jdfas[J.jdfa_begin + q];
@@ -6936,7 +6949,8 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
       const uint64_t fm = x.gm & S.gmask;
       for (uint32_t q = 0; q < S.val_count; q++) {
         const DScanVal sv = P.svals[S.val_begin + q];
-        if (!(fm & sv.fmask)) continue;
+        // (the body stage's entries are body fields: the prefix tests ran in the first stage)
+        if (!(fm & sv.fmask) || (B.stage == 2 && sv.prefix)) continue;
         bool res;
         if (sv.kind == OP_DETECT_SQLI) {
           // (k_stream listed the value for some val of the masked streams: the
@@ -6978,7 +6992,8 @@ __global__ void __launch_bounds__(256) k_scan_slow(DProgram P, DBatch B) {
     GI_BOUND(x.req < B.n_req && x.stream < P.n_streams && x.off + x.len <= B.slow_bytes_cap, x.req, x.stream);
     const DStream S = P.streams[x.stream];
     for (uint32_t j = S.job_begin; j < S.job_begin + S.job_count; j++)
-      scan_value_global(P, B, x.req, x.vix, P.jobs[j], x.fm, (x.flags & 1) != 0, B.slow_bytes + x.off, x.len);
+      if (stage_runs(B, (x.flags & 2) != 0, P.jobs[j].prefix))
+        scan_value_global(P, B, x.req, x.vix, P.jobs[j], x.fm, (x.flags & 1) != 0, B.slow_bytes + x.off, x.len);
   }
 }
 

@@ -96,6 +96,14 @@ struct gi_ctx {
   DevBuf pend, plist;  // phase-1 gate (launch_pipeline): pending flags + list
   uint32_t long_cap = 0, long_grid = GI_LONG_GRID;
   uint32_t wave_fields = GI_EVAL_WAVE_FIELDS, wave_rules = GI_EVAL_WAVE_RULES;  // k_eval_wave thresholds
+  // The phase gate (kernels.hip launch_pipeline) pays off when its first stage
+  // decides many of the requests with a body; when most stay pending (the body
+  // stage scans and evaluates them anyway) it costs a second evaluation.  The
+  // context tracks the pending share of its gated batches and runs ungated
+  // while it stays above GI_GATE_PENDING_MAX, re-probing every 16th batch.
+  // Results do not depend on the choice (both forms are exact).
+  double gate_pending_share = -1.0;  // last gated batch (-1: none yet)
+  bool gate_ran = false;             // the batch in flight ran gated
   // A staged batch runs as consecutive request chunks, each a full pipeline
   // pass over its requests, so the phase-A buffers (items, queue pool, detect
   // / slow / long lists) are sized for one chunk, not for the whole batch.
@@ -1213,9 +1221,13 @@ int gi_run_staged(gi_ctx* c) {
     B.wave_rules = c->wave_rules;
     B.rstride = c->n_req;
     // the phase-1 gate (GI_GATE=0: one pass, bodies parsed before phase 1)
-    static const bool gate_env = !(getenv("GI_GATE") && atoi(getenv("GI_GATE")) == 0);
+    // GI_GATE: 0 off, 1 always, unset adaptive (gi_ctx::gate_pending_share)
+    static const int gate_env = getenv("GI_GATE") ? atoi(getenv("GI_GATE")) : -1;
+    const bool adaptive_on = c->gate_pending_share < 0 || c->gate_pending_share <= GI_GATE_PENDING_MAX ||
+                             c->stats.batches % 16 == 0;
     B.stage = 0;
-    B.gate = gate_env ? 1u : 0u;
+    B.gate = (gate_env == 1 || (gate_env < 0 && adaptive_on)) ? 1u : 0u;
+    c->gate_ran = B.gate != 0;
     B.pend = (uint8_t*)c->pend.p;
     B.plist = (uint32_t*)c->plist.p;
     B.pcount = (uint32_t*)(cp + 512);
@@ -1247,6 +1259,7 @@ int gi_run_staged(gi_ctx* c) {
   c->log.n = 0;
   (void)hipEventRecord(c->log.ev[0], c->stream);
   c->stats.gate_requests = 0;
+  c->stats.gate_pending = 0;
   for (size_t k = 0; k < c->chunks.size(); k++) {
     const gi_ctx::Chunk& ch = c->chunks[k];
     if (B.gate && ch.n_body && c->prog.body_access) c->stats.gate_requests += ch.n_body;
@@ -1307,6 +1320,8 @@ int gi_sync(gi_ctx* c) {
     uint32_t gate_pending = 0;  // DBatch.pcount[1] (kernels.hip eval_request)
     if (c->ctr.p) (void)hipMemcpy(&gate_pending, (uint8_t*)c->ctr.p + 516, 4, hipMemcpyDeviceToHost);
     c->stats.gate_pending = c->stats.gate_requests ? gate_pending : 0;
+    if (c->gate_ran && c->stats.gate_requests)
+      c->gate_pending_share = (double)c->stats.gate_pending / (double)c->stats.gate_requests;
     // one record per launch name: a chunked batch repeats the pipeline, its
     // launches of one name are summed
     uint32_t nrec = 0;
