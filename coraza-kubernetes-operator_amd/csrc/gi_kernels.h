@@ -119,6 +119,12 @@ struct DBatch {
   uint32_t* plist;            // the pending requests (stage-1 k_eval appends), *pcount of them
   uint32_t* pcount;
   uint32_t prefix_budget;     // RF2_BODY_PA rules a first-stage request evaluates over its unscanned body
+  // k_detect's memo of libinjection results by value (kernels.hip det_memo):
+  // the same header / cookie value recurs across requests (User-Agent,
+  // Referer); open addressing on a 64-bit hash, entries verified byte for byte
+  unsigned long long* dmemo_keys;  // [dmemo_mask + 1] (0: empty); nullptr: no memo
+  uint4* dmemo_info;               // per entry: canonical copy offset (lo, hi) in det_bytes, length, state bits
+  uint32_t dmemo_mask;
 };
 
 // k_scan launch plan: job lists for the small-LDS and big-LDS launches.

@@ -6907,6 +6907,99 @@ __global__ void __launch_bounds__(64) k_long(DProgram P, DBatch B) {
 // @detectSQLi / @detectXSS candidates, one lane per entry: libinjection with
 // the tokenizer state in LDS; each detector runs at most once per entry and
 // its result serves every admitting val of the masked streams.
+// k_detect's cross-request memo of detector results (DBatch.dmemo_*): the
+// detectors are pure functions of the value's bytes, and many candidates
+// repeat across the requests of a batch (the same User-Agent or Referer
+// string).  A thread claims an empty slot for its value's 64-bit hash, records
+// where the value's bytes are (its det_bytes copy) and publishes each result
+// as it computes it; a thread that finds the hash reuses a published result
+// only after comparing the bytes with that copy (exact, whatever the hash),
+// and otherwise computes the value itself.  Nobody waits on anybody.
+#define GI_DM_VALID 1u
+#define GI_DM_SQ_KNOWN 2u
+#define GI_DM_SQ 4u
+#define GI_DM_XS_KNOWN 8u
+#define GI_DM_XS 16u
+#define GI_DM_PROBES 16
+__device__ __forceinline__ unsigned long long dm_hash(const uint8_t* v, uint32_t n) {
+  unsigned long long h = 1469598103934665603ull ^ n;
+  for (uint32_t i = 0; i < n; i++) h = (h ^ v[i]) * 1099511628211ull;
+  return h | 1ull;  // never 0 (the empty key)
+}
+__device__ __forceinline__ bool dm_same(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+// Results of the detectors the entry needs (bit 0 SQLi, bit 1 XSS).
+__device__ uint32_t det_results(const DBatch& B, const uint8_t* v, uint32_t n, uint64_t off, bool need_s, bool need_x,
+                                LiSqli* st, const LiTables& T, uint64_t* dsteps) {
+  auto compute = [&](bool s) -> bool {
+    if (!li_candidate(s, v, n)) return false;
+    *dsteps += n;
+    return s ? li_detect_sqli(v, n, st, T) : li_detect_xss(v, n);
+  };
+  uint32_t out = 0;
+  if (!B.dmemo_keys) {
+    if (need_s && compute(true)) out |= 1u;
+    if (need_x && compute(false)) out |= 2u;
+    return out;
+  }
+  const unsigned long long h = dm_hash(v, n);
+  int32_t slot = -1;
+  uint32_t state = 0;
+  for (uint32_t p = 0; p < GI_DM_PROBES; p++) {
+    const uint32_t i = (uint32_t)(h + p) & B.dmemo_mask;
+    unsigned long long k = __atomic_load_n(&B.dmemo_keys[i], __ATOMIC_RELAXED);
+    if (k == 0) {
+      k = atomicCAS(&B.dmemo_keys[i], 0ull, h);
+      if (k == 0) {  // claimed: record the canonical copy, then the results as they come
+        B.dmemo_info[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32), n, 0u);
+        __threadfence();
+        atomicOr(&B.dmemo_info[i].w, GI_DM_VALID);
+        slot = (int32_t)i;
+        state = GI_DM_VALID;
+        break;
+      }
+    }
+    if (k == h) {
+      const uint32_t w = __atomic_load_n(&B.dmemo_info[i].w, __ATOMIC_ACQUIRE);
+      if (w & GI_DM_VALID) {
+        const uint4 inf = B.dmemo_info[i];
+        const uint64_t coff = (uint64_t)inf.x | ((uint64_t)inf.y << 32);
+        if (inf.z == n && coff + n <= B.det_bytes_cap && dm_same(v, B.det_bytes + coff, n)) {
+          slot = (int32_t)i;
+          state = w;
+        }
+      }
+      break;  // (another value with this hash, or not published yet: compute alone)
+    }
+  }
+  uint32_t pub = 0;
+  if (need_s) {
+    bool r;
+    if (state & GI_DM_SQ_KNOWN) {
+      r = (state & GI_DM_SQ) != 0;
+    } else {
+      r = compute(true);
+      pub |= GI_DM_SQ_KNOWN | (r ? GI_DM_SQ : 0u);
+    }
+    out |= r ? 1u : 0u;
+  }
+  if (need_x) {
+    bool r;
+    if (state & GI_DM_XS_KNOWN) {
+      r = (state & GI_DM_XS) != 0;
+    } else {
+      r = compute(false);
+      pub |= GI_DM_XS_KNOWN | (r ? GI_DM_XS : 0u);
+    }
+    out |= r ? 2u : 0u;
+  }
+  if (slot >= 0 && pub) atomicOr(&B.dmemo_info[slot].w, pub);
+  return out;
+}
+
 __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
   __shared__ LiSqli st[256];
   // the keyword tables in LDS: every word lookup is a hash probe + compare
@@ -6942,7 +7035,9 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
       }
       v = (const uint8_t*)dst;
     }
-    int sq = -1, xs = -1;
+    // which detectors the entry's admitting value tests need, then their
+    // results (memoised across the batch), then the hit bits
+    bool need_s = false, need_x = false;
     for (uint32_t d = 0; d < P.n_det_streams; d++) {
       if (!((x.mask >> d) & 1u)) continue;
       const DStream S = P.streams[P.det_streams[d]];
@@ -6951,30 +7046,20 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
         const DScanVal sv = P.svals[S.val_begin + q];
         // (the body stage's entries are body fields: the prefix tests ran in the first stage)
         if (!(fm & sv.fmask) || (B.stage == 2 && sv.prefix)) continue;
-        bool res;
-        if (sv.kind == OP_DETECT_SQLI) {
-          // (k_stream listed the value for some val of the masked streams: the
-          // other kind's prefilter may still settle it)
-          if (sq < 0) {
-            sq = 0;
-            if (li_candidate(true, v, x.len)) {
-              dsteps += x.len;
-              sq = li_detect_sqli(v, x.len, &st[threadIdx.x], T) ? 1 : 0;
-            }
-          }
-          res = sq != 0;
-        } else if (sv.kind == OP_DETECT_XSS) {
-          if (xs < 0) {
-            xs = 0;
-            if (li_candidate(false, v, x.len)) {
-              dsteps += x.len;
-              xs = li_detect_xss(v, x.len) ? 1 : 0;
-            }
-          }
-          res = xs != 0;
-        } else {
-          continue;
-        }
+        need_s = need_s || sv.kind == OP_DETECT_SQLI;
+        need_x = need_x || sv.kind == OP_DETECT_XSS;
+      }
+    }
+    const uint32_t res2 = det_results(B, v, x.len, x.off, need_s, need_x, &st[threadIdx.x], T, &dsteps);
+    for (uint32_t d = 0; d < P.n_det_streams; d++) {
+      if (!((x.mask >> d) & 1u)) continue;
+      const DStream S = P.streams[P.det_streams[d]];
+      const uint64_t fm = x.gm & S.gmask;
+      for (uint32_t q = 0; q < S.val_count; q++) {
+        const DScanVal sv = P.svals[S.val_begin + q];
+        if (!(fm & sv.fmask) || (B.stage == 2 && sv.prefix)) continue;
+        if (sv.kind != OP_DETECT_SQLI && sv.kind != OP_DETECT_XSS) continue;
+        const bool res = (res2 >> (sv.kind == OP_DETECT_SQLI ? 0 : 1)) & 1u;
         if (res != (sv.negate != 0)) hit_value(B, sv.slot, x.req, x.vix);
       }
     }
@@ -7551,7 +7636,10 @@ static void launch_phase_a(const DProgram& P, const DBatch& B, const ScanLaunch&
   GI_LAUNCH(s2 ? "k_stream2.2" : "k_stream2", (k_stream<64, 68, 1>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 2u);
   GI_LAUNCH(s2 ? "k_stream3.2" : "k_stream3", (k_stream<128, 132, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
   GI_LAUNCH(s2 ? "k_stream4.2" : "k_stream4", (k_stream<0, 0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
-  if (P.n_det_streams) GI_LAUNCH(s2 ? "k_detect.2" : "k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
+  if (P.n_det_streams) {
+    if (B.dmemo_keys) (void)hipMemsetAsync(B.dmemo_keys, 0, 8ull * (B.dmemo_mask + 1), stream);  // the det arena restarts
+    GI_LAUNCH(s2 ? "k_detect.2" : "k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
+  }
   if (B.long_cap) GI_LAUNCH(s2 ? "k_long.2" : "k_long", k_long, dim3(B.long_grid), dim3(64), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[1], stream);
   for (int big = 0; big < 2; big++)

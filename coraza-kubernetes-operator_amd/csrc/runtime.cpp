@@ -94,6 +94,8 @@ struct gi_ctx {
   // phase A
   DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf, wlist;
   DevBuf pend, plist;  // phase-1 gate (launch_pipeline): pending flags + list
+  DevBuf dmemo_keys, dmemo_info;  // k_detect's detector-result memo
+  uint32_t dmemo_mask = 0;
   uint32_t long_cap = 0, long_grid = GI_LONG_GRID;
   uint32_t wave_fields = GI_EVAL_WAVE_FIELDS, wave_rules = GI_EVAL_WAVE_RULES;  // k_eval_wave thresholds
   // The phase gate (kernels.hip launch_pipeline) pays off when its first stage
@@ -641,7 +643,7 @@ void gi_ctx_free(gi_ctx* c) {
   c->prof.release();
   for (DevBuf* b : {&c->caprec, &c->capbytes, &c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->hset, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
-                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist, &c->pend, &c->plist,
+                    &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist, &c->pend, &c->plist, &c->dmemo_keys, &c->dmemo_info,
                     &c->cappool, &c->progdev})
     b->release();
   for (auto& ev : c->evs)
@@ -1093,6 +1095,16 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     c->det_cap = c->prog.n_det_streams ? (uint32_t)det_max : 0;
     c->det_bytes_cap = c->prog.n_det_streams ? detb_max : 0;
     if ((e = c->det.ensure(std::max<uint64_t>(32ull * c->det_cap, 64))) != hipSuccess) return hip_fail(c, e, "alloc detect list");
+    // detector memo: a power of two >= 2 x the candidates (at most 2^25 slots, 24 B each)
+    c->dmemo_mask = 0;
+    static const bool memo_env = !(getenv("GI_DET_MEMO") && atoi(getenv("GI_DET_MEMO")) == 0);
+    if (c->det_cap && memo_env) {
+      uint64_t cap = 1024;
+      while (cap < 2ull * c->det_cap && cap < (1ull << 25)) cap <<= 1;
+      if ((e = c->dmemo_keys.ensure(8 * cap)) != hipSuccess) return hip_fail(c, e, "alloc detect memo");
+      if ((e = c->dmemo_info.ensure(16 * cap)) != hipSuccess) return hip_fail(c, e, "alloc detect memo");
+      c->dmemo_mask = (uint32_t)(cap - 1);
+    }
     if ((e = c->det_bytes.ensure(c->det_bytes_cap + 16)) != hipSuccess) return hip_fail(c, e, "alloc detect bytes");
   }
   // k_eval -> k_eval_wave request list (its counter lives in ctr)
@@ -1204,6 +1216,9 @@ int gi_run_staged(gi_ctx* c) {
     B.det_bytes = (uint8_t*)c->det_bytes.p;
     B.det_bytes_cap = c->det_bytes_cap;
     B.det_used = (unsigned long long*)(cp + 32);
+    B.dmemo_keys = c->dmemo_mask ? (unsigned long long*)c->dmemo_keys.p : nullptr;
+    B.dmemo_info = c->dmemo_mask ? (uint4*)c->dmemo_info.p : nullptr;
+    B.dmemo_mask = c->dmemo_mask;
     B.diag = nullptr;
     B.prof = nullptr;
     if (c->prof_on && c->prof.ensure(1024 + 8000) == hipSuccess) {
