@@ -235,7 +235,7 @@ GI_HD __forceinline__ uint32_t go_itoa(int64_t v, uint8_t* buf) {
 }
 
 // utf8.DecodeRune
-GI_HD inline uint32_t decode_rune(const uint8_t* b, uint32_t n, uint32_t i, uint32_t* w) {
+GI_HD __forceinline__ uint32_t decode_rune(const uint8_t* b, uint32_t n, uint32_t i, uint32_t* w) {
   uint8_t c0 = b[i];
   if (c0 < 0x80) {
     *w = 1;
@@ -264,7 +264,7 @@ GI_HD inline uint32_t decode_rune(const uint8_t* b, uint32_t n, uint32_t i, uint
   return ((c0 & 0x07) << 18) | ((c1 & 0x3F) << 12) | ((b[i + 2] & 0x3F) << 6) | (b[i + 3] & 0x3F);
 }
 
-GI_HD inline uint32_t encode_rune(uint32_t r, uint8_t* o) {
+GI_HD __forceinline__ uint32_t encode_rune(uint32_t r, uint8_t* o) {
   if (r < 0x80) { o[0] = (uint8_t)r; return 1; }
   if (r < 0x800) { o[0] = 0xC0 | (r >> 6); o[1] = 0x80 | (r & 0x3F); return 2; }
   if (r < 0x10000) {
@@ -1226,6 +1226,28 @@ GI_HD __forceinline__ int64_t apply_transform_inl(const DProgram& P, uint8_t cod
     case T_NORMALIZEPATHWIN: return t_normpath(true, s, n, d, cap);
     case T_JSDECODE: return t_jsdecode(s, n, d, cap);
     default: return code >= T_BASE64DECODE ? t_ext(code, s, n, d, cap) : t_simple(code, s, n, d, cap);
+  }
+}
+
+// The chunkable transformations (t_chunkable) with every callee inlined, for
+// k_body's LDS tiles: a buffer access through a generic pointer in an
+// out-of-line callee becomes a FLAT op, and the compiler merges adjacent byte
+// stores into misaligned wider ones -- which fault on an LDS address.  Inlined
+// into the tile loop, the accesses are ds_* ops.
+GI_HD __forceinline__ int64_t apply_transform_tile(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n,
+                                                   uint8_t* d, uint32_t cap) {
+  switch (code) {
+    case T_UTF8TOUNICODE: [[clang::always_inline]] return t_utf8tounicode(s, n, d, cap);
+    case T_LOWERCASE: [[clang::always_inline]] return t_lowercase(P, s, n, d, cap);
+    case T_URLDECODE: [[clang::always_inline]] return t_urldecode(s, n, d, cap);
+    case T_URLDECODEUNI: [[clang::always_inline]] return t_urldecodeuni(s, n, d, cap);
+    case T_HTMLENTITYDECODE: [[clang::always_inline]] return t_htmlentitydecode(s, n, d, cap);
+    case T_JSDECODE: [[clang::always_inline]] return t_jsdecode(s, n, d, cap);
+    case T_CSSDECODE: [[clang::always_inline]] return t_cssdecode(s, n, d, cap);
+    case T_URLENCODE: [[clang::always_inline]] return t_urlencode(s, n, d, cap);
+    case T_HEXENCODE: [[clang::always_inline]] return t_hexencode(s, n, d, cap);
+    case T_BASE64ENCODE: [[clang::always_inline]] return t_b64encode(s, n, d, cap);
+    default: [[clang::always_inline]] return t_simple(code, s, n, d, cap);  // removeNulls, replaceNulls, (compress|remove)Whitespace, cmdLine
   }
 }
 
@@ -6555,7 +6577,7 @@ __device__ __forceinline__ bool no_byte_before(const uint8_t* s, uint32_t p, uin
 // Is position p (0 < p < n) of s a sync point of transformation `code`?
 // (the sequential state at p is initial, and no escape sequence starting
 // before p reads s[p]: see the transformation's code above)
-__device__ bool t_sync(uint8_t code, const uint8_t* s, uint32_t p) {
+__device__ __forceinline__ bool t_sync(uint8_t code, const uint8_t* s, uint32_t p) {
   const uint8_t c = s[p - 1];
   switch (code) {
     case T_LOWERCASE: case T_UTF8TOUNICODE: return s[p] < 0x80;  // a rune start (ASCII never continues one)
@@ -6688,12 +6710,104 @@ __device__ bool wave_validate(const DOp& o, const uint8_t* s, uint32_t n) {
   return __ballot(r) != 0;
 }
 
+// Chunkable transformation `code` of src[0, n) into dst (cap bytes, never
+// src) by the whole wave, through LDS tiles of GI_TT_IN input bytes: the tile
+// is read coalesced into LDS, each lane transforms the chunk between its sync
+// points (t_sync) LDS -> LDS, and the compacted output is written coalesced.
+// A lane streaming its own chunk straight from HBM touches one cache line per
+// lane per byte, and 64 lanes x 8+ waves of such streams thrash the CU's L1
+// (k_body spent ~1.6 ms per 23 KB body on a 3-transform chain that way).
+// A tile that is not the last ends at the last lane's sync point (that
+// lane's chunk starts the next tile), so every chunk lies between two sync
+// points exactly as in the one-shot split; sync points are tested on
+// tile-relative positions, which is exact because the tile start is itself
+// a sync point of the same rule (no escape byte within the look-back window
+// before it; base64Encode's p % 3 holds since the start is 0 mod 3).  A tile
+// without an inner sync point is done by lane 0 from HBM up to the next one.
+// Returns the output length, -1 on overflow; *psumm = byte summary of it.
+#define GI_TT_IN 3072
+#define GI_TT_LDS (GI_TT_IN + 3 * GI_TT_IN + 8 * 64 + 2 * 65 * 4)
+static_assert(GI_TT_LDS <= 16384, "k_body's LDS slot holds the transformation tiles");
+__device__ __forceinline__ int64_t wave_transform_lds(const DProgram& P, uint8_t code, const uint8_t* src, uint32_t n, uint8_t* dst,
+                                      uint64_t cap, uint8_t* lds, uint32_t* psumm) {
+  const uint32_t L = lane_id();
+  uint8_t* in = lds;
+  uint8_t* out = lds + GI_TT_IN;  // lane slots at 3 * a + 8 * L (3x + 8 bytes each, as apply_transform allows)
+  uint32_t* offs = (uint32_t*)(out + 3 * GI_TT_IN + 8 * 64);  // [65] output offsets
+  uint32_t* slot = offs + 65;                                  // [64] slot starts
+  uint64_t o = 0;
+  uint32_t summ = 0;
+  uint32_t base = 0;
+  while (base < n) {
+    const uint32_t tn = min(n - base, (uint32_t)GI_TT_IN);
+    const bool last = base + tn == n;
+    __syncthreads();  // the previous tile's LDS reads are done
+    for (uint32_t k = L; k < tn; k += 64) in[k] = src[base + k];
+    __syncthreads();
+    uint32_t a, e;
+    wave_chunks(tn, [&](uint32_t p) { return t_sync(code, in, p); }, &a, &e);
+    bool act = a != 0xFFFFFFFFu && e > a;
+    uint32_t adv = tn;
+    if (!last) {  // the last lane with a sync point carries its chunk to the next tile
+      const uint64_t v = __ballot(a != 0xFFFFFFFFu);
+      const int hi = 63 - __builtin_clzll((unsigned long long)v);
+      if (hi == 0) {  // no sync point inside the tile: lane 0 runs to the next one, from HBM
+        int64_t m = 0;
+        uint32_t sm = 0, stop = n;
+        if (L == 0) {
+          for (uint32_t p = base + tn; p < n; p++)
+            if (t_sync(code, src + base, p - base)) {
+              stop = p;
+              break;
+            }
+          m = apply_transform(P, code, src + base, stop - base, dst + o, (uint32_t)min(cap - o, (uint64_t)0xFFFFFFFFu));
+          if (m > 0) sm = value_summary(dst + o, (uint32_t)m);
+        }
+        m = __shfl(m, 0, 64);
+        if (m < 0) return -1;
+        summ |= sm;
+        o += (uint64_t)m;
+        base = __shfl(stop, 0, 64);
+        continue;
+      }
+      adv = __shfl(a, hi, 64);
+      if ((int)L == hi) act = false;
+    }
+    int64_t m = act ? apply_transform_tile(P, code, in + a, e - a, out + 3u * a + 8u * L, 3 * (e - a) + 8) : 0;
+    if (__ballot(m < 0) != 0) return -1;
+    uint32_t tot = 0;
+    const uint32_t o0 = wave_excl_sum((uint32_t)m, &tot);
+    if (o + tot > cap) return -1;
+    const uint32_t st = act ? 3u * a + 8u * L : 0u;
+    for (uint32_t i = 0; i < (uint32_t)max(m, (int64_t)0); i++) summ |= byte_summary(out[st + i]);
+    offs[L] = o0;
+    slot[L] = st;
+    if (L == 0) offs[64] = tot;
+    __syncthreads();
+    uint32_t k = 0;
+    for (uint32_t j = L; j < tot; j += 64) {
+      while (k < 63 && offs[k + 1] <= j) k++;
+      dst[o + j] = out[slot[k] + (j - offs[k])];
+    }
+    o += tot;
+    base += adv;
+  }
+  for (int x = 32; x > 0; x >>= 1) summ |= (uint32_t)__shfl_xor((int)summ, x, 64);
+  *psumm = summ;
+  return (int64_t)o;
+}
+
 // One wave runs transformation chain (off, len) over v[0, *cn): chunk-parallel
 // for the chunkable transformations (t_sync boundaries), lane 0 otherwise.
 // t0 / t1 are the two cap-byte buffers; *cur / *cn are the input on entry
 // and the output on return; false on overflow.  summ = byte summary of v.
-__device__ bool wave_run_chain(const DProgram& P, uint32_t off, uint32_t len, const uint8_t* src0, uint8_t* t0,
-                               uint8_t* t1, uint64_t cap, uint32_t summ, const uint8_t** pcur, uint32_t* pcn) {
+// tiles: the chunkable ones run LDS-tiled in lds (GI_TT_LDS bytes of the
+// workgroup's LDS; inlined, so every tile access is a ds_* op -- a generic
+// pointer would let the compiler merge byte stores into misaligned wider
+// flat stores, which fault on an LDS address).
+__device__ __forceinline__ bool wave_run_chain(const DProgram& P, uint32_t off, uint32_t len, const uint8_t* src0, uint8_t* t0,
+                               uint8_t* t1, uint64_t cap, uint32_t summ, const uint8_t** pcur, uint32_t* pcn,
+                               uint8_t* lds = nullptr, bool tiles = false) {
   const uint32_t L = threadIdx.x;
   const uint8_t* cur = *pcur;
   uint32_t cn = *pcn;
@@ -6701,6 +6815,19 @@ __device__ bool wave_run_chain(const DProgram& P, uint32_t off, uint32_t len, co
   for (uint32_t q = 0; q < len && ok; q++) {
     const uint8_t code = (uint8_t)P.tchains[off + q];
     if (transform_identity(summ, code)) continue;
+    if (tiles && t_chunkable(code)) {
+      uint8_t* dst = cur == t0 ? t1 : t0;
+      uint32_t sm = 0;
+      const int64_t m = wave_transform_lds(P, code, cur, cn, dst, cap, lds, &sm);
+      if (m < 0) {
+        ok = false;
+      } else {
+        cur = dst;
+        cn = (uint32_t)m;
+        summ = sm;
+      }
+      continue;
+    }
     // buffers: tmp / dst are the two transformation buffers other than cur
     uint8_t* tmp = cur == t1 ? t0 : t1;
     uint8_t* dst = cur == src0 ? t0 : (uint8_t*)cur;
@@ -6749,7 +6876,10 @@ __device__ bool wave_run_chain(const DProgram& P, uint32_t off, uint32_t len, co
   return ok;
 }
 
-__global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
+// Two waves per SIMD (the inlined LDS tile path would otherwise take the
+// whole register file: 1 wave, k_body 68 -> 83 ms on C3 at 50k; with the cap,
+// 17 spilled VGPRs and 46 ms).
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8))) k_body(DProgram P, DBatch B) {
   __shared__ __attribute__((aligned(16))) uint8_t kb_lds[GI_BODY_LDS];
   const uint32_t L = threadIdx.x;
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
@@ -6787,7 +6917,7 @@ __global__ void __launch_bounds__(64) k_body(DProgram P, DBatch B) {
           for (int q = 32; q > 0; q >>= 1) m |= (uint32_t)__shfl_xor((int)m, q, 64);
           summ = m;
         }
-        ok = wave_run_chain(P, R.tchain_off, R.tchain_len, body, g.t0, g.t1, g.cap_t, summ, &cur, &cn);
+        ok = wave_run_chain(P, R.tchain_off, R.tchain_len, body, g.t0, g.t1, g.cap_t, summ, &cur, &cn, kb_lds, B.body_tiles != 0);
       }
       const uint64_t c1 = B.prof ? gi_clock() : 0;
       bool hit;

@@ -1150,7 +1150,7 @@ int gi_run_staged(gi_ctx* c) {
   if (e == hipSuccess)
     e = hipMemsetAsync(c->tally_ext.p, 0, 4ull * (GI_SCORE_BINS + c->tally_ids.size()), c->stream);
   if (e != hipSuccess) return hip_fail(c, e, "memset tally");
-  DBatch B;
+  DBatch B{};
   B.data = (const uint8_t*)c->data.p;
   B.reqs = (const gi_request*)c->reqs.p;
   B.headers = (const gi_header*)c->hdrs.p;
@@ -1249,6 +1249,8 @@ int gi_run_staged(gi_ctx* c) {
     static const uint32_t budget_env =
         getenv("GI_PREFIX_BUDGET") ? (uint32_t)atoi(getenv("GI_PREFIX_BUDGET")) : GI_PREFIX_BUDGET;
     B.prefix_budget = budget_env;
+    static const uint32_t tiles_env = getenv("GI_BODY_TILES") ? (uint32_t)atoi(getenv("GI_BODY_TILES")) : 1u;
+    B.body_tiles = tiles_env;
     B.bparse_lds = (uint32_t)std::min<uint64_t>(c->bparse_lds, (c->max_body + 15) & ~15ull);
   }
   (void)hipEventRecord(c->ev0, c->stream);

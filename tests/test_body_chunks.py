@@ -72,6 +72,14 @@ def bodies(n, seed=7):
     return out
 
 
+def tile_edge_bodies():
+    """Stretches longer than k_body's 3 KB LDS tile without a sync point of
+    some transformation (lane 0 then runs to the next one), and sequences
+    straddling the tile boundaries."""
+    return [b"k" * 7000 + b"&lt;script", b"%" * 7000 + b"3cscript", b"\\" * 5001 + b"u003cscript",
+            b"ab%u003c" * 1500, b"&#x3c;script " * 900, (b"%u003c" + b"k" * 3066) * 3 + b"script"]
+
+
 def batch_of(bs):
     txs = []
     for b in bs:
@@ -88,9 +96,7 @@ def test_oracle_rules_parse():
     gpuinspect.Ruleset(RULES)
 
 
-@pytest.mark.gpu
-def test_gpu_body_chunks_parity():
-    bs = bodies(500)
+def _parity(bs):
     batch = batch_of(bs)
     rs = gpuinspect.Ruleset(RULES)
     res = gpuinspect.Engine(rs).inspect(batch)
@@ -98,6 +104,17 @@ def test_gpu_body_chunks_parity():
     verdicts = compare.oracle_verdicts(cfg, batch, rs.exports)
     bad = compare.compare(res, verdicts)
     assert not bad, bad[:5]
+    return verdicts
+
+
+@pytest.mark.gpu
+def test_gpu_body_chunks_tile_edges():
+    _parity(tile_edge_bodies() + bodies(8, seed=3))
+
+
+@pytest.mark.gpu
+def test_gpu_body_chunks_parity():
+    verdicts = _parity(bodies(500))
     # the rules do fire (the test is not vacuous)
     fired = {}
     for v in verdicts.values():
