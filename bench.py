@@ -66,6 +66,9 @@ CONFIGS = {
            "CRS-shaped v4 PL4 (blocking paranoia 4: +35 PL2-4 rules, @detectSQLi/@detectXSS) x C3 mix "
            "(50% POST 4-64 KB urlencoded/JSON), 200k requests per GPU per batch; SURVEY C4 = 10M across 8 GPUs "
            "= this batch per GPU, repeated"),
+    "c2x": ("rulesets/crs_pl1_rxstress.conf", 1_000_000, 0.0,
+            "C2 traffic x the PL1 stand-in + 20 CRS-scale assembled regexes of 2-6 KB (tools/gen_rxstress.py; "
+            "two past the DFA state cap, run as NFA position tables): the regex-stress line"),
     "c5": (None, 32, 1.0,
            "generated 10k @rx rules + 100k-phrase @pmFromFile (traffic.c5_ruleset) x ~1 MB multipart bodies "
            "(traffic.c5_batch)"),
@@ -356,7 +359,8 @@ def main():
                            "hbm_bytes_per_launch": {k: v["hbm_bytes_per_launch"] for k, v in kt.items()}}
     steps_s = launch_steps.get(dom, 0) / (avg_launch[dom] * 1e-3)
     metric_set = {"c1": "config/samples RuleSet", "c2": "CRS-shaped v4 PL1 stand-in", "c3": "CRS-shaped v4 PL1 stand-in",
-                  "c4": "CRS-shaped v4 PL4 stand-in", "c5": "generated 10k-rule set"}[args.config]
+                  "c4": "CRS-shaped v4 PL4 stand-in", "c5": "generated 10k-rule set",
+                  "c2x": "CRS-shaped v4 PL1 stand-in + 20 CRS-scale regexes"}[args.config]
     out = {
         "metric": "requests inspected/sec (node), " + metric_set,
         "value": round(value, 1),

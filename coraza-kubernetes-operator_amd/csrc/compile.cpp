@@ -1693,6 +1693,7 @@ struct Lower {
     std::vector<DScanVal> vals;
   };
   std::vector<StreamBuild> sbuild;
+  std::vector<uint32_t> relaxed_slots;  // hit slots whose phase-A automaton is a superset relaxation
   uint32_t n_det = 0;  // streams with detect vals (DStream.det_id)
   std::map<std::string, size_t> sindex;
 
@@ -1971,7 +1972,10 @@ struct Lower {
         for (int lvl = 1; lvl <= 3; lvl++) {
           Regex rr = re;
           relax_regex(&rr, lvl);
-          if (build_regex_dfa(rr, out, &err, cap)) return true;
+          if (build_regex_dfa(rr, out, &err, cap)) {
+            relaxed_slots.push_back(pe.slot);
+            return true;
+          }
         }
         return false;
       };
@@ -2035,6 +2039,7 @@ struct Lower {
         size_t n = 0;         // patterns of the group
         bool unioned = false;
         bool always = false;  // no automaton at all
+        bool relaxed = false;  // the automaton is a superset relaxation of its one pattern
       };
       std::vector<std::pair<size_t, size_t>> chunks;  // [begin, end): kPackChunk runs of each part
       for (size_t b0 = 0; b0 < n_pre_u; b0 += kPackChunk) chunks.push_back({b0, std::min(n_pre_u, b0 + kPackChunk)});
@@ -2078,6 +2083,7 @@ struct Lower {
             Regex rr = *unionable[i].second;
             relax_regex(&rr, lvl);
             ok = build_regex_dfa(rr, &g.ab.d, &lerr, cap);
+            g.relaxed = ok;
           }
           g.ab.pes = {&pe};
           g.n = 1;
@@ -2107,6 +2113,7 @@ struct Lower {
         size_t gi = 0, left = 0;  // current group, its patterns not yet visited
         Group* open = nullptr;    // union waiting for its flush
         auto emit = [&](Group* g) {
+          if (g->relaxed) relaxed_slots.push_back(g->ab.pes[0]->slot);
           if (g->always) P->always_slots.push_back(g->ab.pes[0]->slot);
           else autos.push_back(std::move(g->ab));
         };
@@ -3317,6 +3324,13 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
       }
     }
     L.finish_streams();
+    {  // a phase-A hit of a relaxed automaton is never an exact match (field_filter re-runs the operator)
+      std::vector<char> rel(out->n_hit_slots, 0);
+      for (uint32_t sl : L.relaxed_slots)
+        if (sl < rel.size()) rel[sl] = 1;
+      for (DRule& d : out->rules)
+        if (d.hit_slot >= 0 && (uint32_t)d.hit_slot < rel.size() && rel[d.hit_slot]) d.flags2 |= RF2_PA_RELAXED;
+    }
     lap("scan plan");
     // ctl removal groups: each top-level rule's membership (its tags / msg)
     out->n_rm_groups = (uint32_t)L.rm_groups.size();

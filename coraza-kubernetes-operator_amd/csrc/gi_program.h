@@ -218,6 +218,8 @@ enum RuleFlags2 : uint8_t {
   RF2_PREFIX = 8,   // (any link) a link of a phase-2 rule before the first RF2_BODY_PA rule: its phase-A
                     // streams are "prefix" streams (DStream.prefix), which the gate's first stage runs over
                     // the body fields too -- its hit bits are complete there
+  RF2_PA_RELAXED = 16,  // the link's phase-A automaton is a superset relaxation (its exact DFA exceeds the state
+                        // cap): a phase-A hit is never an exact per-value match (k_eval re-runs the operator)
 };
 
 enum ActKind : uint8_t {

@@ -4342,6 +4342,7 @@ GI_HD __forceinline__ uint32_t field_filter(Tx& t, const DRule& R, const DVarRef
     if (vexact) {
       hres = hset_lookup(t.hset, t.hmask, (uint32_t)R.hit_slot, vb);
       if (!hres) return 0;
+      if (R.flags2 & RF2_PA_RELAXED) hres = 2;  // a superset automaton's hit: evaluate the value
     }
   }
   if (vr.key_mode == 1) {

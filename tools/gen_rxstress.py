@@ -46,17 +46,16 @@ XSS_STEMS = ["onload", "onerror", "onclick", "onmouseover", "onfocus", "onblur",
              "button", "details", "marquee", "video", "audio", "source", "template", "frameset", "isindex"]
 
 
-def words(kind: str, n: int, seed: int):
-    """n distinct lowercase words of the family: real stems plus seeded
-    syllable compounds around them (deterministic)."""
+def words(kind: str, n: int, seed: int, stems: bool = True):
+    """n distinct lowercase words of the family: real stems (unless stems is
+    False) plus seeded syllable compounds around them (deterministic)."""
     rng = np.random.default_rng(seed)
+    with_stems = stems
     stems = {"sql": SQL_STEMS, "cmd": CMD_STEMS, "xss": XSS_STEMS}[kind]
     out = []
-    seen = set()
-    for w in stems:
-        if w not in seen:
-            seen.add(w)
-            out.append(w)
+    seen = set(stems)
+    if with_stems:
+        out += list(stems)
     while len(out) < n:
         k = int(rng.integers(0, 3))
         stem = stems[int(rng.integers(0, len(stems)))]
@@ -111,12 +110,12 @@ def trie_regex(ws):
     return emit(trie)
 
 
-def sized_words(kind, seed, lo_bytes, hi_bytes):
+def sized_words(kind, seed, lo_bytes, hi_bytes, stems=True):
     """a word list whose trie regex lands in [lo_bytes, hi_bytes]"""
     target = (lo_bytes + hi_bytes) // 2
     n = 64
     while True:
-        ws = words(kind, n, seed)
+        ws = words(kind, n, seed, stems)
         size = len(trie_regex(ws))
         if size >= lo_bytes or n > 4000:
             break
@@ -163,8 +162,8 @@ def rules():
                     "XSS Filter - Category %d: assembled tag / handler set" % i, "attack-xss", "xss_score", (ws,), i % 4))
         rid += 1
     for i in range(2):  # wide context: beyond the DFA state cap -> NFA position tables
-        ws1 = sized_words("sql", SEED + 300 + i, 1200, 1800)
-        ws2 = words("sql", 40, SEED + 400 + i)
+        ws1 = sized_words("sql", SEED + 300 + i, 1200, 1800, stems=False)
+        ws2 = words("sql", 40, SEED + 400 + i, stems=False)
         out.append((rid, "wide", "(?i)" + trie_regex(ws1) + r"[^\n]{0,%d}?" % (24 + 8 * i) + trie_regex(ws2) + r"\b",
                     T_SQL, "SQL Injection Attack (keyword pair within a window %d)" % i, "attack-sqli",
                     "sql_injection_score", (ws1, ws2), 24 + 8 * i))
