@@ -126,6 +126,7 @@ struct DBatch {
   unsigned long long* dmemo_keys;  // [dmemo_mask + 1] (0: empty); nullptr: no memo
   uint4* dmemo_info;               // per entry: canonical copy offset (lo, hi) in det_bytes, length, state bits
   uint32_t dmemo_mask;
+  uint32_t dmemo_min;  // shortest value the memo serves (GI_DET_MEMO_MIN; shorter ones are cheaper to detect)
 };
 
 // k_scan launch plan: job lists for the small-LDS and big-LDS launches.

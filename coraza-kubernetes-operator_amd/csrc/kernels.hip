@@ -7071,7 +7071,7 @@ __device__ uint32_t det_results(const DBatch& B, const uint8_t* v, uint32_t n, u
     return s ? li_detect_sqli(v, n, st, T) : li_detect_xss(v, n);
   };
   uint32_t out = 0;
-  if (!B.dmemo_keys) {
+  if (!B.dmemo_keys || n < B.dmemo_min) {  // (a short unique value costs more in memo round trips than to detect)
     if (need_s && compute(true)) out |= 1u;
     if (need_x && compute(false)) out |= 2u;
     return out;

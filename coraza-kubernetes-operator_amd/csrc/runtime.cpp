@@ -1219,6 +1219,8 @@ int gi_run_staged(gi_ctx* c) {
     B.dmemo_keys = c->dmemo_mask ? (unsigned long long*)c->dmemo_keys.p : nullptr;
     B.dmemo_info = c->dmemo_mask ? (uint4*)c->dmemo_info.p : nullptr;
     B.dmemo_mask = c->dmemo_mask;
+    static const uint32_t dm_min_env = getenv("GI_DET_MEMO_MIN") ? (uint32_t)atoi(getenv("GI_DET_MEMO_MIN")) : 32u;
+    B.dmemo_min = dm_min_env;
     B.diag = nullptr;
     B.prof = nullptr;
     if (c->prof_on && c->prof.ensure(1024 + 8000) == hipSuccess) {
