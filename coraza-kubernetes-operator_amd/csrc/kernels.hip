@@ -6458,11 +6458,27 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GI_SC
   const uint32_t n_iw = min(B.ibk[3 * GI_NB], B.qcap);
   const uint32_t per_unit = blockDim.x;  // entries per unit
   const uint32_t nu_job = (n_iw + per_unit - 1) / per_unit;
-  const uint64_t n_units = (uint64_t)nu_job * n_jl;
+  // Unit order.  XCD-grouped (default): the jobs of one chunk of queue blocks
+  // are consecutive units of one XCD (workgroup b runs on XCD b % 8 and the
+  // grid is a multiple of 8), so the jobs of a stream -- adjacent in jl --
+  // read that chunk's queue words while they are in the XCD's L2 instead of
+  // each fetching them from HBM.  GI_SCAN_MODE bit 5 (32): job-major (each
+  // job sweeps all chunks, the round-4 order).
+  const bool xcd = !(mode & 32) && (gridDim.x & 7) == 0;
+  const uint32_t ngrp = (nu_job + 7) / 8;
+  const uint64_t n_units = xcd ? (uint64_t)ngrp * 8 * n_jl : (uint64_t)nu_job * n_jl;
   uint32_t loaded = 0xFFFFFFFFu;
   for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
-    const uint32_t jj = (uint32_t)(u / nu_job);
-    const uint32_t chunk = (uint32_t)(u - (uint64_t)jj * nu_job);
+    uint32_t jj, chunk;
+    if (xcd) {
+      const uint64_t q = u >> 3;
+      jj = (uint32_t)(q % n_jl);
+      chunk = (uint32_t)(q / n_jl) * 8u + (uint32_t)(u & 7u);
+      if (chunk >= nu_job) continue;  // (block-uniform)
+    } else {
+      jj = (uint32_t)(u / nu_job);
+      chunk = (uint32_t)(u - (uint64_t)jj * nu_job);
+    }
     const uint32_t j = jl[jj];
     const DJob J = gi_cload(P.jobs, j);
     const uint8_t* img = P.images + J.img_off;
