@@ -118,6 +118,7 @@ struct DBatch {
   uint8_t* pend;              // [n_req] stage 1 -> 2: 1 = the request continues to the body stage
   uint32_t* plist;            // the pending requests (stage-1 k_eval appends), *pcount of them
   uint32_t* pcount;
+  uint32_t wave_stage2;       // the body stage's pending requests all go to k_eval_wave (GI_EVAL_WAVE_STAGE2=0: by size)
   uint32_t body_tiles;        // k_body runs its chunkable transformations LDS-tiled (GI_BODY_TILES=0: off)
   uint32_t prefix_budget;     // RF2_BODY_PA rules a first-stage request evaluates over its unscanned body
   // k_detect's memo of libinjection results by value (kernels.hip det_memo):

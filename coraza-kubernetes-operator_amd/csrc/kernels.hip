@@ -7566,6 +7566,10 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
 // the rule walk instead of one lane doing both alone.
 GI_HD __forceinline__ bool eval_heavy(const DProgram& P, const DBatch& B, uint32_t r) {
   if (!B.wlist) return false;
+  // the gate's body stage: its few pending requests are the heavy ones (long
+  // bodies, every body rule still to run), one lane each would leave most of
+  // the GPU idle -- a wave each (DBatch.wave_stage2, GI_EVAL_WAVE_STAGE2)
+  if (B.stage == 2 && B.wave_stage2) return true;
   if (B.wave_rules && P.top_end[1] - P.top_begin[0] >= B.wave_rules) return true;
   const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
   return B.wave_fields && H->nf + H->n_post >= B.wave_fields;

@@ -1253,6 +1253,8 @@ int gi_run_staged(gi_ctx* c) {
     B.prefix_budget = budget_env;
     static const uint32_t tiles_env = getenv("GI_BODY_TILES") ? (uint32_t)atoi(getenv("GI_BODY_TILES")) : 1u;
     B.body_tiles = tiles_env;
+    static const uint32_t ws2_env = getenv("GI_EVAL_WAVE_STAGE2") ? (uint32_t)atoi(getenv("GI_EVAL_WAVE_STAGE2")) : 1u;
+    B.wave_stage2 = ws2_env;
     B.bparse_lds = (uint32_t)std::min<uint64_t>(c->bparse_lds, (c->max_body + 15) & ~15ull);
   }
   (void)hipEventRecord(c->ev0, c->stream);
