@@ -6915,6 +6915,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8)))
     uint32_t prev_off = 0xFFFFFFFFu, prev_len = 0;
     for (uint32_t k = 0; k < P.n_body_links; k++) {
       const DRule R = gi_cload(P.rules, (uint64_t)P.body_links[k]);
+      // the gate: the first stage runs the links of the phase-2 prefix (its
+      // k_eval stops before any other), the body stage the rest, for the
+      // pending requests only
+      if (B.stage && (B.stage == 1) != ((R.flags2 & RF2_PREFIX) != 0)) continue;
       const DOp o = gi_cload(P.ops, (uint64_t)R.op);
       const uint64_t c0 = B.prof ? gi_clock() : 0;
       bool same = R.tchain_len == prev_len;
@@ -7831,7 +7835,7 @@ void launch_pipeline(const DProgram& P, const DBatch& B0, const ScanLaunch& S, h
   int nk = 0;  // (the caller resets *log and records its ev[0] before the first chunk)
   const uint32_t cb = (B0.n_req + 255) / 256;
   // The gate: when the batch has bodies, the first stage parses them and runs
-  // k_body (REQUEST_BODY links) but scans only the phase-1 items, and
+  // k_body's prefix links (REQUEST_BODY) but scans only the phase-1 items, and
   // evaluates every request up to the first phase-2 rule that needs its body
   // fields' phase-A scan (RF2_BODY_PA): requests with no body, and those phase
   // 1 or the phase-2 rules before it decide (CRS's ARGS-count / byte-range
@@ -7866,6 +7870,7 @@ void launch_pipeline(const DProgram& P, const DBatch& B0, const ScanLaunch& S, h
       GI_LAUNCH("k_bcounts", k_bcounts, dim3(cb), dim3(256), 0, stream, P, B2);
       launch_phase_a(P, B2, S, stream, nullptr, stop_after, log, nk);
     }
+    if (P.n_body_links) GI_LAUNCH("k_body.2", k_body, dim3(std::min<uint32_t>(B2.n_body, 1u << 20)), dim3(64), 0, stream, P, B2);
     launch_eval(P, B2, stream, stop_after, log, nk);
   }
   {
