@@ -1726,18 +1726,25 @@ GI_HD inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
 template <class C>
 GI_HD __forceinline__ void json_fold_keys(C& t, uint32_t f0) {
   const uint32_t nf = t.nf - f0;
-  const uint32_t tsize = t.cap_t / 4;  // > body/2 + 2 >= nf (runtime.cpp sizing)
+  const uint32_t cap = t.cap_t / 4;  // > body/2 + 2 >= nf (runtime.cpp sizing)
   if (nf < 2) return;
-  if (nf >= tsize) {
+  if (nf >= cap) {
     t.flags |= GI_REQ_OVERFLOW;
     return;
   }
+  // the smallest power of two >= 2 nf that the scratch holds (the fold does
+  // not depend on the table size; zeroing cap words cost more than the parse)
+  uint32_t tsize = 16;
+  while (tsize < 2 * nf && 2 * tsize <= cap) tsize *= 2;
+  if (tsize > cap || tsize <= nf) tsize = cap;  // (cap > nf: an empty slot always remains)
+  const bool pow2 = (tsize & (tsize - 1)) == 0;
   uint32_t* tab = (uint32_t*)t.t1;
   for (uint32_t k = 0; k < tsize; k++) tab[k] = 0;
   bool any = false;
   for (uint32_t i = f0; i < t.nf; i++) {
     Field& f = t.fields[i];
-    uint32_t h = gi_fnv1a(f.k, f.kn, false) % tsize;
+    const uint32_t hv = gi_fnv1a(f.k, f.kn, false);
+    uint32_t h = pow2 ? (hv & (tsize - 1)) : hv % tsize;
     while (true) {
       const uint32_t e = tab[h];
       if (e == 0) {
