@@ -6471,8 +6471,10 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GI_SC
   // read that chunk's queue words while they are in the XCD's L2 instead of
   // each fetching them from HBM.  GI_SCAN_MODE bit 5 (32): job-major (each
   // job sweeps all chunks, the round-4 order).
-  const bool xcd = !(mode & 32) && (gridDim.x & 7) == 0;
+  // (a job with fewer than 8 chunks -- few requests, e.g. C5's 32 -- would
+  // leave the XCDs past its last chunk idle: job-major then)
   const uint32_t ngrp = (nu_job + 7) / 8;
+  const bool xcd = !(mode & 32) && (gridDim.x & 7) == 0 && nu_job >= 8;
   const uint64_t n_units = xcd ? (uint64_t)ngrp * 8 * n_jl : (uint64_t)nu_job * n_jl;
   uint32_t loaded = 0xFFFFFFFFu;
   for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
