@@ -6752,13 +6752,13 @@ __device__ bool wave_validate(const DOp& o, const uint8_t* s, uint32_t n) {
 // without an inner sync point is done by lane 0 from HBM up to the next one.
 // Returns the output length, -1 on overflow; *psumm = byte summary of it.
 #define GI_TT_IN 3072
-#define GI_TT_LDS (GI_TT_IN + 3 * GI_TT_IN + 8 * 64 + 2 * 65 * 4)
+#define GI_TT_LDS (GI_TT_IN + 32 + 3 * GI_TT_IN + 8 * 64 + 2 * 65 * 4)
 static_assert(GI_TT_LDS <= 16384, "k_body's LDS slot holds the transformation tiles");
 __device__ __forceinline__ int64_t wave_transform_lds(const DProgram& P, uint8_t code, const uint8_t* src, uint32_t n, uint8_t* dst,
                                       uint64_t cap, uint8_t* lds, uint32_t* psumm) {
   const uint32_t L = lane_id();
-  uint8_t* in = lds;
-  uint8_t* out = lds + GI_TT_IN;  // lane slots at 3 * a + 8 * L (3x + 8 bytes each, as apply_transform allows)
+  uint8_t* const inb = lds;                // the tile's 16-byte words (GI_TT_IN + 32 bytes)
+  uint8_t* out = lds + GI_TT_IN + 32;  // lane slots at 3 * a + 8 * L (3x + 8 bytes each, as apply_transform allows)
   uint32_t* offs = (uint32_t*)(out + 3 * GI_TT_IN + 8 * 64);  // [65] output offsets
   uint32_t* slot = offs + 65;                                  // [64] slot starts
   uint64_t o = 0;
@@ -6768,7 +6768,14 @@ __device__ __forceinline__ int64_t wave_transform_lds(const DProgram& P, uint8_t
     const uint32_t tn = min(n - base, (uint32_t)GI_TT_IN);
     const bool last = base + tn == n;
     __syncthreads();  // the previous tile's LDS reads are done
-    for (uint32_t k = L; k < tn; k += 64) in[k] = src[base + k];
+    // the tile as aligned 16-byte words, all loads in flight at once (the
+    // sources -- the body arena, the request's 16-byte aligned t0 / t1 --
+    // are readable 15 bytes either side)
+    const uintptr_t a0 = (uintptr_t)(src + base);
+    const uint32_t sh = (uint32_t)(a0 & 15u);
+    const uint4* w = (const uint4*)(a0 - sh);
+    for (uint32_t k = L; k < (sh + tn + 15) / 16; k += 64) ((uint4*)inb)[k] = w[k];
+    const uint8_t* in = inb + sh;
     __syncthreads();
     uint32_t a, e;
     wave_chunks(tn, [&](uint32_t p) { return t_sync(code, in, p); }, &a, &e);
