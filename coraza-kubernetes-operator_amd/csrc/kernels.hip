@@ -6675,6 +6675,22 @@ __device__ __forceinline__ uint32_t dfa_steps(const DProgram& P, const DDfa& d, 
   return st;
 }
 
+// k_body's operators other than automata / @validate*, on lane 0 (rare: the
+// compiler keeps detectors out of k_body).  Out of line, so the interpreter
+// state it needs stays out of k_body's register budget.
+__device__ __noinline__ bool body_other_op(const DProgram& P, const Region& g, const DOp& o, const uint8_t* s,
+                                           uint32_t n) {
+  Tx t;
+  t.P = &P;
+  t.t0 = g.t0;
+  t.t1 = g.t1;
+  t.cap_t = g.cap_t;
+  t.mt = g.mt;
+  t.cap_mt = g.cap_mt;
+  t.flags = 0;
+  return eval_op<false>(t, o, s, n);
+}
+
 #define GI_BODY_LDS 16384  // k_body's LDS automaton slot (bytes): 8 one-wave workgroups per CU
 
 // Exact "d matches somewhere in s[0, n)" by the whole wave (see above).
@@ -6969,17 +6985,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8)))
         hit = wave_validate(o, cur, cn) != (o.negate != 0);
       } else {  // any other operator: lane 0, side-effect free
         bool h = false;
-        if (L == 0) {
-          Tx t;
-          t.P = &P;
-          t.t0 = g.t0;
-          t.t1 = g.t1;
-          t.cap_t = g.cap_t;
-          t.mt = g.mt;
-          t.cap_mt = g.cap_mt;
-          t.flags = 0;
-          h = eval_op<false>(t, o, cur, cn);
-        }
+        if (L == 0) h = body_other_op(P, g, o, cur, cn);
         hit = __shfl((int)h, 0, 64) != 0;
       }
       if (hit && L == 0) set_hit(B, (uint32_t)R.hit_slot, r);
