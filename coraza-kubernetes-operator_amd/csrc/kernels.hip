@@ -4107,7 +4107,9 @@ GI_HD __noinline__ uint32_t run_capture(const DProgram& P, uint32_t* capws, uint
       x.n = len;
     }
     if (H->rec) {  // capture record {rule id, group, byte offset in the request's row, length}
-      if (H->nrec < H->rec_cap && H->nbytes + len <= H->bytes_cap) {
+      // (the first record that does not fit ends the list: the records kept
+      // are a prefix of Coraza's, which GI_REQ_CAPTURE_TRUNC promises)
+      if (!H->trunc && H->nrec < H->rec_cap && H->nbytes + len <= H->bytes_cap) {
         uint32_t* r = H->rec + 4ull * H->nrec;
         r[0] = rule_id;
         r[1] = g;
