@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r05rx}
 echo "== parity $(date +%T)"
-timeout -k 10 200 python -u -m pytest tests/test_rxstress.py ${EXTRA_TESTS:-} -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/${TAG}_parity.log 2>&1 || { tail -30 gpurun_out/${TAG}_parity.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_rxstress.py ${EXTRA_TESTS:-} -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/${TAG}_parity.log 2>&1 || { tail -30 gpurun_out/${TAG}_parity.log; exit 1; }
 tail -1 gpurun_out/${TAG}_parity.log
 echo "== c2x $(date +%T)"
 timeout -k 10 400 python -u bench.py --config c2x --steps 5 --warmup 1 --e2e-iters 0 > gpurun_out/${TAG}_c2x_bench.json 2> gpurun_out/${TAG}_c2x.err || { tail -20 gpurun_out/${TAG}_c2x.err; exit 1; }
