@@ -6018,8 +6018,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
       gm = item_gmask(P, it);
       B.igm[base + ii] = gm;  // k_scan's per-lane filter mask (the queue lanes carry the item index)
       src = it.vp;
-      if (IN && IN <= 32) {  // stage the scanned bytes once for all streams: the aligned words
-        // covering the value, all loads in flight at once (<= 3 bytes past its end: padded sources)
+      if (IN) {  // stage the scanned bytes once for all streams (bucket: vn <= IN): the
+        // aligned words covering the value, all loads in flight at once (<= 3 bytes past its
+        // end: padded sources)
         const uint32_t n = min(it.vn, IN);
         const uintptr_t a = (uintptr_t)it.vp;
         const uint32_t sh = (uint32_t)(a & 3u);
@@ -6031,10 +6032,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_STRE
 #pragma unroll
         for (uint32_t k = 0; k < IN / 4; k++)
           if (4 * k < n) *(uint32_t*)(li + 4 * k) = sh ? __builtin_amdgcn_alignbyte(wv[k + 1], wv[k], sh) : wv[k];
-        src = li;
-      } else if (IN) {  // stage the scanned bytes once for all streams (bucket: vn <= IN), a word at a time
-        const uint32_t n = min(it.vn, IN);
-        for (uint32_t i = 0; i < n; i += 4) *(uint32_t*)(li + i) = load_u32u(it.vp + i);
         src = li;
       }
       summ = value_summary_lut(sumlut, src, it.vn);
