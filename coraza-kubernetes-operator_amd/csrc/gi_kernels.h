@@ -120,7 +120,6 @@ struct DBatch {
   uint32_t* pcount;
   uint32_t wave_stage2;       // the body stage's pending requests all go to k_eval_wave (GI_EVAL_WAVE_STAGE2=0: by size)
   uint32_t body_tiles;        // k_body runs its chunkable transformations LDS-tiled (GI_BODY_TILES=0: off)
-  uint32_t prefix_budget;     // RF2_BODY_PA rules a first-stage request evaluates over its unscanned body
   // k_detect's memo of libinjection results by value (kernels.hip det_memo):
   // the same header / cookie value recurs across requests (User-Agent,
   // Referer); open addressing on a 64-bit hash, entries verified byte for byte
@@ -156,8 +155,6 @@ struct ScanLaunch {
 #define GI_EVAL_WAVE_RULES 2048
 #define GI_BPARSE_LDS 0              // k_bparse LDS copy of JSON bodies up to this size (GI_BPARSE_LDS env; 0: off --
                                      // measured: 32 KB made C3's k_bparse 81 -> 272 ms, the LDS cut its occupancy)
-#define GI_PREFIX_BUDGET 0             // default DBatch.prefix_budget (GI_PREFIX_BUDGET env; round 5: the
-                                     // interpreter is ~500 cycles per body byte per automaton link)
 #define GI_GATE_PENDING_MAX 0.5       // the adaptive gate runs while at most this share of body requests stays pending
 #define GI_CHUNK_POOL_WORDS 16e9     // queue-pool words (estimate) one request chunk of a batch may need
 

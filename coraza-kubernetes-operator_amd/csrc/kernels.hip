@@ -1443,8 +1443,8 @@ struct Tx {
   uint32_t cur_groups;       // removal groups of the top-level rule being evaluated
   uint8_t allow;             // allow action in effect (D_ALLOW_*; 0: none)
   bool prefix;               // gate stage 1, the request's body processed: stop at the first RF2_BODY_PA rule
+  bool prefix_spec;          // ... and its body fields are the speculative parser's (scanned by the prefix streams)
   bool bail;                 // ... and it stopped there (the body stage re-evaluates it)
-  uint32_t pa_budget;        // RF2_BODY_PA rules the first stage still evaluates itself (DBatch.prefix_budget)
   uint8_t engine, body_access, body_proc, phase;
   uint8_t force_body;
   int32_t skip_after;
@@ -4169,10 +4169,13 @@ GI_HD __noinline__ bool target_removed_in(const Tx::RmTarget* rt, uint32_t n, co
   target_removed_in((t).rtgt, (t).nrtgt, (t).P->strpool, (id), (t).cur_groups, (var), (k), (kn))
 
 // The link's phase-A bits are void: it can see ARGS_POST / body fields phase A
-// did not scan for it (the gate's first stage scans body fields only through
-// the prefix streams, so there a RF2_PREFIX link's bits stay valid).
+// did not scan for it (the gate's first stage scans the speculative parser's
+// body fields only through the prefix streams, so there a RF2_PREFIX link's
+// bits stay valid -- but not when the interpreter parsed the body itself:
+// a processor phase 1 chose differently, a ProcessPartial body over the
+// limit; phase A never saw those fields).
 GI_HD __forceinline__ bool bodydep_void(const Tx& t, const DRule& R) {
-  return (R.flags & RF_BODYDEP) && t.has_post && !(t.prefix && (R.flags2 & RF2_PREFIX));
+  return (R.flags & RF_BODYDEP) && t.has_post && !(t.prefix_spec && (R.flags2 & RF2_PREFIX));
 }
 
 GI_HD __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
@@ -4848,12 +4851,9 @@ GI_HD __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u))
       continue;  // phase A proved the first link matches nothing
     if ((R.flags & RF_CONST) && R._pad2 == 0) continue;  // folded: matches nothing for any request
-    if (t.prefix && (R.flags2 & RF2_BODY_PA)) {  // evaluated over the unscanned body by the interpreter, up to
-      if (t.pa_budget == 0) {                     // a budget of such rules; then the first stage ends here
-        t.bail = true;
-        break;
-      }
-      t.pa_budget--;
+    if (t.prefix && (R.flags2 & RF2_BODY_PA)) {  // needs the body's phase-A scan: the first stage ends here
+      t.bail = true;
+      break;
     }
     eval_top<W>(t, ri);
     if (t.allow) {  // the allow rule ends this phase's walk (allow:phase: only this one)
@@ -7327,8 +7327,8 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
   t.cur_groups = 0;
   t.allow = 0;
   t.prefix = false;
+  t.prefix_spec = false;
   t.bail = false;
-  t.pa_budget = B.prefix_budget;
   t.kx = nullptr;
   t.engine = P.rule_engine;
   t.body_access = P.body_access;
@@ -7445,6 +7445,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
               t.nf += H->n_post;  // k_bparse's fields: scanned through the prefix streams only
               t.nf_pa = t.nf;      // (value map valid for RF2_PREFIX links; the others' bits are void)
               t.has_post = H->n_post > 0;
+              t.prefix_spec = true;
               t.body_spec = true;  // k_body (first stage) tested REQUEST_BODY
             } else if (t.body_proc == H->spec_proc) {
               t.nf += H->n_post;  // k_bparse's fields, already in phase A
@@ -7480,6 +7481,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
               t.nf += H->n_post;  // k_mpparse's fields: scanned through the prefix streams only
               t.nf_pa = t.nf;
               t.has_post = H->n_post > 0;
+              t.prefix_spec = true;
               err = H->spec_err;
             } else if (H->spec_proc == BP_MULTIPART) {
               t.nf += H->n_post;  // k_mpparse's fields (ARGS_POST already in phase A)
@@ -7827,7 +7829,11 @@ static void launch_phase_a(const DProgram& P, const DBatch& B, const ScanLaunch&
   GI_LAUNCH(s2 ? "k_stream3.2" : "k_stream3", (k_stream<128, 132, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 3u);
   GI_LAUNCH(s2 ? "k_stream4.2" : "k_stream4", (k_stream<0, 0, 0>), dim3(GI_STREAM_GRID), dim3(64), 0, stream, P, B, 4u);
   if (P.n_det_streams) {
-    if (B.dmemo_keys) (void)hipMemsetAsync(B.dmemo_keys, 0, 8ull * (B.dmemo_mask + 1), stream);  // the det arena restarts
+    if (B.dmemo_keys) {  // the det arena restarts: keys AND result words (a reader that sees a fresh claimer's
+      // key before the claimer's info store must find w == 0, never the previous stage's or batch's VALID bits)
+      (void)hipMemsetAsync(B.dmemo_keys, 0, 8ull * (B.dmemo_mask + 1), stream);
+      (void)hipMemsetAsync(B.dmemo_info, 0, 16ull * (B.dmemo_mask + 1), stream);
+    }
     GI_LAUNCH(s2 ? "k_detect.2" : "k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
   }
   if (B.long_cap) GI_LAUNCH(s2 ? "k_long.2" : "k_long", k_long, dim3(B.long_grid), dim3(64), 0, stream, P, B);

@@ -1248,9 +1248,6 @@ int gi_run_staged(gi_ctx* c) {
     B.pend = (uint8_t*)c->pend.p;
     B.plist = (uint32_t*)c->plist.p;
     B.pcount = (uint32_t*)(cp + 512);
-    static const uint32_t budget_env =
-        getenv("GI_PREFIX_BUDGET") ? (uint32_t)atoi(getenv("GI_PREFIX_BUDGET")) : GI_PREFIX_BUDGET;
-    B.prefix_budget = budget_env;
     static const uint32_t tiles_env = getenv("GI_BODY_TILES") ? (uint32_t)atoi(getenv("GI_BODY_TILES")) : 1u;
     B.body_tiles = tiles_env;
     static const uint32_t ws2_env = getenv("GI_EVAL_WAVE_STAGE2") ? (uint32_t)atoi(getenv("GI_EVAL_WAVE_STAGE2")) : 1u;

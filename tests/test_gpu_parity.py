@@ -471,6 +471,52 @@ def test_gpu_body_limit(engine, action):
                    for i in range(len(txs)))
 
 
+PARTIAL_PREFIX_RULES = """SecRuleEngine On
+SecRequestBodyAccess On
+SecRequestBodyLimit 64
+SecRequestBodyLimitAction ProcessPartial
+SecRule ARGS "@validateByteRange 32-126" "id:10,phase:2,pass,t:none,setvar:tx.bad=1"
+SecRule ARGS_POST "@contains evil" "id:13,phase:2,pass,t:none,setvar:tx.evil=1"
+SecRule REQUEST_HEADERS:X "@streq stop" "id:11,phase:2,deny,status:403"
+SecRule ARGS "@rx mon[k]ey" "id:12,phase:2,deny,status:403,t:none"
+"""
+
+
+def test_gpu_gate_prefix_partial_body():
+    """in the gate's first stage a RF2_PREFIX link's
+    phase-A bits are trusted only when the body fields are the speculative
+    parser's.  A ProcessPartial body over SecRequestBodyLimit is parsed by the
+    interpreter (k_bparse skips it), so phase A never saw its fields: rule 10
+    (@validateByteRange over ARGS) must still match it, and rule 11's
+    interruption makes the first stage final (no bail to the body stage).
+    A fresh engine runs its first batch with the gate on."""
+    txs = []
+    for n in (10, 40, 63, 64, 65, 100, 300):
+        for stop in (False, True):
+            for bad_at in (3, 50):
+                body = bytearray(b"a=" + b"x" * max(0, n - 2))[:n]
+                if n > bad_at + 3:
+                    body[bad_at:bad_at + 3] = b"%01"
+                if n > 30:
+                    body[20:28] = b"&e=evil&"
+                t = gpuinspect.Transaction(method=b"POST", uri=b"/?g=1")
+                t.add_request_header("Content-Type", "application/x-www-form-urlencoded")
+                t.add_request_header("X", "stop" if stop else "go")
+                t.write_request_body(bytes(body))
+                txs.append(t)
+    rs = gpuinspect.Ruleset(PARTIAL_PREFIX_RULES, tx_exports=["bad", "evil"])
+    eng = gpuinspect.Engine(rs)
+    batch = gpuinspect.pack(txs)
+    res = eng.inspect(batch)
+    orc = compare.oracle_verdicts(coraza.parse_seclang(PARTIAL_PREFIX_RULES), batch, rs.exports)
+    bad = compare.compare(res, orc)
+    assert not bad, bad
+    assert eng.stats()["gate_requests"] > 0, "the first batch of a context runs gated"
+    # over-limit bodies with an out-of-range byte in the first 64 bytes, stopped by rule 11
+    hit = [i for i in range(batch.n_req) if 10 in res.matched_rules(i) and 11 in res.matched_rules(i)]
+    assert hit
+
+
 def test_gpu_large_body_next_to_small():
     """One 24 MB body among small requests stages and runs (bounded k_long
     buffers: ADVICE r02) and every verdict matches the oracle."""
