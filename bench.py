@@ -443,6 +443,16 @@ def main():
     t3 = time.perf_counter()
     res = eng.fetch()
     t4 = time.perf_counter()
+    # which rules decide the verdicts: the interrupting rule of every
+    # interrupted request (0: the 413 of SecRequestBodyLimitAction Reject), and
+    # the most-matched ids without the request-independent ones (the folded
+    # initialisation SecActions match every request)
+    iv = res.verdicts[res.verdicts["status"] != 0]["rule_id"]
+    ids_i, cnt_i = np.unique(iv, return_counts=True)
+    out["tally"]["interrupting_rules"] = [[int(i), int(c)] for c, i in sorted(zip(cnt_i, ids_i), reverse=True)[:8]]
+    out["tally"]["top_rules_request_dependent"] = sorted(
+        ([int(i), int(h)] for i, h in zip(detail["rule_ids"], node_tally["rule_hits"]) if 0 < h < node_tally["n_req"]),
+        key=lambda x: -x[1])[:8]
     out["e2e"] = {"requests_per_s": round(batch.n_req / (t4 - t1), 1), "ms": round((t4 - t1) * 1e3, 2),
                   "stage_ms": round((t2 - t1) * 1e3, 2), "run_ms": round((t3 - t2) * 1e3, 2),
                   "fetch_ms": round((t4 - t3) * 1e3, 2),
