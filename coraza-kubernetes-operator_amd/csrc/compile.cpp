@@ -1717,6 +1717,7 @@ struct Lower {
   // capture analysis (capture_analysis): every capture is observable, or only these links'
   bool cap_global = true;
   std::set<const IrRule*> cap_links;
+  std::map<const IrRule*, std::string> pa_rx;  // first link -> its phase-A pattern (within_chain_filters)
 
   int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
     if (!r.has_op || no_scan) return -1;
@@ -1880,7 +1881,8 @@ struct Lower {
       pe.fmask = 1ull << sb.gids[fid];
       if (o.kind == OP_RX) {
         pe.kind = 0;
-        pe.rx = "(?sm)" + r.op_arg;
+        const auto ov = pa_rx.find(&r);
+        pe.rx = ov != pa_rx.end() ? ov->second : "(?sm)" + r.op_arg;
       } else if (o.kind == OP_PM && r.op_name == "pmfromfile") {
         pe.kind = 1;
         pe.phrases = r.phrases;
@@ -2595,6 +2597,228 @@ static void capture_analysis(const IrWaf& waf, const std::vector<std::string>& e
   }
 }
 
+// ------------------------------------------ restricted-name chains (CRS 920450)
+// CRS v4 920450 / 920451:
+//   SecRule REQUEST_HEADERS_NAMES "@rx ^.*$" "capture,t:none,t:lowercase,
+//       setvar:'tx.<P>%{tx.0}=/%{tx.0}/',chain"
+//     SecRule TX:/^<P>/ "@within %{tx.<LIST>}" "..."
+// The first link matches every name and files each one under a run-time TX
+// key; the chain then asks whether some filed "/name/" is a substring of the
+// list.  Phase A's "^.*$" bit is therefore set for every request with a
+// header, and k_eval ran the capture, the macro-key setvar and the @within
+// walk on every header of every request.  The chain can only match if some
+// transformed name v has "/" + v + "/" inside a value LIST can hold, i.e. v is
+// one of the finite set of strings between two '/' of that value.  When the
+// keys <P>* and the capture are observable nowhere else, the names outside
+// that set have no observable effect, so the first link's phase-A pattern
+// becomes that set (exact): a clear bit skips the rule, and a set bit lets
+// only the names in the set through field_filter (each still runs the link's
+// capture and setvar in Coraza's order, so the chain sees the same keys it
+// would have matched).  Conditions (anything else: no override):
+//  * no capture group is observable outside its feeding chains (cap_global);
+//  * the first link: @rx "^.*$", not negated, no multiMatch, last
+//    transformation t:lowercase (so equal keys mean equal values), collection
+//    targets only (no TX, no MATCHED_*, no counts), one setvar
+//    'tx.<P>%{tx.0}=/%{tx.0}/' and no ctl, exactly one chained link;
+//  * the chained link: TX:/^<P>/ with <P> a plain key literal, @within
+//    "%{tx.<LIST>}", no transformation, capture or multiMatch;
+//  * no other link, macro, setvar key or export can name a key starting with
+//    <P> (so no other writer can interleave with the filed keys);
+//  * no first link reads MATCHED_VAR / MATCHED_VAR_NAME (the names it skips
+//    would otherwise have left them set);
+//  * every setvar of <LIST> is a literal (the possible list values are those
+//    literals and ""), ASCII, with at most 64 '/'.
+// Returns first link -> the phase-A regex.
+static std::map<const IrRule*, std::string> within_chain_filters(const IrWaf& waf,
+                                                                  const std::vector<std::string>& exports,
+                                                                  bool cap_global) {
+  std::map<const IrRule*, std::string> out;
+  if (cap_global) return out;
+  auto lowerc = [](std::string x) {
+    for (auto& c : x) c = (char)tolower((unsigned char)c);
+    return x;
+  };
+  auto keychar = [](char c) { return isalnum((unsigned char)c) || c == '_' || c == '-' || c == '.'; };
+  auto is_key_lit = [&](const std::string& s) {
+    if (s.empty()) return false;
+    for (char c : s)
+      if (!keychar(c)) return false;
+    return true;
+  };
+  // every TX key a macro in s reads, lowercased ("" when the key is not a plain literal)
+  auto macro_keys = [&](const std::string& s) {
+    std::vector<std::string> ks;
+    const std::string l = lowerc(s);
+    for (size_t p = l.find("%{"); p != std::string::npos; p = l.find("%{", p + 2)) {
+      size_t q = p + 2;
+      while (q < l.size() && (l[q] == ' ' || l[q] == '\t')) q++;
+      if (l.compare(q, 2, "tx") != 0 || q + 2 >= l.size() || (l[q + 2] != '.' && l[q + 2] != ':')) continue;
+      size_t e = q + 3;
+      while (e < l.size() && keychar(l[e])) e++;
+      ks.push_back(e < l.size() && l[e] == '}' ? l.substr(q + 3, e - q - 3) : std::string());
+    }
+    return ks;
+  };
+  auto reads_mv1 = [&](const std::string& s) {
+    const std::string l = lowerc(s);
+    for (size_t p = l.find("matched_var"); p != std::string::npos; p = l.find("matched_var", p + 1))
+      if (l.compare(p, 12, "matched_vars") != 0) return true;
+    return false;
+  };
+  std::vector<const IrRule*> links;
+  for (const IrRule& t : waf.rules) {
+    links.push_back(&t);
+    for (const IrRule& c : t.children) links.push_back(&c);
+  }
+  // no first link may read MATCHED_VAR / MATCHED_VAR_NAME before its own match
+  for (const IrRule& t : waf.rules) {
+    for (const IrVar& v : t.vars) {
+      const std::string n = lowerc(v.name);
+      if (n == "matched_var" || n == "matched_var_name") return out;
+    }
+    if (t.has_op && reads_mv1(t.op_arg)) return out;
+    if (!t.has_op)
+      for (const IrNd& a : t.nd)
+        if (reads_mv1(a.sv_key) || reads_mv1(a.sv_value) || reads_mv1(a.ctl_value)) return out;
+  }
+  const std::string m0 = "%{tx.0}";
+  for (const IrRule& r : waf.rules) {
+    if (!r.has_op || r.op_name != "rx" || r.op_neg || r.op_arg != "^.*$" || !r.capture || r.multimatch) continue;
+    if (r.transforms.empty() || lowerc(r.transforms.back()) != "lowercase") continue;
+    if (r.children.size() != 1 || r.nd.size() != 1 || !r.nd[0].is_setvar || r.nd[0].sv_remove) continue;
+    bool ok = !r.vars.empty();
+    for (const IrVar& v : r.vars) {
+      const std::string n = lowerc(v.name);
+      if (v.count || n == "tx" || n.rfind("matched_var", 0) == 0 || single_id(v.name) >= 0) ok = false;
+    }
+    const std::string sk = lowerc(r.nd[0].sv_key), sv = lowerc(r.nd[0].sv_value);
+    if (!ok || sk.size() <= m0.size() || sk.compare(sk.size() - m0.size(), m0.size(), m0) != 0 ||
+        sv != "/" + m0 + "/")
+      continue;
+    const std::string pre = sk.substr(0, sk.size() - m0.size());
+    if (!is_key_lit(pre)) continue;
+    const IrRule& c = r.children[0];
+    if (!c.has_op || c.op_name != "within" || c.op_neg || c.capture || c.multimatch || c.vars.size() != 1) continue;
+    bool tnone = true;
+    for (const auto& tf : c.transforms) tnone = tnone && lowerc(tf) == "none";
+    const IrVar& cv = c.vars[0];
+    if (!tnone || lowerc(cv.name) != "tx" || !cv.key_rx || cv.count || !cv.exc.empty() ||
+        lowerc(cv.key) != "^" + pre)
+      continue;
+    const std::string ca = lowerc(trim(c.op_arg));
+    if (ca.size() < 7 || ca.compare(0, 5, "%{tx.") != 0 || ca.back() != '}') continue;
+    const std::string list = ca.substr(5, ca.size() - 6);
+    if (!is_key_lit(list)) continue;
+    // the keys <pre>* are named by nothing but r's setvar and c's target
+    auto hits_pre = [&](const std::string& k) {  // a key (or key prefix) that can overlap <pre>*
+      return k.compare(0, pre.size(), pre) == 0 || pre.compare(0, k.size(), k) == 0;
+    };
+    for (const std::string& e : exports) {
+      std::string k = lowerc(e);
+      if (k.rfind("tx.", 0) == 0) k = k.substr(3);
+      if (k.compare(0, pre.size(), pre) == 0) ok = false;
+    }
+    std::set<std::string> values{""};  // what tx.<list> can hold
+    std::set<std::string> extra;        // foreign key regexes a filed key can meet
+    for (const IrRule* x : links) {
+      if (!ok) break;
+      for (const IrVar& v : x->vars) {
+        if (lowerc(v.name) != "tx" || x == &c) continue;
+        if (v.key.empty()) {
+          ok = false;
+        } else if (v.key_rx) {
+          const std::string k = lowerc(v.key);
+          if (k.size() > 1 && k[0] == '^' && is_key_lit(k.substr(1))) {
+            if (hits_pre(k.substr(1))) ok = false;
+            continue;
+          }
+          // an unanchored key regex F (CRS 921180's TX:/paramcounter_.*/) can match a
+          // filed key <pre>v: when every match of F starts with a literal Lf that
+          // neither occurs in <pre> nor starts inside it, and F has no context
+          // assertion, F matches <pre>v iff it matches v -- so those names stay
+          // visible too (the filter takes (?is:F) as well: a superset)
+          size_t e = 0;
+          while (e < k.size() && keychar(k[e]) && k[e] != '.') e++;
+          const std::string lf = k.substr(0, e);
+          bool straddle = lf.empty() || pre.find(lf) != std::string::npos;
+          for (size_t q = 1; q < lf.size() && q <= pre.size() && !straddle; q++)
+            if (pre.compare(pre.size() - q, q, lf, 0, q) == 0) straddle = true;  // Lf could start inside <pre>
+          if (straddle || k.find('^') != std::string::npos || k.find("\\b") != std::string::npos ||
+              k.find("\\B") != std::string::npos || k.find("\\A") != std::string::npos) {
+            ok = false;
+          } else {
+            extra.insert(v.key);
+          }
+        } else if (lowerc(v.key).compare(0, pre.size(), pre) == 0) {
+          ok = false;
+        }
+      }
+      std::vector<std::string> srcs;
+      if (x->has_op) srcs.push_back(x->op_arg);
+      for (const IrNd& a : x->nd) {
+        srcs.push_back(a.sv_value);
+        srcs.push_back(a.ctl_value);
+        if (!a.is_setvar) continue;
+        const std::string k = lowerc(a.sv_key);
+        const size_t mp = k.find("%{");
+        if (x != &r) {
+          if (mp == std::string::npos ? k.compare(0, pre.size(), pre) == 0 : hits_pre(k.substr(0, mp))) ok = false;
+          srcs.push_back(a.sv_key);
+        }
+        // the list's writers: literal values only
+        if (mp != std::string::npos ? list.compare(0, mp, k, 0, mp) == 0 : k == list) {
+          if (mp != std::string::npos) {
+            ok = false;
+          } else if (a.sv_remove) {
+            values.insert("");
+          } else {
+            const std::string& val = a.sv_value;
+            if (val.find("%{") != std::string::npos || (!val.empty() && (val[0] == '+' || val[0] == '-'))) ok = false;
+            values.insert(val);
+          }
+        }
+      }
+      for (const std::string& s : srcs)
+        for (const std::string& k : macro_keys(s))
+          if (k.empty() ? false : k.compare(0, pre.size(), pre) == 0) ok = false;
+    }
+    if (!ok) continue;
+    // the strings between two '/' of a possible list value
+    std::set<std::string> names;
+    for (const std::string& val : values) {
+      std::vector<size_t> sl;
+      for (size_t i = 0; i < val.size(); i++) {
+        if ((unsigned char)val[i] >= 0x80) ok = false;
+        if (val[i] == '/') sl.push_back(i);
+      }
+      if (sl.size() > 64) ok = false;
+      for (size_t a = 0; a < sl.size() && ok; a++)
+        for (size_t b = a + 1; b < sl.size(); b++) names.insert(val.substr(sl[a] + 1, sl[b] - sl[a] - 1));
+    }
+    if (!ok) continue;
+    std::vector<std::string> alts;
+    if (!names.empty()) {
+      std::string a = "^(?:";
+      bool first = true;
+      for (const std::string& n : names) {
+        if (!first) a += "|";
+        first = false;
+        for (char ch : n) {
+          if (ch && strchr("\\.+*?()|[]{}^$", ch)) a += '\\';
+          a += ch;
+        }
+      }
+      alts.push_back(a + ")$");
+    }
+    for (const std::string& f : extra) alts.push_back("(?is:" + f + ")");
+    if (alts.empty()) continue;  // (the chain never matches and nothing else sees the keys: nothing to gain)
+    std::string rx;
+    for (const std::string& a : alts) rx += (rx.empty() ? "" : "|") + a;
+    out[&r] = rx;
+  }
+  return out;
+}
+
 // ------------------------------------------------ constant folding
 // CRS starts phase 1 with rules that read nothing but TX variables earlier
 // rules set to constants (the 901 initialisation: `SecRule &TX:x "@eq 0"
@@ -3277,6 +3501,11 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
     // disruptive action wins (apply_actions), so nothing else is needed here.
     const std::vector<bool> gated = gated_rules(waf);
     capture_analysis(waf, exports, &L.cap_global, &L.cap_links);
+    L.pa_rx = within_chain_filters(waf, exports, L.cap_global);
+    if (timing) fprintf(stderr, "gi_compile: captures observable globally: %d\n", (int)L.cap_global);
+    if (timing)
+      for (const auto& kv : L.pa_rx)
+        fprintf(stderr, "gi_compile: rule %d: phase-A filter %zu bytes\n", kv.first->id, kv.second.size());
     for (size_t ti = 0; ti < waf.rules.size(); ti++) {
       const IrRule& r = waf.rules[ti];
       L.no_scan = gated[ti];

@@ -16,7 +16,7 @@ namespace gi {
 // even when the record layout stays the same.  gi_compile folds it into the
 // source digest and the artifact stores it, so an artifact written by another
 // compiler revision is rejected (and recompiled from the rules text).
-constexpr const char* kCompilerRev = "gi-seclang-compiler/17";
+constexpr const char* kCompilerRev = "gi-seclang-compiler/18";
 
 struct Program {
   std::vector<DRule> rules;

@@ -581,7 +581,11 @@ def _restricted_header_batch():
     macro key + a chain over TX:/^header_name_9204xx_/ @within the restricted
     list) and the 921170 / 921180 parameter counters (PL3)."""
     names = ["Proxy", "Lock-Token", "Content-Range", "If", "Accept-Charset", "X-Http-Method-Override",
-             "content-encoding", "PROXY", "If-None-Match", "Proxy-Connection", "X-Custom", "iF", "Ifx"]
+             "content-encoding", "PROXY", "If-None-Match", "Proxy-Connection", "X-Custom", "iF", "Ifx",
+             # the phase-A name filter (compile.cpp within_chain_filters): names spanning list
+             # entries, slashes, and names another TX key regex (921180's /paramcounter_.*/) can see
+             "proxy/ /lock-token", "If/ /X-Http-Method", "/proxy", "proxy/", "X-Method-Override/ /x-middleware",
+             "paramcounter_a", "X-Paramcounter_args:a", "ParamCounter_"]
     txs = []
     for i, n in enumerate(names):
         for extra in ([], [("Proxy", "b")], [(n, "again")], [("X-%d" % k, "v") for k in range(40)]):
@@ -593,10 +597,13 @@ def _restricted_header_batch():
                 t.add_request_header(k, v)
             txs.append(t)
     for uri in (b"/?a=1&a=2", b"/?a[]=1&a[]=2", b"/?a=1&b=2&A=3", b"/?x=1&x=2&x=3&y[]=1&y[]=2", b"/?q=evilmonkey"):
-        t = gpuinspect.Transaction(method=b"GET", uri=uri)
-        t.add_request_header("Host", "example.com")
-        t.add_request_header("Accept", "*/*")
-        txs.append(t)
+        for hn in (None, "paramcounter_x", "paramcounter_args:a"):
+            t = gpuinspect.Transaction(method=b"GET", uri=uri)
+            t.add_request_header("Host", "example.com")
+            t.add_request_header("Accept", "*/*")
+            if hn:
+                t.add_request_header(hn, "1")
+            txs.append(t)
     t = gpuinspect.Transaction(method=b"POST", uri=b"/form?a=1")
     t.add_request_header("Host", "example.com")
     t.add_request_header("Content-Type", "application/x-www-form-urlencoded")
