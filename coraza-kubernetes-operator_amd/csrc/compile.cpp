@@ -2403,6 +2403,7 @@ struct Lower {
     // -- exactly those that do not make the link match -- so it is always
     // evaluated by the interpreter (no phase-A bit)
     d.hit_slot = (cap_obs && r.op_neg) ? -1 : plan(r, d, &d.flags);
+    if (d.hit_slot >= 0 && pa_rx.count(&r)) d.flags2 |= RF2_PA_FILTER;
     P->rules.push_back(d);
     const uint32_t idx = (uint32_t)P->rules.size() - 1;
     if (d.hit_slot >= 0 && (d.flags & RF_RESIDUAL) && d.phase >= 2 && d.op >= 0)

@@ -220,6 +220,9 @@ enum RuleFlags2 : uint8_t {
                     // the body fields too -- its hit bits are complete there
   RF2_PA_RELAXED = 16,  // the link's phase-A automaton is a superset relaxation (its exact DFA exceeds the state
                         // cap): a phase-A hit is never an exact per-value match (k_eval re-runs the operator)
+  RF2_PA_FILTER = 32,   // (first link) the phase-A pattern is a filter stronger than the operator (compile.cpp
+                        // within_chain_filters): a value outside it has no effect but its capture record, so
+                        // with capture records on k_eval visits the link and records those values' captures only
 };
 
 enum ActKind : uint8_t {

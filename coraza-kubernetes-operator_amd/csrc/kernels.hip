@@ -1458,6 +1458,7 @@ struct Tx {
   uint32_t mcap;
   MvState* mv;               // matched-variable state (nullptr unless DProgram.mv_used)
   uint32_t* capws;           // pike_match workspace (observable captures; nullptr: none)
+  bool crec;                 // capture records are written (capws and the batch's record rows)
   uint8_t* capbuf;           // per capture group g: cap_t bytes holding TX.g's value
   uint8_t* dyn;              // TX keys macro-key setvars created (DynHdr; nullptr: the program has none)
   uint64_t wm0, wm1;         // TX slots < 128 this request owns (written); the others read the snapshot
@@ -4350,12 +4351,15 @@ GI_HD __forceinline__ uint32_t field_filter(Tx& t, const DRule& R, const DVarRef
   uint32_t hres = 2;
   if (vskip && f < t.nf_pa && fl.kind <= FK_FILE_SIZE) {  // phase-A item kinds only
     const uint32_t vb = 2 * f + (*names ? 1u : 0u);
-    if (!((t.vmap[vb] >> ((uint32_t)R.hit_slot & 31u)) & 1u)) return 0;
-    if (vexact) {
+    // a value a filter link's phase-A pattern rejects: only its capture record (3), or nothing
+    const uint32_t out = ((R.flags2 & RF2_PA_FILTER) && t.crec) ? 3u : 0u;
+    if (!((t.vmap[vb] >> ((uint32_t)R.hit_slot & 31u)) & 1u)) hres = out;
+    else if (vexact) {
       hres = hset_lookup(t.hset, t.hmask, (uint32_t)R.hit_slot, vb);
-      if (!hres) return 0;
-      if (R.flags2 & RF2_PA_RELAXED) hres = 2;  // a superset automaton's hit: evaluate the value
+      if (!hres) hres = out;
+      else if (R.flags2 & RF2_PA_RELAXED) hres = 2;  // a superset automaton's hit: evaluate the value
     }
+    if (!hres) return 0;
   }
   if (vr.key_mode == 1) {
     if (vr.ci ? !eq_ascii_ci(fl.k, fl.kn, P.strpool + vr.key_off, vr.key_len)
@@ -4386,7 +4390,8 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
   // bit (match or "maybe") falls through to the full evaluation below.
   if (R.hit_slot >= 0 && !t.pa_void && !bodydep_void(t, R)) {
     const uint32_t w = t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride];
-    if (!((w >> (R.hit_slot & 31)) & 1u)) {
+    if (!((w >> (R.hit_slot & 31)) & 1u) && !((R.flags2 & RF2_PA_FILTER) && t.crec)) {
+      // (a filter link with capture records on walks its values for their records: field_filter)
       if (!(R.flags & RF_RESIDUAL)) return 0;
       // phase A cleared every other target: only the residual (body-phase)
       // singles can match; test them without side effects, and evaluate the
@@ -4455,7 +4460,7 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
     const uint8_t* cv = nullptr;
     const uint8_t* ck = nullptr;
     uint32_t cvn = 0, cvar = 0, ckn = 0;
-    bool cex = false, have = false;
+    bool cex = false, conly = false, have = false;
     while (!have) {
       if (!in_var) {
         if (vi >= R.var_count) break;
@@ -4640,6 +4645,7 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
             ck = fl.k;
             ckn = fl.kn;
             cex = hres == 1;
+            conly = hres == 3;
             have = true;
             continue;
           }
@@ -4661,6 +4667,7 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
             ck = fl.k;
             ckn = fl.kn;
             cex = hb == 1;
+            conly = hb == 3;
             have = true;
             continue;
           }
@@ -4701,6 +4708,14 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
       }
     }
     if (!have) break;
+    if (conly) {  // RF2_PA_FILTER: the value changes nothing but the capture records
+      if (!((const CapHdr*)t.capws)->trunc) {
+        bool ok;
+        const Str tv = transform(t, R, cv, cvn, &ok);
+        if (ok) t.flags |= run_capture(*t.P, t.capws, t.capbuf, t.cap_t, t.slots, t.n_req, t.cur_id, o.pike, tv.p, tv.n);
+      }
+      continue;
+    }
     nmatch += test_value(t, R, o, cv, cvn, cvar, ck, ckn, cex);
   }
   return nmatch;
@@ -4766,7 +4781,8 @@ GI_HD __forceinline__ bool rule_noop(Tx& t, const DRule& R, uint32_t ri) {
   if (R.flags & RF_MARKER) return true;
   if ((R.flags & RF_CONST) && R._pad2 == 0) return true;  // a folded link that matches nothing
   return R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !bodydep_void(t, R) &&
-         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u);
+         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u) &&
+         !((R.flags2 & RF2_PA_FILTER) && t.crec);
 }
 
 // RuleGroup.Eval [upstream corazawaf/rulegroup.go]
@@ -4848,8 +4864,9 @@ GI_HD __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
       t.mv->nb = 0;
     }
     if (R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !bodydep_void(t, R) &&
-        !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u))
-      continue;  // phase A proved the first link matches nothing
+        !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u) &&
+        !((R.flags2 & RF2_PA_FILTER) && t.crec))
+      continue;  // phase A proved the first link matches nothing (a filter link: and records no capture)
     if ((R.flags & RF_CONST) && R._pad2 == 0) continue;  // folded: matches nothing for any request
     if (t.prefix && (R.flags2 & RF2_BODY_PA)) {  // needs the body's phase-A scan: the first stage ends here
       t.bail = true;
@@ -7353,6 +7370,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
     CH->bytes_cap = B.cbcap;
     CH->trunc = 0;
   }
+  t.crec = t.capws && B.caprec;
   t.mcap = B.mcap;
   // TX: copy on write over the folded snapshot; slots >= 128 and the capture
   // groups (run_capture writes those directly) start owned and unset

@@ -1417,7 +1417,7 @@ int gi_sync(gi_ctx* c) {
           std::vector<std::pair<unsigned long long, uint32_t>> v;
           for (uint32_t i = 0; i < 1000 && i < c->rs->prog.rules.size(); i++) v.push_back({rc[i], i});
           std::sort(v.rbegin(), v.rend());
-          for (int k = 0; k < 12 && k < (int)v.size(); k++) {
+          for (int k = 0; k < 40 && k < (int)v.size(); k++) {
             const DRule& R = c->rs->prog.rules[v[k].second];
             fprintf(stderr, "  rule link %u id %d phase %d hit_slot %d op %d vars %u chain %u: %.0f cyc/req\n",
                     v[k].second, R.id, R.phase, R.hit_slot, R.op >= 0 ? c->rs->prog.ops[R.op].kind : -1,

@@ -8,5 +8,5 @@ TAG=${TAG:-prof}
 for c in ${CONFIGS:-c2 c4}; do
   echo "== $c $(date +%T)"
   GI_PROF=1 timeout -k 10 300 python -u bench.py --config $c --steps 1 --warmup 1 --no-cpu-baseline ${ARGS:-} > gpurun_out/${TAG}_prof_${c}_bench.json 2> gpurun_out/${TAG}_prof_${c}.err || { tail -20 gpurun_out/${TAG}_prof_${c}.err; exit 1; }
-  grep GI_PROF -A13 gpurun_out/${TAG}_prof_${c}.err | tail -40
+  grep GI_PROF -A41 gpurun_out/${TAG}_prof_${c}.err | tail -40
 done
