@@ -98,12 +98,15 @@ class RuleSetEntry:
         return d
 
     def size(self) -> int:
-        """Bytes the entry holds: len(Rules) as cache.go:113-124 counts it,
-        plus the string fields of the GPU artifact stored beside it (the
-        reference stores no artifact; its base64 program -- automata included,
-        often larger than the rules text -- must count against the same
-        SizeLimit or PruneBySize would not bound the cache's memory)."""
-        return len(self.rules) + sum(len(v) for v in self.artifact.values() if isinstance(v, (str, bytes)))
+        """len(Rules), exactly as cache.go:113-124 (TotalSize) and
+        cache.go:188-220 (PruneBySize) count an entry: the same SizeLimit
+        prunes the same entries as the reference does."""
+        return len(self.rules)
+
+    def artifact_size(self) -> int:
+        """Bytes of the GPU artifact's string fields stored beside the entry
+        (not part of the reference's accounting: RuleSetCache.artifact_bytes)."""
+        return sum(len(v) for v in self.artifact.values() if isinstance(v, (str, bytes)))
 
 
 class RuleSetCache:
@@ -170,8 +173,22 @@ class RuleSetCache:
             return list(self._entries)
 
     def total_size(self) -> int:
+        """cache.go:113-124: the sum of len(Rules) over every stored entry."""
         with self._mu:
             return sum(e.size() for _, ents in self._entries.values() for e in ents)
+
+    def artifact_bytes(self) -> int:
+        """Memory the GPU artifacts hold, tracked apart from total_size (the
+        reference has no artifact).  An artifact reused by several entries
+        (unchanged rules, _artifact_of) is one object and counts once."""
+        with self._mu:
+            seen = {}  # the reused artifact's fields are the same string objects
+            for _, ents in self._entries.values():
+                for e in ents:
+                    for v in e.artifact.values():
+                        if isinstance(v, (str, bytes)):
+                            seen[id(v)] = len(v)
+            return sum(seen.values())
 
     def set_entry_timestamp(self, instance: str, index: int, timestamp_ns: int) -> None:
         with self._mu:
@@ -201,9 +218,9 @@ class RuleSetCache:
             return pruned
 
     def prune_by_size(self, max_size: int) -> int:
-        """Drop the oldest entries (instance by instance) until the total
-        entry size (RuleSetEntry.size) is at most max_size, never an
-        instance's latest."""
+        """cache.go:188-220: drop the oldest entries (instance by instance)
+        until the total len(Rules) is at most max_size, never an instance's
+        latest."""
         with self._mu:
             cur = sum(e.size() for _, ents in self._entries.values() for e in ents)
             if cur <= max_size:

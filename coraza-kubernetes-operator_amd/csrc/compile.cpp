@@ -3502,7 +3502,8 @@ int compile_program(const std::string& text, const std::vector<std::string>& exp
     // disruptive action wins (apply_actions), so nothing else is needed here.
     const std::vector<bool> gated = gated_rules(waf);
     capture_analysis(waf, exports, &L.cap_global, &L.cap_links);
-    L.pa_rx = within_chain_filters(waf, exports, L.cap_global);
+    static const bool pa_filter_env = !(getenv("GI_PA_FILTER") && atoi(getenv("GI_PA_FILTER")) == 0);  // A/B knob
+    if (pa_filter_env) L.pa_rx = within_chain_filters(waf, exports, L.cap_global);
     if (timing) fprintf(stderr, "gi_compile: captures observable globally: %d\n", (int)L.cap_global);
     if (timing)
       for (const auto& kv : L.pa_rx)

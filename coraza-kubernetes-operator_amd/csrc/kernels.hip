@@ -1465,7 +1465,7 @@ struct Tx {
   bool snap;                 // the folded prefix ran (phase 1 started): unowned slots read DProgram.tx_snap
   uint32_t cur_id;           // id of the top-level rule being evaluated (capture records)
   bool profon;               // GI_PROF counters (diagnostics)
-  uint32_t prof_visits, prof_evals, prof_rules;
+  uint32_t prof_visits, prof_evals, prof_rules, prof_ops;
   uint64_t prof_eval_cyc, prof_act_cyc;
   unsigned long long* prof_rule_cyc;  // [rule link] cycles (GI_PROF)
 };
@@ -4295,6 +4295,7 @@ GI_HD __forceinline__ uint32_t test_value(Tx& t, const DRule& R, const DOp& o, c
   // lost while other lanes of the wave took the identity path).
   for (bool fresh = true;; k++) {
     if (fresh) {
+      if (t.profon && !exact) t.prof_ops++;
       const bool hit = exact || eval_op(t, o, cp, cn);
       // capturing @rx: a value the regex matches writes TX.0-TX.8 -- for a
       // negated operator exactly the values that do not make the link match
@@ -4736,11 +4737,16 @@ GI_HD __forceinline__ void eval_top(Tx& t, uint32_t ri) {
   for (int32_t ci = (int32_t)ri; ci >= 0;) {
     const DRule C = gi_cload(P.rules, (uint64_t)ci);
     const uint64_t c0 = t.profon ? gi_clock() : 0;
+    const uint32_t o0 = t.prof_ops;
     const uint32_t nm = eval_rule<W>(t, C);
     if (t.profon) {
       const uint64_t dc = gi_clock() - c0;
       t.prof_eval_cyc += dc;
-      if (ci < 1000) gi_prof_add(&t.prof_rule_cyc[ci], (unsigned long long)dc);
+      if (ci < 1000) {  // cycles, lanes entering, operator runs (not phase-A exact) per link
+        gi_prof_add(&t.prof_rule_cyc[ci], (unsigned long long)dc);
+        gi_prof_add(&t.prof_rule_cyc[1000 + ci], 1ull);
+        gi_prof_add(&t.prof_rule_cyc[2000 + ci], (unsigned long long)(t.prof_ops - o0));
+      }
     }
     if (nm == 0) return;
     ci = C.chain_next;
@@ -7311,7 +7317,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
   Region g = region_of(P, B, r);
   ReqHdr* H = g.hdr;
   Tx t;
-  t.prof_visits = t.prof_evals = t.prof_rules = 0;
+  t.prof_visits = t.prof_evals = t.prof_rules = t.prof_ops = 0;
   t.prof_eval_cyc = t.prof_act_cyc = 0;
   const bool lead = !W || (gi_tid() & 63u) == 0;  // the lane that writes shared counters
   t.profon = B.prof != nullptr && lead;
@@ -7634,6 +7640,62 @@ GI_HD __forceinline__ bool eval_heavy(const DProgram& P, const DBatch& B, uint32
   return B.wave_fields && H->nf + H->n_post >= B.wave_fields;
 }
 
+// k_eval's request order.  A wave of k_eval runs its 64 requests' rule walks
+// in lockstep, so one request with many set hit bits (an attack: detectors,
+// chains and actions to re-run) holds the other 63 lanes; with 5 % attacks
+// nearly every wave has one.  Grouping requests by their number of set
+// phase-A hit bits (a counting sort into GI_EORD_BINS bins; void requests,
+// which evaluate every link, in the last) gives waves of like requests.  The
+// order changes no result: each request is evaluated on its own.
+GI_HD __forceinline__ uint32_t eord_key(const DBatch& B, uint32_t r) {
+  const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
+  if (H->pa_void) return GI_EORD_BINS - 1;
+  const uint32_t nw = (B.n_hit_slots + 31) / 32;
+  uint32_t c = 0;
+  for (uint32_t w = 0; w < nw; w++) c += __popc(B.hits[(uint64_t)w * B.rstride + r]);
+  return min(c, (uint32_t)GI_EORD_BINS - 2);
+}
+__global__ void __launch_bounds__(256) k_eord_count(DBatch B) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t key = r < B.n_req ? (int32_t)eord_key(B, r) : -1;
+  uint64_t active = __ballot(key >= 0);
+  while (active) {  // one atomic per distinct key in the wave
+    const int leader = __ffsll((unsigned long long)active) - 1;
+    const int32_t lk = __shfl(key, leader, 64);
+    const uint64_t same = __ballot(key == lk) & active;
+    if (lane_id() == (uint32_t)leader) atomicAdd(&B.eord_bins[lk], (uint32_t)__popcll(same));
+    active &= ~same;
+  }
+}
+__global__ void __launch_bounds__(256) k_eord_scatter(DBatch B) {
+  __shared__ uint32_t base[GI_EORD_BINS];
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    for (uint32_t k = 0; k < GI_EORD_BINS; k++) {
+      base[k] = a;
+      a += B.eord_bins[k];
+    }
+  }
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t key = r < B.n_req ? (int32_t)eord_key(B, r) : -1;
+  // wave-aggregated cursor claims: one atomic per distinct key in the wave
+  uint64_t active = __ballot(key >= 0);
+  while (active) {
+    const int leader = __ffsll((unsigned long long)active) - 1;
+    const int32_t lk = __shfl(key, leader, 64);
+    const uint64_t same = __ballot(key == lk) & active;
+    uint32_t first = 0;
+    if (lane_id() == (uint32_t)leader) first = atomicAdd(&B.eord_bins[GI_EORD_BINS + lk], (uint32_t)__popcll(same));
+    first = (uint32_t)__shfl((int)first, leader, 64);
+    if (key == lk) {
+      const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane_id()) - 1ull));
+      B.eorder[base[lk] + first + rank] = r;
+    }
+    active &= ~same;
+  }
+}
+
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVAL_WPE, 8))) k_eval(DProgram P, DBatch B) {
   __shared__ unsigned long long red[7];
   // the block's hit words in LDS ([word][thread]): the rule walk tests one per
@@ -7643,15 +7705,14 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GI_EVA
   if (threadIdx.x < 7) red[threadIdx.x] = 0;
   const uint32_t nw = (B.n_hit_slots + 31) / 32;
   const bool in_lds = nw <= GI_EVAL_LDS_WORDS && blockDim.x <= 128;
-  {
-    const uint32_t rl = B.stage == 2 ? (r < *B.pcount ? B.plist[r] : 0xFFFFFFFFu) : r;
-    if (in_lds && rl < B.n_req)
-      for (uint32_t w = 0; w < nw; w++) lhits[w * blockDim.x + threadIdx.x] = B.hits[(uint64_t)w * B.rstride + rl];
-  }
+  // the gate's body stage: the pending requests of the phase-1 stage, in its
+  // list; otherwise k_eord's order when there is one
+  const uint32_t rr = B.stage == 2 ? (r < *B.pcount ? B.plist[r] : 0xFFFFFFFFu)
+                      : (B.eorder && r < B.n_req) ? B.eorder[r] : r;
+  if (in_lds && rr < B.n_req)
+    for (uint32_t w = 0; w < nw; w++) lhits[w * blockDim.x + threadIdx.x] = B.hits[(uint64_t)w * B.rstride + rr];
   __syncthreads();
   unsigned long long my[7] = {0, 0, 0, 0, 0, 0, 0};
-  // the gate's body stage: the pending requests of the phase-1 stage, in its list
-  const uint32_t rr = B.stage == 2 ? (r < *B.pcount ? B.plist[r] : 0xFFFFFFFFu) : r;
   if (rr < B.n_req) {
     if (eval_heavy(P, B, rr)) B.wlist[atomicAdd(B.wcount, 1u)] = rr;
     else eval_request<false>(P, B, rr, in_lds ? lhits + threadIdx.x : nullptr, blockDim.x, my);
@@ -7873,12 +7934,20 @@ static void launch_phase_a(const DProgram& P, const DBatch& B, const ScanLaunch&
 
 static void launch_eval(const DProgram& P, const DBatch& B, hipStream_t stream, int stop_after, LaunchLog* log,
                         int& nk) {
+  DBatch Be = B;
+  if (B.n_req < 4096 || B.stage == 2) Be.eorder = nullptr;  // (a small batch: its few waves gain nothing)
+  if (Be.eorder) {
+    const uint32_t cb = (B.n_req + 255) / 256;
+    (void)hipMemsetAsync(B.eord_bins, 0, 8 * GI_EORD_BINS, stream);
+    GI_LAUNCH(B.stage == 1 ? "k_eord_count.1" : "k_eord_count", k_eord_count, dim3(cb), dim3(256), 0, stream, B);
+    GI_LAUNCH(B.stage == 1 ? "k_eord_scatter.1" : "k_eord_scatter", k_eord_scatter, dim3(cb), dim3(256), 0, stream, B);
+  }
   {  // small batches (fewer than 4 workgroups of 128 per CU): one wave per workgroup to spread over all CUs
     // GI_EVAL_BS A/B (C2, 1M): 128 threads 26.2 ms, 64 threads 32.1 ms
     static const uint32_t ev_env = getenv("GI_EVAL_BS") ? (uint32_t)atoi(getenv("GI_EVAL_BS")) : 0u;
     const uint32_t ev_bs = (ev_env == 64 || ev_env == 128) ? ev_env : (B.n_req + 127) / 128 < 1024 ? 64u : 128u;
     GI_LAUNCH(B.stage == 2 ? "k_eval.2" : "k_eval", k_eval, dim3((B.n_req + ev_bs - 1) / ev_bs), dim3(ev_bs), 0, stream, P,
-              B);
+              Be);
   }
   if (B.wlist) {  // heavy requests, one wave each (persistent over k_eval's list)
     const uint32_t nw = (B.n_hit_slots + 31) / 32;

@@ -94,6 +94,7 @@ struct gi_ctx {
   // phase A
   DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf, wlist;
   DevBuf pend, plist;  // phase-1 gate (launch_pipeline): pending flags + list
+  DevBuf eorder;       // k_eval's request order (k_eord_*: requests grouped by phase-A hit count)
   DevBuf dmemo_keys, dmemo_info;  // k_detect's detector-result memo
   uint32_t dmemo_mask = 0;
   uint32_t long_cap = 0, long_grid = GI_LONG_GRID;
@@ -644,7 +645,7 @@ void gi_ctx_free(gi_ctx* c) {
   for (DevBuf* b : {&c->caprec, &c->capbytes, &c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->hset, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist, &c->pend, &c->plist, &c->dmemo_keys, &c->dmemo_info,
-                    &c->cappool, &c->progdev})
+                    &c->eorder, &c->cappool, &c->progdev})
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
@@ -1110,6 +1111,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   // k_eval -> k_eval_wave request list (its counter lives in ctr)
   if ((e = c->ctr.ensure(4096 + 8ull * ((4 * GI_NCLS + 63) & ~63))) != hipSuccess) return hip_fail(c, e, "alloc counters");
   if ((e = c->wlist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc wave list");
+  if ((e = c->eorder.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc eval order");
   if ((e = c->pend.ensure(std::max<uint64_t>(n, 16))) != hipSuccess) return hip_fail(c, e, "alloc gate flags");
   if ((e = c->plist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc gate list");
   const auto t_h2d0 = std::chrono::steady_clock::now();
@@ -1223,9 +1225,9 @@ int gi_run_staged(gi_ctx* c) {
     B.dmemo_min = dm_min_env;
     B.diag = nullptr;
     B.prof = nullptr;
-    if (c->prof_on && c->prof.ensure(1024 + 8000) == hipSuccess) {
+    if (c->prof_on && c->prof.ensure(1024 + 24000) == hipSuccess) {
       B.prof = (unsigned long long*)c->prof.p;
-      (void)hipMemsetAsync(c->prof.p, 0, 1024 + 8000, c->stream);
+      (void)hipMemsetAsync(c->prof.p, 0, 1024 + 24000, c->stream);
     }
     B.items_cap = c->items_cap;
     B.n_hit_slots = c->rs->prog.n_hit_slots;
@@ -1248,6 +1250,10 @@ int gi_run_staged(gi_ctx* c) {
     B.pend = (uint8_t*)c->pend.p;
     B.plist = (uint32_t*)c->plist.p;
     B.pcount = (uint32_t*)(cp + 512);
+    // k_eval's request order (GI_EVAL_ORDER=0: identity): bins + cursors at ctr[1024, 1024 + 8 * GI_EORD_BINS)
+    static const bool eord_env = !(getenv("GI_EVAL_ORDER") && atoi(getenv("GI_EVAL_ORDER")) == 0);
+    B.eorder = eord_env ? (uint32_t*)c->eorder.p : nullptr;
+    B.eord_bins = (uint32_t*)(cp + 1024);
     static const uint32_t tiles_env = getenv("GI_BODY_TILES") ? (uint32_t)atoi(getenv("GI_BODY_TILES")) : 1u;
     B.body_tiles = tiles_env;
     static const uint32_t ws2_env = getenv("GI_EVAL_WAVE_STAGE2") ? (uint32_t)atoi(getenv("GI_EVAL_WAVE_STAGE2")) : 1u;
@@ -1297,6 +1303,7 @@ int gi_run_staged(gi_ctx* c) {
     Bc.txslots = (Slot*)((uint8_t*)B.txslots + (uint64_t)GI_SLOT_BYTES * ch.r0);
     Bc.body_list = B.body_list + ch.blist_off;
     Bc.pend = B.pend ? B.pend + ch.r0 : nullptr;
+    Bc.eorder = B.eorder ? B.eorder + ch.r0 : nullptr;
     Bc.n_body = ch.n_body;
     Bc.n_mp_body = ch.n_mp;
     launch_pipeline(c->prog, Bc, c->scan, c->stream, c->evs, c->stop_after, &c->log,
@@ -1412,16 +1419,19 @@ int gi_sync(gi_ctx* c) {
                 "GI_PROF k_eval_wave per request: fields filtered %.1f, survivors exact %.1f / evaluated %.1f; "
                 "filter %.0f cyc, ordered tests %.0f cyc\n",
                 h[17] / n, h[18] / n, h[19] / n, h[20] / n, h[21] / n);
-        std::vector<unsigned long long> rc(1000);
-        if (hipMemcpy(rc.data(), (uint8_t*)c->prof.p + 1024, 8000, hipMemcpyDeviceToHost) == hipSuccess) {
+        std::vector<unsigned long long> rc(3000);
+        if (hipMemcpy(rc.data(), (uint8_t*)c->prof.p + 1024, 24000, hipMemcpyDeviceToHost) == hipSuccess) {
           std::vector<std::pair<unsigned long long, uint32_t>> v;
           for (uint32_t i = 0; i < 1000 && i < c->rs->prog.rules.size(); i++) v.push_back({rc[i], i});
           std::sort(v.rbegin(), v.rend());
           for (int k = 0; k < 40 && k < (int)v.size(); k++) {
             const DRule& R = c->rs->prog.rules[v[k].second];
-            fprintf(stderr, "  rule link %u id %d phase %d hit_slot %d op %d vars %u chain %u: %.0f cyc/req\n",
+            const double ent = (double)rc[1000 + v[k].second];
+            fprintf(stderr, "  rule link %u id %d phase %d hit_slot %d op %d vars %u chain %u: %.0f cyc/req; "
+                    "entered by %.1f%% of requests, %.0f cyc and %.2f operator runs per entry\n",
                     v[k].second, R.id, R.phase, R.hit_slot, R.op >= 0 ? c->rs->prog.ops[R.op].kind : -1,
-                    R.var_count, R.tchain_len, v[k].first / n);
+                    R.var_count, R.tchain_len, v[k].first / n, 100.0 * ent / n, ent > 0 ? v[k].first / ent : 0.0,
+                    ent > 0 ? rc[2000 + v[k].second] / ent : 0.0);
           }
         }
       }

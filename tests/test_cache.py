@@ -294,15 +294,17 @@ def test_cache_concurrent_put_get():
     assert all(c.get("i%d" % k).rules == "r199" for k in range(4))
 
 
-def test_artifact_reused_for_unchanged_rules_and_counted_in_size():
+def test_artifact_reused_for_unchanged_rules_and_counted_apart():
     """A reconcile with unchanged rules (ruleset_controller.go:181 Puts every
-    time) reuses the stored artifact instead of recompiling; the artifact's
-    bytes count against the size limit (RuleSetEntry.size)."""
+    time) reuses the stored artifact instead of recompiling.  Sizes follow the
+    reference: total_size / prune_by_size count len(Rules) only
+    (cache.go:113-124, 188-220); the artifacts' memory is tracked apart, a
+    shared artifact once."""
     calls = []
 
     def emitter(rules):
         calls.append(rules)
-        return {"gpu_artifact": "A" * 100, "gpu_artifact_version": 1}
+        return {"gpu_artifact": rules.ljust(100, "A"), "gpu_artifact_version": 1}
 
     c = C.RuleSetCache(emitter=emitter)
     a = c.put("ns/r", "rules-v1")
@@ -310,9 +312,12 @@ def test_artifact_reused_for_unchanged_rules_and_counted_in_size():
     assert a.uuid != b.uuid and b.artifact == a.artifact and calls == ["rules-v1"]
     c.put("ns/r", "rules-v2")
     assert calls == ["rules-v1", "rules-v2"]
-    assert c.total_size() == 3 * (8 + 100)
-    # the size limit now bounds the artifacts too: the two old entries go
-    assert c.prune_by_size(150) == 2 and c.count_entries("ns/r") == 1
+    assert c.total_size() == 3 * 8
+    assert c.artifact_bytes() == 2 * 100  # v1's artifact is shared by two entries
+    # the reference's SizeLimit semantics: 24 bytes of rules fit 24, 16 prunes the two old entries
+    assert c.prune_by_size(24) == 0
+    assert c.prune_by_size(16) == 2 and c.count_entries("ns/r") == 1
+    assert c.artifact_bytes() == 100
     # another instance with the same text compiles its own (no cross-instance sharing)
     c.put("ns/other", "rules-v2")
     assert calls[-1] == "rules-v2" and len(calls) == 3
