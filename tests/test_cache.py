@@ -314,9 +314,9 @@ def test_artifact_reused_for_unchanged_rules_and_counted_apart():
     assert calls == ["rules-v1", "rules-v2"]
     assert c.total_size() == 3 * 8
     assert c.artifact_bytes() == 2 * 100  # v1's artifact is shared by two entries
-    # the reference's SizeLimit semantics: 24 bytes of rules fit 24, 16 prunes the two old entries
+    # the reference's SizeLimit semantics: 24 bytes of rules fit 24, 8 prunes the two old entries
     assert c.prune_by_size(24) == 0
-    assert c.prune_by_size(16) == 2 and c.count_entries("ns/r") == 1
+    assert c.prune_by_size(8) == 2 and c.count_entries("ns/r") == 1
     assert c.artifact_bytes() == 100
     # another instance with the same text compiles its own (no cross-instance sharing)
     c.put("ns/other", "rules-v2")
