@@ -1719,18 +1719,18 @@ struct Lower {
   std::set<const IrRule*> cap_links;
   std::map<const IrRule*, std::string> pa_rx;  // first link -> its phase-A pattern (within_chain_filters)
 
-  int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags) {
+  int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags, uint8_t* flags2) {
     if (!r.has_op || no_scan) return -1;
     const std::string& n = r.op_name;
     bool scannable = n == "rx" || n == "pm" || n == "pmfromfile" || n == "validatebyterange" || n == "validateurlencoding" ||
                      n == "validateutf8encoding" || n == "detectsqli" || n == "detectxss" ||
                      (n == "contains" && r.op_arg.find("%{") == std::string::npos);
     if (!scannable) return -1;
-    bool bodydep = false, residual = false;
+    bool bodydep = false, residual = false, res_single = false;
     for (auto& v : r.vars) {
       if (v.count) return -1;
       int sid = single_id(v.name);
-      if (sid >= 0 && !immutable_single(sid)) residual = true;  // tested by k_eval on a clear bit
+      if (sid >= 0 && !immutable_single(sid)) residual = res_single = true;  // tested by k_eval on a clear bit
       if (sid < 0 && v.name == "TX") return -1;
       if (v.name.rfind("MATCHED_VAR", 0) == 0) return -1;  // transaction state, not a request variable
       if (residual_collection(v.name)) residual = true;  // body collections phase A does not scan
@@ -1756,6 +1756,7 @@ struct Lower {
     const int32_t slot = (int32_t)P->n_hit_slots++;
     if (bodydep) *flags |= RF_BODYDEP;
     if (residual) *flags |= RF_RESIDUAL;
+    if (residual && !res_single) *flags2 |= RF2_RESID_COLL;  // only body collections: empty without such a body
     const DOp& o = P->ops[d.op];
     DVarRef* vrs = &P->vars[d.var_begin];
     for (uint32_t vi = 0; vi < d.var_count; vi++) {
@@ -2402,7 +2403,7 @@ struct Lower {
     // a negated capturing link writes captures on values whose regex matches
     // -- exactly those that do not make the link match -- so it is always
     // evaluated by the interpreter (no phase-A bit)
-    d.hit_slot = (cap_obs && r.op_neg) ? -1 : plan(r, d, &d.flags);
+    d.hit_slot = (cap_obs && r.op_neg) ? -1 : plan(r, d, &d.flags, &d.flags2);
     if (d.hit_slot >= 0 && pa_rx.count(&r)) d.flags2 |= RF2_PA_FILTER;
     P->rules.push_back(d);
     const uint32_t idx = (uint32_t)P->rules.size() - 1;
@@ -2617,8 +2618,8 @@ static void capture_analysis(const IrWaf& waf, const std::vector<std::string>& e
 // capture and setvar in Coraza's order, so the chain sees the same keys it
 // would have matched).  Conditions (anything else: no override):
 //  * no capture group is observable outside its feeding chains (cap_global);
-//  * the first link: @rx "^.*$", not negated, no multiMatch, last
-//    transformation t:lowercase (so equal keys mean equal values), collection
+//  * the first link: @rx "^.*$", not negated, no multiMatch, transformations
+//    t:none / t:lowercase ending in t:lowercase (so equal keys mean equal values), collection
 //    targets only (no TX, no MATCHED_*, no counts), one setvar
 //    'tx.<P>%{tx.0}=/%{tx.0}/' and no ctl, exactly one chained link;
 //  * the chained link: TX:/^<P>/ with <P> a plain key literal, @within
@@ -2685,7 +2686,11 @@ static std::map<const IrRule*, std::string> within_chain_filters(const IrWaf& wa
   const std::string m0 = "%{tx.0}";
   for (const IrRule& r : waf.rules) {
     if (!r.has_op || r.op_name != "rx" || r.op_neg || r.op_arg != "^.*$" || !r.capture || r.multimatch) continue;
-    if (r.transforms.empty() || lowerc(r.transforms.back()) != "lowercase") continue;
+    // t:lowercase last, and nothing but t:none / t:lowercase (k_eval records the
+    // captures of the names the filter rejects by lowercasing them inline)
+    bool lc_only = !r.transforms.empty() && lowerc(r.transforms.back()) == "lowercase";
+    for (const auto& tf : r.transforms) lc_only = lc_only && (lowerc(tf) == "lowercase" || lowerc(tf) == "none");
+    if (!lc_only) continue;
     if (r.children.size() != 1 || r.nd.size() != 1 || !r.nd[0].is_setvar || r.nd[0].sv_remove) continue;
     bool ok = !r.vars.empty();
     for (const IrVar& v : r.vars) {

@@ -223,6 +223,10 @@ enum RuleFlags2 : uint8_t {
   RF2_PA_FILTER = 32,   // (first link) the phase-A pattern is a filter stronger than the operator (compile.cpp
                         // within_chain_filters): a value outside it has no effect but its capture record, so
                         // with capture records on k_eval visits the link and records those values' captures only
+                        // (the link captures the whole value through t:lowercase: recorded inline)
+  RF2_RESID_COLL = 64,  // RF_RESIDUAL only through body collections phase A does not scan (XML, part headers,
+                        // FILES_TMPNAMES): empty -- so a clear bit is final -- unless the request's body went
+                        // through the XML or multipart processor
 };
 
 enum ActKind : uint8_t {

@@ -1459,6 +1459,8 @@ struct Tx {
   MvState* mv;               // matched-variable state (nullptr unless DProgram.mv_used)
   uint32_t* capws;           // pike_match workspace (observable captures; nullptr: none)
   bool crec;                 // capture records are written (capws and the batch's record rows)
+  bool rcoll;                // the body went through the XML / multipart processor: residual body collections
+                             // (RF2_RESID_COLL) may have entries
   uint8_t* capbuf;           // per capture group g: cap_t bytes holding TX.g's value
   uint8_t* dyn;              // TX keys macro-key setvars created (DynHdr; nullptr: the program has none)
   uint64_t wm0, wm1;         // TX slots < 128 this request owns (written); the others read the snapshot
@@ -4179,6 +4181,12 @@ GI_HD __forceinline__ bool bodydep_void(const Tx& t, const DRule& R) {
   return (R.flags & RF_BODYDEP) && t.has_post && !(t.prefix_spec && (R.flags2 & RF2_PREFIX));
 }
 
+// A clear hit bit does not settle the link: some residual target (a mutable
+// single, or a body collection the request actually has) is still to test.
+GI_HD __forceinline__ bool residual_live(const Tx& t, const DRule& R) {
+  return (R.flags & RF_RESIDUAL) && (t.rcoll || !(R.flags2 & RF2_RESID_COLL));
+}
+
 GI_HD __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
   const DProgram& P = *t.P;
   for (uint32_t e = 0; e < vr.exc_count; e++) {
@@ -4393,7 +4401,7 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
     const uint32_t w = t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride];
     if (!((w >> (R.hit_slot & 31)) & 1u) && !((R.flags2 & RF2_PA_FILTER) && t.crec)) {
       // (a filter link with capture records on walks its values for their records: field_filter)
-      if (!(R.flags & RF_RESIDUAL)) return 0;
+      if (!residual_live(t, R)) return 0;
       // phase A cleared every other target: only the residual (body-phase)
       // singles can match; test them without side effects, and evaluate the
       // whole link in order only if one does
@@ -4710,10 +4718,32 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
     }
     if (!have) break;
     if (conly) {  // RF2_PA_FILTER: the value changes nothing but the capture records
-      if (!((const CapHdr*)t.capws)->trunc) {
-        bool ok;
-        const Str tv = transform(t, R, cv, cvn, &ok);
-        if (ok) t.flags |= run_capture(*t.P, t.capws, t.capbuf, t.cap_t, t.slots, t.n_req, t.cur_id, o.pike, tv.p, tv.n);
+      CapHdr* CH = (CapHdr*)t.capws;
+      if (!CH->trunc) {
+        bool ascii = cvn <= t.cap_t;
+        for (uint32_t i = 0; i < cvn && ascii; i++) ascii = cv[i] < 0x80;
+        if (ascii) {
+          // the link captures the whole t:lowercase value (compile.cpp within_chain_filters):
+          // lowercase straight into the record row -- run_capture's record, without the call
+          // or the TX.0 copy nobody reads (captures are not observable outside this chain)
+          if (CH->nrec < CH->rec_cap && CH->nbytes + cvn <= CH->bytes_cap) {
+            uint8_t* d = CH->bytes + CH->nbytes;
+            for (uint32_t i = 0; i < cvn; i++) d[i] = (cv[i] >= 'A' && cv[i] <= 'Z') ? (uint8_t)(cv[i] + 32) : cv[i];
+            uint32_t* rr = CH->rec + 4ull * CH->nrec;
+            rr[0] = t.cur_id;
+            rr[1] = 0u;
+            rr[2] = CH->nbytes;
+            rr[3] = cvn;
+            CH->nbytes += cvn;
+            CH->nrec++;
+          } else {
+            CH->trunc = 1;
+          }
+        } else {
+          bool ok;
+          const Str tv = transform(t, R, cv, cvn, &ok);
+          if (ok) t.flags |= run_capture(*t.P, t.capws, t.capbuf, t.cap_t, t.slots, t.n_req, t.cur_id, o.pike, tv.p, tv.n);
+        }
       }
       continue;
     }
@@ -4786,7 +4816,7 @@ GI_HD __forceinline__ bool rule_noop(Tx& t, const DRule& R, uint32_t ri) {
   if (t.skip_after >= 0) return R.marker != t.skip_after;
   if (R.flags & RF_MARKER) return true;
   if ((R.flags & RF_CONST) && R._pad2 == 0) return true;  // a folded link that matches nothing
-  return R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !bodydep_void(t, R) &&
+  return R.hit_slot >= 0 && !residual_live(t, R) && !t.pa_void && !bodydep_void(t, R) &&
          !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u) &&
          !((R.flags2 & RF2_PA_FILTER) && t.crec);
 }
@@ -4869,7 +4899,7 @@ GI_HD __forceinline__ void eval_phase(Tx& t, uint8_t phase) {
       t.mv->n = 0;
       t.mv->nb = 0;
     }
-    if (R.hit_slot >= 0 && !(R.flags & RF_RESIDUAL) && !t.pa_void && !bodydep_void(t, R) &&
+    if (R.hit_slot >= 0 && !residual_live(t, R) && !t.pa_void && !bodydep_void(t, R) &&
         !((t.hits[(uint64_t)(R.hit_slot >> 5) * t.hstride] >> (R.hit_slot & 31)) & 1u) &&
         !((R.flags2 & RF2_PA_FILTER) && t.crec))
       continue;  // phase A proved the first link matches nothing (a filter link: and records no capture)
@@ -7377,6 +7407,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
     CH->trunc = 0;
   }
   t.crec = t.capws && B.caprec;
+  t.rcoll = false;
   t.mcap = B.mcap;
   // TX: copy on write over the folded snapshot; slots >= 128 and the capture
   // groups (run_capture writes those directly) start owned and unset
@@ -7500,6 +7531,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
             // [upstream multipart.go]: collections, no REQUEST_BODY; an error
             // -> MULTIPART_STRICT_ERROR + generateRequestBodyError (rules
             // 200002 / 200003 deny with 400)
+            t.rcoll = true;  // part headers (MULTIPART_PART_HEADERS) and FILES_TMPNAMES
             uint8_t err;
             if (H->spec_proc == BP_MULTIPART && B.stage == 1) {
               t.nf += H->n_post;  // k_mpparse's fields: scanned through the prefix streams only
@@ -7536,6 +7568,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
           } else if (t.body_proc == BP_XML) {
             // [upstream xml.go]: XML "//@*" / "/*", no REQUEST_BODY; an error ->
             // generateRequestBodyError (REQBODY_ERROR_MSG "XML: <error>")
+            t.rcoll = true;
             JsonCtx jc{t.fields, t.nf, t.cap_f, t.bytes, t.nb, t.cap_b, t.t1, t.cap_t, t.flags};
             Str msg{CS_ZERO, 0};
             const int xr = parse_xml(jc, D + rq.body.off, bn, (uint32_t*)t.t0, t.cap_t / 4, &msg);
