@@ -1710,6 +1710,28 @@ struct Lower {
            sid == S_SERVER_NAME;
   }
 
+  // Does the link's transformation chain + operator reject the empty value?
+  // (Every transformation here maps "" to ""; the operator finds nothing in "".)
+  static bool link_rejects_empty(const IrRule& r) {
+    if (!r.has_op || r.op_neg || r.multimatch) return false;
+    for (const auto& tf : r.transforms) {
+      const std::string t = lower(tf);
+      if (t == "length" || t == "sha1" || t == "md5") return false;
+    }
+    const std::string& n = r.op_name;
+    if (n == "rx") {
+      Regex re;
+      Dfa d;
+      std::string err;
+      if (!re_parse("(?sm)" + r.op_arg, &re, &err) || !build_regex_dfa(re, &d, &err)) return false;
+      return !dfa_host_match(d, (const uint8_t*)"", 0);
+    }
+    if (n == "pm" || n == "pmfromfile") return !r.phrases.empty() || !trim(r.op_arg).empty();
+    if (n == "contains" || n == "containsword") return !r.op_arg.empty() && r.op_arg.find("%{") == std::string::npos;
+    return n == "detectsqli" || n == "detectxss" || n == "validatebyterange" || n == "validateurlencoding" ||
+           n == "validateutf8encoding";
+  }
+
   // Assigns a hit slot and registers the link's patterns, or returns -1 when
   // the link stays interpreter-only (TX / count targets, macro arguments,
   // operators without an automaton form, mutable singles).
@@ -1726,11 +1748,12 @@ struct Lower {
                      n == "validateutf8encoding" || n == "detectsqli" || n == "detectxss" ||
                      (n == "contains" && r.op_arg.find("%{") == std::string::npos);
     if (!scannable) return -1;
-    bool bodydep = false, residual = false, res_single = false;
+    bool bodydep = false, residual = false, res_single = false, rb_only = true;
     for (auto& v : r.vars) {
       if (v.count) return -1;
       int sid = single_id(v.name);
       if (sid >= 0 && !immutable_single(sid)) residual = res_single = true;  // tested by k_eval on a clear bit
+      if (sid >= 0 && !immutable_single(sid) && sid != S_REQUEST_BODY) rb_only = false;
       if (sid < 0 && v.name == "TX") return -1;
       if (v.name.rfind("MATCHED_VAR", 0) == 0) return -1;  // transaction state, not a request variable
       if (residual_collection(v.name)) residual = true;  // body collections phase A does not scan
@@ -1757,6 +1780,7 @@ struct Lower {
     if (bodydep) *flags |= RF_BODYDEP;
     if (residual) *flags |= RF_RESIDUAL;
     if (residual && !res_single) *flags2 |= RF2_RESID_COLL;  // only body collections: empty without such a body
+    if (residual && res_single && rb_only && link_rejects_empty(r)) *flags2 |= RF2_RESID_RB;
     const DOp& o = P->ops[d.op];
     DVarRef* vrs = &P->vars[d.var_begin];
     for (uint32_t vi = 0; vi < d.var_count; vi++) {

@@ -227,6 +227,9 @@ enum RuleFlags2 : uint8_t {
   RF2_RESID_COLL = 64,  // RF_RESIDUAL only through body collections phase A does not scan (XML, part headers,
                         // FILES_TMPNAMES): empty -- so a clear bit is final -- unless the request's body went
                         // through the XML or multipart processor
+  RF2_RESID_RB = 128,   // RF_RESIDUAL through REQUEST_BODY (and maybe body collections) only, and the link's
+                        // chain + operator reject "": a clear bit is final while REQUEST_BODY is empty (and no
+                        // XML / multipart body)
 };
 
 enum ActKind : uint8_t {

@@ -1461,6 +1461,7 @@ struct Tx {
   bool crec;                 // capture records are written (capws and the batch's record rows)
   bool rcoll;                // the body went through the XML / multipart processor: residual body collections
                              // (RF2_RESID_COLL) may have entries
+  bool rbody;                // REQUEST_BODY is not empty (RF2_RESID_RB)
   uint8_t* capbuf;           // per capture group g: cap_t bytes holding TX.g's value
   uint8_t* dyn;              // TX keys macro-key setvars created (DynHdr; nullptr: the program has none)
   uint64_t wm0, wm1;         // TX slots < 128 this request owns (written); the others read the snapshot
@@ -4184,7 +4185,8 @@ GI_HD __forceinline__ bool bodydep_void(const Tx& t, const DRule& R) {
 // A clear hit bit does not settle the link: some residual target (a mutable
 // single, or a body collection the request actually has) is still to test.
 GI_HD __forceinline__ bool residual_live(const Tx& t, const DRule& R) {
-  return (R.flags & RF_RESIDUAL) && (t.rcoll || !(R.flags2 & RF2_RESID_COLL));
+  if (!(R.flags & RF_RESIDUAL) || t.rcoll) return (R.flags & RF_RESIDUAL) != 0;
+  return !(R.flags2 & RF2_RESID_COLL) && !((R.flags2 & RF2_RESID_RB) && !t.rbody);
 }
 
 GI_HD __forceinline__ bool key_excluded(Tx& t, const DVarRef& vr, const uint8_t* k, uint32_t kn) {
@@ -7408,6 +7410,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
   }
   t.crec = t.capws && B.caprec;
   t.rcoll = false;
+  t.rbody = false;
   t.mcap = B.mcap;
   // TX: copy on write over the folded snapshot; slots >= 128 and the capture
   // groups (run_capture writes those directly) start owned and unset
@@ -7586,6 +7589,7 @@ GI_HD __forceinline__ void eval_request(const DProgram& Pk, const DBatch& B, uin
         }
       }
       if ((t.flags & GI_REQ_ERROR_MASK) || !run2) break;
+      t.rbody = t.single[S_REQUEST_BODY].n > 0;
       // (body fields or a REQUEST_BODY phase A has not seen: XML values are never phase-A items)
       t.prefix = B.stage == 1 && (t.has_post || t.single[S_REQUEST_BODY].n > 0);
     }
