@@ -120,6 +120,7 @@ struct DBatch {
   uint32_t* eorder;           // k_eval's request order (nullptr: identity): requests grouped by their count of
                               // set phase-A hit bits, so a wave's lanes walk similar rule paths (k_eord_*)
   uint32_t* eord_bins;        // [GI_EORD_BINS] counts, then [GI_EORD_BINS] cursors (ctr)
+  uint8_t* eord_key;          // per request: its bin (k_eord_count -> k_eord_scatter)
   uint32_t* pcount;
   uint32_t wave_stage2;       // the body stage's pending requests all go to k_eval_wave (GI_EVAL_WAVE_STAGE2=0: by size)
   uint32_t body_tiles;        // k_body runs its chunkable transformations LDS-tiled (GI_BODY_TILES=0: off)
@@ -158,7 +159,7 @@ struct ScanLaunch {
 #define GI_EVAL_WAVE_RULES 2048
 #define GI_BPARSE_LDS 0              // k_bparse LDS copy of JSON bodies up to this size (GI_BPARSE_LDS env; 0: off --
                                      // measured: 32 KB made C3's k_bparse 81 -> 272 ms, the LDS cut its occupancy)
-#define GI_EORD_BINS 32               // k_eval order: bins of hit-bit counts (the last one also takes void requests)
+#define GI_EORD_BINS 32               // k_eval order: bins of hit-bit counts
 #define GI_GATE_PENDING_MAX 0.5       // the adaptive gate runs while at most this share of body requests stays pending
 #define GI_CHUNK_POOL_WORDS 16e9     // queue-pool words (estimate) one request chunk of a batch may need
 

@@ -7684,17 +7684,17 @@ GI_HD __forceinline__ bool eval_heavy(const DProgram& P, const DBatch& B, uint32
 // phase-A hit bits (a counting sort into GI_EORD_BINS bins; void requests,
 // which evaluate every link, in the last) gives waves of like requests.  The
 // order changes no result: each request is evaluated on its own.
+// (k_eord_count keeps each request's bin in eord_key[r] for k_eord_scatter.)
 GI_HD __forceinline__ uint32_t eord_key(const DBatch& B, uint32_t r) {
-  const ReqHdr* H = (const ReqHdr*)(B.scratch + B.layout[r].base);
-  if (H->pa_void) return GI_EORD_BINS - 1;
   const uint32_t nw = (B.n_hit_slots + 31) / 32;
   uint32_t c = 0;
   for (uint32_t w = 0; w < nw; w++) c += __popc(B.hits[(uint64_t)w * B.rstride + r]);
-  return min(c, (uint32_t)GI_EORD_BINS - 2);
+  return min(c, (uint32_t)GI_EORD_BINS - 1);
 }
 __global__ void __launch_bounds__(256) k_eord_count(DBatch B) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t key = r < B.n_req ? (int32_t)eord_key(B, r) : -1;
+  if (r < B.n_req) B.eord_key[r] = (uint8_t)key;
   uint64_t active = __ballot(key >= 0);
   while (active) {  // one atomic per distinct key in the wave
     const int leader = __ffsll((unsigned long long)active) - 1;
@@ -7715,7 +7715,7 @@ __global__ void __launch_bounds__(256) k_eord_scatter(DBatch B) {
   }
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  const int32_t key = r < B.n_req ? (int32_t)eord_key(B, r) : -1;
+  const int32_t key = r < B.n_req ? (int32_t)B.eord_key[r] : -1;
   // wave-aggregated cursor claims: one atomic per distinct key in the wave
   uint64_t active = __ballot(key >= 0);
   while (active) {

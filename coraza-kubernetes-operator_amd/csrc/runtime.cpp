@@ -94,7 +94,7 @@ struct gi_ctx {
   // phase A
   DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf, wlist;
   DevBuf pend, plist;  // phase-1 gate (launch_pipeline): pending flags + list
-  DevBuf eorder;       // k_eval's request order (k_eord_*: requests grouped by phase-A hit count)
+  DevBuf eorder, ekey;  // k_eval's request order (k_eord_*: requests grouped by phase-A hit count), bins
   DevBuf dmemo_keys, dmemo_info;  // k_detect's detector-result memo
   uint32_t dmemo_mask = 0;
   uint32_t long_cap = 0, long_grid = GI_LONG_GRID;
@@ -645,7 +645,7 @@ void gi_ctx_free(gi_ctx* c) {
   for (DevBuf* b : {&c->caprec, &c->capbytes, &c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->hset, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist, &c->pend, &c->plist, &c->dmemo_keys, &c->dmemo_info,
-                    &c->eorder, &c->cappool, &c->progdev})
+                    &c->eorder, &c->ekey, &c->cappool, &c->progdev})
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
@@ -1112,6 +1112,7 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
   if ((e = c->ctr.ensure(4096 + 8ull * ((4 * GI_NCLS + 63) & ~63))) != hipSuccess) return hip_fail(c, e, "alloc counters");
   if ((e = c->wlist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc wave list");
   if ((e = c->eorder.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc eval order");
+  if ((e = c->ekey.ensure(std::max<uint64_t>(n, 16))) != hipSuccess) return hip_fail(c, e, "alloc eval order keys");
   if ((e = c->pend.ensure(std::max<uint64_t>(n, 16))) != hipSuccess) return hip_fail(c, e, "alloc gate flags");
   if ((e = c->plist.ensure(4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return hip_fail(c, e, "alloc gate list");
   const auto t_h2d0 = std::chrono::steady_clock::now();
@@ -1254,6 +1255,7 @@ int gi_run_staged(gi_ctx* c) {
     static const bool eord_env = !(getenv("GI_EVAL_ORDER") && atoi(getenv("GI_EVAL_ORDER")) == 0);
     B.eorder = eord_env ? (uint32_t*)c->eorder.p : nullptr;
     B.eord_bins = (uint32_t*)(cp + 1024);
+    B.eord_key = (uint8_t*)c->ekey.p;
     static const uint32_t tiles_env = getenv("GI_BODY_TILES") ? (uint32_t)atoi(getenv("GI_BODY_TILES")) : 1u;
     B.body_tiles = tiles_env;
     static const uint32_t ws2_env = getenv("GI_EVAL_WAVE_STAGE2") ? (uint32_t)atoi(getenv("GI_EVAL_WAVE_STAGE2")) : 1u;
@@ -1304,6 +1306,7 @@ int gi_run_staged(gi_ctx* c) {
     Bc.body_list = B.body_list + ch.blist_off;
     Bc.pend = B.pend ? B.pend + ch.r0 : nullptr;
     Bc.eorder = B.eorder ? B.eorder + ch.r0 : nullptr;
+    Bc.eord_key = B.eord_key ? B.eord_key + ch.r0 : nullptr;
     Bc.n_body = ch.n_body;
     Bc.n_mp_body = ch.n_mp;
     launch_pipeline(c->prog, Bc, c->scan, c->stream, c->evs, c->stop_after, &c->log,
