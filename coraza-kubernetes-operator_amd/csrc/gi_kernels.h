@@ -160,6 +160,7 @@ struct ScanLaunch {
 #define GI_BPARSE_LDS 0              // k_bparse LDS copy of JSON bodies up to this size (GI_BPARSE_LDS env; 0: off --
                                      // measured: 32 KB made C3's k_bparse 81 -> 272 ms, the LDS cut its occupancy)
 #define GI_EORD_BINS 32               // k_eval order: bins of hit-bit counts
+#define GI_EORD_GRID 512              // k_eord_* workgroups (each a contiguous chunk of requests)
 #define GI_GATE_PENDING_MAX 0.5       // the adaptive gate runs while at most this share of body requests stays pending
 #define GI_CHUNK_POOL_WORDS 16e9     // queue-pool words (estimate) one request chunk of a batch may need
 

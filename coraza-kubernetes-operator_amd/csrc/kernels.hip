@@ -7691,45 +7691,46 @@ GI_HD __forceinline__ uint32_t eord_key(const DBatch& B, uint32_t r) {
   for (uint32_t w = 0; w < nw; w++) c += __popc(B.hits[(uint64_t)w * B.rstride + r]);
   return min(c, (uint32_t)GI_EORD_BINS - 1);
 }
-__global__ void __launch_bounds__(256) k_eord_count(DBatch B) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  const int32_t key = r < B.n_req ? (int32_t)eord_key(B, r) : -1;
-  if (r < B.n_req) B.eord_key[r] = (uint8_t)key;
-  uint64_t active = __ballot(key >= 0);
-  while (active) {  // one atomic per distinct key in the wave
-    const int leader = __ffsll((unsigned long long)active) - 1;
-    const int32_t lk = __shfl(key, leader, 64);
-    const uint64_t same = __ballot(key == lk) & active;
-    if (lane_id() == (uint32_t)leader) atomicAdd(&B.eord_bins[lk], (uint32_t)__popcll(same));
-    active &= ~same;
-  }
+// Both launches run GI_EORD_GRID workgroups, each over one contiguous chunk of
+// requests, with the bins counted in LDS: one global atomic per (workgroup,
+// bin) instead of one per (wave, bin) on 32 hot counters.
+__device__ __forceinline__ void eord_chunk(const DBatch& B, uint32_t* r0, uint32_t* r1) {
+  const uint32_t per = (B.n_req + gridDim.x - 1) / gridDim.x;
+  *r0 = min(B.n_req, blockIdx.x * per);
+  *r1 = min(B.n_req, *r0 + per);
 }
-__global__ void __launch_bounds__(256) k_eord_scatter(DBatch B) {
-  __shared__ uint32_t base[GI_EORD_BINS];
-  if (threadIdx.x == 0) {
-    uint32_t a = 0;
-    for (uint32_t k = 0; k < GI_EORD_BINS; k++) {
-      base[k] = a;
-      a += B.eord_bins[k];
-    }
+__global__ void __launch_bounds__(256) k_eord_count(DBatch B) {
+  __shared__ uint32_t h[GI_EORD_BINS];
+  if (threadIdx.x < GI_EORD_BINS) h[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t r0, r1;
+  eord_chunk(B, &r0, &r1);
+  for (uint32_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+    const uint32_t key = eord_key(B, r);
+    B.eord_key[r] = (uint8_t)key;
+    atomicAdd(&h[key], 1u);
   }
   __syncthreads();
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  const int32_t key = r < B.n_req ? (int32_t)B.eord_key[r] : -1;
-  // wave-aggregated cursor claims: one atomic per distinct key in the wave
-  uint64_t active = __ballot(key >= 0);
-  while (active) {
-    const int leader = __ffsll((unsigned long long)active) - 1;
-    const int32_t lk = __shfl(key, leader, 64);
-    const uint64_t same = __ballot(key == lk) & active;
-    uint32_t first = 0;
-    if (lane_id() == (uint32_t)leader) first = atomicAdd(&B.eord_bins[GI_EORD_BINS + lk], (uint32_t)__popcll(same));
-    first = (uint32_t)__shfl((int)first, leader, 64);
-    if (key == lk) {
-      const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane_id()) - 1ull));
-      B.eorder[base[lk] + first + rank] = r;
-    }
-    active &= ~same;
+  if (threadIdx.x < GI_EORD_BINS && h[threadIdx.x]) atomicAdd(&B.eord_bins[threadIdx.x], h[threadIdx.x]);
+}
+__global__ void __launch_bounds__(256) k_eord_scatter(DBatch B) {
+  __shared__ uint32_t h[GI_EORD_BINS], base[GI_EORD_BINS];
+  if (threadIdx.x < GI_EORD_BINS) h[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t r0, r1;
+  eord_chunk(B, &r0, &r1);
+  for (uint32_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) atomicAdd(&h[B.eord_key[r]], 1u);
+  __syncthreads();
+  if (threadIdx.x < GI_EORD_BINS) {  // this workgroup's run of each bin
+    uint32_t a = 0;
+    for (uint32_t k = 0; k < threadIdx.x; k++) a += B.eord_bins[k];
+    base[threadIdx.x] = a + (h[threadIdx.x] ? atomicAdd(&B.eord_bins[GI_EORD_BINS + threadIdx.x], h[threadIdx.x]) : 0u);
+    h[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  for (uint32_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+    const uint32_t key = B.eord_key[r];
+    B.eorder[base[key] + atomicAdd(&h[key], 1u)] = r;
   }
 }
 
@@ -7976,8 +7977,9 @@ static void launch_eval(const DProgram& P, const DBatch& B, hipStream_t stream, 
   if (Be.eorder) {
     const uint32_t cb = (B.n_req + 255) / 256;
     (void)hipMemsetAsync(B.eord_bins, 0, 8 * GI_EORD_BINS, stream);
-    GI_LAUNCH(B.stage == 1 ? "k_eord_count.1" : "k_eord_count", k_eord_count, dim3(cb), dim3(256), 0, stream, B);
-    GI_LAUNCH(B.stage == 1 ? "k_eord_scatter.1" : "k_eord_scatter", k_eord_scatter, dim3(cb), dim3(256), 0, stream, B);
+    const uint32_t eg = std::min<uint32_t>(cb, GI_EORD_GRID);
+    GI_LAUNCH(B.stage == 1 ? "k_eord_count.1" : "k_eord_count", k_eord_count, dim3(eg), dim3(256), 0, stream, B);
+    GI_LAUNCH(B.stage == 1 ? "k_eord_scatter.1" : "k_eord_scatter", k_eord_scatter, dim3(eg), dim3(256), 0, stream, B);
   }
   {  // small batches (fewer than 4 workgroups of 128 per CU): one wave per workgroup to spread over all CUs
     // GI_EVAL_BS A/B (C2, 1M): 128 threads 26.2 ms, 64 threads 32.1 ms
