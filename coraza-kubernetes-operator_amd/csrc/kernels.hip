@@ -91,6 +91,27 @@ GI_HD __forceinline__ uint32_t load_u32u(const uint8_t* p) {
 #endif
 }
 
+// LDS byte pointers (k_body's tiles): the transformations below are templates
+// over their source / destination pointer types, so a tile's accesses are
+// ds_* ops whether or not the compiler inlines them -- never FLAT ops on an
+// LDS address (which the compiler may merge into misaligned wide stores).
+typedef __attribute__((address_space(3))) uint8_t gi_lds_u8;
+typedef __attribute__((address_space(3))) uint32_t gi_lds_u32;
+__device__ __forceinline__ uint32_t load_u32u(const gi_lds_u8* p) {
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  const gi_lds_u32* w = (const gi_lds_u32*)(uintptr_t)(a & ~3u);
+  const uint32_t sh = a & 3u;
+  const uint32_t lo = w[0];
+#if defined(__HIP_DEVICE_COMPILE__)
+  return sh ? __builtin_amdgcn_alignbyte(w[1], lo, sh) : lo;
+#else
+  return sh ? (uint32_t)((((uint64_t)w[1] << 32) | lo) >> (8 * sh)) : lo;
+#endif
+}
+__device__ __forceinline__ void store_u32a(gi_lds_u8* p, uint32_t v) { *(gi_lds_u32*)p = v; }
+// a dword store at a 4-byte aligned address
+GI_HD __forceinline__ void store_u32a(uint8_t* p, uint32_t v) { *(uint32_t*)p = v; }
+
 // Word-at-a-time byte helpers for the interpreter's per-request strings
 // (k_eval: one lane per request, so every byte access is a scattered memory
 // instruction of its own).  Sources must be padded buffers (the batch data,
@@ -235,7 +256,8 @@ GI_HD __forceinline__ uint32_t go_itoa(int64_t v, uint8_t* buf) {
 }
 
 // utf8.DecodeRune
-GI_HD __forceinline__ uint32_t decode_rune(const uint8_t* b, uint32_t n, uint32_t i, uint32_t* w) {
+template <class S>
+GI_HD __forceinline__ uint32_t decode_rune(S b, uint32_t n, uint32_t i, uint32_t* w) {
   uint8_t c0 = b[i];
   if (c0 < 0x80) {
     *w = 1;
@@ -264,7 +286,8 @@ GI_HD __forceinline__ uint32_t decode_rune(const uint8_t* b, uint32_t n, uint32_
   return ((c0 & 0x07) << 18) | ((c1 & 0x3F) << 12) | ((b[i + 2] & 0x3F) << 6) | (b[i + 3] & 0x3F);
 }
 
-GI_HD __forceinline__ uint32_t encode_rune(uint32_t r, uint8_t* o) {
+template <class D>
+GI_HD __forceinline__ uint32_t encode_rune(uint32_t r, D o) {
   if (r < 0x80) { o[0] = (uint8_t)r; return 1; }
   if (r < 0x800) { o[0] = 0xC0 | (r >> 6); o[1] = 0x80 | (r & 0x3F); return 2; }
   if (r < 0x10000) {
@@ -455,7 +478,8 @@ GI_HD uint32_t lower_rune(const DProgram& P, uint32_t r) {
 }
 
 // Go strings.ToLower
-GI_HD int64_t t_lowercase(const DProgram& P, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_lowercase(const DProgram& P, S s, uint32_t n, D d, uint32_t cap) {
   bool ascii = true;
   for (uint32_t i = 0; i < n && ascii; i += 4) {
     uint32_t x = load_u32u(s + i);
@@ -469,7 +493,7 @@ GI_HD int64_t t_lowercase(const DProgram& P, const uint8_t* s, uint32_t n, uint8
         const uint32_t x = load_u32u(s + i);
         const uint32_t ge_a = (x & 0x7F7F7F7Fu) + 0x3F3F3F3Fu;  // bit 7: byte >= 'A'
         const uint32_t gt_z = (x & 0x7F7F7F7Fu) + 0x25252525u;  // bit 7: byte > 'Z'
-        *(uint32_t*)(d + i) = x | (((ge_a ^ gt_z) & ~x & 0x80808080u) >> 2);
+        store_u32a(d + i, x | (((ge_a ^ gt_z) & ~x & 0x80808080u) >> 2));
       }
     } else {
       for (uint32_t i = 0; i < n; i++) d[i] = alower(s[i]);
@@ -498,7 +522,8 @@ GI_HD int64_t t_lowercase(const DProgram& P, const uint8_t* s, uint32_t n, uint8
 }
 
 // ModSecurity urldecode_nonstrict (t:urlDecode)
-GI_HD int64_t t_urldecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_urldecode(S s, uint32_t n, D d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -520,7 +545,8 @@ GI_HD int64_t t_urldecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap
 }
 
 // ModSecurity urldecode_uni_nonstrict (t:urlDecodeUni; %uXXXX low byte, full-width +0x20)
-GI_HD int64_t t_urldecodeuni(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_urldecodeuni(S s, uint32_t n, D d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -553,7 +579,8 @@ GI_HD int64_t t_urldecodeuni(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t 
 }
 
 // strtol(digits, base) & 0xFF, saturating like strtol/ParseInt on overflow
-GI_HD uint8_t strtol_byte(const uint8_t* s, uint32_t n, uint32_t base) {
+template <class S>
+GI_HD uint8_t strtol_byte(S s, uint32_t n, uint32_t base) {
   uint64_t acc = 0;
   for (uint32_t i = 0; i < n; i++) {
     uint32_t v = base == 16 ? hexv(s[i]) : (uint32_t)(s[i] - '0');
@@ -564,7 +591,8 @@ GI_HD uint8_t strtol_byte(const uint8_t* s, uint32_t n, uint32_t base) {
 }
 
 // ModSecurity html_entities_decode_inplace (t:htmlEntityDecode)
-GI_HD int64_t t_htmlentitydecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_htmlentitydecode(S s, uint32_t n, D d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -603,7 +631,7 @@ GI_HD int64_t t_htmlentitydecode(const uint8_t* s, uint32_t n, uint8_t* d, uint3
         if (j > k) {
           uint32_t len = j - k;
           int ent = -1;
-          const uint8_t* x = s + k;
+          const auto x = s + k;
           if (len == 4 && alower(x[0]) == 'q' && alower(x[1]) == 'u' && alower(x[2]) == 'o' && alower(x[3]) == 't') ent = '"';
           else if (len == 3 && alower(x[0]) == 'a' && alower(x[1]) == 'm' && alower(x[2]) == 'p') ent = '&';
           else if (len == 2 && alower(x[0]) == 'l' && alower(x[1]) == 't') ent = '<';
@@ -625,7 +653,8 @@ GI_HD int64_t t_htmlentitydecode(const uint8_t* s, uint32_t n, uint8_t* d, uint3
 
 GI_HD inline bool ws_or_nbsp(uint8_t c) { return isws(c) || c == 0xA0; }
 
-GI_HD int64_t t_simple(uint8_t code, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_simple(uint8_t code, S s, uint32_t n, D d, uint32_t cap) {
   if (n + 1 > cap) return -1;
   uint32_t o = 0;
   switch (code) {
@@ -803,7 +832,8 @@ GI_HD int64_t t_normpath(bool win, const uint8_t* s, uint32_t n, uint8_t* d, uin
 GI_HD inline bool isodigit(uint8_t c) { return c >= '0' && c <= '7'; }
 
 // ModSecurity js_decode_nonstrict_inplace (t:jsDecode)
-GI_HD int64_t t_jsdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_jsdecode(S s, uint32_t n, D d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -854,7 +884,8 @@ GI_HD int64_t t_jsdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap)
 
 // t:utf8toUnicode: valid multi-byte UTF-8 -> %uXXXX (lowercase hex, >= 4
 // digits); ASCII and invalid bytes copied.  [upstream utf8toUnicode.go]
-GI_HD int64_t t_utf8tounicode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_utf8tounicode(S s, uint32_t n, D d, uint32_t cap) {
   uint32_t o = 0, i = 0;
   const char* hx = "0123456789abcdef";
   while (i < n) {
@@ -927,7 +958,8 @@ GI_HD int64_t t_b64decode(bool ext, const uint8_t* s, uint32_t n, uint8_t* d, ui
   return o;
 }
 
-GI_HD int64_t t_b64encode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_b64encode(S s, uint32_t n, D d, uint32_t cap) {
   const char* al = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
   const uint64_t out = 4ull * ((n + 2) / 3);
   if (out > cap) return -1;
@@ -960,7 +992,8 @@ GI_HD int64_t t_hexdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap
   return n / 2;
 }
 
-GI_HD int64_t t_hexencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_hexencode(S s, uint32_t n, D d, uint32_t cap) {
   if (2ull * n > cap) return -1;
   const char* hx = "0123456789abcdef";
   for (uint32_t i = 0; i < n; i++) {
@@ -970,7 +1003,8 @@ GI_HD int64_t t_hexencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap
   return 2 * n;
 }
 
-GI_HD int64_t t_urlencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_urlencode(S s, uint32_t n, D d, uint32_t cap) {
   const char* hx = "0123456789abcdef";
   uint32_t o = 0;
   for (uint32_t i = 0; i < n; i++) {
@@ -992,7 +1026,8 @@ GI_HD int64_t t_urlencode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap
 GI_HD inline bool c_isspace(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
 
 // ModSecurity css_decode_inplace
-GI_HD int64_t t_cssdecode(const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap) {
+template <class S, class D>
+GI_HD int64_t t_cssdecode(S s, uint32_t n, D d, uint32_t cap) {
   if (n > cap) return -1;
   uint32_t o = 0, i = 0;
   while (i < n) {
@@ -1229,25 +1264,29 @@ GI_HD __forceinline__ int64_t apply_transform_inl(const DProgram& P, uint8_t cod
   }
 }
 
-// The chunkable transformations (t_chunkable) with every callee inlined, for
-// k_body's LDS tiles: a buffer access through a generic pointer in an
-// out-of-line callee becomes a FLAT op, and the compiler merges adjacent byte
-// stores into misaligned wider ones -- which fault on an LDS address.  Inlined
-// into the tile loop, the accesses are ds_* ops.
-GI_HD __forceinline__ int64_t apply_transform_tile(const DProgram& P, uint8_t code, const uint8_t* s, uint32_t n,
-                                                   uint8_t* d, uint32_t cap) {
+// The chunkable transformations (t_chunkable) over k_body's LDS tiles: the
+// pointers are LDS-typed (gi_lds_u8), so every access of the instantiated
+// transformations is a ds_* op -- inlined or not (GI_TILE_NOINLINE builds it
+// out of line, the A/B check of tests/test_body_chunks.py).
+#ifdef GI_TILE_NOINLINE
+#define GI_TILE_INL __noinline__
+#else
+#define GI_TILE_INL __forceinline__
+#endif
+__device__ GI_TILE_INL int64_t apply_transform_tile(const DProgram& P, uint8_t code, const gi_lds_u8* s, uint32_t n,
+                                                    gi_lds_u8* d, uint32_t cap) {
   switch (code) {
-    case T_UTF8TOUNICODE: [[clang::always_inline]] return t_utf8tounicode(s, n, d, cap);
-    case T_LOWERCASE: [[clang::always_inline]] return t_lowercase(P, s, n, d, cap);
-    case T_URLDECODE: [[clang::always_inline]] return t_urldecode(s, n, d, cap);
-    case T_URLDECODEUNI: [[clang::always_inline]] return t_urldecodeuni(s, n, d, cap);
-    case T_HTMLENTITYDECODE: [[clang::always_inline]] return t_htmlentitydecode(s, n, d, cap);
-    case T_JSDECODE: [[clang::always_inline]] return t_jsdecode(s, n, d, cap);
-    case T_CSSDECODE: [[clang::always_inline]] return t_cssdecode(s, n, d, cap);
-    case T_URLENCODE: [[clang::always_inline]] return t_urlencode(s, n, d, cap);
-    case T_HEXENCODE: [[clang::always_inline]] return t_hexencode(s, n, d, cap);
-    case T_BASE64ENCODE: [[clang::always_inline]] return t_b64encode(s, n, d, cap);
-    default: [[clang::always_inline]] return t_simple(code, s, n, d, cap);  // removeNulls, replaceNulls, (compress|remove)Whitespace, cmdLine
+    case T_UTF8TOUNICODE: return t_utf8tounicode(s, n, d, cap);
+    case T_LOWERCASE: return t_lowercase(P, s, n, d, cap);
+    case T_URLDECODE: return t_urldecode(s, n, d, cap);
+    case T_URLDECODEUNI: return t_urldecodeuni(s, n, d, cap);
+    case T_HTMLENTITYDECODE: return t_htmlentitydecode(s, n, d, cap);
+    case T_JSDECODE: return t_jsdecode(s, n, d, cap);
+    case T_CSSDECODE: return t_cssdecode(s, n, d, cap);
+    case T_URLENCODE: return t_urlencode(s, n, d, cap);
+    case T_HEXENCODE: return t_hexencode(s, n, d, cap);
+    case T_BASE64ENCODE: return t_b64encode(s, n, d, cap);
+    default: return t_simple(code, s, n, d, cap);  // removeNulls, replaceNulls, (compress|remove)Whitespace, cmdLine
   }
 }
 
@@ -6890,7 +6929,10 @@ __device__ __forceinline__ int64_t wave_transform_lds(const DProgram& P, uint8_t
       adv = __shfl(a, hi, 64);
       if ((int)L == hi) act = false;
     }
-    int64_t m = act ? apply_transform_tile(P, code, in + a, e - a, out + 3u * a + 8u * L, 3 * (e - a) + 8) : 0;
+    // (the tile pointers as LDS pointers: the transformation's accesses are ds_* ops)
+    int64_t m = act ? apply_transform_tile(P, code, (const gi_lds_u8*)(in + a), e - a,
+                                           (gi_lds_u8*)(out + 3u * a + 8u * L), 3 * (e - a) + 8)
+                    : 0;
     if (__ballot(m < 0) != 0) return -1;
     uint32_t tot = 0;
     const uint32_t o0 = wave_excl_sum((uint32_t)m, &tot);
