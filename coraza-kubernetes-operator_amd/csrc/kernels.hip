@@ -23,6 +23,16 @@
 #include "html_entities.h"
 #include "libinj.h"
 
+// k_detect's own copy of the detectors (libinj_body.h again, in gi::lid): its
+// out-of-line functions are called by k_detect alone, so they are compiled
+// for k_detect's register budget instead of the largest one among k_eval /
+// k_stream / k_long, which share the gi:: copy.
+namespace gi {
+namespace lid {
+#include "libinj_body.h"
+}  // namespace lid
+}  // namespace gi
+
 namespace gi {
 
 // ------------------------------------------------------------ small utils
@@ -7216,11 +7226,11 @@ __device__ __forceinline__ bool dm_same(const uint8_t* a, const uint8_t* b, uint
 }
 // Results of the detectors the entry needs (bit 0 SQLi, bit 1 XSS).
 __device__ uint32_t det_results(const DBatch& B, const uint8_t* v, uint32_t n, uint64_t off, bool need_s, bool need_x,
-                                LiSqli* st, const LiTables& T, uint64_t* dsteps) {
+                                lid::LiSqli* st, const lid::LiTables& T, uint64_t* dsteps) {
   auto compute = [&](bool s) -> bool {
-    if (!li_candidate(s, v, n)) return false;
+    if (!lid::li_candidate(s, v, n)) return false;
     *dsteps += n;
-    return s ? li_detect_sqli(v, n, st, T) : li_detect_xss(v, n);
+    return s ? lid::li_detect_sqli(v, n, st, T) : lid::li_detect_xss(v, n);
   };
   uint32_t out = 0;
   if (!B.dmemo_keys || n < B.dmemo_min) {  // (a short unique value costs more in memo round trips than to detect)
@@ -7284,7 +7294,7 @@ __device__ uint32_t det_results(const DBatch& B, const uint8_t* v, uint32_t n, u
 }
 
 __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
-  __shared__ LiSqli st[256];
+  __shared__ lid::LiSqli st[256];
   // the keyword tables in LDS: every word lookup is a hash probe + compare
   __shared__ uint32_t lw[LI_NWORDS];
   __shared__ uint16_t lh[LI_HASH_SIZE];
@@ -7296,7 +7306,7 @@ __global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
   for (uint32_t i = threadIdx.x; i < LI_HASH_SIZE; i += blockDim.x) lh[i] = kLiHash[i];
   for (uint32_t i = threadIdx.x; i < sizeof(kLiPool); i += blockDim.x) lp[i] = kLiPool[i];
   __syncthreads();
-  LiTables T;  // (member-wise: an aggregate of LDS addresses would become a static initializer)
+  lid::LiTables T;  // (member-wise: an aggregate of LDS addresses would become a static initializer)
   T.words = lw;
   T.pool = lp;
   T.hash = lh;
