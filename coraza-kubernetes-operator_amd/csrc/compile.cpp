@@ -1744,13 +1744,40 @@ struct Lower {
   int32_t plan(const IrRule& r, const DRule& d, uint8_t* flags, uint8_t* flags2) {
     if (!r.has_op || no_scan) return -1;
     const std::string& n = r.op_name;
+    // A link whose targets are all collection counts (&ARGS_POST:_charset_) and
+    // whose numeric comparison fails on a zero count ("!@eq 0"): phase A sets its
+    // bit iff some entry the targets admit exists (an always-true value test on
+    // their filters), so a clear bit means every count is 0 and the link cannot
+    // match -- the interpreter no longer walks a 2 500-field ARGS_POST for it.
+    bool count_exists = false;
+    {
+      bool any = false, all = true;
+      for (auto& v : r.vars) {
+        any = any || v.count;
+        all = all && v.count;
+      }
+      if (any) {
+        if (!all || r.multimatch) return -1;
+        const bool cmp = n == "eq" || n == "ge" || n == "gt" || n == "le" || n == "lt";
+        int64_t k = 0;
+        if (!cmp || r.op_arg.find("%{") != std::string::npos || !go_atoi(trim(r.op_arg), &k)) return -1;
+        bool m0 = n == "eq" ? 0 == k : n == "ge" ? 0 >= k : n == "gt" ? 0 > k : n == "le" ? 0 <= k : 0 < k;
+        if (r.op_neg) m0 = !m0;
+        if (m0) return -1;  // a zero count matches: the bit could not settle it
+        for (auto& v : r.vars)
+          if (single_id(v.name) >= 0 || v.name == "TX" || v.name.rfind("MATCHED_VAR", 0) == 0 ||
+              residual_collection(v.name))
+            return -1;
+        count_exists = true;
+      }
+    }
     bool scannable = n == "rx" || n == "pm" || n == "pmfromfile" || n == "validatebyterange" || n == "validateurlencoding" ||
                      n == "validateutf8encoding" || n == "detectsqli" || n == "detectxss" ||
-                     (n == "contains" && r.op_arg.find("%{") == std::string::npos);
+                     (n == "contains" && r.op_arg.find("%{") == std::string::npos) || count_exists;
     if (!scannable) return -1;
     bool bodydep = false, residual = false, res_single = false, rb_only = true;
     for (auto& v : r.vars) {
-      if (v.count) return -1;
+      if (v.count && !count_exists) return -1;
       int sid = single_id(v.name);
       if (sid >= 0 && !immutable_single(sid)) residual = res_single = true;  // tested by k_eval on a clear bit
       if (sid >= 0 && !immutable_single(sid) && sid != S_REQUEST_BODY) rb_only = false;
@@ -1882,14 +1909,14 @@ struct Lower {
       }
       StreamBuild& sb = sbuild[si];
       if (o.kind == OP_VALIDATE_BYTE_RANGE || o.kind == OP_VALIDATE_URL_ENCODING || o.kind == OP_VALIDATE_UTF8 ||
-          o.kind == OP_DETECT_SQLI || o.kind == OP_DETECT_XSS) {
+          o.kind == OP_DETECT_SQLI || o.kind == OP_DETECT_XSS || count_exists) {
         bool merged = false;
         for (auto& sv : sb.vals)
           if (sv.slot == (uint32_t)slot) sv.fmask |= 1ull << sb.gids[fid], merged = true;
         if (merged) continue;
         DScanVal sv{};
-        sv.kind = o.kind;
-        sv.negate = o.negate;
+        sv.kind = count_exists ? (uint8_t)OP_UNCONDITIONAL : o.kind;
+        sv.negate = count_exists ? 0 : o.negate;
         sv.fmask = 1ull << sb.gids[fid];
         sv.slot = (uint32_t)slot;
         for (int k = 0; k < 8; k++) sv.bits[k] = o.bits[k];

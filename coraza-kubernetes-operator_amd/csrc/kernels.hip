@@ -5059,6 +5059,7 @@ GI_HD inline void tx_bind(Tx& t, const DProgram& P, const Region& g) {
 }
 
 GI_HD inline bool validate_op(uint8_t kind, const uint32_t* bits, const uint8_t* s, uint32_t n) {
+  if (kind == OP_UNCONDITIONAL) return true;  // a count link's "an admitted entry exists" (compile.cpp plan)
   if (kind == OP_VALIDATE_BYTE_RANGE) {
     for (uint32_t i = 0; i < n; i++)
       if (!((bits[s[i] >> 5] >> (s[i] & 31)) & 1)) return true;
@@ -6860,6 +6861,7 @@ __device__ bool wave_dfa_match(const DProgram& P, const DDfa& d, const uint8_t* 
 
 // @validate* over s[0, n) by the whole wave: chunk results OR-ed
 __device__ bool wave_validate(const DOp& o, const uint8_t* s, uint32_t n) {
+  if (o.kind == OP_UNCONDITIONAL) return true;
   uint32_t a, e;
   if (o.kind == OP_VALIDATE_BYTE_RANGE) wave_chunks(n, [&](uint32_t) { return true; }, &a, &e);
   else if (o.kind == OP_VALIDATE_URL_ENCODING) wave_chunks(n, [&](uint32_t p) { return no_byte_before(s, p, 2, '%'); }, &a, &e);
@@ -7741,7 +7743,9 @@ GI_HD __forceinline__ uint32_t eord_key(const DBatch& B, uint32_t r) {
   const uint32_t nw = (B.n_hit_slots + 31) / 32;
   uint32_t c = 0;
   for (uint32_t w = 0; w < nw; w++) c += __popc(B.hits[(uint64_t)w * B.rstride + r]);
-  return min(c, (uint32_t)GI_EORD_BINS - 1);
+  // most set bits first: the heaviest waves start first and the light ones
+  // fill the tail (longest-processing-time-first across the CUs)
+  return (uint32_t)GI_EORD_BINS - 1 - min(c, (uint32_t)GI_EORD_BINS - 1);
 }
 // Both launches run GI_EORD_GRID workgroups, each over one contiguous chunk of
 // requests, with the bins counted in LDS: one global atomic per (workgroup,
