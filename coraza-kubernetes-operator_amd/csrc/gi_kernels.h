@@ -96,7 +96,7 @@ struct DBatch {
   uint64_t det_bytes_cap;
   unsigned long long* det_used;
   unsigned long long* diag;   // optional diagnostic counters (gi_stats.diag)
-  unsigned long long* vcause; // [5] phase-A void events per cause (GI_VOID_*, kernels.hip)
+  unsigned long long* vcause; // [6] phase-A void events per cause (GI_VOID_*, kernels.hip)
   uint32_t* dbg;              // debug-build bounds-violation record (-DGI_DEBUG)
   unsigned long long* prof;   // GI_PROF=1: k_eval cycle / rule counters (stderr at gi_sync)
   uint64_t items_cap;
@@ -121,6 +121,11 @@ struct DBatch {
                               // set phase-A hit bits, so a wave's lanes walk similar rule paths (k_eord_*)
   uint32_t* eord_bins;        // [GI_EORD_BINS] counts, then [GI_EORD_BINS] cursors (ctr)
   uint8_t* eord_key;          // per request: its bin (k_eord_count -> k_eord_scatter)
+  // header dedup (k_collect -> k_dspread): keys (hash | 1, 0 = empty) and per entry
+  // (canonical request + 1) << 32 | (field * 2 + side), 0 until published; nullptr: off
+  unsigned long long* hdkeys;
+  unsigned long long* hdinfo;
+  uint32_t hdmask;
   uint32_t* pcount;
   uint32_t wave_stage2;       // the body stage's pending requests all go to k_eval_wave (GI_EVAL_WAVE_STAGE2=0: by size)
   uint32_t body_tiles;        // k_body runs its chunkable transformations LDS-tiled (GI_BODY_TILES=0: off)

@@ -5121,6 +5121,7 @@ __device__ inline void set_hit(const DBatch& B, uint32_t slot, uint32_t r) {
 #define GI_VOID_SLOW 2
 #define GI_VOID_QCAP 3
 #define GI_VOID_POOL 4
+#define GI_VOID_DEDUP 5  // a header copy whose canonical occurrence's results are not exactly known
 GI_HD __forceinline__ void void_request(const DBatch& B, uint32_t r, uint32_t cause) {
   ReqHdr* H = (ReqHdr*)(B.scratch + B.layout[r].base);
   H->pa_void = 1;
@@ -5201,7 +5202,7 @@ GI_HD __forceinline__ uint64_t wave_sum(uint64_t x) {
 // body fields alone.
 template <class F>
 GI_HD __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H, const Field* Fd, F&& f,
-                                         uint32_t part = 0) {
+                                         uint32_t part = 0, bool dedup = false) {
   if (part != 2)
     for (uint32_t m = P.item_singles; m; m &= m - 1) {
       const uint32_t sg = __ffs(m) - 1;
@@ -5215,7 +5216,9 @@ GI_HD __forceinline__ void for_each_item(const DProgram& P, const ReqHdr* H, con
     // FILES_SIZES are phase-A items, part headers are not
     const uint8_t kind = i < n_get ? FK_ARG_GET : i < n_get + n_hdr ? FK_HEADER : i < n_pre ? FK_COOKIE : (uint8_t)fl.kind;
     if (kind < FK_ARG_GET || kind > FK_FILE_SIZE) continue;
-    const uint8_t sides = P.item_sides[kind];
+    // (a header side k_collect found a copy of elsewhere in the chunk: no item,
+    // k_dspread copies the copy's phase-A results -- Field._pad bit = side)
+    const uint8_t sides = P.item_sides[kind] & (dedup && kind == FK_HEADER ? ~(uint8_t)fl._pad : 0xFFu);
     if (sides & 1) f(kind, (uint8_t)0, 0u, i, fl.vn);
     if (sides & 2) f(kind, (uint8_t)0, 1u, i, fl.kn);
   }
@@ -5607,6 +5610,85 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
   }
 }
 
+// ------------------------------------------------------- header dedup
+// A chunk's requests repeat most header lines byte for byte (User-Agent,
+// Accept*, Host, ...), and phase A's results for a (field kind, side, key,
+// value) are the same wherever it occurs: the filters admitting it depend on
+// the kind, side and key, the chains, automata, validators and detectors on
+// the bytes.  k_collect keys every header side by its bytes in a chunk-wide
+// table: the first occurrence claims the entry (the canonical one, scanned as
+// usual), a later byte-equal one becomes no item at all (Field._pad bit
+// `side`).  After phase A, k_dspread gives each such copy the canonical
+// value's results: its value-signature word, and per slot of that signature
+// the exact / maybe key of the canonical's hit set -> hit bit + the copy's own
+// hit-set key.  Exact: a canonical whose results are not exactly known (its
+// hit set overflowed, its request voided or flagged) voids the copy's request
+// (k_eval then evaluates it in full).  Nobody waits: an entry seen before its
+// claimer published it just leaves this occurrence canonical-less (scanned).
+#define GI_HD_PROBES 16
+__device__ __forceinline__ unsigned long long hdr_hash(uint32_t side, const Field& f) {
+  unsigned long long h = (1469598103934665603ull ^ (side + 1u)) * 1099511628211ull;
+  h = (h ^ f.kn) * 1099511628211ull;
+  for (uint32_t i = 0; i < f.kn; i++) h = (h ^ f.k[i]) * 1099511628211ull;
+  if (side == 0) {
+    h = (h ^ (0x100000000ull | f.vn)) * 1099511628211ull;
+    for (uint32_t i = 0; i < f.vn; i++) h = (h ^ f.v[i]) * 1099511628211ull;
+  }
+  return h | 1ull;
+}
+__device__ __forceinline__ bool hdr_same(uint32_t side, const Field& a, const Field& b) {
+  if (a.kn != b.kn || (side == 0 && a.vn != b.vn)) return false;
+  for (uint32_t i = 0; i < a.kn; i++)
+    if (a.k[i] != b.k[i]) return false;
+  if (side == 0)
+    for (uint32_t i = 0; i < a.vn; i++)
+      if (a.v[i] != b.v[i]) return false;
+  return true;
+}
+// The canonical occurrence of header side (f, side) of request r: true with
+// (*r0, *f0) when a published, byte-equal entry exists; claim: take an empty
+// entry on the way (this occurrence becomes canonical).
+__device__ bool hdr_find(const DBatch& B, unsigned long long h, uint32_t side, const Field& f, uint32_t r, uint32_t fi,
+                         bool claim, uint32_t* r0, uint32_t* f0) {
+  for (uint32_t p = 0; p < GI_HD_PROBES; p++) {
+    const uint32_t e = (uint32_t)(h + p) & B.hdmask;
+    unsigned long long k = __atomic_load_n(&B.hdkeys[e], __ATOMIC_RELAXED);
+    if (k == 0) {
+      if (!claim) return false;
+      k = atomicCAS(&B.hdkeys[e], 0ull, h);
+      if (k == 0) {  // canonical: publish where its fields are (written before the fence)
+        __threadfence();
+        atomicExch(&B.hdinfo[e], ((unsigned long long)(r + 1u) << 32) | (2ull * fi + side));
+        return false;
+      }
+    }
+    if (k != h) continue;
+    const unsigned long long inf = __atomic_load_n(&B.hdinfo[e], __ATOMIC_ACQUIRE);
+    if (inf == 0) return false;  // not published yet: this occurrence stays canonical-less
+    const uint32_t cr = (uint32_t)(inf >> 32) - 1u, cf = (uint32_t)inf >> 1;
+    if (((uint32_t)inf & 1u) != side || cr >= B.n_req || cr == r) continue;
+    const Field* Fc = (const Field*)(B.scratch + B.layout[cr].base + GI_REQHDR_BYTES);
+    if (!hdr_same(side, f, Fc[cf])) continue;
+    *r0 = cr;
+    *f0 = cf;
+    return true;
+  }
+  return false;
+}
+__device__ void hdr_dedup(const DProgram& P, const DBatch& B, uint32_t r, const ReqHdr* H, Field* Fd) {
+  const uint32_t sides = P.item_sides[FK_HEADER];
+  for (uint32_t i = H->n_get; i < H->n_get + H->n_hdr; i++) {
+    const Field fl = Fd[i];
+    uint32_t mark = 0;
+    for (uint32_t side = 0; side < 2; side++) {
+      if (!((sides >> side) & 1u)) continue;
+      uint32_t r0, f0;
+      if (hdr_find(B, hdr_hash(side, fl), side, fl, r, i, true, &r0, &f0)) mark |= 1u << side;
+    }
+    Fd[i]._pad = mark;
+  }
+}
+
 // ProcessURI + AddRequestHeader* for one request per thread, then the
 // per-block item counts per length bucket (k_ioffsets / k_items) and the hit
 // bits of links without an automaton image.
@@ -5621,10 +5703,12 @@ __global__ void __launch_bounds__(256) k_collect(DProgram P, DBatch B) {
       const ReqLayout L = B.layout[r];
       const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
       if (!(H->flags & GI_REQ_ERROR_MASK)) {
-        for_each_item(P, H, (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES),
+        Field* Fd = (Field*)(B.scratch + L.base + GI_REQHDR_BYTES);
+        if (B.hdkeys) hdr_dedup(P, B, r, H, Fd);
+        for_each_item(P, H, Fd,
                       [&](uint8_t kind, uint8_t, uint32_t side, uint32_t, uint32_t n) {
                         atomicAdd(&hist[item_class(kind, side, n)], 1u);
-                      });
+                      }, 0u, B.hdkeys != nullptr);
       }
       for (uint32_t k = 0; k < P.n_always; k++) set_hit(B, P.always_slots[k], r);
     }
@@ -5818,7 +5902,7 @@ __global__ void __launch_bounds__(256) k_items(DProgram P, DBatch B) {
         if (kind && fi > GI_MAX_ITEM_FIELD) void_request(B, r, GI_VOID_FIELD);  // no value-map index: no phase-A bit trusted
         ((Item*)B.items)[at] = it;
         atomicAdd(&ibytes[b], (unsigned long long)n);
-      }, B.stage == 2 ? 2u : 0u);  // the body stage: the pending requests' body fields
+      }, B.stage == 2 ? 2u : 0u, B.hdkeys != nullptr);  // the body stage: the pending requests' body fields
     }
   }
   __syncthreads();
@@ -7986,6 +8070,52 @@ void cpu_inspect_one(const DProgram& P, const DBatch& B) {
   eval_request<false>(P, B, 0, nullptr, 0, my);
 }
 
+// The copies' phase-A results from their canonical occurrences (hdr_dedup),
+// one thread per request, after every phase-A producer of the stage.
+__global__ void __launch_bounds__(256) k_dspread(DProgram P, DBatch B) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B.n_req) return;
+  const ReqLayout L = B.layout[r];
+  const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
+  if (H->flags & GI_REQ_ERROR_MASK) return;
+  const Field* Fd = (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES);
+  bool voided = false;
+  for (uint32_t i = H->n_get; i < H->n_get + H->n_hdr && !voided; i++) {
+    const Field fl = Fd[i];
+    for (uint32_t side = 0; side < 2 && !voided; side++) {
+      if (!((fl._pad >> side) & 1u)) continue;
+      uint32_t r0, f0;
+      bool ok = hdr_find(B, hdr_hash(side, fl), side, fl, r, i, false, &r0, &f0);
+      ReqLayout L0{};
+      const uint32_t* tab0 = nullptr;
+      if (ok) {
+        L0 = B.layout[r0];
+        const ReqHdr* H0 = (const ReqHdr*)(B.scratch + L0.base);
+        tab0 = B.hset + L0.hset_word;
+        ok = !H0->pa_void && !(H0->flags & GI_REQ_ERROR_MASK) && L0.hset_mask && tab0[0] == 0u;
+      }
+      if (!ok) {  // the canonical's results are not exactly known: evaluate this request in full
+        void_request(B, r, GI_VOID_DEDUP);
+        voided = true;
+        continue;
+      }
+      const uint32_t vix0 = 2u * f0 + side, vix = 2u * i + side;
+      GI_BOUND(vix0 < L0.vmap_bits && vix < L.vmap_bits, vix0, vix);
+      const uint32_t vb = B.vmap[L0.vmap_bit + vix0];
+      if (!vb) continue;
+      atomicOr(&B.vmap[L.vmap_bit + vix], vb);
+      for (uint32_t m = vb; m; m &= m - 1) {
+        for (uint32_t s = (uint32_t)(__ffs(m) - 1); s < B.n_hit_slots; s += 32) {
+          const uint32_t res = hset_lookup(tab0, L0.hset_mask, s, vix0);
+          if (!res) continue;
+          set_hit(B, s, r);
+          if (L.hset_mask) hset_insert(B, L, s, vix, res == 2 ? 1u : 0u);
+        }
+      }
+    }
+  }
+}
+
 // Phase A over the items of the current stage: item records, the streams'
 // transformation chains, libinjection, long values and the automaton scans.
 static void launch_phase_a(const DProgram& P, const DBatch& B, const ScanLaunch& S, hipStream_t stream,
@@ -8024,6 +8154,8 @@ static void launch_phase_a(const DProgram& P, const DBatch& B, const ScanLaunch&
     GI_LAUNCH(s2 ? "k_scan_hbm.2" : "k_scan_hbm", (k_scan<false, false>), dim3(S.blocks[2]), dim3(1024), 0, stream, P, B, S.global_jobs,
               S.n_global, S.mode, 2u);
   GI_LAUNCH(s2 ? "k_scan_slow.2" : "k_scan_slow", k_scan_slow, dim3(1024), dim3(256), 0, stream, P, B);
+  // (the copies are header sides: phase-1 items, all scanned in the first / only stage)
+  if (B.hdkeys && !s2) GI_LAUNCH("k_dspread", k_dspread, dim3((B.n_req + 255) / 256), dim3(256), 0, stream, P, B);
 }
 
 static void launch_eval(const DProgram& P, const DBatch& B, hipStream_t stream, int stop_after, LaunchLog* log,

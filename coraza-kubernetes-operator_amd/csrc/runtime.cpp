@@ -95,6 +95,8 @@ struct gi_ctx {
   DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf, wlist;
   DevBuf pend, plist;  // phase-1 gate (launch_pipeline): pending flags + list
   DevBuf eorder, ekey;  // k_eval's request order (k_eord_*: requests grouped by phase-A hit count), bins
+  DevBuf hdkeys, hdinfo;  // header dedup table (k_collect / k_dspread)
+  uint32_t hdmask = 0;
   DevBuf dmemo_keys, dmemo_info;  // k_detect's detector-result memo
   uint32_t dmemo_mask = 0;
   uint32_t long_cap = 0, long_grid = GI_LONG_GRID;
@@ -645,7 +647,7 @@ void gi_ctx_free(gi_ctx* c) {
   for (DevBuf* b : {&c->caprec, &c->capbytes, &c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->hset, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist, &c->pend, &c->plist, &c->dmemo_keys, &c->dmemo_info,
-                    &c->eorder, &c->ekey, &c->cappool, &c->progdev})
+                    &c->eorder, &c->ekey, &c->hdkeys, &c->hdinfo, &c->cappool, &c->progdev})
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
@@ -1048,6 +1050,16 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
     const uint32_t cb = (uint32_t)((cmax.n + 255) / 256);
     const uint32_t ns = (uint32_t)PG.streams.size();
     c->items_cap = std::max<uint64_t>(cmax.items, 1);
+    // header dedup table: a power of two >= the chunk's items (<= 2^24 entries, 16 B each)
+    c->hdmask = 0;
+    static const bool hd_env = !(getenv("GI_DEDUP") && atoi(getenv("GI_DEDUP")) == 0);
+    if (hd_env && PG.item_sides[FK_HEADER] && cmax.n >= 4096) {
+      uint64_t cap = 1024;
+      while (cap < cmax.items && cap < (1ull << 24)) cap <<= 1;
+      if ((e = c->hdkeys.ensure(8 * cap)) != hipSuccess) return hip_fail(c, e, "alloc header dedup table");
+      if ((e = c->hdinfo.ensure(8 * cap)) != hipSuccess) return hip_fail(c, e, "alloc header dedup table");
+      c->hdmask = (uint32_t)(cap - 1);
+    }
     c->lcap = (std::min<uint32_t>(max_cap_t, 4096) + 15) & ~15u;
     // chunked reservations leave at most one partial chunk per (k_stream
     // wave, launch) unused: both capacities carry that slack
@@ -1232,7 +1244,7 @@ int gi_run_staged(gi_ctx* c) {
     }
     B.items_cap = c->items_cap;
     B.n_hit_slots = c->rs->prog.n_hit_slots;
-    B.vcause = (unsigned long long*)(cp + 288);  // 5 void-cause counters
+    B.vcause = (unsigned long long*)(cp + 288);  // 6 void-cause counters
     B.dbg = (uint32_t*)(cp + 128);  // 4 words (only written by -DGI_DEBUG builds)
     const bool wave = (c->wave_fields || c->wave_rules) && c->wlist.p && cp;
     B.wlist = wave ? (uint32_t*)c->wlist.p : nullptr;
@@ -1256,6 +1268,9 @@ int gi_run_staged(gi_ctx* c) {
     B.eorder = eord_env ? (uint32_t*)c->eorder.p : nullptr;
     B.eord_bins = (uint32_t*)(cp + 1024);
     B.eord_key = (uint8_t*)c->ekey.p;
+    B.hdkeys = c->hdmask ? (unsigned long long*)c->hdkeys.p : nullptr;
+    B.hdinfo = c->hdmask ? (unsigned long long*)c->hdinfo.p : nullptr;
+    B.hdmask = c->hdmask;
     static const uint32_t tiles_env = getenv("GI_BODY_TILES") ? (uint32_t)atoi(getenv("GI_BODY_TILES")) : 1u;
     B.body_tiles = tiles_env;
     static const uint32_t ws2_env = getenv("GI_EVAL_WAVE_STAGE2") ? (uint32_t)atoi(getenv("GI_EVAL_WAVE_STAGE2")) : 1u;
@@ -1292,6 +1307,11 @@ int gi_run_staged(gi_ctx* c) {
     if (k && c->ctr.p) {
       e = hipMemsetAsync(c->ctr.p, 0, 128, c->stream);
       if (e != hipSuccess) return hip_fail(c, e, "memset chunk counters");
+    }
+    if (B.hdkeys) {  // the dedup table is per chunk (its entries name chunk-local requests)
+      e = hipMemsetAsync(B.hdkeys, 0, 8ull * (c->hdmask + 1), c->stream);
+      if (e == hipSuccess) e = hipMemsetAsync(B.hdinfo, 0, 8ull * (c->hdmask + 1), c->stream);
+      if (e != hipSuccess) return hip_fail(c, e, "memset header dedup table");
     }
     DBatch Bc = B;
     Bc.n_req = ch.n;
