@@ -125,6 +125,7 @@ struct DBatch {
   // (canonical request + 1) << 32 | (field * 2 + side), 0 until published; nullptr: off
   unsigned long long* hdkeys;
   unsigned long long* hdinfo;
+  uint32_t* hdref;            // [2 * header slot + side]: a copy's canonical entry + 1 (0: none)
   uint32_t hdmask;
   uint32_t* pcount;
   uint32_t wave_stage2;       // the body stage's pending requests all go to k_eval_wave (GI_EVAL_WAVE_STAGE2=0: by size)

@@ -5626,30 +5626,39 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
 // (k_eval then evaluates it in full).  Nobody waits: an entry seen before its
 // claimer published it just leaves this occurrence canonical-less (scanned).
 #define GI_HD_PROBES 16
-__device__ __forceinline__ unsigned long long hdr_hash(uint32_t side, const Field& f) {
-  unsigned long long h = (1469598103934665603ull ^ (side + 1u)) * 1099511628211ull;
-  h = (h ^ f.kn) * 1099511628211ull;
-  for (uint32_t i = 0; i < f.kn; i++) h = (h ^ f.k[i]) * 1099511628211ull;
-  if (side == 0) {
-    h = (h ^ (0x100000000ull | f.vn)) * 1099511628211ull;
-    for (uint32_t i = 0; i < f.vn; i++) h = (h ^ f.v[i]) * 1099511628211ull;
+// (a word at a time: header bytes sit in the padded request arena)
+__device__ __forceinline__ unsigned long long hdr_mix(unsigned long long h, const uint8_t* p, uint32_t n) {
+  h = (h ^ (0x100000000ull | n)) * 1099511628211ull;
+  for (uint32_t i = 0; i < n; i += 4) {
+    uint32_t w = load_u32u(p + i);
+    if (n - i < 4) w &= (1u << (8 * (n - i))) - 1u;
+    h = (h ^ w) * 1099511628211ull;
   }
+  return h;
+}
+__device__ __forceinline__ unsigned long long hdr_hash(uint32_t side, const Field& f) {
+  unsigned long long h = hdr_mix((1469598103934665603ull ^ (side + 1u)) * 1099511628211ull, f.k, f.kn);
+  if (side == 0) h = hdr_mix(h, f.v, f.vn);
   return h | 1ull;
+}
+__device__ __forceinline__ bool hdr_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  bool eq = true;
+  for (uint32_t i = 0; i < n && eq; i += 4) {
+    uint32_t x = load_u32u(a + i) ^ load_u32u(b + i);
+    if (n - i < 4) x &= (1u << (8 * (n - i))) - 1u;
+    eq = x == 0;
+  }
+  return eq;
 }
 __device__ __forceinline__ bool hdr_same(uint32_t side, const Field& a, const Field& b) {
   if (a.kn != b.kn || (side == 0 && a.vn != b.vn)) return false;
-  for (uint32_t i = 0; i < a.kn; i++)
-    if (a.k[i] != b.k[i]) return false;
-  if (side == 0)
-    for (uint32_t i = 0; i < a.vn; i++)
-      if (a.v[i] != b.v[i]) return false;
-  return true;
+  return hdr_eq(a.k, b.k, a.kn) && (side != 0 || hdr_eq(a.v, b.v, a.vn));
 }
 // The canonical occurrence of header side (f, side) of request r: true with
 // (*r0, *f0) when a published, byte-equal entry exists; claim: take an empty
 // entry on the way (this occurrence becomes canonical).
 __device__ bool hdr_find(const DBatch& B, unsigned long long h, uint32_t side, const Field& f, uint32_t r, uint32_t fi,
-                         bool claim, uint32_t* r0, uint32_t* f0) {
+                         bool claim, uint32_t* r0, uint32_t* f0, uint32_t* ent) {
   for (uint32_t p = 0; p < GI_HD_PROBES; p++) {
     const uint32_t e = (uint32_t)(h + p) & B.hdmask;
     unsigned long long k = __atomic_load_n(&B.hdkeys[e], __ATOMIC_RELAXED);
@@ -5671,19 +5680,26 @@ __device__ bool hdr_find(const DBatch& B, unsigned long long h, uint32_t side, c
     if (!hdr_same(side, f, Fc[cf])) continue;
     *r0 = cr;
     *f0 = cf;
+    *ent = e;
     return true;
   }
   return false;
 }
+// (a copy's canonical entry + 1 goes to hdref[2 * (the request's header slot
+// hdr_begin + i - n_get) + side]: k_dspread reads it instead of probing again)
 __device__ void hdr_dedup(const DProgram& P, const DBatch& B, uint32_t r, const ReqHdr* H, Field* Fd) {
   const uint32_t sides = P.item_sides[FK_HEADER];
+  const uint32_t hb = B.reqs[r].hdr_begin;
   for (uint32_t i = H->n_get; i < H->n_get + H->n_hdr; i++) {
     const Field fl = Fd[i];
     uint32_t mark = 0;
     for (uint32_t side = 0; side < 2; side++) {
       if (!((sides >> side) & 1u)) continue;
-      uint32_t r0, f0;
-      if (hdr_find(B, hdr_hash(side, fl), side, fl, r, i, true, &r0, &f0)) mark |= 1u << side;
+      uint32_t r0, f0, e;
+      if (hdr_find(B, hdr_hash(side, fl), side, fl, r, i, true, &r0, &f0, &e)) {
+        mark |= 1u << side;
+        B.hdref[2ull * (hb + i - H->n_get) + side] = e + 1u;
+      }
     }
     Fd[i]._pad = mark;
   }
@@ -8084,8 +8100,15 @@ __global__ void __launch_bounds__(256) k_dspread(DProgram P, DBatch B) {
     const Field fl = Fd[i];
     for (uint32_t side = 0; side < 2 && !voided; side++) {
       if (!((fl._pad >> side) & 1u)) continue;
-      uint32_t r0, f0;
-      bool ok = hdr_find(B, hdr_hash(side, fl), side, fl, r, i, false, &r0, &f0);
+      const uint32_t e1 = B.hdref[2ull * (B.reqs[r].hdr_begin + i - H->n_get) + side];
+      bool ok = e1 != 0 && e1 - 1u <= B.hdmask;
+      uint32_t r0 = 0, f0 = 0;
+      if (ok) {  // (published before hdr_dedup recorded it: k_collect, a launch earlier)
+        const unsigned long long inf = B.hdinfo[e1 - 1u];
+        r0 = (uint32_t)(inf >> 32) - 1u;
+        f0 = (uint32_t)inf >> 1;
+        ok = inf != 0 && r0 < B.n_req;
+      }
       ReqLayout L0{};
       const uint32_t* tab0 = nullptr;
       if (ok) {
@@ -8161,7 +8184,9 @@ static void launch_phase_a(const DProgram& P, const DBatch& B, const ScanLaunch&
 static void launch_eval(const DProgram& P, const DBatch& B, hipStream_t stream, int stop_after, LaunchLog* log,
                         int& nk) {
   DBatch Be = B;
-  if (B.n_req < 4096 || B.stage == 2) Be.eorder = nullptr;  // (a small batch: its few waves gain nothing)
+  // the order pays on header-only traffic (C2: k_eval 15.2 -> 12.8 ms); with bodies in more than
+  // 1 of 8 requests the waves of many-field requests it builds cost more (C3: 170 -> 259 ms)
+  if (B.n_req < 4096 || B.stage == 2 || 8ull * B.n_body > B.n_req) Be.eorder = nullptr;
   if (Be.eorder) {
     const uint32_t cb = (B.n_req + 255) / 256;
     (void)hipMemsetAsync(B.eord_bins, 0, 8 * GI_EORD_BINS, stream);

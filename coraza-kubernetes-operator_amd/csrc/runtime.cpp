@@ -95,7 +95,7 @@ struct gi_ctx {
   DevBuf bcounts, boffs, items, igm, lscratch, pool, qblk, ctr, slow, slow_bytes, det, det_bytes, long_list, long_buf, wlist;
   DevBuf pend, plist;  // phase-1 gate (launch_pipeline): pending flags + list
   DevBuf eorder, ekey;  // k_eval's request order (k_eord_*: requests grouped by phase-A hit count), bins
-  DevBuf hdkeys, hdinfo;  // header dedup table (k_collect / k_dspread)
+  DevBuf hdkeys, hdinfo, hdref;  // header dedup table (k_collect / k_dspread), copies' entries
   uint32_t hdmask = 0;
   DevBuf dmemo_keys, dmemo_info;  // k_detect's detector-result memo
   uint32_t dmemo_mask = 0;
@@ -647,7 +647,7 @@ void gi_ctx_free(gi_ctx* c) {
   for (DevBuf* b : {&c->caprec, &c->capbytes, &c->data, &c->reqs, &c->hdrs, &c->layout, &c->scratch, &c->verdicts, &c->matched, &c->tally, &c->tally_ext, &c->tally_idbuf,
                     &c->hits, &c->vmap, &c->hset, &c->blist, &c->joblist, &c->txslots, &c->bcounts, &c->boffs, &c->items, &c->igm, &c->lscratch, &c->pool, &c->qblk,
                     &c->ctr, &c->slow, &c->slow_bytes, &c->det, &c->det_bytes, &c->long_list, &c->long_buf, &c->wlist, &c->pend, &c->plist, &c->dmemo_keys, &c->dmemo_info,
-                    &c->eorder, &c->ekey, &c->hdkeys, &c->hdinfo, &c->cappool, &c->progdev})
+                    &c->eorder, &c->ekey, &c->hdkeys, &c->hdinfo, &c->hdref, &c->cappool, &c->progdev})
     b->release();
   for (auto& ev : c->evs)
     if (ev) (void)hipEventDestroy(ev);
@@ -1058,6 +1058,8 @@ int gi_stage_batch(gi_ctx* c, const gi_batch* in) {
       while (cap < cmax.items && cap < (1ull << 24)) cap <<= 1;
       if ((e = c->hdkeys.ensure(8 * cap)) != hipSuccess) return hip_fail(c, e, "alloc header dedup table");
       if ((e = c->hdinfo.ensure(8 * cap)) != hipSuccess) return hip_fail(c, e, "alloc header dedup table");
+      if ((e = c->hdref.ensure(std::max<uint64_t>(8ull * in->n_headers, 16))) != hipSuccess)
+        return hip_fail(c, e, "alloc header dedup refs");
       c->hdmask = (uint32_t)(cap - 1);
     }
     c->lcap = (std::min<uint32_t>(max_cap_t, 4096) + 15) & ~15u;
@@ -1270,6 +1272,7 @@ int gi_run_staged(gi_ctx* c) {
     B.eord_key = (uint8_t*)c->ekey.p;
     B.hdkeys = c->hdmask ? (unsigned long long*)c->hdkeys.p : nullptr;
     B.hdinfo = c->hdmask ? (unsigned long long*)c->hdinfo.p : nullptr;
+    B.hdref = c->hdmask ? (uint32_t*)c->hdref.p : nullptr;
     B.hdmask = c->hdmask;
     static const uint32_t tiles_env = getenv("GI_BODY_TILES") ? (uint32_t)atoi(getenv("GI_BODY_TILES")) : 1u;
     B.body_tiles = tiles_env;
