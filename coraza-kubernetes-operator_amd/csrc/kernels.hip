@@ -5654,51 +5654,67 @@ __device__ __forceinline__ bool hdr_same(uint32_t side, const Field& a, const Fi
   if (a.kn != b.kn || (side == 0 && a.vn != b.vn)) return false;
   return hdr_eq(a.k, b.k, a.kn) && (side != 0 || hdr_eq(a.v, b.v, a.vn));
 }
-// The canonical occurrence of header side (f, side) of request r: true with
-// (*r0, *f0) when a published, byte-equal entry exists; claim: take an empty
-// entry on the way (this occurrence becomes canonical).
+// Entry info word, published once with one 64-bit atomic store: (global
+// header index + 1) << 37 | request << 13 | (field * 2 + side).  A reader
+// compares its bytes with the canonical's through the global header record
+// and the request arena -- input data, immutable -- so it needs no acquire
+// ordering (and pays no cache invalidation) to trust what it compares.
+#define GI_HD_INFO(g, r, fs) ((((unsigned long long)(g) + 1ull) << 37) | ((unsigned long long)(r) << 13) | (fs))
+__device__ __forceinline__ uint32_t hd_info_req(unsigned long long inf) { return (uint32_t)(inf >> 13) & 0xFFFFFFu; }
+__device__ __forceinline__ uint32_t hd_info_fs(unsigned long long inf) { return (uint32_t)inf & 0x1FFFu; }
+__device__ __forceinline__ uint32_t hd_info_hdr(unsigned long long inf) { return (uint32_t)(inf >> 37) - 1u; }
+
+// The canonical occurrence of header side (f, side) of request r (global
+// header index g, field fi): true with its entry when a published byte-equal
+// entry exists; otherwise an empty entry on the way is claimed (this
+// occurrence becomes canonical).
 __device__ bool hdr_find(const DBatch& B, unsigned long long h, uint32_t side, const Field& f, uint32_t r, uint32_t fi,
-                         bool claim, uint32_t* r0, uint32_t* f0, uint32_t* ent) {
+                         uint32_t g, uint32_t* ent) {
+  const bool can_claim = g + 1u < (1u << 27) && r < (1u << 24) && 2u * fi + side < (1u << 13);
   for (uint32_t p = 0; p < GI_HD_PROBES; p++) {
     const uint32_t e = (uint32_t)(h + p) & B.hdmask;
     unsigned long long k = __atomic_load_n(&B.hdkeys[e], __ATOMIC_RELAXED);
     if (k == 0) {
-      if (!claim) return false;
+      if (!can_claim) return false;
       k = atomicCAS(&B.hdkeys[e], 0ull, h);
-      if (k == 0) {  // canonical: publish where its fields are (written before the fence)
-        __threadfence();
-        atomicExch(&B.hdinfo[e], ((unsigned long long)(r + 1u) << 32) | (2ull * fi + side));
+      if (k == 0) {
+        atomicExch(&B.hdinfo[e], GI_HD_INFO(g, r, 2u * fi + side));
         return false;
       }
     }
     if (k != h) continue;
-    const unsigned long long inf = __atomic_load_n(&B.hdinfo[e], __ATOMIC_ACQUIRE);
+    const unsigned long long inf = __atomic_load_n(&B.hdinfo[e], __ATOMIC_RELAXED);
     if (inf == 0) return false;  // not published yet: this occurrence stays canonical-less
-    const uint32_t cr = (uint32_t)(inf >> 32) - 1u, cf = (uint32_t)inf >> 1;
-    if (((uint32_t)inf & 1u) != side || cr >= B.n_req || cr == r) continue;
-    const Field* Fc = (const Field*)(B.scratch + B.layout[cr].base + GI_REQHDR_BYTES);
-    if (!hdr_same(side, f, Fc[cf])) continue;
-    *r0 = cr;
-    *f0 = cf;
+    if ((hd_info_fs(inf) & 1u) != side || hd_info_req(inf) == r) continue;
+    const gi_header hd = B.headers[hd_info_hdr(inf)];
+    Field c;
+    c.k = B.data + hd.name.off;
+    c.kn = hd.name.len;
+    c.v = B.data + hd.value.off;
+    c.vn = hd.value.len;
+    if (!hdr_same(side, f, c)) continue;
     *ent = e;
     return true;
   }
   return false;
 }
-// (a copy's canonical entry + 1 goes to hdref[2 * (the request's header slot
-// hdr_begin + i - n_get) + side]: k_dspread reads it instead of probing again)
+// (a copy's canonical entry + 1 goes to hdref[2 * global header index + side]:
+// k_dspread reads it instead of probing again)
 __device__ void hdr_dedup(const DProgram& P, const DBatch& B, uint32_t r, const ReqHdr* H, Field* Fd) {
   const uint32_t sides = P.item_sides[FK_HEADER];
-  const uint32_t hb = B.reqs[r].hdr_begin;
+  const gi_request rq = B.reqs[r];
+  uint32_t hx = 0;  // header record of field i (collect_request skips empty names)
   for (uint32_t i = H->n_get; i < H->n_get + H->n_hdr; i++) {
+    while (hx < rq.hdr_count && B.headers[rq.hdr_begin + hx].name.len == 0) hx++;
+    const uint32_t g = rq.hdr_begin + hx++;
     const Field fl = Fd[i];
     uint32_t mark = 0;
     for (uint32_t side = 0; side < 2; side++) {
       if (!((sides >> side) & 1u)) continue;
-      uint32_t r0, f0, e;
-      if (hdr_find(B, hdr_hash(side, fl), side, fl, r, i, true, &r0, &f0, &e)) {
+      uint32_t e;
+      if (hdr_find(B, hdr_hash(side, fl), side, fl, r, i, g, &e)) {
         mark |= 1u << side;
-        B.hdref[2ull * (hb + i - H->n_get) + side] = e + 1u;
+        B.hdref[2ull * g + side] = e + 1u;
       }
     }
     Fd[i]._pad = mark;
@@ -8095,18 +8111,22 @@ __global__ void __launch_bounds__(256) k_dspread(DProgram P, DBatch B) {
   const ReqHdr* H = (const ReqHdr*)(B.scratch + L.base);
   if (H->flags & GI_REQ_ERROR_MASK) return;
   const Field* Fd = (const Field*)(B.scratch + L.base + GI_REQHDR_BYTES);
+  const gi_request rq = B.reqs[r];
   bool voided = false;
+  uint32_t hx = 0;
   for (uint32_t i = H->n_get; i < H->n_get + H->n_hdr && !voided; i++) {
+    while (hx < rq.hdr_count && B.headers[rq.hdr_begin + hx].name.len == 0) hx++;
+    const uint32_t g = rq.hdr_begin + hx++;
     const Field fl = Fd[i];
     for (uint32_t side = 0; side < 2 && !voided; side++) {
       if (!((fl._pad >> side) & 1u)) continue;
-      const uint32_t e1 = B.hdref[2ull * (B.reqs[r].hdr_begin + i - H->n_get) + side];
+      const uint32_t e1 = B.hdref[2ull * g + side];
       bool ok = e1 != 0 && e1 - 1u <= B.hdmask;
       uint32_t r0 = 0, f0 = 0;
       if (ok) {  // (published before hdr_dedup recorded it: k_collect, a launch earlier)
         const unsigned long long inf = B.hdinfo[e1 - 1u];
-        r0 = (uint32_t)(inf >> 32) - 1u;
-        f0 = (uint32_t)inf >> 1;
+        r0 = hd_info_req(inf);
+        f0 = hd_info_fs(inf) >> 1;
         ok = inf != 0 && r0 < B.n_req;
       }
       ReqLayout L0{};
