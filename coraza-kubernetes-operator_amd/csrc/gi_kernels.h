@@ -105,6 +105,7 @@ struct DBatch {
   uint32_t* wcount;
   uint32_t wave_fields;       // k_eval_wave: requests with this many fields (0: none)
   uint32_t wave_rules;        // k_eval_wave: every request when the program walks this many rules (0: never)
+  uint32_t bparse_wave;        // k_bparse: JSON bodies parsed by the whole wave (wave_parse_json; GI_BPARSE_WAVE=0: lane 0)
   uint32_t bparse_lds;        // k_bparse: JSON bodies up to this many bytes are parsed from LDS (its dynamic LDS)
   uint32_t rstride;           // request stride of the request-major SoA arrays (hits, txslots): the staged
                               // batch's size (a chunk view of it has n_req <= rstride)
@@ -165,6 +166,7 @@ struct ScanLaunch {
 #define GI_EVAL_WAVE_RULES 2048
 #define GI_BPARSE_LDS 0              // k_bparse LDS copy of JSON bodies up to this size (GI_BPARSE_LDS env; 0: off --
                                      // measured: 32 KB made C3's k_bparse 81 -> 272 ms, the LDS cut its occupancy)
+#define GI_BPARSE_WIN 4096           // wave_parse_json's LDS window over a JSON body (GI_BPARSE_WIN env, >= 2048)
 #define GI_EORD_BINS 32               // k_eval order: bins of hit-bit counts
 #define GI_EORD_GRID 512              // k_eord_* workgroups (each a contiguous chunk of requests)
 #define GI_GATE_PENDING_MAX 0.5       // the adaptive gate runs while at most this share of body requests stays pending

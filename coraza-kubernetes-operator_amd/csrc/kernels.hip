@@ -5378,11 +5378,403 @@ __device__ __forceinline__ void urlenc_segment(const uint8_t* q, uint32_t n, uin
   *vesc = ve;
 }
 
+// ---------------------------------------------------- wave-uniform JSON parse
+// parse_json_body restated for one wave: every lane runs the same control
+// flow on the same (uniform) parser state, so the wave can do the byte work
+// 64 bytes at a time -- a string's end is one ballot over 64 bytes of an LDS
+// window of the body, a flattened key is built in an LDS path buffer (a
+// member's key extends its container's, which is a prefix of it) and copied
+// to the arena by the lanes together, and its hash is a wave reduction.  The
+// fields, their order, the arena allocations and the limits are exactly
+// parse_json_body's; whatever it would reject (syntax, limits, capacity) or
+// this restatement cannot hold (a key longer than the path buffer) returns
+// false: the speculative parse then leaves no fields and k_eval parses the
+// body itself.  Repeated keys: a parallel insert into a hash table of the key
+// hashes finds whether any key repeats; if one does, lane 0 runs the
+// sequential json_fold_keys (the fold itself is rare).
+#define GI_JW_PATH 1024
+struct JWFrame {
+  uint32_t koff, kn;  // the container's own key (offset into the arena)
+  uint32_t count;
+  uint32_t is_arr;
+  uint32_t h;         // its hash (wave_key_hash)
+};
+
+// decimal digits of v, and the digits written to d[0, nd)
+__device__ __forceinline__ uint32_t dec_len(uint32_t v) {
+  uint32_t nd = 1;
+  for (; v >= 10; v /= 10) nd++;
+  return nd;
+}
+template <class D>
+__device__ __forceinline__ void dec_put(uint32_t v, uint32_t nd, D* d) {
+  for (uint32_t k = nd; k > 0; k--) {
+    d[k - 1] = (uint8_t)('0' + v % 10);
+    v /= 10;
+  }
+}
+
+struct JWin {  // q[wb, we) is in win
+  const uint8_t* q;
+  gi_lds_u8* win;
+  uint32_t n, W, wb, we;
+};
+
+__device__ __forceinline__ void jw_refill(JWin& w, uint32_t i) {
+  __syncthreads();  // every lane is done reading the old window
+  w.wb = i & ~3u;
+  w.we = min(w.n, w.wb + w.W);
+  for (uint32_t k = w.wb + lane_id(); k < w.we; k += 64) w.win[k - w.wb] = w.q[k];
+  __syncthreads();
+}
+// byte i (i < n) of the body; the window moves forward (or back) to cover it
+__device__ __forceinline__ uint8_t jw_at(JWin& w, uint32_t i) {
+  if (i < w.wb || i >= w.we) jw_refill(w, i);
+  return w.win[i - w.wb];
+}
+// the window covers [i, min(i + k, n)) (k <= W - 4)
+__device__ __forceinline__ void jw_cover(JWin& w, uint32_t i, uint32_t k) {
+  if (i < w.wb || min(i + k, w.n) > w.we) jw_refill(w, i);
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+  for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, 64);
+  return x;
+}
+
+// a hash of path[0, kn): equal keys hash equal (any function of the bytes does)
+__device__ __forceinline__ uint32_t wave_key_hash(const gi_lds_u8* path, uint32_t kn) {
+  const uint32_t L = lane_id();
+  uint32_t acc = 0;
+  for (uint32_t base = 0; base < kn; base += 256) {
+    const uint32_t j = base + 4 * L;
+    uint32_t x = 0;
+    if (j < kn) {
+      uint32_t w = 0;
+      for (uint32_t b = 0; b < 4; b++)
+        if (j + b < kn) w |= (uint32_t)path[j + b] << (8 * b);
+      x = (w ^ (j * 0x9E3779B1u)) * 0x85EBCA6Bu;
+      x ^= x >> 13;
+      x *= 0xC2B2AE35u;
+      x ^= x >> 16;
+    }
+    acc += x;
+  }
+  return wave_sum(acc) ^ (kn * 0x27D4EB2Fu);
+}
+
+// json_string_end over the window: the string whose quote is at i
+__device__ uint32_t jw_string_end(JWin& w, uint32_t i, bool* esc) {
+  const uint32_t L = lane_id();
+  *esc = false;
+  uint32_t p = i + 1;
+  while (true) {
+    if (p >= w.n) return 0;
+    jw_cover(w, p, 64);
+    const uint32_t x = p + L;
+    const uint8_t c = x < w.we ? w.win[x - w.wb] : (uint8_t)'a';
+    const uint64_t m = __ballot(x < w.n && (c == '"' || c == '\\' || c < 0x20));
+    if (!m) {
+      p += 64;
+      continue;
+    }
+    p += (uint32_t)(__ffsll((unsigned long long)m) - 1);
+    const uint8_t c0 = w.win[p - w.wb];
+    if (c0 == '"') return p + 1;
+    if (c0 < 0x20) return 0;
+    if (p + 1 >= w.n) return 0;
+    const uint8_t e = jw_at(w, p + 1);
+    *esc = true;
+    if (e == 'u') {
+      if (p + 6 > w.n) return 0;
+      for (uint32_t k = 2; k < 6; k++)
+        if (!ishex(jw_at(w, p + k))) return 0;
+      p += 6;
+      continue;
+    }
+    if (e != '"' && e != '\\' && e != '/' && e != 'b' && e != 'f' && e != 'n' && e != 'r' && e != 't') return 0;
+    p += 2;
+  }
+}
+
+// json_unescape of the validated string body q[i, i + n) into d (global or
+// LDS); lane 0 stores when `one`
+template <class D>
+__device__ uint32_t jw_unescape(JWin& w, uint32_t i, uint32_t n, D* d, bool one) {
+  const bool st = !one || lane_id() == 0;
+  uint32_t o = 0, k = 0;
+  uint8_t u[4];
+  while (k < n) {
+    const uint8_t c = jw_at(w, i + k);
+    if (c != '\\') {
+      if (st) d[o] = c;
+      o++;
+      k++;
+      continue;
+    }
+    const uint8_t e = jw_at(w, i + k + 1);
+    if (e != 'u') {
+      if (st) d[o] = e == 'b' ? 8 : e == 'f' ? 12 : e == 'n' ? 10 : e == 'r' ? 13 : e == 't' ? 9 : e;
+      o++;
+      k += 2;
+      continue;
+    }
+    uint32_t r = 0;
+    for (uint32_t b = 0; b < 4; b++) r = (r << 4) | hexv(jw_at(w, i + k + 2 + b));
+    k += 6;
+    if (r >= 0xD800 && r < 0xE000) {  // utf16.IsSurrogate: consume a following \uXXXX
+      if (n - k >= 6 && jw_at(w, i + k) == '\\' && jw_at(w, i + k + 1) == 'u') {
+        uint32_t r2 = 0;
+        for (uint32_t b = 0; b < 4; b++) r2 = (r2 << 4) | hexv(jw_at(w, i + k + 2 + b));
+        k += 6;
+        r = (r < 0xDC00 && r2 >= 0xDC00 && r2 < 0xE000) ? 0x10000 + ((r - 0xD800) << 10) + (r2 - 0xDC00) : 0xFFFD;
+      } else {
+        r = 0xFFFD;
+      }
+    }
+    const uint32_t un = utf8_put(r, u);
+    if (st)
+      for (uint32_t b = 0; b < un; b++) d[o + b] = u[b];
+    o += un;
+  }
+  return o;
+}
+
+__device__ uint32_t jw_number_end(JWin& w, uint32_t i) {
+  const uint32_t n = w.n;
+  auto dg = [&](uint32_t k) { const uint8_t c = jw_at(w, k); return c >= '0' && c <= '9'; };
+  if (i < n && jw_at(w, i) == '-') i++;
+  if (i >= n || !dg(i)) return 0;
+  if (jw_at(w, i) == '0') {
+    i++;
+  } else {
+    while (i < n && dg(i)) i++;
+  }
+  if (i < n && jw_at(w, i) == '.') {
+    i++;
+    if (i >= n || !dg(i)) return 0;
+    while (i < n && dg(i)) i++;
+  }
+  if (i < n && (jw_at(w, i) == 'e' || jw_at(w, i) == 'E')) {
+    i++;
+    if (i < n && (jw_at(w, i) == '+' || jw_at(w, i) == '-')) i++;
+    if (i >= n || !dg(i)) return 0;
+    while (i < n && dg(i)) i++;
+  }
+  return i;
+}
+
+// Fields [nf0, *nf) and the arena [nb0, *nb) as parse_json_body(+ fold) makes
+// them; false: no fields (not parsed here).
+__device__ bool wave_parse_json(const Region& g, const uint8_t* q, uint32_t n, uint32_t nf0, uint32_t nb0,
+                                gi_lds_u8* win, uint32_t W, gi_lds_u8* path, JWFrame* st, uint32_t* nf_out,
+                                uint32_t* nb_out) {
+  const uint32_t L = lane_id();
+  const bool l0 = L == 0;
+  JWin w{q, win, n, W, 0, 0};
+  uint32_t nf = nf0, nb = nb0;
+  uint32_t i = 0;
+  while (i < n && json_ws(jw_at(w, i))) i++;
+  if (i >= n || (jw_at(w, i) != '{' && jw_at(w, i) != '[')) return false;
+  // the sequential parser's frame stack and root key allocations
+  const uint32_t stn = (GI_JSON_MAX_DEPTH + 1) * sizeof(JFrame) + 8;
+  if (nb + stn + 4 > g.cap_b) return false;
+  nb += stn;
+  const uint32_t root = nb;
+  nb += 4;
+  if (l0) {
+    g.bytes[root] = 'j'; g.bytes[root + 1] = 's'; g.bytes[root + 2] = 'o'; g.bytes[root + 3] = 'n';
+  }
+  if (L < 4) path[L] = "json"[L];
+  __syncthreads();
+  uint32_t d = 1;
+  if (l0) st[0] = {root, 4, 0, jw_at(w, i) == '[' ? 1u : 0u, wave_key_hash(path, 4)};
+  else (void)wave_key_hash(path, 4);
+  __syncthreads();
+  const uint64_t lim = 4ull * n + 1024;
+  uint64_t jb = 0;
+  i++;
+  auto add = [&](uint32_t koff, uint32_t kn, uint32_t h, const uint8_t* v, uint32_t vn) -> bool {
+    if (nf >= g.cap_f) return false;
+    if (l0) {
+      Field f;
+      f.k = g.bytes + koff;
+      f.v = v;
+      f.kn = kn;
+      f.vn = vn;
+      f.kind = FK_ARG_POST;
+      f._pad = h;
+      g.fields[nf] = f;
+    }
+    nf++;
+    return true;
+  };
+  while (d > 0) {
+    JWFrame F = st[d - 1];
+    while (i < n && json_ws(jw_at(w, i))) i++;
+    if (i >= n) return false;
+    if (jw_at(w, i) == (F.is_arr ? ']' : '}')) {
+      i++;
+      if (F.is_arr && F.count) {
+        if (nb + 12 > g.cap_b) return false;
+        const uint32_t dn = dec_len(F.count);
+        if (l0) dec_put(F.count, dn, g.bytes + nb);
+        const uint32_t vo = nb;
+        nb += dn;
+        jb += dn;
+        if (jb > lim) return false;
+        if (!add(F.koff, F.kn, F.h, g.bytes + vo, dn)) return false;
+      }
+      d--;
+      continue;
+    }
+    if (F.count) {
+      if (jw_at(w, i) != ',') return false;
+      i++;
+      while (i < n && json_ws(jw_at(w, i))) i++;
+    }
+    // the element's key: the container's (path[0, F.kn)) + '.' + name / index
+    uint32_t kn;
+    const uint32_t koff = nb;
+    if (F.is_arr) {
+      if (nb + F.kn + 12 > g.cap_b) return false;
+      const uint32_t dn = dec_len(F.count);
+      kn = F.kn + 1 + dn;
+      if (kn > GI_JW_PATH) return false;
+      if (l0) {
+        path[F.kn] = '.';
+        dec_put(F.count, dn, path + F.kn + 1);
+      }
+      jb += kn;
+      if (jb > lim) return false;
+    } else {
+      if (i >= n || jw_at(w, i) != '"') return false;
+      bool esc;
+      const uint32_t e = jw_string_end(w, i, &esc);
+      if (!e) return false;
+      const uint32_t rn = e - i - 2;
+      if (nb + F.kn + 1 + rn > g.cap_b) return false;
+      if (F.kn + 1 + rn > GI_JW_PATH) return false;
+      if (L == 0) path[F.kn] = '.';
+      uint32_t sn = rn;
+      if (esc) {
+        sn = jw_unescape(w, i + 1, rn, path + F.kn + 1, false);
+      } else {
+        jw_cover(w, i + 1, rn);
+        for (uint32_t k = L; k < rn; k += 64) path[F.kn + 1 + k] = w.win[i + 1 + k - w.wb];
+      }
+      kn = F.kn + 1 + sn;
+      jb += kn;
+      if (jb > lim) return false;
+      i = e;
+      while (i < n && json_ws(jw_at(w, i))) i++;
+      if (i >= n || jw_at(w, i) != ':') return false;
+      i++;
+      while (i < n && json_ws(jw_at(w, i))) i++;
+    }
+    __syncthreads();  // path written
+    for (uint32_t k = L; k < kn; k += 64) g.bytes[koff + k] = path[k];
+    const uint32_t kh = wave_key_hash(path, kn);
+    nb += kn;
+    F.count++;
+    if (l0) st[d - 1].count = F.count;
+    if (i >= n) return false;
+    const uint8_t c = jw_at(w, i);
+    if (c == '{' || c == '[') {
+      if (d >= GI_JSON_MAX_DEPTH) return false;
+      if (l0) st[d] = {koff, kn, 0, c == '[' ? 1u : 0u, kh};
+      d++;
+      i++;
+    } else if (c == '"') {
+      bool esc;
+      const uint32_t e = jw_string_end(w, i, &esc);
+      if (!e) return false;
+      const uint32_t rn = e - i - 2;
+      if (esc) {
+        if (nb + rn > g.cap_b) return false;
+        const uint32_t vo = nb;
+        const uint32_t vn = jw_unescape(w, i + 1, rn, g.bytes + vo, true);
+        nb += vn;
+        jb += vn;
+        if (jb > lim) return false;
+        if (!add(koff, kn, kh, g.bytes + vo, vn)) return false;
+      } else {
+        if (!add(koff, kn, kh, q + i + 1, rn)) return false;
+      }
+      i = e;
+    } else if (c == 't' || c == 'f' || c == 'n') {
+      const uint32_t ln = c == 'f' ? 5 : 4;
+      const char* lit = c == 't' ? "true" : c == 'f' ? "false" : "null";
+      if (i + ln > n) return false;
+      for (uint32_t k = 0; k < ln; k++)
+        if (jw_at(w, i + k) != (uint8_t)lit[k]) return false;
+      if (!add(koff, kn, kh, q + i, c == 'n' ? 0 : ln)) return false;
+      i += ln;
+    } else {
+      const uint32_t e = jw_number_end(w, i);
+      if (!e) return false;
+      if (!add(koff, kn, kh, q + i, e - i)) return false;
+      i = e;
+    }
+    __syncthreads();  // st written
+  }
+  while (i < n && json_ws(jw_at(w, i))) i++;
+  if (i != n) return false;
+  // repeated keys (json_fold_keys: first position, last value)
+  const uint32_t nk = nf - nf0;
+  if (nk >= 2) {
+    const uint32_t cap = g.cap_t / 4;
+    if (nk >= cap) return false;
+    uint32_t tsize = 16;
+    while (tsize < 2 * nk && 2 * tsize <= cap) tsize *= 2;
+    if (tsize > cap || tsize <= nk) tsize = cap;
+    uint32_t* tab = (uint32_t*)g.t1;
+    for (uint32_t k = L; k < tsize; k += 64) tab[k] = 0;
+    __syncthreads();  // the table and the fields lane 0 wrote
+    bool dup = false;
+    for (uint32_t b = nf0; b < nf; b += 64) {
+      const uint32_t fi = b + L;
+      if (fi < nf) {
+        const Field f = g.fields[fi];
+        uint32_t s = f._pad % tsize;
+        while (true) {
+          const uint32_t old = atomicCAS(&tab[s], 0u, fi + 1);
+          if (old == 0) break;
+          const Field o = g.fields[old - 1];
+          if (o._pad == f._pad && o.kn == f.kn && bytes_equal(o.k, f.k, f.kn)) {
+            dup = true;
+            break;
+          }
+          s = s + 1 == tsize ? 0 : s + 1;
+        }
+      }
+    }
+    if (__ballot(dup)) {
+      __syncthreads();
+      uint32_t res[2] = {0, 0};
+      if (l0) {
+        JsonCtx jc{g.fields, nf, g.cap_f, g.bytes, nb, g.cap_b, g.t1, g.cap_t, 0};
+        json_fold_keys(jc, nf0);
+        res[0] = jc.nf;
+        res[1] = jc.flags;
+      }
+      nf = __shfl(res[0], 0, 64);
+      if (__shfl(res[1], 0, 64)) return false;
+    }
+  }
+  for (uint32_t k = nf0 + L; k < nf; k += 64) g.fields[k]._pad = 0;
+  *nf_out = nf;
+  *nb_out = nb;
+  return true;
+}
+
 __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
   // JSON bodies up to B.bparse_lds bytes are parsed out of an LDS copy (the
   // sequential parser then waits on LDS, not on global memory, per byte)
   extern __shared__ __attribute__((aligned(16))) uint8_t jlds[];
   __shared__ uint32_t chist[GI_NCLS];  // item counts per class of this body's fields
+  __shared__ __attribute__((aligned(16))) uint8_t jpath[GI_JW_PATH];  // wave_parse_json's key path
+  __shared__ JWFrame jst[GI_JSON_MAX_DEPTH + 1];                       // and frame stack
   const uint32_t L = threadIdx.x;
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
     const uint32_t r = B.body_list[bi];
@@ -5441,6 +5833,13 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
         }
         nb = nb0 + wave_max(used);
       }
+    } else if (sp == BP_JSON && B.bparse_lds >= 2048 && B.bparse_wave) {
+      // the body through an LDS window of B.bparse_lds bytes, the whole wave parsing
+      uint32_t nfo = nf0;
+      ok = wave_parse_json(g, q, n, nf0, nb0, (gi_lds_u8*)jlds, B.bparse_lds, (gi_lds_u8*)jpath,
+                           jst, &nfo, &nb);
+      n_post = nfo - nf0;
+      __syncthreads();  // the next body reuses the window
     } else {  // JSON (or an urlencoded body the arena bound does not cover): lane 0, sequential
       uint32_t res[3] = {0, 0, 0};
       if (L == 0) {

@@ -126,6 +126,8 @@ struct gi_ctx {
   uint32_t lay_host_cap = 0;
   bool stage_prof = false;
   uint32_t bparse_lds = GI_BPARSE_LDS;  // GI_BPARSE_LDS env
+  uint32_t bparse_wave = 1;              // GI_BPARSE_WAVE env (0: JSON bodies on lane 0, A/B)
+  uint32_t bparse_win = GI_BPARSE_WIN;   // GI_BPARSE_WIN env: wave_parse_json's LDS window
   uint64_t max_body = 0;                // longest body of the staged batch        // GI_STAGE_PROF=1: gi_stage_batch phase times on stderr  // queue-pool estimate a chunk may reach (GI_CHUNK_POOL_WORDS env)
   uint64_t long_bufcap = 0;
   uint32_t lcap = 0, qcap = 0, slow_cap = 0, det_cap = 0;
@@ -593,6 +595,8 @@ int gi_ctx_create(const gi_ruleset* rs, int device, uint32_t matched_cap, gi_ctx
   if (getenv("GI_EVAL_WAVE_FIELDS")) c->wave_fields = (uint32_t)atoi(getenv("GI_EVAL_WAVE_FIELDS"));  // A/B, 0: off
   if (getenv("GI_EVAL_WAVE_RULES")) c->wave_rules = (uint32_t)atoi(getenv("GI_EVAL_WAVE_RULES"));
   c->stage_prof = getenv("GI_STAGE_PROF") && atoi(getenv("GI_STAGE_PROF")) > 0;
+  if (getenv("GI_BPARSE_WAVE")) c->bparse_wave = (uint32_t)atoi(getenv("GI_BPARSE_WAVE"));
+  if (getenv("GI_BPARSE_WIN")) c->bparse_win = (uint32_t)std::min(65536, std::max(2048, atoi(getenv("GI_BPARSE_WIN")))) & ~15u;
   if (getenv("GI_BPARSE_LDS")) c->bparse_lds = (uint32_t)std::min(65536, std::max(0, atoi(getenv("GI_BPARSE_LDS"))));
   if (getenv("GI_CHUNK_POOL_WORDS")) c->chunk_pool_words = std::max(1e6, atof(getenv("GI_CHUNK_POOL_WORDS")));
   if (getenv("GI_CHUNK_CAP_BYTES")) c->chunk_cap_bytes = std::max<uint64_t>(1ull << 16, strtoull(getenv("GI_CHUNK_CAP_BYTES"), nullptr, 10));
@@ -1278,7 +1282,9 @@ int gi_run_staged(gi_ctx* c) {
     B.body_tiles = tiles_env;
     static const uint32_t ws2_env = getenv("GI_EVAL_WAVE_STAGE2") ? (uint32_t)atoi(getenv("GI_EVAL_WAVE_STAGE2")) : 1u;
     B.wave_stage2 = ws2_env;
-    B.bparse_lds = (uint32_t)std::min<uint64_t>(c->bparse_lds, (c->max_body + 15) & ~15ull);
+    B.bparse_wave = c->bparse_wave;
+    B.bparse_lds = c->bparse_wave ? c->bparse_win
+                                  : (uint32_t)std::min<uint64_t>(c->bparse_lds, (c->max_body + 15) & ~15ull);
   }
   (void)hipEventRecord(c->ev0, c->stream);
   if (c->ctr.p) {

@@ -144,7 +144,12 @@ def test_gpu_json_edge_bodies():
                b'{"s": "\\u003cimg src=x onerror=alert(1)\\u003e"}',
                b'{"a": "' + b"A" * 5000 + b'", "b": [' + b",".join(b"%d" % i for i in range(2000)) + b"]}",
                b'[' + b",".join(b'{"k":"v%d","k":"w%d"}' % (i, i) for i in range(300)) + b"]",
-               b"\n\t {\"ws\" : [ 1 , 2 ] } \r\n"]
+               b"\n\t {\"ws\" : [ 1 , 2 ] } \r\n",
+               # wave_parse_json: a key past its 1 KB path buffer (k_eval parses the body), keys and
+               # escaped strings across its 4 KB LDS windows, a repeated key 200 fields apart
+               b'{"' + b"k" * 1500 + b'": 1, "x": "<script>alert(1)</script>"}',
+               b'{' + b",".join(b'"f\\u00e9%d": "v\\n%s"' % (i, b"x" * (i % 97)) for i in range(400)) + b'}',
+               b'{"d": 1, ' + b",".join(b'"e%d": [%d, "s"]' % (i, i) for i in range(200)) + b', "d": "<script>"}']
     txs = [_json_tx(b) for b in bodies]
     txs += [_json_tx(b, ctype=b"application/vnd.api+json") for b in bodies[:4]]
     res, orc = _parity(text, gpuinspect.pack(txs))
