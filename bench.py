@@ -275,7 +275,12 @@ def main():
     if args.config == "c5":
         batch = traffic.c5_batch(n_req, seed=shard.shard_seed(traffic.SEED, rank))
     else:
-        batch = traffic.TrafficGen(shard.shard_seed(traffic.SEED, rank)).batch(n_req, post_frac=post_frac)
+        # GI_BENCH_JSON_FRAC: a diagnostic A/B of the body mix (the configs' lines use the default 0.4)
+        jf = float(os.environ.get("GI_BENCH_JSON_FRAC", "0.4"))
+        batch = traffic.TrafficGen(shard.shard_seed(traffic.SEED, rank)).batch(n_req, post_frac=post_frac,
+                                                                                json_frac=jf)
+        if jf != 0.4:
+            log("DIAGNOSTIC body mix: json_frac %.2f (not the config's)" % jf)
     split = None
     if dist is not None and not args.no_balance:
         log("rebalancing the request set by bytes across %d ranks" % world)
@@ -376,7 +381,9 @@ def main():
         "data": "synthetic (seeded generator coraza-kubernetes-operator_amd/traffic.py, seed 0xC0A2A+rank)",
         "config": {"workload": desc, "config": args.config, "requests_per_gpu": batch.n_req,
                    "bytes_per_request": round(raw / batch.n_req, 1), "parallelism": "dp%d" % world,
-                   "rules": rs.info["n_rules"], "dfas": rs.info["n_dfas"]},
+                   "rules": rs.info["n_rules"], "dfas": rs.info["n_dfas"],
+                   **({"diagnostic_json_frac": float(os.environ["GI_BENCH_JSON_FRAC"])}
+                      if os.environ.get("GI_BENCH_JSON_FRAC", "0.4") not in ("0.4", "") else {})},
         "gb_per_s_scanned": round(gbs, 3),
         "interrupted_frac": round(tally["n_interrupted"] / max(tally["n_req"], 1), 4),
         "pa_void_requests": int(tally["n_pa_void"]),

@@ -5768,6 +5768,225 @@ __device__ bool wave_parse_json(const Region& g, const uint8_t* q, uint32_t n, u
   return true;
 }
 
+// ------------------------------------------------ wave urlencoded parse
+// parse_query(body, ARGS_POST) for one wave, 4 KB of the body per step: lane
+// L classifies bytes [64 L, 64 L + 64) of the step ('&', '=', '%' / '+' bit
+// masks from aligned word loads), a segmented scan over the lanes carries the
+// open segment (start, first '=', escapes before / after it) across lanes and
+// steps, and each lane emits the fields of the segments its '&'s end, in body
+// order (a wave prefix sum of the counts).  Keys / values with escapes decode
+// into the arena at the segment's own body offset (a decoding is never longer
+// than its input, so segments cannot collide), as before.
+struct UrlSeg {
+  uint32_t amp;  // start of the open segment (one past its '&')
+  uint32_t eq;   // its first '=' (fl & 2)
+  uint32_t fl;   // 1: the range holds an '&'; 2: the open segment has an '='; 4: '%' / '+' before its
+                 // first '=' (anywhere, without one); 8: after it
+};
+__device__ __forceinline__ UrlSeg useg_cat(const UrlSeg& A, const UrlSeg& B) {
+  if (B.fl & 1u) return B;
+  UrlSeg R;
+  R.amp = A.amp;
+  R.fl = A.fl & 1u;
+  if (A.fl & 2u) {
+    R.eq = A.eq;
+    R.fl |= 2u | (A.fl & 12u) | ((B.fl & 12u) ? 8u : 0u);
+  } else if (B.fl & 2u) {
+    R.eq = B.eq;
+    R.fl |= 2u | (A.fl & 4u) | (B.fl & 12u);
+  } else {
+    R.eq = 0;
+    R.fl |= (A.fl & 4u) | (B.fl & 4u);
+  }
+  return R;
+}
+// the summary of bits `rm` of a slice at body offset sb (no '&' among them)
+__device__ __forceinline__ UrlSeg useg_range(uint64_t eqm, uint64_t escm, uint64_t rm, uint32_t sb) {
+  UrlSeg S{0u, 0u, 0u};
+  const uint64_t e = eqm & rm;
+  if (e) {
+    const uint32_t f = (uint32_t)__builtin_ctzll(e);
+    S.eq = sb + f;
+    const uint64_t below = (1ull << f) - 1ull;
+    S.fl = 2u | ((escm & rm & below) ? 4u : 0u) | ((escm & rm & ~below & ~(1ull << f)) ? 8u : 0u);
+  } else {
+    S.fl = (escm & rm) ? 4u : 0u;
+  }
+  return S;
+}
+// zero bytes of x as a 4-bit mask
+__device__ __forceinline__ uint32_t zbytes4(uint32_t x) {
+  const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+  const uint32_t z = ~nz & 0x80808080u;
+  return ((z >> 7) | (z >> 14) | (z >> 21) | (z >> 28)) & 0xFu;
+}
+
+// Fields [nf0, *nf) for the urlencoded body q[0, n) (g.cap_b >= nb0 + n);
+// false: more fields than the table holds
+__device__ bool wave_parse_urlenc(const Region& g, const uint8_t* q, uint32_t n, uint32_t nf0, uint32_t nb0,
+                                  uint32_t* nf_out, uint32_t* nb_out) {
+  const uint32_t L = lane_id();
+  UrlSeg C{0u, 0u, 1u};  // as if an '&' ended just before the body
+  uint32_t nf = nf0, used = 0;
+  const uint32_t s = (uint32_t)((uintptr_t)q & 3u);
+  for (uint32_t wb = 0; wb < n; wb += 4096) {
+    const uint32_t sb = wb + 64 * L;
+    uint64_t amp = 0, eqm = 0, escm = 0;
+    if (sb < n) {
+      auto classify = [&](uint32_t x, uint32_t k) {
+        amp |= (uint64_t)zbytes4(x ^ 0x26262626u) << (4 * k);
+        eqm |= (uint64_t)zbytes4(x ^ 0x3D3D3D3Du) << (4 * k);
+        escm |= (uint64_t)(zbytes4(x ^ 0x25252525u) | zbytes4(x ^ 0x2B2B2B2Bu)) << (4 * k);
+      };
+      if (sb + 68 <= n) {  // 17 aligned words hold the slice
+        const uint32_t* pw = (const uint32_t*)(q + sb - s);
+        uint32_t prev = pw[0];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+          const uint32_t nxt = pw[k + 1];
+          classify(s ? __builtin_amdgcn_alignbyte(nxt, prev, s) : prev, k);
+          prev = nxt;
+        }
+      } else {
+        for (uint32_t k = 0; k < 16; k++) {
+          uint32_t x = 0;
+          for (uint32_t b = 0; b < 4; b++)
+            if (sb + 4 * k + b < n) x |= (uint32_t)q[sb + 4 * k + b] << (8 * b);
+          classify(x, k);
+        }
+      }
+      if (n - sb < 64) {  // (bytes past the body read as 0: no flags, but mask them anyway)
+        const uint64_t vm = (1ull << (n - sb)) - 1ull;
+        amp &= vm;
+        eqm &= vm;
+        escm &= vm;
+      }
+    }
+    // this lane's summary: its tail after the last '&' (or the whole slice)
+    UrlSeg S;
+    if (amp) {
+      const uint32_t last = 63u - (uint32_t)__builtin_clzll(amp);
+      const uint64_t tm = last == 63 ? 0ull : ~0ull << (last + 1);
+      S = useg_range(eqm, escm, tm, sb);
+      S.fl |= 1u;
+      S.amp = sb + last + 1;
+    } else {
+      S = useg_range(eqm, escm, ~0ull, sb);
+      S.amp = 0;
+    }
+    // inclusive segmented scan over the lanes, then the open segment at this slice's start
+    UrlSeg I = S;
+    for (int o = 1; o < 64; o <<= 1) {
+      UrlSeg Y;
+      Y.amp = __shfl_up(I.amp, o, 64);
+      Y.eq = __shfl_up(I.eq, o, 64);
+      Y.fl = __shfl_up(I.fl, o, 64);
+      if (L >= (uint32_t)o) I = useg_cat(Y, I);
+    }
+    UrlSeg X;
+    X.amp = __shfl_up(I.amp, 1, 64);
+    X.eq = __shfl_up(I.eq, 1, 64);
+    X.fl = __shfl_up(I.fl, 1, 64);
+    X = L == 0 ? C : useg_cat(C, X);
+    UrlSeg T;
+    T.amp = __shfl(I.amp, 63, 64);
+    T.eq = __shfl(I.eq, 63, 64);
+    T.fl = __shfl(I.fl, 63, 64);
+    const UrlSeg Cn = useg_cat(C, T);
+    // the non-empty segments this lane's '&'s end
+    uint32_t cnt = 0;
+    {
+      uint32_t start = X.amp;
+      for (uint64_t m = amp; m; m &= m - 1) {
+        const uint32_t e = sb + (uint32_t)__builtin_ctzll(m);
+        cnt += e > start ? 1u : 0u;
+        start = e + 1;
+      }
+    }
+    uint32_t tot;
+    const uint32_t idx0 = nf + wave_excl_sum(cnt, &tot);
+    if ((uint64_t)nf + tot + 1 > g.cap_f) return false;  // (+1: the body's last segment)
+    uint32_t idx = idx0;
+    UrlSeg O = X;
+    uint32_t cur = 0;  // bit where the open segment's bytes in this slice begin
+    for (uint64_t m = amp; m; m &= m - 1) {
+      const uint32_t b = (uint32_t)__builtin_ctzll(m);
+      const uint32_t e = sb + b;
+      const uint64_t rm = (b > cur ? (~0ull >> (64 - (b - cur))) << cur : 0ull);
+      const UrlSeg G = useg_cat(O, useg_range(eqm, escm, rm, sb));
+      const uint32_t st = O.amp;
+      if (e > st) {
+        const bool he = G.fl & 2u;
+        const uint8_t* k = q + st;
+        uint32_t kn = (he ? G.eq : e) - st;
+        const uint8_t* v = q + (he ? G.eq + 1 : e);
+        uint32_t vn = he ? e - G.eq - 1 : 0;
+        if (G.fl & 4u) {
+          uint8_t* d = g.bytes + nb0 + st;
+          kn = query_unescape(k, kn, d);
+          k = d;
+          used = max(used, st + kn);
+        }
+        if (G.fl & 8u) {
+          const uint32_t vo = (uint32_t)(v - q);
+          uint8_t* d = g.bytes + nb0 + vo;
+          vn = query_unescape(v, vn, d);
+          v = d;
+          used = max(used, vo + vn);
+        }
+        Field f;
+        f.k = k;
+        f.v = v;
+        f.kn = kn;
+        f.vn = vn;
+        f.kind = FK_ARG_POST;
+        f._pad = 0;
+        g.fields[idx++] = f;
+      }
+      O = UrlSeg{e + 1, 0u, 1u};
+      cur = b + 1;
+    }
+    nf += tot;
+    C = Cn;
+  }
+  // the body's last segment (no '&' after it)
+  if (n > C.amp) {
+    if (L == 0) {
+      const uint32_t st = C.amp, e = n;
+      const bool he = C.fl & 2u;
+      const uint8_t* k = q + st;
+      uint32_t kn = (he ? C.eq : e) - st;
+      const uint8_t* v = q + (he ? C.eq + 1 : e);
+      uint32_t vn = he ? e - C.eq - 1 : 0;
+      if (C.fl & 4u) {
+        uint8_t* d = g.bytes + nb0 + st;
+        kn = query_unescape(k, kn, d);
+        k = d;
+        used = max(used, st + kn);
+      }
+      if (C.fl & 8u) {
+        const uint32_t vo = (uint32_t)(v - q);
+        uint8_t* d = g.bytes + nb0 + vo;
+        vn = query_unescape(v, vn, d);
+        v = d;
+        used = max(used, vo + vn);
+      }
+      Field f;
+      f.k = k;
+      f.v = v;
+      f.kn = kn;
+      f.vn = vn;
+      f.kind = FK_ARG_POST;
+      f._pad = 0;
+      g.fields[nf] = f;
+    }
+    nf++;
+  }
+  *nf_out = nf;
+  *nb_out = nb0 + wave_max(used);
+  return true;
+}
+
 __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
   // JSON bodies up to B.bparse_lds bytes are parsed out of an LDS copy (the
   // sequential parser then waits on LDS, not on global memory, per byte)
@@ -5790,7 +6009,11 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
     const uint32_t nf0 = H->nf, nb0 = H->nb;
     uint32_t n_post = 0, nb = nb0;
     bool ok = true;
-    if (sp == BP_URLENCODED && (uint64_t)nb0 + n <= g.cap_b) {
+    if (sp == BP_URLENCODED && (uint64_t)nb0 + n <= g.cap_b && B.bparse_wave) {
+      uint32_t nfo = nf0;
+      ok = wave_parse_urlenc(g, q, n, nf0, nb0, &nfo, &nb);
+      n_post = nfo - nf0;
+    } else if (sp == BP_URLENCODED && (uint64_t)nb0 + n <= g.cap_b) {
       const uint32_t a0 = (uint32_t)((uint64_t)n * L / 64), a1 = (uint32_t)((uint64_t)n * (L + 1) / 64);
       uint32_t c = 0;
       for (uint32_t p = a0; p < a1; p++) c += (q[p] != '&' && (p == 0 || q[p - 1] == '&')) ? 1u : 0u;
