@@ -29,7 +29,14 @@
 // k_stream / k_long, which share the gi:: copy.
 namespace gi {
 namespace lid {
+// the keyword tables in k_detect's LDS (loaded at its start): every word
+// lookup is a hash probe + compare there, and the lane state needs no pointers
+__shared__ uint32_t li_lw[LI_NWORDS];
+__shared__ uint16_t li_lh[LI_HASH_SIZE];
+__shared__ __attribute__((aligned(16))) uint8_t li_lp[sizeof(kLiPool)];
+#define LI_LDS_TABLES (LiTables{li_lw, li_lp, li_lh})
 #include "libinj_body.h"
+#undef LI_LDS_TABLES
 }  // namespace lid
 }  // namespace gi
 
@@ -8033,31 +8040,39 @@ __device__ uint32_t det_results(const DBatch& B, const uint8_t* v, uint32_t n, u
   return out;
 }
 
-__global__ void __launch_bounds__(256) k_detect(DProgram P, DBatch B) {
+#ifndef GI_DETECT_LVAL
+#define GI_DETECT_LVAL 0  // 1: short candidates staged in LDS (66 KB per workgroup: 2 workgroups per CU)
+#endif
+#ifndef GI_DETECT_WPE
+#define GI_DETECT_WPE 3   // minimum waves per SIMD k_detect is compiled for.  Round 6, C2 A/B on one box: LVAL 0 +
+                          // 3 waves (166 VGPRs, 48.3 KB LDS: 3 workgroups per CU) 10.9 ms, LVAL 1 + 1 wave (248
+                          // VGPRs, 2 workgroups per CU) 12.9 ms; C3 198 vs 210 ms (make ab-det1 builds the latter)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GI_DETECT_WPE))) k_detect(DProgram P,
+                                                                                                   DBatch B) {
   __shared__ lid::LiSqli st[256];
-  // the keyword tables in LDS: every word lookup is a hash probe + compare
-  __shared__ uint32_t lw[LI_NWORDS];
-  __shared__ uint16_t lh[LI_HASH_SIZE];
-  __shared__ __attribute__((aligned(16))) uint8_t lp[sizeof(kLiPool)];
+#if GI_DETECT_LVAL
   // short candidates (<= 64 B, most of them) are read from LDS: stride 68 B =
   // 17 dwords per lane, conflict-free
   __shared__ __attribute__((aligned(16))) uint32_t lval[256 * 17];
-  for (uint32_t i = threadIdx.x; i < LI_NWORDS; i += blockDim.x) lw[i] = kLiWords[i];
-  for (uint32_t i = threadIdx.x; i < LI_HASH_SIZE; i += blockDim.x) lh[i] = kLiHash[i];
-  for (uint32_t i = threadIdx.x; i < sizeof(kLiPool); i += blockDim.x) lp[i] = kLiPool[i];
+#endif
+  for (uint32_t i = threadIdx.x; i < LI_NWORDS; i += blockDim.x) lid::li_lw[i] = kLiWords[i];
+  for (uint32_t i = threadIdx.x; i < LI_HASH_SIZE; i += blockDim.x) lid::li_lh[i] = kLiHash[i];
+  for (uint32_t i = threadIdx.x; i < sizeof(kLiPool); i += blockDim.x) lid::li_lp[i] = kLiPool[i];
   __syncthreads();
-  lid::LiTables T;  // (member-wise: an aggregate of LDS addresses would become a static initializer)
-  T.words = lw;
-  T.pool = lp;
-  T.hash = lh;
+  const lid::LiTables T{nullptr, nullptr, nullptr};  // (the copy reads lid::li_* itself)
   const uint32_t n = min(*B.det_count, B.det_cap);
   uint64_t dsteps = 0;  // value bytes through libinjection (secondary roofline)
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const DetEnt x = ((const DetEnt*)B.det)[e];
     GI_BOUND(x.req < B.n_req && x.off + x.len <= B.det_bytes_cap, x.req, x.off);
     const uint8_t* v = B.det_bytes + x.off;
-    if (x.len <= 64) {  // the arena offset is 16-byte aligned: four 16-byte loads
+    if (GI_DETECT_LVAL && x.len <= 64) {  // the arena offset is 16-byte aligned: four 16-byte loads
+#if GI_DETECT_LVAL
       uint32_t* dst = lval + threadIdx.x * 17;
+#else
+      uint32_t* dst = nullptr;
+#endif
       const uint4* src = (const uint4*)v;
       for (uint32_t k = 0; k < (x.len + 15) / 16; k++) {
         const uint4 w = src[k];

@@ -29,14 +29,26 @@ struct LiTables {
   const uint16_t* hash;   // kLiHash
 };
 
+// LI_LDS_TABLES (k_detect's copy): an expression for the keyword tables in
+// LDS; the state then carries no table pointers (168 B instead of 200 B)
 struct LiSqli {
   const uint8_t* s;
   uint32_t slen, flags, pos, cur;
   uint32_t ddx, hash, ntok;
+#ifndef LI_LDS_TABLES
   LiTables T;
+#endif
   LiTok tv[8];
+#ifndef LI_LDS_TABLES
   uint32_t _pad[2];  // 200 B = 50 dwords: k_detect's per-lane LDS states hit ~2-way, not 16-way, bank conflicts
+#endif
 };
+#undef LI_T
+#ifdef LI_LDS_TABLES
+#define LI_T(S) LI_LDS_TABLES
+#else
+#define LI_T(S) ((S).T)
+#endif
 
 GI_HD __forceinline__ LiTables li_tables_const() { return LiTables{kLiWords, kLiPool, kLiHash}; }
 
@@ -223,7 +235,7 @@ GI_HD __forceinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos) 
   for (uint32_t i = 0; i < c.len; i++) {
     const uint8_t d = c.p[i];
     if (d == '.' || d == '`') {
-      const uint8_t ch = li_lookup(S.T, c.p, i);
+      const uint8_t ch = li_lookup(LI_T(S), c.p, i);
       if (ch != 0 && ch != 'n') {
         li_clear(c);
         li_assign(c, ch, s + pos, i);
@@ -232,7 +244,7 @@ GI_HD __forceinline__ uint32_t li_parse_word(LiSqli& S, LiTok& c, uint32_t pos) 
     }
   }
   if (wlen < LI_TOKEN_SIZE) {
-    const uint8_t ch = li_lookup(S.T, c.p, wlen);
+    const uint8_t ch = li_lookup(LI_T(S), c.p, wlen);
     c.type = ch ? ch : 'n';
   }
   return pos + wlen;
@@ -275,7 +287,7 @@ GI_HD uint32_t li_parse_estring(LiSqli& S, LiTok& c, uint32_t pos) {
 
 GI_HD uint32_t li_parse_tick(LiSqli& S, LiTok& c, uint32_t pos) {
   const uint32_t np = li_string_core(S.s, S.slen, pos, c, '`', 1);
-  const uint8_t ch = li_lookup(S.T, c.p, c.len);
+  const uint8_t ch = li_lookup(LI_T(S), c.p, c.len);
   c.type = ch == 'f' ? 'f' : 'n';
   return np;
 }
@@ -441,7 +453,7 @@ GI_HD __forceinline__ uint32_t li_parse(LiSqli& S, LiTok& c) {
         li_assign(c, 'o', s + pos, 3);
         return pos + 3;
       }
-      const uint8_t t = li_lookup(S.T, s + pos, 2);
+      const uint8_t t = li_lookup(LI_T(S), s + pos, 2);
       if (t) {
         li_assign(c, t, s + pos, 2);
         return pos + 2;
@@ -627,7 +639,7 @@ GI_HD __noinline__ uint32_t li_fold(LiSqli& S) {
     if (a.type == ';' && b.type == ';') { pos--; continue; }
     if ((a.type == 'o' || a.type == '&') && (li_unary(b) || b.type == 't')) { pos--; left = 0; continue; }
     if (a.type == '(' && li_unary(b)) { pos--; if (left > 0) left--; continue; }
-    if (li_merge(S.T, a, b)) { pos--; if (left > 0) left--; continue; }
+    if (li_merge(LI_T(S), a, b)) { pos--; if (left > 0) left--; continue; }
     if (a.type == ';' && b.type == 'f' && b.len >= 2 && (b.p[0] == 'I' || b.p[0] == 'i') && (b.p[1] == 'F' || b.p[1] == 'f')) {
       b.type = 'T';
       continue;
@@ -845,7 +857,11 @@ GI_HD __noinline__ bool li_sqli_ctx(LiSqli& S, uint32_t flags) {
 GI_HD __noinline__ bool li_detect_sqli(const uint8_t* s, uint32_t n, LiSqli* st, const LiTables& T) {
   if (n == 0) return false;
   LiSqli& S = *st;
+#ifndef LI_LDS_TABLES
   S.T = T;
+#else
+  (void)T;
+#endif
   S.s = s;
   S.slen = n;
   if (li_sqli_ctx(S, LI_FLAG_QUOTE_NONE | LI_FLAG_SQL_ANSI)) return true;
