@@ -2197,6 +2197,7 @@ GI_HD __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, c
                                                 uint64_t* combined, bool* combined_set,
                                                 const uint32_t* cand = nullptr, uint32_t ncand = 0) {
   uint32_t ci = 0;  // next candidate
+  const uint32_t f_begin = t.nf;  // (FILES_SIZES entries exist only from here on)
   *combined = 0;
   *combined_set = false;
   uint32_t ts, te;
@@ -2424,7 +2425,7 @@ GI_HD __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, c
       const uint32_t szn = go_itoa((int64_t)dn, sz);
       t.nb -= 24 - szn;
       bool set = false;
-      for (uint32_t f = 0; f < t.nf && !set; f++) {  // FILES_SIZES.SetIndex(file name, 0, size)
+      for (uint32_t f = f_begin; f < t.nf && !set; f++) {  // FILES_SIZES.SetIndex(file name, 0, size)
         Field& F = t.fields[f];
         if (F.kind == FK_FILE_SIZE && F.kn == fname.n && eq_ascii_ci_both(F.k, fname.p, fname.n)) {
           F.v = sz;
