@@ -105,6 +105,7 @@ struct DBatch {
   uint32_t* wcount;
   uint32_t wave_fields;       // k_eval_wave: requests with this many fields (0: none)
   uint32_t wave_rules;        // k_eval_wave: every request when the program walks this many rules (0: never)
+  uint32_t mp_wave;            // k_mpparse: parts split over the lanes (wave_multipart; GI_MP_WAVE=0: lane 0 alone)
   uint32_t bparse_wave;        // k_bparse: JSON bodies parsed by the whole wave (wave_parse_json; GI_BPARSE_WAVE=0: lane 0)
   uint32_t bparse_lds;        // k_bparse: JSON bodies up to this many bytes are parsed from LDS (its dynamic LDS)
   uint32_t rstride;           // request stride of the request-major SoA arrays (hits, txslots): the staged

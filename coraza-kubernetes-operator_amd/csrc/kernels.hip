@@ -2192,10 +2192,16 @@ GI_HD inline bool mp_after_ok(const uint8_t* s, uint32_t n, uint32_t k) {
 // cand (optional, k_mpparse): every position k of a '\n' followed by
 // "--" + boundary, ascending -- the delimiter search of a part's data then
 // walks this list instead of every byte of the part.
+// Segments (k_mpparse's part-parallel parse, wave_multipart): i0 = where
+// the parse starts (a delimiter line; 0 = the body), stop = a delimiter line
+// at or after this position ends it with MP_SEG before that part (seg[0] =
+// parts parsed, seg[1] = where that line starts).
+#define MP_SEG 0xFE
 template <class C>
 GI_HD __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, const uint8_t* ct, uint32_t ctn,
                                                 uint64_t* combined, bool* combined_set,
-                                                const uint32_t* cand = nullptr, uint32_t ncand = 0) {
+                                                const uint32_t* cand = nullptr, uint32_t ncand = 0,
+                                                uint32_t i0 = 0, uint32_t stop = 0xFFFFFFFFu, uint32_t* seg = nullptr) {
   uint32_t ci = 0;  // next candidate
   const uint32_t f_begin = t.nf;  // (FILES_SIZES entries exist only from here on)
   *combined = 0;
@@ -2213,8 +2219,9 @@ GI_HD __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, c
   const uint8_t* bd = bstr.p;
   const uint32_t bn = bstr.n;
   bool lf = false;
-  uint32_t parts = 0, i = 0;
+  uint32_t parts = 0, i = i0;
   uint64_t total = 0;
+  if (seg) seg[0] = 0;
   for (;;) {
     // Reader.nextPart: lines until a delimiter line
     bool expect_new = false;
@@ -2234,7 +2241,13 @@ GI_HD __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, c
         uint32_t r = ls + 2 + bn;
         while (r < le && mp_lws(s[r])) r++;
         if (parts == 0 && le - r == 1) lf = true;  // first delimiter line ends in a bare LF: LF mode
-        if (lf ? (le - r == 1) : (le - r == 2 && s[r] == '\r')) break;
+        if (lf ? (le - r == 1) : (le - r == 2 && s[r] == '\r')) {
+          if (ls >= stop) {
+            seg[1] = ls;
+            return MP_SEG;
+          }
+          break;
+        }
       }
       if (mp_is_final(s, ls, le, bd, bn, lf)) return MP_OK;
       if (expect_new) return MP_E_EXPECT;
@@ -2246,6 +2259,7 @@ GI_HD __noinline__ uint8_t parse_multipart(C& t, const uint8_t* s, uint32_t n, c
       return MP_E_UNEXP;
     }
     parts++;
+    if (seg) seg[0] = parts;
     // textproto.ReadMIMEHeader: FK_PART_HEADER fields (key, value) for now
     const uint32_t h0 = t.nf;
     uint8_t herr = MP_OK;
@@ -6150,6 +6164,130 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
 // part-data delimiter search walks that list instead of the part's bytes.
 // On failure the request keeps no fields (k_eval parses it again).
 #define GI_MP_MAX_BOUNDARY 256
+
+// The body's parts split over the lanes: the delimiters are the candidates
+// with '\r' before them that Go's matchAfterPrefix accepts (V); the part
+// ending at V[j] starts at the delimiter line V[j - 1] + 1, and the first V
+// entry whose line is the final delimiter ends the last part.  Lane L parses
+// parts [a, b) with the sequential parse_multipart itself, started at its
+// first part's delimiter line and stopped at the next lane's, into its own
+// slice of the t1 scratch (fields) and of the arena; the slices are then
+// concatenated in lane order -- the order, and the allocations, of one
+// sequential pass.  Anything a lane cannot reproduce exactly (an error, a
+// segment that does not end where the next begins, a file name two lanes
+// both size, a quota overflow) returns false: lane 0 then parses the body
+// alone.  res = k_mpparse's result words.
+__device__ bool wave_multipart(const Region& g, const uint8_t* s, uint32_t n, Str ct, const uint8_t* sbd, uint32_t bn,
+                               uint32_t* cand, uint32_t ncand, uint32_t nf0, uint32_t nb0, uint32_t* res) {
+  const uint32_t L = lane_id();
+  if (8ull * ncand > g.cap_t || g.cap_b <= nb0) return false;
+  uint32_t* V = cand + ncand;
+  // V: the delimiters, in body order
+  uint32_t nv = 0;
+  for (uint32_t c0 = 0; c0 < ncand; c0 += 64) {
+    const uint32_t c = c0 + L;
+    bool v = false;
+    if (c < ncand) {
+      const uint32_t k = cand[c];
+      v = k >= 1 && s[k - 1] == '\r' && mp_after_ok(s, n, k + 3 + bn);
+    }
+    const uint64_t m = __ballot(v);
+    if (v) V[nv + mask_rank(m)] = cand[c];
+    nv += (uint32_t)__popcll(m);
+  }
+  // f: the first delimiter whose line is the final one
+  uint32_t f = 0xFFFFFFFFu;
+  for (uint32_t j0 = 0; j0 < nv && f == 0xFFFFFFFFu; j0 += 64) {
+    const uint32_t j = j0 + L;
+    bool fin = false;
+    if (j < nv) {
+      const uint32_t ls = V[j] + 1;
+      uint32_t e = ls + 2 + bn;
+      while (e < n && e < ls + 2 + bn + 64 && s[e] != '\n') e++;
+      if (e < n && s[e] == '\n') e++;
+      fin = (e >= n || s[e - 1] == '\n') && mp_is_final(s, ls, e, sbd, bn, false);
+    }
+    const uint64_t m = __ballot(fin);
+    if (m) f = j0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+  }
+  if (f == 0xFFFFFFFFu) return false;
+  const uint32_t np = f + 1;  // parts
+  const uint32_t nl = min(64u, np);
+  const uint32_t fq = g.cap_t / (uint32_t)sizeof(Field) / 64;  // fields per lane
+  const uint32_t aq = ((g.cap_b - nb0) / 64) & ~7u;            // arena bytes per lane
+  uint32_t err = MP_OK, cnt = 0, used = 0;
+  uint64_t comb = 0;
+  bool cset = false, good = true;
+  if (L < nl) {
+    const uint32_t a = (uint32_t)((uint64_t)np * L / nl), b = (uint32_t)((uint64_t)np * (L + 1) / nl);
+    const uint32_t i0 = a == 0 ? 0u : V[a - 1] + 1;
+    const uint32_t stop = b == np ? 0xFFFFFFFFu : V[b - 1] + 1;
+    if (a > 0) {  // a lane after the first starts at a plain "--boundary\r\n" line
+      good = i0 + 4 + bn <= n && s[i0] == '-' && s[i0 + 1] == '-' && s[i0 + 2 + bn] == '\r' && s[i0 + 3 + bn] == '\n';
+      for (uint32_t q = 0; q < bn && good; q++) good = s[i0 + 2 + q] == sbd[q];
+    }
+    if (good) {
+      Field* fl = (Field*)g.t1 + (uint64_t)L * fq;
+      JsonCtx jc{fl, 0, fq, g.bytes, nb0 + L * aq, nb0 + (L + 1) * aq, nullptr, 0, 0};
+      uint32_t seg[2] = {0, 0};
+      err = parse_multipart(jc, s, n, ct.p, ct.n, &comb, &cset, cand, ncand, i0, stop, seg);
+      good = jc.flags == 0 && seg[0] == b - a && (b == np ? err == MP_OK : (err == MP_SEG && seg[1] == stop));
+      cnt = jc.nf;
+      used = jc.nb - (nb0 + L * aq);
+    }
+  }
+  if (__ballot(!good)) return false;
+  uint32_t ftot, btot;
+  const uint32_t fo = wave_excl_sum(cnt, &ftot), bo = wave_excl_sum(used, &btot);
+  if ((uint64_t)nf0 + ftot > g.cap_f) return false;
+  // the arena slices, moved down in lane order (a forward copy: dst <= src)
+  for (uint32_t l2 = 0; l2 < nl; l2++) {
+    const uint32_t u2 = __shfl(used, (int)l2, 64), o2 = __shfl(bo, (int)l2, 64);
+    const uint32_t src = nb0 + l2 * aq, dst = nb0 + o2;
+    if (src != dst)
+      for (uint32_t k0 = 0; k0 < u2; k0 += 64) {
+        uint8_t x = 0;
+        if (k0 + L < u2) x = g.bytes[src + k0 + L];
+        __syncthreads();
+        if (k0 + L < u2) g.bytes[dst + k0 + L] = x;
+        __syncthreads();
+      }
+  }
+  // the fields, in lane order, arena pointers rebased
+  {
+    const Field* fl = (const Field*)g.t1 + (uint64_t)L * fq;
+    const uint8_t* lo = g.bytes + nb0 + L * aq;
+    const uint8_t* hi = lo + aq;
+    const uint64_t shift = (uint64_t)L * aq - bo;
+    for (uint32_t i = 0; i < cnt; i++) {
+      Field x = fl[i];
+      if (x.k >= lo && x.k < hi) x.k -= shift;
+      if (x.v >= lo && x.v < hi) x.v -= shift;
+      g.fields[nf0 + fo + i] = x;
+    }
+  }
+  __syncthreads();
+  // FILES_SIZES: one entry per file name (eq_ascii_ci_both) across the lanes
+  bool dup = false;
+  for (uint32_t i = nf0 + L; i < nf0 + ftot; i += 64) {
+    const Field x = g.fields[i];
+    if (x.kind != FK_FILE_SIZE) continue;
+    for (uint32_t j = nf0; j < i && !dup; j++) {
+      const Field y = g.fields[j];
+      if (y.kind == FK_FILE_SIZE && y.kn == x.kn && eq_ascii_ci_both(y.k, x.k, x.kn)) dup = true;
+    }
+  }
+  if (__ballot(dup)) return false;
+  uint64_t ctot = wave_sum((uint64_t)comb);
+  const bool cs = __ballot(cset) != 0;
+  res[0] = MP_OK;
+  res[1] = nf0 + ftot;
+  res[2] = nb0 + btot;
+  res[3] = (uint32_t)ctot;
+  res[4] = (uint32_t)(ctot >> 32) | (cs ? 0x80000000u : 0u);
+  return true;
+}
+
 __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
   __shared__ uint8_t sbd[GI_MP_MAX_BOUNDARY];
   __shared__ uint32_t sbn;
@@ -6201,38 +6339,56 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
       ncand = tot;
     }
     __syncthreads();
-    if (L == 0) {
-      JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
-      uint64_t comb;
-      bool comb_set;
-      const uint8_t err = parse_multipart(jc, s, n, ct.p, ct.n, &comb, &comb_set, use ? cand : nullptr, use ? ncand : 0u);
-      bool ok = !jc.flags;
-      if (ok && comb_set) {
-        uint8_t* cb = tx_alloc(jc, 24);
-        if (!cb) {
-          ok = false;
-        } else {
-          const uint32_t cn2 = go_itoa((int64_t)comb, cb);
-          jc.nb -= 24 - cn2;
-          H->single[S_FILES_COMBINED_SIZE] = {cb, cn2};
-        }
+    // the part-parallel parse (wave_multipart), else lane 0 alone
+    uint32_t res[5];  // err, fields after, arena after, FILES_COMBINED_SIZE (lo, hi | set << 31)
+    bool done = false;
+    if (use && ncand && B.mp_wave) done = wave_multipart(g, s, n, ct, sbd, bn, cand, ncand, nf0, nb0, res);
+    if (!done) {
+      if (L == 0) {
+        JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
+        uint64_t comb;
+        bool comb_set;
+        const uint8_t err = parse_multipart(jc, s, n, ct.p, ct.n, &comb, &comb_set, use ? cand : nullptr, use ? ncand : 0u);
+        res[0] = jc.flags ? 0xFFu : err;
+        res[1] = jc.nf;
+        res[2] = jc.nb;
+        res[3] = (uint32_t)comb;
+        res[4] = (uint32_t)(comb >> 32) | (comb_set ? 0x80000000u : 0u);
       }
-      if (!ok) {  // an engine limit / unsupported input: k_eval decides
-        H->spec_proc = BP_NONE;
+      for (int k = 0; k < 5; k++) res[k] = __shfl(res[k], 0, 64);
+    }
+    bool ok = res[0] != 0xFFu;
+    uint32_t nfe = res[1], nbe = res[2];
+    if (L == 0 && ok && (res[4] >> 31)) {
+      const uint64_t comb = (uint64_t)res[3] | ((uint64_t)(res[4] & 0x7FFFFFFFu) << 32);
+      if (nbe + 24 > g.cap_b) {
+        ok = false;
       } else {
-        H->spec_err = err;
-        H->n_post = jc.nf - nf0;
-        H->nb = jc.nb;
-        // phase-A item counts per length class of its ARGS_POST and FILES*
-        // fields (for_each_item's kinds)
-        if (P.n_streams) {
-          for (uint32_t f = nf0; f < jc.nf; f++) {
-            const Field fl = g.fields[f];
-            if (fl.kind < FK_ARG_GET || fl.kind > FK_FILE_SIZE) continue;
-            const uint32_t sides = P.item_sides[fl.kind];
-            if (sides & 1) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.kind, 0, fl.vn)], 1u);
-            if (sides & 2) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.kind, 1, fl.kn)], 1u);
-          }
+        uint8_t* cb = g.bytes + nbe;
+        const uint32_t cn2 = go_itoa((int64_t)comb, cb);
+        nbe += cn2;
+        H->single[S_FILES_COMBINED_SIZE] = {cb, cn2};
+      }
+    }
+    ok = __shfl((int)ok, 0, 64) != 0;
+    nbe = __shfl(nbe, 0, 64);
+    if (!ok) {  // an engine limit / unsupported input: k_eval decides
+      if (L == 0) H->spec_proc = BP_NONE;
+    } else {
+      if (L == 0) {
+        H->spec_err = (uint8_t)res[0];
+        H->n_post = nfe - nf0;
+        H->nb = nbe;
+      }
+      // phase-A item counts per length class of its ARGS_POST and FILES*
+      // fields (for_each_item's kinds)
+      if (P.n_streams) {
+        for (uint32_t f = nf0 + L; f < nfe; f += 64) {
+          const Field fl = g.fields[f];
+          if (fl.kind < FK_ARG_GET || fl.kind > FK_FILE_SIZE) continue;
+          const uint32_t sides = P.item_sides[fl.kind];
+          if (sides & 1) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.kind, 0, fl.vn)], 1u);
+          if (sides & 2) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class(fl.kind, 1, fl.kn)], 1u);
         }
       }
     }

@@ -1283,6 +1283,8 @@ int gi_run_staged(gi_ctx* c) {
     static const uint32_t ws2_env = getenv("GI_EVAL_WAVE_STAGE2") ? (uint32_t)atoi(getenv("GI_EVAL_WAVE_STAGE2")) : 1u;
     B.wave_stage2 = ws2_env;
     B.bparse_wave = c->bparse_wave;
+    static const uint32_t mpw_env = getenv("GI_MP_WAVE") ? (uint32_t)atoi(getenv("GI_MP_WAVE")) : 1u;
+    B.mp_wave = mpw_env;
     B.bparse_lds = c->bparse_wave ? c->bparse_win
                                   : (uint32_t)std::min<uint64_t>(c->bparse_lds, (c->max_body + 15) & ~15ull);
   }

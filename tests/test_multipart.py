@@ -186,3 +186,36 @@ def test_gpu_multipart_parity():
     for rid in (301, 302, 303, 304, 305, 306, 307, 308, 310, 311, 313, 314, 200002):
         assert fired.get(rid, 0) > 0, (rid, fired)
     assert 309 not in fired and 312 not in fired
+
+
+def many_parts(n, seed=12):
+    """Bodies of 40-300 parts (k_mpparse splits them over the lanes:
+    wave_multipart), file names repeated across the split (FILES_SIZES keeps
+    one entry per name), some with an epilogue or a broken part late in the body."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        b = b"mAnY%d" % i
+        parts = [_part(rng, k, True) for k in range(int(rng.integers(40, 300)))]
+        if i % 4 == 1:  # one file name in many parts, in two cases
+            parts += [b'Content-Disposition: form-data; name="u"; filename="%s"\r\n\r\nxyz' % fn
+                      for fn in (b"dup.php", b"DUP.php", b"dup.php")]
+        body = b"".join(b"--" + b + b"\r\n" + p + b"\r\n" for p in parts) + b"--" + b + b"--\r\n"
+        if i % 5 == 2:
+            body += b"epilogue --" + b + b"\r\nmore"
+        if i % 7 == 3:
+            body = body.replace(b"Content-Disposition", b"Content Disposition", 1 + int(rng.integers(0, 40)))
+        if i % 11 == 5:
+            body = body[:len(body) - int(rng.integers(1, 200))]
+        out.append((b"multipart/form-data; boundary=" + b, body))
+    return out
+
+
+@pytest.mark.gpu
+def test_gpu_multipart_many_parts_parity():
+    batch = batch_of(many_parts(48))
+    rs = gpuinspect.Ruleset(RULES)
+    res = gpuinspect.Engine(rs).inspect(batch)
+    verdicts = compare.oracle_verdicts(coraza.parse_seclang(RULES), batch, rs.exports)
+    bad = compare.compare(res, verdicts)
+    assert not bad, bad[:5]
