@@ -2192,7 +2192,7 @@ GI_HD inline bool mp_after_ok(const uint8_t* s, uint32_t n, uint32_t k) {
 // cand (optional, k_mpparse): every position k of a '\n' followed by
 // "--" + boundary, ascending -- the delimiter search of a part's data then
 // walks this list instead of every byte of the part.
-// Segments (k_mpparse's part-parallel parse, wave_multipart): i0 = where
+// Segments (k_mpparse's part-parallel parse, block_multipart): i0 = where
 // the parse starts (a delimiter line; 0 = the body), stop = a delimiter line
 // at or after this position ends it with MP_SEG before that part (seg[0] =
 // parts parsed, seg[1] = where that line starts).
@@ -6157,108 +6157,144 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
   }
 }
 
-// Speculative multipart ProcessRequestBody: one wave per body.  The wave
-// first lists every '\n' + "--" + boundary position of the body (lanes scan
-// 1/64 each, a prefix sum orders the lists) into the request's t0 buffer;
-// lane 0 then runs the sequential parser (Go mime/multipart restated), whose
-// part-data delimiter search walks that list instead of the part's bytes.
+// Speculative multipart ProcessRequestBody: one workgroup per body.  Its
+// threads first list every '\n' + "--" + boundary position of the body (each
+// scans 1/GI_MP_T, a prefix sum orders the lists) into the request's t0
+// buffer; the parts are then parsed in parallel (block_multipart) or, when
+// that is not exact, by thread 0 alone with the sequential parser (Go
+// mime/multipart restated), whose part-data delimiter search walks the list.
 // On failure the request keeps no fields (k_eval parses it again).
 #define GI_MP_MAX_BOUNDARY 256
 
-// The body's parts split over the lanes: the delimiters are the candidates
-// with '\r' before them that Go's matchAfterPrefix accepts (V); the part
-// ending at V[j] starts at the delimiter line V[j - 1] + 1, and the first V
-// entry whose line is the final delimiter ends the last part.  Lane L parses
-// parts [a, b) with the sequential parse_multipart itself, started at its
-// first part's delimiter line and stopped at the next lane's, into its own
-// slice of the t1 scratch (fields) and of the arena; the slices are then
-// concatenated in lane order -- the order, and the allocations, of one
-// sequential pass.  Anything a lane cannot reproduce exactly (an error, a
-// segment that does not end where the next begins, a file name two lanes
-// both size, a quota overflow) returns false: lane 0 then parses the body
-// alone.  res = k_mpparse's result words.
-__device__ bool wave_multipart(const Region& g, const uint8_t* s, uint32_t n, Str ct, const uint8_t* sbd, uint32_t bn,
-                               uint32_t* cand, uint32_t ncand, uint32_t nf0, uint32_t nb0, uint32_t* res) {
-  const uint32_t L = lane_id();
+// The body's parts split over the block's GI_MP_T threads: the delimiters
+// are the candidates with '\r' before them that Go's matchAfterPrefix accepts
+// (V); the part ending at V[j] starts at the delimiter line V[j - 1] + 1, and
+// the first V entry whose line is the final delimiter ends the last part.
+// Thread T parses parts [a, b) with the sequential parse_multipart itself,
+// started at its first part's delimiter line and stopped at the next
+// thread's, into its own slice of the t1 scratch (fields) and of the arena;
+// the slices are then concatenated in thread order -- the order, and the
+// allocations, of one sequential pass.  Anything a thread cannot reproduce
+// exactly (an error, a segment that does not end where the next begins, a
+// file name two threads both size, a quota overflow) returns false: thread 0
+// then parses the body alone.  Every return is block-uniform.
+#define GI_MP_T 256
+struct MpShared {
+  uint32_t wsum[GI_MP_T / 64];
+  uint32_t used[GI_MP_T], bo[GI_MP_T];
+  uint32_t res[5];
+  uint32_t f;
+  unsigned long long comb;
+};
+
+// exclusive prefix sum over the block (every thread calls it)
+__device__ __forceinline__ uint32_t block_excl_sum(uint32_t x, uint32_t* total, uint32_t* wsum) {
+  const uint32_t W = threadIdx.x >> 6;
+  uint32_t wt;
+  const uint32_t e = wave_excl_sum(x, &wt);
+  if ((threadIdx.x & 63) == 0) wsum[W] = wt;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (uint32_t w = 0; w < GI_MP_T / 64; w++) {
+    const uint32_t v = wsum[w];
+    off += w < W ? v : 0u;
+    tot += v;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + e;
+}
+
+__device__ bool block_multipart(const Region& g, const uint8_t* s, uint32_t n, Str ct, const uint8_t* sbd, uint32_t bn,
+                                uint32_t* cand, uint32_t ncand, uint32_t nf0, uint32_t nb0, MpShared& sh) {
+  const uint32_t T = threadIdx.x;
   if (8ull * ncand > g.cap_t || g.cap_b <= nb0) return false;
   uint32_t* V = cand + ncand;
   // V: the delimiters, in body order
   uint32_t nv = 0;
-  for (uint32_t c0 = 0; c0 < ncand; c0 += 64) {
-    const uint32_t c = c0 + L;
+  for (uint32_t c0 = 0; c0 < ncand; c0 += GI_MP_T) {
+    const uint32_t c = c0 + T;
     bool v = false;
     if (c < ncand) {
       const uint32_t k = cand[c];
       v = k >= 1 && s[k - 1] == '\r' && mp_after_ok(s, n, k + 3 + bn);
     }
-    const uint64_t m = __ballot(v);
-    if (v) V[nv + mask_rank(m)] = cand[c];
-    nv += (uint32_t)__popcll(m);
+    uint32_t tot;
+    const uint32_t at = block_excl_sum(v ? 1u : 0u, &tot, sh.wsum);
+    if (v) V[nv + at] = cand[c];
+    nv += tot;
   }
   // f: the first delimiter whose line is the final one
-  uint32_t f = 0xFFFFFFFFu;
-  for (uint32_t j0 = 0; j0 < nv && f == 0xFFFFFFFFu; j0 += 64) {
-    const uint32_t j = j0 + L;
-    bool fin = false;
+  if (T == 0) sh.f = 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t j0 = 0; j0 < nv; j0 += GI_MP_T) {
+    const uint32_t j = j0 + T;
     if (j < nv) {
       const uint32_t ls = V[j] + 1;
       uint32_t e = ls + 2 + bn;
       while (e < n && e < ls + 2 + bn + 64 && s[e] != '\n') e++;
       if (e < n && s[e] == '\n') e++;
-      fin = (e >= n || s[e - 1] == '\n') && mp_is_final(s, ls, e, sbd, bn, false);
+      if ((e >= n || s[e - 1] == '\n') && mp_is_final(s, ls, e, sbd, bn, false)) atomicMin(&sh.f, j);
     }
-    const uint64_t m = __ballot(fin);
-    if (m) f = j0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+    __syncthreads();
+    const bool found = sh.f != 0xFFFFFFFFu;
+    __syncthreads();  // (everyone read it before the next round's atomicMin)
+    if (found) break;
   }
+  const uint32_t f = sh.f;
   if (f == 0xFFFFFFFFu) return false;
   const uint32_t np = f + 1;  // parts
-  const uint32_t nl = min(64u, np);
-  const uint32_t fq = g.cap_t / (uint32_t)sizeof(Field) / 64;  // fields per lane
-  const uint32_t aq = ((g.cap_b - nb0) / 64) & ~7u;            // arena bytes per lane
+  const uint32_t nl = min((uint32_t)GI_MP_T, np);
+  const uint32_t fq = g.cap_t / (uint32_t)sizeof(Field) / GI_MP_T;  // fields per thread
+  const uint32_t aq = ((g.cap_b - nb0) / GI_MP_T) & ~7u;            // arena bytes per thread
   uint32_t err = MP_OK, cnt = 0, used = 0;
   uint64_t comb = 0;
   bool cset = false, good = true;
-  if (L < nl) {
-    const uint32_t a = (uint32_t)((uint64_t)np * L / nl), b = (uint32_t)((uint64_t)np * (L + 1) / nl);
+  if (T < nl) {
+    const uint32_t a = (uint32_t)((uint64_t)np * T / nl), b = (uint32_t)((uint64_t)np * (T + 1) / nl);
     const uint32_t i0 = a == 0 ? 0u : V[a - 1] + 1;
     const uint32_t stop = b == np ? 0xFFFFFFFFu : V[b - 1] + 1;
-    if (a > 0) {  // a lane after the first starts at a plain "--boundary\r\n" line
+    if (a > 0) {  // a thread after the first starts at a plain "--boundary\r\n" line
       good = i0 + 4 + bn <= n && s[i0] == '-' && s[i0 + 1] == '-' && s[i0 + 2 + bn] == '\r' && s[i0 + 3 + bn] == '\n';
       for (uint32_t q = 0; q < bn && good; q++) good = s[i0 + 2 + q] == sbd[q];
     }
     if (good) {
-      Field* fl = (Field*)g.t1 + (uint64_t)L * fq;
-      JsonCtx jc{fl, 0, fq, g.bytes, nb0 + L * aq, nb0 + (L + 1) * aq, nullptr, 0, 0};
+      Field* fl = (Field*)g.t1 + (uint64_t)T * fq;
+      JsonCtx jc{fl, 0, fq, g.bytes, nb0 + T * aq, nb0 + (T + 1) * aq, nullptr, 0, 0};
       uint32_t seg[2] = {0, 0};
       err = parse_multipart(jc, s, n, ct.p, ct.n, &comb, &cset, cand, ncand, i0, stop, seg);
       good = jc.flags == 0 && seg[0] == b - a && (b == np ? err == MP_OK : (err == MP_SEG && seg[1] == stop));
       cnt = jc.nf;
-      used = jc.nb - (nb0 + L * aq);
+      used = jc.nb - (nb0 + T * aq);
     }
   }
-  if (__ballot(!good)) return false;
+  if (__syncthreads_or(!good)) return false;
   uint32_t ftot, btot;
-  const uint32_t fo = wave_excl_sum(cnt, &ftot), bo = wave_excl_sum(used, &btot);
+  const uint32_t fo = block_excl_sum(cnt, &ftot, sh.wsum);
+  const uint32_t bo = block_excl_sum(used, &btot, sh.wsum);
   if ((uint64_t)nf0 + ftot > g.cap_f) return false;
-  // the arena slices, moved down in lane order (a forward copy: dst <= src)
+  sh.used[T] = used;
+  sh.bo[T] = bo;
+  if (T == 0) sh.comb = 0;
+  __syncthreads();
+  // the arena slices, moved down in thread order (a forward copy: dst <= src)
   for (uint32_t l2 = 0; l2 < nl; l2++) {
-    const uint32_t u2 = __shfl(used, (int)l2, 64), o2 = __shfl(bo, (int)l2, 64);
-    const uint32_t src = nb0 + l2 * aq, dst = nb0 + o2;
-    if (src != dst)
-      for (uint32_t k0 = 0; k0 < u2; k0 += 64) {
-        uint8_t x = 0;
-        if (k0 + L < u2) x = g.bytes[src + k0 + L];
-        __syncthreads();
-        if (k0 + L < u2) g.bytes[dst + k0 + L] = x;
-        __syncthreads();
-      }
+    const uint32_t u2 = sh.used[l2], src = nb0 + l2 * aq, dst = nb0 + sh.bo[l2];
+    if (src == dst) continue;
+    for (uint32_t k0 = 0; k0 < u2; k0 += GI_MP_T) {
+      uint8_t x = 0;
+      if (k0 + T < u2) x = g.bytes[src + k0 + T];
+      __syncthreads();
+      if (k0 + T < u2) g.bytes[dst + k0 + T] = x;
+      __syncthreads();
+    }
   }
-  // the fields, in lane order, arena pointers rebased
-  {
-    const Field* fl = (const Field*)g.t1 + (uint64_t)L * fq;
-    const uint8_t* lo = g.bytes + nb0 + L * aq;
+  // the fields, in thread order, arena pointers rebased
+  if (cnt) {
+    const Field* fl = (const Field*)g.t1 + (uint64_t)T * fq;
+    const uint8_t* lo = g.bytes + nb0 + T * aq;
     const uint8_t* hi = lo + aq;
-    const uint64_t shift = (uint64_t)L * aq - bo;
+    const uint64_t shift = (uint64_t)T * aq - bo;
     for (uint32_t i = 0; i < cnt; i++) {
       Field x = fl[i];
       if (x.k >= lo && x.k < hi) x.k -= shift;
@@ -6266,10 +6302,11 @@ __device__ bool wave_multipart(const Region& g, const uint8_t* s, uint32_t n, St
       g.fields[nf0 + fo + i] = x;
     }
   }
+  if (comb) atomicAdd(&sh.comb, (unsigned long long)comb);
   __syncthreads();
-  // FILES_SIZES: one entry per file name (eq_ascii_ci_both) across the lanes
+  // FILES_SIZES: one entry per file name (eq_ascii_ci_both) across the threads
   bool dup = false;
-  for (uint32_t i = nf0 + L; i < nf0 + ftot; i += 64) {
+  for (uint32_t i = nf0 + T; i < nf0 + ftot; i += GI_MP_T) {
     const Field x = g.fields[i];
     if (x.kind != FK_FILE_SIZE) continue;
     for (uint32_t j = nf0; j < i && !dup; j++) {
@@ -6277,34 +6314,39 @@ __device__ bool wave_multipart(const Region& g, const uint8_t* s, uint32_t n, St
       if (y.kind == FK_FILE_SIZE && y.kn == x.kn && eq_ascii_ci_both(y.k, x.k, x.kn)) dup = true;
     }
   }
-  if (__ballot(dup)) return false;
-  uint64_t ctot = wave_sum((uint64_t)comb);
-  const bool cs = __ballot(cset) != 0;
-  res[0] = MP_OK;
-  res[1] = nf0 + ftot;
-  res[2] = nb0 + btot;
-  res[3] = (uint32_t)ctot;
-  res[4] = (uint32_t)(ctot >> 32) | (cs ? 0x80000000u : 0u);
+  if (__syncthreads_or(dup)) return false;
+  const bool cs = __syncthreads_or(cset) != 0;
+  if (T == 0) {
+    const uint64_t ctot = sh.comb;
+    sh.res[0] = MP_OK;
+    sh.res[1] = nf0 + ftot;
+    sh.res[2] = nb0 + btot;
+    sh.res[3] = (uint32_t)ctot;
+    sh.res[4] = (uint32_t)(ctot >> 32) | (cs ? 0x80000000u : 0u);
+  }
+  __syncthreads();
   return true;
 }
 
-__global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
+__global__ void __launch_bounds__(GI_MP_T) k_mpparse(DProgram P, DBatch B) {
   __shared__ uint8_t sbd[GI_MP_MAX_BOUNDARY];
   __shared__ uint32_t sbn;
-  const uint32_t L = threadIdx.x;
+  __shared__ MpShared sh;
+  const uint32_t T = threadIdx.x;
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
     const uint32_t r = B.body_list[bi];
     GI_BOUND(r < B.n_req, r, bi);
-    if (B.stage == 2 && !B.pend[r]) continue;  // decided in phase 1 (wave-uniform)
+    if (B.stage == 2 && !B.pend[r]) continue;  // decided in phase 1 (block-uniform)
     Region g = region_of(P, B, r);
     ReqHdr* H = g.hdr;
-    if (H->spec_proc != BP_MULTIPART || (H->flags & GI_REQ_ERROR_MASK)) continue;  // wave-uniform
+    if (H->spec_proc != BP_MULTIPART || (H->flags & GI_REQ_ERROR_MASK)) continue;  // block-uniform
     const gi_span bs = B.reqs[r].body;
     const uint8_t* s = B.data + bs.off;
     const uint32_t n = bs.len;
     const uint32_t nf0 = H->nf, nb0 = H->nb;
     const Str ct = first_content_type(B, B.reqs[r]);
-    if (L == 0) {  // the boundary (a throw-away arena copy: parse_multipart parses the media type again)
+    __syncthreads();  // (every thread read H before thread 0 rewrites it below)
+    if (T == 0) {  // the boundary (a throw-away arena copy: parse_multipart parses the media type again)
       JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
       uint32_t ts, te;
       Str bstr;
@@ -6321,7 +6363,7 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
     uint32_t ncand = 0;
     bool use = false;
     if (bn) {
-      const uint32_t a0 = (uint32_t)((uint64_t)n * L / 64), a1 = (uint32_t)((uint64_t)n * (L + 1) / 64);
+      const uint32_t a0 = (uint32_t)((uint64_t)n * T / GI_MP_T), a1 = (uint32_t)((uint64_t)n * (T + 1) / GI_MP_T);
       auto hit = [&](uint32_t k) {
         if (s[k] != '\n' || k + 3 + bn > n || s[k + 1] != '-' || s[k + 2] != '-') return false;
         for (uint32_t q = 0; q < bn; q++)
@@ -6331,7 +6373,7 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
       uint32_t c = 0;
       for (uint32_t k = a0; k < a1; k++) c += hit(k) ? 1u : 0u;
       uint32_t tot;
-      uint32_t at = wave_excl_sum(c, &tot);
+      uint32_t at = block_excl_sum(c, &tot, sh.wsum);
       use = 4ull * tot <= g.cap_t;
       if (use)
         for (uint32_t k = a0; k < a1; k++)
@@ -6339,27 +6381,29 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
       ncand = tot;
     }
     __syncthreads();
-    // the part-parallel parse (wave_multipart), else lane 0 alone
-    uint32_t res[5];  // err, fields after, arena after, FILES_COMBINED_SIZE (lo, hi | set << 31)
+    // the part-parallel parse (block_multipart), else thread 0 alone
     bool done = false;
-    if (use && ncand && B.mp_wave) done = wave_multipart(g, s, n, ct, sbd, bn, cand, ncand, nf0, nb0, res);
+    if (use && ncand && B.mp_wave) done = block_multipart(g, s, n, ct, sbd, bn, cand, ncand, nf0, nb0, sh);
     if (!done) {
-      if (L == 0) {
+      if (T == 0) {
         JsonCtx jc{g.fields, nf0, g.cap_f, g.bytes, nb0, g.cap_b, g.t1, g.cap_t, 0};
         uint64_t comb;
         bool comb_set;
         const uint8_t err = parse_multipart(jc, s, n, ct.p, ct.n, &comb, &comb_set, use ? cand : nullptr, use ? ncand : 0u);
-        res[0] = jc.flags ? 0xFFu : err;
-        res[1] = jc.nf;
-        res[2] = jc.nb;
-        res[3] = (uint32_t)comb;
-        res[4] = (uint32_t)(comb >> 32) | (comb_set ? 0x80000000u : 0u);
+        sh.res[0] = jc.flags ? 0xFFu : err;
+        sh.res[1] = jc.nf;
+        sh.res[2] = jc.nb;
+        sh.res[3] = (uint32_t)comb;
+        sh.res[4] = (uint32_t)(comb >> 32) | (comb_set ? 0x80000000u : 0u);
       }
-      for (int k = 0; k < 5; k++) res[k] = __shfl(res[k], 0, 64);
+      __syncthreads();
     }
+    uint32_t res[5];
+    for (int k = 0; k < 5; k++) res[k] = sh.res[k];
+    __syncthreads();  // (sh.res is rewritten below)
     bool ok = res[0] != 0xFFu;
     uint32_t nfe = res[1], nbe = res[2];
-    if (L == 0 && ok && (res[4] >> 31)) {
+    if (T == 0 && ok && (res[4] >> 31)) {
       const uint64_t comb = (uint64_t)res[3] | ((uint64_t)(res[4] & 0x7FFFFFFFu) << 32);
       if (nbe + 24 > g.cap_b) {
         ok = false;
@@ -6370,12 +6414,17 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
         H->single[S_FILES_COMBINED_SIZE] = {cb, cn2};
       }
     }
-    ok = __shfl((int)ok, 0, 64) != 0;
-    nbe = __shfl(nbe, 0, 64);
+    if (T == 0) {
+      sh.res[0] = ok;
+      sh.res[1] = nbe;
+    }
+    __syncthreads();
+    ok = sh.res[0] != 0;
+    nbe = sh.res[1];
     if (!ok) {  // an engine limit / unsupported input: k_eval decides
-      if (L == 0) H->spec_proc = BP_NONE;
+      if (T == 0) H->spec_proc = BP_NONE;
     } else {
-      if (L == 0) {
+      if (T == 0) {
         H->spec_err = (uint8_t)res[0];
         H->n_post = nfe - nf0;
         H->nb = nbe;
@@ -6383,7 +6432,7 @@ __global__ void __launch_bounds__(64) k_mpparse(DProgram P, DBatch B) {
       // phase-A item counts per length class of its ARGS_POST and FILES*
       // fields (for_each_item's kinds)
       if (P.n_streams) {
-        for (uint32_t f = nf0 + L; f < nfe; f += 64) {
+        for (uint32_t f = nf0 + T; f < nfe; f += GI_MP_T) {
           const Field fl = g.fields[f];
           if (fl.kind < FK_ARG_GET || fl.kind > FK_FILE_SIZE) continue;
           const uint32_t sides = P.item_sides[fl.kind];
@@ -9042,7 +9091,7 @@ void launch_pipeline(const DProgram& P, const DBatch& B0, const ScanLaunch& S, h
   GI_LAUNCH("k_collect", k_collect, dim3(cb), dim3(256), 0, stream, P, B);
   if (B.n_body && P.body_access) {
     GI_LAUNCH("k_bparse", k_bparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), B.bparse_lds, stream, P, B);
-    if (B.n_mp_body) GI_LAUNCH("k_mpparse", k_mpparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(64), 0, stream, P, B);
+    if (B.n_mp_body) GI_LAUNCH("k_mpparse", k_mpparse, dim3(std::min<uint32_t>(B.n_body, 1u << 20)), dim3(GI_MP_T), 0, stream, P, B);
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (P.n_streams) launch_phase_a(P, B, S, stream, ev, stop_after, log, nk);
