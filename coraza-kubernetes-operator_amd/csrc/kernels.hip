@@ -6183,7 +6183,7 @@ struct MpShared {
   uint32_t wsum[GI_MP_T / 64];
   uint32_t used[GI_MP_T], bo[GI_MP_T];
   uint32_t res[5];
-  uint32_t f;
+  uint32_t f, nfs;
   unsigned long long comb;
 };
 
@@ -6277,16 +6277,25 @@ __device__ bool block_multipart(const Region& g, const uint8_t* s, uint32_t n, S
   sh.bo[T] = bo;
   if (T == 0) sh.comb = 0;
   __syncthreads();
-  // the arena slices, moved down in thread order (a forward copy: dst <= src)
-  for (uint32_t l2 = 0; l2 < nl; l2++) {
-    const uint32_t u2 = sh.used[l2], src = nb0 + l2 * aq, dst = nb0 + sh.bo[l2];
-    if (src == dst) continue;
-    for (uint32_t k0 = 0; k0 < u2; k0 += GI_MP_T) {
-      uint8_t x = 0;
-      if (k0 + T < u2) x = g.bytes[src + k0 + T];
-      __syncthreads();
-      if (k0 + T < u2) g.bytes[dst + k0 + T] = x;
-      __syncthreads();
+  // the arena slices, moved down in thread order: through the t0 scratch
+  // after V when it holds them all (every thread its own slice), else slice
+  // by slice by the whole block (a forward copy: dst <= src)
+  if (8ull * ncand + btot <= g.cap_t) {
+    uint8_t* tmp = (uint8_t*)(V + ncand);
+    for (uint32_t k = 0; k < used; k++) tmp[bo + k] = g.bytes[nb0 + T * aq + k];
+    __syncthreads();
+    for (uint32_t k = T; k < btot; k += GI_MP_T) g.bytes[nb0 + k] = tmp[k];
+  } else {
+    for (uint32_t l2 = 0; l2 < nl; l2++) {
+      const uint32_t u2 = sh.used[l2], src = nb0 + l2 * aq, dst = nb0 + sh.bo[l2];
+      if (src == dst) continue;
+      for (uint32_t k0 = 0; k0 < u2; k0 += GI_MP_T) {
+        uint8_t x = 0;
+        if (k0 + T < u2) x = g.bytes[src + k0 + T];
+        __syncthreads();
+        if (k0 + T < u2) g.bytes[dst + k0 + T] = x;
+        __syncthreads();
+      }
     }
   }
   // the fields, in thread order, arena pointers rebased
@@ -6304,15 +6313,24 @@ __device__ bool block_multipart(const Region& g, const uint8_t* s, uint32_t n, S
   }
   if (comb) atomicAdd(&sh.comb, (unsigned long long)comb);
   __syncthreads();
-  // FILES_SIZES: one entry per file name (eq_ascii_ci_both) across the threads
-  bool dup = false;
-  for (uint32_t i = nf0 + T; i < nf0 + ftot; i += GI_MP_T) {
-    const Field x = g.fields[i];
-    if (x.kind != FK_FILE_SIZE) continue;
-    for (uint32_t j = nf0; j < i && !dup; j++) {
-      const Field y = g.fields[j];
-      if (y.kind == FK_FILE_SIZE && y.kn == x.kn && eq_ascii_ci_both(y.k, x.k, x.kn)) dup = true;
+  // FILES_SIZES: one entry per file name (eq_ascii_ci_both) across the
+  // threads: the entries listed in LDS, then compared pairwise
+  if (T == 0) sh.nfs = 0;
+  __syncthreads();
+  for (uint32_t i = nf0 + T; i < nf0 + ftot; i += GI_MP_T)
+    if (g.fields[i].kind == FK_FILE_SIZE) {
+      const uint32_t k = atomicAdd(&sh.nfs, 1u);
+      if (k < GI_MP_T) sh.used[k] = i;
     }
+  __syncthreads();
+  const uint32_t nfs = sh.nfs;
+  if (nfs > GI_MP_T) return false;
+  bool dup = false;
+  for (uint32_t a = T; a < nfs * nfs; a += GI_MP_T) {
+    const uint32_t i = a / nfs, j = a % nfs;
+    if (j >= i) continue;
+    const Field x = g.fields[sh.used[i]], y = g.fields[sh.used[j]];
+    if (y.kn == x.kn && eq_ascii_ci_both(y.k, x.k, x.kn)) dup = true;
   }
   if (__syncthreads_or(dup)) return false;
   const bool cs = __syncthreads_or(cset) != 0;
@@ -6370,14 +6388,36 @@ __global__ void __launch_bounds__(GI_MP_T) k_mpparse(DProgram P, DBatch B) {
           if (s[k + 3 + q] != sbd[q]) return false;
         return true;
       };
-      uint32_t c = 0;
-      for (uint32_t k = a0; k < a1; k++) c += hit(k) ? 1u : 0u;
+      // the '\n' bytes of the slice from aligned words, then the full test at each
+      auto scan = [&](uint32_t* out, uint32_t at) {
+        uint32_t c = 0;
+        uint32_t k = a0;
+        for (; k < a1 && ((uintptr_t)(s + k) & 3u); k++)
+          if (hit(k)) {
+            if (out) out[at + c] = k;
+            c++;
+          }
+        for (; k + 4 <= a1; k += 4) {
+          for (uint32_t m = zbytes4(*(const uint32_t*)(s + k) ^ 0x0A0A0A0Au); m; m &= m - 1) {
+            const uint32_t kk = k + (uint32_t)__builtin_ctz(m);
+            if (hit(kk)) {
+              if (out) out[at + c] = kk;
+              c++;
+            }
+          }
+        }
+        for (; k < a1; k++)
+          if (hit(k)) {
+            if (out) out[at + c] = k;
+            c++;
+          }
+        return c;
+      };
+      const uint32_t c = scan(nullptr, 0);
       uint32_t tot;
-      uint32_t at = block_excl_sum(c, &tot, sh.wsum);
+      const uint32_t at = block_excl_sum(c, &tot, sh.wsum);
       use = 4ull * tot <= g.cap_t;
-      if (use)
-        for (uint32_t k = a0; k < a1; k++)
-          if (hit(k)) cand[at++] = k;
+      if (use) scan(cand, at);
       ncand = tot;
     }
     __syncthreads();
