@@ -4793,22 +4793,34 @@ GI_HD __forceinline__ uint32_t eval_rule(Tx& t, const DRule& R) {
     if (conly) {  // RF2_PA_FILTER: the value changes nothing but the capture records
       CapHdr* CH = (CapHdr*)t.capws;
       if (!CH->trunc) {
+        // the link captures the whole t:lowercase value (compile.cpp within_chain_filters):
+        // lowercase straight into the record row -- run_capture's record, without the call
+        // or the TX.0 copy nobody reads (captures are not observable outside this chain).
+        // One pass with no early exit (the loads pipeline): copy, then keep it if ASCII.
+        const uint32_t nrec = CH->nrec, nbytes = CH->nbytes;
         bool ascii = cvn <= t.cap_t;
-        for (uint32_t i = 0; i < cvn && ascii; i++) ascii = cv[i] < 0x80;
+        bool fits = nrec < CH->rec_cap && nbytes + cvn <= CH->bytes_cap;
+        if (ascii && fits) {
+          uint8_t* d = CH->bytes + nbytes;
+          uint32_t acc = 0;
+          for (uint32_t i = 0; i < cvn; i++) {
+            const uint8_t c = cv[i];
+            acc |= c;
+            d[i] = (c >= 'A' && c <= 'Z') ? (uint8_t)(c + 32) : c;
+          }
+          ascii = acc < 0x80;
+        } else if (ascii) {
+          for (uint32_t i = 0; i < cvn && ascii; i++) ascii = cv[i] < 0x80;
+        }
         if (ascii) {
-          // the link captures the whole t:lowercase value (compile.cpp within_chain_filters):
-          // lowercase straight into the record row -- run_capture's record, without the call
-          // or the TX.0 copy nobody reads (captures are not observable outside this chain)
-          if (CH->nrec < CH->rec_cap && CH->nbytes + cvn <= CH->bytes_cap) {
-            uint8_t* d = CH->bytes + CH->nbytes;
-            for (uint32_t i = 0; i < cvn; i++) d[i] = (cv[i] >= 'A' && cv[i] <= 'Z') ? (uint8_t)(cv[i] + 32) : cv[i];
-            uint32_t* rr = CH->rec + 4ull * CH->nrec;
+          if (fits) {
+            uint32_t* rr = CH->rec + 4ull * nrec;
             rr[0] = t.cur_id;
             rr[1] = 0u;
-            rr[2] = CH->nbytes;
+            rr[2] = nbytes;
             rr[3] = cvn;
-            CH->nbytes += cvn;
-            CH->nrec++;
+            CH->nbytes = nbytes + cvn;
+            CH->nrec = nrec + 1;
           } else {
             CH->trunc = 1;
           }
