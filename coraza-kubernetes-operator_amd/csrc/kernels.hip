@@ -5197,6 +5197,24 @@ __device__ __forceinline__ uint32_t item_class(uint32_t kind, uint32_t side, uin
   return kClsBase[b] + g * kClsN[b] + lc;
 }
 
+// one source group's classes, numbered 0 .. GI_NCLS / 16 - 1 (k_bparse's
+// per-body counts of the ARGS_POST groups), and back to the global class
+__device__ __forceinline__ uint32_t item_class_in_group(uint32_t n) {
+  const uint32_t b = item_bucket(n);
+  const uint32_t lc = b < 4 ? n - kClsLo[b] : min(15u, (n - 129u) / 128u);
+  uint32_t pre = 0;
+  for (uint32_t k = 0; k < b; k++) pre += kClsN[k];
+  return pre + lc;
+}
+__device__ __forceinline__ uint32_t item_class_of_group(uint32_t g, uint32_t r) {
+  uint32_t b = 0;
+  while (b + 1 < GI_NB && r >= kClsN[b]) {
+    r -= kClsN[b];
+    b++;
+  }
+  return kClsBase[b] + g * kClsN[b] + r;
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // rank of this lane among the lanes of mask below it
@@ -5448,18 +5466,33 @@ __device__ __forceinline__ void dec_put(uint32_t v, uint32_t nd, D* d) {
   }
 }
 
+// LDS written by some lanes of the (single-wave) workgroup, read by others:
+// LDS operations of one wave execute in order, so only the compiler must not
+// move them across this point -- unlike __syncthreads, no wait for the
+// wave's outstanding global stores (the parser's field and key stores)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 struct JWin {  // q[wb, we) is in win
   const uint8_t* q;
   gi_lds_u8* win;
   uint32_t n, W, wb, we;
+  uint64_t rc;  // GI_PROF: cycles in refills
+  uint32_t nr;  // refills
 };
 
 __device__ __forceinline__ void jw_refill(JWin& w, uint32_t i) {
-  __syncthreads();  // every lane is done reading the old window
+  const uint64_t c0 = gi_clock();
+  w.nr++;
+  wave_lds_sync();  // every lane is done reading the old window
   w.wb = i & ~3u;
   w.we = min(w.n, w.wb + w.W);
   for (uint32_t k = w.wb + lane_id(); k < w.we; k += 64) w.win[k - w.wb] = w.q[k];
-  __syncthreads();
+  wave_lds_sync();
+  w.rc += gi_clock() - c0;
 }
 // byte i (i < n) of the body; the window moves forward (or back) to cover it
 __device__ __forceinline__ uint8_t jw_at(JWin& w, uint32_t i) {
@@ -5476,24 +5509,19 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
   return x;
 }
 
-// a hash of path[0, kn): equal keys hash equal (any function of the bytes does)
+// a hash of a key: the wave sum of jw_hmix(byte j, j) over its bytes (the
+// lane holding byte j mixes it), ^ its length -- equal keys hash equal; the
+// slow and the fast member paths compute the same function
+__device__ __forceinline__ uint32_t jw_hmix(uint32_t b, uint32_t j) {
+  uint32_t x = (b | (j << 8)) * 0x9E3779B1u;
+  x ^= x >> 15;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  return x;
+}
 __device__ __forceinline__ uint32_t wave_key_hash(const gi_lds_u8* path, uint32_t kn) {
-  const uint32_t L = lane_id();
   uint32_t acc = 0;
-  for (uint32_t base = 0; base < kn; base += 256) {
-    const uint32_t j = base + 4 * L;
-    uint32_t x = 0;
-    if (j < kn) {
-      uint32_t w = 0;
-      for (uint32_t b = 0; b < 4; b++)
-        if (j + b < kn) w |= (uint32_t)path[j + b] << (8 * b);
-      x = (w ^ (j * 0x9E3779B1u)) * 0x85EBCA6Bu;
-      x ^= x >> 13;
-      x *= 0xC2B2AE35u;
-      x ^= x >> 16;
-    }
-    acc += x;
-  }
+  for (uint32_t j = lane_id(); j < kn; j += 64) acc += jw_hmix(path[j], j);
   return wave_sum(acc) ^ (kn * 0x27D4EB2Fu);
 }
 
@@ -5598,14 +5626,195 @@ __device__ uint32_t jw_number_end(JWin& w, uint32_t i) {
   return i;
 }
 
+// bits [a, 64) / [a, b) of a 64-bit mask
+__device__ __forceinline__ uint64_t jw_from(uint32_t a) { return a >= 64 ? 0ull : ~0ull << a; }
+__device__ __forceinline__ uint64_t jw_range(uint32_t a, uint32_t b) { return jw_from(a) & ~jw_from(b); }
+__device__ __forceinline__ bool jw_bit(uint64_t m, uint32_t p) { return p < 64 && ((m >> p) & 1ull); }
+
+// wave_parse_json's member step from 64 bytes of the window at i, lane L
+// holding byte i + L, every test a ballot mask: a container's close, or
+// [','] '"' name '"' ':' value / [','] value with the value a container
+// opener, an unescaped string, a number or a literal -- all inside the 64
+// bytes.  Its state changes (fields, arena, key path, frames, i, d) are the
+// ones the general path makes for that member, in the same order; anything
+// else returns 0 before changing anything (the general path then runs).
+__device__ int jw_fast_member(const Region& g, JWin& w, const uint8_t* q, uint32_t& i, uint32_t& d, uint32_t& nf,
+                              uint32_t& nb, uint64_t& jb, uint64_t lim, gi_lds_u8* path, JWFrame* st) {
+  const uint32_t L = lane_id();
+  const uint32_t n = w.n;
+  if (i >= n) return 0;
+  jw_cover(w, i, 64);
+  const uint32_t cl = min(64u, n - i);  // bytes of the chunk
+  const uint8_t c = L < cl ? w.win[i + L - w.wb] : (uint8_t)0;
+  const JWFrame F = st[d - 1];
+  const bool in = L < cl;
+  const uint64_t WS = __ballot(in && json_ws(c)), Q = __ballot(in && c == '"');
+  const uint64_t BAD = __ballot(in && (c == '\\' || c < 0x20));  // escapes / control bytes end the fast path
+  const uint64_t DG = __ballot(in && c >= '0' && c <= '9');
+  const uint64_t valid = jw_range(0, cl);
+  auto nonws = [&](uint32_t p) -> uint32_t {
+    const uint64_t m = ~WS & valid & jw_from(p);
+    return m ? (uint32_t)__builtin_ctzll(m) : 64u;
+  };
+  auto is = [&](uint32_t p, uint8_t ch) -> bool { return p < cl && (__ballot(in && c == ch) >> p) & 1ull; };
+  uint32_t p = nonws(0);
+  if (p >= cl) return 0;
+  if (is(p, F.is_arr ? ']' : '}')) {  // the container's close
+    uint32_t dn = 0;
+    if (F.is_arr && F.count) {
+      dn = dec_len(F.count);
+      if (nb + 12 > g.cap_b || jb + dn > lim || nf >= g.cap_f) return 0;
+      if (L == 0) {
+        dec_put(F.count, dn, g.bytes + nb);
+        Field f;
+        f.k = g.bytes + F.koff;
+        f.v = g.bytes + nb;
+        f.kn = F.kn;
+        f.vn = dn;
+        f.kind = FK_ARG_POST;
+        f._pad = F.h;
+        g.fields[nf] = f;
+      }
+      nb += dn;
+      jb += dn;
+      nf++;
+    }
+    i += p + 1;
+    d--;
+    return 1;
+  }
+  if (F.count) {
+    if (!is(p, ',')) return 0;
+    p = nonws(p + 1);
+    if (p >= cl) return 0;
+  }
+  uint32_t kn, ns = 0, dn = 0, v;
+  if (!F.is_arr) {
+    if (!jw_bit(Q, p)) return 0;
+    ns = p + 1;
+    const uint64_t mq = Q & jw_from(ns);
+    if (!mq) return 0;
+    const uint32_t qe = (uint32_t)__builtin_ctzll(mq);
+    if (BAD & jw_range(ns, qe)) return 0;
+    const uint32_t co = nonws(qe + 1);
+    if (co >= cl || !is(co, ':')) return 0;
+    v = nonws(co + 1);
+    if (v >= cl) return 0;
+    kn = F.kn + 1 + (qe - ns);
+    if (nb + kn > g.cap_b) return 0;
+  } else {
+    v = p;
+    dn = dec_len(F.count);
+    kn = F.kn + 1 + dn;
+    if (nb + F.kn + 12 > g.cap_b) return 0;
+  }
+  if (kn > GI_JW_PATH || jb + kn > lim) return 0;
+  // the value: kind 0 container, 1 string, 2 number / literal; [vs, ve) its bytes, e = the chunk offset after it
+  int kind;
+  uint32_t vs = v, ve, e;
+  bool arr = false;
+  if (is(v, '{') || is(v, '[')) {
+    if (d >= GI_JSON_MAX_DEPTH) return 0;
+    kind = 0;
+    arr = is(v, '[');
+    ve = e = v + 1;
+  } else if (jw_bit(Q, v)) {
+    const uint64_t mq = Q & jw_from(v + 1);
+    if (!mq) return 0;
+    ve = (uint32_t)__builtin_ctzll(mq);
+    if (BAD & jw_range(v + 1, ve)) return 0;
+    kind = 1;
+    vs = v + 1;
+    e = ve + 1;
+  } else if (is(v, 't') || is(v, 'f') || is(v, 'n')) {
+    const uint32_t ln = is(v, 'f') ? 5u : 4u;
+    const char* lit = is(v, 't') ? "true" : is(v, 'f') ? "false" : "null";
+    if (v + ln > cl) return 0;
+    const uint64_t ok = __ballot(L >= v && L < v + ln && c == (uint8_t)lit[L - v]);
+    if (ok != jw_range(v, v + ln)) return 0;
+    kind = 2;
+    ve = is(v, 'n') ? v : v + ln;
+    e = v + ln;
+  } else {  // json_number_end over the masks
+    auto nondig = [&](uint32_t a) -> uint32_t {
+      const uint64_t m = ~DG & jw_from(a);
+      return m ? (uint32_t)__builtin_ctzll(m) : 64u;
+    };
+    uint32_t x = v;
+    if (is(x, '-')) x++;
+    if (!jw_bit(DG, x)) return 0;
+    x = is(x, '0') ? x + 1 : nondig(x);
+    if (x < cl && is(x, '.')) {
+      x++;
+      if (!jw_bit(DG, x)) return 0;
+      x = nondig(x);
+    }
+    if (x < cl && (is(x, 'e') || is(x, 'E'))) {
+      x++;
+      if (x < cl && (is(x, '+') || is(x, '-'))) x++;
+      if (!jw_bit(DG, x)) return 0;
+      x = nondig(x);
+    }
+    if (x >= cl) return 0;  // (it may go on past the chunk)
+    kind = 2;
+    ve = e = x;
+  }
+  if (kind != 0 && nf >= g.cap_f) return 0;
+  // commit: the key (path + arena) and its hash, the frame count, the value
+  const uint32_t koff = nb;
+  uint32_t acc = 0;
+  for (uint32_t j = L; j < kn; j += 64) {
+    uint8_t b;
+    if (j < F.kn) {
+      b = path[j];
+    } else if (j == F.kn) {
+      b = '.';
+    } else if (!F.is_arr) {
+      b = w.win[i + ns + (j - F.kn - 1) - w.wb];
+    } else {
+      uint32_t x = F.count;
+      for (uint32_t k = j - F.kn - 1; k + 1 < dn; k++) x /= 10;
+      b = (uint8_t)('0' + x % 10);
+    }
+    g.bytes[koff + j] = b;
+    if (j >= F.kn) path[j] = b;
+    acc += jw_hmix(b, j);
+  }
+  const uint32_t kh = wave_sum(acc) ^ (kn * 0x27D4EB2Fu);
+  nb += kn;
+  jb += kn;
+  if (L == 0) st[d - 1].count = F.count + 1;
+  if (kind == 0) {
+    if (L == 0) st[d] = {koff, kn, 0, arr ? 1u : 0u, kh};
+    d++;
+  } else {
+    if (L == 0) {
+      Field f;
+      f.k = g.bytes + koff;
+      f.v = q + i + vs;
+      f.kn = kn;
+      f.vn = ve - vs;
+      f.kind = FK_ARG_POST;
+      f._pad = kh;
+      g.fields[nf] = f;
+    }
+    nf++;
+  }
+  i += e;
+  return 1;
+}
+
 // Fields [nf0, *nf) and the arena [nb0, *nb) as parse_json_body(+ fold) makes
 // them; false: no fields (not parsed here).
 __device__ bool wave_parse_json(const Region& g, const uint8_t* q, uint32_t n, uint32_t nf0, uint32_t nb0,
                                 gi_lds_u8* win, uint32_t W, gi_lds_u8* path, JWFrame* st, uint32_t* nf_out,
-                                uint32_t* nb_out) {
+                                uint32_t* nb_out, unsigned long long* prof) {
   const uint32_t L = lane_id();
   const bool l0 = L == 0;
-  JWin w{q, win, n, W, 0, 0};
+  JWin w{q, win, n, W, 0, 0, 0, 0};
+  const bool fast = W >= 256;
+  uint64_t pk = 0, pb = 0, pv = 0, pm = 0, c_0 = 0;  // GI_PROF: key, build, value cycles, members
+  const uint64_t c_start = gi_clock();
   uint32_t nf = nf0, nb = nb0;
   uint32_t i = 0;
   while (i < n && json_ws(jw_at(w, i))) i++;
@@ -5622,8 +5831,9 @@ __device__ bool wave_parse_json(const Region& g, const uint8_t* q, uint32_t n, u
   if (L < 4) path[L] = "json"[L];
   __syncthreads();
   uint32_t d = 1;
-  if (l0) st[0] = {root, 4, 0, jw_at(w, i) == '[' ? 1u : 0u, wave_key_hash(path, 4)};
-  else (void)wave_key_hash(path, 4);
+  const uint32_t h0 = wave_key_hash(path, 4);
+  const uint32_t arr0 = jw_at(w, i) == '[' ? 1u : 0u;
+  if (l0) st[0] = {root, 4, 0, arr0, h0};
   __syncthreads();
   const uint64_t lim = 4ull * n + 1024;
   uint64_t jb = 0;
@@ -5644,6 +5854,16 @@ __device__ bool wave_parse_json(const Region& g, const uint8_t* q, uint32_t n, u
     return true;
   };
   while (d > 0) {
+    if (fast) {
+      // one member (or element, or a container's close) read from 64 bytes of
+      // the window at i with bit masks; 0: not that simple -- the member takes
+      // the path below, which also decides every error
+      const int r = jw_fast_member(g, w, q, i, d, nf, nb, jb, lim, path, st);
+      if (r) {
+        wave_lds_sync();  // path / st written
+        continue;
+      }
+    }
     JWFrame F = st[d - 1];
     while (i < n && json_ws(jw_at(w, i))) i++;
     if (i >= n) return false;
@@ -5670,6 +5890,7 @@ __device__ bool wave_parse_json(const Region& g, const uint8_t* q, uint32_t n, u
     // the element's key: the container's (path[0, F.kn)) + '.' + name / index
     uint32_t kn;
     const uint32_t koff = nb;
+    if (prof) c_0 = gi_clock();
     if (F.is_arr) {
       if (nb + F.kn + 12 > g.cap_b) return false;
       const uint32_t dn = dec_len(F.count);
@@ -5706,10 +5927,12 @@ __device__ bool wave_parse_json(const Region& g, const uint8_t* q, uint32_t n, u
       i++;
       while (i < n && json_ws(jw_at(w, i))) i++;
     }
-    __syncthreads();  // path written
+    uint64_t c_1 = prof ? gi_clock() : 0;
+    wave_lds_sync();  // path written
     for (uint32_t k = L; k < kn; k += 64) g.bytes[koff + k] = path[k];
     const uint32_t kh = wave_key_hash(path, kn);
     nb += kn;
+    uint64_t c_2 = prof ? gi_clock() : 0;
     F.count++;
     if (l0) st[d - 1].count = F.count;
     if (i >= n) return false;
@@ -5750,10 +5973,27 @@ __device__ bool wave_parse_json(const Region& g, const uint8_t* q, uint32_t n, u
       if (!add(koff, kn, kh, q + i, e - i)) return false;
       i = e;
     }
-    __syncthreads();  // st written
+    wave_lds_sync();  // st written
+    if (prof) {
+      const uint64_t c_3 = gi_clock();
+      pk += c_1 - c_0;
+      pb += c_2 - c_1;
+      pv += c_3 - c_2;
+      pm++;
+    }
   }
   while (i < n && json_ws(jw_at(w, i))) i++;
   if (i != n) return false;
+  if (prof && l0) {
+    atomicAdd(&prof[9], (unsigned long long)(gi_clock() - c_start));
+    atomicAdd(&prof[10], (unsigned long long)w.rc);
+    atomicAdd(&prof[11], (unsigned long long)w.nr);
+    atomicAdd(&prof[12], (unsigned long long)pk);
+    atomicAdd(&prof[13], (unsigned long long)pb);
+    atomicAdd(&prof[14], (unsigned long long)pv);
+    atomicAdd(&prof[15], (unsigned long long)pm);
+    atomicAdd(&prof[16], 1ull);
+  }
   // repeated keys (json_fold_keys: first position, last value)
   const uint32_t nk = nf - nf0;
   if (nk >= 2) {
@@ -6021,11 +6261,11 @@ __device__ bool wave_parse_urlenc(const Region& g, const uint8_t* q, uint32_t n,
   return true;
 }
 
-__global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_bparse(DProgram P, DBatch B) {
   // JSON bodies up to B.bparse_lds bytes are parsed out of an LDS copy (the
   // sequential parser then waits on LDS, not on global memory, per byte)
   extern __shared__ __attribute__((aligned(16))) uint8_t jlds[];
-  __shared__ uint32_t chist[GI_NCLS];  // item counts per class of this body's fields
+  __shared__ uint32_t chist[2 * (GI_NCLS / 16)];  // item counts per class of this body's ARGS_POST values / keys
   __shared__ __attribute__((aligned(16))) uint8_t jpath[GI_JW_PATH];  // wave_parse_json's key path
   __shared__ JWFrame jst[GI_JSON_MAX_DEPTH + 1];                       // and frame stack
   const uint32_t L = threadIdx.x;
@@ -6094,7 +6334,7 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
       // the body through an LDS window of B.bparse_lds bytes, the whole wave parsing
       uint32_t nfo = nf0;
       ok = wave_parse_json(g, q, n, nf0, nb0, (gi_lds_u8*)jlds, B.bparse_lds, (gi_lds_u8*)jpath,
-                           jst, &nfo, &nb);
+                           jst, &nfo, &nb, B.prof);
       n_post = nfo - nf0;
       __syncthreads();  // the next body reuses the window
     } else {  // JSON (or an urlencoded body the arena bound does not cover): lane 0, sequential
@@ -6153,17 +6393,20 @@ __global__ void __launch_bounds__(64) k_bparse(DProgram P, DBatch B) {
     // sides some filter reads), aggregated in LDS
     const uint32_t sides = P.n_streams ? P.item_sides[FK_ARG_POST] : 0u;
     if (sides) {
-      for (uint32_t k = L; k < GI_NCLS; k += 64) chist[k] = 0;
+      constexpr uint32_t NG = GI_NCLS / 16;
+      for (uint32_t k = L; k < 2 * NG; k += 64) chist[k] = 0;
       __syncthreads();
       for (uint32_t i = L; i < n_post; i += 64) {
         const Field fl = g.fields[nf0 + i];
         if (fl.kind != FK_ARG_POST) continue;
-        if (sides & 1) atomicAdd(&chist[item_class(FK_ARG_POST, 0, fl.vn)], 1u);
-        if (sides & 2) atomicAdd(&chist[item_class(FK_ARG_POST, 1, fl.kn)], 1u);
+        if (sides & 1) atomicAdd(&chist[item_class_in_group(fl.vn)], 1u);
+        if (sides & 2) atomicAdd(&chist[NG + item_class_in_group(fl.kn)], 1u);
       }
       __syncthreads();
-      for (uint32_t k = L; k < GI_NCLS; k += 64)
-        if (chist[k]) atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + k], chist[k]);
+      for (uint32_t k = L; k < 2 * NG; k += 64)
+        if (chist[k])
+          atomicAdd(&B.bcounts[(r / 256) * GI_NCLS + item_class_of_group((FK_ARG_POST << 1) | (k / NG), k % NG)],
+                    chist[k]);
       __syncthreads();
     }
   }

@@ -1444,6 +1444,13 @@ int gi_sync(gi_ctx* c) {
                   c->rs->prog.body_links[k], R.id, R.tchain_len, c->rs->prog.ops[R.op].kind, h[96 + 2 * k] / 1e6,
                   h[97 + 2 * k] / 1e6);
         }
+        if (h[16])
+          fprintf(stderr,
+                  "GI_PROF wave_parse_json per body (%.0f bodies): total %.0f cyc, refills %.1f (%.0f cyc), members %.0f: "
+                  "key %.0f, build+hash %.0f, value+add %.0f cyc per member\n",
+                  (double)h[16], (double)h[9] / h[16], (double)h[11] / h[16], (double)h[10] / h[16],
+                  (double)h[15] / h[16], (double)h[12] / std::max(1.0, (double)h[15]),
+                  (double)h[13] / std::max(1.0, (double)h[15]), (double)h[14] / std::max(1.0, (double)h[15]));
         const double n = c->n_req;
         fprintf(stderr,
                 "GI_PROF k_eval per request: init %.0f cyc, phase1 %.0f, phase2 %.0f, total %.0f; rule visits %.1f, "
