@@ -6261,7 +6261,11 @@ __device__ bool wave_parse_urlenc(const Region& g, const uint8_t* q, uint32_t n,
   return true;
 }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_bparse(DProgram P, DBatch B) {
+#ifndef GI_BPARSE_WPE
+#define GI_BPARSE_WPE 4  // k_bparse's register budget (waves per SIMD).  C3/C4 A/B: 4 (128 VGPRs, 30 spilled) 62 ms,
+                         // 3 (168 VGPRs, no spills) 73 ms -- the parsers are latency chains, occupancy hides them
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_BPARSE_WPE))) k_bparse(DProgram P, DBatch B) {
   // JSON bodies up to B.bparse_lds bytes are parsed out of an LDS copy (the
   // sequential parser then waits on LDS, not on global memory, per byte)
   extern __shared__ __attribute__((aligned(16))) uint8_t jlds[];
