@@ -8300,7 +8300,10 @@ __device__ __forceinline__ bool wave_run_chain(const DProgram& P, uint32_t off, 
 // Two waves per SIMD (the inlined LDS tile path would otherwise take the
 // whole register file: 1 wave, k_body 68 -> 83 ms on C3 at 50k; with the cap,
 // 17 spilled VGPRs and 46 ms).
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8))) k_body(DProgram P, DBatch B) {
+#ifndef GI_BODY_WPE
+#define GI_BODY_WPE 3  // C3 A/B: 3 waves/SIMD (168 VGPRs, 84 spilled) 164 ms, 2 waves (256 VGPRs) 174 ms
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GI_BODY_WPE, 8))) k_body(DProgram P, DBatch B) {
   __shared__ __attribute__((aligned(16))) uint8_t kb_lds[GI_BODY_LDS];
   const uint32_t L = threadIdx.x;
   for (uint32_t bi = blockIdx.x; bi < B.n_body; bi += gridDim.x) {
