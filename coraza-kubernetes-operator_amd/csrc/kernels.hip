@@ -9325,7 +9325,11 @@ static void launch_phase_a(const DProgram& P, const DBatch& B, const ScanLaunch&
       (void)hipMemsetAsync(B.dmemo_keys, 0, 8ull * (B.dmemo_mask + 1), stream);
       (void)hipMemsetAsync(B.dmemo_info, 0, 16ull * (B.dmemo_mask + 1), stream);
     }
-    GI_LAUNCH(s2 ? "k_detect.2" : "k_detect", k_detect, dim3(2048), dim3(256), 0, stream, P, B);
+    // grid: 12 rounds of resident workgroups (3 per CU at 48 KB of LDS x 256
+    // CUs): finer grid-stride shares balance the divergent detectors.  C2 A/B
+    // (GI_DETECT_GRID): 768 11.9 ms, 2048 10.9, 3072 10.7, 6144 10.2, 9216 10.1
+    static const uint32_t det_grid = getenv("GI_DETECT_GRID") ? (uint32_t)atoi(getenv("GI_DETECT_GRID")) : 9216u;
+    GI_LAUNCH(s2 ? "k_detect.2" : "k_detect", k_detect, dim3(det_grid), dim3(256), 0, stream, P, B);
   }
   if (B.long_cap) GI_LAUNCH(s2 ? "k_long.2" : "k_long", k_long, dim3(B.long_grid), dim3(64), 0, stream, P, B);
   if (ev) (void)hipEventRecord(ev[1], stream);
